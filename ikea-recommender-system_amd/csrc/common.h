@@ -1,0 +1,78 @@
+// Shared helpers for the gfx950 (MI355X / CDNA4) kernels of the GRU4Rec /
+// SQN / SMORL training path.  Wave64 everywhere; fp32 data; exact-f32 MFMA
+// (v_mfma_f32_32x32x2_f32 / v_mfma_f32_16x16x4_f32, bitwise an fmaf chain).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+typedef float f4 __attribute__((ext_vector_type(4)));
+typedef float f16v __attribute__((ext_vector_type(16)));
+
+#define RG_OK 0
+#define RG_ERR_ARG (-1)
+#define RG_ERR_LAUNCH (-2)
+#define RG_ERR_SHAPE (-3)
+
+#define RG_LAUNCH_CHECK()                                  \
+  do {                                                     \
+    hipError_t e_ = hipGetLastError();                     \
+    if (e_ != hipSuccess) return RG_ERR_LAUNCH;            \
+  } while (0)
+
+__device__ __forceinline__ f4 mfma16(float a, float b, f4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ f16v mfma32(float a, float b, f16v c) {
+  return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
+}
+
+// Row of a 32x32 MFMA accumulator register r held by lane half h (= lane>>5).
+__device__ __forceinline__ int acc32_row(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
+
+__device__ __forceinline__ float sigmoidf_ref(float x) {
+  // torch CPU sigmoid: 1 / (1 + exp(-x))
+  return 1.0f / (1.0f + expf(-x));
+}
+
+// online (max, sum-exp, argmax) merge; ties keep the smaller index
+struct LseState {
+  float m;
+  float s;
+  int arg;
+};
+__device__ __forceinline__ void lse_merge(float& m, float& s, int& arg, float m2, float s2, int arg2) {
+  if (m2 > m || (m2 == m && arg2 < arg)) {
+    float nm = m2;
+    s = s * expf(m - nm) + s2;
+    m = nm;
+    arg = arg2;
+  } else {
+    s = s + s2 * expf(m2 - m);
+  }
+}
+
+__device__ __forceinline__ int wave_lane() { return threadIdx.x & 63; }
+
+// torch.optim.Adam (defaults: amsgrad=False, weight_decay=0, maximize=False),
+// _single_tensor_adam op by op:
+//   exp_avg.lerp_(grad, 1-β1)          -> m + w1*(g - m)         (weight < 0.5 branch)
+//   exp_avg_sq.mul_(β2).addcmul_(g, g, value=1-β2)
+//   denom = (exp_avg_sq.sqrt() / bias_correction2_sqrt).add_(eps)
+//   param.addcdiv_(exp_avg, denom, value=-step_size)
+// Scalars arrive already rounded to fp32 the way the CPU kernels see them.
+struct AdamArgs {
+  float w1;        // 1 - beta1
+  float beta2;     // beta2
+  float c2;        // 1 - beta2
+  float bc2_sqrt;  // sqrt(1 - beta2^t)
+  float eps;
+  float neg_step;  // -lr / (1 - beta1^t)
+};
+
+__device__ __forceinline__ void adam_elem(float& p, float& m, float& v, float g, const AdamArgs& a) {
+  m = m + a.w1 * (g - m);
+  v = v * a.beta2;
+  v = v + a.c2 * g * g;
+  const float denom = sqrtf(v) / a.bc2_sqrt + a.eps;
+  p = p + a.neg_step * (m / denom);
+}

@@ -1,0 +1,151 @@
+// Generic exact-f32 MFMA GEMM for the GRU's dense contractions:
+//   input projection  Gi  = X · W_ihᵀ + b_ih      (T × 3H, K = E)
+//   input gradient    dX  = dGi · W_ih             (T × E,  K = 3H)
+//   weight gradients  dW  = dGᵀ · X / Hprev        (3H × E, K = T, split-K)
+// C(m,n) = Σ_k A(m,k)·B(k,n) with A(m,k) = A[m*sam + k*sak], B(k,n) =
+// B[k*sbk + n*sbn]; M and K may be read from device memory (T is only known
+// on the device after packing).  64×64 block tile, BK = 16, four waves each
+// owning one 32×32 v_mfma_f32_32x32x2_f32 accumulator.  Split-K writes one
+// slab per grid.z; rg_reduce_slabs sums them in slab order (deterministic).
+#include "common.h"
+
+#define GB_M 64
+#define GB_N 64
+#define GB_K 16
+#define GB_PAD 4
+
+template <bool A_KCONTIG, bool B_NCONTIG>
+__global__ __launch_bounds__(256) void k_gemm_f32(const float* __restrict__ A, int64_t sam, int64_t sak,
+                                                  const float* __restrict__ Bm, int64_t sbk,
+                                                  int64_t sbn, float* __restrict__ C, int64_t ldc,
+                                                  int64_t slab, const float* __restrict__ bias, int M_,
+                                                  const int32_t* __restrict__ Mptr, int N, int K_,
+                                                  const int32_t* __restrict__ Kptr, int kchunk) {
+  __shared__ float As[GB_K][GB_M + GB_PAD];
+  __shared__ float Bs[GB_K][GB_N + GB_PAD];
+  const int M = Mptr ? *Mptr : M_;
+  const int K = Kptr ? *Kptr : K_;
+  const int m0 = blockIdx.y * GB_M;
+  const int n0 = blockIdx.x * GB_N;
+  const int kbeg = blockIdx.z * kchunk;
+  const int kend = min(K, kbeg + kchunk);
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int w = tid >> 6;
+  const int wm = w >> 1, wn = w & 1;
+  float* Cz = C + (int64_t)blockIdx.z * slab;
+  if (m0 >= M) return;  // whole tile beyond the device-side row count
+  f16v acc = {};
+  for (int k0 = kbeg; k0 < kend; k0 += GB_K) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      int e = tid + 256 * i;
+      int kk, mm;
+      if (A_KCONTIG) {
+        kk = e & 15;
+        mm = e >> 4;
+      } else {
+        mm = e & 63;
+        kk = e >> 6;
+      }
+      int m = m0 + mm, k = k0 + kk;
+      As[kk][mm] = (m < M && k < kend) ? A[(int64_t)m * sam + (int64_t)k * sak] : 0.0f;
+      int nn;
+      if (B_NCONTIG) {
+        nn = e & 63;
+        kk = e >> 6;
+      } else {
+        kk = e & 15;
+        nn = e >> 4;
+      }
+      int n = n0 + nn;
+      k = k0 + kk;
+      Bs[kk][nn] = (n < N && k < kend) ? Bm[(int64_t)k * sbk + (int64_t)n * sbn] : 0.0f;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int s = 0; s < GB_K / 2; ++s) {
+      float a = As[2 * s + (lane >> 5)][wm * 32 + (lane & 31)];
+      float b = Bs[2 * s + (lane >> 5)][wn * 32 + (lane & 31)];
+      acc = mfma32(a, b, acc);
+    }
+    __syncthreads();
+  }
+  const int col = n0 + wn * 32 + (lane & 31);
+  if (col >= N) return;
+  const float bv = bias ? bias[col] : 0.0f;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    int row = m0 + wm * 32 + acc32_row(r, lane >> 5);
+    if (row < M) Cz[(int64_t)row * ldc + col] = acc[r] + bv;
+  }
+}
+
+extern "C" int rg_gemm_f32(const float* A, int64_t sam, int64_t sak, const float* B, int64_t sbk,
+                           int64_t sbn, float* C, int64_t ldc, const float* bias, int M, const int32_t* Mptr,
+                           int N, int K, const int32_t* Kptr, int splits, hipStream_t stream) {
+  if (M <= 0 || N <= 0 || K <= 0 || splits <= 0) return RG_ERR_ARG;
+  if (!(sak == 1 || sam == 1) || !(sbn == 1 || sbk == 1)) return RG_ERR_ARG;
+  int kchunk = (K + splits - 1) / splits;
+  kchunk = (kchunk + GB_K - 1) / GB_K * GB_K;
+  int64_t slab = (int64_t)M * ldc;
+  if (splits > 1 && bias) return RG_ERR_ARG;  // bias is added by the slab reduction
+  dim3 grid((N + GB_N - 1) / GB_N, (M + GB_M - 1) / GB_M, splits);
+  bool ak = (sak == 1), bn = (sbn == 1);
+#define GL(AK, BN)                                                                                     \
+  hipLaunchKernelGGL((k_gemm_f32<AK, BN>), grid, dim3(256), 0, stream, A, sam, sak, B, sbk, sbn, C, ldc, \
+                     slab, bias, M, Mptr, N, K, Kptr, kchunk)
+  if (ak && bn) GL(true, true);
+  else if (ak && !bn) GL(true, false);
+  else if (!ak && bn) GL(false, true);
+  else GL(false, false);
+#undef GL
+  RG_LAUNCH_CHECK();
+  return RG_OK;
+}
+
+// out[i] = Σ_z slabs[z*n + i] (+ bias[i % ncol]), z in order.
+__global__ void k_reduce_slabs(const float* __restrict__ slabs, int nslab, int64_t n, float* __restrict__ out,
+                               const float* __restrict__ bias, int ncol, int accumulate) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    float s = 0.0f;
+    for (int z = 0; z < nslab; ++z) s += slabs[(int64_t)z * n + i];
+    if (bias) s += bias[i % ncol];
+    out[i] = accumulate ? out[i] + s : s;
+  }
+}
+
+extern "C" int rg_reduce_slabs(const float* slabs, int nslab, int64_t n, float* out, const float* bias, int ncol,
+                               int accumulate, hipStream_t stream) {
+  if (n <= 0 || nslab <= 0) return RG_ERR_ARG;
+  int blocks = (int)((n + 255) / 256);
+  if (blocks > 8192) blocks = 8192;
+  hipLaunchKernelGGL(k_reduce_slabs, dim3(blocks), dim3(256), 0, stream, slabs, nslab, n, out, bias, ncol,
+                     accumulate);
+  RG_LAUNCH_CHECK();
+  return RG_OK;
+}
+
+// Column sums of a row-major (rows × ncol) matrix, split over rows into
+// slabs: slabs[z*ncol + c] = Σ_{rows in split z} X[r*ncol + c].
+__global__ void k_colsum(const float* __restrict__ X, int ncol, int rows_, const int32_t* __restrict__ rows_ptr,
+                         int rchunk, float* __restrict__ slabs) {
+  const int rows = rows_ptr ? *rows_ptr : rows_;
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= ncol) return;
+  const int r0 = blockIdx.y * rchunk;
+  const int r1 = min(rows, r0 + rchunk);
+  float s = 0.0f;
+  for (int r = r0; r < r1; ++r) s += X[(int64_t)r * ncol + c];
+  slabs[(int64_t)blockIdx.y * ncol + c] = s;
+}
+
+extern "C" int rg_colsum(const float* X, int ncol, int rows, const int32_t* rows_ptr, int splits, float* slabs,
+                         hipStream_t stream) {
+  if (ncol <= 0 || splits <= 0 || rows <= 0) return RG_ERR_ARG;
+  int rchunk = (rows + splits - 1) / splits;
+  dim3 grid((ncol + 255) / 256, splits);
+  hipLaunchKernelGGL(k_colsum, grid, dim3(256), 0, stream, X, ncol, rows, rows_ptr, rchunk, slabs);
+  RG_LAUNCH_CHECK();
+  return RG_OK;
+}

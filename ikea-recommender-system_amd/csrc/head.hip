@@ -1,0 +1,590 @@
+// Full-softmax output head (SURVEY §8 A6, A7, A8-for-the-head, A14 argmax).
+//
+// Reference: Z = h·Wᵀ + b (nn.Linear(H→A), GRU4Rec/model.py:58-60,80),
+// loss = CrossEntropyLoss(mean)(Z, a) (:121,146), dense Adam step (:149-153).
+//
+// Layout choice: logits are kept TRANSPOSED, Zᵀ[j][b] (A × ldz, ldz ≥ B), so
+// every store and every re-read in backward is a run of consecutive batch
+// rows (128-B segments per half-wave) — the MFMA D layout writes columns, and
+// both backward GEMMs stream Zᵀ rows.
+//
+//  k_head_fwd   : Zᵀ tile = W_tile · h_chunkᵀ on v_mfma_f32_32x32x2_f32 with the
+//                 128×HF W tile resident in VGPRs (64 regs/lane at HF=128) and
+//                 32-row h chunks double-buffered through LDS; epilogue adds the
+//                 bias, stores Zᵀ and emits per-(item-block, row) online
+//                 (max, Σexp, argmax) partials — the softmax never re-reads Zᵀ.
+//  k_lse_*      : merge partials -> lse[b], argmax[b], loss_b = lse_b − Z[a_b,b].
+//  k_head_dh    : dh = dZ·W, dZ = (exp(Z−lse) − onehot)·g recomputed on load;
+//                 split over the item axis into deterministic slabs.
+//  k_head_dw_adam: dW = dZᵀ·h and db = Σ_b dZ for a 128-item tile, accumulated
+//                 over all rows in VGPRs, then the Adam update of those W/b rows
+//                 in the same kernel (no gradient tensor ever reaches HBM).
+#include "common.h"
+
+#define NEG_INF (-__builtin_inff())
+
+__device__ __forceinline__ void stat_merge(float& m, float& s, int& a, float m2, float s2, int a2) {
+  if (a2 == INT32_MAX) return;  // empty partial
+  if (a == INT32_MAX) {
+    m = m2;
+    s = s2;
+    a = a2;
+    return;
+  }
+  if (m2 > m || (m2 == m && a2 < a)) {
+    s = s * expf(m - m2) + s2;
+    m = m2;
+    a = a2;
+  } else {
+    s = s + s2 * expf(m2 - m);
+  }
+}
+
+// ------------------------------------------------------------------ fwd ----
+template <int HF>
+__global__ __launch_bounds__(256) void k_head_fwd(const float* __restrict__ h, const float* __restrict__ W,
+                                                  const float* __restrict__ bias, int B, int A,
+                                                  float* __restrict__ ZT, int64_t ldz, float* __restrict__ pmax,
+                                                  float* __restrict__ psum, int32_t* __restrict__ parg,
+                                                  int want_sum) {
+  constexpr int KH = HF / 2;
+  constexpr int LDB = HF + 4;
+  constexpr int NV = 8 * HF;                 // float4 per 32-row chunk
+  constexpr int NL = (NV + 255) / 256;       // float4 per thread per chunk
+  __shared__ __attribute__((aligned(16))) float hbuf[2][32][LDB];
+  __shared__ float sm[2][4][32];
+  __shared__ float ss[2][4][32];
+  __shared__ int sa[2][4][32];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, half = lane >> 5, l32 = lane & 31;
+  const int jw = blockIdx.x * 128 + 32 * w;
+
+  float Wreg[KH];
+  {
+    const int jr = jw + l32;
+    if (jr < A) {
+      const float* src = W + (int64_t)jr * HF + half * KH;
+#pragma unroll
+      for (int s = 0; s < KH; s += 4) {
+        f4 v = *reinterpret_cast<const f4*>(src + s);
+        Wreg[s] = v.x;
+        Wreg[s + 1] = v.y;
+        Wreg[s + 2] = v.z;
+        Wreg[s + 3] = v.w;
+      }
+    } else {
+#pragma unroll
+      for (int s = 0; s < KH; ++s) Wreg[s] = 0.f;
+    }
+  }
+  float bj[16];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    int j = jw + acc32_row(r, half);
+    bj[r] = (j < A) ? bias[j] : 0.f;
+  }
+  const int nch = (B + 31) / 32;
+  f4 pre[NL];
+  auto load_chunk = [&](int c) {
+#pragma unroll
+    for (int i = 0; i < NL; ++i) {
+      int e = tid + 256 * i;
+      int rr = e / (HF / 4), c4 = e % (HF / 4);
+      int b = c * 32 + rr;
+      f4 v = {0.f, 0.f, 0.f, 0.f};
+      if (e < NV && b < B) v = *reinterpret_cast<const f4*>(h + (int64_t)b * HF + 4 * c4);
+      pre[i] = v;
+    }
+  };
+  auto store_chunk = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < NL; ++i) {
+      int e = tid + 256 * i;
+      if (e < NV) {
+        int rr = e / (HF / 4), c4 = e % (HF / 4);
+        *reinterpret_cast<f4*>(&hbuf[buf][rr][4 * c4]) = pre[i];
+      }
+    }
+  };
+  load_chunk(0);
+  store_chunk(0);
+  __syncthreads();
+  int cur = 0;
+  for (int c = 0; c < nch; ++c) {
+    if (c + 1 < nch) load_chunk(c + 1);
+    f16v acc = {};
+    const float* hb = &hbuf[cur][l32][half * KH];
+#pragma unroll
+    for (int s = 0; s < KH; s += 4) {
+      f4 hv = *reinterpret_cast<const f4*>(hb + s);
+      acc = mfma32(Wreg[s], hv.x, acc);
+      acc = mfma32(Wreg[s + 1], hv.y, acc);
+      acc = mfma32(Wreg[s + 2], hv.z, acc);
+      acc = mfma32(Wreg[s + 3], hv.w, acc);
+    }
+    const int b = c * 32 + l32;
+    const bool bv = b < B;
+    float m = NEG_INF, sum = 0.f;
+    int arg = INT32_MAX;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int j = jw + acc32_row(r, half);
+      const float z = acc[r] + bj[r];
+      acc[r] = z;
+      if (j < A) {
+        if (ZT && bv) ZT[(int64_t)j * ldz + b] = z;
+        if (z > m) {
+          m = z;
+          arg = j;
+        }
+      }
+    }
+    if (want_sum && arg != INT32_MAX) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int j = jw + acc32_row(r, half);
+        if (j < A) sum += expf(acc[r] - m);
+      }
+    }
+    {
+      float m2 = __shfl_xor(m, 32);
+      float s2 = __shfl_xor(sum, 32);
+      int a2 = __shfl_xor(arg, 32);
+      stat_merge(m, sum, arg, m2, s2, a2);
+    }
+    if (half == 0) {
+      sm[cur][w][l32] = m;
+      ss[cur][w][l32] = sum;
+      sa[cur][w][l32] = arg;
+    }
+    if (c + 1 < nch) store_chunk(cur ^ 1);
+    __syncthreads();
+    if (w == 0 && half == 0 && bv) {
+      float M = sm[cur][0][l32], S = ss[cur][0][l32];
+      int AR = sa[cur][0][l32];
+#pragma unroll
+      for (int q = 1; q < 4; ++q) stat_merge(M, S, AR, sm[cur][q][l32], ss[cur][q][l32], sa[cur][q][l32]);
+      const int64_t o = (int64_t)blockIdx.x * B + b;
+      pmax[o] = M;
+      if (psum) psum[o] = S;
+      parg[o] = AR;
+    }
+    cur ^= 1;
+  }
+}
+
+extern "C" int rg_head_fwd(const float* h, const float* W, const float* bias, int B, int A, int HF, float* ZT,
+                           int64_t ldz, float* pmax, float* psum, int32_t* parg, int want_sum, hipStream_t stream) {
+  if (B <= 0 || A <= 0) return RG_ERR_ARG;
+  if (ZT && ldz < B) return RG_ERR_ARG;
+  dim3 grid((A + 127) / 128);
+#define HL(HFV)                                                                                                \
+  hipLaunchKernelGGL(k_head_fwd<HFV>, grid, dim3(256), 0, stream, h, W, bias, B, A, ZT, ldz, pmax, psum, parg, \
+                     want_sum)
+  switch (HF) {
+    case 16: HL(16); break;
+    case 32: HL(32); break;
+    case 64: HL(64); break;
+    case 128: HL(128); break;
+    case 256: HL(256); break;
+    default: return RG_ERR_SHAPE;
+  }
+#undef HL
+  RG_LAUNCH_CHECK();
+  return RG_OK;
+}
+
+// --------------------------------------------------------- lse combine ----
+// stage 1: split the nJ partials of each row into S groups.
+__global__ void k_lse_stage1(const float* __restrict__ pmax, const float* __restrict__ psum,
+                             const int32_t* __restrict__ parg, int B, int nJ, int jchunk, float* __restrict__ omax,
+                             float* __restrict__ osum, int32_t* __restrict__ oarg) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  const int z = blockIdx.y;
+  const int j0 = z * jchunk, j1 = min(nJ, j0 + jchunk);
+  float m = NEG_INF, s = 0.f;
+  int a = INT32_MAX;
+  for (int j = j0; j < j1; ++j) {
+    const int64_t o = (int64_t)j * B + b;
+    stat_merge(m, s, a, pmax[o], psum ? psum[o] : 0.f, parg[o]);
+  }
+  const int64_t o = (int64_t)z * B + b;
+  omax[o] = m;
+  osum[o] = s;
+  oarg[o] = a;
+}
+
+// stage 2: lse[b], argmax[b], and (when ZT/tgt are given) loss_b = lse_b − Zᵀ[a_b][b].
+__global__ void k_lse_final(const float* __restrict__ omax, const float* __restrict__ osum,
+                            const int32_t* __restrict__ oarg, int B, int S, const float* __restrict__ ZT,
+                            int64_t ldz, const int64_t* __restrict__ tgt, float* __restrict__ lse,
+                            int32_t* __restrict__ amax, float* __restrict__ loss_row) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  float m = NEG_INF, s = 0.f;
+  int a = INT32_MAX;
+  for (int z = 0; z < S; ++z) {
+    const int64_t o = (int64_t)z * B + b;
+    stat_merge(m, s, a, omax[o], osum[o], oarg[o]);
+  }
+  const float l = m + logf(s);
+  if (lse) lse[b] = l;
+  if (amax) amax[b] = a;
+  if (loss_row && ZT && tgt) loss_row[b] = l - ZT[tgt[b] * ldz + b];
+}
+
+extern "C" int rg_lse_combine(const float* pmax, const float* psum, const int32_t* parg, int B, int nJ,
+                              float* work, const float* ZT, int64_t ldz, const int64_t* tgt, float* lse,
+                              int32_t* amax, float* loss_row, hipStream_t stream) {
+  if (B <= 0 || nJ <= 0) return RG_ERR_ARG;
+  int S = 64;
+  if (S > nJ) S = nJ;
+  int jchunk = (nJ + S - 1) / S;
+  S = (nJ + jchunk - 1) / jchunk;
+  float* omax = work;
+  float* osum = work + (int64_t)S * B;
+  int32_t* oarg = reinterpret_cast<int32_t*>(work + 2 * (int64_t)S * B);
+  hipLaunchKernelGGL(k_lse_stage1, dim3((B + 255) / 256, S), dim3(256), 0, stream, pmax, psum, parg, B, nJ, jchunk,
+                     omax, osum, oarg);
+  hipLaunchKernelGGL(k_lse_final, dim3((B + 255) / 256), dim3(256), 0, stream, omax, osum, oarg, B, S, ZT, ldz,
+                     tgt, lse, amax, loss_row);
+  RG_LAUNCH_CHECK();
+  return RG_OK;
+}
+
+// out[0] = (Σ x[i]) · scale  (one workgroup, fixed tree: deterministic)
+__global__ __launch_bounds__(1024) void k_sum_scale(const float* __restrict__ x, int n, float scale,
+                                                    float* __restrict__ out, double* __restrict__ out64) {
+  __shared__ double red[1024];
+  double s = 0.0;
+  for (int i = threadIdx.x; i < n; i += 1024) s += (double)x[i];
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int d = 512; d > 0; d >>= 1) {
+    if ((int)threadIdx.x < d) red[threadIdx.x] += red[threadIdx.x + d];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    if (out) out[0] = (float)(red[0] * (double)scale);
+    if (out64) out64[0] = red[0] * (double)scale;
+  }
+}
+
+extern "C" int rg_sum_scale(const float* x, int n, float scale, float* out, double* out64, hipStream_t stream) {
+  if (n <= 0) return RG_ERR_ARG;
+  hipLaunchKernelGGL(k_sum_scale, dim3(1), dim3(1024), 0, stream, x, n, scale, out, out64);
+  RG_LAUNCH_CHECK();
+  return RG_OK;
+}
+
+// ------------------------------------------------------------ dh ----------
+// dh_slab[z][b][c] = Σ_{j in split z} dZᵀ[j][b] · W[j][c]
+template <int HF>
+__global__ __launch_bounds__(256) void k_head_dh(const float* __restrict__ ZT, int64_t ldz,
+                                                 const float* __restrict__ lse, const int64_t* __restrict__ tgt,
+                                                 float gscale, const float* __restrict__ W, int B, int A,
+                                                 int jsplit, float* __restrict__ slabs) {
+  constexpr int NCT = HF / 32 > 0 ? HF / 32 : 1;
+  constexpr int JC = 32;
+  constexpr int LDW = (HF < 32 ? 32 : HF) + 4;
+  constexpr int NW4 = JC * HF / 4;            // float4 of W per chunk
+  constexpr int NWL = (NW4 + 255) / 256;
+  __shared__ __attribute__((aligned(16))) float zt[2][JC][128 + 4];
+  __shared__ __attribute__((aligned(16))) float wt[2][JC][LDW];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, half = lane >> 5, l32 = lane & 31;
+  const int b0 = blockIdx.x * 128;
+  const int jb = blockIdx.y * jsplit;
+  const int je = min(A, jb + jsplit);
+  // this thread's 4 batch columns of every Zᵀ chunk
+  const int c4 = tid & 31;
+  const int bq = b0 + 4 * c4;
+  float l4[4];
+  int64_t t4[4];
+  bool v4[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    v4[q] = (bq + q) < B;
+    l4[q] = v4[q] ? lse[bq + q] : 0.f;
+    t4[q] = v4[q] ? tgt[bq + q] : -1;
+  }
+  f4 zp[4];
+  f4 wp[NWL];
+  auto load = [&](int j0) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int jj = (tid >> 5) + 8 * i;
+      const int j = j0 + jj;
+      f4 z = {0.f, 0.f, 0.f, 0.f};
+      if (j < je && bq < B) z = *reinterpret_cast<const f4*>(ZT + (int64_t)j * ldz + bq);
+      zp[i] = z;
+    }
+#pragma unroll
+    for (int i = 0; i < NWL; ++i) {
+      const int e = tid + 256 * i;
+      const int jj = e / (HF / 4), cc = e % (HF / 4);
+      const int j = j0 + jj;
+      f4 v = {0.f, 0.f, 0.f, 0.f};
+      if (e < NW4 && j < je) v = *reinterpret_cast<const f4*>(W + (int64_t)j * HF + 4 * cc);
+      wp[i] = v;
+    }
+  };
+  auto store = [&](int buf, int j0) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int jj = (tid >> 5) + 8 * i;
+      const int j = j0 + jj;
+      f4 d;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        float p = expf(zp[i][q] - l4[q]) - ((int64_t)j == t4[q] ? 1.0f : 0.0f);
+        d[q] = (v4[q] && j < je) ? p * gscale : 0.0f;
+      }
+      *reinterpret_cast<f4*>(&zt[buf][jj][4 * c4]) = d;
+    }
+#pragma unroll
+    for (int i = 0; i < NWL; ++i) {
+      const int e = tid + 256 * i;
+      if (e < NW4) {
+        const int jj = e / (HF / 4), cc = e % (HF / 4);
+        *reinterpret_cast<f4*>(&wt[buf][jj][4 * cc]) = wp[i];
+      }
+    }
+  };
+  f16v acc[NCT];
+#pragma unroll
+  for (int ct = 0; ct < NCT; ++ct) acc[ct] = f16v{};
+  if (jb < je) {
+    load(jb);
+    store(0, jb);
+  }
+  __syncthreads();
+  int cur = 0;
+  for (int j0 = jb; j0 < je; j0 += JC) {
+    const bool more = j0 + JC < je;
+    if (more) load(j0 + JC);
+#pragma unroll 4
+    for (int s = 0; s < JC / 2; ++s) {
+      const float a = zt[cur][2 * s + half][32 * w + l32];
+#pragma unroll
+      for (int ct = 0; ct < NCT; ++ct) {
+        const float bb = (HF >= 32 || l32 < HF) ? wt[cur][2 * s + half][ct * 32 + l32] : 0.f;
+        acc[ct] = mfma32(a, bb, acc[ct]);
+      }
+    }
+    if (more) store(cur ^ 1, j0 + JC);
+    __syncthreads();
+    cur ^= 1;
+  }
+  float* out = slabs + (int64_t)blockIdx.y * B * HF;
+#pragma unroll
+  for (int ct = 0; ct < NCT; ++ct) {
+    const int c = ct * 32 + l32;
+    if (c >= HF) continue;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int b = b0 + 32 * w + acc32_row(r, half);
+      if (b < B) out[(int64_t)b * HF + c] = acc[ct][r];
+    }
+  }
+}
+
+extern "C" int rg_head_dh(const float* ZT, int64_t ldz, const float* lse, const int64_t* tgt, float gscale,
+                          const float* W, int B, int A, int HF, int splits, float* slabs, hipStream_t stream) {
+  if (B <= 0 || A <= 0 || splits <= 0) return RG_ERR_ARG;
+  if (ldz < ((B + 3) / 4) * 4) return RG_ERR_ARG;
+  int jsplit = (A + splits - 1) / splits;
+  jsplit = (jsplit + 31) / 32 * 32;
+  splits = (A + jsplit - 1) / jsplit;
+  dim3 grid((B + 127) / 128, splits);
+#define DL(HFV)                                                                                              \
+  hipLaunchKernelGGL(k_head_dh<HFV>, grid, dim3(256), 0, stream, ZT, ldz, lse, tgt, gscale, W, B, A, jsplit, \
+                     slabs)
+  switch (HF) {
+    case 16: DL(16); break;
+    case 32: DL(32); break;
+    case 64: DL(64); break;
+    case 128: DL(128); break;
+    case 256: DL(256); break;
+    default: return RG_ERR_SHAPE;
+  }
+#undef DL
+  RG_LAUNCH_CHECK();
+  return splits;  // number of slabs written (>0)
+}
+
+// ------------------------------------------------------ dW + Adam ---------
+template <int HF>
+__global__ __launch_bounds__(256) void k_head_dw_adam(const float* __restrict__ ZT, int64_t ldz,
+                                                      const float* __restrict__ lse,
+                                                      const int64_t* __restrict__ tgt, float gscale,
+                                                      const float* __restrict__ h, int B, int A,
+                                                      float* __restrict__ W, float* __restrict__ mW,
+                                                      float* __restrict__ vW, float* __restrict__ bias,
+                                                      float* __restrict__ mb, float* __restrict__ vb, AdamArgs args,
+                                                      float* __restrict__ dW_out, float* __restrict__ db_out) {
+  constexpr int NCT = HF / 32 > 0 ? HF / 32 : 1;
+  constexpr int BC = 32;
+  constexpr int LDZ = BC + 4;
+  constexpr int LDH = (HF < 32 ? 32 : HF) + 4;
+  constexpr int NH4 = BC * HF / 4;
+  constexpr int NHL = (NH4 + 255) / 256;
+  __shared__ __attribute__((aligned(16))) float zt[2][128][LDZ];
+  __shared__ __attribute__((aligned(16))) float hs[2][BC][LDH];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, half = lane >> 5, l32 = lane & 31;
+  const int j0 = blockIdx.x * 128;
+  const int c4 = tid & 7;     // this thread's 4 batch columns within a chunk
+  const int jr0 = tid >> 3;   // rows jr0 + 32 i, i < 4
+  float dbp[4] = {0.f, 0.f, 0.f, 0.f};
+  f4 zp[4];
+  f4 hp[NHL];
+  float l4[4];
+  int64_t t4[4];
+  auto load = [&](int b0) {
+    const int bq = b0 + 4 * c4;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const bool v = (bq + q) < B;
+      l4[q] = v ? lse[bq + q] : 0.f;
+      t4[q] = v ? tgt[bq + q] : -2;
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int j = j0 + jr0 + 32 * i;
+      f4 z = {0.f, 0.f, 0.f, 0.f};
+      if (j < A && bq < B) z = *reinterpret_cast<const f4*>(ZT + (int64_t)j * ldz + bq);
+      zp[i] = z;
+    }
+#pragma unroll
+    for (int i = 0; i < NHL; ++i) {
+      const int e = tid + 256 * i;
+      const int rr = e / (HF / 4), cc = e % (HF / 4);
+      f4 v = {0.f, 0.f, 0.f, 0.f};
+      if (e < NH4 && b0 + rr < B) v = *reinterpret_cast<const f4*>(h + (int64_t)(b0 + rr) * HF + 4 * cc);
+      hp[i] = v;
+    }
+  };
+  auto store = [&](int buf, int b0) {
+    const int bq = b0 + 4 * c4;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int jj = jr0 + 32 * i;
+      const int j = j0 + jj;
+      f4 d;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        float p = expf(zp[i][q] - l4[q]) - ((int64_t)j == t4[q] ? 1.0f : 0.0f);
+        d[q] = ((bq + q) < B && j < A) ? p * gscale : 0.0f;
+      }
+      dbp[i] += (d[0] + d[1]) + (d[2] + d[3]);
+      *reinterpret_cast<f4*>(&zt[buf][jj][4 * c4]) = d;
+    }
+#pragma unroll
+    for (int i = 0; i < NHL; ++i) {
+      const int e = tid + 256 * i;
+      if (e < NH4) {
+        const int rr = e / (HF / 4), cc = e % (HF / 4);
+        *reinterpret_cast<f4*>(&hs[buf][rr][4 * cc]) = hp[i];
+      }
+    }
+  };
+  f16v acc[NCT];
+#pragma unroll
+  for (int ct = 0; ct < NCT; ++ct) acc[ct] = f16v{};
+  const int nch = (B + BC - 1) / BC;
+  load(0);
+  store(0, 0);
+  __syncthreads();
+  int cur = 0;
+  for (int c = 0; c < nch; ++c) {
+    const bool more = c + 1 < nch;
+    if (more) load((c + 1) * BC);
+    const float* za = &zt[cur][32 * w + l32][half * (BC / 2)];
+#pragma unroll
+    for (int s = 0; s < BC / 2; s += 4) {
+      f4 av = *reinterpret_cast<const f4*>(za + s);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int bb = half * (BC / 2) + s + q;
+#pragma unroll
+        for (int ct = 0; ct < NCT; ++ct) {
+          const float hv = (HF >= 32 || l32 < HF) ? hs[cur][bb][ct * 32 + l32] : 0.f;
+          acc[ct] = mfma32(av[q], hv, acc[ct]);
+        }
+      }
+    }
+    if (more) store(cur ^ 1, (c + 1) * BC);
+    __syncthreads();
+    cur ^= 1;
+  }
+  // db: the 8 lanes sharing a row (consecutive tid) reduce their partials
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    float v = dbp[i];
+    v += __shfl_xor(v, 1);
+    v += __shfl_xor(v, 2);
+    v += __shfl_xor(v, 4);
+    dbp[i] = v;
+  }
+  if (c4 == 0) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int j = j0 + jr0 + 32 * i;
+      if (j >= A) continue;
+      if (db_out) {
+        db_out[j] = dbp[i];
+      } else {
+        float p = bias[j], m = mb[j], v = vb[j];
+        adam_elem(p, m, v, dbp[i], args);
+        bias[j] = p;
+        mb[j] = m;
+        vb[j] = v;
+      }
+    }
+  }
+#pragma unroll
+  for (int ct = 0; ct < NCT; ++ct) {
+    const int cc = ct * 32 + l32;
+    if (cc >= HF) continue;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int j = j0 + 32 * w + acc32_row(r, half);
+      if (j >= A) continue;
+      const int64_t o = (int64_t)j * HF + cc;
+      if (dW_out) {
+        dW_out[o] = acc[ct][r];
+      } else {
+        float p = W[o], m = mW[o], v = vW[o];
+        adam_elem(p, m, v, acc[ct][r], args);
+        W[o] = p;
+        mW[o] = m;
+        vW[o] = v;
+      }
+    }
+  }
+}
+
+extern "C" int rg_head_dw_adam(const float* ZT, int64_t ldz, const float* lse, const int64_t* tgt, float gscale,
+                               const float* h, int B, int A, int HF, float* W, float* mW, float* vW, float* bias,
+                               float* mb, float* vb, const float* adam6, float* dW_out, float* db_out,
+                               hipStream_t stream) {
+  if (B <= 0 || A <= 0) return RG_ERR_ARG;
+  if (ldz < ((B + 3) / 4) * 4) return RG_ERR_ARG;
+  if (!dW_out && !adam6) return RG_ERR_ARG;
+  AdamArgs a{};
+  if (adam6) a = AdamArgs{adam6[0], adam6[1], adam6[2], adam6[3], adam6[4], adam6[5]};
+  dim3 grid((A + 127) / 128);
+#define WL(HFV)                                                                                                 \
+  hipLaunchKernelGGL(k_head_dw_adam<HFV>, grid, dim3(256), 0, stream, ZT, ldz, lse, tgt, gscale, h, B, A, W, mW, \
+                     vW, bias, mb, vb, a, dW_out, db_out)
+  switch (HF) {
+    case 16: WL(16); break;
+    case 32: WL(32); break;
+    case 64: WL(64); break;
+    case 128: WL(128); break;
+    case 256: WL(256); break;
+    default: return RG_ERR_SHAPE;
+  }
+#undef WL
+  RG_LAUNCH_CHECK();
+  return RG_OK;
+}

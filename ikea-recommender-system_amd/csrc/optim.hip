@@ -1,0 +1,135 @@
+// Dense Adam sweeps.
+//
+// Reference: torch.optim.Adam over every parameter, dense gradients
+// (GRU4Rec/model.py:124-127,149-153; sqn_gru.py:173-181,248-252).  The
+// embedding and Q-head tables receive row-sparse gradients, but the reference
+// materialises them densely, so every row's moments decay and every row with
+// non-zero m moves.  k_adam_rows reproduces that exactly without a dense
+// gradient tensor: rows tagged with this step's epoch read their gradient
+// from the (kept-zero) accumulation table and clear it; every other row takes
+// g = 0.  28 B/param of HBM traffic (p, m, v read+write, tag / gradient rows
+// only where touched).
+#include "common.h"
+
+static inline AdamArgs to_args(const float* a6) { return AdamArgs{a6[0], a6[1], a6[2], a6[3], a6[4], a6[5]}; }
+
+__global__ void k_adam_dense(float* __restrict__ P, float* __restrict__ M, float* __restrict__ V,
+                             float* __restrict__ G, int64_t n, AdamArgs a, int zero_grad) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    float p = P[i], m = M[i], v = V[i];
+    adam_elem(p, m, v, G[i], a);
+    P[i] = p;
+    M[i] = m;
+    V[i] = v;
+    if (zero_grad) G[i] = 0.f;
+  }
+}
+
+extern "C" int rg_adam_dense(float* P, float* M, float* V, float* G, int64_t n, const float* adam6, int zero_grad,
+                             hipStream_t stream) {
+  if (n <= 0) return RG_ERR_ARG;
+  int blocks = (int)((n + 255) / 256);
+  if (blocks > 16384) blocks = 16384;
+  hipLaunchKernelGGL(k_adam_dense, dim3(blocks), dim3(256), 0, stream, P, M, V, G, n, to_args(adam6), zero_grad);
+  RG_LAUNCH_CHECK();
+  return RG_OK;
+}
+
+// Row-sparse-gradient dense Adam.  cols % 4 == 0: one float4 per thread.
+__global__ void k_adam_rows4(float* __restrict__ P, float* __restrict__ M, float* __restrict__ V,
+                             float* __restrict__ G, const int32_t* __restrict__ tags, int32_t tag, int64_t rows,
+                             int cols, AdamArgs a) {
+  const int c4n = cols >> 2;
+  const int64_t n4 = rows * c4n;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t row = i / c4n;
+    const bool hit = tags[row] == tag;
+    f4 p = reinterpret_cast<f4*>(P)[i];
+    f4 m = reinterpret_cast<f4*>(M)[i];
+    f4 v = reinterpret_cast<f4*>(V)[i];
+    f4 g = {0.f, 0.f, 0.f, 0.f};
+    if (hit) {
+      g = reinterpret_cast<f4*>(G)[i];
+      reinterpret_cast<f4*>(G)[i] = f4{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      float pq = p[q], mq = m[q], vq = v[q];
+      adam_elem(pq, mq, vq, g[q], a);
+      p[q] = pq;
+      m[q] = mq;
+      v[q] = vq;
+    }
+    reinterpret_cast<f4*>(P)[i] = p;
+    reinterpret_cast<f4*>(M)[i] = m;
+    reinterpret_cast<f4*>(V)[i] = v;
+  }
+}
+
+__global__ void k_adam_rows1(float* __restrict__ P, float* __restrict__ M, float* __restrict__ V,
+                             float* __restrict__ G, const int32_t* __restrict__ tags, int32_t tag, int64_t rows,
+                             int cols, AdamArgs a) {
+  const int64_t n = rows * cols;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t row = i / cols;
+    float g = 0.f;
+    if (tags[row] == tag) {
+      g = G[i];
+      G[i] = 0.f;
+    }
+    float p = P[i], m = M[i], v = V[i];
+    adam_elem(p, m, v, g, a);
+    P[i] = p;
+    M[i] = m;
+    V[i] = v;
+  }
+}
+
+extern "C" int rg_adam_rows(float* P, float* M, float* V, float* G, const int32_t* tags, int32_t tag, int64_t rows,
+                            int cols, const float* adam6, hipStream_t stream) {
+  if (rows <= 0 || cols <= 0) return RG_ERR_ARG;
+  const int64_t n = (cols % 4 == 0) ? rows * (cols / 4) : rows * cols;
+  int blocks = (int)((n + 255) / 256);
+  if (blocks > 32768) blocks = 32768;
+  if (cols % 4 == 0)
+    hipLaunchKernelGGL(k_adam_rows4, dim3(blocks), dim3(256), 0, stream, P, M, V, G, tags, tag, rows, cols,
+                       to_args(adam6));
+  else
+    hipLaunchKernelGGL(k_adam_rows1, dim3(blocks), dim3(256), 0, stream, P, M, V, G, tags, tag, rows, cols,
+                       to_args(adam6));
+  RG_LAUNCH_CHECK();
+  return RG_OK;
+}
+
+// Fused slab reduction (split-K weight gradients) + Adam; optional extra
+// gradient term (e.g. bias column sums) added in slab order first.
+__global__ void k_adam_slabs(float* __restrict__ P, float* __restrict__ M, float* __restrict__ V,
+                             const float* __restrict__ slabs, int nslab, int64_t n, AdamArgs a,
+                             float* __restrict__ g_out) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    float g = 0.f;
+    for (int z = 0; z < nslab; ++z) g += slabs[(int64_t)z * n + i];
+    if (g_out) {
+      g_out[i] = g;
+      continue;
+    }
+    float p = P[i], m = M[i], v = V[i];
+    adam_elem(p, m, v, g, a);
+    P[i] = p;
+    M[i] = m;
+    V[i] = v;
+  }
+}
+
+extern "C" int rg_adam_slabs(float* P, float* M, float* V, const float* slabs, int nslab, int64_t n,
+                             const float* adam6, float* g_out, hipStream_t stream) {
+  if (n <= 0 || nslab <= 0) return RG_ERR_ARG;
+  AdamArgs a{};
+  if (adam6) a = to_args(adam6);
+  else if (!g_out) return RG_ERR_ARG;
+  int blocks = (int)((n + 255) / 256);
+  if (blocks > 8192) blocks = 8192;
+  hipLaunchKernelGGL(k_adam_slabs, dim3(blocks), dim3(256), 0, stream, P, M, V, slabs, nslab, n, a, g_out);
+  RG_LAUNCH_CHECK();
+  return RG_OK;
+}

@@ -1,0 +1,182 @@
+// Ragged packing and item-embedding gather / scatter (A3).
+//
+// Reference: recommenders/models/GRU4Rec/model.py:68-74 —
+//   emb = nn.Embedding(s); pack_padded_sequence(emb, lengths, enforce_sorted=False)
+// The reference sorts on the host and materialises (B, L, E) embeddings incl.
+// pads.  Here: one device pass sorts rows by length (descending, stable), writes
+// CSR offsets over the sorted rows, and the gather writes only the T valid
+// tokens as a packed (T, E) fp32 matrix plus their int32 item ids.
+#include "common.h"
+
+// ---------------------------------------------------------------- pack -----
+// One workgroup of 1024 threads.  lens (int64, B) are clamped to [1, L] (the
+// host shim validates CPU lengths like pack_padded_sequence does).  With
+// unpacked=1 every row runs all L steps (GRU4Rec/model.py:73-74: the
+// unpacked GRU consumes pads and returns the state after step L).
+// Outputs: perm[r] = original row of sorted row r, lsort[r], offs[r] (r<=B).
+#define PACK_THREADS 1024
+#define PACK_MAXL 512
+__global__ __launch_bounds__(PACK_THREADS) void k_pack(const int64_t* __restrict__ lens, int B, int L,
+                                                       int unpacked, int32_t* __restrict__ perm,
+                                                       int32_t* __restrict__ lsort,
+                                                       int32_t* __restrict__ offs) {
+  __shared__ int cnt[PACK_MAXL + 1];
+  __shared__ int start[PACK_MAXL + 2];
+  __shared__ int chunk_len[PACK_THREADS];
+  __shared__ int scan[PACK_THREADS];
+  __shared__ int carry;
+  const int tid = threadIdx.x;
+  for (int v = tid; v <= PACK_MAXL; v += PACK_THREADS) cnt[v] = 0;
+  __syncthreads();
+  for (int b = tid; b < B; b += PACK_THREADS) {
+    int l = unpacked ? L : (int)lens[b];
+    l = l < 1 ? 1 : (l > L ? L : l);
+    atomicAdd(&cnt[l], 1);
+  }
+  __syncthreads();
+  if (tid == 0) {
+    int acc = 0;
+    for (int v = L; v >= 1; --v) {  // descending length order
+      start[v] = acc;
+      acc += cnt[v];
+    }
+  }
+  __syncthreads();
+  // stable rank within each length bin, chunk by chunk
+  for (int c0 = 0; c0 < B; c0 += PACK_THREADS) {
+    int b = c0 + tid;
+    int l = 0;
+    if (b < B) {
+      l = unpacked ? L : (int)lens[b];
+      l = l < 1 ? 1 : (l > L ? L : l);
+    }
+    chunk_len[tid] = (b < B) ? l : -1;
+    __syncthreads();
+    if (b < B) {
+      int before = 0;
+      for (int j = 0; j < tid; ++j) before += (chunk_len[j] == l);
+      int r = start[l] + before;
+      perm[r] = b;
+      lsort[r] = l;
+    }
+    __syncthreads();
+    // advance bin starts by this chunk's counts
+    if (tid <= L && tid >= 1) {
+      int add = 0;
+      int n = min(PACK_THREADS, B - c0);
+      for (int j = 0; j < n; ++j) add += (chunk_len[j] == tid);
+      start[tid] += add;
+    }
+    __syncthreads();
+  }
+  // exclusive scan of lsort -> offs (offs[B] = T)
+  if (tid == 0) carry = 0;
+  __syncthreads();
+  for (int c0 = 0; c0 < B; c0 += PACK_THREADS) {
+    int r = c0 + tid;
+    int v = (r < B) ? lsort[r] : 0;
+    scan[tid] = v;
+    __syncthreads();
+    for (int d = 1; d < PACK_THREADS; d <<= 1) {
+      int x = (tid >= d) ? scan[tid - d] : 0;
+      __syncthreads();
+      scan[tid] += x;
+      __syncthreads();
+    }
+    if (r < B) offs[r] = carry + scan[tid] - v;
+    __syncthreads();
+    if (tid == PACK_THREADS - 1) carry += scan[tid];
+    __syncthreads();
+  }
+  if (tid == 0) offs[B] = carry;
+}
+
+extern "C" int rg_pack(const int64_t* lens, int B, int L, int unpacked, int32_t* perm, int32_t* lsort,
+                       int32_t* offs, hipStream_t stream) {
+  if (B <= 0 || L <= 0 || L > PACK_MAXL) return RG_ERR_ARG;
+  hipLaunchKernelGGL(k_pack, dim3(1), dim3(PACK_THREADS), 0, stream, lens, B, L, unpacked, perm, lsort,
+                     offs);
+  RG_LAUNCH_CHECK();
+  return RG_OK;
+}
+
+// -------------------------------------------------------------- gather -----
+// One workgroup per sorted row r; token (r, t) lives at offs[r] + t.
+// reverse=1 stores the row's tokens in reverse time order (the backward
+// direction of the bidirectional GRU reads its valid prefix back to front).
+// E is a multiple of 4: one float4 per lane, a 512-B row per 32 lanes (E=128).
+__global__ __launch_bounds__(256) void k_gather(const int64_t* __restrict__ s, int L,
+                                                const int32_t* __restrict__ perm,
+                                                const int32_t* __restrict__ lsort,
+                                                const int32_t* __restrict__ offs,
+                                                const float* __restrict__ emb, int E, int reverse,
+                                                int32_t* __restrict__ tok_id, float* __restrict__ X) {
+  const int r = blockIdx.x;
+  const int b = perm[r];
+  const int len = lsort[r];
+  const int base = offs[r];
+  const int v4 = E >> 2;
+  const int total = len * v4;
+  for (int e = threadIdx.x; e < total; e += blockDim.x) {
+    int t = e / v4;
+    int c = e - t * v4;
+    int64_t id = s[(int64_t)b * L + (reverse ? len - 1 - t : t)];
+    int tok = base + t;
+    const f4 val = reinterpret_cast<const f4*>(emb + id * E)[c];
+    reinterpret_cast<f4*>(X + (int64_t)tok * E)[c] = val;
+    if (c == 0) tok_id[tok] = (int32_t)id;
+  }
+}
+
+extern "C" int rg_gather(const int64_t* s, int B, int L, const int32_t* perm, const int32_t* lsort,
+                         const int32_t* offs, const float* emb, int E, int reverse, int32_t* tok_id,
+                         float* X, hipStream_t stream) {
+  if (B <= 0 || (E & 3)) return RG_ERR_ARG;
+  hipLaunchKernelGGL(k_gather, dim3(B), dim3(256), 0, stream, s, L, perm, lsort, offs, emb, E, reverse, tok_id, X);
+  RG_LAUNCH_CHECK();
+  return RG_OK;
+}
+
+// ------------------------------------------------------- scatter-add ----
+// dEmb[tok_id[t]] += dX[t] into a dense gradient table that is kept at zero
+// between steps, and tag touched rows with this step's epoch (the row-sparse
+// Adam sweep reads and clears the gradient of tagged rows).  skip_id (>= 0) is the non-trainable padding row (nn.Embedding
+// padding_idx: its gradient is identically zero).
+__global__ __launch_bounds__(256) void k_scatter_add(const int32_t* __restrict__ tok_id,
+                                                     const float* __restrict__ dX, int E,
+                                                     const int32_t* __restrict__ ntok_ptr,
+                                                     int skip_id, float* __restrict__ G,
+                                                     int32_t* __restrict__ tags, int32_t tag) {
+  const int T = *ntok_ptr;
+  const int per_block = blockDim.x / (E >> 2) > 0 ? blockDim.x / (E >> 2) : 1;
+  const int v4 = E >> 2;
+  for (int t0 = blockIdx.x * per_block; t0 < T; t0 += gridDim.x * per_block) {
+    int t = t0 + threadIdx.x / v4;
+    int c = threadIdx.x % v4;
+    if (threadIdx.x / v4 >= per_block || t >= T) continue;
+    int id = tok_id[t];
+    if (id == skip_id) continue;
+    f4 g = reinterpret_cast<const f4*>(dX + (int64_t)t * E)[c];
+    float* dst = G + (int64_t)id * E + 4 * c;
+    atomicAdd(dst + 0, g.x);
+    atomicAdd(dst + 1, g.y);
+    atomicAdd(dst + 2, g.z);
+    atomicAdd(dst + 3, g.w);
+    if (c == 0) tags[id] = tag;
+  }
+}
+
+extern "C" int rg_scatter_add(const int32_t* tok_id, const float* dX, int E, const int32_t* ntok_ptr,
+                              int max_tokens, int skip_id, float* G, int32_t* tags, int32_t tag,
+                              hipStream_t stream) {
+  if ((E & 3) || E > 1024) return RG_ERR_ARG;
+  int per_block = 256 / (E / 4);
+  if (per_block < 1) per_block = 1;
+  int blocks = (max_tokens + per_block - 1) / per_block;
+  if (blocks > 4096) blocks = 4096;
+  if (blocks < 1) blocks = 1;
+  hipLaunchKernelGGL(k_scatter_add, dim3(blocks), dim3(256), 0, stream, tok_id, dX, E, ntok_ptr, skip_id,
+                     G, tags, tag);
+  RG_LAUNCH_CHECK();
+  return RG_OK;
+}

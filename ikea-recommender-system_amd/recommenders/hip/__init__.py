@@ -1,0 +1,106 @@
+"""ctypes binding of the gfx950 C-ABI library (include/ikea_rec_hip.h).
+
+This is the only route to compute in the package: there is no CPU or
+PyTorch fallback.  If the library is missing, or no MI355X is visible, the
+trainers raise instead of silently running something else.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import torch
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libikea_rec_hip.so")
+
+P = C.c_void_p
+I = C.c_int
+I64 = C.c_int64
+F = C.c_float
+D = C.c_double
+I32 = C.c_int32
+
+# name -> argtypes (restype int for all)
+SIGNATURES = {
+    "rg_abi_version": [],
+    "rg_pack": [P, I, I, I, P, P, P, P],
+    "rg_gather": [P, I, I, P, P, P, P, I, I, P, P, P],
+    "rg_scatter_add": [P, P, I, P, I, I, P, P, I32, P],
+    "rg_gemm_f32": [P, I64, I64, P, I64, I64, P, I64, P, I, P, I, I, P, I, P],
+    "rg_reduce_slabs": [P, I, I64, P, P, I, I, P],
+    "rg_colsum": [P, I, I, P, I, P, P],
+    "rg_gru_fwd": [P, P, P, P, P, P, I, I, P, I, I, P, I64, P],
+    "rg_gru_bwd": [P, I64, P, P, P, P, I, I, P, I, I, P, P, P],
+    "rg_head_fwd": [P, P, P, I, I, I, P, I64, P, P, P, I, P],
+    "rg_lse_combine": [P, P, P, I, I, P, P, I64, P, P, P, P, P],
+    "rg_sum_scale": [P, I, F, P, P, P],
+    "rg_head_dh": [P, I64, P, P, F, P, I, I, I, I, P, P],
+    "rg_head_dw_adam": [P, I64, P, P, F, P, I, I, I, P, P, P, P, P, P, P, P, P, P],
+    "rg_adam_dense": [P, P, P, P, I64, P, I, P],
+    "rg_adam_rows": [P, P, P, P, P, I32, I64, I, P, P],
+    "rg_adam_slabs": [P, P, P, P, I, I64, P, P, P],
+    "rg_q_gather": [P, I, P, P, I, P, P, I, P, P],
+    "rg_q_backward": [P, I, P, P, P, P, I, P, I, P, P, I32, P],
+    "rg_sqn_td": [P, P, P, P, F, I, D, P, P, P],
+    "rg_smorl_td": [P, P, P, P, P, I, F, F, I, P, P, P],
+    "rg_sum64": [P, I, D, P, P, P],
+    "rg_diversity": [P, I, P, I, P, I, P, I, F, I, P, P],
+    "rg_novelty": [P, I, P, F, I, P, P],
+    "rg_mask_scale": [P, P, F, I64, P, P],
+    "rg_weighted_sum": [P, P, I, I64, P, P],
+}
+
+_lib = None
+
+
+def load_library(path: str = LIB_PATH):
+    """Load the .so and type every exported entry point (works without a GPU)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise RuntimeError(
+            f"MI355X kernel library not built: {path} (run ikea-recommender-system_amd/build.py)")
+    lib = C.CDLL(path)
+    for name, argtypes in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.argtypes = argtypes
+        fn.restype = C.c_int
+    _lib = lib
+    return lib
+
+
+def require_gpu(device) -> torch.device:
+    dev = torch.device(device)
+    if dev.type != "cuda" or not torch.cuda.is_available():
+        raise RuntimeError(
+            "the GRU4Rec/SQN/SMORL step path runs only on an MI355X (HIP device); "
+            f"got device={device!r}, torch.cuda.is_available()={torch.cuda.is_available()}")
+    load_library()
+    return dev
+
+
+def stream_ptr(device=None) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def ptr(t) -> int | None:
+    return None if t is None else t.data_ptr()
+
+
+def call(name: str, *args) -> int:
+    lib = load_library()
+    rc = getattr(lib, name)(*args)
+    if rc < 0:
+        raise RuntimeError(f"{name} failed with status {rc}")
+    return rc
+
+
+def host_ptr_array(tensors):
+    """HOST array of device pointers (for the multi-head entry points)."""
+    arr = (C.c_void_p * len(tensors))(*[t.data_ptr() for t in tensors])
+    return arr
+
+
+def host_floats(vals):
+    return (C.c_float * len(vals))(*[float(v) for v in vals])

@@ -1,0 +1,344 @@
+"""Host orchestration of one training step on the MI355X (Python on
+PyTorch-ROCm; every FLOP runs in the HIP kernels of csrc/ via the C ABI).
+
+PyTorch is used for device memory (parameters, Adam moments, workspaces are
+torch tensors), streams and one-time CPU initialisation; nothing here
+computes the step with torch ops.
+
+Objects
+-------
+Param        p / m / v fp32 device tensors of one reference parameter.
+AdamClock    per-optimizer step counter -> the six fp32 scalars the kernels
+             need, rounded like torch's CPU Adam sees them.
+Trunk        embedding + GRU (layer 0; optional reverse direction) — the
+             SURVEY §8 rows A3/A4/A5 — forward, BPTT, gradient reductions and
+             the Adam sweeps of its parameters.
+SoftmaxHead  full-softmax Linear + CE (A6/A7) with fused dW+Adam (A8).
+LinearHead   a Linear(H→A) used only through row gathers / argmax (Q heads).
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+import torch
+
+from . import call, host_floats, host_ptr_array, ptr, stream_ptr
+
+
+def _f32(x: float) -> float:
+    return float(np.float32(x))
+
+
+# --------------------------------------------------------------- params ----
+class Param:
+    __slots__ = ("name", "p", "m", "v")
+
+    def __init__(self, name, cpu_tensor, device):
+        self.name = name
+        self.p = cpu_tensor.to(device=device, dtype=torch.float32).contiguous()
+        self.m = torch.zeros_like(self.p)
+        self.v = torch.zeros_like(self.p)
+
+    def numel(self):
+        return self.p.numel()
+
+
+class AdamClock:
+    """torch.optim.Adam hyper-parameters + step counter (GRU4Rec/model.py:124-127)."""
+
+    def __init__(self, lr, betas=(0.9, 0.999), eps=1e-8):
+        self.lr, self.b1, self.b2, self.eps = float(lr), betas[0], betas[1], eps
+        self.t = 0
+
+    def next_args(self):
+        self.t += 1
+        t = float(self.t)
+        bc1 = 1 - self.b1 ** t
+        bc2 = 1 - self.b2 ** t
+        step_size = self.lr / bc1
+        bc2_sqrt = bc2 ** 0.5
+        return host_floats([_f32(1 - self.b1), _f32(self.b2), _f32(1 - self.b2), _f32(bc2_sqrt),
+                            _f32(self.eps), _f32(-step_size)])
+
+    def state(self):
+        return {"step": self.t, "lr": self.lr, "betas": (self.b1, self.b2), "eps": self.eps}
+
+
+# --------------------------------------------------------- reference init ---
+# RNG consumption order = the reference's module construction order after
+# torch.manual_seed(torch_rand_seed) (GRU4Rec/model.py:103-104).
+
+def init_embedding(n_rows, dim, pad, train_pad):
+    w = torch.empty(n_rows, dim)
+    torch.nn.init.normal_(w)                     # nn.Embedding.reset_parameters
+    if not train_pad:
+        with torch.no_grad():
+            w[pad].fill_(0)
+    w.normal_(mean=0, std=0.01)                  # GRU4Rec/model.py:42
+    if not train_pad:
+        with torch.no_grad():
+            w[pad] = torch.zeros(dim)            # :45-47
+    return w
+
+
+def init_gru(input_size, hidden, layers, bidir):
+    """nn.GRU.reset_parameters: U(-1/sqrt(H), 1/sqrt(H)) over parameters in
+    registration order (l0: w_ih, w_hh, b_ih, b_hh, [l0_reverse ...], l1 ...)."""
+    stdv = 1.0 / math.sqrt(hidden)
+    out = []
+    ndir = 2 if bidir else 1
+    for layer in range(layers):
+        in_sz = input_size if layer == 0 else hidden * ndir
+        for d in range(ndir):
+            sfx = f"_l{layer}" + ("_reverse" if d == 1 else "")
+            shapes = [("weight_ih" + sfx, (3 * hidden, in_sz)), ("weight_hh" + sfx, (3 * hidden, hidden)),
+                      ("bias_ih" + sfx, (3 * hidden,)), ("bias_hh" + sfx, (3 * hidden,))]
+            for name, shp in shapes:
+                out.append((name, torch.empty(shp)))
+    for _, t in out:
+        torch.nn.init.uniform_(t, -stdv, stdv)
+    return out
+
+
+def init_linear(in_f, out_f):
+    """nn.Linear.reset_parameters: kaiming_uniform_(a=sqrt(5)) + U(-1/sqrt(in), 1/sqrt(in))."""
+    w = torch.empty(out_f, in_f)
+    torch.nn.init.kaiming_uniform_(w, a=math.sqrt(5))
+    b = torch.empty(out_f)
+    bound = 1 / math.sqrt(in_f) if in_f > 0 else 0
+    torch.nn.init.uniform_(b, -bound, bound)
+    return w, b
+
+
+def _round_up(x, m):
+    return (x + m - 1) // m * m
+
+
+# ---------------------------------------------------------------- trunk ----
+class _TrunkWS:
+    """Workspace of one trunk pass for a (B, L) batch shape."""
+
+    def __init__(self, B, L, E, H, ndir, save, device):
+        TM = B * L  # token upper bound (T is only known on the device)
+        z = lambda *s, dt=torch.float32: torch.empty(*s, dtype=dt, device=device)
+        self.B, self.L, self.TM = B, L, TM
+        self.lens = z(B, dt=torch.int64)
+        self.perm = z(B, dt=torch.int32)
+        self.lsort = z(B, dt=torch.int32)
+        self.offs = z(B + 1, dt=torch.int32)
+        self.tok_id = [z(TM, dt=torch.int32) for _ in range(ndir)]
+        self.X = [z(TM, E) for _ in range(ndir)]
+        self.Gi = [z(TM, 3 * H) for _ in range(ndir)]
+        self.h = torch.zeros(B, ndir * H, device=device)
+        self.plane = TM * H
+        self.saved = [z(5, TM, H) for _ in range(ndir)] if save else None
+        if save:
+            self.dGi = [z(TM, 3 * H) for _ in range(ndir)]
+            self.dGh = [z(TM, 3 * H) for _ in range(ndir)]
+            self.dX = [z(TM, E) for _ in range(ndir)]
+            self.splits = int(min(64, max(1, TM // 2048)))
+            S = self.splits
+            self.sl_ih = z(S, 3 * H, E)
+            self.sl_hh = z(S, 3 * H, H)
+            self.cs_ih = z(S, 3 * H)
+            self.cs_hh = z(S, 3 * H)
+
+    @property
+    def ntok_ptr(self):
+        return self.offs.data_ptr() + 4 * self.B  # &offs[B] = T
+
+
+class Trunk:
+    """Item embedding + GRU trunk.  Only layer 0 feeds the heads (h[0] quirk,
+    GRU4Rec/model.py:77); deeper layers are initialised for RNG / state_dict
+    parity but are mathematically inert (zero gradient => Adam leaves them
+    unchanged), so they are not computed."""
+
+    def __init__(self, gru_attr, item_num, E, H, layers, train_pad_embed, packed, pad_idx, bidir, device):
+        self.gru_attr = gru_attr
+        self.N1 = item_num + 1
+        self.E, self.H, self.layers, self.bidir = E, H, layers, bidir
+        self.ndir = 2 if bidir else 1
+        self.packed = packed
+        self.pad = pad_idx
+        self.train_pad = train_pad_embed
+        self.device = device
+        if E % 4 or H not in (16, 32, 64, 128):
+            raise RuntimeError(f"unsupported trunk shape E={E} H={H} (E % 4 == 0, H in 16/32/64/128)")
+        self.emb = Param("embedding.weight", init_embedding(self.N1, E, pad_idx, train_pad_embed), device)
+        gru = init_gru(E, H, layers, bidir)
+        self.gru_params = [Param(f"{gru_attr}.{n}", t, device) for n, t in gru]
+        per = 4
+        self.dirs = [self.gru_params[d * per:(d + 1) * per] for d in range(self.ndir)]  # layer 0
+        self.G_emb = torch.zeros_like(self.emb.p)
+        self.tags = torch.zeros(self.N1, dtype=torch.int32, device=device)
+        self._ws = {}
+
+    # parameters in reference registration order
+    def named_params(self):
+        return [self.emb] + self.gru_params
+
+    def ws(self, slot, B, L, save):
+        key = (slot, B, L, save)
+        w = self._ws.get(key)
+        if w is None:
+            # keep one shape per slot (drop stale shapes, e.g. a short last batch)
+            for k in [k for k in self._ws if k[0] == slot]:
+                del self._ws[k]
+            w = _TrunkWS(B, L, self.E, self.H, self.ndir, save, self.device)
+            self._ws[key] = w
+        return w
+
+    def forward(self, s, lens, slot="main", save=False):
+        """s: int64 (B, L) device; lens: int64 (B,) device or CPU. Returns h (B, ndir*H)."""
+        B, L = s.shape
+        w = self.ws(slot, B, L, save)
+        st = stream_ptr()
+        if lens.device.type == "cpu":
+            w.lens.copy_(lens, non_blocking=False)
+        else:
+            w.lens.copy_(lens)
+        call("rg_pack", w.lens.data_ptr(), B, L, 0 if self.packed else 1, w.perm.data_ptr(), w.lsort.data_ptr(),
+             w.offs.data_ptr(), st)
+        H, E = self.H, self.E
+        for d in range(self.ndir):
+            w_ih, w_hh, b_ih, b_hh = self.dirs[d]
+            call("rg_gather", s.data_ptr(), B, L, w.perm.data_ptr(), w.lsort.data_ptr(), w.offs.data_ptr(),
+                 self.emb.p.data_ptr(), E, d, w.tok_id[d].data_ptr(), w.X[d].data_ptr(), st)
+            call("rg_gemm_f32", w.X[d].data_ptr(), E, 1, w_ih.p.data_ptr(), 1, E, w.Gi[d].data_ptr(), 3 * H,
+                 b_ih.p.data_ptr(), w.TM, w.ntok_ptr, 3 * H, E, None, 1, st)
+            call("rg_gru_fwd", w.Gi[d].data_ptr(), w_hh.p.data_ptr(), b_hh.p.data_ptr(), w.perm.data_ptr(),
+                 w.lsort.data_ptr(), w.offs.data_ptr(), B, H, w.h.data_ptr(), self.ndir * H, d * H,
+                 w.saved[d].data_ptr() if save else None, w.plane, st)
+        return w.h
+
+    def backward(self, dh, slot="main"):
+        """BPTT + gradient reductions.  dh: (B, ndir*H).  Leaves embedding grads
+        in G_emb (tagged) and GRU grads in slabs; call step() afterwards."""
+        w = next(v for k, v in self._ws.items() if k[0] == slot and k[3])
+        st = stream_ptr()
+        H, E, B, TM, S = self.H, self.E, w.B, w.TM, w.splits
+        for d in range(self.ndir):
+            w_ih, w_hh, _, _ = self.dirs[d]
+            call("rg_gru_bwd", w.saved[d].data_ptr(), w.plane, w_hh.p.data_ptr(), w.perm.data_ptr(),
+                 w.lsort.data_ptr(), w.offs.data_ptr(), B, H, dh.data_ptr(), self.ndir * H, d * H,
+                 w.dGi[d].data_ptr(), w.dGh[d].data_ptr(), st)
+        self._pending = (w, S)
+
+    def step(self, adam6, tag):
+        """Weight gradients + Adam for the trunk (after every use of the weights)."""
+        w, S = self._pending
+        st = stream_ptr()
+        H, E, TM = self.H, self.E, w.TM
+        skip = -1 if self.train_pad else self.pad
+        for d in range(self.ndir):
+            w_ih, w_hh, b_ih, b_hh = self.dirs[d]
+            # dX = dGi · W_ih  (T × E)
+            call("rg_gemm_f32", w.dGi[d].data_ptr(), 3 * H, 1, w_ih.p.data_ptr(), E, 1, w.dX[d].data_ptr(), E,
+                 None, TM, w.ntok_ptr, E, 3 * H, None, 1, st)
+            # dW_ih = dGiᵀ · X ; dW_hh = dGhᵀ · H_prev  (split over tokens)
+            call("rg_gemm_f32", w.dGi[d].data_ptr(), 1, 3 * H, w.X[d].data_ptr(), E, 1, w.sl_ih.data_ptr(), E,
+                 None, 3 * H, None, E, TM, w.ntok_ptr, S, st)
+            call("rg_gemm_f32", w.dGh[d].data_ptr(), 1, 3 * H, w.saved[d].data_ptr(), H, 1, w.sl_hh.data_ptr(),
+                 H, None, 3 * H, None, H, TM, w.ntok_ptr, S, st)
+            call("rg_colsum", w.dGi[d].data_ptr(), 3 * H, TM, w.ntok_ptr, S, w.cs_ih.data_ptr(), st)
+            call("rg_colsum", w.dGh[d].data_ptr(), 3 * H, TM, w.ntok_ptr, S, w.cs_hh.data_ptr(), st)
+            call("rg_scatter_add", w.tok_id[d].data_ptr(), w.dX[d].data_ptr(), E, w.ntok_ptr, TM, skip,
+                 self.G_emb.data_ptr(), self.tags.data_ptr(), tag, st)
+            for prm, sl in ((w_ih, w.sl_ih), (w_hh, w.sl_hh), (b_ih, w.cs_ih), (b_hh, w.cs_hh)):
+                call("rg_adam_slabs", prm.p.data_ptr(), prm.m.data_ptr(), prm.v.data_ptr(), sl.data_ptr(), S,
+                     prm.numel(), adam6, None, st)
+        call("rg_adam_rows", self.emb.p.data_ptr(), self.emb.m.data_ptr(), self.emb.v.data_ptr(),
+             self.G_emb.data_ptr(), self.tags.data_ptr(), tag, self.N1, E, adam6, st)
+        self._pending = None
+
+
+# ----------------------------------------------------------------- heads ----
+class _HeadWS:
+    def __init__(self, B, A, HF, store_z, device):
+        self.B = B
+        self.ldz = _round_up(B, 4)
+        self.nJ = (A + 127) // 128
+        z = lambda *s, dt=torch.float32: torch.empty(*s, dtype=dt, device=device)
+        self.ZT = z(A, self.ldz) if store_z else None
+        self.pmax = z(self.nJ, B)
+        self.psum = z(self.nJ, B)
+        self.parg = z(self.nJ, B, dt=torch.int32)
+        S = min(64, self.nJ)
+        self.work = z(3 * S * B)
+        self.lse = z(B)
+        self.amax = z(B, dt=torch.int32)
+        self.loss_row = z(B)
+        self.loss = torch.zeros(1, device=device)
+        self.dh_splits = 16 if A >= 16 * 4096 else max(1, A // 4096)
+        self.dh_slabs = z(self.dh_splits, B, HF) if store_z else None
+
+
+class SoftmaxHead:
+    """Linear(HF→A) + CrossEntropyLoss(mean) with fused backward/Adam."""
+
+    def __init__(self, name, A, HF, device):
+        self.name, self.A, self.HF, self.device = name, A, HF, device
+        w, b = init_linear(HF, A)
+        self.W = Param(f"{name}.weight", w, device)
+        self.b = Param(f"{name}.bias", b, device)
+        self._ws = {}
+
+    def named_params(self):
+        return [self.W, self.b]
+
+    def ws(self, slot, B, store_z):
+        key = (slot, B, store_z)
+        w = self._ws.get(key)
+        if w is None:
+            for k in [k for k in self._ws if k[0] == slot]:
+                del self._ws[k]
+            w = _HeadWS(B, self.A, self.HF, store_z, self.device)
+            self._ws[key] = w
+        return w
+
+    def logits_T(self, h, slot="eval"):
+        """Zᵀ (A × ldz) for h; returns the (B, A) logical view (no copy)."""
+        B = h.shape[0]
+        w = self.ws(slot, B, True)
+        call("rg_head_fwd", h.data_ptr(), self.W.p.data_ptr(), self.b.p.data_ptr(), B, self.A, self.HF,
+             w.ZT.data_ptr(), w.ldz, w.pmax.data_ptr(), w.psum.data_ptr(), w.parg.data_ptr(), 1, stream_ptr())
+        return w, w.ZT[:, :B].t()
+
+    def forward_loss(self, h, tgt, slot="main"):
+        """CE(mean) of Z = h·Wᵀ + b against tgt; keeps Zᵀ / lse for backward.
+        Returns the device loss tensor (1,) and the workspace."""
+        B = h.shape[0]
+        w = self.ws(slot, B, True)
+        st = stream_ptr()
+        call("rg_head_fwd", h.data_ptr(), self.W.p.data_ptr(), self.b.p.data_ptr(), B, self.A, self.HF,
+             w.ZT.data_ptr(), w.ldz, w.pmax.data_ptr(), w.psum.data_ptr(), w.parg.data_ptr(), 1, st)
+        call("rg_lse_combine", w.pmax.data_ptr(), w.psum.data_ptr(), w.parg.data_ptr(), B, w.nJ, w.work.data_ptr(),
+             w.ZT.data_ptr(), w.ldz, tgt.data_ptr(), w.lse.data_ptr(), w.amax.data_ptr(), w.loss_row.data_ptr(), st)
+        call("rg_sum_scale", w.loss_row.data_ptr(), B, _f32(1.0 / B), w.loss.data_ptr(), None, st)
+        return w.loss, w
+
+    def backward_step(self, h, tgt, dh_out, adam6, slot="main", gscale=None):
+        """dh_out (B, HF) := ∂loss/∂h (overwrites); then the fused dW/db + Adam."""
+        B = h.shape[0]
+        w = self.ws(slot, B, True)
+        st = stream_ptr()
+        g = _f32(1.0 / B) if gscale is None else gscale
+        n = call("rg_head_dh", w.ZT.data_ptr(), w.ldz, w.lse.data_ptr(), tgt.data_ptr(), g, self.W.p.data_ptr(), B,
+                 self.A, self.HF, w.dh_splits, w.dh_slabs.data_ptr(), st)
+        call("rg_reduce_slabs", w.dh_slabs.data_ptr(), n, B * self.HF, dh_out.data_ptr(), None, self.HF, 0, st)
+        call("rg_head_dw_adam", w.ZT.data_ptr(), w.ldz, w.lse.data_ptr(), tgt.data_ptr(), g, h.data_ptr(), B,
+             self.A, self.HF, self.W.p.data_ptr(), self.W.m.data_ptr(), self.W.v.data_ptr(), self.b.p.data_ptr(),
+             self.b.m.data_ptr(), self.b.v.data_ptr(), adam6, None, None, st)
+
+    def argmax(self, h, slot="argmax"):
+        """argmax_j (h·Wᵀ + b)[b, j] without storing Z (first maximum)."""
+        B = h.shape[0]
+        w = self.ws(slot, B, False)
+        st = stream_ptr()
+        call("rg_head_fwd", h.data_ptr(), self.W.p.data_ptr(), self.b.p.data_ptr(), B, self.A, self.HF, None, 0,
+             w.pmax.data_ptr(), w.psum.data_ptr(), w.parg.data_ptr(), 0, st)
+        call("rg_lse_combine", w.pmax.data_ptr(), w.psum.data_ptr(), w.parg.data_ptr(), B, w.nJ, w.work.data_ptr(),
+             None, 0, None, None, w.amax.data_ptr(), None, st)
+        return w.amax

@@ -1,0 +1,111 @@
+"""Model objects mirroring the reference nn.Modules' public surface
+(``forward(s, lengths)``, ``.action_dim`` / ``.hidden_dim`` / ``.item_num`` /
+``.state_size`` / ``.embedding_dim``, ``train()/eval()/.training``,
+``state_dict()/load_state_dict()`` with the reference key names — SURVEY §8b),
+backed by the HIP trunk and heads of engine.py.
+"""
+from __future__ import annotations
+
+from collections import OrderedDict
+
+import numpy as np
+import torch
+
+from . import call, stream_ptr
+from .engine import SoftmaxHead, Trunk
+
+
+class HipNet:
+    """Embedding + GRU trunk + linear heads, parameters on one MI355X."""
+
+    kind = "gru4rec"
+
+    def __init__(self, *, trunk_attr, head_names, hidden_dim, embedding_dim, item_num, state_size, action_dim,
+                 gru_layers, use_packed_seq, train_pad_embed, padding_idx, bidir, device, dropout=0.0):
+        self.hidden_dim = hidden_dim
+        self.embedding_dim = embedding_dim
+        self.item_num = int(item_num)
+        self.state_size = state_size
+        self.action_dim = action_dim
+        self.use_packed_seq = use_packed_seq
+        self.gru_layers = gru_layers
+        self.layers = gru_layers
+        self.device = torch.device(device)
+        self.padding_idx = self.item_num if padding_idx is None else padding_idx
+        self.dropout_p = float(dropout)
+        self.training = True
+        self.trunk = Trunk(trunk_attr, self.item_num, embedding_dim, hidden_dim, gru_layers, train_pad_embed,
+                           use_packed_seq, self.padding_idx, bidir, self.device)
+        self.hf = hidden_dim * (2 if bidir else 1)
+        self.heads = OrderedDict((n, SoftmaxHead(n, action_dim, self.hf, self.device)) for n in head_names)
+        for n, hd in self.heads.items():
+            setattr(self, n, hd)
+        self._dh = {}
+        self._hd = {}
+
+    # ------------------------------------------------------- nn.Module-ish --
+    def named_param_objs(self):
+        out = list(self.trunk.named_params())
+        for hd in self.heads.values():
+            out += hd.named_params()
+        return out
+
+    def state_dict(self):
+        return OrderedDict((p.name, p.p.detach()) for p in self.named_param_objs())
+
+    def load_state_dict(self, sd, strict=True):
+        objs = {p.name: p for p in self.named_param_objs()}
+        missing = [k for k in objs if k not in sd]
+        unexpected = [k for k in sd if k not in objs]
+        if strict and (missing or unexpected):
+            raise RuntimeError(f"state_dict mismatch: missing={missing} unexpected={unexpected}")
+        with torch.no_grad():
+            for k, v in sd.items():
+                if k in objs:
+                    objs[k].p.copy_(torch.as_tensor(v).to(objs[k].p.device, torch.float32))
+        return self
+
+    def parameters(self):
+        return [p.p for p in self.named_param_objs()]
+
+    def named_parameters(self):
+        return [(p.name, p.p) for p in self.named_param_objs()]
+
+    def train(self, mode=True):
+        self.training = mode
+        return self
+
+    def eval(self):
+        return self.train(False)
+
+    def to(self, device):
+        if torch.device(device) != self.device and not (torch.device(device).type == "cuda" and
+                                                         self.device.type == "cuda"):
+            raise RuntimeError("HIP nets live on the MI355X they were built on")
+        return self
+
+    def __call__(self, s, lengths):
+        return self.forward(s, lengths)
+
+    # ------------------------------------------------------------ helpers --
+    def dh_buffer(self, B):
+        t = self._dh.get(B)
+        if t is None:
+            self._dh = {B: torch.empty(B, self.hf, device=self.device)}
+            t = self._dh[B]
+        return t
+
+    def hidden(self, s, lengths, slot="eval", save=False):
+        s = s.to(self.device)
+        return self.trunk.forward(s, lengths, slot=slot, save=save)
+
+    def dropout_mask(self, B):
+        """Bernoulli(1-p) mask drawn from the CPU generator exactly like the
+        reference's CPU F.dropout (noise.bernoulli_(1-p).div_(1-p))."""
+        noise = torch.empty(B, self.hf).bernoulli_(1 - self.dropout_p)
+        noise.div_(1 - self.dropout_p)
+        return noise.to(self.device)
+
+    def apply_mask(self, x, mask, out):
+        call("rg_mask_scale", x.data_ptr(), mask.data_ptr(), 1.0, x.numel(), out.data_ptr(), stream_ptr())
+        return out

@@ -1,0 +1,54 @@
+"""One supervised (full-softmax CE) training step on the MI355X — the shared
+body of GRU4Rec_trainer and BidirGRU4Rec_trainer
+(GRU4Rec/model.py:129-155, BidirGRU4Rec/model.py:150-176):
+
+  pack -> gather -> W_ih GEMM -> GRU recurrence -> [dropout] -> logits + online
+  LSE -> CE loss -> dh (split-K) + fused dW/db/Adam of the head -> BPTT ->
+  dX / dW_ih / dW_hh / bias sums -> embedding scatter -> Adam sweeps.
+"""
+from __future__ import annotations
+
+import torch
+
+from .nets import HipNet
+
+
+class SupervisedNet(HipNet):
+    def forward(self, s, lengths):
+        h = self.hidden(s, lengths, slot="eval", save=False)
+        if self.training and self.dropout_p > 0:
+            mask = self.dropout_mask(h.shape[0])
+            h = self.apply_mask(h, mask, torch.empty_like(h))
+        head = next(iter(self.heads.values()))
+        _, z = head.logits_T(h, slot="eval")
+        return z
+
+
+def supervised_step(net: SupervisedNet, clock, s, a, true_len):
+    """Returns the device loss tensor (1,) — the caller does the .item()."""
+    dev = net.device
+    s = s.to(dev, non_blocking=True)
+    a = a.to(dev, non_blocking=True)
+    head = next(iter(net.heads.values()))
+    h = net.trunk.forward(s, true_len, slot="main", save=True)
+    B = h.shape[0]
+    mask = None
+    if net.training and net.dropout_p > 0:
+        mask = net.dropout_mask(B)
+        hd = net._hd.get(B)
+        if hd is None:
+            net._hd = {B: torch.empty_like(h)}
+            hd = net._hd[B]
+        h_in = net.apply_mask(h, mask, hd)
+    else:
+        h_in = h
+    loss, _ = head.forward_loss(h_in, a, slot="main")
+    adam6 = clock.next_args()
+    net.trunk_tag = getattr(net, "trunk_tag", 0) + 1
+    dh = net.dh_buffer(B)
+    head.backward_step(h_in, a, dh, adam6, slot="main")
+    if mask is not None:
+        net.apply_mask(dh, mask, dh)
+    net.trunk.backward(dh, slot="main")
+    net.trunk.step(adam6, net.trunk_tag)
+    return loss

@@ -1,0 +1,80 @@
+"""Drop-in ``GRU4Rec`` / ``GRU4Rec_trainer`` for the MI355X.
+
+Same import path, constructor signatures and methods as the reference
+(``recommenders/models/GRU4Rec/model.py:6-173``); the step runs as HIP kernels
+through the C ABI (recommenders/hip).  Reference quirks kept: final hidden is
+``h[0]`` (layer 0) for any ``gru_layers``; init RNG order = nn.Embedding,
+normal_(0, 0.01), nn.GRU, nn.Linear after ``torch.manual_seed``.
+"""
+import random
+
+import torch
+import torch.nn as nn
+
+from recommenders.hip import require_gpu
+from recommenders.hip.engine import AdamClock
+from recommenders.hip.supervised import SupervisedNet, supervised_step
+
+
+class GRU4Rec(SupervisedNet):
+    """embedding -> GRU -> h[0] -> Linear(H -> A) (reference ``:6-82``)."""
+
+    def __init__(self, hidden_size, embedding_dim, item_num, state_size, action_dim, gru_layers=1,
+                 use_packed_seq=True, train_pad_embed=True, padding_idx=None, device="cuda"):
+        super().__init__(trunk_attr="gru", head_names=["output"], hidden_dim=hidden_size,
+                         embedding_dim=embedding_dim, item_num=item_num, state_size=state_size,
+                         action_dim=action_dim, gru_layers=gru_layers, use_packed_seq=use_packed_seq,
+                         train_pad_embed=train_pad_embed, padding_idx=padding_idx, bidir=False, device=device)
+
+
+class _AdamFacade:
+    """Stands where the reference keeps its torch.optim.Adam (``:124-127``)."""
+
+    def __init__(self, clock, nets):
+        self.clock = clock
+        self.nets = nets
+        self.param_groups = [{"lr": clock.lr, "betas": (clock.b1, clock.b2), "eps": clock.eps}]
+
+    def zero_grad(self, set_to_none=True):
+        pass  # gradients never persist between steps on the HIP path
+
+    def state_dict(self):
+        st = {}
+        for net in self.nets:
+            for p in net.named_param_objs():
+                st[p.name] = {"step": self.clock.t, "exp_avg": p.m.detach(), "exp_avg_sq": p.v.detach()}
+        return {"state": st, "param_groups": self.param_groups}
+
+
+class GRU4Rec_trainer:
+    def __init__(self, hidden_dim, embedding_dim, gru_layers, train_pad_embed, use_packed_seq, learning_rate,
+                 item_num, state_size, action_dim, device, padding_idx=None, torch_rand_seed=118,
+                 python_rand_seed=999):
+        torch.manual_seed(torch_rand_seed)
+        random.seed(python_rand_seed)
+        self.device = require_gpu(device)
+        self.gru_model = GRU4Rec(hidden_size=hidden_dim, embedding_dim=embedding_dim, item_num=item_num,
+                                 state_size=state_size, action_dim=action_dim, gru_layers=gru_layers,
+                                 use_packed_seq=use_packed_seq, train_pad_embed=train_pad_embed,
+                                 padding_idx=padding_idx, device=self.device)
+        self.learning_rate = learning_rate
+        self.cross_entropy_loss = nn.CrossEntropyLoss(weight=None, reduction="mean")
+        self.clock = AdamClock(learning_rate)
+        self.optimizer = _AdamFacade(self.clock, [self.gru_model])
+
+    def train_step(self, s, a, true_len):
+        """One step on (s, a, true_len); returns the CE loss as a Python float."""
+        return supervised_step(self.gru_model, self.clock, s, a, true_len).item()
+
+    def train_step_async(self, s, a, true_len):
+        """Same step without the host sync; returns the device loss tensor."""
+        return supervised_step(self.gru_model, self.clock, s, a, true_len)
+
+    def set_train(self):
+        self.gru_model.train()
+
+    def set_eval(self):
+        self.gru_model.eval()
+
+    def send_to_device(self):
+        self.gru_model.to(self.device)

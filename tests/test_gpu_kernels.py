@@ -1,0 +1,264 @@
+"""Per-kernel GPU numerics through the C ABI, each against a plain PyTorch
+(CPU, fp64 where it matters) reference of the same op."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+dev = "cuda"
+
+
+def C():
+    from recommenders import hip
+    return hip
+
+
+def st():
+    return C().stream_ptr()
+
+
+def pack(lens, L, unpacked=0):
+    B = lens.numel()
+    perm = torch.empty(B, dtype=torch.int32, device=dev)
+    ls = torch.empty(B, dtype=torch.int32, device=dev)
+    offs = torch.empty(B + 1, dtype=torch.int32, device=dev)
+    C().call("rg_pack", lens.to(dev).data_ptr(), B, L, unpacked, perm.data_ptr(), ls.data_ptr(), offs.data_ptr(),
+             st())
+    return perm, ls, offs
+
+
+def test_pack_stable_descending():
+    g = torch.Generator().manual_seed(0)
+    for B, L in [(7, 5), (1000, 20), (4096, 50), (3000, 3)]:
+        lens = torch.randint(1, L + 1, (B,), generator=g)
+        perm, ls, offs = pack(lens, L)
+        order = np.argsort(-lens.numpy(), kind="stable")
+        assert np.array_equal(perm.cpu().numpy(), order)
+        assert np.array_equal(ls.cpu().numpy(), lens.numpy()[order])
+        assert np.array_equal(offs.cpu().numpy(), np.concatenate([[0], np.cumsum(lens.numpy()[order])]))
+        perm, ls, offs = pack(lens, L, unpacked=1)
+        assert int(offs[-1]) == B * L
+
+
+def test_gather_packed_and_reverse():
+    g = torch.Generator().manual_seed(1)
+    B, L, N, E = 33, 6, 100, 16
+    s = torch.randint(0, N + 1, (B, L), generator=g)
+    lens = torch.randint(1, L + 1, (B,), generator=g)
+    emb = torch.randn(N + 1, E, generator=g)
+    perm, ls, offs = pack(lens, L)
+    for rev in (0, 1):
+        X = torch.zeros(B * L, E, device=dev)
+        ids = torch.zeros(B * L, dtype=torch.int32, device=dev)
+        C().call("rg_gather", s.to(dev).data_ptr(), B, L, perm.data_ptr(), ls.data_ptr(), offs.data_ptr(),
+                 emb.to(dev).data_ptr(), E, rev, ids.data_ptr(), X.data_ptr(), st())
+        rows = []
+        for r in perm.cpu().tolist():
+            t = list(range(int(lens[r])))
+            if rev:
+                t = t[::-1]
+            rows += [int(s[r, i]) for i in t]
+        T = len(rows)
+        assert ids[:T].cpu().tolist() == rows
+        torch.testing.assert_close(X[:T].cpu(), emb[rows], rtol=0, atol=0)
+
+
+@pytest.mark.parametrize("M,N,K,splits", [(100, 384, 128, 1), (1000, 96, 32, 1), (384, 128, 5000, 8),
+                                          (48, 16, 37, 3)])
+def test_gemm_layouts(M, N, K, splits):
+    g = torch.Generator().manual_seed(2)
+    A = torch.randn(M, K, generator=g)
+    Bm = torch.randn(K, N, generator=g)
+    ref = (A.double() @ Bm.double()).float()
+    Ad, Bd = A.to(dev), Bm.to(dev)
+    AT, BT = A.t().contiguous().to(dev), Bm.t().contiguous().to(dev)
+    for (a, sam, sak) in ((Ad, K, 1), (AT, 1, M)):
+        for (b, sbk, sbn) in ((Bd, N, 1), (BT, 1, K)):
+            out = torch.zeros(splits, M, N, device=dev)
+            C().call("rg_gemm_f32", a.data_ptr(), sam, sak, b.data_ptr(), sbk, sbn, out.data_ptr(), N, None, M,
+                     None, N, K, None, splits, st())
+            torch.testing.assert_close(out.sum(0).cpu(), ref, rtol=1e-5, atol=1e-4)
+
+
+def gru_ref(X_rows, lens, perm_order, Wih, Whh, bih, bhh, H):
+    """fp64 GRU over each (unsorted) row; returns final h per original row and saved states."""
+    hs = {}
+    for r, xs in X_rows.items():
+        h = torch.zeros(H, dtype=torch.float64)
+        for x in xs:
+            gi = Wih @ x + bih
+            gh = Whh @ h + bhh
+            rr = torch.sigmoid(gi[:H] + gh[:H])
+            zz = torch.sigmoid(gi[H:2 * H] + gh[H:2 * H])
+            nn_ = torch.tanh(gi[2 * H:] + rr * gh[2 * H:])
+            h = (1 - zz) * nn_ + zz * h
+        hs[r] = h
+    return hs
+
+
+@pytest.mark.parametrize("H", [16, 32, 64, 128])
+def test_gru_forward_backward(H):
+    g = torch.Generator().manual_seed(3)
+    B, L, E = 37, 7, H
+    lens = torch.randint(1, L + 1, (B,), generator=g)
+    X = torch.randn(B, L, E, generator=g) * 0.5
+    k = 1 / H ** 0.5
+    Wih = (torch.rand(3 * H, E, generator=g) * 2 - 1) * k
+    Whh = (torch.rand(3 * H, H, generator=g) * 2 - 1) * k
+    bih = (torch.rand(3 * H, generator=g) * 2 - 1) * k
+    bhh = (torch.rand(3 * H, generator=g) * 2 - 1) * k
+    perm, ls, offs = pack(lens, L)
+    order = perm.cpu().tolist()
+    packed = torch.cat([X[r, :int(lens[r])] for r in order])
+    T = packed.shape[0]
+    Gi = (packed.double() @ Wih.double().t() + bih.double()).float().to(dev)
+    hout = torch.zeros(B, H, device=dev)
+    saved = torch.zeros(5, T, H, device=dev)
+    C().call("rg_gru_fwd", Gi.data_ptr(), Whh.to(dev).data_ptr(), bhh.to(dev).data_ptr(), perm.data_ptr(),
+             ls.data_ptr(), offs.data_ptr(), B, H, hout.data_ptr(), H, 0, saved.data_ptr(), T * H, st())
+    # autograd reference (float64)
+    Xd = X.double().requires_grad_(True)
+    P = [t.double().requires_grad_(True) for t in (Wih, Whh, bih, bhh)]
+    hs = []
+    for r in range(B):
+        h = torch.zeros(H, dtype=torch.float64)
+        for t in range(int(lens[r])):
+            gi = P[0] @ Xd[r, t] + P[2]
+            gh = P[1] @ h + P[3]
+            rr = torch.sigmoid(gi[:H] + gh[:H])
+            zz = torch.sigmoid(gi[H:2 * H] + gh[H:2 * H])
+            nn_ = torch.tanh(gi[2 * H:] + rr * gh[2 * H:])
+            h = (h - nn_) * zz + nn_
+        hs.append(h)
+    href = torch.stack(hs)
+    torch.testing.assert_close(hout.cpu().double(), href.detach(), rtol=0, atol=2e-6)
+    dh = torch.randn(B, H, generator=g)
+    (href * dh.double()).sum().backward()
+    dGi = torch.zeros(T, 3 * H, device=dev)
+    dGh = torch.zeros(T, 3 * H, device=dev)
+    C().call("rg_gru_bwd", saved.data_ptr(), T * H, Whh.to(dev).data_ptr(), perm.data_ptr(), ls.data_ptr(),
+             offs.data_ptr(), B, H, dh.to(dev).data_ptr(), H, 0, dGi.data_ptr(), dGh.data_ptr(), st())
+    # dX = dGi · W_ih (packed order) vs autograd
+    dX = (dGi.cpu().double() @ Wih.double())
+    ref_dX = torch.cat([Xd.grad[r, :int(lens[r])] for r in order])
+    torch.testing.assert_close(dX, ref_dX, rtol=0, atol=2e-5)
+    dWhh = dGh.cpu().double().t() @ saved[0].cpu().double()
+    torch.testing.assert_close(dWhh, P[1].grad, rtol=0, atol=5e-5)
+    torch.testing.assert_close(dGh.cpu().double().sum(0), P[3].grad, rtol=0, atol=5e-5)
+    torch.testing.assert_close(dGi.cpu().double().sum(0), P[2].grad, rtol=0, atol=5e-5)
+
+
+@pytest.mark.parametrize("B,A,HF", [(64, 1000, 16), (100, 3000, 32), (256, 5000, 64), (260, 20000, 128),
+                                    (96, 4100, 256)])
+def test_head_forward_backward(B, A, HF):
+    g = torch.Generator().manual_seed(4)
+    h = torch.randn(B, HF, generator=g) * 0.5
+    W = torch.randn(A, HF, generator=g) * 0.1
+    b = torch.randn(A, generator=g) * 0.1
+    tgt = torch.randint(0, A, (B,), generator=g)
+    hd, Wd, bd, td = h.to(dev), W.to(dev), b.to(dev), tgt.to(dev)
+    ldz = (B + 3) // 4 * 4
+    nJ = (A + 127) // 128
+    ZT = torch.zeros(A, ldz, device=dev)
+    pm = torch.zeros(nJ, B, device=dev)
+    ps = torch.zeros(nJ, B, device=dev)
+    pa = torch.zeros(nJ, B, dtype=torch.int32, device=dev)
+    C().call("rg_head_fwd", hd.data_ptr(), Wd.data_ptr(), bd.data_ptr(), B, A, HF, ZT.data_ptr(), ldz,
+             pm.data_ptr(), ps.data_ptr(), pa.data_ptr(), 1, st())
+    Zref = (h.double() @ W.double().t() + b.double())
+    torch.testing.assert_close(ZT[:, :B].t().cpu().double(), Zref, rtol=0, atol=1e-5)
+    work = torch.zeros(3 * min(64, nJ) * B, device=dev)
+    lse = torch.zeros(B, device=dev)
+    amax = torch.zeros(B, dtype=torch.int32, device=dev)
+    lrow = torch.zeros(B, device=dev)
+    C().call("rg_lse_combine", pm.data_ptr(), ps.data_ptr(), pa.data_ptr(), B, nJ, work.data_ptr(), ZT.data_ptr(),
+             ldz, td.data_ptr(), lse.data_ptr(), amax.data_ptr(), lrow.data_ptr(), st())
+    torch.testing.assert_close(lse.cpu().double(), torch.logsumexp(Zref, 1), rtol=0, atol=2e-5)
+    Zg = ZT[:, :B].t().cpu()
+    assert torch.equal(amax.cpu().long(), torch.argmax(Zg, 1))
+    ce = torch.nn.functional.cross_entropy(Zref, tgt, reduction="none")
+    torch.testing.assert_close(lrow.cpu().double(), ce, rtol=0, atol=2e-5)
+    # backward w.r.t. h, W, b (grad-only hook of the fused Adam kernel)
+    Wr = W.double().requires_grad_(True)
+    br = b.double().requires_grad_(True)
+    hr = h.double().requires_grad_(True)
+    torch.nn.functional.cross_entropy(hr @ Wr.t() + br, tgt).backward()
+    gs = float(np.float32(1.0 / B))
+    splits = 8
+    slabs = torch.zeros(splits, B, HF, device=dev)
+    n = C().call("rg_head_dh", ZT.data_ptr(), ldz, lse.data_ptr(), td.data_ptr(), gs, Wd.data_ptr(), B, A, HF,
+                 splits, slabs.data_ptr(), st())
+    torch.testing.assert_close(slabs[:n].sum(0).cpu().double(), hr.grad, rtol=0, atol=1e-6)
+    dW = torch.zeros(A, HF, device=dev)
+    db = torch.zeros(A, device=dev)
+    C().call("rg_head_dw_adam", ZT.data_ptr(), ldz, lse.data_ptr(), td.data_ptr(), gs, hd.data_ptr(), B, A, HF,
+             None, None, None, None, None, None, None, dW.data_ptr(), db.data_ptr(), st())
+    torch.testing.assert_close(dW.cpu().double(), Wr.grad, rtol=0, atol=1e-7)
+    torch.testing.assert_close(db.cpu().double(), br.grad, rtol=0, atol=1e-7)
+
+
+def test_adam_kernels_match_torch():
+    from recommenders.hip.engine import AdamClock
+    g = torch.Generator().manual_seed(5)
+    rows, cols = 300, 16
+    p0 = torch.randn(rows, cols, generator=g)
+    grads = [torch.randn(rows, cols, generator=g) for _ in range(3)]
+    touched = [torch.rand(rows, generator=g) < 0.3 for _ in range(3)]
+    pt = p0.clone().requires_grad_(True)
+    opt = torch.optim.Adam([pt], lr=0.01)
+    P = p0.to(dev)
+    M = torch.zeros_like(P)
+    V = torch.zeros_like(P)
+    G = torch.zeros_like(P)
+    tags = torch.zeros(rows, dtype=torch.int32, device=dev)
+    clock = AdamClock(0.01)
+    for i in range(3):
+        gi = grads[i] * touched[i].float().unsqueeze(1)
+        pt.grad = gi.clone()
+        opt.step()
+        G[touched[i].to(dev)] = gi[touched[i]].to(dev)
+        tags[touched[i].to(dev)] = i + 1
+        C().call("rg_adam_rows", P.data_ptr(), M.data_ptr(), V.data_ptr(), G.data_ptr(), tags.data_ptr(), i + 1,
+                 rows, cols, clock.next_args(), st())
+    torch.testing.assert_close(P.cpu(), pt.detach(), rtol=0, atol=2e-6)
+    assert float(G.abs().max()) == 0.0
+
+
+def test_q_kernels_and_rewards():
+    g = torch.Generator().manual_seed(6)
+    B, A, HF, Ed = 50, 400, 32, 8
+    h = torch.randn(B, HF, generator=g)
+    Ws = [torch.randn(A, HF, generator=g) for _ in range(3)]
+    bs = [torch.randn(A, generator=g) for _ in range(3)]
+    idx = torch.randint(0, A, (B,), generator=g)
+    hd = h.to(dev)
+    Wd = [w.to(dev) for w in Ws]
+    bd = [b.to(dev) for b in bs]
+    q = torch.zeros(B, 3, device=dev)
+    hip = C()
+    hip.call("rg_q_gather", hd.data_ptr(), HF, hip.host_ptr_array(Wd), hip.host_ptr_array(bd), 3,
+             idx.to(dev).data_ptr(), None, B, q.data_ptr(), st())
+    ref = torch.stack([(h * Ws[i][idx]).sum(1) + bs[i][idx] for i in range(3)], 1)
+    torch.testing.assert_close(q.cpu(), ref, rtol=0, atol=1e-5)
+    # diversity / novelty
+    from oracle import metrics as om
+    L = 5
+    s = torch.randint(0, A, (B, L), generator=g)
+    lens = torch.randint(1, L + 1, (B,), generator=g)
+    table = torch.randn(A + 1, Ed, generator=g)
+    preds = torch.randn(B, A, generator=g)
+    top = torch.topk(preds, 3).indices.to(torch.int32)
+    out = torch.zeros(B, device=dev)
+    hip.call("rg_diversity", s.to(dev).data_ptr(), L, lens.to(dev).data_ptr(), 1, top.to(dev).data_ptr(), 3,
+             table.to(dev).data_ptr(), Ed, 1e-6, B, out.data_ptr(), st())
+    torch.testing.assert_close(out.cpu(), om.batch_diversity_rewards(s, preds, lens, "end", 3, table), rtol=0,
+                               atol=1e-6)
+    unpop = set(range(0, A, 3))
+    bm = np.zeros((A + 31) // 32, dtype=np.uint32)
+    for j in unpop:
+        bm[j >> 5] |= np.uint32(1 << (j & 31))
+    outn = torch.zeros(B, device=dev)
+    hip.call("rg_novelty", top.to(dev).data_ptr(), 3, torch.from_numpy(bm.view(np.int32)).to(dev).data_ptr(), 2.0,
+             B, outn.data_ptr(), st())
+    np.testing.assert_allclose(outn.cpu().numpy(), om.batch_novelty_rewards(preds, unpop, 2.0, 3), atol=1e-6)
