@@ -109,8 +109,9 @@ __global__ __launch_bounds__(256) void k_gather(const int64_t* __restrict__ s, i
                                                 const int32_t* __restrict__ perm,
                                                 const int32_t* __restrict__ lsort,
                                                 const int32_t* __restrict__ offs,
-                                                const float* __restrict__ emb, int E, int reverse,
-                                                int32_t* __restrict__ tok_id, float* __restrict__ X) {
+                                                const float* __restrict__ emb, int64_t n_rows, int E,
+                                                int reverse, int32_t* __restrict__ tok_id,
+                                                float* __restrict__ X, int32_t* __restrict__ err) {
   const int r = blockIdx.x;
   const int b = perm[r];
   const int len = lsort[r];
@@ -122,17 +123,23 @@ __global__ __launch_bounds__(256) void k_gather(const int64_t* __restrict__ s, i
     int c = e - t * v4;
     int64_t id = s[(int64_t)b * L + (reverse ? len - 1 - t : t)];
     int tok = base + t;
-    const f4 val = reinterpret_cast<const f4*>(emb + id * E)[c];
+    f4 val = {0.f, 0.f, 0.f, 0.f};
+    const bool ok = id >= 0 && id < n_rows;  // nn.Embedding raises on such ids
+    if (ok) val = reinterpret_cast<const f4*>(emb + id * E)[c];
     reinterpret_cast<f4*>(X + (int64_t)tok * E)[c] = val;
-    if (c == 0) tok_id[tok] = (int32_t)id;
+    if (c == 0) {
+      tok_id[tok] = ok ? (int32_t)id : -1;
+      if (!ok && err) atomicOr(err, 1);
+    }
   }
 }
 
 extern "C" int rg_gather(const int64_t* s, int B, int L, const int32_t* perm, const int32_t* lsort,
-                         const int32_t* offs, const float* emb, int E, int reverse, int32_t* tok_id,
-                         float* X, hipStream_t stream) {
+                         const int32_t* offs, const float* emb, int64_t n_rows, int E, int reverse,
+                         int32_t* tok_id, float* X, int32_t* err, hipStream_t stream) {
   if (B <= 0 || (E & 3)) return RG_ERR_ARG;
-  hipLaunchKernelGGL(k_gather, dim3(B), dim3(256), 0, stream, s, L, perm, lsort, offs, emb, E, reverse, tok_id, X);
+  hipLaunchKernelGGL(k_gather, dim3(B), dim3(256), 0, stream, s, L, perm, lsort, offs, emb, n_rows, E, reverse,
+                     tok_id, X, err);
   RG_LAUNCH_CHECK();
   return RG_OK;
 }
@@ -155,7 +162,7 @@ __global__ __launch_bounds__(256) void k_scatter_add(const int32_t* __restrict__
     int c = threadIdx.x % v4;
     if (threadIdx.x / v4 >= per_block || t >= T) continue;
     int id = tok_id[t];
-    if (id == skip_id) continue;
+    if (id == skip_id || id < 0) continue;
     f4 g = reinterpret_cast<const f4*>(dX + (int64_t)t * E)[c];
     float* dst = G + (int64_t)id * E + 4 * c;
     atomicAdd(dst + 0, g.x);

@@ -24,7 +24,7 @@ I32 = C.c_int32
 SIGNATURES = {
     "rg_abi_version": [],
     "rg_pack": [P, I, I, I, P, P, P, P],
-    "rg_gather": [P, I, I, P, P, P, P, I, I, P, P, P],
+    "rg_gather": [P, I, I, P, P, P, P, I64, I, I, P, P, P, P],
     "rg_scatter_add": [P, P, I, P, I, I, P, P, I32, P],
     "rg_gemm_f32": [P, I64, I64, P, I64, I64, P, I64, P, I, P, I, I, P, I, P],
     "rg_reduce_slabs": [P, I, I64, P, P, I, I, P],
@@ -32,7 +32,7 @@ SIGNATURES = {
     "rg_gru_fwd": [P, P, P, P, P, P, I, I, P, I, I, P, I64, P],
     "rg_gru_bwd": [P, I64, P, P, P, P, I, I, P, I, I, P, P, P],
     "rg_head_fwd": [P, P, P, I, I, I, P, I64, P, P, P, I, P],
-    "rg_lse_combine": [P, P, P, I, I, P, P, I64, P, P, P, P, P],
+    "rg_lse_combine": [P, P, P, I, I, P, P, I64, P, I, P, P, P, P],
     "rg_sum_scale": [P, I, F, P, P, P],
     "rg_head_dh": [P, I64, P, P, F, P, I, I, I, I, P, P],
     "rg_head_dw_adam": [P, I64, P, P, F, P, I, I, I, P, P, P, P, P, P, P, P, P, P],

@@ -173,6 +173,7 @@ class Trunk:
         self.dirs = [self.gru_params[d * per:(d + 1) * per] for d in range(self.ndir)]  # layer 0
         self.G_emb = torch.zeros_like(self.emb.p)
         self.tags = torch.zeros(self.N1, dtype=torch.int32, device=device)
+        self.err = torch.zeros(1, dtype=torch.int32, device=device)  # out-of-range item ids seen
         self._ws = {}
 
     # parameters in reference registration order
@@ -205,7 +206,8 @@ class Trunk:
         for d in range(self.ndir):
             w_ih, w_hh, b_ih, b_hh = self.dirs[d]
             call("rg_gather", s.data_ptr(), B, L, w.perm.data_ptr(), w.lsort.data_ptr(), w.offs.data_ptr(),
-                 self.emb.p.data_ptr(), E, d, w.tok_id[d].data_ptr(), w.X[d].data_ptr(), st)
+                 self.emb.p.data_ptr(), self.N1, E, d, w.tok_id[d].data_ptr(), w.X[d].data_ptr(),
+                 self.err.data_ptr(), st)
             call("rg_gemm_f32", w.X[d].data_ptr(), E, 1, w_ih.p.data_ptr(), 1, E, w.Gi[d].data_ptr(), 3 * H,
                  b_ih.p.data_ptr(), w.TM, w.ntok_ptr, 3 * H, E, None, 1, st)
             call("rg_gru_fwd", w.Gi[d].data_ptr(), w_hh.p.data_ptr(), b_hh.p.data_ptr(), w.perm.data_ptr(),
@@ -315,7 +317,8 @@ class SoftmaxHead:
         call("rg_head_fwd", h.data_ptr(), self.W.p.data_ptr(), self.b.p.data_ptr(), B, self.A, self.HF,
              w.ZT.data_ptr(), w.ldz, w.pmax.data_ptr(), w.psum.data_ptr(), w.parg.data_ptr(), 1, st)
         call("rg_lse_combine", w.pmax.data_ptr(), w.psum.data_ptr(), w.parg.data_ptr(), B, w.nJ, w.work.data_ptr(),
-             w.ZT.data_ptr(), w.ldz, tgt.data_ptr(), w.lse.data_ptr(), w.amax.data_ptr(), w.loss_row.data_ptr(), st)
+             w.ZT.data_ptr(), w.ldz, tgt.data_ptr(), self.A, w.lse.data_ptr(), w.amax.data_ptr(),
+             w.loss_row.data_ptr(), st)
         call("rg_sum_scale", w.loss_row.data_ptr(), B, _f32(1.0 / B), w.loss.data_ptr(), None, st)
         return w.loss, w
 
@@ -340,5 +343,5 @@ class SoftmaxHead:
         call("rg_head_fwd", h.data_ptr(), self.W.p.data_ptr(), self.b.p.data_ptr(), B, self.A, self.HF, None, 0,
              w.pmax.data_ptr(), w.psum.data_ptr(), w.parg.data_ptr(), 0, st)
         call("rg_lse_combine", w.pmax.data_ptr(), w.psum.data_ptr(), w.parg.data_ptr(), B, w.nJ, w.work.data_ptr(),
-             None, 0, None, None, w.amax.data_ptr(), None, st)
+             None, 0, None, self.A, None, w.amax.data_ptr(), None, st)
         return w.amax

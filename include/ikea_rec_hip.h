@@ -36,9 +36,12 @@ int rg_pack(const int64_t* lens, int B, int L, int unpacked, int32_t* perm, int3
 /* ---- A3 embedding gather: replaces self.embedding(s) (nn.Embedding forward,
  * GRU4Rec/model.py:69,74).  Writes only the T valid tokens, packed (T, E), and
  * their int32 ids.  reverse=1: tokens of a row in reverse time order (the
- * backward direction of BidirGRU4Rec, BidirGRU4Rec/model.py:51-58). */
+ * backward direction of BidirGRU4Rec, BidirGRU4Rec/model.py:51-58).  Ids
+ * outside [0, n_rows) (nn.Embedding raises) gather zeros, get tok_id -1 and
+ * set *err |= 1 (err optional). */
 int rg_gather(const int64_t* s, int B, int L, const int32_t* perm, const int32_t* lsort, const int32_t* offs,
-              const float* emb, int E, int reverse, int32_t* tok_id, float* X, rg_stream_t stream);
+              const float* emb, int64_t n_rows, int E, int reverse, int32_t* tok_id, float* X, int32_t* err,
+              rg_stream_t stream);
 
 /* ---- A3 embedding backward: replaces embedding_dense_backward (autograd of
  * nn.Embedding, incl. padding_idx masking when train_pad_embed=False,
@@ -85,8 +88,8 @@ int rg_head_fwd(const float* h, const float* W, const float* bias, int B, int A,
 /* partials -> lse (B), argmax (B) (torch.argmax semantics: first maximum),
  * loss_row (B) = lse - Z[a_b, b].  work: 3*min(64,nJ)*B floats. */
 int rg_lse_combine(const float* pmax, const float* psum, const int32_t* parg, int B, int nJ, float* work,
-                   const float* ZT, int64_t ldz, const int64_t* tgt, float* lse, int32_t* amax, float* loss_row,
-                   rg_stream_t stream);
+                   const float* ZT, int64_t ldz, const int64_t* tgt, int A, float* lse, int32_t* amax,
+                   float* loss_row, rg_stream_t stream);
 int rg_sum_scale(const float* x, int n, float scale, float* out, double* out64, rg_stream_t stream);
 /* backward of CE + Linear w.r.t. h: dh slabs (returns number of slabs > 0). */
 int rg_head_dh(const float* ZT, int64_t ldz, const float* lse, const int64_t* tgt, float gscale, const float* W,

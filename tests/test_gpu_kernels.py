@@ -18,12 +18,23 @@ def st():
     return C().stream_ptr()
 
 
+_KEEP = []
+
+
+def D(t):
+    """Device copy kept alive for the whole test (a temporary's block would be
+    recycled by the caching allocator before an async kernel reads it)."""
+    d = t.to(dev)
+    _KEEP.append(d)
+    return d
+
+
 def pack(lens, L, unpacked=0):
     B = lens.numel()
     perm = torch.empty(B, dtype=torch.int32, device=dev)
     ls = torch.empty(B, dtype=torch.int32, device=dev)
     offs = torch.empty(B + 1, dtype=torch.int32, device=dev)
-    C().call("rg_pack", lens.to(dev).data_ptr(), B, L, unpacked, perm.data_ptr(), ls.data_ptr(), offs.data_ptr(),
+    C().call("rg_pack", D(lens).data_ptr(), B, L, unpacked, perm.data_ptr(), ls.data_ptr(), offs.data_ptr(),
              st())
     return perm, ls, offs
 
@@ -51,8 +62,8 @@ def test_gather_packed_and_reverse():
     for rev in (0, 1):
         X = torch.zeros(B * L, E, device=dev)
         ids = torch.zeros(B * L, dtype=torch.int32, device=dev)
-        C().call("rg_gather", s.to(dev).data_ptr(), B, L, perm.data_ptr(), ls.data_ptr(), offs.data_ptr(),
-                 emb.to(dev).data_ptr(), E, rev, ids.data_ptr(), X.data_ptr(), st())
+        C().call("rg_gather", D(s).data_ptr(), B, L, perm.data_ptr(), ls.data_ptr(), offs.data_ptr(),
+                 D(emb).data_ptr(), N + 1, E, rev, ids.data_ptr(), X.data_ptr(), None, st())
         rows = []
         for r in perm.cpu().tolist():
             t = list(range(int(lens[r])))
@@ -78,7 +89,7 @@ def test_gemm_layouts(M, N, K, splits):
             out = torch.zeros(splits, M, N, device=dev)
             C().call("rg_gemm_f32", a.data_ptr(), sam, sak, b.data_ptr(), sbk, sbn, out.data_ptr(), N, None, M,
                      None, N, K, None, splits, st())
-            torch.testing.assert_close(out.sum(0).cpu(), ref, rtol=1e-5, atol=1e-4)
+            torch.testing.assert_close(out.sum(0).cpu(), ref, rtol=1e-5, atol=1e-4 * max(1.0, K / 1000))
 
 
 def gru_ref(X_rows, lens, perm_order, Wih, Whh, bih, bhh, H):
@@ -115,7 +126,7 @@ def test_gru_forward_backward(H):
     Gi = (packed.double() @ Wih.double().t() + bih.double()).float().to(dev)
     hout = torch.zeros(B, H, device=dev)
     saved = torch.zeros(5, T, H, device=dev)
-    C().call("rg_gru_fwd", Gi.data_ptr(), Whh.to(dev).data_ptr(), bhh.to(dev).data_ptr(), perm.data_ptr(),
+    C().call("rg_gru_fwd", Gi.data_ptr(), D(Whh).data_ptr(), D(bhh).data_ptr(), perm.data_ptr(),
              ls.data_ptr(), offs.data_ptr(), B, H, hout.data_ptr(), H, 0, saved.data_ptr(), T * H, st())
     # autograd reference (float64)
     Xd = X.double().requires_grad_(True)
@@ -137,8 +148,8 @@ def test_gru_forward_backward(H):
     (href * dh.double()).sum().backward()
     dGi = torch.zeros(T, 3 * H, device=dev)
     dGh = torch.zeros(T, 3 * H, device=dev)
-    C().call("rg_gru_bwd", saved.data_ptr(), T * H, Whh.to(dev).data_ptr(), perm.data_ptr(), ls.data_ptr(),
-             offs.data_ptr(), B, H, dh.to(dev).data_ptr(), H, 0, dGi.data_ptr(), dGh.data_ptr(), st())
+    C().call("rg_gru_bwd", saved.data_ptr(), T * H, D(Whh).data_ptr(), perm.data_ptr(), ls.data_ptr(),
+             offs.data_ptr(), B, H, D(dh).data_ptr(), H, 0, dGi.data_ptr(), dGh.data_ptr(), st())
     # dX = dGi · W_ih (packed order) vs autograd
     dX = (dGi.cpu().double() @ Wih.double())
     ref_dX = torch.cat([Xd.grad[r, :int(lens[r])] for r in order])
@@ -173,7 +184,7 @@ def test_head_forward_backward(B, A, HF):
     amax = torch.zeros(B, dtype=torch.int32, device=dev)
     lrow = torch.zeros(B, device=dev)
     C().call("rg_lse_combine", pm.data_ptr(), ps.data_ptr(), pa.data_ptr(), B, nJ, work.data_ptr(), ZT.data_ptr(),
-             ldz, td.data_ptr(), lse.data_ptr(), amax.data_ptr(), lrow.data_ptr(), st())
+             ldz, td.data_ptr(), A, lse.data_ptr(), amax.data_ptr(), lrow.data_ptr(), st())
     torch.testing.assert_close(lse.cpu().double(), torch.logsumexp(Zref, 1), rtol=0, atol=2e-5)
     Zg = ZT[:, :B].t().cpu()
     assert torch.equal(amax.cpu().long(), torch.argmax(Zg, 1))
@@ -238,7 +249,7 @@ def test_q_kernels_and_rewards():
     q = torch.zeros(B, 3, device=dev)
     hip = C()
     hip.call("rg_q_gather", hd.data_ptr(), HF, hip.host_ptr_array(Wd), hip.host_ptr_array(bd), 3,
-             idx.to(dev).data_ptr(), None, B, q.data_ptr(), st())
+             D(idx).data_ptr(), None, B, q.data_ptr(), st())
     ref = torch.stack([(h * Ws[i][idx]).sum(1) + bs[i][idx] for i in range(3)], 1)
     torch.testing.assert_close(q.cpu(), ref, rtol=0, atol=1e-5)
     # diversity / novelty
@@ -250,8 +261,8 @@ def test_q_kernels_and_rewards():
     preds = torch.randn(B, A, generator=g)
     top = torch.topk(preds, 3).indices.to(torch.int32)
     out = torch.zeros(B, device=dev)
-    hip.call("rg_diversity", s.to(dev).data_ptr(), L, lens.to(dev).data_ptr(), 1, top.to(dev).data_ptr(), 3,
-             table.to(dev).data_ptr(), Ed, 1e-6, B, out.data_ptr(), st())
+    hip.call("rg_diversity", D(s).data_ptr(), L, D(lens).data_ptr(), 1, D(top).data_ptr(), 3,
+             D(table).data_ptr(), Ed, 1e-6, B, out.data_ptr(), st())
     torch.testing.assert_close(out.cpu(), om.batch_diversity_rewards(s, preds, lens, "end", 3, table), rtol=0,
                                atol=1e-6)
     unpop = set(range(0, A, 3))
@@ -259,6 +270,6 @@ def test_q_kernels_and_rewards():
     for j in unpop:
         bm[j >> 5] |= np.uint32(1 << (j & 31))
     outn = torch.zeros(B, device=dev)
-    hip.call("rg_novelty", top.to(dev).data_ptr(), 3, torch.from_numpy(bm.view(np.int32)).to(dev).data_ptr(), 2.0,
+    hip.call("rg_novelty", D(top).data_ptr(), 3, D(torch.from_numpy(bm.view(np.int32))).data_ptr(), 2.0,
              B, outn.data_ptr(), st())
     np.testing.assert_allclose(outn.cpu().numpy(), om.batch_novelty_rewards(preds, unpop, 2.0, 3), atol=1e-6)
