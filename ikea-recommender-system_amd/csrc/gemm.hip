@@ -149,3 +149,110 @@ extern "C" int rg_colsum(const float* X, int ncol, int rows, const int32_t* rows
   RG_LAUNCH_CHECK();
   return RG_OK;
 }
+
+// ---------------------------------------------------------------------------
+// Weight gradient of a dense layer over packed tokens, fused with the bias
+// gradient:  dW[m][n] = Σ_t G[t][m]·X[t][n],  db[m] = Σ_t G[t][m]
+// (nn.GRU backward: dW_ih = dGiᵀ·X, dW_hh = dGhᵀ·H_prev, b_ih/b_hh sums).
+// G is (T × M) row-major, X is (T × N); T is read from the device.  One
+// workgroup = a 128-row M tile × all N columns (N ≤ 128) over one token split;
+// per 32-token step the G and X tiles go through LDS once and feed
+// 16 k-steps × N/32 v_mfma_f32_32x32x2_f32 per wave; the bias column sums come
+// from the same staged G values.  Slab z of dW / db holds split z.
+template <int N>
+__global__ __launch_bounds__(256) void k_wgrad(const float* __restrict__ G, int M, const float* __restrict__ X,
+                                               const int32_t* __restrict__ Tptr, int tchunk,
+                                               float* __restrict__ dw_slabs, float* __restrict__ db_slabs) {
+  constexpr int NP = N < 32 ? 32 : N;
+  constexpr int NCT = NP / 32;
+  constexpr int TB = 32;
+  constexpr int NX4 = TB * N / 4;
+  constexpr int NXL = (NX4 + 255) / 256;
+  __shared__ __attribute__((aligned(16))) float gs[TB][128 + 4];
+  __shared__ __attribute__((aligned(16))) float xs[TB][NP + 4];
+  __shared__ float csum[8][128];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, half = lane >> 5, l32 = lane & 31;
+  const int T = *Tptr;
+  const int m0 = blockIdx.x * 128;
+  const int t0 = blockIdx.y * tchunk;
+  const int t1 = min(T, t0 + tchunk);
+  const int c4 = tid & 31;  // this thread's 4 G columns
+  const int tr = tid >> 5;  // rows tr + 8i
+  f4 cs = {0.f, 0.f, 0.f, 0.f};
+  f16v acc[NCT];
+#pragma unroll
+  for (int ct = 0; ct < NCT; ++ct) acc[ct] = f16v{};
+  for (int tb = t0; tb < t1; tb += TB) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int t = tb + tr + 8 * i;
+      const int m = m0 + 4 * c4;
+      f4 v = {0.f, 0.f, 0.f, 0.f};
+      if (t < t1 && m < M) v = *reinterpret_cast<const f4*>(G + (int64_t)t * M + m);
+      cs += v;
+      *reinterpret_cast<f4*>(&gs[tr + 8 * i][4 * c4]) = v;
+    }
+#pragma unroll
+    for (int i = 0; i < NXL; ++i) {
+      const int e = tid + 256 * i;
+      if (e < NX4) {
+        const int rr = e / (N / 4), cc = e % (N / 4);
+        const int t = tb + rr;
+        f4 v = {0.f, 0.f, 0.f, 0.f};
+        if (t < t1) v = *reinterpret_cast<const f4*>(X + (int64_t)t * N + 4 * cc);
+        *reinterpret_cast<f4*>(&xs[rr][4 * cc]) = v;
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int s = 0; s < TB / 2; ++s) {
+      const int t = half * (TB / 2) + s;
+      const float a = gs[t][32 * w + l32];
+#pragma unroll
+      for (int ct = 0; ct < NCT; ++ct) {
+        const float b = (N >= 32 || l32 < N) ? xs[t][ct * 32 + l32] : 0.f;
+        acc[ct] = mfma32(a, b, acc[ct]);
+      }
+    }
+    __syncthreads();
+  }
+  float* dw = dw_slabs + (int64_t)blockIdx.y * M * N;
+#pragma unroll
+  for (int ct = 0; ct < NCT; ++ct) {
+    const int n = ct * 32 + l32;
+    if (n >= N) continue;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int m = m0 + 32 * w + acc32_row(r, half);
+      if (m < M) dw[(int64_t)m * N + n] = acc[ct][r];
+    }
+  }
+  *reinterpret_cast<f4*>(&csum[tr][4 * c4]) = cs;
+  __syncthreads();
+  if (tid < 128) {
+    float s = 0.f;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) s += csum[q][tid];
+    const int m = m0 + tid;
+    if (m < M) db_slabs[(int64_t)blockIdx.y * M + m] = s;
+  }
+}
+
+extern "C" int rg_wgrad(const float* G, int M, const float* X, int N, int T_max, const int32_t* Tptr, int splits,
+                        float* dw_slabs, float* db_slabs, hipStream_t stream) {
+  if (M <= 0 || M % 4 || T_max <= 0 || splits <= 0 || !Tptr) return RG_ERR_ARG;
+  int tchunk = (T_max + splits - 1) / splits;
+  tchunk = (tchunk + 31) / 32 * 32;
+  dim3 grid((M + 127) / 128, splits);
+#define WG(NV) hipLaunchKernelGGL(k_wgrad<NV>, grid, dim3(256), 0, stream, G, M, X, Tptr, tchunk, dw_slabs, db_slabs)
+  switch (N) {
+    case 16: WG(16); break;
+    case 32: WG(32); break;
+    case 64: WG(64); break;
+    case 128: WG(128); break;
+    default: return RG_ERR_SHAPE;
+  }
+#undef WG
+  RG_LAUNCH_CHECK();
+  return RG_OK;
+}

@@ -154,33 +154,26 @@ __global__ __launch_bounds__(256) void k_scatter_add(const int32_t* __restrict__
                                                      const int32_t* __restrict__ ntok_ptr,
                                                      int skip_id, float* __restrict__ G,
                                                      int32_t* __restrict__ tags, int32_t tag) {
+  // one wave per token; consecutive lanes add consecutive floats (256-B
+  // contiguous atomic wave-instructions, the full-rate shape)
   const int T = *ntok_ptr;
-  const int per_block = blockDim.x / (E >> 2) > 0 ? blockDim.x / (E >> 2) : 1;
-  const int v4 = E >> 2;
-  for (int t0 = blockIdx.x * per_block; t0 < T; t0 += gridDim.x * per_block) {
-    int t = t0 + threadIdx.x / v4;
-    int c = threadIdx.x % v4;
-    if (threadIdx.x / v4 >= per_block || t >= T) continue;
-    int id = tok_id[t];
+  const int lane = threadIdx.x & 63;
+  for (int t = blockIdx.x * 4 + (threadIdx.x >> 6); t < T; t += gridDim.x * 4) {
+    const int id = tok_id[t];
     if (id == skip_id || id < 0) continue;
-    f4 g = reinterpret_cast<const f4*>(dX + (int64_t)t * E)[c];
-    float* dst = G + (int64_t)id * E + 4 * c;
-    atomicAdd(dst + 0, g.x);
-    atomicAdd(dst + 1, g.y);
-    atomicAdd(dst + 2, g.z);
-    atomicAdd(dst + 3, g.w);
-    if (c == 0) tags[id] = tag;
+    const float* src = dX + (int64_t)t * E;
+    float* dst = G + (int64_t)id * E;
+    for (int c = lane; c < E; c += 64) atomicAdd(dst + c, src[c]);
+    if (lane == 0) tags[id] = tag;
   }
 }
 
 extern "C" int rg_scatter_add(const int32_t* tok_id, const float* dX, int E, const int32_t* ntok_ptr,
                               int max_tokens, int skip_id, float* G, int32_t* tags, int32_t tag,
                               hipStream_t stream) {
-  if ((E & 3) || E > 1024) return RG_ERR_ARG;
-  int per_block = 256 / (E / 4);
-  if (per_block < 1) per_block = 1;
-  int blocks = (max_tokens + per_block - 1) / per_block;
-  if (blocks > 4096) blocks = 4096;
+  if (E <= 0) return RG_ERR_ARG;
+  int blocks = (max_tokens + 3) / 4;
+  if (blocks > 8192) blocks = 8192;
   if (blocks < 1) blocks = 1;
   hipLaunchKernelGGL(k_scatter_add, dim3(blocks), dim3(256), 0, stream, tok_id, dX, E, ntok_ptr, skip_id,
                      G, tags, tag);

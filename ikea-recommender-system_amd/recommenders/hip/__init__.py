@@ -29,6 +29,7 @@ SIGNATURES = {
     "rg_gemm_f32": [P, I64, I64, P, I64, I64, P, I64, P, I, P, I, I, P, I, P],
     "rg_reduce_slabs": [P, I, I64, P, P, I, I, P],
     "rg_colsum": [P, I, I, P, I, P, P],
+    "rg_wgrad": [P, I, P, I, I, P, I, P, P, P],
     "rg_gru_fwd": [P, P, P, P, P, P, I, I, P, I, I, P, I64, P],
     "rg_gru_bwd": [P, I64, P, P, P, P, I, I, P, I, I, P, P, P],
     "rg_head_fwd": [P, P, P, I, I, I, P, I64, P, P, P, I, P],

@@ -24,6 +24,7 @@ import numpy as np
 import torch
 
 from . import call, host_floats, host_ptr_array, ptr, stream_ptr
+from .timing import region
 
 
 def _f32(x: float) -> float:
@@ -137,7 +138,7 @@ class _TrunkWS:
             self.dGi = [z(TM, 3 * H) for _ in range(ndir)]
             self.dGh = [z(TM, 3 * H) for _ in range(ndir)]
             self.dX = [z(TM, E) for _ in range(ndir)]
-            self.splits = int(min(64, max(1, TM // 2048)))
+            self.splits = int(min(128, max(1, TM // 1024)))
             S = self.splits
             self.sl_ih = z(S, 3 * H, E)
             self.sl_hh = z(S, 3 * H, H)
@@ -200,19 +201,23 @@ class Trunk:
             w.lens.copy_(lens, non_blocking=False)
         else:
             w.lens.copy_(lens)
-        call("rg_pack", w.lens.data_ptr(), B, L, 0 if self.packed else 1, w.perm.data_ptr(), w.lsort.data_ptr(),
-             w.offs.data_ptr(), st)
+        with region("pack"):
+            call("rg_pack", w.lens.data_ptr(), B, L, 0 if self.packed else 1, w.perm.data_ptr(),
+                 w.lsort.data_ptr(), w.offs.data_ptr(), st)
         H, E = self.H, self.E
         for d in range(self.ndir):
             w_ih, w_hh, b_ih, b_hh = self.dirs[d]
-            call("rg_gather", s.data_ptr(), B, L, w.perm.data_ptr(), w.lsort.data_ptr(), w.offs.data_ptr(),
-                 self.emb.p.data_ptr(), self.N1, E, d, w.tok_id[d].data_ptr(), w.X[d].data_ptr(),
-                 self.err.data_ptr(), st)
-            call("rg_gemm_f32", w.X[d].data_ptr(), E, 1, w_ih.p.data_ptr(), 1, E, w.Gi[d].data_ptr(), 3 * H,
-                 b_ih.p.data_ptr(), w.TM, w.ntok_ptr, 3 * H, E, None, 1, st)
-            call("rg_gru_fwd", w.Gi[d].data_ptr(), w_hh.p.data_ptr(), b_hh.p.data_ptr(), w.perm.data_ptr(),
-                 w.lsort.data_ptr(), w.offs.data_ptr(), B, H, w.h.data_ptr(), self.ndir * H, d * H,
-                 w.saved[d].data_ptr() if save else None, w.plane, st)
+            with region("gather"):
+                call("rg_gather", s.data_ptr(), B, L, w.perm.data_ptr(), w.lsort.data_ptr(), w.offs.data_ptr(),
+                     self.emb.p.data_ptr(), self.N1, E, d, w.tok_id[d].data_ptr(), w.X[d].data_ptr(),
+                     self.err.data_ptr(), st)
+            with region("gemm_ih"):
+                call("rg_gemm_f32", w.X[d].data_ptr(), E, 1, w_ih.p.data_ptr(), 1, E, w.Gi[d].data_ptr(), 3 * H,
+                     b_ih.p.data_ptr(), w.TM, w.ntok_ptr, 3 * H, E, None, 1, st)
+            with region("gru_fwd"):
+                call("rg_gru_fwd", w.Gi[d].data_ptr(), w_hh.p.data_ptr(), b_hh.p.data_ptr(), w.perm.data_ptr(),
+                     w.lsort.data_ptr(), w.offs.data_ptr(), B, H, w.h.data_ptr(), self.ndir * H, d * H,
+                     w.saved[d].data_ptr() if save else None, w.plane, st)
         return w.h
 
     def backward(self, dh, slot="main"):
@@ -223,13 +228,17 @@ class Trunk:
         H, E, B, TM, S = self.H, self.E, w.B, w.TM, w.splits
         for d in range(self.ndir):
             w_ih, w_hh, _, _ = self.dirs[d]
-            call("rg_gru_bwd", w.saved[d].data_ptr(), w.plane, w_hh.p.data_ptr(), w.perm.data_ptr(),
-                 w.lsort.data_ptr(), w.offs.data_ptr(), B, H, dh.data_ptr(), self.ndir * H, d * H,
-                 w.dGi[d].data_ptr(), w.dGh[d].data_ptr(), st)
+            with region("gru_bwd"):
+                call("rg_gru_bwd", w.saved[d].data_ptr(), w.plane, w_hh.p.data_ptr(), w.perm.data_ptr(),
+                     w.lsort.data_ptr(), w.offs.data_ptr(), B, H, dh.data_ptr(), self.ndir * H, d * H,
+                     w.dGi[d].data_ptr(), w.dGh[d].data_ptr(), st)
         self._pending = (w, S)
 
     def step(self, adam6, tag):
         """Weight gradients + Adam for the trunk (after every use of the weights)."""
+        self._step(adam6, tag)
+
+    def _step(self, adam6, tag):
         w, S = self._pending
         st = stream_ptr()
         H, E, TM = self.H, self.E, w.TM
@@ -237,22 +246,24 @@ class Trunk:
         for d in range(self.ndir):
             w_ih, w_hh, b_ih, b_hh = self.dirs[d]
             # dX = dGi · W_ih  (T × E)
-            call("rg_gemm_f32", w.dGi[d].data_ptr(), 3 * H, 1, w_ih.p.data_ptr(), E, 1, w.dX[d].data_ptr(), E,
-                 None, TM, w.ntok_ptr, E, 3 * H, None, 1, st)
-            # dW_ih = dGiᵀ · X ; dW_hh = dGhᵀ · H_prev  (split over tokens)
-            call("rg_gemm_f32", w.dGi[d].data_ptr(), 1, 3 * H, w.X[d].data_ptr(), E, 1, w.sl_ih.data_ptr(), E,
-                 None, 3 * H, None, E, TM, w.ntok_ptr, S, st)
-            call("rg_gemm_f32", w.dGh[d].data_ptr(), 1, 3 * H, w.saved[d].data_ptr(), H, 1, w.sl_hh.data_ptr(),
-                 H, None, 3 * H, None, H, TM, w.ntok_ptr, S, st)
-            call("rg_colsum", w.dGi[d].data_ptr(), 3 * H, TM, w.ntok_ptr, S, w.cs_ih.data_ptr(), st)
-            call("rg_colsum", w.dGh[d].data_ptr(), 3 * H, TM, w.ntok_ptr, S, w.cs_hh.data_ptr(), st)
-            call("rg_scatter_add", w.tok_id[d].data_ptr(), w.dX[d].data_ptr(), E, w.ntok_ptr, TM, skip,
-                 self.G_emb.data_ptr(), self.tags.data_ptr(), tag, st)
+            with region("gemm_dx"):
+                call("rg_gemm_f32", w.dGi[d].data_ptr(), 3 * H, 1, w_ih.p.data_ptr(), E, 1, w.dX[d].data_ptr(),
+                     E, None, TM, w.ntok_ptr, E, 3 * H, None, 1, st)
+            # dW_ih = dGiᵀ·X, db_ih = Σ dGi ; dW_hh = dGhᵀ·H_prev, db_hh = Σ dGh  (token splits)
+            with region("wgrad"):
+                call("rg_wgrad", w.dGi[d].data_ptr(), 3 * H, w.X[d].data_ptr(), E, TM, w.ntok_ptr, S,
+                     w.sl_ih.data_ptr(), w.cs_ih.data_ptr(), st)
+                call("rg_wgrad", w.dGh[d].data_ptr(), 3 * H, w.saved[d].data_ptr(), H, TM, w.ntok_ptr, S,
+                     w.sl_hh.data_ptr(), w.cs_hh.data_ptr(), st)
+            with region("scatter"):
+                call("rg_scatter_add", w.tok_id[d].data_ptr(), w.dX[d].data_ptr(), E, w.ntok_ptr, TM, skip,
+                     self.G_emb.data_ptr(), self.tags.data_ptr(), tag, st)
             for prm, sl in ((w_ih, w.sl_ih), (w_hh, w.sl_hh), (b_ih, w.cs_ih), (b_hh, w.cs_hh)):
                 call("rg_adam_slabs", prm.p.data_ptr(), prm.m.data_ptr(), prm.v.data_ptr(), sl.data_ptr(), S,
                      prm.numel(), adam6, None, st)
-        call("rg_adam_rows", self.emb.p.data_ptr(), self.emb.m.data_ptr(), self.emb.v.data_ptr(),
-             self.G_emb.data_ptr(), self.tags.data_ptr(), tag, self.N1, E, adam6, st)
+        with region("adam_emb"):
+            call("rg_adam_rows", self.emb.p.data_ptr(), self.emb.m.data_ptr(), self.emb.v.data_ptr(),
+                 self.G_emb.data_ptr(), self.tags.data_ptr(), tag, self.N1, E, adam6, st)
         self._pending = None
 
 
@@ -314,8 +325,9 @@ class SoftmaxHead:
         B = h.shape[0]
         w = self.ws(slot, B, True)
         st = stream_ptr()
-        call("rg_head_fwd", h.data_ptr(), self.W.p.data_ptr(), self.b.p.data_ptr(), B, self.A, self.HF,
-             w.ZT.data_ptr(), w.ldz, w.pmax.data_ptr(), w.psum.data_ptr(), w.parg.data_ptr(), 1, st)
+        with region("head_fwd"):
+            call("rg_head_fwd", h.data_ptr(), self.W.p.data_ptr(), self.b.p.data_ptr(), B, self.A, self.HF,
+                 w.ZT.data_ptr(), w.ldz, w.pmax.data_ptr(), w.psum.data_ptr(), w.parg.data_ptr(), 1, st)
         call("rg_lse_combine", w.pmax.data_ptr(), w.psum.data_ptr(), w.parg.data_ptr(), B, w.nJ, w.work.data_ptr(),
              w.ZT.data_ptr(), w.ldz, tgt.data_ptr(), self.A, w.lse.data_ptr(), w.amax.data_ptr(),
              w.loss_row.data_ptr(), st)
@@ -328,12 +340,14 @@ class SoftmaxHead:
         w = self.ws(slot, B, True)
         st = stream_ptr()
         g = _f32(1.0 / B) if gscale is None else gscale
-        n = call("rg_head_dh", w.ZT.data_ptr(), w.ldz, w.lse.data_ptr(), tgt.data_ptr(), g, self.W.p.data_ptr(), B,
-                 self.A, self.HF, w.dh_splits, w.dh_slabs.data_ptr(), st)
+        with region("head_dh"):
+            n = call("rg_head_dh", w.ZT.data_ptr(), w.ldz, w.lse.data_ptr(), tgt.data_ptr(), g, self.W.p.data_ptr(),
+                     B, self.A, self.HF, w.dh_splits, w.dh_slabs.data_ptr(), st)
         call("rg_reduce_slabs", w.dh_slabs.data_ptr(), n, B * self.HF, dh_out.data_ptr(), None, self.HF, 0, st)
-        call("rg_head_dw_adam", w.ZT.data_ptr(), w.ldz, w.lse.data_ptr(), tgt.data_ptr(), g, h.data_ptr(), B,
-             self.A, self.HF, self.W.p.data_ptr(), self.W.m.data_ptr(), self.W.v.data_ptr(), self.b.p.data_ptr(),
-             self.b.m.data_ptr(), self.b.v.data_ptr(), adam6, None, None, st)
+        with region("head_dw_adam"):
+            call("rg_head_dw_adam", w.ZT.data_ptr(), w.ldz, w.lse.data_ptr(), tgt.data_ptr(), g, h.data_ptr(), B,
+                 self.A, self.HF, self.W.p.data_ptr(), self.W.m.data_ptr(), self.W.v.data_ptr(),
+                 self.b.p.data_ptr(), self.b.m.data_ptr(), self.b.v.data_ptr(), adam6, None, None, st)
 
     def argmax(self, h, slot="argmax"):
         """argmax_j (h·Wᵀ + b)[b, j] without storing Z (first maximum)."""

@@ -62,6 +62,12 @@ int rg_reduce_slabs(const float* slabs, int nslab, int64_t n, float* out, const 
                     rg_stream_t stream);
 int rg_colsum(const float* X, int ncol, int rows, const int32_t* rows_ptr, int splits, float* slabs,
               rg_stream_t stream);
+/* weight + bias gradient over packed tokens in one pass (nn.GRU backward's
+ * dW_ih = dGi^T X, db_ih = sum dGi; dW_hh = dGh^T H_prev, db_hh = sum dGh):
+ * dw_slabs (splits x M x N), db_slabs (splits x M); T read from *Tptr;
+ * N in {16, 32, 64, 128}, M % 4 == 0. */
+int rg_wgrad(const float* G, int M, const float* X, int N, int T_max, const int32_t* Tptr, int splits,
+             float* dw_slabs, float* db_slabs, rg_stream_t stream);
 
 /* ---- A5 GRU recurrence: replaces nn.GRU forward over the packed sequence and
  * `h = h[0, :, :]` (GRU4Rec/model.py:76-77; layer 0 only, the reference's

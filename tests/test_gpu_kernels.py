@@ -273,3 +273,18 @@ def test_q_kernels_and_rewards():
     hip.call("rg_novelty", D(top).data_ptr(), 3, D(torch.from_numpy(bm.view(np.int32))).data_ptr(), 2.0,
              B, outn.data_ptr(), st())
     np.testing.assert_allclose(outn.cpu().numpy(), om.batch_novelty_rewards(preds, unpop, 2.0, 3), atol=1e-6)
+
+
+@pytest.mark.parametrize("M,N,T,splits", [(384, 128, 5000, 16), (48, 16, 77, 3), (192, 64, 3000, 128)])
+def test_wgrad_fused_bias(M, N, T, splits):
+    g = torch.Generator().manual_seed(7)
+    G = torch.randn(T + 40, M, generator=g)
+    X = torch.randn(T + 40, N, generator=g)
+    Tdev = D(torch.tensor([T], dtype=torch.int32))
+    dw = torch.zeros(splits, M, N, device=dev)
+    db = torch.zeros(splits, M, device=dev)
+    C().call("rg_wgrad", D(G).data_ptr(), M, D(X).data_ptr(), N, T + 40, Tdev.data_ptr(), splits, dw.data_ptr(),
+             db.data_ptr(), st())
+    ref = G[:T].double().t() @ X[:T].double()
+    torch.testing.assert_close(dw.sum(0).cpu().double(), ref, rtol=0, atol=2e-6 * T)
+    torch.testing.assert_close(db.sum(0).cpu().double(), G[:T].double().sum(0), rtol=0, atol=2e-6 * T)
