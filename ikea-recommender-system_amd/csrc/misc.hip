@@ -48,3 +48,22 @@ extern "C" int rg_weighted_sum(const float* const* X, const float* w, int nh, in
 }
 
 extern "C" int rg_abi_version(void) { return 1; }
+
+// SMORL reward matrix r = stack([r_acc, r_div, r_nov], 1).to(float32)
+// (smorl_gru.py:311-314 with the third reward): f64 -> f32 per column.
+__global__ void k_stack_rewards(const double* __restrict__ r_acc, const float* __restrict__ r_div,
+                                const float* __restrict__ r_nov, int B, float* __restrict__ r) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  r[3 * b + 0] = (float)r_acc[b];
+  r[3 * b + 1] = r_div[b];
+  r[3 * b + 2] = r_nov[b];
+}
+
+extern "C" int rg_stack_rewards(const double* r_acc, const float* r_div, const float* r_nov, int B, float* r,
+                                hipStream_t stream) {
+  if (B <= 0) return RG_ERR_ARG;
+  hipLaunchKernelGGL(k_stack_rewards, dim3((B + 255) / 256), dim3(256), 0, stream, r_acc, r_div, r_nov, B, r);
+  RG_LAUNCH_CHECK();
+  return RG_OK;
+}

@@ -49,6 +49,7 @@ SIGNATURES = {
     "rg_novelty": [P, I, P, F, I, P, P],
     "rg_mask_scale": [P, P, F, I64, P, P],
     "rg_weighted_sum": [P, P, I, I64, P, P],
+    "rg_stack_rewards": [P, P, P, I, P, P],
 }
 
 _lib = None

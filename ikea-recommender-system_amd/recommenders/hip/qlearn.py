@@ -1,0 +1,203 @@
+"""Double-Q training steps on the MI355X.
+
+SQN  (SQN/sqn_gru.py:183-254): supervised head + one Q head, double-Q target.
+SMORL (SMORL/smorl_gru.py:233-334, 3-reward form of SURVEY §3.4): supervised
+head + Q heads (acc, div, nov), weighted-argmax target, online diversity and
+novelty rewards.
+
+Per step: trunk(s) with saved state; sup head CE (Zᵀ kept for backward);
+Q(s, a) as B dot products; trunk(s') of the main net -> argmax of the
+(weighted) Q head without storing Z; trunk(s') of the boot net with
+``true_len`` (reference quirk) -> Q_boot(s', a*) gathers; TD loss;
+backward: sup head (dh + fused dW/Adam), Q-head row scatter, BPTT, Adam
+sweeps of every main-net parameter (dense semantics).
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from . import call, host_floats, host_ptr_array, stream_ptr
+from .engine import SoftmaxHead, _f32
+from .nets import HipNet
+from .timing import region
+
+
+class QHead(SoftmaxHead):
+    """Linear(H -> A) used through row gathers, argmax (fused GEMM pass, no Z
+    stored) and row-sparse gradients; logits_T for evaluation."""
+
+    def __init__(self, name, A, HF, device):
+        super().__init__(name, A, HF, device)
+        self.G = torch.zeros_like(self.W.p)
+        self.Gb = torch.zeros_like(self.b.p)
+        self.tags = torch.zeros(A, dtype=torch.int32, device=device)
+
+    def adam(self, adam6, tag):
+        st = stream_ptr()
+        call("rg_adam_rows", self.W.p.data_ptr(), self.W.m.data_ptr(), self.W.v.data_ptr(), self.G.data_ptr(),
+             self.tags.data_ptr(), tag, self.A, self.HF, adam6, st)
+        call("rg_adam_rows", self.b.p.data_ptr(), self.b.m.data_ptr(), self.b.v.data_ptr(), self.Gb.data_ptr(),
+             self.tags.data_ptr(), tag, self.A, 1, adam6, st)
+
+
+class _T:
+    """Bare parameter holder (.p) for derived device tensors."""
+
+    def __init__(self, t):
+        self.p = t
+
+
+class QNet(HipNet):
+    """Trunk + supervised softmax head + Q heads (reference key names)."""
+
+    def __init__(self, *, q_names, **kw):
+        super().__init__(head_names=["sup_head_output"], **kw)
+        self.q_heads = [QHead(n, self.action_dim, self.hf, self.device) for n in q_names]
+        for q in self.q_heads:
+            setattr(self, q.name, q)
+        self._argmax_head = None
+        self._buf = {}
+
+    def named_param_objs(self):
+        out = list(self.trunk.named_params()) + self.sup_head_output.named_params()
+        for q in self.q_heads:
+            out += q.named_params()
+        return out
+
+    def buf(self, name, shape, dtype=torch.float32):
+        t = self._buf.get(name)
+        if t is None or tuple(t.shape) != tuple(shape) or t.dtype != dtype:
+            t = torch.empty(*shape, dtype=dtype, device=self.device)
+            self._buf[name] = t
+        return t
+
+    def forward(self, s, lengths):
+        """(sup (B, A), q (B, A)) for SQN; (sup, q_all (B, heads, A)) for SMORL,
+        as the reference's nn.Module forward returns (sqn_gru.py:87-112)."""
+        h = self.hidden(s, lengths, slot="eval", save=False)
+        _, sup = self.sup_head_output.logits_T(h, slot="eval")
+        outs = [q.logits_T(h, slot="eval")[1] for q in self.q_heads]
+        if len(outs) == 1:
+            return sup, outs[0]
+        return sup, torch.stack(outs, dim=1)
+
+    def argmax_q(self, h, weights=None):
+        """argmax_a Σ_i w_i Q_i(s, a) via one fused GEMM+argmax pass over the
+        combined head (W_c = Σ w_i W_i, b_c = Σ w_i b_i)."""
+        if len(self.q_heads) == 1:
+            return self.q_heads[0].argmax(h, slot="argmax")
+        if self._argmax_head is None:
+            hd = SoftmaxHead.__new__(SoftmaxHead)
+            hd.name, hd.A, hd.HF, hd.device, hd._ws = "qcomb", self.action_dim, self.hf, self.device, {}
+            hd.W = _T(torch.empty_like(self.q_heads[0].W.p))
+            hd.b = _T(torch.empty_like(self.q_heads[0].b.p))
+            self._argmax_head = hd
+        hd = self._argmax_head
+        wts = host_floats(weights)
+        st = stream_ptr()
+        call("rg_weighted_sum", host_ptr_array([q.W.p for q in self.q_heads]), wts, len(self.q_heads),
+             hd.W.p.numel(), hd.W.p.data_ptr(), st)
+        call("rg_weighted_sum", host_ptr_array([q.b.p for q in self.q_heads]), wts, len(self.q_heads),
+             hd.b.p.numel(), hd.b.p.data_ptr(), st)
+        return hd.argmax(h, slot="argmax")
+
+    def gather_q(self, h, idx64=None, idx32=None, out=None):
+        B = h.shape[0]
+        nh = len(self.q_heads)
+        q = out if out is not None else torch.empty(B, nh, device=self.device)
+        call("rg_q_gather", h.data_ptr(), self.hf, host_ptr_array([x.W.p for x in self.q_heads]),
+             host_ptr_array([x.b.p for x in self.q_heads]), nh, None if idx64 is None else idx64.data_ptr(),
+             None if idx32 is None else idx32.data_ptr(), B, q.data_ptr(), stream_ptr())
+        return q
+
+
+def _dev(x, dev, dtype=None):
+    x = x.to(dev, non_blocking=True)
+    return x if dtype is None else x.to(dtype)
+
+
+def double_q_step(nets, clocks, k, s, a, r, s_next, true_len, true_next_len, is_end, *, gamma, smorl=None):
+    """One SQN (smorl=None) or SMORL step with main = nets[k].  Returns device
+    (sup_loss (1,) f32, q_loss (1,) f64 for SQN / f32 for SMORL)."""
+    main, boot = nets[k], nets[1 - k]
+    dev = main.device
+    s = _dev(s, dev)
+    a = _dev(a, dev)
+    s_next = _dev(s_next, dev)
+    end8 = _dev(is_end, dev, torch.uint8)
+    B = s.shape[0]
+    nh = len(main.q_heads)
+    st = stream_ptr()
+    with region("sqn_trunk_main"):
+        h = main.trunk.forward(s, true_len, slot="main", save=True)
+    sup_loss, _ = main.sup_head_output.forward_loss(h, a, slot="main")
+    q = main.gather_q(h, idx64=a, out=main.buf("q", (B, nh)))
+    with region("sqn_target"):
+        h_n = main.trunk.forward(s_next, true_next_len, slot="next", save=False)
+        a_star = main.argmax_q(h_n, None if smorl is None else smorl["w"])
+        h_b = boot.trunk.forward(s_next, true_len, slot="boot", save=False)   # quirk: true_len
+        qn = boot.gather_q(h_b, idx32=a_star, out=main.buf("qn", (B, nh)))
+    dq = main.buf("dq", (B, nh))
+    if smorl is None:
+        r64 = _dev(r, dev, torch.float64)
+        sq = main.buf("sq", (B,), torch.float64)
+        q_loss = main.buf("qloss64", (1,), torch.float64)
+        call("rg_sqn_td", q.data_ptr(), qn.data_ptr(), r64.data_ptr(), end8.data_ptr(), _f32(gamma), B, 1.0 / B,
+             sq.data_ptr(), dq.data_ptr(), st)
+        call("rg_sum64", sq.data_ptr(), B, 1.0 / B, q_loss.data_ptr(), None, st)
+    else:
+        rr = smorl_rewards(main, smorl, s, a, r, true_next_len, B)
+        row = main.buf("qrow", (B,))
+        q_loss = main.buf("qloss32", (1,))
+        grad_row = _f32(np.float32(smorl["alpha"]) / np.float32(B))
+        call("rg_smorl_td", q.data_ptr(), qn.data_ptr(), rr.data_ptr(), end8.data_ptr(), smorl["w_dev"].data_ptr(),
+             nh, _f32(gamma), grad_row, B, row.data_ptr(), dq.data_ptr(), st)
+        call("rg_sum_scale", row.data_ptr(), B, _f32(1.0 / B), q_loss.data_ptr(), None, st)
+    # ---- backward + Adam (main network, its own optimizer clock) ----
+    adam6 = clocks[k].next_args()
+    main.trunk_tag = getattr(main, "trunk_tag", 0) + 1
+    tag = main.trunk_tag
+    dh = main.dh_buffer(B)
+    main.sup_head_output.backward_step(h, a, dh, adam6, slot="main")
+    call("rg_q_backward", h.data_ptr(), main.hf, host_ptr_array([x.W.p for x in main.q_heads]),
+         host_ptr_array([x.G for x in main.q_heads]), host_ptr_array([x.Gb for x in main.q_heads]),
+         host_ptr_array([x.tags for x in main.q_heads]), nh, a.data_ptr(), B, dq.data_ptr(), dh.data_ptr(), tag, st)
+    for qh in main.q_heads:
+        qh.adam(adam6, tag)
+    main.trunk.backward(dh, slot="main")
+    main.trunk.step(adam6, tag)
+    return sup_loss, q_loss
+
+
+def smorl_rewards(main, smorl, s, a, r_acc, true_next_len, B):
+    """r = stack([r_acc, r_div, r_nov]).float32."""
+    dev = main.device
+    st = stream_ptr()
+    head = main.sup_head_output
+    w = head.ws("main", B, True)
+    k_div, k_nov = smorl["topk_div"], smorl["topk_nov"]
+    if k_div != 1 or k_nov != 1:
+        raise NotImplementedError("top-k > 1 rewards need the top-k kernel (rg_topk)")
+    idx = w.amax  # argmax of the supervised logits = topk(sup, 1)
+    r_div = main.buf("r_div", (B,))
+    lens = _dev(true_next_len, dev, torch.int64)   # quirk: diversity uses true_next_len
+    call("rg_diversity", s.data_ptr(), s.shape[1], lens.data_ptr(), 1 if smorl["pad_end"] else 0, idx.data_ptr(),
+         k_div, smorl["div_table"].data_ptr(), smorl["div_table"].shape[1], _f32(1e-6), B, r_div.data_ptr(), st)
+    r_nov = main.buf("r_nov", (B,))
+    call("rg_novelty", idx.data_ptr(), k_nov, smorl["bitmap"].data_ptr(), _f32(smorl["nov_rew_sig"]), B,
+         r_nov.data_ptr(), st)
+    r64 = _dev(r_acc, dev, torch.float64)
+    rr = main.buf("rr", (B, 3))
+    call("rg_stack_rewards", r64.data_ptr(), r_div.data_ptr(), r_nov.data_ptr(), B, rr.data_ptr(), st)
+    main._last_rewards = rr
+    return rr
+
+
+def unpopular_bitmap(unpopular, n_actions, device):
+    bm = np.zeros((n_actions + 31) // 32, dtype=np.uint32)
+    for j in unpopular:
+        j = int(j)
+        if 0 <= j < n_actions:
+            bm[j >> 5] |= np.uint32(1) << np.uint32(j & 31)
+    return torch.from_numpy(bm.view(np.int32)).to(device)

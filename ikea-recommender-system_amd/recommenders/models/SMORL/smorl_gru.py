@@ -1,0 +1,117 @@
+"""Drop-in ``SMORL_GRU_Net`` / ``SMORL_trainer`` for the MI355X
+(reference ``recommenders/models/SMORL/smorl_gru.py:14-359``).
+
+The shipped reference step stacks two rewards against three Q heads and
+raises (:311 vs :137).  This step implements the 3-reward form it was written
+for: r = stack([r_acc, r_div, r_nov]).float32 with the novelty
+reward of ``recommenders/evaluate/novelty.py:12-47``; the stubbed kwargs
+``topk_nov`` / ``nov_rew_sig`` (:219-220) are accepted.  Weighted target
+argmax over Σ w_i Q_i(s', ·) runs as one fused GEMM+argmax pass over the
+combined head.  Parity is pinned to the reference helpers composed in that
+order (tests/golden/smorl_composed.npz).
+"""
+import random
+
+import torch
+import torch.nn as nn
+
+from recommenders.hip import require_gpu
+from recommenders.hip.engine import AdamClock
+from recommenders.hip.qlearn import QNet, double_q_step, unpopular_bitmap
+from recommenders.models.GRU4Rec.model import _AdamFacade
+
+
+class SMORL_GRU_Net(QNet):
+    def __init__(self, hidden_dim, embedding_dim, item_num, state_size, action_dim, q_weights, gamma, gru_layers=1,
+                 random_embed_init=True, train_pad_embed=True, use_packed_seq=False, padding_idx=None,
+                 name="SMORL_GRU_Network", device="cuda"):
+        if not random_embed_init:
+            raise NotImplementedError("TODO: Pretrained embedings.")
+        if use_packed_seq:
+            train_pad_embed = True
+        super().__init__(q_names=["q_head_acc", "q_head_div", "q_head_nov"], trunk_attr="base_model",
+                         hidden_dim=hidden_dim, embedding_dim=embedding_dim, item_num=item_num,
+                         state_size=state_size, action_dim=action_dim, gru_layers=gru_layers,
+                         use_packed_seq=use_packed_seq, train_pad_embed=train_pad_embed, padding_idx=padding_idx,
+                         bidir=False, device=device)
+        self.q_weights = q_weights
+        self.gamma = gamma
+        self.name = name
+
+
+class SMORL_trainer:
+    def __init__(self, hidden_dim, embedding_dim, padding_pos, train_pad_embed, use_packed_seq, learning_rate,
+                 item_num, state_size, action_dim, gamma, gru_layers, q_weights, alpha, div_embedding,
+                 unpopular_actions_set, topk_div, device, input_tokenizer=None, output_tokenizer=None,
+                 padding_idx=None, torch_rand_seed=118, python_rand_seed=999, name_1="SMORL_1", name_2="SMORL_2",
+                 topk_nov=1, nov_rew_sig=1):
+        torch.manual_seed(torch_rand_seed)
+        random.seed(python_rand_seed)
+        self.device = require_gpu(device)
+        if input_tokenizer is not None or output_tokenizer is not None:
+            raise NotImplementedError("tokenizer remap (SURVEY §8f rank 4) is not on the device path yet")
+        mk = lambda name: SMORL_GRU_Net(hidden_dim=hidden_dim, item_num=item_num, state_size=state_size,
+                                        action_dim=action_dim, gru_layers=gru_layers, gamma=gamma,
+                                        q_weights=q_weights, embedding_dim=embedding_dim,
+                                        train_pad_embed=train_pad_embed, use_packed_seq=use_packed_seq,
+                                        padding_idx=padding_idx, name=name, device=self.device)
+        self.SMORL_1 = mk(name_1)
+        self.SMORL_2 = mk(name_2)
+        self.gamma = gamma
+        self.alpha = alpha
+        self.q_weights = q_weights
+        self.padding_pos = padding_pos
+        self.learning_rate = learning_rate
+        self.cross_entropy_loss = nn.CrossEntropyLoss(weight=None, reduction="mean")
+        self.input_tokenizer = input_tokenizer
+        self.output_tokenizer = output_tokenizer
+        self.div_embedding = div_embedding
+        self.topk_div = topk_div
+        self.topk_nov = topk_nov
+        self.nov_rew_signal = nov_rew_sig
+        self.unpopular_actions_set = unpopular_actions_set
+        table = div_embedding.weight if hasattr(div_embedding, "weight") else div_embedding
+        w = torch.as_tensor(q_weights, dtype=torch.float32).flatten()
+        self._smorl = {
+            "w": [float(x) for x in w.tolist()],
+            "w_dev": w.to(self.device),
+            "alpha": float(alpha),
+            "topk_div": int(topk_div),
+            "topk_nov": int(topk_nov),
+            "nov_rew_sig": float(nov_rew_sig),
+            "pad_end": padding_pos == "end",
+            "div_table": table.detach().to(self.device, torch.float32).contiguous(),
+            "bitmap": unpopular_bitmap(unpopular_actions_set, action_dim, self.device),
+        }
+        self.clock_1 = AdamClock(learning_rate)
+        self.clock_2 = AdamClock(learning_rate)
+        self.optimizer_1 = _AdamFacade(self.clock_1, [self.SMORL_1])
+        self.optimizer_2 = _AdamFacade(self.clock_2, [self.SMORL_2])
+        self.last_main = None
+
+    def train_step_async(self, s, a, r_acc, s_next, true_len, true_next_len, is_end):
+        k = 0 if random.uniform(0, 1) <= 0.5 else 1
+        self.last_main = k
+        return double_q_step([self.SMORL_1, self.SMORL_2], [self.clock_1, self.clock_2], k, s, a, r_acc, s_next,
+                             true_len, true_next_len, is_end, gamma=self.gamma, smorl=self._smorl)
+
+    def train_step(self, s, a, r_acc, s_next, true_len, true_next_len, is_end):
+        sup, q = self.train_step_async(s, a, r_acc, s_next, true_len, true_next_len, is_end)
+        return sup.item(), q.item()
+
+    @property
+    def last_rewards(self):
+        net = self.SMORL_1 if self.last_main == 0 else self.SMORL_2
+        return net._last_rewards
+
+    def set_train(self):
+        self.SMORL_1.train()
+        self.SMORL_2.train()
+
+    def set_eval(self):
+        self.SMORL_1.eval()
+        self.SMORL_2.eval()
+
+    def send_to_device(self):
+        self.SMORL_1.to(self.device)
+        self.SMORL_2.to(self.device)

@@ -1,0 +1,82 @@
+"""Drop-in ``SQN_Network`` / ``SQN_trainer`` for the MI355X
+(reference ``recommenders/models/SQN/sqn_gru.py:10-277``).
+
+Double-Q: the main/boot choice is the reference's ``random.uniform(0, 1) <= 0.5``
+on Python's global RNG (seeded at construction, :137, :207-216); only the main
+network's optimizer steps; the bootstrap net runs on ``s_next`` with
+``true_len`` (reference quirk, :231); the TD loss is evaluated in float64 like
+the reference's float64-reward promotion.
+"""
+import random
+
+import torch
+import torch.nn as nn
+
+from recommenders.hip import require_gpu
+from recommenders.hip.engine import AdamClock
+from recommenders.hip.qlearn import QNet, double_q_step
+from recommenders.models.GRU4Rec.model import _AdamFacade
+
+
+class SQN_Network(QNet):
+    def __init__(self, hidden_dim, item_num, state_size, action_dim, gamma, gru_layers, embedding_dim=50,
+                 random_embed_init=True, train_pad_embed=True, use_packed_seq=False, padding_idx=None,
+                 name="DQNetwork", device="cuda"):
+        if not random_embed_init:
+            raise NotImplementedError("TODO: Pretrained embedings.")  # as the reference (:67-68)
+        if use_packed_seq:
+            train_pad_embed = True  # sqn_gru.py:45-48
+        super().__init__(q_names=["q_head_output"], trunk_attr="base_model", hidden_dim=hidden_dim,
+                         embedding_dim=embedding_dim, item_num=item_num, state_size=state_size,
+                         action_dim=action_dim, gru_layers=gru_layers, use_packed_seq=use_packed_seq,
+                         train_pad_embed=train_pad_embed, padding_idx=padding_idx, bidir=False, device=device)
+        self.gamma = gamma
+        self.name = name
+        self.random_embed_init = random_embed_init
+
+
+class SQN_trainer:
+    def __init__(self, hidden_dim, embedding_dim, train_pad_embed, use_packed_seq, learning_rate, item_num,
+                 state_size, action_dim, gamma, gru_layers, device, padding_idx=None, torch_rand_seed=118,
+                 python_rand_seed=999, name_1="SQN_1", name_2="SQN_2"):
+        torch.manual_seed(torch_rand_seed)
+        random.seed(python_rand_seed)
+        self.device = require_gpu(device)
+        mk = lambda name: SQN_Network(hidden_dim=hidden_dim, item_num=item_num, state_size=state_size,
+                                      action_dim=action_dim, gamma=gamma, gru_layers=gru_layers,
+                                      embedding_dim=embedding_dim, train_pad_embed=train_pad_embed,
+                                      use_packed_seq=use_packed_seq, padding_idx=padding_idx, name=name,
+                                      device=self.device)
+        self.DQN_1 = mk(name_1)
+        self.DQN_2 = mk(name_2)
+        self.gamma = gamma
+        self.learning_rate = learning_rate
+        self.cross_entropy_loss = nn.CrossEntropyLoss(weight=None, reduction="mean")
+        self.clock_1 = AdamClock(learning_rate)
+        self.clock_2 = AdamClock(learning_rate)
+        self.optimizer_1 = _AdamFacade(self.clock_1, [self.DQN_1])
+        self.optimizer_2 = _AdamFacade(self.clock_2, [self.DQN_2])
+        self.last_main = None
+
+    def train_step_async(self, s, a, r, s_next, true_len, true_next_len, is_end):
+        k = 0 if random.uniform(0, 1) <= 0.5 else 1
+        self.last_main = k
+        return double_q_step([self.DQN_1, self.DQN_2], [self.clock_1, self.clock_2], k, s, a, r, s_next, true_len,
+                             true_next_len, is_end, gamma=self.gamma)
+
+    def train_step(self, s, a, r, s_next, true_len, true_next_len, is_end):
+        """One double-Q step; returns (sup_loss, q_loss) as Python floats."""
+        sup, q = self.train_step_async(s, a, r, s_next, true_len, true_next_len, is_end)
+        return sup.item(), q.item()
+
+    def set_train(self):
+        self.DQN_1.train()
+        self.DQN_2.train()
+
+    def set_eval(self):
+        self.DQN_1.eval()
+        self.DQN_2.eval()
+
+    def send_to_device(self):
+        self.DQN_1.to(self.device)
+        self.DQN_2.to(self.device)

@@ -146,6 +146,8 @@ int rg_novelty(const int32_t* idx, int k, const uint32_t* bitmap, float reward, 
 int rg_mask_scale(const float* x, const float* mask, float scale, int64_t n, float* y, rg_stream_t stream);
 /* W_comb = sum_i w_i W_i (SMORL target weights, tensor_operations.py:50-70) */
 int rg_weighted_sum(const float* const* X, const float* w, int nh, int64_t n, float* out, rg_stream_t stream);
+/* SMORL reward matrix r (B, 3) f32 = stack([r_acc f64, r_div, r_nov]) (SMORL/smorl_gru.py:311-314, 3 rewards) */
+int rg_stack_rewards(const double* r_acc, const float* r_div, const float* r_nov, int B, float* r, rg_stream_t stream);
 
 int rg_abi_version(void);
 

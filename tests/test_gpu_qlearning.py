@@ -1,0 +1,89 @@
+"""GPU parity: SQN double-Q and SMORL 3-reward steps vs the reference's golden
+vectors (tests/golden/sqn_packed.npz — the reference SQN_trainer itself;
+smorl_composed.npz — the reference helpers composed, since the shipped SMORL
+step raises).  Tolerances as tests/test_gpu_supervised.py; Q losses 1e-5."""
+import json
+import os
+import random
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import GOLDEN
+from test_gpu_supervised import bt, compare_params, load
+
+pytestmark = pytest.mark.gpu
+
+META = json.load(open(os.path.join(GOLDEN, "meta.json")))
+
+
+def test_sqn_matches_reference_golden():
+    from recommenders.models.SQN.sqn_gru import SQN_trainer
+    g = load("sqn_packed")
+    cfg = META["cases"]["sqn_packed"]["config"]
+    tr = SQN_trainer(device="cuda", **cfg)
+    for net, pre in ((tr.DQN_1, "init1."), (tr.DQN_2, "init2.")):
+        for k, v in net.state_dict().items():
+            np.testing.assert_array_equal(v.cpu().numpy(), g[pre + k], err_msg=k)
+    sup, q, mains = [], [], []
+    for i in range(g["in_s"].shape[0]):
+        x, y = tr.train_step(*bt(g, i))
+        sup.append(x)
+        q.append(y)
+        mains.append(tr.last_main)
+    np.testing.assert_array_equal(mains, g["main_idx"])
+    np.testing.assert_allclose(sup, g["sup_losses"], rtol=0, atol=1e-4)
+    np.testing.assert_allclose(q, g["q_losses"], rtol=0, atol=1e-5)
+    compare_params(tr.DQN_1.state_dict(), g, "final1.", cfg["learning_rate"])
+    compare_params(tr.DQN_2.state_dict(), g, "final2.", cfg["learning_rate"])
+
+
+def test_smorl_matches_composed_reference_golden():
+    from recommenders.models.SMORL.smorl_gru import SMORL_trainer
+    g = load("smorl_composed")
+    cfg = dict(META["cases"]["smorl_composed"]["config"])
+    table = torch.nn.Embedding.from_pretrained(torch.from_numpy(g["div_table"]), freeze=True)
+    unpop = set(int(x) for x in g["unpopular"])
+    q_weights = torch.tensor(cfg.pop("q_weights"))
+    tr = SMORL_trainer(device="cuda", div_embedding=table, unpopular_actions_set=unpop, q_weights=q_weights,
+                       **cfg)
+    for net, pre in ((tr.SMORL_1, "init1."), (tr.SMORL_2, "init2.")):
+        for k, v in net.state_dict().items():
+            np.testing.assert_array_equal(v.cpu().numpy(), g[pre + k], err_msg=k)
+    sup, q, rw = [], [], []
+    for i in range(g["in_s"].shape[0]):
+        x, y = tr.train_step(*bt(g, i))
+        sup.append(x)
+        q.append(y)
+        rw.append(tr.last_rewards.cpu().numpy().copy())
+    np.testing.assert_allclose(np.stack(rw), g["rewards"], rtol=0, atol=1e-5)
+    np.testing.assert_allclose(sup, g["sup_losses"], rtol=0, atol=1e-4)
+    np.testing.assert_allclose(q, g["q_losses"], rtol=0, atol=1e-5)
+    compare_params(tr.SMORL_1.state_dict(), g, "final1.", cfg["learning_rate"])
+    compare_params(tr.SMORL_2.state_dict(), g, "final2.", cfg["learning_rate"])
+
+
+def test_sqn_matches_oracle_medium():
+    from oracle.models import OracleSQN
+    from recommenders.data_utils.synthetic import SessionStream
+    from recommenders.models.SQN.sqn_gru import SQN_trainer
+    N, L, B, H = 20000, 20, 512, 64
+    cfg = dict(hidden_dim=H, embedding_dim=H, train_pad_embed=True, use_packed_seq=True, learning_rate=0.005,
+               item_num=N, state_size=L, action_dim=N, gamma=0.5, gru_layers=1)
+    torch.set_num_threads(8)
+    orc = OracleSQN(**cfg)
+    rs_o = random.getstate()
+    tr = SQN_trainer(device="cuda", **cfg)
+    rs_t = random.getstate()
+    st = SessionStream(N, L, B * 4, seed=9)
+    for i in range(4):
+        b = st.batch(i, B)
+        random.setstate(rs_o)   # both draw main/boot from Python's global RNG
+        so, qo = orc.step(*b)
+        rs_o = random.getstate()
+        random.setstate(rs_t)
+        sg, qg = tr.train_step(*b)
+        rs_t = random.getstate()
+        assert orc.last_main == tr.last_main
+        assert abs(so - sg) < 1e-4 and abs(qo - qg) < 1e-5, (i, so, sg, qo, qg)
