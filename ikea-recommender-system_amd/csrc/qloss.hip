@@ -184,7 +184,7 @@ extern "C" int rg_sum64(const double* x, int n, double scale, double* out64, flo
 // per-vector norms clamped at eps (torch cosine_similarity).  One wave per row.
 __global__ __launch_bounds__(256) void k_diversity(const int64_t* __restrict__ s, int L,
                                                    const int64_t* __restrict__ lens, int pad_end,
-                                                   const int32_t* __restrict__ idx, int k,
+                                                   const int32_t* __restrict__ idx, int k, int ldi,
                                                    const float* __restrict__ D, int Ed, float eps, int B,
                                                    float* __restrict__ out) {
   const int b = blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -197,7 +197,7 @@ __global__ __launch_bounds__(256) void k_diversity(const int64_t* __restrict__ s
   n1 = fmaxf(sqrtf(wave_sum(n1)), eps);
   float tot = 0.f;
   for (int q = 0; q < k; ++q) {
-    const float* x2 = D + (int64_t)idx[(int64_t)b * k + q] * Ed;
+    const float* x2 = D + (int64_t)idx[(int64_t)b * ldi + q] * Ed;
     float n2 = 0.f;
     for (int c = lane; c < Ed; c += 64) n2 += x2[c] * x2[c];
     n2 = fmaxf(sqrtf(wave_sum(n2)), eps);
@@ -209,32 +209,32 @@ __global__ __launch_bounds__(256) void k_diversity(const int64_t* __restrict__ s
 }
 
 extern "C" int rg_diversity(const int64_t* s, int L, const int64_t* lens, int pad_end, const int32_t* idx, int k,
-                            const float* D, int Ed, float eps, int B, float* out, hipStream_t stream) {
-  if (B <= 0 || k <= 0) return RG_ERR_ARG;
-  hipLaunchKernelGGL(k_diversity, dim3((B + 3) / 4), dim3(256), 0, stream, s, L, lens, pad_end, idx, k, D, Ed, eps,
-                     B, out);
+                            int ldi, const float* D, int Ed, float eps, int B, float* out, hipStream_t stream) {
+  if (B <= 0 || k <= 0 || ldi < k) return RG_ERR_ARG;
+  hipLaunchKernelGGL(k_diversity, dim3((B + 3) / 4), dim3(256), 0, stream, s, L, lens, pad_end, idx, k, ldi, D, Ed,
+                     eps, B, out);
   RG_LAUNCH_CHECK();
   return RG_OK;
 }
 
 // Novelty reward (novelty.py:12-47): mean_k [idx_bk ∈ U]·reward, U as a bitmap.
-__global__ void k_novelty(const int32_t* __restrict__ idx, int k, const uint32_t* __restrict__ bitmap,
+__global__ void k_novelty(const int32_t* __restrict__ idx, int k, int ldi, const uint32_t* __restrict__ bitmap,
                           float reward, int B, float* __restrict__ out) {
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= B) return;
   double acc = 0.0;
   for (int q = 0; q < k; ++q) {
-    const int j = idx[(int64_t)b * k + q];
+    const int j = idx[(int64_t)b * ldi + q];
     const bool u = (bitmap[j >> 5] >> (j & 31)) & 1u;
     acc += u ? (double)reward : 0.0;
   }
   out[b] = (float)(acc / k);
 }
 
-extern "C" int rg_novelty(const int32_t* idx, int k, const uint32_t* bitmap, float reward, int B, float* out,
+extern "C" int rg_novelty(const int32_t* idx, int k, int ldi, const uint32_t* bitmap, float reward, int B, float* out,
                           hipStream_t stream) {
-  if (B <= 0 || k <= 0) return RG_ERR_ARG;
-  hipLaunchKernelGGL(k_novelty, dim3((B + 255) / 256), dim3(256), 0, stream, idx, k, bitmap, reward, B, out);
+  if (B <= 0 || k <= 0 || ldi < k) return RG_ERR_ARG;
+  hipLaunchKernelGGL(k_novelty, dim3((B + 255) / 256), dim3(256), 0, stream, idx, k, ldi, bitmap, reward, B, out);
   RG_LAUNCH_CHECK();
   return RG_OK;
 }

@@ -45,8 +45,10 @@ SIGNATURES = {
     "rg_sqn_td": [P, P, P, P, F, I, D, P, P, P],
     "rg_smorl_td": [P, P, P, P, P, I, F, F, I, P, P, P],
     "rg_sum64": [P, I, D, P, P, P],
-    "rg_diversity": [P, I, P, I, P, I, P, I, F, I, P, P],
-    "rg_novelty": [P, I, P, F, I, P, P],
+    "rg_diversity": [P, I, P, I, P, I, I, P, I, F, I, P, P],
+    "rg_novelty": [P, I, I, P, F, I, P, P],
+    "rg_topk": [P, I64, P, I, I, I, P, P, P, P],
+    "rg_hits_ndcg": [P, I, P, I, P, I, P, P],
     "rg_mask_scale": [P, P, F, I64, P, P],
     "rg_weighted_sum": [P, P, I, I64, P, P],
     "rg_stack_rewards": [P, P, P, I, P, P],

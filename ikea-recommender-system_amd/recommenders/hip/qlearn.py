@@ -177,15 +177,18 @@ def smorl_rewards(main, smorl, s, a, r_acc, true_next_len, B):
     head = main.sup_head_output
     w = head.ws("main", B, True)
     k_div, k_nov = smorl["topk_div"], smorl["topk_nov"]
-    if k_div != 1 or k_nov != 1:
-        raise NotImplementedError("top-k > 1 rewards need the top-k kernel (rg_topk)")
-    idx = w.amax  # argmax of the supervised logits = topk(sup, 1)
+    K = max(k_div, k_nov)
+    if K == 1:
+        idx = w.amax  # argmax of the supervised logits = topk(sup, 1)
+    else:
+        idx = main.buf("topk_idx", (B, K), torch.int32)
+        call("rg_topk", w.ZT.data_ptr(), w.ldz, w.pmax.data_ptr(), B, head.A, K, idx.data_ptr(), None, None, st)
     r_div = main.buf("r_div", (B,))
     lens = _dev(true_next_len, dev, torch.int64)   # quirk: diversity uses true_next_len
     call("rg_diversity", s.data_ptr(), s.shape[1], lens.data_ptr(), 1 if smorl["pad_end"] else 0, idx.data_ptr(),
-         k_div, smorl["div_table"].data_ptr(), smorl["div_table"].shape[1], _f32(1e-6), B, r_div.data_ptr(), st)
+         k_div, K, smorl["div_table"].data_ptr(), smorl["div_table"].shape[1], _f32(1e-6), B, r_div.data_ptr(), st)
     r_nov = main.buf("r_nov", (B,))
-    call("rg_novelty", idx.data_ptr(), k_nov, smorl["bitmap"].data_ptr(), _f32(smorl["nov_rew_sig"]), B,
+    call("rg_novelty", idx.data_ptr(), k_nov, K, smorl["bitmap"].data_ptr(), _f32(smorl["nov_rew_sig"]), B,
          r_nov.data_ptr(), st)
     r64 = _dev(r_acc, dev, torch.float64)
     rr = main.buf("rr", (B, 3))

@@ -136,11 +136,23 @@ int rg_smorl_td(const float* q, float* qn, const float* r, const uint8_t* is_end
                 float gamma, float grad_row, int B, float* row_loss, float* dq, rg_stream_t stream);
 int rg_sum64(const double* x, int n, double scale, double* out64, float* out32, rg_stream_t stream);
 /* A12 diversity reward: recommenders/evaluate/diversity.py:15-73. */
-int rg_diversity(const int64_t* s, int L, const int64_t* lens, int pad_end, const int32_t* idx, int k, const float* D,
-                 int Ed, float eps, int B, float* out, rg_stream_t stream);
+int rg_diversity(const int64_t* s, int L, const int64_t* lens, int pad_end, const int32_t* idx, int k, int ldi,
+                 const float* D, int Ed, float eps, int B, float* out, rg_stream_t stream);
 /* A13 novelty reward: recommenders/evaluate/novelty.py:12-47 (U as bitmap). */
-int rg_novelty(const int32_t* idx, int k, const uint32_t* bitmap, float reward, int B, float* out,
+int rg_novelty(const int32_t* idx, int k, int ldi, const uint32_t* bitmap, float reward, int B, float* out,
                rg_stream_t stream);
+
+/* ---- A14 / A12 / A13 top-k: replaces torch.topk(preds, k) on host-copied
+ * (B, A) logits (recommenders/evaluate/eval_protocol.py:75,199; diversity.py:51;
+ * novelty.py:33).  Exact; ties ordered (value desc, index asc).  Uses the
+ * forward kernel's block maxima pmax (nJ x B) to prune.  out_idx (B, k),
+ * out_val (B, k) optional; *err |= 2 on candidate overflow (massive ties). */
+int rg_topk(const float* ZT, int64_t ldz, const float* pmax, int B, int A, int k, int32_t* out_idx, float* out_val,
+            int32_t* err, rg_stream_t stream);
+/* HR@k / NDCG@k sums (eval_protocol.py:26-100) accumulated into out
+ * (2*nk doubles: hits..., ndcg...); ks: HOST int array, k <= K. */
+int rg_hits_ndcg(const int32_t* idx, int K, const int64_t* tgt, int B, const int* ks, int nk, double* out,
+                 rg_stream_t stream);
 
 /* misc elementwise: y = x * mask * scale (dropout fwd/bwd, BidirGRU4Rec/model.py:60,93) */
 int rg_mask_scale(const float* x, const float* mask, float scale, int64_t n, float* y, rg_stream_t stream);

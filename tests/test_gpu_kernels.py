@@ -261,7 +261,7 @@ def test_q_kernels_and_rewards():
     preds = torch.randn(B, A, generator=g)
     top = torch.topk(preds, 3).indices.to(torch.int32)
     out = torch.zeros(B, device=dev)
-    hip.call("rg_diversity", D(s).data_ptr(), L, D(lens).data_ptr(), 1, D(top).data_ptr(), 3,
+    hip.call("rg_diversity", D(s).data_ptr(), L, D(lens).data_ptr(), 1, D(top).data_ptr(), 3, 3,
              D(table).data_ptr(), Ed, 1e-6, B, out.data_ptr(), st())
     torch.testing.assert_close(out.cpu(), om.batch_diversity_rewards(s, preds, lens, "end", 3, table), rtol=0,
                                atol=1e-6)
@@ -270,7 +270,7 @@ def test_q_kernels_and_rewards():
     for j in unpop:
         bm[j >> 5] |= np.uint32(1 << (j & 31))
     outn = torch.zeros(B, device=dev)
-    hip.call("rg_novelty", D(top).data_ptr(), 3, D(torch.from_numpy(bm.view(np.int32))).data_ptr(), 2.0,
+    hip.call("rg_novelty", D(top).data_ptr(), 3, 3, D(torch.from_numpy(bm.view(np.int32))).data_ptr(), 2.0,
              B, outn.data_ptr(), st())
     np.testing.assert_allclose(outn.cpu().numpy(), om.batch_novelty_rewards(preds, unpop, 2.0, 3), atol=1e-6)
 
