@@ -45,7 +45,7 @@ def parse():
     ap.add_argument("--seq", type=int, default=SEQ)
     ap.add_argument("--batch", type=int, default=BATCH)
     ap.add_argument("--cpu-batch", type=int, default=512)
-    ap.add_argument("--cpu-steps", type=int, default=2)
+    ap.add_argument("--cpu-steps", type=int, default=6)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-timing", action="store_true")
     return ap.parse_args()
