@@ -591,3 +591,58 @@ extern "C" int rg_head_dw_adam(const float* ZT, int64_t ldz, const float* lse, c
   RG_LAUNCH_CHECK();
   return RG_OK;
 }
+
+// ---------------------------------------------------- item-sharded head ----
+// Multi-GPU: rank r owns items [lo, hi).  lse over all items of row b =
+// logsumexp over ranks of the per-rank lse (nr × B, rank-major).
+__global__ void k_lse_merge_ranks(const float* __restrict__ lse_r, int nr, int B, float* __restrict__ lse) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  float m = -__builtin_inff();
+  for (int q = 0; q < nr; ++q) m = fmaxf(m, lse_r[(int64_t)q * B + b]);
+  float s = 0.f;
+  for (int q = 0; q < nr; ++q) s += expf(lse_r[(int64_t)q * B + b] - m);
+  lse[b] = m + logf(s);
+}
+
+extern "C" int rg_lse_merge_ranks(const float* lse_r, int nr, int B, float* lse, hipStream_t stream) {
+  if (B <= 0 || nr <= 0) return RG_ERR_ARG;
+  hipLaunchKernelGGL(k_lse_merge_ranks, dim3((B + 255) / 256), dim3(256), 0, stream, lse_r, nr, B, lse);
+  RG_LAUNCH_CHECK();
+  return RG_OK;
+}
+
+// zt[b] = Zᵀ[a_b − lo][b] when lo ≤ a_b < hi else 0 (summed over ranks
+// afterwards); tgt_loc[b] = a_b − lo (out-of-shard targets never match a
+// local item in the backward kernels).
+__global__ void k_shard_targets(const float* __restrict__ ZT, int64_t ldz, const int64_t* __restrict__ tgt, int64_t lo,
+                                int64_t hi, int B, float* __restrict__ zt, int64_t* __restrict__ tgt_loc) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  const int64_t t = tgt[b];
+  const bool own = t >= lo && t < hi;
+  zt[b] = own ? ZT[(t - lo) * ldz + b] : 0.0f;
+  tgt_loc[b] = t - lo;
+}
+
+extern "C" int rg_shard_targets(const float* ZT, int64_t ldz, const int64_t* tgt, int64_t lo, int64_t hi, int B,
+                                float* zt, int64_t* tgt_loc, hipStream_t stream) {
+  if (B <= 0 || hi <= lo) return RG_ERR_ARG;
+  hipLaunchKernelGGL(k_shard_targets, dim3((B + 255) / 256), dim3(256), 0, stream, ZT, ldz, tgt, lo, hi, B, zt,
+                     tgt_loc);
+  RG_LAUNCH_CHECK();
+  return RG_OK;
+}
+
+// loss_row[b] = lse[b] − zt[b]
+__global__ void k_sub(const float* __restrict__ a, const float* __restrict__ b, int n, float* __restrict__ out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = a[i] - b[i];
+}
+
+extern "C" int rg_sub(const float* a, const float* b, int n, float* out, hipStream_t stream) {
+  if (n <= 0) return RG_ERR_ARG;
+  hipLaunchKernelGGL(k_sub, dim3((n + 255) / 256), dim3(256), 0, stream, a, b, n, out);
+  RG_LAUNCH_CHECK();
+  return RG_OK;
+}

@@ -35,6 +35,9 @@ SIGNATURES = {
     "rg_head_fwd": [P, P, P, I, I, I, P, I64, P, P, P, I, P],
     "rg_lse_combine": [P, P, P, I, I, P, P, I64, P, I, P, P, P, P],
     "rg_sum_scale": [P, I, F, P, P, P],
+    "rg_lse_merge_ranks": [P, I, I, P, P],
+    "rg_shard_targets": [P, I64, P, I64, I64, I, P, P, P],
+    "rg_sub": [P, P, I, P, P],
     "rg_head_dh": [P, I64, P, P, F, P, I, I, I, I, P, P],
     "rg_head_dw_adam": [P, I64, P, P, F, P, I, I, I, P, P, P, P, P, P, P, P, P, P],
     "rg_adam_dense": [P, P, P, P, I64, P, I, P],

@@ -140,10 +140,10 @@ class _TrunkWS:
             self.dX = [z(TM, E) for _ in range(ndir)]
             self.splits = int(min(128, max(1, TM // 1024)))
             S = self.splits
-            self.sl_ih = z(S, 3 * H, E)
-            self.sl_hh = z(S, 3 * H, H)
-            self.cs_ih = z(S, 3 * H)
-            self.cs_hh = z(S, 3 * H)
+            self.sl_ih = [z(S, 3 * H, E) for _ in range(ndir)]
+            self.sl_hh = [z(S, 3 * H, H) for _ in range(ndir)]
+            self.cs_ih = [z(S, 3 * H) for _ in range(ndir)]
+            self.cs_hh = [z(S, 3 * H) for _ in range(ndir)]
 
     @property
     def ntok_ptr(self):
@@ -236,15 +236,25 @@ class Trunk:
 
     def step(self, adam6, tag):
         """Weight gradients + Adam for the trunk (after every use of the weights)."""
-        self._step(adam6, tag)
-
-    def _step(self, adam6, tag):
         w, S = self._pending
+        self._grads(w, S, tag)
+        st = stream_ptr()
+        for d in range(self.ndir):
+            w_ih, w_hh, b_ih, b_hh = self.dirs[d]
+            for prm, sl in ((w_ih, w.sl_ih[d]), (w_hh, w.sl_hh[d]), (b_ih, w.cs_ih[d]), (b_hh, w.cs_hh[d])):
+                call("rg_adam_slabs", prm.p.data_ptr(), prm.m.data_ptr(), prm.v.data_ptr(), sl.data_ptr(), S,
+                     prm.numel(), adam6, None, st)
+        with region("adam_emb"):
+            call("rg_adam_rows", self.emb.p.data_ptr(), self.emb.m.data_ptr(), self.emb.v.data_ptr(),
+                 self.G_emb.data_ptr(), self.tags.data_ptr(), tag, self.N1, self.E, adam6, st)
+        self._pending = None
+
+    def _grads(self, w, S, tag):
         st = stream_ptr()
         H, E, TM = self.H, self.E, w.TM
         skip = -1 if self.train_pad else self.pad
         for d in range(self.ndir):
-            w_ih, w_hh, b_ih, b_hh = self.dirs[d]
+            w_ih = self.dirs[d][0]
             # dX = dGi · W_ih  (T × E)
             with region("gemm_dx"):
                 call("rg_gemm_f32", w.dGi[d].data_ptr(), 3 * H, 1, w_ih.p.data_ptr(), E, 1, w.dX[d].data_ptr(),
@@ -252,18 +262,46 @@ class Trunk:
             # dW_ih = dGiᵀ·X, db_ih = Σ dGi ; dW_hh = dGhᵀ·H_prev, db_hh = Σ dGh  (token splits)
             with region("wgrad"):
                 call("rg_wgrad", w.dGi[d].data_ptr(), 3 * H, w.X[d].data_ptr(), E, TM, w.ntok_ptr, S,
-                     w.sl_ih.data_ptr(), w.cs_ih.data_ptr(), st)
+                     w.sl_ih[d].data_ptr(), w.cs_ih[d].data_ptr(), st)
                 call("rg_wgrad", w.dGh[d].data_ptr(), 3 * H, w.saved[d].data_ptr(), H, TM, w.ntok_ptr, S,
-                     w.sl_hh.data_ptr(), w.cs_hh.data_ptr(), st)
+                     w.sl_hh[d].data_ptr(), w.cs_hh[d].data_ptr(), st)
             with region("scatter"):
                 call("rg_scatter_add", w.tok_id[d].data_ptr(), w.dX[d].data_ptr(), E, w.ntok_ptr, TM, skip,
                      self.G_emb.data_ptr(), self.tags.data_ptr(), tag, st)
-            for prm, sl in ((w_ih, w.sl_ih), (w_hh, w.sl_hh), (b_ih, w.cs_ih), (b_hh, w.cs_hh)):
-                call("rg_adam_slabs", prm.p.data_ptr(), prm.m.data_ptr(), prm.v.data_ptr(), sl.data_ptr(), S,
-                     prm.numel(), adam6, None, st)
+
+    # ---- data-parallel variant: gradients summed over ranks before Adam ----
+    def grads_for_allreduce(self, tag):
+        """Compute this rank's trunk gradients into flat buffers (GRU: gflat,
+        embedding: the dense G_emb table) ready for a SUM all-reduce."""
+        w, S = self._pending
+        self._grads(w, S, tag)
+        if getattr(self, "gflat", None) is None:
+            n = sum(p.numel() for p in self.gru_params[:4 * self.ndir])
+            self.gflat = torch.zeros(n, device=self.device)
+        st = stream_ptr()
+        off = 0
+        for d in range(self.ndir):
+            for prm, sl in zip(self.dirs[d], (w.sl_ih[d], w.sl_hh[d], w.cs_ih[d], w.cs_hh[d])):
+                n = prm.numel()
+                call("rg_adam_slabs", prm.p.data_ptr(), prm.m.data_ptr(), prm.v.data_ptr(), sl.data_ptr(), S, n,
+                     None, self.gflat.data_ptr() + 4 * off, st)
+                off += n
+
+    def allreduce_start(self, comm):
+        return [comm.all_reduce(self.gflat, async_op=True), comm.all_reduce(self.G_emb, async_op=True)]
+
+    def adam_after_allreduce(self, adam6):
+        st = stream_ptr()
+        off = 0
+        for d in range(self.ndir):
+            for prm in self.dirs[d]:
+                n = prm.numel()
+                call("rg_adam_dense", prm.p.data_ptr(), prm.m.data_ptr(), prm.v.data_ptr(),
+                     self.gflat.data_ptr() + 4 * off, n, adam6, 0, st)
+                off += n
         with region("adam_emb"):
-            call("rg_adam_rows", self.emb.p.data_ptr(), self.emb.m.data_ptr(), self.emb.v.data_ptr(),
-                 self.G_emb.data_ptr(), self.tags.data_ptr(), tag, self.N1, E, adam6, st)
+            call("rg_adam_dense", self.emb.p.data_ptr(), self.emb.m.data_ptr(), self.emb.v.data_ptr(),
+                 self.G_emb.data_ptr(), self.emb.numel(), adam6, 1, st)
         self._pending = None
 
 
@@ -289,11 +327,18 @@ class _HeadWS:
 
 
 class SoftmaxHead:
-    """Linear(HF→A) + CrossEntropyLoss(mean) with fused backward/Adam."""
+    """Linear(HF→A) + CrossEntropyLoss(mean) with fused backward/Adam.
+    With ``shard=(lo, hi)`` only items [lo, hi) are held (multi-GPU item
+    sharding); the full init is drawn first so every rank consumes the RNG
+    exactly like the single-GPU (and reference) construction."""
 
-    def __init__(self, name, A, HF, device):
-        self.name, self.A, self.HF, self.device = name, A, HF, device
+    def __init__(self, name, A, HF, device, shard=None):
         w, b = init_linear(HF, A)
+        self.lo, self.hi = (0, A) if shard is None else shard
+        self.A_full = A
+        if shard is not None:
+            w, b = w[self.lo:self.hi].contiguous(), b[self.lo:self.hi].contiguous()
+        self.name, self.A, self.HF, self.device = name, self.hi - self.lo, HF, device
         self.W = Param(f"{name}.weight", w, device)
         self.b = Param(f"{name}.bias", b, device)
         self._ws = {}

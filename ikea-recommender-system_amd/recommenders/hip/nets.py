@@ -21,7 +21,8 @@ class HipNet:
     kind = "gru4rec"
 
     def __init__(self, *, trunk_attr, head_names, hidden_dim, embedding_dim, item_num, state_size, action_dim,
-                 gru_layers, use_packed_seq, train_pad_embed, padding_idx, bidir, device, dropout=0.0):
+                 gru_layers, use_packed_seq, train_pad_embed, padding_idx, bidir, device, dropout=0.0,
+                 comm=None):
         self.hidden_dim = hidden_dim
         self.embedding_dim = embedding_dim
         self.item_num = int(item_num)
@@ -37,7 +38,13 @@ class HipNet:
         self.trunk = Trunk(trunk_attr, self.item_num, embedding_dim, hidden_dim, gru_layers, train_pad_embed,
                            use_packed_seq, self.padding_idx, bidir, self.device)
         self.hf = hidden_dim * (2 if bidir else 1)
-        self.heads = OrderedDict((n, SoftmaxHead(n, action_dim, self.hf, self.device)) for n in head_names)
+        self.comm = comm
+        shard = None
+        if comm is not None:
+            from .dist import item_shard
+            shard = item_shard(action_dim, comm.world, comm.rank)
+        self.heads = OrderedDict((n, SoftmaxHead(n, action_dim, self.hf, self.device, shard=shard))
+                                 for n in head_names)
         for n, hd in self.heads.items():
             setattr(self, n, hd)
         self._dh = {}

@@ -13,6 +13,8 @@ import torch.nn as nn
 
 from recommenders.hip import require_gpu
 from recommenders.hip.engine import AdamClock
+from recommenders.hip.dist import Comm
+from recommenders.hip.sharded import sharded_supervised_step
 from recommenders.hip.supervised import SupervisedNet, supervised_step
 
 
@@ -20,11 +22,12 @@ class GRU4Rec(SupervisedNet):
     """embedding -> GRU -> h[0] -> Linear(H -> A) (reference ``:6-82``)."""
 
     def __init__(self, hidden_size, embedding_dim, item_num, state_size, action_dim, gru_layers=1,
-                 use_packed_seq=True, train_pad_embed=True, padding_idx=None, device="cuda"):
+                 use_packed_seq=True, train_pad_embed=True, padding_idx=None, device="cuda", comm=None):
         super().__init__(trunk_attr="gru", head_names=["output"], hidden_dim=hidden_size,
                          embedding_dim=embedding_dim, item_num=item_num, state_size=state_size,
                          action_dim=action_dim, gru_layers=gru_layers, use_packed_seq=use_packed_seq,
-                         train_pad_embed=train_pad_embed, padding_idx=padding_idx, bidir=False, device=device)
+                         train_pad_embed=train_pad_embed, padding_idx=padding_idx, bidir=False, device=device,
+                         comm=comm)
 
 
 class _AdamFacade:
@@ -49,25 +52,32 @@ class _AdamFacade:
 class GRU4Rec_trainer:
     def __init__(self, hidden_dim, embedding_dim, gru_layers, train_pad_embed, use_packed_seq, learning_rate,
                  item_num, state_size, action_dim, device, padding_idx=None, torch_rand_seed=118,
-                 python_rand_seed=999):
+                 python_rand_seed=999, shard_items=False, process_group=None):
         torch.manual_seed(torch_rand_seed)
         random.seed(python_rand_seed)
         self.device = require_gpu(device)
+        # shard_items (build extension, off by default): multi-GPU weak scaling —
+        # this rank trains its own batch shard, the output layer is split over
+        # the ranks by item id (recommenders/hip/sharded.py).
+        self.comm = Comm(process_group) if shard_items else None
         self.gru_model = GRU4Rec(hidden_size=hidden_dim, embedding_dim=embedding_dim, item_num=item_num,
                                  state_size=state_size, action_dim=action_dim, gru_layers=gru_layers,
                                  use_packed_seq=use_packed_seq, train_pad_embed=train_pad_embed,
-                                 padding_idx=padding_idx, device=self.device)
+                                 padding_idx=padding_idx, device=self.device, comm=self.comm)
         self.learning_rate = learning_rate
         self.cross_entropy_loss = nn.CrossEntropyLoss(weight=None, reduction="mean")
         self.clock = AdamClock(learning_rate)
         self.optimizer = _AdamFacade(self.clock, [self.gru_model])
 
     def train_step(self, s, a, true_len):
-        """One step on (s, a, true_len); returns the CE loss as a Python float."""
-        return supervised_step(self.gru_model, self.clock, s, a, true_len).item()
+        """One step on (s, a, true_len); returns the CE loss as a Python float
+        (with shard_items: the mean over every rank's rows)."""
+        return self.train_step_async(s, a, true_len).item()
 
     def train_step_async(self, s, a, true_len):
         """Same step without the host sync; returns the device loss tensor."""
+        if self.comm is not None:
+            return sharded_supervised_step(self.gru_model, self.clock, s, a, true_len)
         return supervised_step(self.gru_model, self.clock, s, a, true_len)
 
     def set_train(self):

@@ -97,6 +97,14 @@ int rg_lse_combine(const float* pmax, const float* psum, const int32_t* parg, in
                    const float* ZT, int64_t ldz, const int64_t* tgt, int A, float* lse, int32_t* amax,
                    float* loss_row, rg_stream_t stream);
 int rg_sum_scale(const float* x, int n, float scale, float* out, double* out64, rg_stream_t stream);
+/* ---- item-sharded head (multi-GPU; no reference counterpart): rank r owns
+ * items [lo, hi).  lse over all items = logsumexp over ranks of the per-rank
+ * lse (nr x B, rank-major); zt[b] = Z[a_b, b] if a_b is local else 0 (then
+ * summed over ranks); tgt_loc = a - lo; out = a - b elementwise. */
+int rg_lse_merge_ranks(const float* lse_r, int nr, int B, float* lse, rg_stream_t stream);
+int rg_shard_targets(const float* ZT, int64_t ldz, const int64_t* tgt, int64_t lo, int64_t hi, int B, float* zt,
+                     int64_t* tgt_loc, rg_stream_t stream);
+int rg_sub(const float* a, const float* b, int n, float* out, rg_stream_t stream);
 /* backward of CE + Linear w.r.t. h: dh slabs (returns number of slabs > 0). */
 int rg_head_dh(const float* ZT, int64_t ldz, const float* lse, const int64_t* tgt, float gscale, const float* W,
                int B, int A, int HF, int splits, float* slabs, rg_stream_t stream);
