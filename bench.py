@@ -9,8 +9,11 @@ job).  One step = one ``GRU4Rec_trainer.train_step(s, a, true_len)`` on the
 MI355X (pack, gather, GRU fwd, logits + CE, backward, dense Adam over every
 parameter, loss ``.item()``), inputs already resident in HBM.
 
-Multi-GPU (torch.distributed.run, one rank per GPU): weak scaling, each rank
-trains on its own batch shard of 4096 rows.
+Multi-GPU (torch.distributed.run, one rank per GPU, RCCL): weak scaling, each
+rank trains its own 4096-row batch shard; the trunk is replicated (gradient
+all-reduce), the output layer is sharded over ranks by item id (all-gather h,
+LSE merge, reduce-scatter dh) — one optimizer step over the global batch
+(see DESIGN.md §5).
 
 Beside it, on rank 0 at N=1 only: the CPU oracle (the reference's PyTorch-CPU
 math, oracle/) timed on a bounded sample of the same workload.
@@ -102,7 +105,8 @@ def main():
         batches.append((s.to(dev), a.to(dev), ln.to(dev)))
         tok.append(int(ln.sum()))
     tr = GRU4Rec_trainer(hidden_dim=E, embedding_dim=E, gru_layers=1, train_pad_embed=True, use_packed_seq=True,
-                         learning_rate=0.01, item_num=N, state_size=L, action_dim=N, device=dev)
+                         learning_rate=0.01, item_num=N, state_size=L, action_dim=N, device=dev,
+                         shard_items=world > 1)
     tr.set_train()
     for i in range(args.warmup):
         tr.train_step(*batches[i])
@@ -161,7 +165,8 @@ def main():
         "vs_baseline": None, "dtype": "f32", "data": "synthetic (seeded Zipf session stream, random-init weights)",
         "config": {"workload": f"GRU4Rec {N} items, dim{E}, seq_len<={L}, batch {B}/GPU, full-softmax logits",
                    "global_batch": B * world, "seq_len": L, "items": N, "dim": E,
-                   "parallelism": f"replicas{world}" if world > 1 else "single",
+                   "parallelism": (f"dp{world} trunk + {world}-way item-sharded head (RCCL)" if world > 1
+                                   else "single"),
                    "tokens_per_batch": int(np.mean(tok))},
         "roofline": roof, "cpu_baseline": cpu, "kernel_ms": kern,
         "loss_first_last": [round(losses[0], 5), round(losses[-1], 5)],
