@@ -51,6 +51,7 @@ def parse():
     ap.add_argument("--cpu-steps", type=int, default=6)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-timing", action="store_true")
+    ap.add_argument("--force-shard", action="store_true", help="item-sharded path even at world 1 (test)")
     return ap.parse_args()
 
 
@@ -85,7 +86,7 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
+    if world > 1 or args.force_shard:
         import torch.distributed as dist
         torch.cuda.set_device(local)
         dist.init_process_group("nccl")
@@ -106,7 +107,7 @@ def main():
         tok.append(int(ln.sum()))
     tr = GRU4Rec_trainer(hidden_dim=E, embedding_dim=E, gru_layers=1, train_pad_embed=True, use_packed_seq=True,
                          learning_rate=0.01, item_num=N, state_size=L, action_dim=N, device=dev,
-                         shard_items=world > 1)
+                         shard_items=world > 1 or args.force_shard)
     tr.set_train()
     for i in range(args.warmup):
         tr.train_step(*batches[i])
@@ -134,7 +135,7 @@ def main():
     if not all(np.isfinite(losses)):
         raise RuntimeError(f"non-finite loss {losses}")
     if rank != 0:
-        if world > 1:
+        if torch.distributed.is_initialized():
             torch.distributed.destroy_process_group()
         return
     ms = dt / args.steps * 1e3
@@ -172,7 +173,7 @@ def main():
         "loss_first_last": [round(losses[0], 5), round(losses[-1], 5)],
     }
     print(json.dumps(line), flush=True)
-    if world > 1:
+    if torch.distributed.is_initialized():
         torch.distributed.destroy_process_group()
 
 

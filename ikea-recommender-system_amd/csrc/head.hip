@@ -84,15 +84,18 @@ __global__ __launch_bounds__(256) void k_head_fwd(const float* __restrict__ h, c
   }
   const int nch = (B + 31) / 32;
   f4 pre[NL];
+  float keep[NL];
   auto load_chunk = [&](int c) {
+    // branch-free: clamp the row and zero it when committing to LDS, so the
+    // loads stay in flight across the MFMA phase
 #pragma unroll
     for (int i = 0; i < NL; ++i) {
-      int e = tid + 256 * i;
-      int rr = e / (HF / 4), c4 = e % (HF / 4);
-      int b = c * 32 + rr;
-      f4 v = {0.f, 0.f, 0.f, 0.f};
-      if (e < NV && b < B) v = *reinterpret_cast<const f4*>(h + (int64_t)b * HF + 4 * c4);
-      pre[i] = v;
+      const int e = tid + 256 * i;
+      const int rr = (e < NV ? e : 0) / (HF / 4), c4 = e % (HF / 4);
+      const int b = c * 32 + rr;
+      const int bc = b < B ? b : B - 1;
+      pre[i] = *reinterpret_cast<const f4*>(h + (int64_t)bc * HF + 4 * c4);
+      keep[i] = (e < NV && b < B) ? 1.f : 0.f;
     }
   };
   auto store_chunk = [&](int buf) {
@@ -101,7 +104,7 @@ __global__ __launch_bounds__(256) void k_head_fwd(const float* __restrict__ h, c
       int e = tid + 256 * i;
       if (e < NV) {
         int rr = e / (HF / 4), c4 = e % (HF / 4);
-        *reinterpret_cast<f4*>(&hbuf[buf][rr][4 * c4]) = pre[i];
+        *reinterpret_cast<f4*>(&hbuf[buf][rr][4 * c4]) = pre[i] * keep[i];
       }
     }
   };
@@ -121,28 +124,54 @@ __global__ __launch_bounds__(256) void k_head_fwd(const float* __restrict__ h, c
       acc = mfma32(Wreg[s + 2], hv.z, acc);
       acc = mfma32(Wreg[s + 3], hv.w, acc);
     }
+    // Commit the prefetched chunk to LDS before this chunk's Zᵀ stores are
+    // issued: vmcnt counts loads and stores in issue order, so waiting for the
+    // prefetch after the stores would stall the wave until the stores retire.
+    if (c + 1 < nch) store_chunk(cur ^ 1);
     const int b = c * 32 + l32;
     const bool bv = b < B;
     float m = NEG_INF, sum = 0.f;
     int arg = INT32_MAX;
+    if (jw + 32 <= A) {  // wave-uniform: every item row of this wave exists
+      if (ZT && bv) {
+        float* zc = ZT + b;
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int j = jw + acc32_row(r, half);
-      const float z = acc[r] + bj[r];
-      acc[r] = z;
-      if (j < A) {
-        if (ZT && bv) ZT[(int64_t)j * ldz + b] = z;
-        if (z > m) {
-          m = z;
-          arg = j;
-        }
+        for (int r = 0; r < 16; ++r) zc[(int64_t)(jw + acc32_row(r, half)) * ldz] = acc[r] + bj[r];
       }
-    }
-    if (want_sum && arg != INT32_MAX) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float z = acc[r] + bj[r];
+        acc[r] = z;
+        const bool gt = z > m;
+        m = gt ? z : m;
+        arg = gt ? jw + acc32_row(r, half) : arg;
+      }
+      if (want_sum) {
+        const float m2 = m * 1.4426950408889634f;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) sum += __builtin_amdgcn_exp2f(fmaf(acc[r], 1.4426950408889634f, -m2));
+      }
+    } else {
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int j = jw + acc32_row(r, half);
-        if (j < A) sum += expf(acc[r] - m);
+        const float z = acc[r] + bj[r];
+        acc[r] = z;
+        if (j < A) {
+          if (ZT && bv) ZT[(int64_t)j * ldz + b] = z;
+          if (z > m) {
+            m = z;
+            arg = j;
+          }
+        }
+      }
+      if (want_sum && arg != INT32_MAX) {
+        const float m2 = m * 1.4426950408889634f;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int j = jw + acc32_row(r, half);
+          if (j < A) sum += __builtin_amdgcn_exp2f(fmaf(acc[r], 1.4426950408889634f, -m2));
+        }
       }
     }
     {
@@ -156,7 +185,6 @@ __global__ __launch_bounds__(256) void k_head_fwd(const float* __restrict__ h, c
       ss[cur][w][l32] = sum;
       sa[cur][w][l32] = arg;
     }
-    if (c + 1 < nch) store_chunk(cur ^ 1);
     __syncthreads();
     if (w == 0 && half == 0 && bv) {
       float M = sm[cur][0][l32], S = ss[cur][0][l32];
@@ -307,7 +335,7 @@ __global__ __launch_bounds__(256) void k_head_dh(const float* __restrict__ ZT, i
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     v4[q] = (bq + q) < B;
-    l4[q] = v4[q] ? lse[bq + q] : 0.f;
+    l4[q] = v4[q] ? lse[bq + q] * 1.4426950408889634f : 0.f;  // lse in log2 units
     t4[q] = v4[q] ? tgt[bq + q] : -1;
   }
   f4 zp[4];
@@ -339,7 +367,8 @@ __global__ __launch_bounds__(256) void k_head_dh(const float* __restrict__ ZT, i
       f4 d;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        float p = expf(zp[i][q] - l4[q]) - ((int64_t)j == t4[q] ? 1.0f : 0.0f);
+        float p = __builtin_amdgcn_exp2f(fmaf(zp[i][q], 1.4426950408889634f, -l4[q])) -
+                  ((int64_t)j == t4[q] ? 1.0f : 0.0f);
         d[q] = (v4[q] && j < je) ? p * gscale : 0.0f;
       }
       *reinterpret_cast<f4*>(&zt[buf][jj][4 * c4]) = d;
@@ -447,7 +476,7 @@ __global__ __launch_bounds__(256) void k_head_dw_adam(const float* __restrict__ 
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const bool v = (bq + q) < B;
-      l4[q] = v ? lse[bq + q] : 0.f;
+      l4[q] = v ? lse[bq + q] * 1.4426950408889634f : 0.f;  // lse in log2 units
       t4[q] = v ? tgt[bq + q] : -2;
     }
 #pragma unroll
@@ -475,7 +504,8 @@ __global__ __launch_bounds__(256) void k_head_dw_adam(const float* __restrict__ 
       f4 d;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        float p = expf(zp[i][q] - l4[q]) - ((int64_t)j == t4[q] ? 1.0f : 0.0f);
+        float p = __builtin_amdgcn_exp2f(fmaf(zp[i][q], 1.4426950408889634f, -l4[q])) -
+                  ((int64_t)j == t4[q] ? 1.0f : 0.0f);
         d[q] = ((bq + q) < B && j < A) ? p * gscale : 0.0f;
       }
       dbp[i] += (d[0] + d[1]) + (d[2] + d[3]);

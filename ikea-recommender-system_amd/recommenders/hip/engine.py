@@ -322,7 +322,8 @@ class _HeadWS:
         self.amax = z(B, dt=torch.int32)
         self.loss_row = z(B)
         self.loss = torch.zeros(1, device=device)
-        self.dh_splits = 16 if A >= 16 * 4096 else max(1, A // 4096)
+        # dh kernel: ~512 workgroups of 128 rows x one item split (2 per CU)
+        self.dh_splits = int(max(1, min(16, 512 // ((B + 127) // 128), A // 1024)))
         self.dh_slabs = z(self.dh_splits, B, HF) if store_z else None
 
 

@@ -1,0 +1,83 @@
+"""Time the three full-softmax head kernels standalone at C2 shapes
+(B 4096, A 1M, H 128) with HIP events; prints ms and fp32 TFLOP/s."""
+import argparse
+import os
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(HERE, "..", "ikea-recommender-system_amd"))
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from recommenders.hip import call, stream_ptr  # noqa: E402
+from recommenders.hip.engine import AdamClock  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--B", type=int, default=4096)
+ap.add_argument("--A", type=int, default=1_000_000)
+ap.add_argument("--H", type=int, default=128)
+ap.add_argument("--iters", type=int, default=5)
+a = ap.parse_args()
+B, A, H = a.B, a.A, a.H
+dev = "cuda"
+g = torch.Generator(device=dev).manual_seed(0)
+h = torch.randn(B, H, device=dev, generator=g) * 0.3
+W = torch.randn(A, H, device=dev, generator=g) * 0.05
+bias = torch.randn(A, device=dev, generator=g) * 0.05
+tgt = torch.randint(0, A, (B,), device=dev, generator=g)
+ldz = (B + 3) // 4 * 4
+nJ = (A + 127) // 128
+ZT = torch.empty(A, ldz, device=dev)
+pm = torch.empty(nJ, B, device=dev)
+ps = torch.empty(nJ, B, device=dev)
+pa = torch.empty(nJ, B, dtype=torch.int32, device=dev)
+work = torch.empty(3 * 64 * B, device=dev)
+lse = torch.empty(B, device=dev)
+amax = torch.empty(B, dtype=torch.int32, device=dev)
+lrow = torch.empty(B, device=dev)
+NS = int(max(1, min(16, 512 // ((B + 127) // 128), A // 1024)))
+slabs = torch.empty(NS, B, H, device=dev)
+mW, vW = torch.zeros_like(W), torch.zeros_like(W)
+mb, vb = torch.zeros_like(bias), torch.zeros_like(bias)
+clock = AdamClock(1e-3)
+st = stream_ptr()
+fl = 2.0 * B * A * H
+
+
+def fwd():
+    call("rg_head_fwd", h.data_ptr(), W.data_ptr(), bias.data_ptr(), B, A, H, ZT.data_ptr(), ldz, pm.data_ptr(),
+         ps.data_ptr(), pa.data_ptr(), 1, st)
+
+
+def lsec():
+    call("rg_lse_combine", pm.data_ptr(), ps.data_ptr(), pa.data_ptr(), B, nJ, work.data_ptr(), ZT.data_ptr(), ldz,
+         tgt.data_ptr(), A, lse.data_ptr(), amax.data_ptr(), lrow.data_ptr(), st)
+
+
+def dh():
+    call("rg_head_dh", ZT.data_ptr(), ldz, lse.data_ptr(), tgt.data_ptr(), 1.0 / B, W.data_ptr(), B, A, H, NS,
+         slabs.data_ptr(), st)
+
+
+def dw():
+    call("rg_head_dw_adam", ZT.data_ptr(), ldz, lse.data_ptr(), tgt.data_ptr(), 1.0 / B, h.data_ptr(), B, A, H,
+         W.data_ptr(), mW.data_ptr(), vW.data_ptr(), bias.data_ptr(), mb.data_ptr(), vb.data_ptr(),
+         clock.next_args(), None, None, st)
+
+
+fwd(); lsec(); dh(); dw()
+torch.cuda.synchronize()
+res = {}
+for name, fn in (("head_fwd", fwd), ("lse", lsec), ("head_dh", dh), ("head_dw_adam", dw)):
+    ts = []
+    for _ in range(a.iters):
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record()
+        fn()
+        e1.record()
+        torch.cuda.synchronize()
+        ts.append(e0.elapsed_time(e1))
+    res[name] = float(np.median(ts))
+for k, v in res.items():
+    print(f"{k:14s} {v:8.3f} ms  {fl / (v * 1e-3) / 1e12:7.1f} TF/s")
