@@ -1,0 +1,339 @@
+// Sampled-softmax output head (SURVEY §8 A7 "sampled/BPR ext.", config C3, and
+// the north-star "embedding gather + sampled logits" step).
+//
+// Not in the reference (its loss is the full-softmax CrossEntropyLoss of
+// GRU4Rec/model.py:121,146); the build defines it (parity pinned
+// by the build's own CPU restatement, oracle/models.py:sampled_ce):
+//   z_b,pos = h_b·W[a_b] + bias[a_b]
+//   z_b,s   = h_b·W[neg_s] + bias[neg_s]            s < S, shared by the batch
+//   loss    = mean_b [ logsumexp(z_b,pos, z_b,0..S-1) − z_b,pos ]
+// Negatives are drawn uniformly on [0, A) with replacement; collisions with
+// the target or with each other are kept and no logQ correction is applied
+// (a uniform proposal shifts every logit by the same constant).
+//
+//  k_sample_uniform: counter-based draw (splitmix64 of seed/step/slot, then
+//                    the high 64 bits of x·A) — reproducible bit-for-bit on
+//                    the host without any RNG state.
+//  k_sampled_fwd   : 128-negative × 128-row logit tile per workgroup.  The
+//                    negatives' W rows are gathered straight from the table
+//                    and staged with the h rows through LDS in 32-wide k
+//                    chunks (double-buffered, register prefetch); four waves
+//                    each own a 64×64 block = 2×2 v_mfma_f32_32x32x2_f32.
+//                    Epilogue: + bias, Zᵀ[s][b] stores (consecutive b per
+//                    half-wave) and per-(tile, row) online (max, Σexp)
+//                    partials.  Row-tile 0 also writes the gathered W/bias
+//                    rows (Wg, bg) that both backward GEMMs consume.
+//  k_sampled_lse   : one wave per row: the positive logit as a wave-shuffle
+//                    dot product, the tile partials merged by shuffles, lse,
+//                    loss_b, and the positive's gradient rows.
+//  k_sampled_dz    : dZᵀ = exp(Zᵀ − lse)·g in place, one workgroup per
+//                    negative, with the bias gradient as its row sum.
+#include "common.h"
+
+#define SF_T 128
+#define SF_KC 32
+#define SF_LD (SF_KC + 4)
+
+__device__ __forceinline__ uint64_t mix64(uint64_t z) {
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+__global__ void k_sample_uniform(uint64_t seed, uint64_t counter, int S, uint64_t A, int32_t* __restrict__ out) {
+  const int s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= S) return;
+  const uint64_t x = mix64(seed + 0x9E3779B97F4A7C15ull * (counter * (uint64_t)S + (uint64_t)s + 1ull));
+  out[s] = (int32_t)__umul64hi(x, A);
+}
+
+extern "C" int rg_sample_uniform(uint64_t seed, uint64_t counter, int S, int64_t A, int32_t* out,
+                                 hipStream_t stream) {
+  if (S <= 0 || A <= 0 || A > INT32_MAX) return RG_ERR_ARG;
+  hipLaunchKernelGGL(k_sample_uniform, dim3((S + 255) / 256), dim3(256), 0, stream, seed, counter, S, (uint64_t)A,
+                     out);
+  RG_LAUNCH_CHECK();
+  return RG_OK;
+}
+
+__device__ __forceinline__ void lse_merge(float& m, float& s, float m2, float s2) {
+  const float M = fmaxf(m, m2);
+  if (M == -__builtin_inff()) return;  // both empty
+  s = s * __expf(m - M) + s2 * __expf(m2 - M);
+  m = M;
+}
+
+// ------------------------------------------------------------------ fwd ----
+template <int HF>
+__global__ __launch_bounds__(256) void k_sampled_fwd(const float* __restrict__ h, const float* __restrict__ W,
+                                                     const float* __restrict__ bias,
+                                                     const int32_t* __restrict__ neg, int B, int S,
+                                                     float* __restrict__ ZT, int64_t ldz,
+                                                     float* __restrict__ pmax, float* __restrict__ psum,
+                                                     float* __restrict__ Wg, float* __restrict__ bg) {
+  constexpr int NK = HF / SF_KC;
+  __shared__ __attribute__((aligned(16))) float Ws[2][SF_T][SF_LD];
+  __shared__ __attribute__((aligned(16))) float Hs[2][SF_T][SF_LD];
+  __shared__ float sb[SF_T];
+  __shared__ float rm[2][SF_T], rs[2][SF_T];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, half = lane >> 5, l32 = lane & 31;
+  const int wm = w >> 1, wn = w & 1;
+  const int s0 = blockIdx.x * SF_T, b0 = blockIdx.y * SF_T;
+  const bool emit = Wg != nullptr && blockIdx.y == 0;
+  // staging: this thread moves float4 column c4 of rows (tid >> 3) + 32 i
+  const int c4 = tid & 7;
+  const float* wrow[4];
+  const float* hrow[4];
+  float wk[4], hk[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int r = (tid >> 3) + 32 * i;
+    const int s = s0 + r, b = b0 + r;
+    const int id = s < S ? neg[s] : 0;
+    wrow[i] = W + (int64_t)id * HF + 4 * c4;
+    wk[i] = s < S ? 1.f : 0.f;
+    hrow[i] = h + (int64_t)(b < B ? b : B - 1) * HF + 4 * c4;
+    hk[i] = b < B ? 1.f : 0.f;
+  }
+  if (tid < SF_T) {
+    const int s = s0 + tid;
+    const float bv = s < S ? bias[neg[s]] : 0.f;
+    sb[tid] = bv;
+    if (emit && s < S) bg[s] = bv;
+  }
+  f4 pw[4], ph[4];
+  auto load = [&](int k0) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      pw[i] = *reinterpret_cast<const f4*>(wrow[i] + k0);
+      ph[i] = *reinterpret_cast<const f4*>(hrow[i] + k0);
+    }
+  };
+  auto commit = [&](int buf, int k0) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int r = (tid >> 3) + 32 * i;
+      const f4 x = pw[i] * wk[i];
+      *reinterpret_cast<f4*>(&Ws[buf][r][4 * c4]) = x;
+      *reinterpret_cast<f4*>(&Hs[buf][r][4 * c4]) = ph[i] * hk[i];
+      if (emit && s0 + r < S) *reinterpret_cast<f4*>(Wg + (int64_t)(s0 + r) * HF + k0 + 4 * c4) = x;
+    }
+  };
+  f16v acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f16v{};
+  load(0);
+  commit(0, 0);
+  __syncthreads();
+  int cur = 0;
+#pragma unroll 1
+  for (int kc = 0; kc < NK; ++kc) {
+    const bool more = kc + 1 < NK;
+    if (more) load((kc + 1) * SF_KC);
+    const float* wa = &Ws[cur][64 * wm + l32][half * (SF_KC / 2)];
+    const float* hb = &Hs[cur][64 * wn + l32][half * (SF_KC / 2)];
+#pragma unroll
+    for (int k = 0; k < SF_KC / 2; k += 4) {
+      const f4 a0 = *reinterpret_cast<const f4*>(wa + k);
+      const f4 a1 = *reinterpret_cast<const f4*>(wa + 32 * SF_LD + k);
+      const f4 x0 = *reinterpret_cast<const f4*>(hb + k);
+      const f4 x1 = *reinterpret_cast<const f4*>(hb + 32 * SF_LD + k);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        acc[0][0] = mfma32(a0[q], x0[q], acc[0][0]);
+        acc[0][1] = mfma32(a0[q], x1[q], acc[0][1]);
+        acc[1][0] = mfma32(a1[q], x0[q], acc[1][0]);
+        acc[1][1] = mfma32(a1[q], x1[q], acc[1][1]);
+      }
+    }
+    if (more) commit(cur ^ 1, (kc + 1) * SF_KC);
+    __syncthreads();
+    cur ^= 1;
+  }
+  // epilogue: bias, Zᵀ stores, online (max, Σexp) over this tile's negatives
+#pragma unroll
+  for (int nb = 0; nb < 2; ++nb) {
+    const int bl = 64 * wn + 32 * nb + l32;
+    const int b = b0 + bl;
+    const bool bv = b < B;
+    float m = -__builtin_inff(), sum = 0.f;
+#pragma unroll
+    for (int mb = 0; mb < 2; ++mb) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int sl = 64 * wm + 32 * mb + acc32_row(r, half);
+        const float z = acc[mb][nb][r] + sb[sl];
+        acc[mb][nb][r] = z;
+        if (s0 + sl < S) {
+          if (bv && ZT) ZT[(int64_t)(s0 + sl) * ldz + b] = z;
+          m = fmaxf(m, z);
+        }
+      }
+    }
+    if (m != -__builtin_inff()) {
+      const float m2 = m * 1.4426950408889634f;
+#pragma unroll
+      for (int mb = 0; mb < 2; ++mb)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int sl = 64 * wm + 32 * mb + acc32_row(r, half);
+          if (s0 + sl < S) sum += __builtin_amdgcn_exp2f(fmaf(acc[mb][nb][r], 1.4426950408889634f, -m2));
+        }
+    }
+    lse_merge(m, sum, __shfl_xor(m, 32), __shfl_xor(sum, 32));
+    if (half == 0) {
+      rm[wm][bl] = m;
+      rs[wm][bl] = sum;
+    }
+  }
+  __syncthreads();
+  if (tid < SF_T && b0 + tid < B) {
+    float m = rm[0][tid], s = rs[0][tid];
+    lse_merge(m, s, rm[1][tid], rs[1][tid]);
+    const int64_t o = (int64_t)blockIdx.x * B + b0 + tid;
+    pmax[o] = m;
+    psum[o] = s;
+  }
+}
+
+extern "C" int rg_sampled_fwd(const float* h, const float* W, const float* bias, const int32_t* neg, int B, int S,
+                              int HF, float* ZT, int64_t ldz, float* pmax, float* psum, float* Wg, float* bg,
+                              hipStream_t stream) {
+  if (B <= 0 || S <= 0) return RG_ERR_ARG;
+  if (ZT && ldz < B) return RG_ERR_ARG;
+  if ((Wg == nullptr) != (bg == nullptr)) return RG_ERR_ARG;
+  dim3 grid((S + SF_T - 1) / SF_T, (B + SF_T - 1) / SF_T);
+#define SFL(HFV)                                                                                            \
+  hipLaunchKernelGGL(k_sampled_fwd<HFV>, grid, dim3(256), 0, stream, h, W, bias, neg, B, S, ZT, ldz, pmax, \
+                     psum, Wg, bg)
+  switch (HF) {
+    case 32: SFL(32); break;
+    case 64: SFL(64); break;
+    case 128: SFL(128); break;
+    case 256: SFL(256); break;
+    default: return RG_ERR_SHAPE;
+  }
+#undef SFL
+  RG_LAUNCH_CHECK();
+  return RG_OK;
+}
+
+// ------------------------------------------------------------------ lse ----
+// One wave per row b.  Outputs: lse[b]; loss_row[b] = lse − z_pos (NaN for an
+// out-of-range target, as CrossEntropyLoss raises); ids[b] = a_b (int32, −1
+// if invalid) for the gradient scatter; dzpos[b] = (p_pos − 1)·g; gpos[b] =
+// dzpos·h_b (∂/∂W[a_b]); dhpos[b] = dzpos·W[a_b] (∂/∂h_b, positive part).
+template <int HF>
+__global__ __launch_bounds__(256) void k_sampled_lse(const float* __restrict__ h, const float* __restrict__ W,
+                                                     const float* __restrict__ bias,
+                                                     const int64_t* __restrict__ tgt, int B, int64_t A,
+                                                     const float* __restrict__ pmax,
+                                                     const float* __restrict__ psum, int nT, float gscale,
+                                                     float* __restrict__ lse, float* __restrict__ loss_row,
+                                                     int32_t* __restrict__ ids, float* __restrict__ dzpos,
+                                                     float* __restrict__ gpos, float* __restrict__ dhpos) {
+  constexpr int PER = HF >= 64 ? HF / 64 : 1;
+  const int lane = threadIdx.x & 63;
+  const int b = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (b >= B) return;  // whole wave
+  const int64_t t = tgt[b];
+  const bool ok = t >= 0 && t < A;
+  const int64_t tt = ok ? t : 0;
+  float hv[PER], wv[PER];
+  float dot = 0.f;
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    const int c = lane + 64 * i;
+    const bool cv = c < HF;
+    hv[i] = cv ? h[(int64_t)b * HF + c] : 0.f;
+    wv[i] = cv ? W[tt * HF + c] : 0.f;
+    dot = fmaf(hv[i], wv[i], dot);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) dot += __shfl_xor(dot, o);
+  const float zp = dot + bias[tt];
+  float m = -__builtin_inff(), s = 0.f;
+  for (int j = lane; j < nT; j += 64) lse_merge(m, s, pmax[(int64_t)j * B + b], psum[(int64_t)j * B + b]);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) lse_merge(m, s, __shfl_xor(m, o), __shfl_xor(s, o));
+  lse_merge(m, s, zp, 1.f);
+  const float l = m + logf(s);
+  const float dp = (expf(zp - l) - 1.f) * gscale;
+  if (lane == 0) {
+    lse[b] = l;
+    loss_row[b] = ok ? l - zp : __builtin_nanf("");
+    ids[b] = ok ? (int32_t)t : -1;
+    dzpos[b] = ok ? dp : 0.f;
+  }
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    const int c = lane + 64 * i;
+    if (c < HF) {
+      gpos[(int64_t)b * HF + c] = ok ? dp * hv[i] : 0.f;
+      dhpos[(int64_t)b * HF + c] = ok ? dp * wv[i] : 0.f;
+    }
+  }
+}
+
+extern "C" int rg_sampled_lse(const float* h, const float* W, const float* bias, const int64_t* tgt, int B,
+                              int64_t A, int HF, const float* pmax, const float* psum, int nT, float gscale,
+                              float* lse, float* loss_row, int32_t* ids, float* dzpos, float* gpos, float* dhpos,
+                              hipStream_t stream) {
+  if (B <= 0 || A <= 0 || nT <= 0) return RG_ERR_ARG;
+  dim3 grid((B + 3) / 4);
+#define SLL(HFV)                                                                                              \
+  hipLaunchKernelGGL(k_sampled_lse<HFV>, grid, dim3(256), 0, stream, h, W, bias, tgt, B, A, pmax, psum, nT, \
+                     gscale, lse, loss_row, ids, dzpos, gpos, dhpos)
+  switch (HF) {
+    case 32: SLL(32); break;
+    case 64: SLL(64); break;
+    case 128: SLL(128); break;
+    case 256: SLL(256); break;
+    default: return RG_ERR_SHAPE;
+  }
+#undef SLL
+  RG_LAUNCH_CHECK();
+  return RG_OK;
+}
+
+// ------------------------------------------------------------------- dZ ----
+// dZᵀ[s][b] = exp(Zᵀ[s][b] − lse[b])·g for b < B (in place); dbg[s] = Σ_b dZᵀ[s][b]
+// in a fixed order (deterministic).  One workgroup per negative s.
+__global__ __launch_bounds__(256) void k_sampled_dz(float* __restrict__ ZT, int64_t ldz,
+                                                    const float* __restrict__ lse, int B, float gscale,
+                                                    float* __restrict__ dbg) {
+  __shared__ float red[4];
+  const int s = blockIdx.x;
+  float* row = ZT + (int64_t)s * ldz;
+  float acc = 0.f;
+  const int nb4 = B >> 2;
+  for (int i = threadIdx.x; i < nb4; i += 256) {
+    f4 z = reinterpret_cast<f4*>(row)[i];
+    const f4 l = reinterpret_cast<const f4*>(lse)[i];
+    f4 d;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) d[q] = __expf(z[q] - l[q]) * gscale;
+    reinterpret_cast<f4*>(row)[i] = d;
+    acc += (d[0] + d[1]) + (d[2] + d[3]);
+  }
+  for (int b = 4 * nb4 + threadIdx.x; b < B; b += 256) {
+    const float d = __expf(row[b] - lse[b]) * gscale;
+    row[b] = d;
+    acc += d;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) dbg[s] = (red[0] + red[1]) + (red[2] + red[3]);
+}
+
+extern "C" int rg_sampled_dz(float* ZT, int64_t ldz, const float* lse, int B, int S, float gscale, float* dbg,
+                             hipStream_t stream) {
+  if (B <= 0 || S <= 0 || ldz < B || (ldz & 3)) return RG_ERR_ARG;
+  hipLaunchKernelGGL(k_sampled_dz, dim3(S), dim3(256), 0, stream, ZT, ldz, lse, B, gscale, dbg);
+  RG_LAUNCH_CHECK();
+  return RG_OK;
+}

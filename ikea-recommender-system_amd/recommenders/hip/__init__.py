@@ -19,6 +19,7 @@ I64 = C.c_int64
 F = C.c_float
 D = C.c_double
 I32 = C.c_int32
+U64 = C.c_uint64
 
 # name -> argtypes (restype int for all)
 SIGNATURES = {
@@ -53,6 +54,10 @@ SIGNATURES = {
     "rg_topk": [P, I64, P, I, I, I, P, P, P, P],
     "rg_hits_ndcg": [P, I, P, I, P, I, P, P],
     "rg_mask_scale": [P, P, F, I64, P, P],
+    "rg_sample_uniform": [U64, U64, I, I64, P, P],
+    "rg_sampled_fwd": [P, P, P, P, I, I, I, P, I64, P, P, P, P, P],
+    "rg_sampled_lse": [P, P, P, P, I, I64, I, P, P, I, F, P, P, P, P, P, P, P],
+    "rg_sampled_dz": [P, I64, P, I, I, F, P, P],
     "rg_weighted_sum": [P, P, I, I64, P, P],
     "rg_stack_rewards": [P, P, P, I, P, P],
 }

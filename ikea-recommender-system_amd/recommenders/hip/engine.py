@@ -405,3 +405,111 @@ class SoftmaxHead:
         call("rg_lse_combine", w.pmax.data_ptr(), w.psum.data_ptr(), w.parg.data_ptr(), B, w.nJ, w.work.data_ptr(),
              None, 0, None, self.A, None, w.amax.data_ptr(), None, st)
         return w.amax
+
+
+# --------------------------------------------------------- sampled head ----
+class _SampledWS:
+    def __init__(self, B, S, HF, device):
+        z = lambda *s, dt=torch.float32: torch.empty(*s, dtype=dt, device=device)
+        self.B, self.S = B, S
+        self.ldz = _round_up(B, 4)
+        self.nT = (S + 127) // 128
+        self.ZT = z(S, self.ldz)
+        self.pmax = z(self.nT, B)
+        self.psum = z(self.nT, B)
+        self.lse = z(B)
+        self.loss_row = z(B)
+        self.loss = torch.zeros(1, device=device)
+        # scatter lists: rows [0, S) = the negatives, [S, S+B) = the targets
+        self.ids = z(S + B, dt=torch.int32)
+        self.grows = z(S + B, HF)       # ∂/∂W rows
+        self.gb = z(S + B)              # ∂/∂bias entries
+        self.nrows = torch.full((1,), S + B, dtype=torch.int32, device=device)
+        self.Wg = z(S, HF)
+        self.bg = z(S)
+        self.dh_splits = max(1, min(8, S // 256))
+        self.dw_splits = max(1, min(16, B // 256))
+        # slab 0 = the positive part of dh (written by rg_sampled_lse)
+        self.dh_slabs = z(self.dh_splits + 1, B, HF)
+        self.dw_slabs = z(self.dw_splits, S, HF)
+
+
+class SampledSoftmaxHead(SoftmaxHead):
+    """Linear(HF→A) trained with a sampled softmax: CE over the target and
+    ``n_neg`` negatives shared by the batch, drawn uniformly with replacement
+    from a counter-based stream (``seed``, draw index) — csrc/sampled.hip.
+    Build-defined (SURVEY §8 A7 ext., config C3); evaluation (``logits_T``,
+    ``argmax``) still scores every item.  Same parameters, init order and
+    state_dict keys as SoftmaxHead; Adam stays dense (rows the step did not
+    touch see g = 0, as torch.optim.Adam would)."""
+
+    def __init__(self, name, A, HF, device, n_neg, seed=0):
+        if HF % 32 or HF > 256:
+            raise ValueError(f"sampled softmax needs head width in {{32, 64, 128, 256}}, got {HF}")
+        if n_neg <= 0:
+            raise ValueError("n_negatives must be positive")
+        super().__init__(name, A, HF, device)
+        self.S = int(n_neg)
+        self.seed = int(seed) & (2**64 - 1)
+        self.draws = 0
+        self.G = torch.zeros_like(self.W.p)
+        self.Gb = torch.zeros_like(self.b.p)
+        self.tags = torch.zeros(A, dtype=torch.int32, device=device)
+        self.tag = 0
+        self._sws = {}
+
+    def sws(self, slot, B):
+        w = self._sws.get(slot)
+        if w is None or w.B != B:
+            w = _SampledWS(B, self.S, self.HF, self.device)
+            self._sws[slot] = w
+        return w
+
+    def forward_loss(self, h, tgt, slot="main"):
+        B = h.shape[0]
+        w = self.sws(slot, B)
+        st = stream_ptr()
+        g = _f32(1.0 / B)
+        call("rg_sample_uniform", self.seed, self.draws, self.S, self.A, w.ids.data_ptr(), st)
+        self.draws += 1
+        with region("sampled_fwd"):
+            call("rg_sampled_fwd", h.data_ptr(), self.W.p.data_ptr(), self.b.p.data_ptr(), w.ids.data_ptr(), B,
+                 self.S, self.HF, w.ZT.data_ptr(), w.ldz, w.pmax.data_ptr(), w.psum.data_ptr(), w.Wg.data_ptr(),
+                 w.bg.data_ptr(), st)
+        call("rg_sampled_lse", h.data_ptr(), self.W.p.data_ptr(), self.b.p.data_ptr(), tgt.data_ptr(), B, self.A,
+             self.HF, w.pmax.data_ptr(), w.psum.data_ptr(), w.nT, g, w.lse.data_ptr(), w.loss_row.data_ptr(),
+             w.ids.data_ptr() + 4 * self.S, w.gb.data_ptr() + 4 * self.S,
+             w.grows.data_ptr() + 4 * self.S * self.HF, w.dh_slabs.data_ptr(), st)
+        call("rg_sum_scale", w.loss_row.data_ptr(), B, g, w.loss.data_ptr(), None, st)
+        return w.loss, w
+
+    def backward_step(self, h, tgt, dh_out, adam6, slot="main", gscale=None):
+        B = h.shape[0]
+        w = self.sws(slot, B)
+        st = stream_ptr()
+        S, HF = self.S, self.HF
+        g = _f32(1.0 / B)
+        if gscale is not None and gscale != g:
+            raise NotImplementedError("sampled softmax: the loss scale is fixed at 1/B (set in forward_loss)")
+        with region("sampled_bwd"):
+            call("rg_sampled_dz", w.ZT.data_ptr(), w.ldz, w.lse.data_ptr(), B, S, g, w.gb.data_ptr(), st)
+            # dh = dZ · Wg (+ the positive part already in slab 0)
+            call("rg_gemm_f32", w.ZT.data_ptr(), 1, w.ldz, w.Wg.data_ptr(), HF, 1,
+                 w.dh_slabs.data_ptr() + 4 * B * HF, HF, None, B, None, HF, S, None, w.dh_splits, st)
+            call("rg_reduce_slabs", w.dh_slabs.data_ptr(), w.dh_splits + 1, B * HF, dh_out.data_ptr(), None, HF, 0,
+                 st)
+            # dWg = dZᵀ · h  -> rows [0, S) of the scatter list
+            call("rg_gemm_f32", w.ZT.data_ptr(), w.ldz, 1, h.data_ptr(), HF, 1, w.dw_slabs.data_ptr(), HF, None,
+                 S, None, HF, B, None, w.dw_splits, st)
+            call("rg_reduce_slabs", w.dw_slabs.data_ptr(), w.dw_splits, S * HF, w.grows.data_ptr(), None, HF, 0,
+                 st)
+            self.tag += 1
+            call("rg_scatter_add", w.ids.data_ptr(), w.grows.data_ptr(), HF, w.nrows.data_ptr(), S + B, -1,
+                 self.G.data_ptr(), self.tags.data_ptr(), self.tag, st)
+            call("rg_scatter_add", w.ids.data_ptr(), w.gb.data_ptr(), 1, w.nrows.data_ptr(), S + B, -1,
+                 self.Gb.data_ptr(), self.tags.data_ptr(), self.tag, st)
+        with region("sampled_adam"):
+            call("rg_adam_rows", self.W.p.data_ptr(), self.W.m.data_ptr(), self.W.v.data_ptr(), self.G.data_ptr(),
+                 self.tags.data_ptr(), self.tag, self.A, HF, adam6, st)
+            call("rg_adam_rows", self.b.p.data_ptr(), self.b.m.data_ptr(), self.b.v.data_ptr(), self.Gb.data_ptr(),
+                 self.tags.data_ptr(), self.tag, self.A, 1, adam6, st)

@@ -22,12 +22,13 @@ class GRU4Rec(SupervisedNet):
     """embedding -> GRU -> h[0] -> Linear(H -> A) (reference ``:6-82``)."""
 
     def __init__(self, hidden_size, embedding_dim, item_num, state_size, action_dim, gru_layers=1,
-                 use_packed_seq=True, train_pad_embed=True, padding_idx=None, device="cuda", comm=None):
+                 use_packed_seq=True, train_pad_embed=True, padding_idx=None, device="cuda", comm=None,
+                 n_negatives=None, neg_seed=0):
         super().__init__(trunk_attr="gru", head_names=["output"], hidden_dim=hidden_size,
                          embedding_dim=embedding_dim, item_num=item_num, state_size=state_size,
                          action_dim=action_dim, gru_layers=gru_layers, use_packed_seq=use_packed_seq,
                          train_pad_embed=train_pad_embed, padding_idx=padding_idx, bidir=False, device=device,
-                         comm=comm)
+                         comm=comm, n_negatives=n_negatives, neg_seed=neg_seed)
 
 
 class _AdamFacade:
@@ -52,7 +53,7 @@ class _AdamFacade:
 class GRU4Rec_trainer:
     def __init__(self, hidden_dim, embedding_dim, gru_layers, train_pad_embed, use_packed_seq, learning_rate,
                  item_num, state_size, action_dim, device, padding_idx=None, torch_rand_seed=118,
-                 python_rand_seed=999, shard_items=False, process_group=None):
+                 python_rand_seed=999, shard_items=False, process_group=None, n_negatives=None, neg_seed=0):
         torch.manual_seed(torch_rand_seed)
         random.seed(python_rand_seed)
         self.device = require_gpu(device)
@@ -60,10 +61,14 @@ class GRU4Rec_trainer:
         # this rank trains its own batch shard, the output layer is split over
         # the ranks by item id (recommenders/hip/sharded.py).
         self.comm = Comm(process_group) if shard_items else None
+        # n_negatives (build extension, off by default): sampled softmax over the
+        # target and n_negatives shared uniform negatives instead of the full
+        # softmax (config C3; recommenders/hip/engine.py:SampledSoftmaxHead).
         self.gru_model = GRU4Rec(hidden_size=hidden_dim, embedding_dim=embedding_dim, item_num=item_num,
                                  state_size=state_size, action_dim=action_dim, gru_layers=gru_layers,
                                  use_packed_seq=use_packed_seq, train_pad_embed=train_pad_embed,
-                                 padding_idx=padding_idx, device=self.device, comm=self.comm)
+                                 padding_idx=padding_idx, device=self.device, comm=self.comm,
+                                 n_negatives=n_negatives, neg_seed=neg_seed)
         self.learning_rate = learning_rate
         self.cross_entropy_loss = nn.CrossEntropyLoss(weight=None, reduction="mean")
         self.clock = AdamClock(learning_rate)

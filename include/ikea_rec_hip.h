@@ -169,6 +169,25 @@ int rg_weighted_sum(const float* const* X, const float* w, int nh, int64_t n, fl
 /* SMORL reward matrix r (B, 3) f32 = stack([r_acc f64, r_div, r_nov]) (SMORL/smorl_gru.py:311-314, 3 rewards) */
 int rg_stack_rewards(const double* r_acc, const float* r_div, const float* r_nov, int B, float* r, rg_stream_t stream);
 
+/* ---- sampled-softmax head (SURVEY §8 A7 sampled ext., config C3; build-defined,
+ * no reference counterpart — replaces the full-softmax CrossEntropyLoss of
+ * GRU4Rec/model.py:121,146 / BidirGRU4Rec/model.py:145,167 when the trainer is
+ * built with n_negatives) ---- */
+/* out[s] = uniform draw on [0, A): hi64(splitmix64(seed + phi*(counter*S + s + 1)) * A) */
+int rg_sample_uniform(uint64_t seed, uint64_t counter, int S, int64_t A, int32_t* out, rg_stream_t stream);
+/* Zᵀ[s][b] = h_b·W[neg_s] + bias[neg_s] (S × ldz) + per-(128-negative tile, row) (max, Σexp)
+ * partials (nT × B); Wg/bg (optional, both or neither): the gathered rows. HF ∈ {32,64,128,256}. */
+int rg_sampled_fwd(const float* h, const float* W, const float* bias, const int32_t* neg, int B, int S, int HF,
+                   float* ZT, int64_t ldz, float* pmax, float* psum, float* Wg, float* bg, rg_stream_t stream);
+/* per row: z_pos = h_b·W[a_b] + bias[a_b]; lse over {z_pos} ∪ partials; loss_row = lse − z_pos;
+ * ids[b] = a_b; dzpos = (exp(z_pos − lse) − 1)·g; gpos = dzpos·h_b; dhpos = dzpos·W[a_b] */
+int rg_sampled_lse(const float* h, const float* W, const float* bias, const int64_t* tgt, int B, int64_t A, int HF,
+                   const float* pmax, const float* psum, int nT, float gscale, float* lse, float* loss_row,
+                   int32_t* ids, float* dzpos, float* gpos, float* dhpos, rg_stream_t stream);
+/* in place dZᵀ = exp(Zᵀ − lse)·g; dbg[s] = Σ_b dZᵀ[s][b] */
+int rg_sampled_dz(float* ZT, int64_t ldz, const float* lse, int B, int S, float gscale, float* dbg,
+                  rg_stream_t stream);
+
 int rg_abi_version(void);
 
 #ifdef __cplusplus

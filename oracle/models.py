@@ -105,21 +105,62 @@ def make_adam(net, lr):
     return torch.optim.Adam(net.parameters(), lr=lr)
 
 
+_M64 = np.uint64(0xFFFFFFFFFFFFFFFF)
+
+
+def _mix64(z):
+    z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+    z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+    return z ^ (z >> np.uint64(31))
+
+
+def sample_uniform(seed, counter, S, A):
+    """Negatives of draw ``counter`` (csrc/sampled.hip:k_sample_uniform):
+    hi64(splitmix64(seed + φ·(counter·S + s + 1)) · A), s < S.  Build-defined:
+    the reference has no sampled softmax."""
+    with np.errstate(over="ignore"):
+        i = np.arange(S, dtype=np.uint64) + np.uint64(counter) * np.uint64(S) + np.uint64(1)
+        x = _mix64(np.uint64(seed) + np.uint64(0x9E3779B97F4A7C15) * i)
+        A = np.uint64(A)
+        hi, lo = x >> np.uint64(32), x & np.uint64(0xFFFFFFFF)
+        r = (hi * A + ((lo * A) >> np.uint64(32))) >> np.uint64(32)
+    return r.astype(np.int64)
+
+
+def sampled_ce(h, weight, bias, a, neg):
+    """mean_b [logsumexp(z_pos, z_neg) − z_pos] with z = h·W[·] + b[·] over the
+    target and the shared negatives (duplicates kept, no logQ correction)."""
+    zpos = (h * weight[a]).sum(1) + bias[a]
+    zneg = h @ weight[neg].t() + bias[neg]
+    logits = torch.cat([zpos[:, None], zneg], 1)
+    return F.cross_entropy(logits, torch.zeros(h.shape[0], dtype=torch.long))
+
+
 class OracleSupervised:
-    """GRU4Rec / BidirGRU4Rec trainer restatement (``GRU4Rec/model.py:86-155``)."""
+    """GRU4Rec / BidirGRU4Rec trainer restatement (``GRU4Rec/model.py:86-155``).
+    ``n_negatives``: the build-defined sampled softmax (config C3)."""
 
     def __init__(self, kind, hidden_dim, embedding_dim, gru_layers, train_pad_embed,
                  use_packed_seq, learning_rate, item_num, state_size, action_dim,
-                 dropout=0.0, padding_idx=None, torch_rand_seed=118, python_rand_seed=999):
+                 dropout=0.0, padding_idx=None, torch_rand_seed=118, python_rand_seed=999,
+                 n_negatives=None, neg_seed=0):
         torch.manual_seed(torch_rand_seed)
         random.seed(python_rand_seed)
         self.net = Net(kind, item_num, action_dim, embedding_dim, hidden_dim, gru_layers,
                        train_pad_embed, use_packed_seq, padding_idx, dropout)
         self.opt = make_adam(self.net, learning_rate)
+        self.n_negatives, self.neg_seed, self.draws = n_negatives, neg_seed, 0
 
     def step(self, s, a, true_len):
-        preds = self.net(s, true_len)
-        loss = F.cross_entropy(preds, a)  # CrossEntropyLoss(reduction="mean")
+        if self.n_negatives:
+            neg = torch.from_numpy(sample_uniform(self.neg_seed, self.draws, self.n_negatives,
+                                                  self.net.action_dim))
+            self.draws += 1
+            head = getattr(self.net, self.net.head_names[0])
+            loss = sampled_ce(self.net.hidden(s, true_len), head.weight, head.bias, a, neg)
+        else:
+            preds = self.net(s, true_len)
+            loss = F.cross_entropy(preds, a)  # CrossEntropyLoss(reduction="mean")
         self.opt.zero_grad()
         loss.backward()
         self.opt.step()

@@ -1,0 +1,159 @@
+"""GPU parity for the sampled-softmax head (config C3; csrc/sampled.hip).
+
+The reference has no sampled softmax: parity is pinned
+to the build's CPU restatement (oracle/models.py: sample_uniform, sampled_ce,
+OracleSupervised(n_negatives=...)).  Tolerances as in test_gpu_supervised.py:
+losses 1e-4 absolute; logits 1e-5; parameters 1e-4 for >= 99.9 % of elements,
+never more than 2·lr (Adam's sign-like first steps).
+"""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def D(x, dt=None):
+    t = torch.as_tensor(x).cuda()
+    return t if dt is None else t.to(dt)
+
+
+def run_head(B, S, A, HF, seed=0, collide=False):
+    """One sampled head step through the C ABI; returns device results and
+    the inputs used."""
+    from recommenders.hip import call, stream_ptr
+    from oracle.models import sample_uniform
+    g = torch.Generator().manual_seed(seed)
+    h = torch.randn(B, HF, generator=g) * 0.5
+    W = torch.randn(A, HF, generator=g) * 0.1
+    bias = torch.randn(A, generator=g) * 0.1
+    neg = torch.from_numpy(sample_uniform(seed, 0, S, A))
+    tgt = torch.randint(0, A, (B,), generator=g)
+    if collide:  # some targets equal negatives (and duplicated negatives)
+        tgt[: min(B, S) // 2] = neg[: min(B, S) // 2]
+    ldz = (B + 3) // 4 * 4
+    nT = (S + 127) // 128
+    dh_, W_, b_, neg_, tgt_ = D(h), D(W), D(bias), D(neg, torch.int32), D(tgt)
+    ZT = torch.full((S, ldz), float("nan"), device="cuda")
+    pm = torch.empty(nT, B, device="cuda")
+    ps = torch.empty(nT, B, device="cuda")
+    Wg = torch.empty(S, HF, device="cuda")
+    bg = torch.empty(S, device="cuda")
+    st = stream_ptr()
+    call("rg_sampled_fwd", dh_.data_ptr(), W_.data_ptr(), b_.data_ptr(), neg_.data_ptr(), B, S, HF, ZT.data_ptr(),
+         ldz, pm.data_ptr(), ps.data_ptr(), Wg.data_ptr(), bg.data_ptr(), st)
+    lse = torch.empty(B, device="cuda")
+    lrow = torch.empty(B, device="cuda")
+    ids = torch.empty(B, dtype=torch.int32, device="cuda")
+    dzp = torch.empty(B, device="cuda")
+    gpos = torch.empty(B, HF, device="cuda")
+    dhp = torch.empty(B, HF, device="cuda")
+    gs = float(np.float32(1.0 / B))
+    call("rg_sampled_lse", dh_.data_ptr(), W_.data_ptr(), b_.data_ptr(), tgt_.data_ptr(), B, A, HF, pm.data_ptr(),
+         ps.data_ptr(), nT, gs, lse.data_ptr(), lrow.data_ptr(), ids.data_ptr(), dzp.data_ptr(), gpos.data_ptr(),
+         dhp.data_ptr(), st)
+    Z = ZT[:, :B].clone()
+    dbg = torch.empty(S, device="cuda")
+    call("rg_sampled_dz", ZT.data_ptr(), ldz, lse.data_ptr(), B, S, gs, dbg.data_ptr(), st)
+    torch.cuda.synchronize()
+    out = dict(Z=Z.cpu(), Wg=Wg.cpu(), bg=bg.cpu(), lse=lse.cpu(), lrow=lrow.cpu(), ids=ids.cpu(), dzp=dzp.cpu(),
+               gpos=gpos.cpu(), dhp=dhp.cpu(), dZ=ZT[:, :B].cpu(), dbg=dbg.cpu())
+    return out, dict(h=h, W=W, bias=bias, neg=neg, tgt=tgt)
+
+
+def test_sample_uniform_matches_oracle_bit_exact():
+    from recommenders.hip import call, stream_ptr
+    from oracle.models import sample_uniform
+    for seed, ctr, S, A in [(0, 0, 2048, 1_000_000), (123456789, 7, 1000, 37), (2**63 + 5, 2**40, 300, 2**31 - 1)]:
+        out = torch.empty(S, dtype=torch.int32, device="cuda")
+        call("rg_sample_uniform", seed, ctr, S, A, out.data_ptr(), stream_ptr())
+        np.testing.assert_array_equal(out.cpu().numpy(), sample_uniform(seed, ctr, S, A))
+
+
+@pytest.mark.parametrize("B,S,A,HF,collide", [(256, 256, 5000, 128, False), (37, 200, 300, 64, True),
+                                              (300, 130, 100, 256, True), (128, 2048, 100000, 32, False)])
+def test_sampled_kernels_match_torch_fp32(B, S, A, HF, collide):
+    o, x = run_head(B, S, A, HF, collide=collide)
+    h, W, bias, neg, tgt = x["h"], x["W"], x["bias"], x["neg"], x["tgt"]
+    zneg = h @ W[neg].t() + bias[neg]                       # (B, S)
+    np.testing.assert_allclose(o["Z"].t().numpy(), zneg.numpy(), rtol=0, atol=1e-5)
+    np.testing.assert_array_equal(o["Wg"].numpy(), W[neg].numpy())
+    np.testing.assert_array_equal(o["bg"].numpy(), bias[neg].numpy())
+    zpos = (h * W[tgt]).sum(1) + bias[tgt]
+    lse = torch.logsumexp(torch.cat([zpos[:, None], zneg], 1), 1)
+    np.testing.assert_allclose(o["lse"].numpy(), lse.numpy(), rtol=0, atol=1e-5)
+    np.testing.assert_allclose(o["lrow"].numpy(), (lse - zpos).numpy(), rtol=0, atol=1e-5)
+    np.testing.assert_array_equal(o["ids"].numpy(), tgt.numpy())
+    g = 1.0 / B
+    dzp = (torch.exp(zpos - lse) - 1) * g
+    np.testing.assert_allclose(o["dzp"].numpy(), dzp.numpy(), rtol=0, atol=1e-6)
+    np.testing.assert_allclose(o["gpos"].numpy(), (dzp[:, None] * h).numpy(), rtol=0, atol=1e-6)
+    np.testing.assert_allclose(o["dhp"].numpy(), (dzp[:, None] * W[tgt]).numpy(), rtol=0, atol=1e-6)
+    dZ = torch.exp(zneg - lse[:, None]) * g
+    np.testing.assert_allclose(o["dZ"].t().numpy(), dZ.numpy(), rtol=1e-4, atol=1e-7)
+    np.testing.assert_allclose(o["dbg"].numpy(), dZ.sum(0).numpy(), rtol=1e-4, atol=1e-6)
+
+
+def test_invalid_target_gives_nan_row():
+    from recommenders.hip import call, stream_ptr
+    B, S, A, HF = 8, 128, 50, 32
+    h = D(torch.randn(B, HF))
+    W = D(torch.randn(A, HF) * 0.1)
+    b = D(torch.zeros(A))
+    neg = D(torch.arange(S) % A, torch.int32)
+    tgt = D(torch.tensor([0, 1, 2, 3, 4, 5, 6, A]))
+    ldz = 8
+    ZT = torch.empty(S, ldz, device="cuda")
+    pm, ps = torch.empty(1, B, device="cuda"), torch.empty(1, B, device="cuda")
+    st = stream_ptr()
+    call("rg_sampled_fwd", h.data_ptr(), W.data_ptr(), b.data_ptr(), neg.data_ptr(), B, S, HF, ZT.data_ptr(), ldz,
+         pm.data_ptr(), ps.data_ptr(), None, None, st)
+    outs = [torch.empty(B, device="cuda") for _ in range(2)]
+    ids = torch.empty(B, dtype=torch.int32, device="cuda")
+    dz = torch.empty(B, device="cuda")
+    g2 = [torch.empty(B, HF, device="cuda") for _ in range(2)]
+    call("rg_sampled_lse", h.data_ptr(), W.data_ptr(), b.data_ptr(), tgt.data_ptr(), B, A, HF, pm.data_ptr(),
+         ps.data_ptr(), 1, 0.125, outs[0].data_ptr(), outs[1].data_ptr(), ids.data_ptr(), dz.data_ptr(),
+         g2[0].data_ptr(), g2[1].data_ptr(), st)
+    lrow = outs[1].cpu()
+    assert torch.isfinite(lrow[:7]).all() and torch.isnan(lrow[7])
+    assert int(ids.cpu()[7]) == -1 and float(dz.cpu()[7]) == 0.0
+
+
+@pytest.mark.parametrize("kind,E,H,N,L,B,S", [("gru4rec", 32, 32, 3000, 10, 256, 512),
+                                              ("gru4rec", 64, 64, 20000, 20, 300, 1000),
+                                              ("bidir", 32, 32, 5000, 12, 200, 256),
+                                              ("gru4rec", 128, 128, 50000, 50, 1024, 2048)])
+def test_sampled_trainer_matches_oracle(kind, E, H, N, L, B, S):
+    from oracle.models import OracleSupervised
+    from recommenders.data_utils.synthetic import SessionStream
+    from recommenders.models.BidirGRU4Rec.model import BidirGRU4Rec_trainer
+    from recommenders.models.GRU4Rec.model import GRU4Rec_trainer
+    cfg = dict(hidden_dim=H, embedding_dim=E, gru_layers=1, train_pad_embed=True, use_packed_seq=True,
+               learning_rate=0.005, item_num=N, state_size=L, action_dim=N, n_negatives=S, neg_seed=11)
+    torch.set_num_threads(8)
+    orc = OracleSupervised(kind=kind, **cfg)
+    if kind == "bidir":
+        tr = BidirGRU4Rec_trainer(device="cuda", dropout=0.0, **cfg)
+    else:
+        tr = GRU4Rec_trainer(device="cuda", **cfg)
+    st = SessionStream(N, L, B * 3, seed=9)
+    for i in range(3):
+        s, a, r, sn, ln, nln, e = st.batch(i, B)
+        lo = orc.step(s, a, ln)
+        lg = tr.train_step(s, a, ln)
+        assert abs(lo - lg) < 1e-4, (i, lo, lg)
+    sd_o = orc.net.state_dict()
+    for k, v in tr.gru_model.state_dict().items():
+        d = (v.cpu() - sd_o[k]).abs()
+        assert float(d.max()) <= 2 * cfg["learning_rate"] + 1e-5, k
+        assert float((d > 1e-4).float().mean()) < 1e-3, (k, float((d > 1e-4).float().mean()))
+    # evaluation still scores every item with the trained head
+    tr.set_eval()
+    s, a, r, sn, ln, nln, e = st.batch(0, B)
+    z = tr.gru_model(s.cuda(), ln).float().cpu()
+    with torch.no_grad():
+        orc.net.eval()
+        zo = orc.net(s, ln)
+    d = (z - zo).abs()
+    assert float(d.mean()) < 1e-4, float(d.mean())
