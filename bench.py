@@ -52,6 +52,10 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-timing", action="store_true")
     ap.add_argument("--force-shard", action="store_true", help="item-sharded path even at world 1 (test)")
+    ap.add_argument("--config", choices=["c2", "c3"], default="c2",
+                    help="c2: headline GRU4Rec full softmax; c3: BidirGRU4Rec with sampled softmax")
+    ap.add_argument("--negatives", type=int, default=2048)
+    ap.add_argument("--no-target", action="store_true", help="skip the north-star gather+sampled-logits side run")
     return ap.parse_args()
 
 
@@ -81,18 +85,95 @@ def cpu_baseline(args):
                        f"{threads} threads, {dt:.1f} s")}
 
 
+def make_trainer(cfg, args, dev, shard):
+    from recommenders.models.BidirGRU4Rec.model import BidirGRU4Rec_trainer
+    from recommenders.models.GRU4Rec.model import GRU4Rec_trainer
+    N, L, E = args.items, args.seq, args.dim
+    common = dict(hidden_dim=E, embedding_dim=E, gru_layers=1, train_pad_embed=True, use_packed_seq=True,
+                  learning_rate=0.01, item_num=N, state_size=L, action_dim=N, device=dev)
+    if cfg == "c2":
+        return GRU4Rec_trainer(shard_items=shard, **common)
+    if cfg == "c2s":   # GRU4Rec at C2 shapes with the sampled head (north-star target step)
+        return GRU4Rec_trainer(n_negatives=args.negatives, **common)
+    if cfg == "c3":
+        return BidirGRU4Rec_trainer(dropout=0.0, n_negatives=args.negatives, **common)
+    raise ValueError(cfg)
+
+
+def timed_run(tr, batches, warmup, steps, world, kernel_timing):
+    """W untimed steps, then K steps between barrier + synchronize; max over ranks."""
+    from recommenders.hip.timing import KernelTimer, timing
+    for i in range(warmup):
+        tr.train_step(*batches[i])
+    timer = KernelTimer()
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    losses = []
+    if kernel_timing:
+        with timing(timer):
+            for i in range(warmup, warmup + steps):
+                losses.append(tr.train_step(*batches[i]))
+    else:
+        for i in range(warmup, warmup + steps):
+            losses.append(tr.train_step(*batches[i]))
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([dt], device=torch.cuda.current_device())
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        dt = float(t)
+    if not all(np.isfinite(losses)):
+        raise RuntimeError(f"non-finite loss {losses}")
+    kern = {}
+    if kernel_timing:
+        kern = {k: round(float(np.mean(v)), 4) for k, v in timer.elapsed_ms().items()}
+    return dt, losses, kern
+
+
+def gather_bytes(T, E):
+    # per token: int64 id read, fp32 table row read, packed row write, int32 token-id write
+    return T * (8 + 2 * 4 * E + 4)
+
+
+def sampled_fwd_bytes(B, S, HF):
+    # h read, negative ids, gathered W rows + bias read, Zᵀ write, (max, Σexp) partials, Wg/bg write
+    nT = (S + 127) // 128
+    return B * HF * 4 + S * 4 + 2 * S * (HF + 1) * 4 + B * S * 4 + nT * B * 8
+
+
+def target_step(kern, T, B, S, E, HF, n_gather):
+    """North-star target: embedding gather + sampled logits (fwd) against the
+    HBM roofline, with the logits' flop rate beside it."""
+    if "gather" not in kern or "sampled_fwd" not in kern:
+        return None
+    tg, ts = kern["gather"] * n_gather, kern["sampled_fwd"]
+    by = n_gather * gather_bytes(T, E) + sampled_fwd_bytes(B, S, HF)
+    gbs = by / ((tg + ts) * 1e-3) / 1e9
+    fl = 2.0 * B * S * HF
+    return {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(gbs / HBM_PEAK_GBS, 4), "bytes_per_step": int(by), "ms": round(tg + ts, 4),
+            "gather_ms": round(tg, 4), "gather_GBs": round(n_gather * gather_bytes(T, E) / (tg * 1e-3) / 1e9, 1),
+            "sampled_fwd_ms": round(ts, 4), "sampled_fwd_TFLOPs": round(fl / (ts * 1e-3) / 1e12, 2),
+            "sampled_fwd_mfma_frac": round(fl / (ts * 1e-3) / 1e12 / FP32_MFMA_PEAK_TFLOPS, 4)}
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    shard = (world > 1 or args.force_shard) and args.config == "c2"
     if world > 1 or args.force_shard:
         import torch.distributed as dist
         torch.cuda.set_device(local)
         dist.init_process_group("nccl")
+    if world > 1 and args.config != "c2":
+        raise SystemExit("multi-GPU bench runs the C2 headline workload only")
     from recommenders.data_utils.synthetic import SessionStream
-    from recommenders.hip.timing import KernelTimer, timing
-    from recommenders.models.GRU4Rec.model import GRU4Rec_trainer
 
     dev = torch.device("cuda", local)
     B, L, N, E = args.batch, args.seq, args.items, args.dim
@@ -105,71 +186,71 @@ def main():
         s, a, r, sn, ln, nln, e = st.batch(i, B)
         batches.append((s.to(dev), a.to(dev), ln.to(dev)))
         tok.append(int(ln.sum()))
-    tr = GRU4Rec_trainer(hidden_dim=E, embedding_dim=E, gru_layers=1, train_pad_embed=True, use_packed_seq=True,
-                         learning_rate=0.01, item_num=N, state_size=L, action_dim=N, device=dev,
-                         shard_items=world > 1 or args.force_shard)
+    T = float(np.mean(tok[args.warmup:]))
+    tr = make_trainer(args.config, args, dev, shard)
     tr.set_train()
-    for i in range(args.warmup):
-        tr.train_step(*batches[i])
-    timer = KernelTimer()
-    if world > 1:
-        torch.distributed.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    losses = []
-    if args.no_kernel_timing:
-        for i in range(args.warmup, nsteps):
-            losses.append(tr.train_step(*batches[i]))
-    else:
-        with timing(timer):
-            for i in range(args.warmup, nsteps):
-                losses.append(tr.train_step(*batches[i]))
-    torch.cuda.synchronize()
-    if world > 1:
-        torch.distributed.barrier()
-    dt = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([dt], device=dev)
-        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
-        dt = float(t)
-    if not all(np.isfinite(losses)):
-        raise RuntimeError(f"non-finite loss {losses}")
+    dt, losses, kern = timed_run(tr, batches, args.warmup, args.steps, world, not args.no_kernel_timing)
     if rank != 0:
         if torch.distributed.is_initialized():
             torch.distributed.destroy_process_group()
         return
     ms = dt / args.steps * 1e3
     value = B * args.steps * world / dt
-    flops_head = 2.0 * B * N * E  # one (B × E)·(E × A) contraction
-    kern = {}
     roof = None
-    if not args.no_kernel_timing:
-        el = timer.elapsed_ms()
-        kern = {k: round(float(np.mean(v)), 4) for k, v in el.items()}
-        heads = {k: kern[k] for k in ("head_fwd", "head_dh", "head_dw_adam") if k in kern}
-        dom = max(heads, key=heads.get)
-        ach = flops_head / (heads[dom] * 1e-3) / 1e12
-        traffic = None
-        pmc = os.path.join(HERE, "profiles", "pmc_traffic.json")
-        if os.path.exists(pmc):
-            traffic = json.load(open(pmc)).get(dom)
-        roof = {"bound": "mfma", "kernel": dom, "achieved": round(ach, 2), "peak": FP32_MFMA_PEAK_TFLOPS,
-                "unit": "TFLOP/s", "frac": round(ach / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": traffic,
-                "flops_per_launch": flops_head}
+    target = None
+    HF = E * (2 if args.config == "c3" else 1)
+    if args.config == "c2":
+        flops_head = 2.0 * B * N * E  # one (B × E)·(E × A) contraction
+        if kern:
+            heads = {k: kern[k] for k in ("head_fwd", "head_dh", "head_dw_adam") if k in kern}
+            dom = max(heads, key=heads.get)
+            ach = flops_head / (heads[dom] * 1e-3) / 1e12
+            traffic = None
+            pmc = os.path.join(HERE, "profiles", "pmc_traffic.json")
+            if os.path.exists(pmc):
+                traffic = json.load(open(pmc)).get(dom)
+            roof = {"bound": "mfma", "kernel": dom, "achieved": round(ach, 2), "peak": FP32_MFMA_PEAK_TFLOPS,
+                    "unit": "TFLOP/s", "frac": round(ach / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": traffic,
+                    "flops_per_launch": flops_head}
+        if world == 1 and not args.no_target and kern:
+            # north-star target step measured on GRU4Rec at C2
+            # shapes with the sampled head: a short side run, own trainer
+            del tr
+            torch.cuda.empty_cache()
+            tr2 = make_trainer("c2s", args, dev, False)
+            tr2.set_train()
+            _, _, k2 = timed_run(tr2, batches, min(2, args.warmup), min(5, args.steps), 1, True)
+            target = target_step(k2, T, B, args.negatives, E, E, 1)
+            if target is not None:
+                target["workload"] = f"GRU4Rec {N} items dim{E} batch {B}, {args.negatives} sampled negatives"
+            del tr2
+    else:
+        target = target_step(kern, T, B, args.negatives, E, HF, 2)
+        roof = dict(target) if target else None
+        if roof:
+            roof["kernel"] = "gather + sampled_fwd"
+            roof["traffic"] = None
     cpu = None
-    if world == 1 and not args.no_cpu_baseline:
+    if world == 1 and not args.no_cpu_baseline and args.config == "c2":
         cpu = cpu_baseline(args)
+    if args.config == "c2":
+        metric = "session-steps/sec at 1M items, dim128, batch 4096; HR@20/NDCG@20 parity"
+        workload = f"GRU4Rec {N} items, dim{E}, seq_len<={L}, batch {B}/GPU, full-softmax logits"
+    else:
+        metric = "session-steps/sec, BidirGRU4Rec 1M items, dim128, batch 4096, 2048 sampled negatives"
+        workload = (f"BidirGRU4Rec {N} items, dim{E}, seq_len<={L}, batch {B}, {args.negatives} shared uniform "
+                    f"negatives (sampled softmax), dropout 0")
     line = {
-        "metric": "session-steps/sec at 1M items, dim128, batch 4096; HR@20/NDCG@20 parity",
+        "metric": metric,
         "value": round(value, 2), "unit": "session-steps/sec", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": "f32", "data": "synthetic (seeded Zipf session stream, random-init weights)",
-        "config": {"workload": f"GRU4Rec {N} items, dim{E}, seq_len<={L}, batch {B}/GPU, full-softmax logits",
+        "config": {"workload": workload,
                    "global_batch": B * world, "seq_len": L, "items": N, "dim": E,
                    "parallelism": (f"dp{world} trunk + {world}-way item-sharded head (RCCL)" if world > 1
                                    else "single"),
-                   "tokens_per_batch": int(np.mean(tok))},
-        "roofline": roof, "cpu_baseline": cpu, "kernel_ms": kern,
+                   "tokens_per_batch": int(T)},
+        "roofline": roof, "cpu_baseline": cpu, "north_star_target": target, "kernel_ms": kern,
         "loss_first_last": [round(losses[0], 5), round(losses[-1], 5)],
     }
     print(json.dumps(line), flush=True)

@@ -17,6 +17,7 @@ ap.add_argument("--B", type=int, default=4096)
 ap.add_argument("--A", type=int, default=1_000_000)
 ap.add_argument("--H", type=int, default=128)
 ap.add_argument("--iters", type=int, default=5)
+ap.add_argument("--variants", action="store_true", help="also time fwd without Zᵀ stores / Σexp, dW without Adam")
 a = ap.parse_args()
 B, A, H = a.B, a.A, a.H
 dev = "cuda"
@@ -65,10 +66,33 @@ def dw():
          clock.next_args(), None, None, st)
 
 
+def fwd_nostore():
+    call("rg_head_fwd", h.data_ptr(), W.data_ptr(), bias.data_ptr(), B, A, H, None, 0, pm.data_ptr(),
+         ps.data_ptr(), pa.data_ptr(), 1, st)
+
+
+def fwd_argmax():
+    call("rg_head_fwd", h.data_ptr(), W.data_ptr(), bias.data_ptr(), B, A, H, None, 0, pm.data_ptr(),
+         ps.data_ptr(), pa.data_ptr(), 0, st)
+
+
+dWo = torch.empty_like(W) if a.variants else None
+dbo = torch.empty_like(bias) if a.variants else None
+
+
+def dw_noadam():
+    call("rg_head_dw_adam", ZT.data_ptr(), ldz, lse.data_ptr(), tgt.data_ptr(), 1.0 / B, h.data_ptr(), B, A, H,
+         W.data_ptr(), mW.data_ptr(), vW.data_ptr(), bias.data_ptr(), mb.data_ptr(), vb.data_ptr(),
+         None, dWo.data_ptr(), dbo.data_ptr(), st)
+
+
 fwd(); lsec(); dh(); dw()
 torch.cuda.synchronize()
 res = {}
-for name, fn in (("head_fwd", fwd), ("lse", lsec), ("head_dh", dh), ("head_dw_adam", dw)):
+cases = [("head_fwd", fwd), ("lse", lsec), ("head_dh", dh), ("head_dw_adam", dw)]
+if a.variants:
+    cases += [("fwd_no_zstore", fwd_nostore), ("fwd_argmax_only", fwd_argmax), ("dw_no_adam", dw_noadam)]
+for name, fn in cases:
     ts = []
     for _ in range(a.iters):
         e0 = torch.cuda.Event(enable_timing=True)
