@@ -11,7 +11,8 @@ import os
 
 import torch
 
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libikea_rec_hip.so")
+LIB_PATH = os.environ.get("IKEA_REC_HIP_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)),
+                                                                "libikea_rec_hip.so")
 
 P = C.c_void_p
 I = C.c_int
