@@ -254,7 +254,7 @@ __global__ void k_lse_stage1(const float* __restrict__ pmax, const float* __rest
 __global__ void k_lse_final(const float* __restrict__ omax, const float* __restrict__ osum,
                             const int32_t* __restrict__ oarg, int B, int S, const float* __restrict__ ZT,
                             int64_t ldz, const int64_t* __restrict__ tgt, int A, float* __restrict__ lse,
-                            int32_t* __restrict__ amax, float* __restrict__ loss_row) {
+                            int32_t* __restrict__ amax, float* __restrict__ loss_row, float* __restrict__ mx) {
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= B) return;
   float m = NEG_INF, s = 0.f;
@@ -266,6 +266,7 @@ __global__ void k_lse_final(const float* __restrict__ omax, const float* __restr
   const float l = m + logf(s);
   if (lse) lse[b] = l;
   if (amax) amax[b] = a;
+  if (mx) mx[b] = m;  // the row maximum itself (exact logit value)
   if (loss_row && ZT && tgt) {
     const int64_t t = tgt[b];  // CrossEntropyLoss raises on out-of-range targets
     loss_row[b] = (t >= 0 && t < A) ? l - ZT[t * ldz + b] : __builtin_nanf("");
@@ -274,7 +275,7 @@ __global__ void k_lse_final(const float* __restrict__ omax, const float* __restr
 
 extern "C" int rg_lse_combine(const float* pmax, const float* psum, const int32_t* parg, int B, int nJ,
                               float* work, const float* ZT, int64_t ldz, const int64_t* tgt, int A, float* lse,
-                              int32_t* amax, float* loss_row, hipStream_t stream) {
+                              int32_t* amax, float* loss_row, float* mx, hipStream_t stream) {
   if (B <= 0 || nJ <= 0) return RG_ERR_ARG;
   int S = 64;
   if (S > nJ) S = nJ;
@@ -286,7 +287,7 @@ extern "C" int rg_lse_combine(const float* pmax, const float* psum, const int32_
   hipLaunchKernelGGL(k_lse_stage1, dim3((B + 255) / 256, S), dim3(256), 0, stream, pmax, psum, parg, B, nJ, jchunk,
                      omax, osum, oarg);
   hipLaunchKernelGGL(k_lse_final, dim3((B + 255) / 256), dim3(256), 0, stream, omax, osum, oarg, B, S, ZT, ldz,
-                     tgt, A, lse, amax, loss_row);
+                     tgt, A, lse, amax, loss_row, mx);
   RG_LAUNCH_CHECK();
   return RG_OK;
 }

@@ -32,6 +32,10 @@ __global__ __launch_bounds__(256) void k_q_gather(const float* __restrict__ h, i
   const int lane = threadIdx.x & 63;
   if (b >= B) return;
   const int64_t j = idx64 ? idx64[b] : (int64_t)idx32[b];
+  if (j < 0) {  // not held here (item-sharded head): contributes 0 to the all-reduce
+    if (lane < nh) q[(int64_t)b * nh + lane] = 0.f;
+    return;
+  }
   for (int i = 0; i < nh; ++i) {
     const float* wr = hp.W[i] + j * HF;
     float s = 0.f;
@@ -65,6 +69,7 @@ __global__ __launch_bounds__(256) void k_q_backward(const float* __restrict__ h,
   const int lane = threadIdx.x & 63;
   if (b >= B) return;
   const int64_t j = idx[b];
+  if (j < 0) return;  // row's action not held here (item-sharded head)
   for (int c = lane; c < HF; c += 64) {
     float acc = dh[(int64_t)b * HF + c];
     const float hv = h[(int64_t)b * HF + c];

@@ -35,10 +35,13 @@ SIGNATURES = {
     "rg_gru_fwd": [P, P, P, P, P, P, I, I, P, I, I, P, I64, P],
     "rg_gru_bwd": [P, I64, P, P, P, P, I, I, P, I, I, P, P, P],
     "rg_head_fwd": [P, P, P, I, I, I, P, I64, P, P, P, I, P],
-    "rg_lse_combine": [P, P, P, I, I, P, P, I64, P, I, P, P, P, P],
+    "rg_lse_combine": [P, P, P, I, I, P, P, I64, P, I, P, P, P, P, P],
     "rg_sum_scale": [P, I, F, P, P, P],
     "rg_lse_merge_ranks": [P, I, I, P, P],
     "rg_shard_targets": [P, I64, P, I64, I64, I, P, P, P],
+    "rg_shard_index": [P, P, I, I64, I64, P, P],
+    "rg_argmax_merge_ranks": [P, P, I, I, I64, P, P, P],
+    "rg_topk_merge_ranks": [P, P, I, I, I, I64, P, P, P],
     "rg_sub": [P, P, I, P, P],
     "rg_head_dh": [P, I64, P, P, F, P, I, I, I, I, P, P],
     "rg_head_dw_adam": [P, I64, P, P, F, P, I, I, I, P, P, P, P, P, P, P, P, P, P],

@@ -320,6 +320,7 @@ class _HeadWS:
         self.work = z(3 * S * B)
         self.lse = z(B)
         self.amax = z(B, dt=torch.int32)
+        self.mx = z(B)                  # row maxima (argmax path)
         self.loss_row = z(B)
         self.loss = torch.zeros(1, device=device)
         # dh kernel: ~512 workgroups of 128 rows x one item split (2 per CU)
@@ -376,7 +377,7 @@ class SoftmaxHead:
                  w.ZT.data_ptr(), w.ldz, w.pmax.data_ptr(), w.psum.data_ptr(), w.parg.data_ptr(), 1, st)
         call("rg_lse_combine", w.pmax.data_ptr(), w.psum.data_ptr(), w.parg.data_ptr(), B, w.nJ, w.work.data_ptr(),
              w.ZT.data_ptr(), w.ldz, tgt.data_ptr(), self.A, w.lse.data_ptr(), w.amax.data_ptr(),
-             w.loss_row.data_ptr(), st)
+             w.loss_row.data_ptr(), None, st)
         call("rg_sum_scale", w.loss_row.data_ptr(), B, _f32(1.0 / B), w.loss.data_ptr(), None, st)
         return w.loss, w
 
@@ -396,14 +397,15 @@ class SoftmaxHead:
                  self.b.p.data_ptr(), self.b.m.data_ptr(), self.b.v.data_ptr(), adam6, None, None, st)
 
     def argmax(self, h, slot="argmax"):
-        """argmax_j (h·Wᵀ + b)[b, j] without storing Z (first maximum)."""
+        """argmax_j (h·Wᵀ + b)[b, j] without storing Z (first maximum); the
+        row maxima are left in ``self.ws(slot, B, False).mx``."""
         B = h.shape[0]
         w = self.ws(slot, B, False)
         st = stream_ptr()
         call("rg_head_fwd", h.data_ptr(), self.W.p.data_ptr(), self.b.p.data_ptr(), B, self.A, self.HF, None, 0,
              w.pmax.data_ptr(), w.psum.data_ptr(), w.parg.data_ptr(), 0, st)
         call("rg_lse_combine", w.pmax.data_ptr(), w.psum.data_ptr(), w.parg.data_ptr(), B, w.nJ, w.work.data_ptr(),
-             None, 0, None, self.A, None, w.amax.data_ptr(), None, st)
+             None, 0, None, self.A, None, w.amax.data_ptr(), None, w.mx.data_ptr(), st)
         return w.amax
 
 

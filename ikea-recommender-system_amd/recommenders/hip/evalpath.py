@@ -53,7 +53,7 @@ def eval_batch(model, s, s_len, a, *, head_idx=0, K=20, ks=(20,), padding_pos="e
     if want_loss:
         call("rg_lse_combine", ws.pmax.data_ptr(), ws.psum.data_ptr(), ws.parg.data_ptr(), B, ws.nJ,
              ws.work.data_ptr(), ws.ZT.data_ptr(), ws.ldz, a.data_ptr(), head.A, ws.lse.data_ptr(),
-             ws.amax.data_ptr(), ws.loss_row.data_ptr(), st)
+             ws.amax.data_ptr(), ws.loss_row.data_ptr(), None, st)
         loss = torch.empty(1, device=dev)
         call("rg_sum_scale", ws.loss_row.data_ptr(), B, _f32(1.0 / B), loss.data_ptr(), None, st)
         out.loss = loss

@@ -43,6 +43,7 @@ class HipNet:
         if comm is not None:
             from .dist import item_shard
             shard = item_shard(action_dim, comm.world, comm.rank)
+        self.shard = shard
         if n_negatives:
             if comm is not None:
                 raise NotImplementedError("sampled softmax with item sharding")

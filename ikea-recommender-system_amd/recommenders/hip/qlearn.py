@@ -27,11 +27,11 @@ class QHead(SoftmaxHead):
     """Linear(H -> A) used through row gathers, argmax (fused GEMM pass, no Z
     stored) and row-sparse gradients; logits_T for evaluation."""
 
-    def __init__(self, name, A, HF, device):
-        super().__init__(name, A, HF, device)
+    def __init__(self, name, A, HF, device, shard=None):
+        super().__init__(name, A, HF, device, shard=shard)
         self.G = torch.zeros_like(self.W.p)
         self.Gb = torch.zeros_like(self.b.p)
-        self.tags = torch.zeros(A, dtype=torch.int32, device=device)
+        self.tags = torch.zeros(self.A, dtype=torch.int32, device=device)
 
     def adam(self, adam6, tag):
         st = stream_ptr()
@@ -53,7 +53,7 @@ class QNet(HipNet):
 
     def __init__(self, *, q_names, **kw):
         super().__init__(head_names=["sup_head_output"], **kw)
-        self.q_heads = [QHead(n, self.action_dim, self.hf, self.device) for n in q_names]
+        self.q_heads = [QHead(n, self.action_dim, self.hf, self.device, shard=self.shard) for n in q_names]
         for q in self.q_heads:
             setattr(self, q.name, q)
         self._argmax_head = None
@@ -75,6 +75,8 @@ class QNet(HipNet):
     def forward(self, s, lengths):
         """(sup (B, A), q (B, A)) for SQN; (sup, q_all (B, heads, A)) for SMORL,
         as the reference's nn.Module forward returns (sqn_gru.py:87-112)."""
+        if self.comm is not None:
+            raise NotImplementedError("forward() of an item-sharded model: each rank holds a slice of the items")
         h = self.hidden(s, lengths, slot="eval", save=False)
         _, sup = self.sup_head_output.logits_T(h, slot="eval")
         outs = [q.logits_T(h, slot="eval")[1] for q in self.q_heads]
@@ -89,7 +91,7 @@ class QNet(HipNet):
             return self.q_heads[0].argmax(h, slot="argmax")
         if self._argmax_head is None:
             hd = SoftmaxHead.__new__(SoftmaxHead)
-            hd.name, hd.A, hd.HF, hd.device, hd._ws = "qcomb", self.action_dim, self.hf, self.device, {}
+            hd.name, hd.A, hd.HF, hd.device, hd._ws = "qcomb", self.q_heads[0].A, self.hf, self.device, {}
             hd.W = _T(torch.empty_like(self.q_heads[0].W.p))
             hd.b = _T(torch.empty_like(self.q_heads[0].b.p))
             self._argmax_head = hd

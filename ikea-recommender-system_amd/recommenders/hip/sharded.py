@@ -21,9 +21,10 @@ The output layer's gradient (A × H, 512 MB at C2) is never communicated.
 """
 from __future__ import annotations
 
+import numpy as np
 import torch
 
-from . import call, stream_ptr
+from . import call, host_ptr_array, stream_ptr
 from .engine import _f32
 from .timing import region
 
@@ -38,31 +39,21 @@ def _buf(net, name, shape, dtype=torch.float32):
     return t
 
 
-def sharded_supervised_step(net, clock, s, a, true_len):
+def _sharded_ce_forward(net, head, H_all, a_all, st, want_argmax=False):
+    """CE(mean over world·B rows) of the item-sharded head: local logits over
+    items [lo, hi) for every gathered row, per-rank LSE merged across ranks,
+    target logit summed from its owner.  Keeps Zᵀ/lse for the backward.  With
+    want_argmax the local (row max, argmax) are left in w.mx / w.amax."""
     comm = net.comm
-    dev = net.device
-    s = s.to(dev, non_blocking=True)
-    a = a.to(dev, non_blocking=True).contiguous()
-    head = next(iter(net.heads.values()))
     W_, HF = comm.world, net.hf
-    st = stream_ptr()
-    h = net.trunk.forward(s, true_len, slot="main", save=True)
-    B = h.shape[0]
-    Bg = W_ * B
-    mask = None
-    h_in = h
-    if net.training and net.dropout_p > 0:
-        mask = net.dropout_mask(B)
-        h_in = net.apply_mask(h, mask, _buf(net, "hd", (B, HF)))
-    with region("comm_fwd"):
-        H_all = comm.all_gather(_buf(net, "H_all", (Bg, HF)), h_in)
-        a_all = comm.all_gather(_buf(net, "a_all", (Bg,), torch.int64), a)
+    Bg = H_all.shape[0]
     w = head.ws("main", Bg, True)
     with region("head_fwd"):
         call("rg_head_fwd", H_all.data_ptr(), head.W.p.data_ptr(), head.b.p.data_ptr(), Bg, head.A, HF,
              w.ZT.data_ptr(), w.ldz, w.pmax.data_ptr(), w.psum.data_ptr(), w.parg.data_ptr(), 1, st)
     call("rg_lse_combine", w.pmax.data_ptr(), w.psum.data_ptr(), w.parg.data_ptr(), Bg, w.nJ, w.work.data_ptr(),
-         None, 0, None, head.A, w.lse.data_ptr(), None, None, st)
+         None, 0, None, head.A, w.lse.data_ptr(), w.amax.data_ptr() if want_argmax else None, None,
+         w.mx.data_ptr() if want_argmax else None, st)
     zt = _buf(net, "zt", (Bg,))
     tgt_loc = _buf(net, "tgt_loc", (Bg,), torch.int64)
     call("rg_shard_targets", w.ZT.data_ptr(), w.ldz, a_all.data_ptr(), head.lo, head.hi, Bg, zt.data_ptr(),
@@ -74,15 +65,57 @@ def sharded_supervised_step(net, clock, s, a, true_len):
     call("rg_lse_merge_ranks", lse_r.data_ptr(), W_, Bg, lse.data_ptr(), st)
     call("rg_sub", lse.data_ptr(), zt.data_ptr(), Bg, w.loss_row.data_ptr(), st)
     call("rg_sum_scale", w.loss_row.data_ptr(), Bg, _f32(1.0 / Bg), w.loss.data_ptr(), None, st)
+    return w, lse, tgt_loc
+
+
+def _sharded_ce_dh(net, head, w, lse, tgt_loc, dH_all, st):
+    """dH_all (world·B × HF) := dZ · W_shard for every gathered row."""
+    Bg = dH_all.shape[0]
+    with region("head_dh"):
+        n = call("rg_head_dh", w.ZT.data_ptr(), w.ldz, lse.data_ptr(), tgt_loc.data_ptr(), _f32(1.0 / Bg),
+                 head.W.p.data_ptr(), Bg, head.A, net.hf, w.dh_splits, w.dh_slabs.data_ptr(), st)
+    call("rg_reduce_slabs", w.dh_slabs.data_ptr(), n, Bg * net.hf, dH_all.data_ptr(), None, net.hf, 0, st)
+
+
+def _sharded_ce_dw_adam(net, head, w, lse, tgt_loc, H_all, adam6, st):
+    Bg = H_all.shape[0]
+    with region("head_dw_adam"):
+        call("rg_head_dw_adam", w.ZT.data_ptr(), w.ldz, lse.data_ptr(), tgt_loc.data_ptr(), _f32(1.0 / Bg),
+             H_all.data_ptr(), Bg, head.A, net.hf, head.W.p.data_ptr(), head.W.m.data_ptr(), head.W.v.data_ptr(),
+             head.b.p.data_ptr(), head.b.m.data_ptr(), head.b.v.data_ptr(), adam6, None, None, st)
+
+
+def _gather_rows(comm, net, name, x):
+    """all_gather of a local (B, ...) tensor into (world·B, ...), rank-major."""
+    out = _buf(net, name, (comm.world * x.shape[0],) + tuple(x.shape[1:]), x.dtype)
+    return comm.all_gather(out, x.contiguous())
+
+
+def sharded_supervised_step(net, clock, s, a, true_len):
+    comm = net.comm
+    dev = net.device
+    s = s.to(dev, non_blocking=True)
+    a = a.to(dev, non_blocking=True).contiguous()
+    head = next(iter(net.heads.values()))
+    HF = net.hf
+    st = stream_ptr()
+    h = net.trunk.forward(s, true_len, slot="main", save=True)
+    B = h.shape[0]
+    Bg = comm.world * B
+    mask = None
+    h_in = h
+    if net.training and net.dropout_p > 0:
+        mask = net.dropout_mask(B)
+        h_in = net.apply_mask(h, mask, _buf(net, "hd", (B, HF)))
+    with region("comm_fwd"):
+        H_all = _gather_rows(comm, net, "H_all", h_in)
+        a_all = _gather_rows(comm, net, "a_all", a)
+    w, lse, tgt_loc = _sharded_ce_forward(net, head, H_all, a_all, st)
     # ---- backward ----
     adam6 = clock.next_args()
     net.trunk_tag = getattr(net, "trunk_tag", 0) + 1
-    g = _f32(1.0 / Bg)
     dH_all = _buf(net, "dH_all", (Bg, HF))
-    with region("head_dh"):
-        n = call("rg_head_dh", w.ZT.data_ptr(), w.ldz, lse.data_ptr(), tgt_loc.data_ptr(), g, head.W.p.data_ptr(),
-                 Bg, head.A, HF, w.dh_splits, w.dh_slabs.data_ptr(), st)
-    call("rg_reduce_slabs", w.dh_slabs.data_ptr(), n, Bg * HF, dH_all.data_ptr(), None, HF, 0, st)
+    _sharded_ce_dh(net, head, w, lse, tgt_loc, dH_all, st)
     dh = net.dh_buffer(B)
     with region("comm_dh"):
         comm.reduce_scatter(dh, dH_all)
@@ -91,13 +124,178 @@ def sharded_supervised_step(net, clock, s, a, true_len):
     net.trunk.backward(dh, slot="main")
     net.trunk.grads_for_allreduce(net.trunk_tag)
     works = net.trunk.allreduce_start(comm)
-    with region("head_dw_adam"):
-        call("rg_head_dw_adam", w.ZT.data_ptr(), w.ldz, lse.data_ptr(), tgt_loc.data_ptr(), g, H_all.data_ptr(),
-             Bg, head.A, HF, head.W.p.data_ptr(), head.W.m.data_ptr(), head.W.v.data_ptr(), head.b.p.data_ptr(),
-             head.b.m.data_ptr(), head.b.v.data_ptr(), adam6, None, None, st)
+    _sharded_ce_dw_adam(net, head, w, lse, tgt_loc, H_all, adam6, st)
     with region("comm_wait"):
         for wk in works:
             if wk is not None:
                 wk.wait()
     net.trunk.adam_after_allreduce(adam6)
     return w.loss
+
+
+# ------------------------------------------------------ double-Q (C4) ------
+def _owner_q(qnet, buf_net, H_all, name, idx64=None, idx32=None):
+    """Q_i(row)[idx] for every gathered row: the rank holding item idx computes
+    it, the others write 0, a SUM all-reduce leaves the owner's exact value on
+    every rank.  Returns (q (world·B, nh), local index (world·B) or −1)."""
+    comm = buf_net.comm
+    st = stream_ptr()
+    Bg = H_all.shape[0]
+    qh = qnet.q_heads[0]
+    loc = _buf(buf_net, name + "_loc", (Bg,), torch.int64)
+    call("rg_shard_index", None if idx64 is None else idx64.data_ptr(), None if idx32 is None else idx32.data_ptr(),
+         Bg, qh.lo, qh.hi, loc.data_ptr(), st)
+    q = qnet.gather_q(H_all, idx64=loc, out=_buf(buf_net, name, (Bg, len(qnet.q_heads))))
+    comm.all_reduce(q)
+    return q, loc
+
+
+def _global_argmax(net, mx, am, A, name):
+    """Merge every rank's (row max, local argmax) into the global first-maximum index."""
+    comm = net.comm
+    Bg = mx.shape[0]
+    mx_r = _gather_rows(comm, net, name + "_mx", mx)
+    am_r = _gather_rows(comm, net, name + "_am", am)
+    out = _buf(net, name, (Bg,), torch.int32)
+    call("rg_argmax_merge_ranks", mx_r.data_ptr(), am_r.data_ptr(), comm.world, Bg, A, out.data_ptr(), None,
+         stream_ptr())
+    return out
+
+
+def _global_topk(net, head, w, K, name):
+    """Canonical top-K of the supervised logits over all items, every gathered row."""
+    comm = net.comm
+    Bg = w.B
+    st = stream_ptr()
+    vals = _buf(net, name + "_v", (Bg, K))
+    idx = _buf(net, name + "_i", (Bg, K), torch.int32)
+    call("rg_topk", w.ZT.data_ptr(), w.ldz, w.pmax.data_ptr(), Bg, head.A, K, idx.data_ptr(), vals.data_ptr(),
+         None, st)
+    v_r = _gather_rows(comm, net, name + "_vr", vals)
+    i_r = _gather_rows(comm, net, name + "_ir", idx)
+    out = _buf(net, name, (Bg, K), torch.int32)
+    call("rg_topk_merge_ranks", v_r.data_ptr(), i_r.data_ptr(), comm.world, Bg, K, head.A_full, out.data_ptr(), None,
+         st)
+    return out
+
+
+def sharded_double_q_step(nets, clocks, k, s, a, r, s_next, true_len, true_next_len, is_end, *, gamma, smorl=None):
+    """SQN / SMORL step over the global batch (every rank's B rows) with the
+    trunk replicated and every head item-sharded:
+
+      trunks      local fwd (main on s and s', boot on s' with true_len)
+      all_gather  h, h', h_boot, a (world·B rows)
+      sup CE      as sharded_supervised_step
+      Q(s, a)     owner computes, SUM all-reduce
+      a*          local argmax of (Σ w_i) Q_main(s', ·) per shard -> all_gather
+                  (max, index) -> first global maximum (rg_argmax_merge_ranks)
+      Q_boot(s', a*)  owner computes, SUM all-reduce
+      TD / SMORL  on the rank's own rows; losses summed over ranks
+      backward    sup dH + Q-head dH accumulate in one (world·B × HF) buffer,
+                  one reduce_scatter; trunk grads all-reduced; head rows and
+                  their Adam moments never leave their owner.
+    Returns device (sup_loss, q_loss) — the global-batch means."""
+    from .qlearn import _dev
+    main, boot = nets[k], nets[1 - k]
+    comm = main.comm
+    dev = main.device
+    s = _dev(s, dev)
+    a = _dev(a, dev).contiguous()
+    s_next = _dev(s_next, dev)
+    end8 = _dev(is_end, dev, torch.uint8)
+    B = s.shape[0]
+    Bg = comm.world * B
+    rows = slice(comm.rank * B, (comm.rank + 1) * B)
+    nh = len(main.q_heads)
+    HF = main.hf
+    A = main.action_dim
+    st = stream_ptr()
+    sup = main.sup_head_output
+    with region("sqn_trunk_main"):
+        h = main.trunk.forward(s, true_len, slot="main", save=True)
+    with region("comm_fwd"):
+        H_all = _gather_rows(comm, main, "H_all", h)
+        a_all = _gather_rows(comm, main, "a_all", a)
+    want_top1 = smorl is not None and max(smorl["topk_div"], smorl["topk_nov"]) == 1
+    w, lse, tgt_loc = _sharded_ce_forward(main, sup, H_all, a_all, st, want_argmax=want_top1)
+    sup_loss = w.loss
+    q_all, a_loc = _owner_q(main, main, H_all, "q", idx64=a_all)
+    with region("sqn_target"):
+        h_n = main.trunk.forward(s_next, true_next_len, slot="next", save=False)
+        Hn_all = _gather_rows(comm, main, "Hn_all", h_n)
+        am = main.argmax_q(Hn_all, None if smorl is None else smorl["w"])
+        head_am = main.q_heads[0] if len(main.q_heads) == 1 else main._argmax_head
+        a_star = _global_argmax(main, head_am.ws("argmax", Bg, False).mx, am, A, "a_star")
+        h_b = boot.trunk.forward(s_next, true_len, slot="boot", save=False)   # quirk: true_len
+        Hb_all = _gather_rows(comm, main, "Hb_all", h_b)
+        qn_all, _ = _owner_q(boot, main, Hb_all, "qn", idx32=a_star)
+    q = q_all[rows]
+    qn = qn_all[rows]
+    dq = _buf(main, "dq", (B, nh))
+    if smorl is None:
+        r64 = _dev(r, dev, torch.float64)
+        sq = _buf(main, "sq", (B,), torch.float64)
+        q_loss = _buf(main, "qloss64", (1,), torch.float64)
+        call("rg_sqn_td", q.data_ptr(), qn.data_ptr(), r64.data_ptr(), end8.data_ptr(), _f32(gamma), B, 1.0 / Bg,
+             sq.data_ptr(), dq.data_ptr(), st)
+        call("rg_sum64", sq.data_ptr(), B, 1.0 / Bg, q_loss.data_ptr(), None, st)
+    else:
+        if want_top1:
+            top = _global_argmax(main, w.mx, w.amax, A, "sup_top1").view(Bg, 1)
+        else:
+            top = _global_topk(main, sup, w, max(smorl["topk_div"], smorl["topk_nov"]), "sup_topk")
+        rr = _smorl_rewards_rows(main, smorl, s, r, true_next_len, top[rows].contiguous(), B)
+        row = _buf(main, "qrow", (B,))
+        q_loss = _buf(main, "qloss32", (1,))
+        grad_row = _f32(np.float32(smorl["alpha"]) / np.float32(Bg))
+        call("rg_smorl_td", q.data_ptr(), qn.data_ptr(), rr.data_ptr(), end8.data_ptr(), smorl["w_dev"].data_ptr(),
+             nh, _f32(gamma), grad_row, B, row.data_ptr(), dq.data_ptr(), st)
+        call("rg_sum_scale", row.data_ptr(), B, _f32(1.0 / Bg), q_loss.data_ptr(), None, st)
+    comm.all_reduce(q_loss)
+    # ---- backward + Adam (main network, its own optimizer clock) ----
+    adam6 = clocks[k].next_args()
+    main.trunk_tag = getattr(main, "trunk_tag", 0) + 1
+    tag = main.trunk_tag
+    dH_all = _buf(main, "dH_all", (Bg, HF))
+    _sharded_ce_dh(main, sup, w, lse, tgt_loc, dH_all, st)
+    dq_all = _gather_rows(comm, main, "dq_all", dq)
+    call("rg_q_backward", H_all.data_ptr(), HF, host_ptr_array([x.W.p for x in main.q_heads]),
+         host_ptr_array([x.G for x in main.q_heads]), host_ptr_array([x.Gb for x in main.q_heads]),
+         host_ptr_array([x.tags for x in main.q_heads]), nh, a_loc.data_ptr(), Bg, dq_all.data_ptr(),
+         dH_all.data_ptr(), tag, st)
+    dh = main.dh_buffer(B)
+    with region("comm_dh"):
+        comm.reduce_scatter(dh, dH_all)
+    main.trunk.backward(dh, slot="main")
+    main.trunk.grads_for_allreduce(tag)
+    works = main.trunk.allreduce_start(comm)
+    _sharded_ce_dw_adam(main, sup, w, lse, tgt_loc, H_all, adam6, st)
+    for qh in main.q_heads:
+        qh.adam(adam6, tag)
+    with region("comm_wait"):
+        for wk in works:
+            if wk is not None:
+                wk.wait()
+    main.trunk.adam_after_allreduce(adam6)
+    return sup_loss, q_loss
+
+
+def _smorl_rewards_rows(main, smorl, s, r_acc, true_next_len, idx, B):
+    """r = stack([r_acc, r_div, r_nov]) for the rank's rows from their global top-k list."""
+    from .qlearn import _dev
+    dev = main.device
+    st = stream_ptr()
+    K = idx.shape[1]
+    r_div = _buf(main, "r_div", (B,))
+    lens = _dev(true_next_len, dev, torch.int64)   # quirk: diversity uses true_next_len
+    call("rg_diversity", s.data_ptr(), s.shape[1], lens.data_ptr(), 1 if smorl["pad_end"] else 0, idx.data_ptr(),
+         smorl["topk_div"], K, smorl["div_table"].data_ptr(), smorl["div_table"].shape[1], _f32(1e-6), B,
+         r_div.data_ptr(), st)
+    r_nov = _buf(main, "r_nov", (B,))
+    call("rg_novelty", idx.data_ptr(), smorl["topk_nov"], K, smorl["bitmap"].data_ptr(), _f32(smorl["nov_rew_sig"]),
+         B, r_nov.data_ptr(), st)
+    r64 = _dev(r_acc, dev, torch.float64)
+    rr = _buf(main, "rr", (B, 3))
+    call("rg_stack_rewards", r64.data_ptr(), r_div.data_ptr(), r_nov.data_ptr(), B, rr.data_ptr(), st)
+    main._last_rewards = rr
+    return rr

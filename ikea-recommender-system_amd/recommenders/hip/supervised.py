@@ -15,6 +15,8 @@ from .nets import HipNet
 
 class SupervisedNet(HipNet):
     def forward(self, s, lengths):
+        if self.comm is not None:
+            raise NotImplementedError("forward() of an item-sharded model: each rank holds a slice of the items")
         h = self.hidden(s, lengths, slot="eval", save=False)
         if self.training and self.dropout_p > 0:
             mask = self.dropout_mask(h.shape[0])

@@ -17,14 +17,16 @@ import torch.nn as nn
 
 from recommenders.hip import require_gpu
 from recommenders.hip.engine import AdamClock
+from recommenders.hip.dist import Comm
 from recommenders.hip.qlearn import QNet, double_q_step, unpopular_bitmap
+from recommenders.hip.sharded import sharded_double_q_step
 from recommenders.models.GRU4Rec.model import _AdamFacade
 
 
 class SMORL_GRU_Net(QNet):
     def __init__(self, hidden_dim, embedding_dim, item_num, state_size, action_dim, q_weights, gamma, gru_layers=1,
                  random_embed_init=True, train_pad_embed=True, use_packed_seq=False, padding_idx=None,
-                 name="SMORL_GRU_Network", device="cuda"):
+                 name="SMORL_GRU_Network", device="cuda", comm=None):
         if not random_embed_init:
             raise NotImplementedError("TODO: Pretrained embedings.")
         if use_packed_seq:
@@ -33,7 +35,7 @@ class SMORL_GRU_Net(QNet):
                          hidden_dim=hidden_dim, embedding_dim=embedding_dim, item_num=item_num,
                          state_size=state_size, action_dim=action_dim, gru_layers=gru_layers,
                          use_packed_seq=use_packed_seq, train_pad_embed=train_pad_embed, padding_idx=padding_idx,
-                         bidir=False, device=device)
+                         bidir=False, device=device, comm=comm)
         self.q_weights = q_weights
         self.gamma = gamma
         self.name = name
@@ -44,17 +46,18 @@ class SMORL_trainer:
                  item_num, state_size, action_dim, gamma, gru_layers, q_weights, alpha, div_embedding,
                  unpopular_actions_set, topk_div, device, input_tokenizer=None, output_tokenizer=None,
                  padding_idx=None, torch_rand_seed=118, python_rand_seed=999, name_1="SMORL_1", name_2="SMORL_2",
-                 topk_nov=1, nov_rew_sig=1):
+                 topk_nov=1, nov_rew_sig=1, shard_items=False, process_group=None):
         torch.manual_seed(torch_rand_seed)
         random.seed(python_rand_seed)
         self.device = require_gpu(device)
+        self.comm = Comm(process_group) if shard_items else None   # item-sharded heads (multi-GPU)
         if input_tokenizer is not None or output_tokenizer is not None:
             raise NotImplementedError("tokenizer remap (SURVEY §8f rank 4) is not on the device path yet")
         mk = lambda name: SMORL_GRU_Net(hidden_dim=hidden_dim, item_num=item_num, state_size=state_size,
                                         action_dim=action_dim, gru_layers=gru_layers, gamma=gamma,
                                         q_weights=q_weights, embedding_dim=embedding_dim,
                                         train_pad_embed=train_pad_embed, use_packed_seq=use_packed_seq,
-                                        padding_idx=padding_idx, name=name, device=self.device)
+                                        padding_idx=padding_idx, name=name, device=self.device, comm=self.comm)
         self.SMORL_1 = mk(name_1)
         self.SMORL_2 = mk(name_2)
         self.gamma = gamma
@@ -92,8 +95,9 @@ class SMORL_trainer:
     def train_step_async(self, s, a, r_acc, s_next, true_len, true_next_len, is_end):
         k = 0 if random.uniform(0, 1) <= 0.5 else 1
         self.last_main = k
-        return double_q_step([self.SMORL_1, self.SMORL_2], [self.clock_1, self.clock_2], k, s, a, r_acc, s_next,
-                             true_len, true_next_len, is_end, gamma=self.gamma, smorl=self._smorl)
+        step = sharded_double_q_step if self.comm is not None else double_q_step
+        return step([self.SMORL_1, self.SMORL_2], [self.clock_1, self.clock_2], k, s, a, r_acc, s_next,
+                    true_len, true_next_len, is_end, gamma=self.gamma, smorl=self._smorl)
 
     def train_step(self, s, a, r_acc, s_next, true_len, true_next_len, is_end):
         sup, q = self.train_step_async(s, a, r_acc, s_next, true_len, true_next_len, is_end)

@@ -14,14 +14,16 @@ import torch.nn as nn
 
 from recommenders.hip import require_gpu
 from recommenders.hip.engine import AdamClock
+from recommenders.hip.dist import Comm
 from recommenders.hip.qlearn import QNet, double_q_step
+from recommenders.hip.sharded import sharded_double_q_step
 from recommenders.models.GRU4Rec.model import _AdamFacade
 
 
 class SQN_Network(QNet):
     def __init__(self, hidden_dim, item_num, state_size, action_dim, gamma, gru_layers, embedding_dim=50,
                  random_embed_init=True, train_pad_embed=True, use_packed_seq=False, padding_idx=None,
-                 name="DQNetwork", device="cuda"):
+                 name="DQNetwork", device="cuda", comm=None):
         if not random_embed_init:
             raise NotImplementedError("TODO: Pretrained embedings.")  # as the reference (:67-68)
         if use_packed_seq:
@@ -29,7 +31,8 @@ class SQN_Network(QNet):
         super().__init__(q_names=["q_head_output"], trunk_attr="base_model", hidden_dim=hidden_dim,
                          embedding_dim=embedding_dim, item_num=item_num, state_size=state_size,
                          action_dim=action_dim, gru_layers=gru_layers, use_packed_seq=use_packed_seq,
-                         train_pad_embed=train_pad_embed, padding_idx=padding_idx, bidir=False, device=device)
+                         train_pad_embed=train_pad_embed, padding_idx=padding_idx, bidir=False, device=device,
+                         comm=comm)
         self.gamma = gamma
         self.name = name
         self.random_embed_init = random_embed_init
@@ -38,15 +41,18 @@ class SQN_Network(QNet):
 class SQN_trainer:
     def __init__(self, hidden_dim, embedding_dim, train_pad_embed, use_packed_seq, learning_rate, item_num,
                  state_size, action_dim, gamma, gru_layers, device, padding_idx=None, torch_rand_seed=118,
-                 python_rand_seed=999, name_1="SQN_1", name_2="SQN_2"):
+                 python_rand_seed=999, name_1="SQN_1", name_2="SQN_2", shard_items=False, process_group=None):
         torch.manual_seed(torch_rand_seed)
         random.seed(python_rand_seed)
         self.device = require_gpu(device)
+        # shard_items (build extension, off by default): multi-GPU weak scaling,
+        # every head item-sharded over the ranks (recommenders/hip/sharded.py)
+        self.comm = Comm(process_group) if shard_items else None
         mk = lambda name: SQN_Network(hidden_dim=hidden_dim, item_num=item_num, state_size=state_size,
                                       action_dim=action_dim, gamma=gamma, gru_layers=gru_layers,
                                       embedding_dim=embedding_dim, train_pad_embed=train_pad_embed,
                                       use_packed_seq=use_packed_seq, padding_idx=padding_idx, name=name,
-                                      device=self.device)
+                                      device=self.device, comm=self.comm)
         self.DQN_1 = mk(name_1)
         self.DQN_2 = mk(name_2)
         self.gamma = gamma
@@ -61,8 +67,9 @@ class SQN_trainer:
     def train_step_async(self, s, a, r, s_next, true_len, true_next_len, is_end):
         k = 0 if random.uniform(0, 1) <= 0.5 else 1
         self.last_main = k
-        return double_q_step([self.DQN_1, self.DQN_2], [self.clock_1, self.clock_2], k, s, a, r, s_next, true_len,
-                             true_next_len, is_end, gamma=self.gamma)
+        step = sharded_double_q_step if self.comm is not None else double_q_step
+        return step([self.DQN_1, self.DQN_2], [self.clock_1, self.clock_2], k, s, a, r, s_next, true_len,
+                    true_next_len, is_end, gamma=self.gamma)
 
     def train_step(self, s, a, r, s_next, true_len, true_next_len, is_end):
         """One double-Q step; returns (sup_loss, q_loss) as Python floats."""

@@ -92,10 +92,11 @@ int rg_gru_bwd(const float* saved, int64_t plane, const float* Whh, const int32_
 int rg_head_fwd(const float* h, const float* W, const float* bias, int B, int A, int HF, float* ZT, int64_t ldz,
                 float* pmax, float* psum, int32_t* parg, int want_sum, rg_stream_t stream);
 /* partials -> lse (B), argmax (B) (torch.argmax semantics: first maximum),
- * loss_row (B) = lse - Z[a_b, b].  work: 3*min(64,nJ)*B floats. */
+ * loss_row (B) = lse - Z[a_b, b], mx (B) = the row maximum.  Every output is
+ * optional.  work: 3*min(64,nJ)*B floats. */
 int rg_lse_combine(const float* pmax, const float* psum, const int32_t* parg, int B, int nJ, float* work,
                    const float* ZT, int64_t ldz, const int64_t* tgt, int A, float* lse, int32_t* amax,
-                   float* loss_row, rg_stream_t stream);
+                   float* loss_row, float* mx, rg_stream_t stream);
 int rg_sum_scale(const float* x, int n, float scale, float* out, double* out64, rg_stream_t stream);
 /* ---- item-sharded head (multi-GPU; no reference counterpart): rank r owns
  * items [lo, hi).  lse over all items = logsumexp over ranks of the per-rank
@@ -105,6 +106,17 @@ int rg_lse_merge_ranks(const float* lse_r, int nr, int B, float* lse, rg_stream_
 int rg_shard_targets(const float* ZT, int64_t ldz, const int64_t* tgt, int64_t lo, int64_t hi, int B, float* zt,
                      int64_t* tgt_loc, rg_stream_t stream);
 int rg_sub(const float* a, const float* b, int n, float* out, rg_stream_t stream);
+/* multi-GPU double-Q (config C4, csrc/shard.hip): out[i] = idx[i] - lo if lo <= idx[i] < hi else -1
+ * (exactly one of idx64/idx32); rg_q_gather / rg_q_backward skip rows with index -1. */
+int rg_shard_index(const int64_t* idx64, const int32_t* idx32, int n, int64_t lo, int64_t hi, int64_t* out,
+                   rg_stream_t stream);
+/* global argmax per row from nr ranks' (row max, local argmax) (rank-major nr x n); ties -> lowest
+ * global index (torch.argmax / sqn_gru.py get_max_action over the whole row) */
+int rg_argmax_merge_ranks(const float* mx, const int32_t* am, int nr, int n, int64_t A, int32_t* out,
+                          float* out_max, rg_stream_t stream);
+/* global canonical top-K per row (value desc, index asc) from nr ranks' local top-K lists (nr x n x K) */
+int rg_topk_merge_ranks(const float* vals, const int32_t* idx, int nr, int n, int K, int64_t A, int32_t* out_idx,
+                        float* out_val, rg_stream_t stream);
 /* backward of CE + Linear w.r.t. h: dh slabs (returns number of slabs > 0). */
 int rg_head_dh(const float* ZT, int64_t ldz, const float* lse, const int64_t* tgt, float gscale, const float* W,
                int B, int A, int HF, int splits, float* slabs, rg_stream_t stream);

@@ -183,9 +183,12 @@ def test_head_forward_backward(B, A, HF):
     lse = torch.zeros(B, device=dev)
     amax = torch.zeros(B, dtype=torch.int32, device=dev)
     lrow = torch.zeros(B, device=dev)
+    mx = torch.zeros(B, device=dev)
     C().call("rg_lse_combine", pm.data_ptr(), ps.data_ptr(), pa.data_ptr(), B, nJ, work.data_ptr(), ZT.data_ptr(),
-             ldz, td.data_ptr(), A, lse.data_ptr(), amax.data_ptr(), lrow.data_ptr(), st())
+             ldz, td.data_ptr(), A, lse.data_ptr(), amax.data_ptr(), lrow.data_ptr(), mx.data_ptr(), st())
     torch.testing.assert_close(lse.cpu().double(), torch.logsumexp(Zref, 1), rtol=0, atol=2e-5)
+    # the row maximum is the exact stored logit at the argmax
+    np.testing.assert_array_equal(mx.cpu().numpy(), ZT[:, :B].t().cpu().max(1).values.numpy())
     Zg = ZT[:, :B].t().cpu()
     assert torch.equal(amax.cpu().long(), torch.argmax(Zg, 1))
     ce = torch.nn.functional.cross_entropy(Zref, tgt, reduction="none")

@@ -18,6 +18,7 @@ ap.add_argument("--A", type=int, default=1_000_000)
 ap.add_argument("--H", type=int, default=128)
 ap.add_argument("--iters", type=int, default=5)
 ap.add_argument("--variants", action="store_true", help="also time fwd without Zᵀ stores / Σexp, dW without Adam")
+ap.add_argument("--zeros", action="store_true", help="zero-filled h/W/bias (power/DVFS diagnostic)")
 a = ap.parse_args()
 B, A, H = a.B, a.A, a.H
 dev = "cuda"
@@ -26,6 +27,8 @@ h = torch.randn(B, H, device=dev, generator=g) * 0.3
 W = torch.randn(A, H, device=dev, generator=g) * 0.05
 bias = torch.randn(A, device=dev, generator=g) * 0.05
 tgt = torch.randint(0, A, (B,), device=dev, generator=g)
+if a.zeros:
+    h.zero_(); W.zero_(); bias.zero_()
 ldz = (B + 3) // 4 * 4
 nJ = (A + 127) // 128
 ZT = torch.empty(A, ldz, device=dev)
@@ -52,7 +55,7 @@ def fwd():
 
 def lsec():
     call("rg_lse_combine", pm.data_ptr(), ps.data_ptr(), pa.data_ptr(), B, nJ, work.data_ptr(), ZT.data_ptr(), ldz,
-         tgt.data_ptr(), A, lse.data_ptr(), amax.data_ptr(), lrow.data_ptr(), st)
+         tgt.data_ptr(), A, lse.data_ptr(), amax.data_ptr(), lrow.data_ptr(), None, st)
 
 
 def dh():
