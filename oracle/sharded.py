@@ -31,3 +31,54 @@ def sharded_ce(h_local, a_local, W_shard, b_shard, lo, hi, comm):
     dW, db = dZ.t() @ H_all, dZ.sum(0)
     dh = comm.reduce_scatter(torch.empty(B, H), dZ @ W_shard)
     return loss, dh, dW, db
+
+
+def sharded_argmax(scores_local, lo, comm):
+    """Global first-maximum index per row from each rank's (max, local argmax)
+    — the merge rule of csrc/shard.hip:k_argmax_merge_ranks (larger value wins,
+    ties keep the lower rank = lower global index)."""
+    world = comm.world
+    n = scores_local.shape[0]
+    mx, am = scores_local.max(1)                     # torch: first maximum
+    mx_r = comm.all_gather(torch.empty(world * n, dtype=mx.dtype), mx).view(world, n)
+    g_r = comm.all_gather(torch.empty(world * n, dtype=torch.int64), am + lo).view(world, n)
+    out = g_r[0].clone()
+    best = mx_r[0].clone()
+    for r in range(1, world):
+        upd = mx_r[r] > best
+        out[upd] = g_r[r][upd]
+        best[upd] = mx_r[r][upd]
+    return out
+
+
+def canonical_topk(scores, K):
+    """(value desc, index asc) first K indices per row."""
+    out = []
+    for row in scores.tolist():
+        out.append(sorted(range(len(row)), key=lambda j: (-row[j], j))[:K])
+    return torch.tensor(out, dtype=torch.int64)
+
+
+def sharded_topk(scores_local, K, lo, comm):
+    """Global canonical top-K per row: merge of every rank's local canonical
+    top-K (csrc/shard.hip:k_topk_merge_ranks)."""
+    world = comm.world
+    n = scores_local.shape[0]
+    loc = canonical_topk(scores_local, K)
+    v = torch.gather(scores_local, 1, loc)
+    v_r = comm.all_gather(torch.empty(world * n * K, dtype=v.dtype), v.reshape(-1)).view(world, n, K)
+    g_r = comm.all_gather(torch.empty(world * n * K, dtype=torch.int64), (loc + lo).reshape(-1)).view(world, n, K)
+    out = torch.empty(n, K, dtype=torch.int64)
+    for i in range(n):
+        pos = [0] * world
+        for q in range(K):
+            best = None
+            for r in range(world):
+                if pos[r] >= K:
+                    continue
+                cand = (-float(v_r[r, i, pos[r]]), int(g_r[r, i, pos[r]]), r)
+                if best is None or cand < best:
+                    best = cand
+            out[i, q] = best[1]
+            pos[best[2]] += 1
+    return out

@@ -56,6 +56,17 @@ def _worker(rank, world, port, q):
         assert torch.allclose(dh, hr.grad[rank * B:(rank + 1) * B], atol=1e-12)
         assert torch.allclose(dW, Wr.grad[lo:hi], atol=1e-12)
         assert torch.allclose(db, br.grad[lo:hi], atol=1e-12)
+        # double-Q target argmax and SMORL top-k over item shards (exact, ties
+        # planted inside and across the shard boundary)
+        from oracle.sharded import canonical_topk, sharded_argmax, sharded_topk
+        S = torch.randint(0, 5, (world * B, A), generator=gen).to(torch.float64)
+        S[0, :] = 3.0                   # every item tied
+        S[1, :] = -1.0
+        S[1, [2, A - 1]] = 9.0          # the tie spans both shards
+        loc = S[:, lo:hi]
+        assert torch.equal(sharded_argmax(loc, lo, comm_f), torch.argmax(S, 1))
+        for K in (1, 3, 7):
+            assert torch.equal(sharded_topk(loc, K, lo, comm_f), canonical_topk(S, K))
         q.put((rank, "ok"))
     except Exception as e:  # pragma: no cover - reported to the parent
         q.put((rank, repr(e)))
