@@ -250,6 +250,7 @@ extern "C" int rg_wgrad(const float* G, int M, const float* X, int N, int T_max,
     case 32: WG(32); break;
     case 64: WG(64); break;
     case 128: WG(128); break;
+    case 256: WG(256); break;
     default: return RG_ERR_SHAPE;
   }
 #undef WG

@@ -248,3 +248,143 @@ extern "C" int rg_gru_bwd(const float* saved, int64_t plane, const float* Whh, c
     default: return RG_ERR_SHAPE;
   }
 }
+
+// ------------------------------------------------ time-stepped path -------
+// For hidden sizes whose recurrent matrix cannot stay register-resident
+// (H = 256, config C5: W_hh is 768 KB), the recurrence runs one timestep per
+// pair of launches from a native loop: Gh = h·W_hhᵀ + b_hh for the rows still
+// active at step t (an MFMA GEMM, rg_gemm_f32, whose row count nact[t] is read
+// on the device), then one fused gate kernel.  Rows are length-sorted
+// descending, so the rows active at t are the prefix [0, nact[t]).  Same
+// formulas, token layout and saved planes as k_gru_fwd / k_gru_bwd.
+extern "C" int rg_gemm_f32(const float* A, int64_t sam, int64_t sak, const float* B, int64_t sbk, int64_t sbn,
+                           float* C, int64_t ldc, const float* bias, int M, const int32_t* Mptr, int N, int K,
+                           const int32_t* Kptr, int splits, hipStream_t stream);
+
+// nact[t] = #rows with length > t, t ≤ tmax (nact[tmax] = 0)
+__global__ void k_gru_counts(const int32_t* __restrict__ lsort, int B, int tmax, int32_t* __restrict__ nact) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t > tmax) return;
+  int lo = 0, hi = B;  // first row with lsort <= t (lsort descending)
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (lsort[mid] > t) lo = mid + 1;
+    else hi = mid;
+  }
+  nact[t] = lo;
+}
+
+__global__ void k_gru_step_fwd(int t, const float* __restrict__ Gi, const float* __restrict__ Gh,
+                               const int32_t* __restrict__ nact, const int32_t* __restrict__ offs, int H,
+                               float* __restrict__ hs, float* __restrict__ saved, int64_t plane) {
+  const int r = blockIdx.x;
+  if (r >= nact[t]) return;
+  const int64_t tok = offs[r] + t;
+  const float* gi = Gi + tok * 3 * H;
+  const float* gh = Gh + (int64_t)r * 3 * H;
+  for (int u = threadIdx.x; u < H; u += blockDim.x) {
+    const float hp = hs[(int64_t)r * H + u];
+    const float rr = sigmoidf_ref(gi[u] + gh[u]);
+    const float zz = sigmoidf_ref(gi[H + u] + gh[H + u]);
+    const float an = gh[2 * H + u];
+    const float nn = tanhf(gi[2 * H + u] + rr * an);
+    hs[(int64_t)r * H + u] = (hp - nn) * zz + nn;
+    if (saved) {
+      const int64_t o = tok * H + u;
+      saved[0 * plane + o] = hp;
+      saved[1 * plane + o] = rr;
+      saved[2 * plane + o] = zz;
+      saved[3 * plane + o] = nn;
+      saved[4 * plane + o] = an;
+    }
+  }
+}
+
+__global__ void k_gru_rows_out(const float* __restrict__ hs, const int32_t* __restrict__ perm, int B, int H,
+                               float* __restrict__ hout, int ldh, int hoff) {
+  const int r = blockIdx.x;
+  for (int u = threadIdx.x; u < H; u += blockDim.x) hout[(int64_t)perm[r] * ldh + hoff + u] = hs[(int64_t)r * H + u];
+}
+
+// dh entering step t: rows continuing from t+1 sum the direct and recurrent
+// terms left by step t+1; rows whose last token is t start from dh_final.
+__global__ void k_gru_step_bwd(int t, const float* __restrict__ saved, int64_t plane,
+                               const int32_t* __restrict__ nact, const int32_t* __restrict__ offs,
+                               const int32_t* __restrict__ perm, int H, const float* __restrict__ dhout, int lddh,
+                               int dhoff, float* __restrict__ dh_dir, const float* __restrict__ dh_mat,
+                               float* __restrict__ dGi, float* __restrict__ dGh, float* __restrict__ dGs) {
+  const int r = blockIdx.x;
+  if (r >= nact[t]) return;
+  const bool cont = r < nact[t + 1];
+  const int64_t tok = offs[r] + t;
+  const int G = 3 * H;
+  for (int u = threadIdx.x; u < H; u += blockDim.x) {
+    const int64_t ri = (int64_t)r * H + u;
+    const float dh = cont ? dh_dir[ri] + dh_mat[ri] : dhout[(int64_t)perm[r] * lddh + dhoff + u];
+    const int64_t o = tok * H + u;
+    const float hp = saved[0 * plane + o], rr = saved[1 * plane + o], zz = saved[2 * plane + o];
+    const float nn = saved[3 * plane + o], gh = saved[4 * plane + o];
+    const float dn = dh * (1.0f - zz);
+    const float dz = dh * (hp - nn);
+    const float dan = dn * (1.0f - nn * nn);
+    const float daz = dz * (zz * (1.0f - zz));
+    const float dar = (dan * gh) * (rr * (1.0f - rr));
+    const float dghn = dan * rr;
+    dh_dir[ri] = dh * zz;
+    float* gi = dGi + tok * G;
+    float* g2 = dGh + tok * G;
+    float* gs = dGs + (int64_t)r * G;
+    gi[u] = dar;
+    gi[H + u] = daz;
+    gi[2 * H + u] = dan;
+    g2[u] = dar;
+    g2[H + u] = daz;
+    g2[2 * H + u] = dghn;
+    gs[u] = dar;
+    gs[H + u] = daz;
+    gs[2 * H + u] = dghn;
+  }
+}
+
+extern "C" int rg_gru_fwd_steps(const float* Gi, const float* Whh, const float* bhh, const int32_t* perm,
+                                const int32_t* lsort, const int32_t* offs, int B, int H, int tmax, float* hout,
+                                int ldh, int hoff, float* saved, int64_t plane, float* work, hipStream_t stream) {
+  if (B <= 0 || H <= 0 || H % 4 || tmax <= 0) return RG_ERR_ARG;
+  float* hs = work;                                               // B × H
+  float* Gh = hs + (int64_t)B * H;                                // B × 3H
+  int32_t* nact = reinterpret_cast<int32_t*>(Gh + (int64_t)B * 3 * H);  // tmax + 1
+  hipLaunchKernelGGL(k_gru_counts, dim3((tmax + 256) / 256), dim3(256), 0, stream, lsort, B, tmax, nact);
+  if (hipMemsetAsync(hs, 0, sizeof(float) * (size_t)B * H, stream) != hipSuccess) return RG_ERR_LAUNCH;
+  const int thr = H < 256 ? H : 256;
+  for (int t = 0; t < tmax; ++t) {
+    int rc = rg_gemm_f32(hs, H, 1, Whh, 1, H, Gh, 3 * H, bhh, B, nact + t, 3 * H, H, nullptr, 1, stream);
+    if (rc != RG_OK) return rc;
+    hipLaunchKernelGGL(k_gru_step_fwd, dim3(B), dim3(thr), 0, stream, t, Gi, Gh, nact, offs, H, hs, saved, plane);
+  }
+  hipLaunchKernelGGL(k_gru_rows_out, dim3(B), dim3(thr), 0, stream, hs, perm, B, H, hout, ldh, hoff);
+  RG_LAUNCH_CHECK();
+  return RG_OK;
+}
+
+extern "C" int rg_gru_bwd_steps(const float* saved, int64_t plane, const float* Whh, const int32_t* perm,
+                                const int32_t* lsort, const int32_t* offs, int B, int H, int tmax,
+                                const float* dhout, int lddh, int dhoff, float* dGi, float* dGh, float* work,
+                                hipStream_t stream) {
+  if (B <= 0 || H <= 0 || H % 4 || tmax <= 0) return RG_ERR_ARG;
+  float* dh_dir = work;                                            // B × H
+  float* dh_mat = dh_dir + (int64_t)B * H;                         // B × H
+  float* dGs = dh_mat + (int64_t)B * H;                            // B × 3H
+  int32_t* nact = reinterpret_cast<int32_t*>(dGs + (int64_t)B * 3 * H);  // tmax + 1
+  hipLaunchKernelGGL(k_gru_counts, dim3((tmax + 256) / 256), dim3(256), 0, stream, lsort, B, tmax, nact);
+  const int thr = H < 256 ? H : 256;
+  for (int t = tmax - 1; t >= 0; --t) {
+    hipLaunchKernelGGL(k_gru_step_bwd, dim3(B), dim3(thr), 0, stream, t, saved, plane, nact, offs, perm, H, dhout,
+                       lddh, dhoff, dh_dir, dh_mat, dGi, dGh, dGs);
+    if (t > 0) {  // recurrent term for step t−1: dGs · W_hh over the active rows
+      int rc = rg_gemm_f32(dGs, 3 * H, 1, Whh, H, 1, dh_mat, H, nullptr, B, nact + t, H, 3 * H, nullptr, 1, stream);
+      if (rc != RG_OK) return rc;
+    }
+  }
+  RG_LAUNCH_CHECK();
+  return RG_OK;
+}

@@ -58,6 +58,8 @@ SIGNATURES = {
     "rg_topk": [P, I64, P, I, I, I, P, P, P, P],
     "rg_hits_ndcg": [P, I, P, I, P, I, P, P],
     "rg_mask_scale": [P, P, F, I64, P, P],
+    "rg_gru_fwd_steps": [P, P, P, P, P, P, I, I, I, P, I, I, P, I64, P, P],
+    "rg_gru_bwd_steps": [P, I64, P, P, P, P, I, I, I, P, I, I, P, P, P, P],
     "rg_sample_uniform": [U64, U64, I, I64, P, P],
     "rg_sampled_fwd": [P, P, P, P, I, I, I, P, I64, P, P, P, P, P],
     "rg_sampled_lse": [P, P, P, P, I, I64, I, P, P, I, F, P, P, P, P, P, P, P],

@@ -112,6 +112,9 @@ def init_linear(in_f, out_f):
     return w, b
 
 
+_WIDTHS = (16, 32, 64, 128, 256)
+
+
 def _round_up(x, m):
     return (x + m - 1) // m * m
 
@@ -133,6 +136,8 @@ class _TrunkWS:
         self.Gi = [z(TM, 3 * H) for _ in range(ndir)]
         self.h = torch.zeros(B, ndir * H, device=device)
         self.plane = TM * H
+        self.step_work = z(5 * B * H + L + 8) if H > 128 else None
+        self.tmax = L
         self.saved = [z(5, TM, H) for _ in range(ndir)] if save else None
         if save:
             self.dGi = [z(TM, 3 * H) for _ in range(ndir)]
@@ -165,8 +170,11 @@ class Trunk:
         self.pad = pad_idx
         self.train_pad = train_pad_embed
         self.device = device
-        if E % 4 or H not in (16, 32, 64, 128):
-            raise RuntimeError(f"unsupported trunk shape E={E} H={H} (E % 4 == 0, H in 16/32/64/128)")
+        if E not in _WIDTHS or H not in _WIDTHS:
+            raise RuntimeError(f"unsupported trunk shape E={E} H={H} (E, H in {_WIDTHS})")
+        # H <= 128: persistent recurrence with W_hh in VGPRs; H = 256: time-stepped
+        # path (W_hh is 768 KB; csrc/gru.hip rg_gru_fwd_steps / rg_gru_bwd_steps)
+        self.stepped = H > 128
         self.emb = Param("embedding.weight", init_embedding(self.N1, E, pad_idx, train_pad_embed), device)
         gru = init_gru(E, H, layers, bidir)
         self.gru_params = [Param(f"{gru_attr}.{n}", t, device) for n, t in gru]
@@ -201,6 +209,8 @@ class Trunk:
             w.lens.copy_(lens, non_blocking=False)
         else:
             w.lens.copy_(lens)
+        if self.stepped:  # host bound of the timestep loop (no device sync)
+            w.tmax = max(1, min(L, int(lens.max()))) if self.packed and lens.device.type == "cpu" else L
         with region("pack"):
             call("rg_pack", w.lens.data_ptr(), B, L, 0 if self.packed else 1, w.perm.data_ptr(),
                  w.lsort.data_ptr(), w.offs.data_ptr(), st)
@@ -215,9 +225,15 @@ class Trunk:
                 call("rg_gemm_f32", w.X[d].data_ptr(), E, 1, w_ih.p.data_ptr(), 1, E, w.Gi[d].data_ptr(), 3 * H,
                      b_ih.p.data_ptr(), w.TM, w.ntok_ptr, 3 * H, E, None, 1, st)
             with region("gru_fwd"):
-                call("rg_gru_fwd", w.Gi[d].data_ptr(), w_hh.p.data_ptr(), b_hh.p.data_ptr(), w.perm.data_ptr(),
-                     w.lsort.data_ptr(), w.offs.data_ptr(), B, H, w.h.data_ptr(), self.ndir * H, d * H,
-                     w.saved[d].data_ptr() if save else None, w.plane, st)
+                if self.stepped:
+                    call("rg_gru_fwd_steps", w.Gi[d].data_ptr(), w_hh.p.data_ptr(), b_hh.p.data_ptr(),
+                         w.perm.data_ptr(), w.lsort.data_ptr(), w.offs.data_ptr(), B, H, w.tmax, w.h.data_ptr(),
+                         self.ndir * H, d * H, w.saved[d].data_ptr() if save else None, w.plane,
+                         w.step_work.data_ptr(), st)
+                else:
+                    call("rg_gru_fwd", w.Gi[d].data_ptr(), w_hh.p.data_ptr(), b_hh.p.data_ptr(),
+                         w.perm.data_ptr(), w.lsort.data_ptr(), w.offs.data_ptr(), B, H, w.h.data_ptr(),
+                         self.ndir * H, d * H, w.saved[d].data_ptr() if save else None, w.plane, st)
         return w.h
 
     def backward(self, dh, slot="main"):
@@ -229,9 +245,14 @@ class Trunk:
         for d in range(self.ndir):
             w_ih, w_hh, _, _ = self.dirs[d]
             with region("gru_bwd"):
-                call("rg_gru_bwd", w.saved[d].data_ptr(), w.plane, w_hh.p.data_ptr(), w.perm.data_ptr(),
-                     w.lsort.data_ptr(), w.offs.data_ptr(), B, H, dh.data_ptr(), self.ndir * H, d * H,
-                     w.dGi[d].data_ptr(), w.dGh[d].data_ptr(), st)
+                if self.stepped:
+                    call("rg_gru_bwd_steps", w.saved[d].data_ptr(), w.plane, w_hh.p.data_ptr(), w.perm.data_ptr(),
+                         w.lsort.data_ptr(), w.offs.data_ptr(), B, H, w.tmax, dh.data_ptr(), self.ndir * H,
+                         d * H, w.dGi[d].data_ptr(), w.dGh[d].data_ptr(), w.step_work.data_ptr(), st)
+                else:
+                    call("rg_gru_bwd", w.saved[d].data_ptr(), w.plane, w_hh.p.data_ptr(), w.perm.data_ptr(),
+                         w.lsort.data_ptr(), w.offs.data_ptr(), B, H, dh.data_ptr(), self.ndir * H, d * H,
+                         w.dGi[d].data_ptr(), w.dGh[d].data_ptr(), st)
         self._pending = (w, S)
 
     def step(self, adam6, tag):

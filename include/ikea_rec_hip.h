@@ -181,6 +181,17 @@ int rg_weighted_sum(const float* const* X, const float* w, int nh, int64_t n, fl
 /* SMORL reward matrix r (B, 3) f32 = stack([r_acc f64, r_div, r_nov]) (SMORL/smorl_gru.py:311-314, 3 rewards) */
 int rg_stack_rewards(const double* r_acc, const float* r_div, const float* r_nov, int B, float* r, rg_stream_t stream);
 
+/* Time-stepped GRU for hidden sizes whose W_hh cannot stay register-resident (H = 256, config C5;
+ * any H % 4 == 0): same contract as rg_gru_fwd / rg_gru_bwd plus tmax (the longest row, host value)
+ * and a workspace of 5*B*H + tmax + 1 floats; the timestep loop runs natively, one MFMA GEMM
+ * (rg_gemm_f32, device-side active-row count) + one fused gate kernel per step. */
+int rg_gru_fwd_steps(const float* Gi, const float* Whh, const float* bhh, const int32_t* perm, const int32_t* lsort,
+                     const int32_t* offs, int B, int H, int tmax, float* hout, int ldh, int hoff, float* saved,
+                     int64_t plane, float* work, rg_stream_t stream);
+int rg_gru_bwd_steps(const float* saved, int64_t plane, const float* Whh, const int32_t* perm, const int32_t* lsort,
+                     const int32_t* offs, int B, int H, int tmax, const float* dhout, int lddh, int dhoff,
+                     float* dGi, float* dGh, float* work, rg_stream_t stream);
+
 /* ---- sampled-softmax head (SURVEY §8 A7 sampled ext., config C3; build-defined,
  * no reference counterpart — replaces the full-softmax CrossEntropyLoss of
  * GRU4Rec/model.py:121,146 / BidirGRU4Rec/model.py:145,167 when the trainer is

@@ -108,8 +108,10 @@ def gru_ref(X_rows, lens, perm_order, Wih, Whh, bih, bhh, H):
     return hs
 
 
-@pytest.mark.parametrize("H", [16, 32, 64, 128])
-def test_gru_forward_backward(H):
+@pytest.mark.parametrize("H,stepped", [(16, False), (32, False), (64, False), (128, False), (64, True),
+                                       (256, True)])
+def test_gru_forward_backward(H, stepped):
+    """stepped: the time-stepped path (per-step MFMA GEMM + gate kernel) used for H = 256."""
     g = torch.Generator().manual_seed(3)
     B, L, E = 37, 7, H
     lens = torch.randint(1, L + 1, (B,), generator=g)
@@ -126,8 +128,14 @@ def test_gru_forward_backward(H):
     Gi = (packed.double() @ Wih.double().t() + bih.double()).float().to(dev)
     hout = torch.zeros(B, H, device=dev)
     saved = torch.zeros(5, T, H, device=dev)
-    C().call("rg_gru_fwd", Gi.data_ptr(), D(Whh).data_ptr(), D(bhh).data_ptr(), perm.data_ptr(),
-             ls.data_ptr(), offs.data_ptr(), B, H, hout.data_ptr(), H, 0, saved.data_ptr(), T * H, st())
+    work = torch.zeros(5 * B * H + L + 8, device=dev)
+    if stepped:
+        C().call("rg_gru_fwd_steps", Gi.data_ptr(), D(Whh).data_ptr(), D(bhh).data_ptr(), perm.data_ptr(),
+                 ls.data_ptr(), offs.data_ptr(), B, H, L, hout.data_ptr(), H, 0, saved.data_ptr(), T * H,
+                 work.data_ptr(), st())
+    else:
+        C().call("rg_gru_fwd", Gi.data_ptr(), D(Whh).data_ptr(), D(bhh).data_ptr(), perm.data_ptr(),
+                 ls.data_ptr(), offs.data_ptr(), B, H, hout.data_ptr(), H, 0, saved.data_ptr(), T * H, st())
     # autograd reference (float64)
     Xd = X.double().requires_grad_(True)
     P = [t.double().requires_grad_(True) for t in (Wih, Whh, bih, bhh)]
@@ -148,8 +156,13 @@ def test_gru_forward_backward(H):
     (href * dh.double()).sum().backward()
     dGi = torch.zeros(T, 3 * H, device=dev)
     dGh = torch.zeros(T, 3 * H, device=dev)
-    C().call("rg_gru_bwd", saved.data_ptr(), T * H, D(Whh).data_ptr(), perm.data_ptr(), ls.data_ptr(),
-             offs.data_ptr(), B, H, D(dh).data_ptr(), H, 0, dGi.data_ptr(), dGh.data_ptr(), st())
+    if stepped:
+        C().call("rg_gru_bwd_steps", saved.data_ptr(), T * H, D(Whh).data_ptr(), perm.data_ptr(), ls.data_ptr(),
+                 offs.data_ptr(), B, H, L, D(dh).data_ptr(), H, 0, dGi.data_ptr(), dGh.data_ptr(), work.data_ptr(),
+                 st())
+    else:
+        C().call("rg_gru_bwd", saved.data_ptr(), T * H, D(Whh).data_ptr(), perm.data_ptr(), ls.data_ptr(),
+                 offs.data_ptr(), B, H, D(dh).data_ptr(), H, 0, dGi.data_ptr(), dGh.data_ptr(), st())
     # dX = dGi · W_ih (packed order) vs autograd
     dX = (dGi.cpu().double() @ Wih.double())
     ref_dX = torch.cat([Xd.grad[r, :int(lens[r])] for r in order])

@@ -64,11 +64,12 @@ def test_smorl_matches_composed_reference_golden():
     compare_params(tr.SMORL_2.state_dict(), g, "final2.", cfg["learning_rate"])
 
 
-def test_sqn_matches_oracle_medium():
+@pytest.mark.parametrize("N,L,B,H", [(20000, 20, 512, 64), (6000, 10, 160, 256)])
+def test_sqn_matches_oracle_medium(N, L, B, H):
+    """H = 256 runs the time-stepped GRU (config C5's hidden size)."""
     from oracle.models import OracleSQN
     from recommenders.data_utils.synthetic import SessionStream
     from recommenders.models.SQN.sqn_gru import SQN_trainer
-    N, L, B, H = 20000, 20, 512, 64
     cfg = dict(hidden_dim=H, embedding_dim=H, train_pad_embed=True, use_packed_seq=True, learning_rate=0.005,
                item_num=N, state_size=L, action_dim=N, gamma=0.5, gru_layers=1)
     torch.set_num_threads(8)

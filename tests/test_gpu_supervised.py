@@ -77,7 +77,7 @@ def test_supervised_matches_reference_golden(name):
 
 
 @pytest.mark.parametrize("E,H,N,L,B", [(32, 32, 3000, 10, 256), (64, 64, 20000, 20, 512),
-                                       (128, 128, 50000, 50, 1024)])
+                                       (128, 128, 50000, 50, 1024), (256, 256, 8000, 12, 200)])
 def test_gru4rec_matches_oracle_medium(E, H, N, L, B):
     from oracle.models import OracleSupervised
     from recommenders.data_utils.synthetic import SessionStream
