@@ -10,6 +10,7 @@
 // g = 0.  28 B/param of HBM traffic (p, m, v read+write, tag / gradient rows
 // only where touched).
 #include "common.h"
+#include <hip/hip_fp16.h>
 
 static inline AdamArgs to_args(const float* a6) { return AdamArgs{a6[0], a6[1], a6[2], a6[3], a6[4], a6[5]}; }
 
@@ -97,6 +98,72 @@ extern "C" int rg_adam_rows(float* P, float* M, float* V, float* G, const int32_
   else
     hipLaunchKernelGGL(k_adam_rows1, dim3(blocks), dim3(256), 0, stream, P, M, V, G, tags, tag, rows, cols,
                        to_args(adam6));
+  RG_LAUNCH_CHECK();
+  return RG_OK;
+}
+
+// Row-sparse dense Adam that also refreshes an fp16 copy of the table
+// (config C5: the gather reads fp16 rows, Adam keeps fp32 master + moments).
+__global__ void k_adam_rows4_h(float* __restrict__ P, float* __restrict__ M, float* __restrict__ V,
+                               float* __restrict__ G, const int32_t* __restrict__ tags, int32_t tag, int64_t rows,
+                               int cols, AdamArgs a, __half* __restrict__ P16) {
+  const int c4n = cols >> 2;
+  const int64_t n4 = rows * c4n;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t row = i / c4n;
+    const bool hit = tags ? tags[row] == tag : true;
+    f4 p = reinterpret_cast<f4*>(P)[i];
+    f4 m = reinterpret_cast<f4*>(M)[i];
+    f4 v = reinterpret_cast<f4*>(V)[i];
+    f4 g = {0.f, 0.f, 0.f, 0.f};
+    if (hit) {
+      g = reinterpret_cast<f4*>(G)[i];
+      reinterpret_cast<f4*>(G)[i] = f4{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      float pq = p[q], mq = m[q], vq = v[q];
+      adam_elem(pq, mq, vq, g[q], a);
+      p[q] = pq;
+      m[q] = mq;
+      v[q] = vq;
+    }
+    reinterpret_cast<f4*>(P)[i] = p;
+    reinterpret_cast<f4*>(M)[i] = m;
+    reinterpret_cast<f4*>(V)[i] = v;
+    const __half2 lo = __floats2half2_rn(p[0], p[1]), hi = __floats2half2_rn(p[2], p[3]);
+    uint2 u;
+    u.x = *reinterpret_cast<const uint32_t*>(&lo);
+    u.y = *reinterpret_cast<const uint32_t*>(&hi);
+    reinterpret_cast<uint2*>(P16)[i] = u;
+  }
+}
+
+// tags == nullptr: every row takes its gradient (the dense all-reduced table
+// of the multi-GPU trunk); the gradient table is cleared either way.
+extern "C" int rg_adam_rows_h(float* P, float* M, float* V, float* G, const int32_t* tags, int32_t tag, int64_t rows,
+                              int cols, const float* adam6, uint16_t* P16, hipStream_t stream) {
+  if (rows <= 0 || cols <= 0 || cols % 4 || !P16) return RG_ERR_ARG;
+  const int64_t n = rows * (cols / 4);
+  int blocks = (int)((n + 255) / 256);
+  if (blocks > 32768) blocks = 32768;
+  hipLaunchKernelGGL(k_adam_rows4_h, dim3(blocks), dim3(256), 0, stream, P, M, V, G, tags, tag, rows, cols,
+                     to_args(adam6), reinterpret_cast<__half*>(P16));
+  RG_LAUNCH_CHECK();
+  return RG_OK;
+}
+
+// out = fp16(x), round to nearest even (initial copy / after load_state_dict)
+__global__ void k_f32_to_f16(const float* __restrict__ x, int64_t n, __half* __restrict__ out) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    out[i] = __float2half_rn(x[i]);
+}
+
+extern "C" int rg_f32_to_f16(const float* x, int64_t n, uint16_t* out, hipStream_t stream) {
+  if (n <= 0) return RG_ERR_ARG;
+  int blocks = (int)((n + 255) / 256);
+  if (blocks > 16384) blocks = 16384;
+  hipLaunchKernelGGL(k_f32_to_f16, dim3(blocks), dim3(256), 0, stream, x, n, reinterpret_cast<__half*>(out));
   RG_LAUNCH_CHECK();
   return RG_OK;
 }

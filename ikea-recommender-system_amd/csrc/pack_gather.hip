@@ -7,6 +7,7 @@
 // CSR offsets over the sorted rows, and the gather writes only the T valid
 // tokens as a packed (T, E) fp32 matrix plus their int32 item ids.
 #include "common.h"
+#include <hip/hip_fp16.h>
 
 // ---------------------------------------------------------------- pack -----
 // One workgroup of 1024 threads.  lens (int64, B) are clamped to [1, L] (the
@@ -105,11 +106,23 @@ extern "C" int rg_pack(const int64_t* lens, int B, int L, int unpacked, int32_t*
 // reverse=1 stores the row's tokens in reverse time order (the backward
 // direction of the bidirectional GRU reads its valid prefix back to front).
 // E is a multiple of 4: one float4 per lane, a 512-B row per 32 lanes (E=128).
+// 4 consecutive table values as fp32 (fp32 table: one 16-B load; fp16 table:
+// one 8-B load + exact widening)
+__device__ __forceinline__ f4 load4(const float* row, int c) { return reinterpret_cast<const f4*>(row)[c]; }
+__device__ __forceinline__ f4 load4(const __half* row, int c) {
+  const uint2 u = reinterpret_cast<const uint2*>(row)[c];
+  const __half2 a = *reinterpret_cast<const __half2*>(&u.x);
+  const __half2 b = *reinterpret_cast<const __half2*>(&u.y);
+  const float2 fa = __half22float2(a), fb = __half22float2(b);
+  return f4{fa.x, fa.y, fb.x, fb.y};
+}
+
+template <typename TE>
 __global__ __launch_bounds__(256) void k_gather(const int64_t* __restrict__ s, int L,
                                                 const int32_t* __restrict__ perm,
                                                 const int32_t* __restrict__ lsort,
                                                 const int32_t* __restrict__ offs,
-                                                const float* __restrict__ emb, int64_t n_rows, int E,
+                                                const TE* __restrict__ emb, int64_t n_rows, int E,
                                                 int reverse, int32_t* __restrict__ tok_id,
                                                 float* __restrict__ X, int32_t* __restrict__ err) {
   const int r = blockIdx.x;
@@ -125,7 +138,7 @@ __global__ __launch_bounds__(256) void k_gather(const int64_t* __restrict__ s, i
     int tok = base + t;
     f4 val = {0.f, 0.f, 0.f, 0.f};
     const bool ok = id >= 0 && id < n_rows;  // nn.Embedding raises on such ids
-    if (ok) val = reinterpret_cast<const f4*>(emb + id * E)[c];
+    if (ok) val = load4(emb + id * E, c);
     reinterpret_cast<f4*>(X + (int64_t)tok * E)[c] = val;
     if (c == 0) {
       tok_id[tok] = ok ? (int32_t)id : -1;
@@ -138,8 +151,20 @@ extern "C" int rg_gather(const int64_t* s, int B, int L, const int32_t* perm, co
                          const int32_t* offs, const float* emb, int64_t n_rows, int E, int reverse,
                          int32_t* tok_id, float* X, int32_t* err, hipStream_t stream) {
   if (B <= 0 || (E & 3)) return RG_ERR_ARG;
-  hipLaunchKernelGGL(k_gather, dim3(B), dim3(256), 0, stream, s, L, perm, lsort, offs, emb, n_rows, E, reverse,
-                     tok_id, X, err);
+  hipLaunchKernelGGL(k_gather<float>, dim3(B), dim3(256), 0, stream, s, L, perm, lsort, offs, emb, n_rows, E,
+                     reverse, tok_id, X, err);
+  RG_LAUNCH_CHECK();
+  return RG_OK;
+}
+
+// Same gather from an fp16 copy of the table (config C5: fp16 embedding
+// storage, fp32 master/Adam; rows widened exactly to fp32 on load).
+extern "C" int rg_gather_h(const int64_t* s, int B, int L, const int32_t* perm, const int32_t* lsort,
+                           const int32_t* offs, const uint16_t* emb16, int64_t n_rows, int E, int reverse,
+                           int32_t* tok_id, float* X, int32_t* err, hipStream_t stream) {
+  if (B <= 0 || (E & 3)) return RG_ERR_ARG;
+  hipLaunchKernelGGL(k_gather<__half>, dim3(B), dim3(256), 0, stream, s, L, perm, lsort, offs,
+                     reinterpret_cast<const __half*>(emb16), n_rows, E, reverse, tok_id, X, err);
   RG_LAUNCH_CHECK();
   return RG_OK;
 }

@@ -60,6 +60,9 @@ SIGNATURES = {
     "rg_mask_scale": [P, P, F, I64, P, P],
     "rg_gru_fwd_steps": [P, P, P, P, P, P, I, I, I, P, I, I, P, I64, P, P],
     "rg_gru_bwd_steps": [P, I64, P, P, P, P, I, I, I, P, I, I, P, P, P, P],
+    "rg_gather_h": [P, I, I, P, P, P, P, I64, I, I, P, P, P, P],
+    "rg_adam_rows_h": [P, P, P, P, P, I32, I64, I, P, P, P],
+    "rg_f32_to_f16": [P, I64, P, P],
     "rg_sample_uniform": [U64, U64, I, I64, P, P],
     "rg_sampled_fwd": [P, P, P, P, I, I, I, P, I64, P, P, P, P, P],
     "rg_sampled_lse": [P, P, P, P, I, I64, I, P, P, I, F, P, P, P, P, P, P, P],

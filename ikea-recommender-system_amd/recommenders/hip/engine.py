@@ -161,7 +161,8 @@ class Trunk:
     parity but are mathematically inert (zero gradient => Adam leaves them
     unchanged), so they are not computed."""
 
-    def __init__(self, gru_attr, item_num, E, H, layers, train_pad_embed, packed, pad_idx, bidir, device):
+    def __init__(self, gru_attr, item_num, E, H, layers, train_pad_embed, packed, pad_idx, bidir, device,
+                 fp16_embeddings=False):
         self.gru_attr = gru_attr
         self.N1 = item_num + 1
         self.E, self.H, self.layers, self.bidir = E, H, layers, bidir
@@ -184,6 +185,15 @@ class Trunk:
         self.tags = torch.zeros(self.N1, dtype=torch.int32, device=device)
         self.err = torch.zeros(1, dtype=torch.int32, device=device)  # out-of-range item ids seen
         self._ws = {}
+        # fp16 embedding storage (config C5): the gather reads this copy, Adam
+        # keeps the fp32 master and refreshes it in the same sweep
+        self.emb16 = torch.empty(self.N1, E, dtype=torch.float16, device=device) if fp16_embeddings else None
+        self.refresh_half()
+
+    def refresh_half(self):
+        """Re-derive the fp16 table from the fp32 master (init, load_state_dict)."""
+        if self.emb16 is not None:
+            call("rg_f32_to_f16", self.emb.p.data_ptr(), self.emb.numel(), self.emb16.data_ptr(), stream_ptr())
 
     # parameters in reference registration order
     def named_params(self):
@@ -218,9 +228,10 @@ class Trunk:
         for d in range(self.ndir):
             w_ih, w_hh, b_ih, b_hh = self.dirs[d]
             with region("gather"):
-                call("rg_gather", s.data_ptr(), B, L, w.perm.data_ptr(), w.lsort.data_ptr(), w.offs.data_ptr(),
-                     self.emb.p.data_ptr(), self.N1, E, d, w.tok_id[d].data_ptr(), w.X[d].data_ptr(),
-                     self.err.data_ptr(), st)
+                call("rg_gather_h" if self.emb16 is not None else "rg_gather", s.data_ptr(), B, L,
+                     w.perm.data_ptr(), w.lsort.data_ptr(), w.offs.data_ptr(),
+                     (self.emb16 if self.emb16 is not None else self.emb.p).data_ptr(), self.N1, E, d,
+                     w.tok_id[d].data_ptr(), w.X[d].data_ptr(), self.err.data_ptr(), st)
             with region("gemm_ih"):
                 call("rg_gemm_f32", w.X[d].data_ptr(), E, 1, w_ih.p.data_ptr(), 1, E, w.Gi[d].data_ptr(), 3 * H,
                      b_ih.p.data_ptr(), w.TM, w.ntok_ptr, 3 * H, E, None, 1, st)
@@ -266,8 +277,13 @@ class Trunk:
                 call("rg_adam_slabs", prm.p.data_ptr(), prm.m.data_ptr(), prm.v.data_ptr(), sl.data_ptr(), S,
                      prm.numel(), adam6, None, st)
         with region("adam_emb"):
-            call("rg_adam_rows", self.emb.p.data_ptr(), self.emb.m.data_ptr(), self.emb.v.data_ptr(),
-                 self.G_emb.data_ptr(), self.tags.data_ptr(), tag, self.N1, self.E, adam6, st)
+            if self.emb16 is not None:
+                call("rg_adam_rows_h", self.emb.p.data_ptr(), self.emb.m.data_ptr(), self.emb.v.data_ptr(),
+                     self.G_emb.data_ptr(), self.tags.data_ptr(), tag, self.N1, self.E, adam6,
+                     self.emb16.data_ptr(), st)
+            else:
+                call("rg_adam_rows", self.emb.p.data_ptr(), self.emb.m.data_ptr(), self.emb.v.data_ptr(),
+                     self.G_emb.data_ptr(), self.tags.data_ptr(), tag, self.N1, self.E, adam6, st)
         self._pending = None
 
     def _grads(self, w, S, tag):
@@ -321,8 +337,12 @@ class Trunk:
                      self.gflat.data_ptr() + 4 * off, n, adam6, 0, st)
                 off += n
         with region("adam_emb"):
-            call("rg_adam_dense", self.emb.p.data_ptr(), self.emb.m.data_ptr(), self.emb.v.data_ptr(),
-                 self.G_emb.data_ptr(), self.emb.numel(), adam6, 1, st)
+            if self.emb16 is not None:  # dense all-reduced gradient: every row, table cleared
+                call("rg_adam_rows_h", self.emb.p.data_ptr(), self.emb.m.data_ptr(), self.emb.v.data_ptr(),
+                     self.G_emb.data_ptr(), None, 0, self.N1, self.E, adam6, self.emb16.data_ptr(), st)
+            else:
+                call("rg_adam_dense", self.emb.p.data_ptr(), self.emb.m.data_ptr(), self.emb.v.data_ptr(),
+                     self.G_emb.data_ptr(), self.emb.numel(), adam6, 1, st)
         self._pending = None
 
 

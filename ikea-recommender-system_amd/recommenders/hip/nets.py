@@ -22,7 +22,7 @@ class HipNet:
 
     def __init__(self, *, trunk_attr, head_names, hidden_dim, embedding_dim, item_num, state_size, action_dim,
                  gru_layers, use_packed_seq, train_pad_embed, padding_idx, bidir, device, dropout=0.0,
-                 comm=None, n_negatives=None, neg_seed=0):
+                 comm=None, n_negatives=None, neg_seed=0, fp16_embeddings=False):
         self.hidden_dim = hidden_dim
         self.embedding_dim = embedding_dim
         self.item_num = int(item_num)
@@ -36,7 +36,7 @@ class HipNet:
         self.dropout_p = float(dropout)
         self.training = True
         self.trunk = Trunk(trunk_attr, self.item_num, embedding_dim, hidden_dim, gru_layers, train_pad_embed,
-                           use_packed_seq, self.padding_idx, bidir, self.device)
+                           use_packed_seq, self.padding_idx, bidir, self.device, fp16_embeddings=fp16_embeddings)
         self.hf = hidden_dim * (2 if bidir else 1)
         self.comm = comm
         shard = None
@@ -77,6 +77,7 @@ class HipNet:
             for k, v in sd.items():
                 if k in objs:
                     objs[k].p.copy_(torch.as_tensor(v).to(objs[k].p.device, torch.float32))
+        self.trunk.refresh_half()
         return self
 
     def parameters(self):

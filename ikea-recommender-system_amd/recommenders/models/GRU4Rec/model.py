@@ -23,12 +23,12 @@ class GRU4Rec(SupervisedNet):
 
     def __init__(self, hidden_size, embedding_dim, item_num, state_size, action_dim, gru_layers=1,
                  use_packed_seq=True, train_pad_embed=True, padding_idx=None, device="cuda", comm=None,
-                 n_negatives=None, neg_seed=0):
+                 n_negatives=None, neg_seed=0, fp16_embeddings=False):
         super().__init__(trunk_attr="gru", head_names=["output"], hidden_dim=hidden_size,
                          embedding_dim=embedding_dim, item_num=item_num, state_size=state_size,
                          action_dim=action_dim, gru_layers=gru_layers, use_packed_seq=use_packed_seq,
                          train_pad_embed=train_pad_embed, padding_idx=padding_idx, bidir=False, device=device,
-                         comm=comm, n_negatives=n_negatives, neg_seed=neg_seed)
+                         comm=comm, n_negatives=n_negatives, neg_seed=neg_seed, fp16_embeddings=fp16_embeddings)
 
 
 class _AdamFacade:
@@ -53,7 +53,8 @@ class _AdamFacade:
 class GRU4Rec_trainer:
     def __init__(self, hidden_dim, embedding_dim, gru_layers, train_pad_embed, use_packed_seq, learning_rate,
                  item_num, state_size, action_dim, device, padding_idx=None, torch_rand_seed=118,
-                 python_rand_seed=999, shard_items=False, process_group=None, n_negatives=None, neg_seed=0):
+                 python_rand_seed=999, shard_items=False, process_group=None, n_negatives=None, neg_seed=0,
+                 fp16_embeddings=False):
         torch.manual_seed(torch_rand_seed)
         random.seed(python_rand_seed)
         self.device = require_gpu(device)
@@ -64,11 +65,13 @@ class GRU4Rec_trainer:
         # n_negatives (build extension, off by default): sampled softmax over the
         # target and n_negatives shared uniform negatives instead of the full
         # softmax (config C3; recommenders/hip/engine.py:SampledSoftmaxHead).
+        # fp16_embeddings (build extension, off by default): the gather reads an
+        # fp16 copy of the item table, Adam keeps the fp32 master (config C5).
         self.gru_model = GRU4Rec(hidden_size=hidden_dim, embedding_dim=embedding_dim, item_num=item_num,
                                  state_size=state_size, action_dim=action_dim, gru_layers=gru_layers,
                                  use_packed_seq=use_packed_seq, train_pad_embed=train_pad_embed,
                                  padding_idx=padding_idx, device=self.device, comm=self.comm,
-                                 n_negatives=n_negatives, neg_seed=neg_seed)
+                                 n_negatives=n_negatives, neg_seed=neg_seed, fp16_embeddings=fp16_embeddings)
         self.learning_rate = learning_rate
         self.cross_entropy_loss = nn.CrossEntropyLoss(weight=None, reduction="mean")
         self.clock = AdamClock(learning_rate)

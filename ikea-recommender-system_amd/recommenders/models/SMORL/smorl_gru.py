@@ -26,7 +26,7 @@ from recommenders.models.GRU4Rec.model import _AdamFacade
 class SMORL_GRU_Net(QNet):
     def __init__(self, hidden_dim, embedding_dim, item_num, state_size, action_dim, q_weights, gamma, gru_layers=1,
                  random_embed_init=True, train_pad_embed=True, use_packed_seq=False, padding_idx=None,
-                 name="SMORL_GRU_Network", device="cuda", comm=None):
+                 name="SMORL_GRU_Network", device="cuda", comm=None, fp16_embeddings=False):
         if not random_embed_init:
             raise NotImplementedError("TODO: Pretrained embedings.")
         if use_packed_seq:
@@ -35,7 +35,7 @@ class SMORL_GRU_Net(QNet):
                          hidden_dim=hidden_dim, embedding_dim=embedding_dim, item_num=item_num,
                          state_size=state_size, action_dim=action_dim, gru_layers=gru_layers,
                          use_packed_seq=use_packed_seq, train_pad_embed=train_pad_embed, padding_idx=padding_idx,
-                         bidir=False, device=device, comm=comm)
+                         bidir=False, device=device, comm=comm, fp16_embeddings=fp16_embeddings)
         self.q_weights = q_weights
         self.gamma = gamma
         self.name = name
@@ -46,7 +46,7 @@ class SMORL_trainer:
                  item_num, state_size, action_dim, gamma, gru_layers, q_weights, alpha, div_embedding,
                  unpopular_actions_set, topk_div, device, input_tokenizer=None, output_tokenizer=None,
                  padding_idx=None, torch_rand_seed=118, python_rand_seed=999, name_1="SMORL_1", name_2="SMORL_2",
-                 topk_nov=1, nov_rew_sig=1, shard_items=False, process_group=None):
+                 topk_nov=1, nov_rew_sig=1, shard_items=False, process_group=None, fp16_embeddings=False):
         torch.manual_seed(torch_rand_seed)
         random.seed(python_rand_seed)
         self.device = require_gpu(device)
@@ -57,7 +57,8 @@ class SMORL_trainer:
                                         action_dim=action_dim, gru_layers=gru_layers, gamma=gamma,
                                         q_weights=q_weights, embedding_dim=embedding_dim,
                                         train_pad_embed=train_pad_embed, use_packed_seq=use_packed_seq,
-                                        padding_idx=padding_idx, name=name, device=self.device, comm=self.comm)
+                                        padding_idx=padding_idx, name=name, device=self.device, comm=self.comm,
+                                        fp16_embeddings=fp16_embeddings)
         self.SMORL_1 = mk(name_1)
         self.SMORL_2 = mk(name_2)
         self.gamma = gamma

@@ -23,7 +23,7 @@ from recommenders.models.GRU4Rec.model import _AdamFacade
 class SQN_Network(QNet):
     def __init__(self, hidden_dim, item_num, state_size, action_dim, gamma, gru_layers, embedding_dim=50,
                  random_embed_init=True, train_pad_embed=True, use_packed_seq=False, padding_idx=None,
-                 name="DQNetwork", device="cuda", comm=None):
+                 name="DQNetwork", device="cuda", comm=None, fp16_embeddings=False):
         if not random_embed_init:
             raise NotImplementedError("TODO: Pretrained embedings.")  # as the reference (:67-68)
         if use_packed_seq:
@@ -32,7 +32,7 @@ class SQN_Network(QNet):
                          embedding_dim=embedding_dim, item_num=item_num, state_size=state_size,
                          action_dim=action_dim, gru_layers=gru_layers, use_packed_seq=use_packed_seq,
                          train_pad_embed=train_pad_embed, padding_idx=padding_idx, bidir=False, device=device,
-                         comm=comm)
+                         comm=comm, fp16_embeddings=fp16_embeddings)
         self.gamma = gamma
         self.name = name
         self.random_embed_init = random_embed_init
@@ -41,7 +41,8 @@ class SQN_Network(QNet):
 class SQN_trainer:
     def __init__(self, hidden_dim, embedding_dim, train_pad_embed, use_packed_seq, learning_rate, item_num,
                  state_size, action_dim, gamma, gru_layers, device, padding_idx=None, torch_rand_seed=118,
-                 python_rand_seed=999, name_1="SQN_1", name_2="SQN_2", shard_items=False, process_group=None):
+                 python_rand_seed=999, name_1="SQN_1", name_2="SQN_2", shard_items=False, process_group=None,
+                 fp16_embeddings=False):
         torch.manual_seed(torch_rand_seed)
         random.seed(python_rand_seed)
         self.device = require_gpu(device)
@@ -52,7 +53,7 @@ class SQN_trainer:
                                       action_dim=action_dim, gamma=gamma, gru_layers=gru_layers,
                                       embedding_dim=embedding_dim, train_pad_embed=train_pad_embed,
                                       use_packed_seq=use_packed_seq, padding_idx=padding_idx, name=name,
-                                      device=self.device, comm=self.comm)
+                                      device=self.device, comm=self.comm, fp16_embeddings=fp16_embeddings)
         self.DQN_1 = mk(name_1)
         self.DQN_2 = mk(name_2)
         self.gamma = gamma

@@ -192,6 +192,16 @@ int rg_gru_bwd_steps(const float* saved, int64_t plane, const float* Whh, const 
                      const int32_t* offs, int B, int H, int tmax, const float* dhout, int lddh, int dhoff,
                      float* dGi, float* dGh, float* work, rg_stream_t stream);
 
+/* ---- fp16 embedding storage (config C5: the gather reads an fp16 copy of the table, Adam keeps the
+ * fp32 master and moments; fp16 = IEEE binary16 bits, round to nearest even) ---- */
+int rg_gather_h(const int64_t* s, int B, int L, const int32_t* perm, const int32_t* lsort, const int32_t* offs,
+                const uint16_t* emb16, int64_t n_rows, int E, int reverse, int32_t* tok_id, float* X, int32_t* err,
+                rg_stream_t stream);
+/* rg_adam_rows (cols % 4 == 0) that also writes P16 = fp16(P); tags == NULL: every row has a gradient */
+int rg_adam_rows_h(float* P, float* M, float* V, float* G, const int32_t* tags, int32_t tag, int64_t rows, int cols,
+                   const float* adam6, uint16_t* P16, rg_stream_t stream);
+int rg_f32_to_f16(const float* x, int64_t n, uint16_t* out, rg_stream_t stream);
+
 /* ---- sampled-softmax head (SURVEY §8 A7 sampled ext., config C3; build-defined,
  * no reference counterpart — replaces the full-softmax CrossEntropyLoss of
  * GRU4Rec/model.py:121,146 / BidirGRU4Rec/model.py:145,167 when the trainer is

@@ -39,6 +39,20 @@ HEADS = {
 }
 
 
+class _Fp16Storage(torch.autograd.Function):
+    """Forward: the table as stored in fp16 (round to nearest even), widened
+    back to fp32.  Backward: the fp32 gradient unchanged (it lands on the fp32
+    master weights).  Build-defined C5 option; no reference counterpart."""
+
+    @staticmethod
+    def forward(ctx, w):
+        return w.half().float()
+
+    @staticmethod
+    def backward(ctx, g):
+        return g
+
+
 class Net(nn.Module):
     """Embedding -> GRU -> layer-0 final hidden -> linear heads.
 
@@ -50,8 +64,9 @@ class Net(nn.Module):
 
     def __init__(self, kind, item_num, action_dim, embedding_dim, hidden_dim,
                  gru_layers=1, train_pad_embed=True, use_packed_seq=True,
-                 padding_idx=None, dropout=0.0):
+                 padding_idx=None, dropout=0.0, emb_fp16=False):
         super().__init__()
+        self.emb_fp16 = emb_fp16
         self.kind = kind
         self.item_num = int(item_num)
         self.action_dim = action_dim
@@ -80,7 +95,11 @@ class Net(nn.Module):
 
     def hidden(self, s, lengths):
         """Final layer-0 hidden (``GRU4Rec/model.py:62-77``; Bidir cat ``:86-93``)."""
-        emb = self.embedding(s)
+        if self.emb_fp16:
+            emb = F.embedding(s, _Fp16Storage.apply(self.embedding.weight),
+                              padding_idx=self.embedding.padding_idx)
+        else:
+            emb = self.embedding(s)
         if self.use_packed_seq:
             emb = nn.utils.rnn.pack_padded_sequence(emb, lengths=lengths, batch_first=True,
                                                     enforce_sorted=False)
@@ -143,11 +162,11 @@ class OracleSupervised:
     def __init__(self, kind, hidden_dim, embedding_dim, gru_layers, train_pad_embed,
                  use_packed_seq, learning_rate, item_num, state_size, action_dim,
                  dropout=0.0, padding_idx=None, torch_rand_seed=118, python_rand_seed=999,
-                 n_negatives=None, neg_seed=0):
+                 n_negatives=None, neg_seed=0, fp16_embeddings=False):
         torch.manual_seed(torch_rand_seed)
         random.seed(python_rand_seed)
         self.net = Net(kind, item_num, action_dim, embedding_dim, hidden_dim, gru_layers,
-                       train_pad_embed, use_packed_seq, padding_idx, dropout)
+                       train_pad_embed, use_packed_seq, padding_idx, dropout, emb_fp16=fp16_embeddings)
         self.opt = make_adam(self.net, learning_rate)
         self.n_negatives, self.neg_seed, self.draws = n_negatives, neg_seed, 0
 
@@ -172,11 +191,11 @@ class OracleSQN:
 
     def __init__(self, hidden_dim, embedding_dim, train_pad_embed, use_packed_seq,
                  learning_rate, item_num, state_size, action_dim, gamma, gru_layers,
-                 padding_idx=None, torch_rand_seed=118, python_rand_seed=999):
+                 padding_idx=None, torch_rand_seed=118, python_rand_seed=999, fp16_embeddings=False):
         torch.manual_seed(torch_rand_seed)
         random.seed(python_rand_seed)
         mk = lambda: Net("sqn", item_num, action_dim, embedding_dim, hidden_dim, gru_layers,
-                         train_pad_embed, use_packed_seq, padding_idx)
+                         train_pad_embed, use_packed_seq, padding_idx, emb_fp16=fp16_embeddings)
         self.nets = [mk(), mk()]
         self.opts = [make_adam(n, learning_rate) for n in self.nets]
         self.gamma = gamma

@@ -98,3 +98,54 @@ def test_gru4rec_matches_oracle_medium(E, H, N, L, B):
         d = (v.cpu() - sd_o[k]).abs()
         assert float(d.max()) <= 2 * cfg["learning_rate"] + 1e-5, k
         assert float((d > 1e-4).float().mean()) < 1e-3, (k, float((d > 1e-4).float().mean()))
+
+
+@pytest.mark.parametrize("kind,E,H,N,L,B", [("gru4rec", 64, 64, 20000, 20, 512), ("sqn", 256, 256, 6000, 10, 160)])
+def test_fp16_embedding_storage_matches_oracle(kind, E, H, N, L, B):
+    """fp16 item table for the gather, fp32 master + Adam (config C5), against
+    the oracle's restatement of the same storage (oracle/models.py _Fp16Storage)."""
+    import random
+    from recommenders.data_utils.synthetic import SessionStream
+    torch.set_num_threads(8)
+    if kind == "gru4rec":
+        from oracle.models import OracleSupervised
+        from recommenders.models.GRU4Rec.model import GRU4Rec_trainer
+        cfg = dict(hidden_dim=H, embedding_dim=E, gru_layers=1, train_pad_embed=True, use_packed_seq=True,
+                   learning_rate=0.005, item_num=N, state_size=L, action_dim=N, fp16_embeddings=True)
+        orc = OracleSupervised(kind="gru4rec", **cfg)
+        tr = GRU4Rec_trainer(device="cuda", **cfg)
+        nets = [(tr.gru_model, orc.net)]
+    else:
+        from oracle.models import OracleSQN
+        from recommenders.models.SQN.sqn_gru import SQN_trainer
+        cfg = dict(hidden_dim=H, embedding_dim=E, train_pad_embed=True, use_packed_seq=True, learning_rate=0.005,
+                   item_num=N, state_size=L, action_dim=N, gamma=0.5, gru_layers=1, fp16_embeddings=True)
+        orc = OracleSQN(**cfg)
+        rs_o = random.getstate()
+        tr = SQN_trainer(device="cuda", **cfg)
+        rs_t = random.getstate()
+        nets = [(tr.DQN_1, orc.nets[0]), (tr.DQN_2, orc.nets[1])]
+    st = SessionStream(N, L, B * 3, seed=13)
+    for i in range(3):
+        b = st.batch(i, B)
+        if kind == "gru4rec":
+            lo, lg = orc.step(b[0], b[1], b[4]), tr.train_step(b[0], b[1], b[4])
+            assert abs(lo - lg) < 1e-4, (i, lo, lg)
+        else:
+            random.setstate(rs_o)
+            so, qo = orc.step(*b)
+            rs_o = random.getstate()
+            random.setstate(rs_t)
+            sg, qg = tr.train_step(*b)
+            rs_t = random.getstate()
+            assert abs(so - sg) < 1e-4 and abs(qo - qg) < 1e-5, (i, so, sg, qo, qg)
+    lr = cfg["learning_rate"]
+    for mine, ref in nets:
+        sd_o = ref.state_dict()
+        for k, v in mine.state_dict().items():
+            d = (v.cpu() - sd_o[k]).abs()
+            assert float(d.max()) <= 2 * lr + 1e-5, k
+            assert float((d > 1e-4).float().mean()) < 1e-3, k
+        # the fp16 table is exactly the rounded fp32 master
+        assert torch.equal(mine.trunk.emb16.cpu(), mine.trunk.emb.p.cpu().half())
+
