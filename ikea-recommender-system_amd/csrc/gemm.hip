@@ -168,53 +168,84 @@ __global__ __launch_bounds__(256) void k_wgrad(const float* __restrict__ G, int 
   constexpr int TB = 32;
   constexpr int NX4 = TB * N / 4;
   constexpr int NXL = (NX4 + 255) / 256;
-  __shared__ __attribute__((aligned(16))) float gs[TB][128 + 4];
-  __shared__ __attribute__((aligned(16))) float xs[TB][NP + 4];
+  __shared__ __attribute__((aligned(16))) float gs[2][TB][128 + 4];
+  __shared__ __attribute__((aligned(16))) float xs[2][TB][NP + 4];
   __shared__ float csum[8][128];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, half = lane >> 5, l32 = lane & 31;
   const int T = *Tptr;
+  // split the tokens actually present (T is only known on the device) evenly
+  if (tchunk <= 0) tchunk = ((T + (int)gridDim.y - 1) / (int)gridDim.y + 31) / 32 * 32;
   const int m0 = blockIdx.x * 128;
   const int t0 = blockIdx.y * tchunk;
   const int t1 = min(T, t0 + tchunk);
   const int c4 = tid & 31;  // this thread's 4 G columns
   const int tr = tid >> 5;  // rows tr + 8i
+  const int m = m0 + 4 * c4;
+  const bool mv = m < M;
+  const int mc = mv ? m : 0;
   f4 cs = {0.f, 0.f, 0.f, 0.f};
   f16v acc[NCT];
 #pragma unroll
   for (int ct = 0; ct < NCT; ++ct) acc[ct] = f16v{};
-  for (int tb = t0; tb < t1; tb += TB) {
+  // register prefetch of one 32-token chunk; addresses clamped so every load
+  // is issued unconditionally and stays in flight across the MFMA phase
+  f4 gp[4], xp[NXL];
+  float gk[4], xk[NXL];
+  const int tlast = t1 > 0 ? t1 - 1 : 0;
+  auto load = [&](int tb) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int t = tb + tr + 8 * i;
-      const int m = m0 + 4 * c4;
-      f4 v = {0.f, 0.f, 0.f, 0.f};
-      if (t < t1 && m < M) v = *reinterpret_cast<const f4*>(G + (int64_t)t * M + m);
+      gp[i] = *reinterpret_cast<const f4*>(G + (int64_t)(t < t1 ? t : tlast) * M + mc);
+      gk[i] = (t < t1 && mv) ? 1.f : 0.f;
+    }
+#pragma unroll
+    for (int i = 0; i < NXL; ++i) {
+      const int e = tid + 256 * i;
+      const int rr = (e < NX4 ? e : 0) / (N / 4), cc = (e < NX4 ? e : 0) % (N / 4);
+      const int t = tb + rr;
+      xp[i] = *reinterpret_cast<const f4*>(X + (int64_t)(t < t1 ? t : tlast) * N + 4 * cc);
+      xk[i] = (e < NX4 && t < t1) ? 1.f : 0.f;
+    }
+  };
+  auto commit = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const f4 v = gp[i] * gk[i];
       cs += v;
-      *reinterpret_cast<f4*>(&gs[tr + 8 * i][4 * c4]) = v;
+      *reinterpret_cast<f4*>(&gs[buf][tr + 8 * i][4 * c4]) = v;
     }
 #pragma unroll
     for (int i = 0; i < NXL; ++i) {
       const int e = tid + 256 * i;
       if (e < NX4) {
         const int rr = e / (N / 4), cc = e % (N / 4);
-        const int t = tb + rr;
-        f4 v = {0.f, 0.f, 0.f, 0.f};
-        if (t < t1) v = *reinterpret_cast<const f4*>(X + (int64_t)t * N + 4 * cc);
-        *reinterpret_cast<f4*>(&xs[rr][4 * cc]) = v;
+        *reinterpret_cast<f4*>(&xs[buf][rr][4 * cc]) = xp[i] * xk[i];
       }
     }
-    __syncthreads();
+  };
+  int cur = 0;
+  if (t0 < t1) {
+    load(t0);
+    commit(0);
+  }
+  __syncthreads();
+  for (int tb = t0; tb < t1; tb += TB) {
+    const bool more = tb + TB < t1;
+    if (more) load(tb + TB);
 #pragma unroll
     for (int s = 0; s < TB / 2; ++s) {
       const int t = half * (TB / 2) + s;
-      const float a = gs[t][32 * w + l32];
+      const float a = gs[cur][t][32 * w + l32];
 #pragma unroll
       for (int ct = 0; ct < NCT; ++ct) {
-        const float b = (N >= 32 || l32 < N) ? xs[t][ct * 32 + l32] : 0.f;
+        const float b = (N >= 32 || l32 < N) ? xs[cur][t][ct * 32 + l32] : 0.f;
         acc[ct] = mfma32(a, b, acc[ct]);
       }
     }
+    if (more) commit(cur ^ 1);
     __syncthreads();
+    cur ^= 1;
   }
   float* dw = dw_slabs + (int64_t)blockIdx.y * M * N;
 #pragma unroll
@@ -223,26 +254,25 @@ __global__ __launch_bounds__(256) void k_wgrad(const float* __restrict__ G, int 
     if (n >= N) continue;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      const int m = m0 + 32 * w + acc32_row(r, half);
-      if (m < M) dw[(int64_t)m * N + n] = acc[ct][r];
+      const int mm = m0 + 32 * w + acc32_row(r, half);
+      if (mm < M) dw[(int64_t)mm * N + n] = acc[ct][r];
     }
   }
   *reinterpret_cast<f4*>(&csum[tr][4 * c4]) = cs;
   __syncthreads();
   if (tid < 128) {
-    float s = 0.f;
+    float sm = 0.f;
 #pragma unroll
-    for (int q = 0; q < 8; ++q) s += csum[q][tid];
-    const int m = m0 + tid;
-    if (m < M) db_slabs[(int64_t)blockIdx.y * M + m] = s;
+    for (int q = 0; q < 8; ++q) sm += csum[q][tid];
+    const int mm = m0 + tid;
+    if (mm < M) db_slabs[(int64_t)blockIdx.y * M + mm] = sm;
   }
 }
 
 extern "C" int rg_wgrad(const float* G, int M, const float* X, int N, int T_max, const int32_t* Tptr, int splits,
                         float* dw_slabs, float* db_slabs, hipStream_t stream) {
   if (M <= 0 || M % 4 || T_max <= 0 || splits <= 0 || !Tptr) return RG_ERR_ARG;
-  int tchunk = (T_max + splits - 1) / splits;
-  tchunk = (tchunk + 31) / 32 * 32;
+  const int tchunk = 0;  // derived from the device-side token count
   dim3 grid((M + 127) / 128, splits);
 #define WG(NV) hipLaunchKernelGGL(k_wgrad<NV>, grid, dim3(256), 0, stream, G, M, X, Tptr, tchunk, dw_slabs, db_slabs)
   switch (N) {

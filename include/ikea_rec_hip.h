@@ -65,7 +65,7 @@ int rg_colsum(const float* X, int ncol, int rows, const int32_t* rows_ptr, int s
 /* weight + bias gradient over packed tokens in one pass (nn.GRU backward's
  * dW_ih = dGi^T X, db_ih = sum dGi; dW_hh = dGh^T H_prev, db_hh = sum dGh):
  * dw_slabs (splits x M x N), db_slabs (splits x M); T read from *Tptr;
- * N in {16, 32, 64, 128}, M % 4 == 0. */
+ * N in {16, 32, 64, 128, 256}, M % 4 == 0; the splits divide the device-side token count evenly. */
 int rg_wgrad(const float* G, int M, const float* X, int N, int T_max, const int32_t* Tptr, int splits,
              float* dw_slabs, float* db_slabs, rg_stream_t stream);
 
