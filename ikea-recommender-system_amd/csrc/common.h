@@ -9,6 +9,8 @@ typedef float f4 __attribute__((ext_vector_type(4)));
 typedef float f16v __attribute__((ext_vector_type(16)));
 
 #define RG_OK 0
+// items per online-softmax (max, Σexp, argmax) partial of the head forward
+#define RG_PBLK 32
 #define RG_ERR_ARG (-1)
 #define RG_ERR_LAUNCH (-2)
 #define RG_ERR_SHAPE (-3)

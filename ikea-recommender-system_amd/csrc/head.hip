@@ -8,11 +8,14 @@
 // rows (128-B segments per half-wave) — the MFMA D layout writes columns, and
 // both backward GEMMs stream Zᵀ rows.
 //
-//  k_head_fwd   : Zᵀ tile = W_tile · h_chunkᵀ on v_mfma_f32_32x32x2_f32 with the
-//                 128×HF W tile resident in VGPRs (64 regs/lane at HF=128) and
-//                 32-row h chunks double-buffered through LDS; epilogue adds the
-//                 bias, stores Zᵀ and emits per-(item-block, row) online
-//                 (max, Σexp, argmax) partials — the softmax never re-reads Zᵀ.
+//  k_head_fwd_w1: Zᵀ tile = W_tile · h_chunkᵀ on v_mfma_f32_32x32x2_f32, one
+//                 wave per 32 items with the W rows resident in VGPRs (64
+//                 regs/lane at HF=128) and h streamed from L2 into registers;
+//                 the epilogue (bias, Zᵀ stores, per-(32-item block, row)
+//                 online (max, Σexp, argmax) partials) of each 32-row chunk is
+//                 interleaved with the next chunk's MFMAs — the softmax never
+//                 re-reads Zᵀ.  k_head_fwd: the same with h staged through LDS
+//                 for 4 waves, used for the remainder items and ragged B.
 //  k_lse_*      : merge partials -> lse[b], argmax[b], loss_b = lse_b − Z[a_b,b].
 //  k_head_dh    : dh = dZ·W, dZ = (exp(Z−lse) − onehot)·g recomputed on load;
 //                 split over the item axis into deterministic slabs.
@@ -46,17 +49,14 @@ __global__ __launch_bounds__(256) void k_head_fwd(const float* __restrict__ h, c
                                                   const float* __restrict__ bias, int B, int A,
                                                   float* __restrict__ ZT, int64_t ldz, float* __restrict__ pmax,
                                                   float* __restrict__ psum, int32_t* __restrict__ parg,
-                                                  int want_sum) {
+                                                  int want_sum, int j0) {
   constexpr int KH = HF / 2;
   constexpr int LDB = HF + 4;
   constexpr int NV = 8 * HF;                 // float4 per 32-row chunk
   constexpr int NL = (NV + 255) / 256;       // float4 per thread per chunk
   __shared__ __attribute__((aligned(16))) float hbuf[2][32][LDB];
-  __shared__ float sm[2][4][32];
-  __shared__ float ss[2][4][32];
-  __shared__ int sa[2][4][32];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, half = lane >> 5, l32 = lane & 31;
-  const int jw = blockIdx.x * 128 + 32 * w;
+  const int jw = j0 + blockIdx.x * 128 + 32 * w;  // this wave's 32 items = one partial block
 
   float Wreg[KH];
   {
@@ -188,23 +188,150 @@ __global__ __launch_bounds__(256) void k_head_fwd(const float* __restrict__ h, c
       int a2 = __shfl_xor(arg, 32);
       stat_merge(m, sum, arg, m2, s2, a2);
     }
-    if (half == 0) {
-      sm[cur][w][l32] = m;
-      ss[cur][w][l32] = sum;
-      sa[cur][w][l32] = arg;
+    if (half == 0 && bv && jw < A) {  // one partial per 32-item block (RG_PBLK)
+      const int64_t o = (int64_t)(jw / RG_PBLK) * B + b;
+      pmax[o] = m;
+      if (psum) psum[o] = sum;
+      parg[o] = arg;
     }
     __syncthreads();
-    if (w == 0 && half == 0 && bv) {
-      float M = sm[cur][0][l32], S = ss[cur][0][l32];
-      int AR = sa[cur][0][l32];
-#pragma unroll
-      for (int q = 1; q < 4; ++q) stat_merge(M, S, AR, sm[cur][q][l32], ss[cur][q][l32], sa[cur][q][l32]);
-      const int64_t o = (int64_t)blockIdx.x * B + b;
-      pmax[o] = M;
-      if (psum) psum[o] = S;
-      parg[o] = AR;
-    }
     cur ^= 1;
+  }
+}
+
+// Interior fast path: one wave per 32 items (every item exists, B % 32 == 0).
+// W rows stay in VGPRs; h is streamed straight from L2 into registers through
+// a 4-group prefetch ring (no LDS, no barriers — nothing couples the waves),
+// and the epilogue of chunk c−1 (bias, Zᵀ stores, max/argmax, Σexp, the
+// per-block partial) is interleaved in program order with the MFMAs of chunk
+// c, two accumulator sets alternating.  Same arithmetic and tie rules as
+// k_head_fwd.
+template <int HF, bool SZ, bool WS>
+__global__ __launch_bounds__(64) void k_head_fwd_w1(const float* __restrict__ h, const float* __restrict__ W,
+                                                    const float* __restrict__ bias, int B,
+                                                    float* __restrict__ ZT, int64_t ldz,
+                                                    float* __restrict__ pmax, float* __restrict__ psum,
+                                                    int32_t* __restrict__ parg) {
+  constexpr int KH = HF / 2;
+  constexpr int NG = KH / 4;                   // 4-MFMA groups per 32-row chunk
+  constexpr int PD = NG < 4 ? NG : 4;          // h prefetch distance in groups
+  constexpr int PER = NG >= 32 ? 1 : 32 / NG;  // epilogue values per group (two passes over 16)
+  constexpr float L2E = 1.4426950408889634f;
+  const int lane = threadIdx.x, half = lane >> 5, l32 = lane & 31;
+  const int jw = blockIdx.x * 32;
+  float Wreg[KH];
+  {
+    const float* src = W + (int64_t)(jw + l32) * HF + half * KH;
+#pragma unroll
+    for (int s = 0; s < KH; s += 4) {
+      const f4 v = *reinterpret_cast<const f4*>(src + s);
+      Wreg[s] = v.x;
+      Wreg[s + 1] = v.y;
+      Wreg[s + 2] = v.z;
+      Wreg[s + 3] = v.w;
+    }
+  }
+  float bj[16];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) bj[r] = bias[jw + acc32_row(r, half)];
+  // Zᵀ stores through a buffer descriptor over the 32 item rows (wave-uniform
+  // base, scalar row offsets): one 32-bit lane offset serves all 16 rows
+  const uint64_t zb = SZ ? (uint64_t)(ZT + (int64_t)jw * ldz) : 0;
+  const uint32_t zlo = __builtin_amdgcn_readfirstlane((uint32_t)zb);
+  const uint32_t zhi = __builtin_amdgcn_readfirstlane((uint32_t)(zb >> 32));
+  const uint32_t znb = __builtin_amdgcn_readfirstlane(SZ ? (uint32_t)(32 * ldz * 4) : 0u);
+  const __amdgpu_buffer_rsrc_t zrs =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)zhi << 32) | zlo), 0, znb, 0x00020000);
+  const int zlane = (4 * half * (int)ldz + l32) * 4;  // bytes
+  const int zrow4 = __builtin_amdgcn_readfirstlane((int)ldz * 4);
+  const int nch = B / 32;
+  const float* hl = h + (int64_t)l32 * HF + half * KH;  // + chunk·32·HF + 4·group
+  float* pm = pmax + (int64_t)blockIdx.x * B + l32;
+  float* ps = WS ? psum + (int64_t)blockIdx.x * B + l32 : nullptr;
+  int32_t* pa = parg + (int64_t)blockIdx.x * B + l32;
+  f4 ring[PD];
+#pragma unroll
+  for (int p = 0; p < PD; ++p) ring[p] = *reinterpret_cast<const f4*>(hl + 4 * p);
+  float em = NEG_INF, es = 0.f;
+  int ea = INT32_MAX;
+  auto epi_slice = [&](f16v& acc, int cc, int g) __attribute__((always_inline)) {
+    if (g < NG / 2) {
+#pragma unroll
+      for (int q = 0; q < PER; ++q) {
+        const int r = g * PER + q;
+        if (r < 16) {
+          const float z = acc[r] + bj[r];
+          acc[r] = z;
+          if (SZ)
+            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(z), zrs, zlane,
+                                                  ((r & 3) + 8 * (r >> 2)) * zrow4 + cc * 128, 0);
+          const bool gt = z > em;
+          em = gt ? z : em;
+          ea = gt ? jw + acc32_row(r, half) : ea;
+        }
+      }
+    } else if (WS) {
+      const float m2 = em * L2E;
+#pragma unroll
+      for (int q = 0; q < PER; ++q) {
+        const int r = (g - NG / 2) * PER + q;
+        if (r < 16) es += __builtin_amdgcn_exp2f(fmaf(acc[r], L2E, -m2));
+      }
+    }
+  };
+  auto epi_finish = [&](int cc) __attribute__((always_inline)) {
+    stat_merge(em, es, ea, __shfl_xor(em, 32), __shfl_xor(es, 32), __shfl_xor(ea, 32));
+    if (half == 0) {
+      pm[cc * 32] = em;
+      if (WS) ps[cc * 32] = es;
+      pa[cc * 32] = ea;
+    }
+    em = NEG_INF;
+    es = 0.f;
+    ea = INT32_MAX;
+  };
+  // MFMAs of chunk c into acc; group g consumes ring[g % PD] and refills it
+  // with group g + PD (possibly of chunk c + 1; clamped past the end)
+  auto chunk = [&](int c, f16v& acc, f16v& prev, int cprev, bool epi) __attribute__((always_inline)) {
+#pragma unroll
+    for (int g = 0; g < NG; ++g) {
+      const f4 hv = ring[g % PD];
+      {
+        const int gg = g + PD;
+        const int cn = gg < NG ? c : (c + 1 < nch ? c + 1 : c);
+        const int gl = gg < NG ? gg : gg - NG;
+        ring[g % PD] = *reinterpret_cast<const f4*>(hl + (int64_t)cn * 32 * HF + 4 * gl);
+      }
+      acc = mfma32(Wreg[4 * g], hv.x, acc);
+      if (epi) epi_slice(prev, cprev, g);
+      acc = mfma32(Wreg[4 * g + 1], hv.y, acc);
+      acc = mfma32(Wreg[4 * g + 2], hv.z, acc);
+      acc = mfma32(Wreg[4 * g + 3], hv.w, acc);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+  f16v accA = {}, accB = {};
+  chunk(0, accA, accB, 0, false);
+  int c = 1;
+  for (; c + 1 < nch; c += 2) {
+    accB = f16v{};
+    chunk(c, accB, accA, c - 1, true);
+    epi_finish(c - 1);
+    accA = f16v{};
+    chunk(c + 1, accA, accB, c, true);
+    epi_finish(c);
+  }
+  if (c < nch) {  // one chunk left: its MFMAs carry the epilogue of chunk c−1
+    accB = f16v{};
+    chunk(c, accB, accA, c - 1, true);
+    epi_finish(c - 1);
+#pragma unroll
+    for (int g = 0; g < NG; ++g) epi_slice(accB, c, g);
+    epi_finish(c);
+  } else {
+#pragma unroll
+    for (int g = 0; g < NG; ++g) epi_slice(accA, c - 1, g);
+    epi_finish(c - 1);
   }
 }
 
@@ -212,25 +339,52 @@ extern "C" int rg_head_fwd(const float* h, const float* W, const float* bias, in
                            int64_t ldz, float* pmax, float* psum, int32_t* parg, int want_sum, hipStream_t stream) {
   if (B <= 0 || A <= 0) return RG_ERR_ARG;
   if (ZT && ldz < B) return RG_ERR_ARG;
-  dim3 grid((A + 127) / 128);
-#define HL(HFV)                                                                                                \
-  hipLaunchKernelGGL(k_head_fwd<HFV>, grid, dim3(256), 0, stream, h, W, bias, B, A, ZT, ldz, pmax, psum, parg, \
-                     want_sum)
-  switch (HF) {
-    case 16: HL(16); break;
-    case 32: HL(32); break;
-    case 64: HL(64); break;
-    case 128: HL(128); break;
-    case 256: HL(256); break;
-    default: return RG_ERR_SHAPE;
+  if (HF != 16 && HF != 32 && HF != 64 && HF != 128 && HF != 256) return RG_ERR_SHAPE;
+  // whole 32-item blocks through the single-wave kernel when every 32-row
+  // chunk is full; the remainder items (and ragged B) through the generic one
+  const bool fast = (B % 32) == 0 && (want_sum ? psum != nullptr : true);
+  const int nfull = fast ? A / RG_PBLK : 0;
+  const int j0 = nfull * RG_PBLK;
+  if (nfull > 0) {
+#define PL(HFV, SZV, WSV)                                                                                        \
+  hipLaunchKernelGGL((k_head_fwd_w1<HFV, SZV, WSV>), dim3(nfull), dim3(64), 0, stream, h, W, bias, B, ZT, ldz, \
+                     pmax, psum, parg)
+#define PH(HFV)                            \
+  if (ZT && want_sum) PL(HFV, true, true); \
+  else if (ZT) PL(HFV, true, false);       \
+  else if (want_sum) PL(HFV, false, true); \
+  else PL(HFV, false, false);
+    switch (HF) {
+      case 16: PH(16); break;
+      case 32: PH(32); break;
+      case 64: PH(64); break;
+      case 128: PH(128); break;
+      case 256: PH(256); break;
+    }
+#undef PH
+#undef PL
   }
+  if (j0 < A) {
+    const int ntail = (A - j0 + 127) / 128;
+#define HL(HFV)                                                                                                 \
+  hipLaunchKernelGGL(k_head_fwd<HFV>, dim3(ntail), dim3(256), 0, stream, h, W, bias, B, A, ZT, ldz, pmax, psum, \
+                     parg, want_sum, j0)
+    switch (HF) {
+      case 16: HL(16); break;
+      case 32: HL(32); break;
+      case 64: HL(64); break;
+      case 128: HL(128); break;
+      case 256: HL(256); break;
+    }
 #undef HL
+  }
   RG_LAUNCH_CHECK();
   return RG_OK;
 }
 
 // --------------------------------------------------------- lse combine ----
-// stage 1: split the nJ partials of each row into S groups.
+// stage 1: split the nJ partials of each row into S groups.  Four partials
+// per iteration are loaded before any is merged (the merge chain is serial).
 __global__ void k_lse_stage1(const float* __restrict__ pmax, const float* __restrict__ psum,
                              const int32_t* __restrict__ parg, int B, int nJ, int jchunk, float* __restrict__ omax,
                              float* __restrict__ osum, int32_t* __restrict__ oarg) {
@@ -240,7 +394,21 @@ __global__ void k_lse_stage1(const float* __restrict__ pmax, const float* __rest
   const int j0 = z * jchunk, j1 = min(nJ, j0 + jchunk);
   float m = NEG_INF, s = 0.f;
   int a = INT32_MAX;
-  for (int j = j0; j < j1; ++j) {
+  int j = j0;
+  for (; j + 4 <= j1; j += 4) {
+    float mv[4], sv[4];
+    int av[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int64_t o = (int64_t)(j + q) * B + b;
+      mv[q] = pmax[o];
+      sv[q] = psum ? psum[o] : 0.f;
+      av[q] = parg[o];
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) stat_merge(m, s, a, mv[q], sv[q], av[q]);
+  }
+  for (; j < j1; ++j) {
     const int64_t o = (int64_t)j * B + b;
     stat_merge(m, s, a, pmax[o], psum ? psum[o] : 0.f, parg[o]);
   }
@@ -277,7 +445,7 @@ extern "C" int rg_lse_combine(const float* pmax, const float* psum, const int32_
                               float* work, const float* ZT, int64_t ldz, const int64_t* tgt, int A, float* lse,
                               int32_t* amax, float* loss_row, float* mx, hipStream_t stream) {
   if (B <= 0 || nJ <= 0) return RG_ERR_ARG;
-  int S = 64;
+  int S = 128;
   if (S > nJ) S = nJ;
   int jchunk = (nJ + S - 1) / S;
   S = (nJ + jchunk - 1) / jchunk;
@@ -286,6 +454,9 @@ extern "C" int rg_lse_combine(const float* pmax, const float* psum, const int32_
   int32_t* oarg = reinterpret_cast<int32_t*>(work + 2 * (int64_t)S * B);
   hipLaunchKernelGGL(k_lse_stage1, dim3((B + 255) / 256, S), dim3(256), 0, stream, pmax, psum, parg, B, nJ, jchunk,
                      omax, osum, oarg);
+  else
+    hipLaunchKernelGGL(k_lse_stage1, dim3((B + 255) / 256, S), dim3(256), 0, stream, pmax, psum, parg, B, nJ,
+                       jchunk, omax, osum, oarg);
   hipLaunchKernelGGL(k_lse_final, dim3((B + 255) / 256), dim3(256), 0, stream, omax, osum, oarg, B, S, ZT, ldz,
                      tgt, A, lse, amax, loss_row, mx);
   RG_LAUNCH_CHECK();

@@ -67,3 +67,7 @@ extern "C" int rg_stack_rewards(const double* r_acc, const float* r_div, const f
   RG_LAUNCH_CHECK();
   return RG_OK;
 }
+
+// items per online-softmax partial block of rg_head_fwd (pmax/psum/parg are
+// ceil(A / rg_partial_block()) × B)
+extern "C" int rg_partial_block(void) { return RG_PBLK; }

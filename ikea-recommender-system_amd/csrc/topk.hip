@@ -5,12 +5,12 @@
 // (recommenders/evaluate/eval_protocol.py:75, :199; diversity.py:51;
 // novelty.py:33).  Here the (B, A) logits never leave HBM:
 //   1. the forward kernel already produced, per row, the maximum of every
-//      128-item block (pmax, nJ × B);
+//      RG_PBLK-item block (pmax, nJ × B);
 //   2. per row, the k-th largest block maximum τ is a lower bound of the row's
 //      k-th largest logit (the top-k block maxima are k distinct elements);
 //      radix-select it over the (coarsened) block maxima in LDS;
 //   3. only blocks whose maximum is ≥ τ can hold a top-k element: scan those
-//      blocks' 128 logits, keep the ones ≥ τ as (value, index) candidates;
+//      blocks' logits, keep the ones ≥ τ as (value, index) candidates;
 //   4. bitonic-sort the candidates by (value desc, index asc) and emit k.
 // Exact for any data; ties are broken by the smaller index (canonical order).
 #include "common.h"
@@ -87,8 +87,8 @@ __global__ __launch_bounds__(TK_THREADS) void k_topk(const float* __restrict__ Z
   const int wv = tid >> 6, lane = tid & 63;
   for (int i = wv; i < nS; i += TK_THREADS / 64) {
     if (by_block && sel[i] < s_prefix) continue;  // block maximum < τ
-    const int j0 = i * coarse * 128;
-    const int j1 = min(A, j0 + coarse * 128);
+    const int j0 = i * coarse * RG_PBLK;
+    const int j1 = min(A, j0 + coarse * RG_PBLK);
     for (int j = j0 + lane; j < j1; j += 64) {
       const float z = ZT[(int64_t)j * ldz + b];
       if (z >= tau) {
@@ -135,7 +135,7 @@ __global__ __launch_bounds__(TK_THREADS) void k_topk(const float* __restrict__ Z
 extern "C" int rg_topk(const float* ZT, int64_t ldz, const float* pmax, int B, int A, int k, int32_t* out_idx,
                        float* out_val, int32_t* err, hipStream_t stream) {
   if (B <= 0 || A <= 0 || k <= 0 || k > 1024 || k > A) return RG_ERR_ARG;
-  const int nJ = (A + 127) / 128;
+  const int nJ = (A + RG_PBLK - 1) / RG_PBLK;
   const int coarse = (nJ + TK_MAXSEL - 1) / TK_MAXSEL;
   hipLaunchKernelGGL(k_topk, dim3(B), dim3(TK_THREADS), 0, stream, ZT, ldz, pmax, B, A, nJ, coarse, k, out_idx,
                      out_val, err);

@@ -25,6 +25,7 @@ U64 = C.c_uint64
 # name -> argtypes (restype int for all)
 SIGNATURES = {
     "rg_abi_version": [],
+    "rg_partial_block": [],
     "rg_pack": [P, I, I, I, P, P, P, P],
     "rg_gather": [P, I, I, P, P, P, P, I64, I, I, P, P, P, P],
     "rg_scatter_add": [P, P, I, P, I, I, P, P, I32, P],

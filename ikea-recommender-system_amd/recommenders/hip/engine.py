@@ -23,7 +23,7 @@ import math
 import numpy as np
 import torch
 
-from . import call, host_floats, host_ptr_array, ptr, stream_ptr
+from . import call, host_floats, host_ptr_array, load_library, ptr, stream_ptr
 from .timing import region
 
 
@@ -351,13 +351,14 @@ class _HeadWS:
     def __init__(self, B, A, HF, store_z, device):
         self.B = B
         self.ldz = _round_up(B, 4)
-        self.nJ = (A + 127) // 128
+        pb = load_library().rg_partial_block()   # items per softmax partial (32)
+        self.nJ = (A + pb - 1) // pb
         z = lambda *s, dt=torch.float32: torch.empty(*s, dtype=dt, device=device)
         self.ZT = z(A, self.ldz) if store_z else None
         self.pmax = z(self.nJ, B)
         self.psum = z(self.nJ, B)
         self.parg = z(self.nJ, B, dt=torch.int32)
-        S = min(64, self.nJ)
+        S = min(128, self.nJ)
         self.work = z(3 * S * B)
         self.lse = z(B)
         self.amax = z(B, dt=torch.int32)

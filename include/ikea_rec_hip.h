@@ -86,14 +86,14 @@ int rg_gru_bwd(const float* saved, int64_t plane, const float* Whh, const int32_
 
 /* ---- A6/A7 full-softmax head: replaces self.output(h) (nn.Linear,
  * GRU4Rec/model.py:58-60,80) + nn.CrossEntropyLoss(mean) (:121,146).
- * Writes Z^T (A x ldz) when ZT != NULL and per-(128-item block, row)
- * (max, sum-exp, argmax) partials (nJ = ceil(A/128) blocks x B).
+ * Writes Z^T (A x ldz) when ZT != NULL and per-(32-item block, row)
+ * (max, sum-exp, argmax) partials (nJ = ceil(A/rg_partial_block()) blocks x B).
  * HF in {16, 32, 64, 128, 256}. */
 int rg_head_fwd(const float* h, const float* W, const float* bias, int B, int A, int HF, float* ZT, int64_t ldz,
                 float* pmax, float* psum, int32_t* parg, int want_sum, rg_stream_t stream);
 /* partials -> lse (B), argmax (B) (torch.argmax semantics: first maximum),
  * loss_row (B) = lse - Z[a_b, b], mx (B) = the row maximum.  Every output is
- * optional.  work: 3*min(64,nJ)*B floats. */
+ * optional.  work: 3*min(128,nJ)*B floats. */
 int rg_lse_combine(const float* pmax, const float* psum, const int32_t* parg, int B, int nJ, float* work,
                    const float* ZT, int64_t ldz, const int64_t* tgt, int A, float* lse, int32_t* amax,
                    float* loss_row, float* mx, rg_stream_t stream);
@@ -221,6 +221,8 @@ int rg_sampled_lse(const float* h, const float* W, const float* bias, const int6
 int rg_sampled_dz(float* ZT, int64_t ldz, const float* lse, int B, int S, float gscale, float* dbg,
                   rg_stream_t stream);
 
+/* items per online-softmax partial block of rg_head_fwd: pmax/psum/parg hold ceil(A/that) x B */
+int rg_partial_block(void);
 int rg_abi_version(void);
 
 #ifdef __cplusplus

@@ -45,8 +45,10 @@ def test_topk_with_planted_ties():
     Z = torch.randn(B, A, generator=g)
     Z[:, 100:140] = 7.0   # 40 exact ties at the top
     ZT = Z.t().contiguous().cuda()
-    nJ = (A + 127) // 128
-    pmax = torch.stack([Z[:, j * 128:(j + 1) * 128].max(1).values for j in range(nJ)]).contiguous().cuda()
+    from recommenders.hip import load_library
+    pb = load_library().rg_partial_block()
+    nJ = (A + pb - 1) // pb
+    pmax = torch.stack([Z[:, j * pb:(j + 1) * pb].max(1).values for j in range(nJ)]).contiguous().cuda()
     idx = torch.empty(B, K, dtype=torch.int32, device="cuda")
     call("rg_topk", ZT.data_ptr(), B, pmax.data_ptr(), B, A, K, idx.data_ptr(), None, None, stream_ptr())
     np.testing.assert_array_equal(idx.cpu().numpy(), np.tile(np.arange(100, 120), (B, 1)))

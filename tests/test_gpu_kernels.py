@@ -183,7 +183,8 @@ def test_head_forward_backward(B, A, HF):
     tgt = torch.randint(0, A, (B,), generator=g)
     hd, Wd, bd, td = h.to(dev), W.to(dev), b.to(dev), tgt.to(dev)
     ldz = (B + 3) // 4 * 4
-    nJ = (A + 127) // 128
+    pb = C().load_library().rg_partial_block()
+    nJ = (A + pb - 1) // pb
     ZT = torch.zeros(A, ldz, device=dev)
     pm = torch.zeros(nJ, B, device=dev)
     ps = torch.zeros(nJ, B, device=dev)
@@ -192,7 +193,7 @@ def test_head_forward_backward(B, A, HF):
              pm.data_ptr(), ps.data_ptr(), pa.data_ptr(), 1, st())
     Zref = (h.double() @ W.double().t() + b.double())
     torch.testing.assert_close(ZT[:, :B].t().cpu().double(), Zref, rtol=0, atol=1e-5)
-    work = torch.zeros(3 * min(64, nJ) * B, device=dev)
+    work = torch.zeros(3 * min(128, nJ) * B, device=dev)
     lse = torch.zeros(B, device=dev)
     amax = torch.zeros(B, dtype=torch.int32, device=dev)
     lrow = torch.zeros(B, device=dev)

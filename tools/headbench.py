@@ -30,12 +30,13 @@ tgt = torch.randint(0, A, (B,), device=dev, generator=g)
 if a.zeros:
     h.zero_(); W.zero_(); bias.zero_()
 ldz = (B + 3) // 4 * 4
-nJ = (A + 127) // 128
+from recommenders.hip import load_library  # noqa: E402
+nJ = (A + load_library().rg_partial_block() - 1) // load_library().rg_partial_block()
 ZT = torch.empty(A, ldz, device=dev)
 pm = torch.empty(nJ, B, device=dev)
 ps = torch.empty(nJ, B, device=dev)
 pa = torch.empty(nJ, B, dtype=torch.int32, device=dev)
-work = torch.empty(3 * 64 * B, device=dev)
+work = torch.empty(3 * 128 * B, device=dev)
 lse = torch.empty(B, device=dev)
 amax = torch.empty(B, dtype=torch.int32, device=dev)
 lrow = torch.empty(B, device=dev)
