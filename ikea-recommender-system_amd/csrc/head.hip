@@ -454,9 +454,6 @@ extern "C" int rg_lse_combine(const float* pmax, const float* psum, const int32_
   int32_t* oarg = reinterpret_cast<int32_t*>(work + 2 * (int64_t)S * B);
   hipLaunchKernelGGL(k_lse_stage1, dim3((B + 255) / 256, S), dim3(256), 0, stream, pmax, psum, parg, B, nJ, jchunk,
                      omax, osum, oarg);
-  else
-    hipLaunchKernelGGL(k_lse_stage1, dim3((B + 255) / 256, S), dim3(256), 0, stream, pmax, psum, parg, B, nJ,
-                       jchunk, omax, osum, oarg);
   hipLaunchKernelGGL(k_lse_final, dim3((B + 255) / 256), dim3(256), 0, stream, omax, osum, oarg, B, S, ZT, ldz,
                      tgt, A, lse, amax, loss_row, mx);
   RG_LAUNCH_CHECK();
