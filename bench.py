@@ -55,6 +55,8 @@ def parse():
     ap.add_argument("--config", choices=["c2", "c3"], default="c2",
                     help="c2: headline GRU4Rec full softmax; c3: BidirGRU4Rec with sampled softmax")
     ap.add_argument("--negatives", type=int, default=2048)
+    ap.add_argument("--precision", choices=["f32", "f32x9", "f32x6"], default="f32",
+                    help="head GEMM arithmetic (hip/engine.py SPLIT_TERMS): native fp32 MFMA or split-bf16")
     ap.add_argument("--no-target", action="store_true", help="skip the north-star gather+sampled-logits side run")
     return ap.parse_args()
 
@@ -94,9 +96,10 @@ def make_trainer(cfg, args, dev, shard):
     if cfg == "c2":
         return GRU4Rec_trainer(shard_items=shard, **common)
     if cfg == "c2s":   # GRU4Rec at C2 shapes with the sampled head (north-star target step)
-        return GRU4Rec_trainer(n_negatives=args.negatives, **common)
+        return GRU4Rec_trainer(n_negatives=args.negatives, matmul_precision=args.precision, **common)
     if cfg == "c3":
-        return BidirGRU4Rec_trainer(dropout=0.0, n_negatives=args.negatives, **common)
+        return BidirGRU4Rec_trainer(dropout=0.0, n_negatives=args.negatives, matmul_precision=args.precision,
+                                    **common)
     raise ValueError(cfg)
 
 

@@ -78,3 +78,51 @@ __device__ __forceinline__ void adam_elem(float& p, float& m, float& v, float g,
   const float denom = sqrtf(v) / a.bc2_sqrt + a.eps;
   p = p + a.neg_step * (m / denom);
 }
+
+// ---- split-bf16 fp32 GEMM (precision "f32x9" / "f32x6") ----
+// x = x0 + x1 + x2 EXACTLY for a normal fp32 x: x0 = bf16(x) (RNE), x1 =
+// bf16(x − x0), x2 = x − x0 − x1 (≤ 8 significant bits left, so it is a bf16).
+// A product a·b is then Σ_{p,q} a_p·b_q, every a_p·b_q exact in the fp32
+// accumulator of v_mfma_f32_32x32x16_bf16.  f32x9 keeps all nine terms (the
+// products are exact; only the fp32 accumulation rounds, as in an fmaf
+// chain); f32x6 drops the three with p+q ≥ 3 (|a1·b2|, |a2·b1| ≤ 2^-24·|ab|,
+// |a2·b2| ≤ 2^-32·|ab|: below fp32's unit roundoff per product).
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ f16v mfma32bf(bf16x8 a, bf16x8 b, f16v c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
+// 8 consecutive fp32 values -> their three bf16 planes
+__device__ __forceinline__ void split3x8(const f4& lo, const f4& hi, bf16x8& p0, bf16x8& p1, bf16x8& p2) {
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const float x = i < 4 ? lo[i] : hi[i - 4];
+    const __bf16 b0 = (__bf16)x;
+    const float r1 = x - (float)b0;
+    const __bf16 b1 = (__bf16)r1;
+    const float r2 = r1 - (float)b1;
+    p0[i] = b0;
+    p1[i] = b1;
+    p2[i] = (__bf16)r2;
+  }
+}
+
+// acc += Σ_terms a_p · b_q over one 16-wide k slice (NT = 6 or 9 terms),
+// smallest terms first
+template <int NT>
+__device__ __forceinline__ f16v mfma_split(const bf16x8& a0, const bf16x8& a1, const bf16x8& a2, const bf16x8& b0,
+                                           const bf16x8& b1, const bf16x8& b2, f16v acc) {
+  if (NT == 9) {
+    acc = mfma32bf(a2, b2, acc);
+    acc = mfma32bf(a1, b2, acc);
+    acc = mfma32bf(a2, b1, acc);
+  }
+  acc = mfma32bf(a0, b2, acc);
+  acc = mfma32bf(a1, b1, acc);
+  acc = mfma32bf(a2, b0, acc);
+  acc = mfma32bf(a0, b1, acc);
+  acc = mfma32bf(a1, b0, acc);
+  acc = mfma32bf(a0, b0, acc);
+  return acc;
+}

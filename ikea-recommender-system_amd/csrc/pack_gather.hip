@@ -147,10 +147,83 @@ __global__ __launch_bounds__(256) void k_gather(const int64_t* __restrict__ s, i
   }
 }
 
+// Compile-time-E variant (E ∈ {32, 64, 128, 256}): V4 = E/4 lanes per token
+// row, 256/V4 tokens per pass, and U passes' loads issued before any store so
+// each lane keeps U independent row reads in flight (the table rows are
+// random: latency, not bandwidth, is what a lane waits on).
+template <typename TE, int E>
+__global__ __launch_bounds__(256) void k_gather_e(const int64_t* __restrict__ s, int L,
+                                                  const int32_t* __restrict__ perm,
+                                                  const int32_t* __restrict__ lsort,
+                                                  const int32_t* __restrict__ offs,
+                                                  const TE* __restrict__ emb, int64_t n_rows, int reverse,
+                                                  int32_t* __restrict__ tok_id, float* __restrict__ X,
+                                                  int32_t* __restrict__ err) {
+  constexpr int V4 = E / 4;
+  constexpr int TPP = 256 / V4;
+  constexpr int U = TPP >= 16 ? 2 : 4;
+  const int r = blockIdx.x;
+  const int b = perm[r];
+  const int len = lsort[r];
+  const int base = offs[r];
+  const int c = threadIdx.x % V4, t0 = threadIdx.x / V4;
+  const int64_t* srow = s + (int64_t)b * L;
+  for (int tb = t0; tb < len; tb += TPP * U) {
+    f4 v[U];
+    int32_t idv[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int t = tb + TPP * u;
+      v[u] = f4{0.f, 0.f, 0.f, 0.f};
+      idv[u] = -1;
+      if (t < len) {
+        const int64_t id = srow[reverse ? len - 1 - t : t];
+        if (id >= 0 && id < n_rows) {  // nn.Embedding raises on such ids
+          idv[u] = (int32_t)id;
+          v[u] = load4(emb + id * E, c);
+        }
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int t = tb + TPP * u;
+      if (t < len) {
+        const int tok = base + t;
+        reinterpret_cast<f4*>(X + (int64_t)tok * E)[c] = v[u];
+        if (c == 0) {
+          tok_id[tok] = idv[u];
+          if (idv[u] < 0 && err) atomicOr(err, 1);
+        }
+      }
+    }
+  }
+}
+
+template <typename TE>
+static bool launch_gather_e(const int64_t* s, int B, int L, const int32_t* perm, const int32_t* lsort,
+                            const int32_t* offs, const TE* emb, int64_t n_rows, int E, int reverse,
+                            int32_t* tok_id, float* X, int32_t* err, hipStream_t stream) {
+#define GE(EV)                                                                                                   \
+  hipLaunchKernelGGL((k_gather_e<TE, EV>), dim3(B), dim3(256), 0, stream, s, L, perm, lsort, offs, emb, n_rows, \
+                     reverse, tok_id, X, err)
+  switch (E) {
+    case 32: GE(32); return true;
+    case 64: GE(64); return true;
+    case 128: GE(128); return true;
+    case 256: GE(256); return true;
+    default: return false;
+  }
+#undef GE
+}
+
 extern "C" int rg_gather(const int64_t* s, int B, int L, const int32_t* perm, const int32_t* lsort,
                          const int32_t* offs, const float* emb, int64_t n_rows, int E, int reverse,
                          int32_t* tok_id, float* X, int32_t* err, hipStream_t stream) {
   if (B <= 0 || (E & 3)) return RG_ERR_ARG;
+  if (launch_gather_e(s, B, L, perm, lsort, offs, emb, n_rows, E, reverse, tok_id, X, err, stream)) {
+    RG_LAUNCH_CHECK();
+    return RG_OK;
+  }
   hipLaunchKernelGGL(k_gather<float>, dim3(B), dim3(256), 0, stream, s, L, perm, lsort, offs, emb, n_rows, E,
                      reverse, tok_id, X, err);
   RG_LAUNCH_CHECK();
@@ -163,6 +236,11 @@ extern "C" int rg_gather_h(const int64_t* s, int B, int L, const int32_t* perm, 
                            const int32_t* offs, const uint16_t* emb16, int64_t n_rows, int E, int reverse,
                            int32_t* tok_id, float* X, int32_t* err, hipStream_t stream) {
   if (B <= 0 || (E & 3)) return RG_ERR_ARG;
+  if (launch_gather_e(s, B, L, perm, lsort, offs, reinterpret_cast<const __half*>(emb16), n_rows, E, reverse, tok_id,
+                      X, err, stream)) {
+    RG_LAUNCH_CHECK();
+    return RG_OK;
+  }
   hipLaunchKernelGGL(k_gather<__half>, dim3(B), dim3(256), 0, stream, s, L, perm, lsort, offs,
                      reinterpret_cast<const __half*>(emb16), n_rows, E, reverse, tok_id, X, err);
   RG_LAUNCH_CHECK();

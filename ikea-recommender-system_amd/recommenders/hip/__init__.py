@@ -22,7 +22,10 @@ D = C.c_double
 I32 = C.c_int32
 U64 = C.c_uint64
 
-# name -> argtypes (restype int for all)
+# entry points returning int64_t (all others return int)
+RESTYPE_I64 = {"rg_sampled_work_bytes"}
+
+# name -> argtypes
 SIGNATURES = {
     "rg_abi_version": [],
     "rg_partial_block": [],
@@ -65,6 +68,9 @@ SIGNATURES = {
     "rg_adam_rows_h": [P, P, P, P, P, I32, I64, I, P, P, P],
     "rg_f32_to_f16": [P, I64, P, P],
     "rg_sample_uniform": [U64, U64, I, I64, P, P],
+    "rg_sampled_nparts": [I, I, I],
+    "rg_sampled_work_bytes": [I, I, I],
+    "rg_sampled_fwd_x": [P, P, P, P, I, U64, U64, I64, I, I, I, I, P, I64, P, P, P, P, P, P],
     "rg_sampled_fwd": [P, P, P, P, I, I, I, P, I64, P, P, P, P, P],
     "rg_sampled_lse": [P, P, P, P, I, I64, I, P, P, I, F, P, P, P, P, P, P, P],
     "rg_sampled_dz": [P, I64, P, I, I, F, P, P],
@@ -87,7 +93,7 @@ def load_library(path: str = LIB_PATH):
     for name, argtypes in SIGNATURES.items():
         fn = getattr(lib, name)
         fn.argtypes = argtypes
-        fn.restype = C.c_int
+        fn.restype = C.c_int64 if name in RESTYPE_I64 else C.c_int
     _lib = lib
     return lib
 

@@ -370,6 +370,20 @@ class _HeadWS:
         self.dh_slabs = z(self.dh_splits, B, HF) if store_z else None
 
 
+# Head-GEMM arithmetic (build extension; the reference computes in fp32):
+#   "f32"   native fp32 MFMA (v_mfma_f32_32x32x2_f32: bitwise an fmaf chain)
+#   "f32x9" fp32 operands split exactly into three bf16 planes, all nine
+#           plane products on bf16 MFMAs (exact products, fp32 accumulation)
+#   "f32x6" the same without the three sub-ulp terms (csrc/common.h)
+SPLIT_TERMS = {"f32x9": 9, "f32x6": 6}
+
+
+def check_precision(precision):
+    if precision not in ("f32", "f32x9", "f32x6"):
+        raise ValueError(f"matmul_precision must be 'f32', 'f32x9' or 'f32x6', got {precision!r}")
+    return precision
+
+
 class SoftmaxHead:
     """Linear(HF→A) + CrossEntropyLoss(mean) with fused backward/Adam.
     With ``shard=(lo, hi)`` only items [lo, hi) are held (multi-GPU item
@@ -383,12 +397,16 @@ class SoftmaxHead:
         if shard is not None:
             w, b = w[self.lo:self.hi].contiguous(), b[self.lo:self.hi].contiguous()
         self.name, self.A, self.HF, self.device = name, self.hi - self.lo, HF, device
+        self.precision = "f32"  # see set_matmul_precision
         self.W = Param(f"{name}.weight", w, device)
         self.b = Param(f"{name}.bias", b, device)
         self._ws = {}
 
     def named_params(self):
         return [self.W, self.b]
+
+    def set_matmul_precision(self, precision):
+        self.precision = check_precision(precision)
 
     def ws(self, slot, B, store_z):
         key = (slot, B, store_z)
@@ -453,11 +471,12 @@ class SoftmaxHead:
 
 # --------------------------------------------------------- sampled head ----
 class _SampledWS:
-    def __init__(self, B, S, HF, device):
+    def __init__(self, B, S, HF, device, terms=0):
         z = lambda *s, dt=torch.float32: torch.empty(*s, dtype=dt, device=device)
         self.B, self.S = B, S
         self.ldz = _round_up(B, 4)
-        self.nT = (S + 127) // 128
+        self.terms = terms  # 0: native fp32 forward, 6 / 9: split-bf16 (rg_sampled_fwd_x)
+        self.nT = call("rg_sampled_nparts", B, S, terms)  # (max, Σexp) partials per row
         self.ZT = z(S, self.ldz)
         self.pmax = z(self.nT, B)
         self.psum = z(self.nT, B)
@@ -471,6 +490,7 @@ class _SampledWS:
         self.nrows = torch.full((1,), S + B, dtype=torch.int32, device=device)
         self.Wg = z(S, HF)
         self.bg = z(S)
+        self.work = None  # split-bf16 operand planes (allocated on first use)
         self.dh_splits = max(1, min(8, S // 256))
         self.dw_splits = max(1, min(16, B // 256))
         # slab 0 = the positive part of dh (written by rg_sampled_lse)
@@ -502,10 +522,17 @@ class SampledSoftmaxHead(SoftmaxHead):
         self.tag = 0
         self._sws = {}
 
+    def split_terms(self, B):
+        """bf16 terms of the forward for batch B (0: native fp32 MFMA)."""
+        if self.precision == "f32" or B % 32 or self.S % 32:
+            return 0
+        return SPLIT_TERMS[self.precision]
+
     def sws(self, slot, B):
         w = self._sws.get(slot)
-        if w is None or w.B != B:
-            w = _SampledWS(B, self.S, self.HF, self.device)
+        terms = self.split_terms(B)
+        if w is None or w.B != B or w.terms != terms:
+            w = _SampledWS(B, self.S, self.HF, self.device, terms)
             self._sws[slot] = w
         return w
 
@@ -514,12 +541,22 @@ class SampledSoftmaxHead(SoftmaxHead):
         w = self.sws(slot, B)
         st = stream_ptr()
         g = _f32(1.0 / B)
-        call("rg_sample_uniform", self.seed, self.draws, self.S, self.A, w.ids.data_ptr(), st)
+        split = w.terms != 0
+        with region("sampled_fwd"):  # the negatives' row gather is part of the timed logits step
+            if split:  # draw + gather + operand split fused into one prep launch
+                if w.work is None:
+                    w.work = torch.empty(call("rg_sampled_work_bytes", B, self.S, self.HF), dtype=torch.uint8,
+                                         device=self.device)
+                call("rg_sampled_fwd_x", h.data_ptr(), self.W.p.data_ptr(), self.b.p.data_ptr(), w.ids.data_ptr(),
+                     1, self.seed, self.draws, self.A, B, self.S, self.HF, w.terms,
+                     w.ZT.data_ptr(), w.ldz, w.pmax.data_ptr(), w.psum.data_ptr(), w.Wg.data_ptr(),
+                     w.bg.data_ptr(), w.work.data_ptr(), st)
+            else:
+                call("rg_sample_uniform", self.seed, self.draws, self.S, self.A, w.ids.data_ptr(), st)
+                call("rg_sampled_fwd", h.data_ptr(), self.W.p.data_ptr(), self.b.p.data_ptr(), w.ids.data_ptr(),
+                     B, self.S, self.HF, w.ZT.data_ptr(), w.ldz, w.pmax.data_ptr(), w.psum.data_ptr(),
+                     w.Wg.data_ptr(), w.bg.data_ptr(), st)
         self.draws += 1
-        with region("sampled_fwd"):
-            call("rg_sampled_fwd", h.data_ptr(), self.W.p.data_ptr(), self.b.p.data_ptr(), w.ids.data_ptr(), B,
-                 self.S, self.HF, w.ZT.data_ptr(), w.ldz, w.pmax.data_ptr(), w.psum.data_ptr(), w.Wg.data_ptr(),
-                 w.bg.data_ptr(), st)
         call("rg_sampled_lse", h.data_ptr(), self.W.p.data_ptr(), self.b.p.data_ptr(), tgt.data_ptr(), B, self.A,
              self.HF, w.pmax.data_ptr(), w.psum.data_ptr(), w.nT, g, w.lse.data_ptr(), w.loss_row.data_ptr(),
              w.ids.data_ptr() + 4 * self.S, w.gb.data_ptr() + 4 * self.S,

@@ -58,6 +58,13 @@ class HipNet:
         self._hd = {}
 
     # ------------------------------------------------------- nn.Module-ish --
+    def set_matmul_precision(self, precision):
+        """Arithmetic of the head GEMMs ("f32" native, "f32x9" / "f32x6"
+        split-bf16, engine.SPLIT_TERMS); only the sampled head uses it so far."""
+        for hd in self.heads.values():
+            hd.set_matmul_precision(precision)
+        return self
+
     def named_param_objs(self):
         out = list(self.trunk.named_params())
         for hd in self.heads.values():

@@ -33,7 +33,8 @@ class BidirGRU4Rec(SupervisedNet):
 class BidirGRU4Rec_trainer:
     def __init__(self, hidden_dim, embedding_dim, gru_layers, dropout, train_pad_embed, use_packed_seq,
                  learning_rate, item_num, state_size, action_dim, device, padding_idx=None, torch_rand_seed=118,
-                 python_rand_seed=999, n_negatives=None, neg_seed=0, fp16_embeddings=False):
+                 python_rand_seed=999, n_negatives=None, neg_seed=0, fp16_embeddings=False,
+                 matmul_precision="f32"):
         torch.manual_seed(torch_rand_seed)
         random.seed(python_rand_seed)
         self.device = require_gpu(device)
@@ -43,6 +44,7 @@ class BidirGRU4Rec_trainer:
                                       train_pad_embed=train_pad_embed, padding_idx=padding_idx,
                                       device=self.device, n_negatives=n_negatives, neg_seed=neg_seed,
                                       fp16_embeddings=fp16_embeddings)
+        self.gru_model.set_matmul_precision(matmul_precision)
         self.learning_rate = learning_rate
         self.cross_entropy_loss = nn.CrossEntropyLoss(weight=None, reduction="mean")
         self.clock = AdamClock(learning_rate)

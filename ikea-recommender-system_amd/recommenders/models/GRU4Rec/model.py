@@ -54,7 +54,7 @@ class GRU4Rec_trainer:
     def __init__(self, hidden_dim, embedding_dim, gru_layers, train_pad_embed, use_packed_seq, learning_rate,
                  item_num, state_size, action_dim, device, padding_idx=None, torch_rand_seed=118,
                  python_rand_seed=999, shard_items=False, process_group=None, n_negatives=None, neg_seed=0,
-                 fp16_embeddings=False):
+                 fp16_embeddings=False, matmul_precision="f32"):
         torch.manual_seed(torch_rand_seed)
         random.seed(python_rand_seed)
         self.device = require_gpu(device)
@@ -72,6 +72,9 @@ class GRU4Rec_trainer:
                                  use_packed_seq=use_packed_seq, train_pad_embed=train_pad_embed,
                                  padding_idx=padding_idx, device=self.device, comm=self.comm,
                                  n_negatives=n_negatives, neg_seed=neg_seed, fp16_embeddings=fp16_embeddings)
+        # matmul_precision (build extension): "f32" (default, native fp32 MFMA)
+        # or the split-bf16 "f32x9" / "f32x6" head GEMMs (hip/engine.py)
+        self.gru_model.set_matmul_precision(matmul_precision)
         self.learning_rate = learning_rate
         self.cross_entropy_loss = nn.CrossEntropyLoss(weight=None, reduction="mean")
         self.clock = AdamClock(learning_rate)

@@ -208,10 +208,25 @@ int rg_f32_to_f16(const float* x, int64_t n, uint16_t* out, rg_stream_t stream);
  * built with n_negatives) ---- */
 /* out[s] = uniform draw on [0, A): hi64(splitmix64(seed + phi*(counter*S + s + 1)) * A) */
 int rg_sample_uniform(uint64_t seed, uint64_t counter, int S, int64_t A, int32_t* out, rg_stream_t stream);
+/* number of (max, Σexp) partials per row the forward writes: terms = 0 (rg_sampled_fwd):
+ * ceil(S/128); terms = 6 / 9 (rg_sampled_fwd_x, S and B multiples of 32): S/32 */
+int rg_sampled_nparts(int B, int S, int terms);
 /* Zᵀ[s][b] = h_b·W[neg_s] + bias[neg_s] (S × ldz) + per-(128-negative tile, row) (max, Σexp)
- * partials (nT × B); Wg/bg (optional, both or neither): the gathered rows. HF ∈ {32,64,128,256}. */
+ * partials (rg_sampled_nparts(B, S, 0) × B); Wg/bg (optional, both or neither): the gathered rows.
+ * HF ∈ {32,64,128,256}. */
 int rg_sampled_fwd(const float* h, const float* W, const float* bias, const int32_t* neg, int B, int S, int HF,
                    float* ZT, int64_t ldz, float* pmax, float* psum, float* Wg, float* bg, rg_stream_t stream);
+/* scratch bytes rg_sampled_fwd_x needs: (S + B)·HF·6 (the bf16 operand planes) */
+int64_t rg_sampled_work_bytes(int B, int S, int HF);
+/* rg_sampled_fwd computed on bf16 MFMAs from an exact three-plane bf16 split of both fp32
+ * operands (csrc/common.h): terms = 9 keeps every plane product (exact products, fp32
+ * accumulation), 6 drops the three below fp32's unit roundoff.  B % 32 == 0, S % 32 == 0;
+ * partials as rg_sampled_nparts(B, S, terms); Wg optional, bg required.  draw = 1: neg is an output
+ * filled with rg_sample_uniform(seed, counter, S, A) (the draw fused into the operand prep);
+ * draw = 0: neg is an input.  work: rg_sampled_work_bytes(B, S, HF) bytes of device scratch. */
+int rg_sampled_fwd_x(const float* h, const float* W, const float* bias, int32_t* neg, int draw, uint64_t seed,
+                     uint64_t counter, int64_t A, int B, int S, int HF, int terms, float* ZT, int64_t ldz,
+                     float* pmax, float* psum, float* Wg, float* bg, void* work, rg_stream_t stream);
 /* per row: z_pos = h_b·W[a_b] + bias[a_b]; lse over {z_pos} ∪ partials; loss_row = lse − z_pos;
  * ids[b] = a_b; dzpos = (exp(z_pos − lse) − 1)·g; gpos = dzpos·h_b; dhpos = dzpos·W[a_b] */
 int rg_sampled_lse(const float* h, const float* W, const float* bias, const int64_t* tgt, int B, int64_t A, int HF,

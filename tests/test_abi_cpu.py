@@ -12,7 +12,7 @@ HDR = os.path.join(REPO, "include", "ikea_rec_hip.h")
 
 def declared_symbols():
     txt = open(HDR).read()
-    return sorted(set(re.findall(r"\bint\s+(rg_\w+)\s*\(", txt)))
+    return sorted(set(re.findall(r"\bint(?:64_t)?\s+(rg_\w+)\s*\(", txt)))
 
 
 def test_header_declares_all_bound_symbols():
