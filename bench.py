@@ -35,6 +35,7 @@ import torch  # noqa: E402
 
 ITEMS, DIM, SEQ, BATCH = 1_000_000, 128, 50, 4096
 FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: dense f32 MFMA (= f32 vector peak)
+BF16_MFMA_PEAK_TFLOPS = 2500.0  # dense bf16 MFMA (no sparsity)
 HBM_PEAK_GBS = 8000.0
 
 
@@ -94,7 +95,7 @@ def make_trainer(cfg, args, dev, shard):
     common = dict(hidden_dim=E, embedding_dim=E, gru_layers=1, train_pad_embed=True, use_packed_seq=True,
                   learning_rate=0.01, item_num=N, state_size=L, action_dim=N, device=dev)
     if cfg == "c2":
-        return GRU4Rec_trainer(shard_items=shard, **common)
+        return GRU4Rec_trainer(shard_items=shard, matmul_precision=args.precision, **common)
     if cfg == "c2s":   # GRU4Rec at C2 shapes with the sampled head (north-star target step)
         return GRU4Rec_trainer(n_negatives=args.negatives, matmul_precision=args.precision, **common)
     if cfg == "c3":
@@ -204,17 +205,32 @@ def main():
     HF = E * (2 if args.config == "c3" else 1)
     if args.config == "c2":
         flops_head = 2.0 * B * N * E  # one (B × E)·(E × A) contraction
+        terms = {"f32x9": 9, "f32x6": 6}.get(args.precision, 0)
         if kern:
             heads = {k: kern[k] for k in ("head_fwd", "head_dh", "head_dw_adam") if k in kern}
             dom = max(heads, key=heads.get)
-            ach = flops_head / (heads[dom] * 1e-3) / 1e12
+            t = heads[dom] * 1e-3
             traffic = None
             pmc = os.path.join(HERE, "profiles", "pmc_traffic.json")
             if os.path.exists(pmc):
-                traffic = json.load(open(pmc)).get(dom)
-            roof = {"bound": "mfma", "kernel": dom, "achieved": round(ach, 2), "peak": FP32_MFMA_PEAK_TFLOPS,
-                    "unit": "TFLOP/s", "frac": round(ach / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": traffic,
-                    "flops_per_launch": flops_head}
+                traffic = json.load(open(pmc)).get(f"{dom}:{args.precision}" if terms else dom)
+            if terms:
+                # fused split-bf16 head (csrc/head_flash.hip): pass 1 (head_fwd: Z and the softmax half of
+                # dh) and pass 2 (head_dw_adam: Z recomputed, dW) each run two contractions, every fp32
+                # product as `terms` exact bf16 plane products on v_mfma_f32_32x32x16_bf16
+                ex = 2 * terms * flops_head if dom in ("head_fwd", "head_dw_adam") else 0.0
+                alg = {"head_fwd": 2, "head_dw_adam": 1}.get(dom, 0) * flops_head
+                ach = ex / t / 1e12
+                roof = {"bound": "mfma", "kernel": dom, "achieved": round(ach, 2), "peak": BF16_MFMA_PEAK_TFLOPS,
+                        "unit": "TFLOP/s", "frac": round(ach / BF16_MFMA_PEAK_TFLOPS, 4), "traffic": traffic,
+                        "flops_per_launch": ex,
+                        "mfma": f"bf16 MFMA, fp32 operands split exactly into 3 bf16 planes, {terms} plane products",
+                        "algorithmic_fp32_TFLOPs": round(alg / t / 1e12, 2)}
+            else:
+                ach = flops_head / t / 1e12
+                roof = {"bound": "mfma", "kernel": dom, "achieved": round(ach, 2), "peak": FP32_MFMA_PEAK_TFLOPS,
+                        "unit": "TFLOP/s", "frac": round(ach / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": traffic,
+                        "flops_per_launch": flops_head}
         if world == 1 and not args.no_target and kern:
             # north-star target step measured on GRU4Rec at C2
             # shapes with the sampled head: a short side run, own trainer
@@ -247,7 +263,8 @@ def main():
         "metric": metric,
         "value": round(value, 2), "unit": "session-steps/sec", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak",
-        "vs_baseline": None, "dtype": "f32", "data": "synthetic (seeded Zipf session stream, random-init weights)",
+        "vs_baseline": None, "dtype": "f32", "matmul_precision": args.precision,
+        "data": "synthetic (seeded Zipf session stream, random-init weights)",
         "config": {"workload": workload,
                    "global_batch": B * world, "seq_len": L, "items": N, "dim": E,
                    "parallelism": (f"dp{world} trunk + {world}-way item-sharded head (RCCL)" if world > 1

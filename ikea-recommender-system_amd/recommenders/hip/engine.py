@@ -370,6 +370,30 @@ class _HeadWS:
         self.dh_slabs = z(self.dh_splits, B, HF) if store_z else None
 
 
+class _FlashWS:
+    """Workspace of the fused split-bf16 training head (csrc/head_flash.hip):
+    bf16 operand planes of h and W (K- and R-layouts), the bias padded with
+    -inf to whole 32-item chunks, per-(split, row) softmax partials and the
+    unnormalised dh partials O (nsplit × HF × B).  No logits are stored."""
+
+    def __init__(self, B, A, HF, device):
+        u8 = lambda n: torch.empty(int(n), dtype=torch.uint8, device=device)  # noqa: E731
+        z = lambda *s: torch.empty(*s, dtype=torch.float32, device=device)  # noqa: E731
+        self.B = B
+        self.terms = 0
+        nrb = -(-B // 256)  # 256-row workgroups of pass 1
+        # about one pass-1 workgroup per CU; a multiple of 8 for the XCD order
+        self.nsplit = _round_up(min(max(1, 256 // nrb), -(-A // 32)), 8)
+        hb, wb = call("rg_head_plane_bytes", B, HF), call("rg_head_plane_bytes", A, HF)
+        self.Hk, self.Hr, self.Wk, self.Wr = u8(hb), u8(hb), u8(wb), u8(wb)
+        self.bias_pad = z(_round_up(A, 32))
+        self.pm, self.pl = z(self.nsplit, B), z(self.nsplit, B)
+        self.pO = z(self.nsplit, HF, B)
+        self.rows = z(B, 2)
+        self.lse, self.zt, self.loss_row = z(B), z(B), z(B)
+        self.loss = torch.zeros(1, device=device)
+
+
 # Head-GEMM arithmetic (build extension; the reference computes in fp32):
 #   "f32"   native fp32 MFMA (v_mfma_f32_32x32x2_f32: bitwise an fmaf chain)
 #   "f32x9" fp32 operands split exactly into three bf16 planes, all nine
@@ -401,12 +425,65 @@ class SoftmaxHead:
         self.W = Param(f"{name}.weight", w, device)
         self.b = Param(f"{name}.bias", b, device)
         self._ws = {}
+        self._fws = {}
+        # callers that read the stored logits after forward_loss (SMORL's
+        # top-k rewards) keep the native path
+        self.keep_logits = False
 
     def named_params(self):
         return [self.W, self.b]
 
     def set_matmul_precision(self, precision):
         self.precision = check_precision(precision)
+
+    # ---- fused training head (csrc/head_flash.hip) ----
+    def flash_terms(self, B):
+        """bf16 terms of the fused training head for a batch of B rows; 0
+        selects the native fp32 path that stores Zᵀ."""
+        if self.precision == "f32" or self.keep_logits or self.HF not in (32, 64, 128) or B % 32:
+            return 0
+        return SPLIT_TERMS[self.precision]
+
+    def fws(self, slot, B):
+        w = self._fws.get(slot)
+        if w is None or w.B != B:
+            self._fws.pop(slot, None)
+            w = _FlashWS(B, self.A, self.HF, self.device)
+            self._fws[slot] = w
+        return w
+
+    def flash_forward(self, h, tgt, slot, terms):
+        """Pass 1 + this head's lse and target logit (zt = 0 when the target
+        lies outside the held items [lo, hi))."""
+        B, A, HF = h.shape[0], self.A, self.HF
+        w = self.fws(slot, B)
+        w.terms = terms
+        st = stream_ptr()
+        W, b = self.W.p.data_ptr(), self.b.p.data_ptr()
+        with region("head_fwd"):
+            call("rg_head_planes", h.data_ptr(), B, HF, w.Hk.data_ptr(), w.Hr.data_ptr(), None, None, st)
+            call("rg_head_planes", W, A, HF, w.Wk.data_ptr(), w.Wr.data_ptr(), b, w.bias_pad.data_ptr(), st)
+            call("rg_flash_fwd", w.Hk.data_ptr(), w.Wk.data_ptr(), w.Wr.data_ptr(), w.bias_pad.data_ptr(), B, A, HF,
+                 terms, w.nsplit, w.pm.data_ptr(), w.pl.data_ptr(), w.pO.data_ptr(), st)
+        call("rg_flash_lse", w.pm.data_ptr(), w.pl.data_ptr(), w.nsplit, h.data_ptr(), W, b, tgt.data_ptr(), self.lo,
+             A, B, HF, w.lse.data_ptr(), w.zt.data_ptr(), st)
+        return w
+
+    def flash_dh(self, w, tgt, lse, g, dh_out):
+        """dh_out := this head's ∂loss/∂h given the (all-rank) lse."""
+        st = stream_ptr()
+        call("rg_flash_rows", lse.data_ptr(), tgt.data_ptr(), self.lo, self.A, w.B, w.rows.data_ptr(), st)
+        with region("head_dh"):
+            call("rg_flash_dh", w.pm.data_ptr(), w.pO.data_ptr(), w.rows.data_ptr(), w.nsplit, self.W.p.data_ptr(), g,
+                 w.B, self.HF, dh_out.data_ptr(), st)
+
+    def flash_dw_adam(self, w, g, adam6):
+        """Pass 2: dW, db and the Adam step of W / b (after flash_dh)."""
+        with region("head_dw_adam"):
+            call("rg_flash_dw_adam", w.Hk.data_ptr(), w.Hr.data_ptr(), w.Wk.data_ptr(), w.bias_pad.data_ptr(),
+                 w.rows.data_ptr(), g, w.B, self.A, self.HF, w.terms, self.W.p.data_ptr(), self.W.m.data_ptr(),
+                 self.W.v.data_ptr(), self.b.p.data_ptr(), self.b.m.data_ptr(), self.b.v.data_ptr(), adam6, None,
+                 None, stream_ptr())
 
     def ws(self, slot, B, store_z):
         key = (slot, B, store_z)
@@ -430,8 +507,14 @@ class SoftmaxHead:
         """CE(mean) of Z = h·Wᵀ + b against tgt; keeps Zᵀ / lse for backward.
         Returns the device loss tensor (1,) and the workspace."""
         B = h.shape[0]
-        w = self.ws(slot, B, True)
         st = stream_ptr()
+        terms = self.flash_terms(B)
+        if terms:  # fused split-bf16 head: no logits stored
+            w = self.flash_forward(h, tgt, slot, terms)
+            call("rg_sub", w.lse.data_ptr(), w.zt.data_ptr(), B, w.loss_row.data_ptr(), st)
+            call("rg_sum_scale", w.loss_row.data_ptr(), B, _f32(1.0 / B), w.loss.data_ptr(), None, st)
+            return w.loss, w
+        w = self.ws(slot, B, True)
         with region("head_fwd"):
             call("rg_head_fwd", h.data_ptr(), self.W.p.data_ptr(), self.b.p.data_ptr(), B, self.A, self.HF,
                  w.ZT.data_ptr(), w.ldz, w.pmax.data_ptr(), w.psum.data_ptr(), w.parg.data_ptr(), 1, st)
@@ -444,9 +527,14 @@ class SoftmaxHead:
     def backward_step(self, h, tgt, dh_out, adam6, slot="main", gscale=None):
         """dh_out (B, HF) := ∂loss/∂h (overwrites); then the fused dW/db + Adam."""
         B = h.shape[0]
+        g = _f32(1.0 / B) if gscale is None else gscale
+        if self.flash_terms(B):
+            w = self.fws(slot, B)
+            self.flash_dh(w, tgt, w.lse, g, dh_out)
+            self.flash_dw_adam(w, g, adam6)
+            return
         w = self.ws(slot, B, True)
         st = stream_ptr()
-        g = _f32(1.0 / B) if gscale is None else gscale
         with region("head_dh"):
             n = call("rg_head_dh", w.ZT.data_ptr(), w.ldz, w.lse.data_ptr(), tgt.data_ptr(), g, self.W.p.data_ptr(),
                      B, self.A, self.HF, w.dh_splits, w.dh_slabs.data_ptr(), st)

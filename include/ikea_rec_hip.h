@@ -91,6 +91,44 @@ int rg_gru_bwd(const float* saved, int64_t plane, const float* Whh, const int32_
  * HF in {16, 32, 64, 128, 256}. */
 int rg_head_fwd(const float* h, const float* W, const float* bias, int B, int A, int HF, float* ZT, int64_t ldz,
                 float* pmax, float* psum, int32_t* parg, int want_sum, rg_stream_t stream);
+/* scratch bytes rg_head_fwd_x needs: B·HF·6 (h's bf16 planes) */
+int64_t rg_head_work_bytes(int B, int HF);
+/* rg_head_fwd on split-bf16 MFMAs (csrc/head_split.hip): terms = 9 (exact products, fp32
+ * accumulation) or 6 (sub-ulp terms dropped); same Zᵀ and partial outputs.  B % 32 == 0,
+ * HF in {32, 64, 128, 256}; work: rg_head_work_bytes(B, HF) bytes of device scratch. */
+int rg_head_fwd_x(const float* h, const float* W, const float* bias, int B, int A, int HF, int terms, float* ZT,
+                  int64_t ldz, float* pmax, float* psum, int32_t* parg, int want_sum, void* work,
+                  rg_stream_t stream);
+/* ---- A6/A7/A8 fused training head (csrc/head_flash.hip): the full-softmax
+ * Linear + CrossEntropyLoss(mean) + Adam step of GRU4Rec/model.py:58-60, 80,
+ * 121, 146, 149-153 without materialising the (B × A) logits, on split-bf16
+ * MFMAs (terms 9: exact products, 6: sub-ulp terms dropped).  HF in {32, 64,
+ * 128}; B % 32 == 0.  Multi-GPU item shards pass their first item `lo` and
+ * merge lse over ranks between rg_flash_lse and rg_flash_rows.
+ * rg_head_plane_bytes: bytes of one operand-plane buffer for `rows` rows.
+ * rg_head_planes: X (rows × HF) -> K-planes / R-planes (either optional);
+ *   with bias: bias_pad (rows rounded up to 32, -inf padded).
+ * rg_flash_fwd: pass 1 — per (split, row) running max pm and Σexp pl (log2
+ *   units) and O = Σ_j 2^(z_j − m)·W_j (nsplit × HF × B).
+ * rg_flash_lse: lse (natural units) over the splits; zt = the target logit
+ *   when the target is one of items [lo, lo + A), else 0.
+ * rg_flash_rows: row records (lse·log2 e, target − lo or -1), B × 8 bytes.
+ * rg_flash_dh: dh = gscale·(Σ_s 2^(m_s − lse)·O_s − W[target]) (B × HF).
+ * rg_flash_dw_adam: pass 2 — dW = dZᵀ·h, db = Σ_b dZ, then Adam (adam6, host
+ *   array) on W / bias / moments; with dW_out / db_out the raw gradients. */
+int64_t rg_head_plane_bytes(int rows, int HF);
+int rg_head_planes(const float* X, int rows, int HF, void* planes_k, void* planes_r, const float* bias,
+                   float* bias_pad, rg_stream_t stream);
+int rg_flash_fwd(const void* Hk, const void* Wk, const void* Wr, const float* bias_pad, int B, int A, int HF,
+                 int terms, int nsplit, float* pm, float* pl, float* pO, rg_stream_t stream);
+int rg_flash_lse(const float* pm, const float* pl, int nsplit, const float* h, const float* W, const float* bias,
+                 const int64_t* tgt, int64_t lo, int A, int B, int HF, float* lse, float* zt, rg_stream_t stream);
+int rg_flash_rows(const float* lse, const int64_t* tgt, int64_t lo, int A, int B, void* rowinfo, rg_stream_t stream);
+int rg_flash_dh(const float* pm, const float* pO, const void* rowinfo, int nsplit, const float* W, float gscale,
+                int B, int HF, float* dh, rg_stream_t stream);
+int rg_flash_dw_adam(const void* Hk, const void* Hr, const void* Wk, const float* bias_pad, const void* rowinfo,
+                     float gscale, int B, int A, int HF, int terms, float* W, float* mW, float* vW, float* bias,
+                     float* mb, float* vb, const float* adam6, float* dW_out, float* db_out, rg_stream_t stream);
 /* partials -> lse (B), argmax (B) (torch.argmax semantics: first maximum),
  * loss_row (B) = lse - Z[a_b, b], mx (B) = the row maximum.  Every output is
  * optional.  work: 3*min(128,nJ)*B floats. */

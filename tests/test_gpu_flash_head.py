@@ -1,0 +1,147 @@
+"""Fused split-bf16 full-softmax training head (csrc/head_flash.hip) against
+an fp64 torch restatement of the reference's nn.Linear + CrossEntropyLoss(mean)
+forward / backward (GRU4Rec/model.py:58-60, 80, 121, 146): pass 1 (logits ->
+online LSE -> unnormalised dh partials), the LSE / dh combine and pass 2 (dW,
+db).  Kernel tolerances are those of the native fp32 path
+(test_gpu_kernels.py::test_head_forward_backward); the trainer test holds the
+north-star loss tolerance (1e-4) against the CPU oracle."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+TERMS = {"f32x9": 9, "f32x6": 6}
+dev = "cuda"
+
+
+def C():
+    import recommenders.hip as h
+    return h
+
+
+def _u8(n):
+    return torch.empty(int(n), dtype=torch.uint8, device=dev)
+
+
+def run_flash(h, W, b, tgt, terms, nsplit, lo=0, lse_global=None):
+    """Every stage of the fused head through the C ABI; pass 2 in its
+    gradient-only mode (dW_out / db_out)."""
+    call, st = C().call, C().stream_ptr()
+    B, HF = h.shape
+    A = W.shape[0]
+    hb, wb = call("rg_head_plane_bytes", B, HF), call("rg_head_plane_bytes", A, HF)
+    Hk, Hr, Wk, Wr = _u8(hb), _u8(hb), _u8(wb), _u8(wb)
+    bp = torch.empty((A + 31) // 32 * 32, device=dev)
+    call("rg_head_planes", h.data_ptr(), B, HF, Hk.data_ptr(), Hr.data_ptr(), None, None, st)
+    call("rg_head_planes", W.data_ptr(), A, HF, Wk.data_ptr(), Wr.data_ptr(), b.data_ptr(), bp.data_ptr(), st)
+    pm = torch.full((nsplit, B), float("nan"), device=dev)
+    pl = torch.full((nsplit, B), float("nan"), device=dev)
+    pO = torch.full((nsplit, HF, B), float("nan"), device=dev)
+    call("rg_flash_fwd", Hk.data_ptr(), Wk.data_ptr(), Wr.data_ptr(), bp.data_ptr(), B, A, HF, terms, nsplit,
+         pm.data_ptr(), pl.data_ptr(), pO.data_ptr(), st)
+    lse = torch.full((B,), float("nan"), device=dev)
+    zt = torch.full((B,), float("nan"), device=dev)
+    call("rg_flash_lse", pm.data_ptr(), pl.data_ptr(), nsplit, h.data_ptr(), W.data_ptr(), b.data_ptr(),
+         tgt.data_ptr(), lo, A, B, HF, lse.data_ptr(), zt.data_ptr(), st)
+    rows = torch.empty(B, 2, device=dev)
+    call("rg_flash_rows", (lse if lse_global is None else lse_global).data_ptr(), tgt.data_ptr(), lo, A, B,
+         rows.data_ptr(), st)
+    g = float(np.float32(1.0 / B))
+    dh = torch.full((B, HF), float("nan"), device=dev)
+    call("rg_flash_dh", pm.data_ptr(), pO.data_ptr(), rows.data_ptr(), nsplit, W.data_ptr(), g, B, HF,
+         dh.data_ptr(), st)
+    dW = torch.full((A, HF), float("nan"), device=dev)
+    db = torch.full((A,), float("nan"), device=dev)
+    call("rg_flash_dw_adam", Hk.data_ptr(), Hr.data_ptr(), Wk.data_ptr(), bp.data_ptr(), rows.data_ptr(), g, B, A,
+         HF, terms, None, None, None, None, None, None, None, dW.data_ptr(), db.data_ptr(), st)
+    torch.cuda.synchronize()
+    return {k: v.cpu().double() for k, v in dict(lse=lse, zt=zt, dh=dh, dW=dW, db=db).items()}
+
+
+def fp64_reference(h, W, b, tgt):
+    Wr = W.double().requires_grad_(True)
+    br = b.double().requires_grad_(True)
+    hr = h.double().requires_grad_(True)
+    Z = hr @ Wr.t() + br
+    torch.nn.functional.cross_entropy(Z, tgt).backward()
+    Z = Z.detach()
+    return dict(Z=Z, lse=torch.logsumexp(Z, 1), zt=Z.gather(1, tgt[:, None])[:, 0], dh=hr.grad, dW=Wr.grad,
+                db=br.grad)
+
+
+def inputs(B, A, HF, seed):
+    g = torch.Generator().manual_seed(seed)
+    h = torch.randn(B, HF, generator=g) * 0.5
+    W = torch.randn(A, HF, generator=g) * 0.1
+    b = torch.randn(A, generator=g) * 0.1
+    tgt = torch.randint(0, A, (B,), generator=g)
+    return h, W, b, tgt
+
+
+# (B, A, HF, nsplit): partial 256-row workgroups (96, 288), ragged last item
+# chunk (A % 32 != 0), empty splits (512 × 2077 with 64 splits), split counts
+# with and without the XCD reorder (total workgroups % 8)
+@pytest.mark.parametrize("precision", ["f32x9", "f32x6"])
+@pytest.mark.parametrize("B,A,HF,nsplit", [(64, 1000, 32, 8), (128, 3001, 64, 16), (256, 4133, 128, 8),
+                                           (512, 2077, 128, 64), (96, 777, 128, 3), (288, 50000, 128, 16)])
+def test_flash_head_matches_fp64(precision, B, A, HF, nsplit):
+    h, W, b, tgt = inputs(B, A, HF, B + A + HF)
+    o = run_flash(h.to(dev), W.to(dev), b.to(dev), tgt.to(dev), TERMS[precision], nsplit)
+    r = fp64_reference(h, W, b, tgt)
+    torch.testing.assert_close(o["lse"], r["lse"], rtol=0, atol=2e-5)
+    torch.testing.assert_close(o["lse"] - o["zt"], r["lse"] - r["zt"], rtol=0, atol=2e-5)  # per-row CE
+    torch.testing.assert_close(o["dh"], r["dh"], rtol=0, atol=1e-6)
+    torch.testing.assert_close(o["dW"], r["dW"], rtol=0, atol=1e-7)
+    torch.testing.assert_close(o["db"], r["db"], rtol=0, atol=1e-7)
+
+
+def test_flash_head_item_shard():
+    """One rank's item shard [lo, hi): local lse and owner-only target logit;
+    the backward with the all-rank lse gives the shard's part of dh and its
+    rows of dW / db (recommenders/hip/sharded.py)."""
+    B, A, HF = 128, 5000, 64
+    lo, hi = 1800, 3900
+    h, W, b, tgt = inputs(B, A, HF, 77)
+    r = fp64_reference(h, W, b, tgt)
+    o = run_flash(h.to(dev), W[lo:hi].contiguous().to(dev), b[lo:hi].contiguous().to(dev), tgt.to(dev), 6, 8,
+                  lo=lo, lse_global=r["lse"].float().to(dev))
+    torch.testing.assert_close(o["lse"], torch.logsumexp(r["Z"][:, lo:hi], 1), rtol=0, atol=2e-5)
+    own = (tgt >= lo) & (tgt < hi)
+    assert 0 < int(own.sum()) < B
+    torch.testing.assert_close(o["zt"], torch.where(own, r["zt"], torch.zeros_like(r["zt"])), rtol=0, atol=1e-5)
+    P = torch.softmax(r["Z"], 1)
+    P[torch.arange(B), tgt] -= 1.0
+    P /= B
+    torch.testing.assert_close(o["dh"], P[:, lo:hi] @ W[lo:hi].double(), rtol=0, atol=1e-6)
+    torch.testing.assert_close(o["dW"], r["dW"][lo:hi], rtol=0, atol=1e-7)
+    torch.testing.assert_close(o["db"], r["db"][lo:hi], rtol=0, atol=1e-7)
+
+
+@pytest.mark.parametrize("precision", ["f32x9", "f32x6"])
+def test_flash_trainer_matches_oracle(precision):
+    """GRU4Rec with the full softmax at C2 widths (H 128, L 50), scaled down, on
+    the fused head: same loss / weight tolerances as the native path
+    (test_gpu_supervised.py::test_gru4rec_matches_oracle_medium)."""
+    from oracle.models import OracleSupervised
+    from recommenders.data_utils.synthetic import SessionStream
+    from recommenders.models.GRU4Rec.model import GRU4Rec_trainer
+    E = H = 128
+    N, L, B = 50000, 50, 1024
+    cfg = dict(hidden_dim=H, embedding_dim=E, gru_layers=1, train_pad_embed=True, use_packed_seq=True,
+               learning_rate=0.005, item_num=N, state_size=L, action_dim=N)
+    torch.set_num_threads(8)
+    orc = OracleSupervised(kind="gru4rec", **cfg)
+    tr = GRU4Rec_trainer(device="cuda", matmul_precision=precision, **cfg)
+    assert tr.gru_model.heads["output"].flash_terms(B) == TERMS[precision]
+    st = SessionStream(N, L, B * 3, seed=9)
+    for i in range(3):
+        s, a, r, sn, ln, nln, e = st.batch(i, B)
+        lo = orc.step(s, a, ln)
+        lg = tr.train_step(s, a, ln)
+        assert abs(lo - lg) < 1e-4, (i, lo, lg)
+    sd_o = orc.net.state_dict()
+    for k, v in tr.gru_model.state_dict().items():
+        d = (v.cpu() - sd_o[k]).abs()
+        assert float(d.max()) <= 2 * cfg["learning_rate"] + 1e-5, k
+        assert float((d > 1e-4).float().mean()) < 1e-3, (k, float((d > 1e-4).float().mean()))
