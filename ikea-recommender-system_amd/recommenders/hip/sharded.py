@@ -47,17 +47,24 @@ def _sharded_ce_forward(net, head, H_all, a_all, st, want_argmax=False):
     comm = net.comm
     W_, HF = comm.world, net.hf
     Bg = H_all.shape[0]
-    w = head.ws("main", Bg, True)
-    with region("head_fwd"):
-        call("rg_head_fwd", H_all.data_ptr(), head.W.p.data_ptr(), head.b.p.data_ptr(), Bg, head.A, HF,
-             w.ZT.data_ptr(), w.ldz, w.pmax.data_ptr(), w.psum.data_ptr(), w.parg.data_ptr(), 1, st)
-    call("rg_lse_combine", w.pmax.data_ptr(), w.psum.data_ptr(), w.parg.data_ptr(), Bg, w.nJ, w.work.data_ptr(),
-         None, 0, None, head.A, w.lse.data_ptr(), w.amax.data_ptr() if want_argmax else None, None,
-         w.mx.data_ptr() if want_argmax else None, st)
-    zt = _buf(net, "zt", (Bg,))
-    tgt_loc = _buf(net, "tgt_loc", (Bg,), torch.int64)
-    call("rg_shard_targets", w.ZT.data_ptr(), w.ldz, a_all.data_ptr(), head.lo, head.hi, Bg, zt.data_ptr(),
-         tgt_loc.data_ptr(), st)
+    terms = 0 if want_argmax else head.flash_terms(Bg)
+    if terms:
+        # fused split-bf16 head (csrc/head_flash.hip): local lse and the
+        # owner's target logit, no logits stored; targets stay global ids
+        w = head.flash_forward(H_all, a_all, "main", terms)
+        zt, tgt_loc = w.zt, a_all
+    else:
+        w = head.ws("main", Bg, True)
+        with region("head_fwd"):
+            call("rg_head_fwd", H_all.data_ptr(), head.W.p.data_ptr(), head.b.p.data_ptr(), Bg, head.A, HF,
+                 w.ZT.data_ptr(), w.ldz, w.pmax.data_ptr(), w.psum.data_ptr(), w.parg.data_ptr(), 1, st)
+        call("rg_lse_combine", w.pmax.data_ptr(), w.psum.data_ptr(), w.parg.data_ptr(), Bg, w.nJ, w.work.data_ptr(),
+             None, 0, None, head.A, w.lse.data_ptr(), w.amax.data_ptr() if want_argmax else None, None,
+             w.mx.data_ptr() if want_argmax else None, st)
+        zt = _buf(net, "zt", (Bg,))
+        tgt_loc = _buf(net, "tgt_loc", (Bg,), torch.int64)
+        call("rg_shard_targets", w.ZT.data_ptr(), w.ldz, a_all.data_ptr(), head.lo, head.hi, Bg, zt.data_ptr(),
+             tgt_loc.data_ptr(), st)
     with region("comm_lse"):
         lse_r = comm.all_gather(_buf(net, "lse_r", (W_ * Bg,)), w.lse)
         comm.all_reduce(zt)
@@ -71,6 +78,9 @@ def _sharded_ce_forward(net, head, H_all, a_all, st, want_argmax=False):
 def _sharded_ce_dh(net, head, w, lse, tgt_loc, dH_all, st):
     """dH_all (world·B × HF) := dZ · W_shard for every gathered row."""
     Bg = dH_all.shape[0]
+    if getattr(w, "terms", 0):  # fused head: tgt_loc holds the global target ids
+        head.flash_dh(w, tgt_loc, lse, _f32(1.0 / Bg), dH_all)
+        return
     with region("head_dh"):
         n = call("rg_head_dh", w.ZT.data_ptr(), w.ldz, lse.data_ptr(), tgt_loc.data_ptr(), _f32(1.0 / Bg),
                  head.W.p.data_ptr(), Bg, head.A, net.hf, w.dh_splits, w.dh_slabs.data_ptr(), st)
@@ -79,6 +89,9 @@ def _sharded_ce_dh(net, head, w, lse, tgt_loc, dH_all, st):
 
 def _sharded_ce_dw_adam(net, head, w, lse, tgt_loc, H_all, adam6, st):
     Bg = H_all.shape[0]
+    if getattr(w, "terms", 0):
+        head.flash_dw_adam(w, _f32(1.0 / Bg), adam6)
+        return
     with region("head_dw_adam"):
         call("rg_head_dw_adam", w.ZT.data_ptr(), w.ldz, lse.data_ptr(), tgt_loc.data_ptr(), _f32(1.0 / Bg),
              H_all.data_ptr(), Bg, head.A, net.hf, head.W.p.data_ptr(), head.W.m.data_ptr(), head.W.v.data_ptr(),
