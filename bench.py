@@ -56,7 +56,11 @@ def parse():
     ap.add_argument("--config", choices=["c2", "c3"], default="c2",
                     help="c2: headline GRU4Rec full softmax; c3: BidirGRU4Rec with sampled softmax")
     ap.add_argument("--negatives", type=int, default=2048)
-    ap.add_argument("--precision", choices=["f32", "f32x9", "f32x6"], default="f32",
+    # f32x6 (default): fp32 operands split exactly into three bf16 planes, the six
+    # plane products above 2^-24 relative on bf16 MFMAs, fp32 accumulation;
+    # tests/test_gpu_flash_head.py::test_flash_error_is_fp32_class measures it
+    # against fp64 next to the native fp32-MFMA path ("f32")
+    ap.add_argument("--precision", choices=["f32", "f32x9", "f32x6"], default="f32x6",
                     help="head GEMM arithmetic (hip/engine.py SPLIT_TERMS): native fp32 MFMA or split-bf16")
     ap.add_argument("--no-target", action="store_true", help="skip the north-star gather+sampled-logits side run")
     return ap.parse_args()

@@ -338,7 +338,8 @@ __global__ __launch_bounds__(FL_T) void k_flash_dw(const bf16x8* __restrict__ Hk
       for (int s = 0; s < NS; ++s)
         sa = mfma_split<NT>(sk[buf][s * 192 + lane], sk[buf][s * 192 + 64 + lane], sk[buf][s * 192 + 128 + lane],
                             wk[s][0], wk[s][1], wk[s][2], sa);
-      // dZ for (row acc32_row(r, hh), item l32)
+      // dZ for (row acc32_row(r, hh), item l32); db summed per chunk first
+      float cdb = 0.f;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const f4 i0 = *reinterpret_cast<const f4*>(&si[buf][8 * q + 4 * hh]);
@@ -350,9 +351,10 @@ __global__ __launch_bounds__(FL_T) void k_flash_dw(const bf16x8* __restrict__ Hk
           const float e = __builtin_amdgcn_exp2f(fmaf(sa[4 * q + u] + bj, L2E, -lse2));
           const float p = g * (e - (tb == item ? 1.f : 0.f));
           sa[4 * q + u] = p;
-          dbs += p;
+          cdb += p;
         }
       }
+      dbs += cdb;
       bf16x8 q0[2], q1[2], q2[2];
 #pragma unroll
       for (int s = 0; s < 2; ++s)
