@@ -165,15 +165,30 @@ __global__ __launch_bounds__(FL_T) void k_flash_fwd(const bf16x8* __restrict__ H
   for (int t = 0; t < NTL; ++t) o[t] = f16v{};
   float m = NEG_INF, l = 0.f;
   __syncthreads();
+#ifdef FL_DIAG_PRIO
+  if (w >= 4) __builtin_amdgcn_s_setprio(1);
+#endif
   for (int c = 0; c < nch; ++c) {
     const int buf = c & 1;
     if (c + 1 < nch) issue(c0 + c + 1, buf ^ 1);
     if (active) {
+#ifndef FL_ACC2
       f16v sa = {};
 #pragma unroll
       for (int s = 0; s < NS; ++s)
         sa = mfma_split<NT>(sk[buf][s * 192 + lane], sk[buf][s * 192 + 64 + lane], sk[buf][s * 192 + 128 + lane],
                             hk[s][0], hk[s][1], hk[s][2], sa);
+#else
+      f16v sa = {}, sb2 = {};
+#pragma unroll
+      for (int s = 0; s < NS; s += 2) {
+        sa = mfma_split<NT>(sk[buf][s * 192 + lane], sk[buf][s * 192 + 64 + lane], sk[buf][s * 192 + 128 + lane],
+                            hk[s][0], hk[s][1], hk[s][2], sa);
+        sb2 = mfma_split<NT>(sk[buf][(s + 1) * 192 + lane], sk[buf][(s + 1) * 192 + 64 + lane],
+                             sk[buf][(s + 1) * 192 + 128 + lane], hk[s + 1][0], hk[s + 1][1], hk[s + 1][2], sb2);
+      }
+      sa += sb2;
+#endif
       // logits in log2 units (item acc32_row(r, hh) of the chunk, row l32)
       float cm = NEG_INF;
 #pragma unroll
@@ -217,7 +232,9 @@ __global__ __launch_bounds__(FL_T) void k_flash_fwd(const bf16x8* __restrict__ H
           o[t] = mfma_split<NT>(sr[buf][e], sr[buf][e + 64], sr[buf][e + 128], q0[s], q1[s], q2[s], o[t]);
         }
     }
+#ifndef FL_DIAG_NOSYNC
     __syncthreads();
+#endif
   }
   if (!active) return;
   l += __shfl_xor(l, 32);
@@ -329,6 +346,9 @@ __global__ __launch_bounds__(FL_T) void k_flash_dw(const bf16x8* __restrict__ Hk
   for (int t = 0; t < NTL; ++t) dw[t] = f16v{};
   float dbs = 0.f;
   __syncthreads();
+#ifdef FL_DIAG_PRIO
+  if (w >= 4) __builtin_amdgcn_s_setprio(1);
+#endif
   for (int c = 0; c < nch; ++c) {
     const int buf = c & 1;
     if (c + 1 < nch) issue(c + 1, buf ^ 1);
@@ -368,7 +388,9 @@ __global__ __launch_bounds__(FL_T) void k_flash_dw(const bf16x8* __restrict__ Hk
           dw[t] = mfma_split<NT>(q0[s], q1[s], q2[s], sr[buf][e], sr[buf][e + 64], sr[buf][e + 128], dw[t]);
         }
     }
+#ifndef FL_DIAG_NOSYNC
     __syncthreads();
+#endif
   }
   if (!active) return;
   dbs += __shfl_xor(dbs, 32);
