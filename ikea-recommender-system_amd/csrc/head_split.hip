@@ -75,7 +75,7 @@ __global__ __launch_bounds__(64 * HX_WAVES_OF(HF)) void k_head_fwd_x(const bf16x
                                                                      float* __restrict__ ZT, int64_t ldz,
                                                                      float* __restrict__ pmax,
                                                                      float* __restrict__ psum,
-                                                                     int32_t* __restrict__ parg) {
+                                                                     int32_t* __restrict__ parg, int rpb) {
   constexpr int NW = HX_WAVES_OF(HF);
   constexpr int NS = HF / 16;
   constexpr int NE = NS * 3 * 64;  // 16-B fragments per 32-row chunk
@@ -86,7 +86,11 @@ __global__ __launch_bounds__(64 * HX_WAVES_OF(HF)) void k_head_fwd_x(const bf16x
   const int jw = blockIdx.x * (32 * NW) + 32 * w;
   const bool active = jw < A;
   const bool full = jw + 32 <= A;
-  const int nch = B / 32;  // B % 32 == 0
+  // rows [rbase, rbase + 32·nch) of this workgroup (grid.y splits B so that a
+  // small A — a sampled head's negatives — still fills the chip)
+  const int rbase = blockIdx.y * rpb;
+  const int nch = min(rpb, B - rbase) / 32;  // B, rpb % 32 == 0
+  const bf16x8* __restrict__ Hb = Hp + (int64_t)(rbase / 32) * NE;
   // chunk 0's fragments first (independent of W), then this wave's W rows
   bf16x8 st[EPT];
   // the scheduling barrier keeps the prefetch at the top of the chunk (left
@@ -99,7 +103,7 @@ __global__ __launch_bounds__(64 * HX_WAVES_OF(HF)) void k_head_fwd_x(const bf16x
 #pragma unroll
     for (int q = 0; q < EPT; ++q) {
       const int e = tid + 64 * NW * q;
-      if (e < NE) st[q] = Hp[(int64_t)c * NE + e];
+      if (e < NE) st[q] = Hb[(int64_t)c * NE + e];
     }
     __builtin_amdgcn_sched_barrier(0);
   };
@@ -139,9 +143,9 @@ __global__ __launch_bounds__(64 * HX_WAVES_OF(HF)) void k_head_fwd_x(const bf16x
     for (int j = 0; j < NS; ++j) split3x8(wl[j][0], wl[j][1], a0[j], a1[j], a2[j]);
   }
   __syncthreads();
-  float* pm = pmax + (int64_t)(jw / RG_PBLK) * B + l32;
-  float* ps = WS ? psum + (int64_t)(jw / RG_PBLK) * B + l32 : nullptr;
-  int32_t* pa = parg + (int64_t)(jw / RG_PBLK) * B + l32;
+  float* pm = pmax + (int64_t)(jw / RG_PBLK) * B + rbase + l32;
+  float* ps = WS ? psum + (int64_t)(jw / RG_PBLK) * B + rbase + l32 : nullptr;
+  int32_t* pa = parg ? parg + (int64_t)(jw / RG_PBLK) * B + rbase + l32 : nullptr;
   // Zᵀ stores through a buffer descriptor over this wave's item rows that
   // exist: stores of items past A fall outside num_records and are dropped,
   // so the epilogue has no per-lane branch (the stores sit between MFMAs)
@@ -172,7 +176,7 @@ __global__ __launch_bounds__(64 * HX_WAVES_OF(HF)) void k_head_fwd_x(const bf16x
 #ifndef HX_DIAG_NOSTORE
           if (SZ)
             __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(z), zrs, zlane,
-                                                  ((r & 3) + 8 * (r >> 2)) * zrow4 + cc * 128, 0);
+                                                  ((r & 3) + 8 * (r >> 2)) * zrow4 + (rbase + 32 * cc) * 4, 0);
 #endif
           const bool gt = z > em;
           em = gt ? z : em;
@@ -193,7 +197,7 @@ __global__ __launch_bounds__(64 * HX_WAVES_OF(HF)) void k_head_fwd_x(const bf16x
     if (half == 0) {
       pm[cc * 32] = em;
       if (WS) ps[cc * 32] = es;
-      pa[cc * 32] = ea;
+      if (pa) pa[cc * 32] = ea;
     }
     em = NEG_INF;
     es = 0.f;
@@ -281,33 +285,33 @@ extern "C" int64_t rg_head_work_bytes(int B, int HF) {
   return (int64_t)B * HF * 6;
 }
 
-// rg_head_fwd on split-bf16 MFMAs (terms 9 / 6).  Same outputs (Zᵀ, per
-// (RG_PBLK items, row) max / Σexp / argmax partials); B % 32 == 0.
-extern "C" int rg_head_fwd_x(const float* h, const float* W, const float* bias, int B, int A, int HF, int terms,
-                             float* ZT, int64_t ldz, float* pmax, float* psum, int32_t* parg, int want_sum,
-                             void* work, hipStream_t stream) {
-  if (B <= 0 || A <= 0 || (B % 32) || work == nullptr) return RG_ERR_ARG;
+// rg_head_fwd on split-bf16 MFMAs (terms 9 / 6) from h's planes (k_split_rows
+// layout).  Same outputs (Zᵀ, per (RG_PBLK items, row) max / Σexp / argmax
+// partials; parg optional); rpb = rows per workgroup (multiple of 32; B for
+// one row block, less to spread a small A over the chip).  B % 32 == 0.
+extern "C" int rg_head_fwd_xp(const void* hplanes, const float* W, const float* bias, int B, int A, int HF,
+                              int terms, int rpb, float* ZT, int64_t ldz, float* pmax, float* psum, int32_t* parg,
+                              int want_sum, hipStream_t stream) {
+  if (B <= 0 || A <= 0 || (B % 32) || rpb <= 0 || (rpb % 32) || hplanes == nullptr) return RG_ERR_ARG;
   if (ZT && ldz < B) return RG_ERR_ARG;
   if (want_sum && psum == nullptr) return RG_ERR_ARG;
   if (terms != 6 && terms != 9) return RG_ERR_ARG;
-  bf16x8* Hp = reinterpret_cast<bf16x8*>(work);
+  const bf16x8* Hp = reinterpret_cast<const bf16x8*>(hplanes);
   const int nw = HX_WAVES_OF(HF);
-  const dim3 gs((unsigned)(((int64_t)B * (HF / 8) + 255) / 256));
-  const dim3 gf((A + 32 * nw - 1) / (32 * nw));
+  const dim3 gf((A + 32 * nw - 1) / (32 * nw), (B + rpb - 1) / rpb);
 #define HXL(HFV, NTV, SZV, WSV)                                                                                \
   hipLaunchKernelGGL((k_head_fwd_x<HFV, NTV, SZV, WSV>), gf, dim3(64 * nw), 0, stream, Hp, W, bias, B, A, ZT, \
-                     ldz, pmax, psum, parg)
+                     ldz, pmax, psum, parg, rpb)
 #define HXT(HFV, NTV)                          \
   if (ZT && want_sum) HXL(HFV, NTV, true, true); \
   else if (ZT) HXL(HFV, NTV, true, false);       \
   else if (want_sum) HXL(HFV, NTV, false, true); \
   else HXL(HFV, NTV, false, false);
-#define HXH(HFV)                                                                                  \
-  hipLaunchKernelGGL(k_split_rows<HFV>, gs, dim3(256), 0, stream, h, B, Hp);                     \
-  if (terms == 9) {                                                                               \
-    HXT(HFV, 9)                                                                                   \
-  } else {                                                                                        \
-    HXT(HFV, 6)                                                                                   \
+#define HXH(HFV)  \
+  if (terms == 9) { \
+    HXT(HFV, 9)   \
+  } else {        \
+    HXT(HFV, 6)   \
   }
   switch (HF) {
     case 32: HXH(32); break;
@@ -321,4 +325,23 @@ extern "C" int rg_head_fwd_x(const float* h, const float* W, const float* bias, 
 #undef HXL
   RG_LAUNCH_CHECK();
   return RG_OK;
+}
+
+// rg_head_fwd on split-bf16 MFMAs (terms 9 / 6).  Same outputs (Zᵀ, per
+// (RG_PBLK items, row) max / Σexp / argmax partials); B % 32 == 0.
+extern "C" int rg_head_fwd_x(const float* h, const float* W, const float* bias, int B, int A, int HF, int terms,
+                             float* ZT, int64_t ldz, float* pmax, float* psum, int32_t* parg, int want_sum,
+                             void* work, hipStream_t stream) {
+  if (B <= 0 || A <= 0 || (B % 32) || work == nullptr) return RG_ERR_ARG;
+  if (terms != 6 && terms != 9) return RG_ERR_ARG;
+  bf16x8* Hp = reinterpret_cast<bf16x8*>(work);
+  const dim3 gs((unsigned)(((int64_t)B * (HF / 8) + 255) / 256));
+  switch (HF) {
+    case 32: hipLaunchKernelGGL(k_split_rows<32>, gs, dim3(256), 0, stream, h, B, Hp); break;
+    case 64: hipLaunchKernelGGL(k_split_rows<64>, gs, dim3(256), 0, stream, h, B, Hp); break;
+    case 128: hipLaunchKernelGGL(k_split_rows<128>, gs, dim3(256), 0, stream, h, B, Hp); break;
+    case 256: hipLaunchKernelGGL(k_split_rows<256>, gs, dim3(256), 0, stream, h, B, Hp); break;
+    default: return RG_ERR_SHAPE;
+  }
+  return rg_head_fwd_xp(Hp, W, bias, B, A, HF, terms, B, ZT, ldz, pmax, psum, parg, want_sum, stream);
 }

@@ -206,20 +206,15 @@ __global__ __launch_bounds__(256) void k_sampled_fwd(const float* __restrict__ h
 //  k_sampled_prep: one thread per (row, 8-value k group) of the S negative
 //    rows and of the B rows of h.  Negatives: optionally draws the id (the
 //    k_sample_uniform stream), gathers the W row piece (coalesced: consecutive
-//    threads read consecutive 32 B of a row), writes Wg/bg (both backward
-//    GEMMs consume them) and the three bf16 planes; h rows: the planes.
-//    Planes are stored in MFMA fragment order, [32-row block][k slice][plane]
-//    [lane] × 16 B, so the GEMM reads every operand as whole 1 KB
-//    wave-instructions and never converts anything.
-//  k_sampled_fwd_xp: a workgroup owns NW·32 negatives × R batch rows.  Wave w
-//    loads its negatives' planes into VGPRs (3·HF/16 bf16x8); the
-//    workgroup's h planes are copied once into LDS [plane][slice][half][row]
-//    (conflict-free ds_read_b128 per plane and slice); one barrier, no k
-//    loop.  Chunks of 32 rows alternate two accumulator sets, so the Zᵀ
-//    stores of chunk c drain under chunk c+1's MFMAs (one set serialises
-//    them: tools/mb/mb_sampled.hip, 15.9 vs 10.5 µs at B 4096, S 2048, HF 128).
-#define SX_WAVES_OF(HF) ((HF) >= 256 ? 4 : 8)
-#define SX_R(HF) ((HF) >= 256 ? 64 : 128)
+//    threads read consecutive 32 B of a row) and writes Wg/bg (the logits
+//    kernel and both backward GEMMs consume them); h rows: the three bf16
+//    planes in MFMA fragment order, [32-row block][k slice][plane][lane] ×
+//    16 B (whole 1 KB wave-instructions, nothing converted in the GEMM).
+//  logits: rg_head_fwd_xp (csrc/head_split.hip) with the gathered negatives
+//    as the item rows — each wave splits its 32 negatives' rows into VGPR
+//    planes once and streams h's planes through an LDS ring, with Zᵀ stores
+//    and the (max, Σexp) partials in the epilogue; the rows are split over
+//    grid.y so S/(32·waves) negative groups still fill the chip.
 
 // fragment-order plane buffer: entry (block, slice j, plane p, lane)
 __device__ __forceinline__ int64_t plane_idx(int blk, int j, int p, int lane, int NS) {
@@ -265,6 +260,7 @@ __global__ __launch_bounds__(256) void k_sampled_prep(const float* __restrict__ 
     *reinterpret_cast<f4*>(dst) = lo;
     *reinterpret_cast<f4*>(dst + 4) = hi;
   }
+  if (isneg && Wp == nullptr) return;  // only h's planes are needed
   bf16x8 p0, p1, p2;
   split3x8(lo, hi, p0, p1, p2);
   bf16x8* dst = isneg ? Wp : Hp;
@@ -274,101 +270,10 @@ __global__ __launch_bounds__(256) void k_sampled_prep(const float* __restrict__ 
   dst[plane_idx(x >> 5, j, 2, lane, NS)] = p2;
 }
 
-template <int HF, int NT>
-__global__ __launch_bounds__(64 * SX_WAVES_OF(HF)) void k_sampled_fwd_xp(const bf16x8* __restrict__ Wp,
-                                                                      const bf16x8* __restrict__ Hp,
-                                                                      const float* __restrict__ bg, int B,
-                                                                      int S, float* __restrict__ ZT,
-                                                                      int64_t ldz, float* __restrict__ pmax,
-                                                                      float* __restrict__ psum) {
-  constexpr int NW = SX_WAVES_OF(HF);
-  constexpr int R = SX_R(HF);
-  constexpr int NS = HF / 16;                    // 16-wide k slices
-  constexpr int NE = (R / 32) * NS * 3 * 64;     // LDS entries
-  constexpr int EPT = (NE + 64 * NW - 1) / (64 * NW);
-  constexpr float L2E = 1.4426950408889634f;
-  __shared__ bf16x8 hs[3][NS][2][R];
-  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, half = lane >> 5, l32 = lane & 31;
-  const int jw = blockIdx.x * (32 * NW) + 32 * w;
-  const bool active = jw < S;  // S % 32 == 0: a wave's 32 negatives all exist or none
-  const int r0 = blockIdx.y * R;
-  const int nc = min(R, B - r0) / 32;  // B % 32 == 0
-  // h planes of this workgroup's rows: whole 1 KB fragments, copied in order
-  bf16x8 st[EPT];
-#pragma unroll
-  for (int q = 0; q < EPT; ++q) {
-    const int e = tid + 64 * NW * q;
-    const int c = e / (NS * 3 * 64);
-    if (e < NE && c < nc) st[q] = Hp[(int64_t)(r0 / 32) * NS * 3 * 64 + e];
-  }
-  bf16x8 a0[NS], a1[NS], a2[NS];
-  float bj[16];
-  if (active) {
-#pragma unroll
-    for (int j = 0; j < NS; ++j) {
-      a0[j] = Wp[plane_idx(jw >> 5, j, 0, lane, NS)];
-      a1[j] = Wp[plane_idx(jw >> 5, j, 1, lane, NS)];
-      a2[j] = Wp[plane_idx(jw >> 5, j, 2, lane, NS)];
-    }
-#pragma unroll
-    for (int r = 0; r < 16; ++r) bj[r] = bg[jw + acc32_row(r, half)];
-  }
-#pragma unroll
-  for (int q = 0; q < EPT; ++q) {
-    const int e = tid + 64 * NW * q;
-    const int c = e / (NS * 3 * 64);
-    if (e < NE && c < nc) {
-      const int rem = e % (NS * 3 * 64);
-      const int j = rem / (3 * 64), p = (rem / 64) % 3, ln = rem & 63;
-      hs[p][j][ln >> 5][32 * c + (ln & 31)] = st[q];
-    }
-  }
-  __syncthreads();
-  if (!active) return;  // after the only barrier
-  float* pm = pmax + (int64_t)(jw / 32) * B + r0 + l32;
-  float* ps = psum + (int64_t)(jw / 32) * B + r0 + l32;
-  float* zrow = ZT ? ZT + (int64_t)jw * ldz + r0 + l32 : nullptr;
-  auto mfmas = [&](int c, f16v& acc) __attribute__((always_inline)) {
-    acc = f16v{};
-#pragma unroll
-    for (int j = 0; j < NS; ++j) {
-      const bf16x8 b0 = hs[0][j][half][32 * c + l32];
-      const bf16x8 b1 = hs[1][j][half][32 * c + l32];
-      const bf16x8 b2 = hs[2][j][half][32 * c + l32];
-      acc = mfma_split<NT>(a0[j], a1[j], a2[j], b0, b1, b2, acc);
-    }
-  };
-  auto epilogue = [&](int c, f16v& acc) __attribute__((always_inline)) {
-    float m = -__builtin_inff(), sum = 0.f;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const float z = acc[r] + bj[r];
-      acc[r] = z;
-      if (zrow) zrow[(int64_t)acc32_row(r, half) * ldz + c * 32] = z;
-      m = fmaxf(m, z);
-    }
-    const float m2 = m * L2E;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) sum += __builtin_amdgcn_exp2f(fmaf(acc[r], L2E, -m2));
-    lse_merge(m, sum, __shfl_xor(m, 32), __shfl_xor(sum, 32));
-    if (half == 0) {
-      pm[c * 32] = m;
-      ps[c * 32] = sum;
-    }
-  };
-  f16v accA, accB;
-  int c = 0;
-  for (; c + 1 < nc; c += 2) {
-    mfmas(c, accA);
-    epilogue(c, accA);
-    mfmas(c + 1, accB);
-    epilogue(c + 1, accB);
-  }
-  if (c < nc) {
-    mfmas(c, accA);
-    epilogue(c, accA);
-  }
-}
+// split-bf16 logits kernel shared with the full-softmax head (csrc/head_split.hip)
+extern "C" int rg_head_fwd_xp(const void* hplanes, const float* W, const float* bias, int B, int A, int HF,
+                              int terms, int rpb, float* ZT, int64_t ldz, float* pmax, float* psum, int32_t* parg,
+                              int want_sum, hipStream_t stream);
 
 // bytes of scratch rg_sampled_fwd_x needs (the two plane buffers)
 extern "C" int64_t rg_sampled_work_bytes(int B, int S, int HF) {
@@ -384,7 +289,8 @@ extern "C" int rg_sampled_fwd_x(const float* h, const float* W, const float* bia
                                 uint64_t seed, uint64_t counter, int64_t A, int B, int S, int HF, int terms,
                                 float* ZT, int64_t ldz, float* pmax, float* psum, float* Wg, float* bg, void* work,
                                 hipStream_t stream) {
-  if (B <= 0 || S <= 0 || (B % 32) || (S % 32) || work == nullptr || bg == nullptr) return RG_ERR_ARG;
+  if (B <= 0 || S <= 0 || (B % 32) || (S % 32) || work == nullptr || bg == nullptr || Wg == nullptr)
+    return RG_ERR_ARG;
   if (ZT && ldz < B) return RG_ERR_ARG;
   if (draw && (A <= 0 || A > INT32_MAX)) return RG_ERR_ARG;
   if (terms != 6 && terms != 9) return RG_ERR_ARG;
@@ -392,18 +298,19 @@ extern "C" int rg_sampled_fwd_x(const float* h, const float* W, const float* bia
   bf16x8* Hp = Wp + (int64_t)S * HF / 8 * 3;
   const int64_t items = ((int64_t)S + B) * (HF / 8);
   const dim3 gp((unsigned)((items + 255) / 256));
-  const int nw = SX_WAVES_OF(HF), R = SX_R(HF);
-  const dim3 grid((S + 32 * nw - 1) / (32 * nw), (B + R - 1) / R);
+  // negatives × rows on k_head_fwd_x (csrc/head_split.hip): each wave holds
+  // 32 gathered negatives' planes in VGPRs, h's planes stream through LDS; the
+  // rows are split over grid.y so the S/(32·waves) negative groups fill the chip
+  const int nw = HF >= 256 ? 4 : 8;
+  const int ngx = (S + 32 * nw - 1) / (32 * nw);
+  const int ny = max(1, 256 / ngx);
+  // rows per workgroup (rows·negatives workgroups ≈ one per CU; the best of
+  // 32..512 swept at B 4096, S 2048: 128 at HF 128, 256 at HF 256)
+  const int rpb = ((B + ny - 1) / ny + 31) / 32 * 32;
 #define SXP(HFV)                                                                                            \
   hipLaunchKernelGGL(k_sampled_prep<HFV>, gp, dim3(256), 0, stream, h, W, bias, neg, draw, seed, counter, \
-                     (uint64_t)A, B, S, Wg, bg, Wp, Hp)
-#define SXL(HFV, NTV)                                                                                             \
-  hipLaunchKernelGGL((k_sampled_fwd_xp<HFV, NTV>), grid, dim3(64 * nw), 0, stream, Wp, Hp, bg, B, S, ZT, ldz, \
-                     pmax, psum)
-#define SXH(HFV)                 \
-  SXP(HFV);                      \
-  if (terms == 9) SXL(HFV, 9);   \
-  else SXL(HFV, 6);
+                     (uint64_t)A, B, S, Wg, bg, (bf16x8*)nullptr, Hp)
+#define SXH(HFV) SXP(HFV);
   switch (HF) {
     case 32: SXH(32); break;
     case 64: SXH(64); break;
@@ -412,10 +319,9 @@ extern "C" int rg_sampled_fwd_x(const float* h, const float* W, const float* bia
     default: return RG_ERR_SHAPE;
   }
 #undef SXH
-#undef SXL
 #undef SXP
   RG_LAUNCH_CHECK();
-  return RG_OK;
+  return rg_head_fwd_xp(Hp, Wg, bg, B, S, HF, terms, rpb, ZT, ldz, pmax, psum, nullptr, 1, stream);
 }
 
 // Number of (max, Σexp) partials per row the forward writes: 128-negative

@@ -41,6 +41,7 @@ SIGNATURES = {
     "rg_head_fwd": [P, P, P, I, I, I, P, I64, P, P, P, I, P],
     "rg_head_work_bytes": [I, I],
     "rg_head_fwd_x": [P, P, P, I, I, I, I, P, I64, P, P, P, I, P, P],
+    "rg_head_fwd_xp": [P, P, P, I, I, I, I, I, P, I64, P, P, P, I, P],
     "rg_head_plane_bytes": [I, I],
     "rg_head_planes": [P, I, I, P, P, P, P, P],
     "rg_flash_fwd": [P, P, P, P, I, I, I, I, I, P, P, P, P],

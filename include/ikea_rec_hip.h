@@ -129,6 +129,12 @@ int rg_flash_dh(const float* pm, const float* pO, const void* rowinfo, int nspli
 int rg_flash_dw_adam(const void* Hk, const void* Hr, const void* Wk, const float* bias_pad, const void* rowinfo,
                      float gscale, int B, int A, int HF, int terms, float* W, float* mW, float* vW, float* bias,
                      float* mb, float* vb, const float* adam6, float* dW_out, float* db_out, rg_stream_t stream);
+/* rg_head_fwd_x from h's planes (rg_head_work_bytes layout) with the rows split
+ * over workgroups: rpb rows per workgroup (multiple of 32), parg optional.
+ * The sampled softmax's split forward (rg_sampled_fwd_x) runs on it with the
+ * gathered negatives' rows as W (A = S). */
+int rg_head_fwd_xp(const void* hplanes, const float* W, const float* bias, int B, int A, int HF, int terms, int rpb,
+                   float* ZT, int64_t ldz, float* pmax, float* psum, int32_t* parg, int want_sum, rg_stream_t stream);
 /* partials -> lse (B), argmax (B) (torch.argmax semantics: first maximum),
  * loss_row (B) = lse - Z[a_b, b], mx (B) = the row maximum.  Every output is
  * optional.  work: 3*min(128,nJ)*B floats. */
