@@ -252,7 +252,11 @@ def main():
         roof = dict(target) if target else None
         if roof:
             roof["kernel"] = "gather + sampled_fwd"
+            # PMC HBM bytes of the same kernels per step (tools/pmc_c3.sh), committed under profiles/
+            pmc = os.path.join(HERE, "profiles", "pmc_traffic.json")
             roof["traffic"] = None
+            if os.path.exists(pmc) and (B, args.negatives, HF, args.precision) == (4096, 2048, 256, "f32x6"):
+                roof["traffic"] = json.load(open(pmc)).get("c3:gather+sampled_fwd")
     cpu = None
     if world == 1 and not args.no_cpu_baseline and args.config == "c2":
         cpu = cpu_baseline(args)
