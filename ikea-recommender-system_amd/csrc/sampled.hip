@@ -229,12 +229,16 @@ __global__ __launch_bounds__(256) void k_sampled_prep(const float* __restrict__ 
                                                       bf16x8* __restrict__ Wp, bf16x8* __restrict__ Hp) {
   constexpr int G = HF / 8;  // 8-value groups per row
   constexpr int NS = HF / 16;
+  // thread order (32-row block, group g, row in block): a wave covers 32 rows
+  // × 2 groups = one k slice, so each of its three plane stores is one
+  // contiguous 1 KB fragment (S and B are multiples of 32)
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  const int64_t nneg = (int64_t)S * G;
-  if (i >= nneg + (int64_t)B * G) return;
-  const bool isneg = i < nneg;
-  const int64_t k = isneg ? i : i - nneg;
-  const int x = (int)(k / G), g = (int)(k % G);
+  const int64_t blk = i / (32 * G);
+  const int rem = (int)(i - blk * (32 * G));
+  const int64_t nblk_neg = S / 32;
+  if (blk >= nblk_neg + B / 32) return;
+  const bool isneg = blk < nblk_neg;
+  const int x = (int)((isneg ? blk : blk - nblk_neg) * 32) + (rem & 31), g = rem >> 5;
   const int j = g >> 1, hh = g & 1;
   const float* src;
   if (isneg) {
