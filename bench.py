@@ -2,27 +2,34 @@
 """Headline benchmark: GRU4Rec training steps at 1M items, dim 128,
 seq_len <= 50, batch 4096, full-softmax logits (BASELINE.json configs[1]).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c4]
 
 metric: session-steps/sec (= batch rows × train_step calls per second, whole
 job).  One step = one ``GRU4Rec_trainer.train_step(s, a, true_len)`` on the
-MI355X (pack, gather, GRU fwd, logits + CE, backward, dense Adam over every
-parameter, loss ``.item()``), inputs already resident in HBM.
+MI355X: H2D of the batch (pinned host tensors, as a DataLoader with
+pin_memory hands them over), pack, gather, GRU fwd, logits + CE, backward,
+dense Adam over every parameter, loss ``.item()``.  Per-step wall times give
+the median / p10 / p90 beside the mean.
 
+After the timed steps the trained model is evaluated on a held-out batch
+(device top-20, HR@20 / NDCG@20).  On rank 0 at N=1 the CPU leg times the
+oracle (the reference's PyTorch-CPU math, oracle/) on a bounded sample of the
+same workload, and scores a 256-row slice of the held-out batch with the
+reference CPU math on the GPU-trained weights: its canonical top-20 lists and
+HR@20 / NDCG@20 next to the device's ("hr_ndcg_parity").
+
+Configs: c2 (headline), c3 (BidirGRU4Rec, 2048 sampled negatives),
+c4 (SMORL: GRU4Rec trunk + supervised head + 3 Q heads, 3-reward double-Q).
 Multi-GPU (torch.distributed.run, one rank per GPU, RCCL): weak scaling, each
-rank trains its own 4096-row batch shard; the trunk is replicated (gradient
-all-reduce), the output layer is sharded over ranks by item id (all-gather h,
-LSE merge, reduce-scatter dh) — one optimizer step over the global batch
-(see DESIGN.md §5).
-
-Beside it, on rank 0 at N=1 only: the CPU oracle (the reference's PyTorch-CPU
-math, oracle/) timed on a bounded sample of the same workload.
+rank trains its own 4096-row batch shard, item tables sharded over the ranks
+(DESIGN.md §5).
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import platform
 import sys
 import time
 
@@ -37,13 +44,14 @@ ITEMS, DIM, SEQ, BATCH = 1_000_000, 128, 50, 4096
 FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: dense f32 MFMA (= f32 vector peak)
 BF16_MFMA_PEAK_TFLOPS = 2500.0  # dense bf16 MFMA (no sparsity)
 HBM_PEAK_GBS = 8000.0
+EVAL_K = 20
 
 
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--items", type=int, default=ITEMS)
     ap.add_argument("--dim", type=int, default=DIM)
     ap.add_argument("--seq", type=int, default=SEQ)
@@ -52,20 +60,36 @@ def parse():
     ap.add_argument("--cpu-steps", type=int, default=6)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-timing", action="store_true")
+    ap.add_argument("--no-eval", action="store_true")
     ap.add_argument("--force-shard", action="store_true", help="item-sharded path even at world 1 (test)")
-    ap.add_argument("--config", choices=["c2", "c3"], default="c2",
-                    help="c2: headline GRU4Rec full softmax; c3: BidirGRU4Rec with sampled softmax")
+    ap.add_argument("--config", choices=["c2", "c3", "c4"], default="c2",
+                    help="c2: headline GRU4Rec full softmax; c3: BidirGRU4Rec with sampled softmax; "
+                         "c4: SMORL 3-reward double-Q")
     ap.add_argument("--negatives", type=int, default=2048)
     # f32x6 (default): fp32 operands split exactly into three bf16 planes, the six
     # plane products above 2^-24 relative on bf16 MFMAs, fp32 accumulation;
     # tests/test_gpu_flash_head.py::test_flash_error_is_fp32_class measures it
-    # against fp64 next to the native fp32-MFMA path ("f32")
+    # against fp64 next to the native fp32-MFMA path ("f32"), and
+    # tests/test_gpu_model_parity.py holds both to the oracle's top-20 / HR@20
     ap.add_argument("--precision", choices=["f32", "f32x9", "f32x6"], default="f32x6",
                     help="head GEMM arithmetic (hip/engine.py SPLIT_TERMS): native fp32 MFMA or split-bf16")
     ap.add_argument("--no-target", action="store_true", help="skip the north-star gather+sampled-logits side run")
+    ap.add_argument("--no-native-side", action="store_true", help="skip the native-f32 side run")
     return ap.parse_args()
 
 
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor() or "unknown"
+
+
+# ------------------------------------------------------------ CPU leg ------
 def cpu_baseline(args):
     """The reference's per-step math on PyTorch-CPU (oracle/, restatement pinned
     to the reference's golden vectors) on a bounded sample: same item count,
@@ -80,18 +104,44 @@ def cpu_baseline(args):
     st = SessionStream(args.items, args.seq, B * (args.cpu_steps + 1), seed=2)
     b = st.batch(0, B)
     orc.step(b[0], b[1], b[4])  # warm-up
-    t0 = time.perf_counter()
+    times = []
     for i in range(1, args.cpu_steps + 1):
         b = st.batch(i, B)
+        t0 = time.perf_counter()
         orc.step(b[0], b[1], b[4])
-    dt = time.perf_counter() - t0
+        times.append(time.perf_counter() - t0)
+    dt = float(np.sum(times))
     return {"value": round(B * args.cpu_steps / dt, 2), "unit": "session-steps/sec", "cores": threads,
-            "kind": "port",
+            "cpu_model": cpu_model(), "kind": "port",
+            "median_ms_per_step": round(float(np.median(times)) * 1e3, 1),
             "sample": (f"oracle (reference PyTorch-CPU math) GRU4Rec {args.items} items dim{args.dim} "
                        f"L<={args.seq}, batch {B}, {args.cpu_steps} timed steps after 1 warm-up, "
                        f"{threads} threads, {dt:.1f} s")}
 
 
+def cpu_eval_parity(net, ev, dev_idx, rows=256):
+    """Reference CPU math (oracle.Net: nn.Embedding, packed nn.GRU, nn.Linear)
+    on the GPU-trained weights for ``rows`` held-out rows: canonical top-20
+    lists and HR@20 / NDCG@20 beside the device's."""
+    from oracle import metrics as om
+    from oracle.models import Net
+    s, a, ln = ev[0][:rows], ev[1][:rows], ev[2][:rows]
+    cpu = Net("gru4rec", net.item_num, net.action_dim, net.embedding_dim, net.hidden_dim)
+    cpu.load_state_dict({k: v.detach().cpu() for k, v in net.state_dict().items()})
+    cpu.eval()
+    with torch.no_grad():
+        z = cpu(s, ln).numpy()
+    ref = om.canonical_topk_fast(z, EVAL_K)
+    got = dev_idx[:rows]
+    h_c, n_c = om.hits_from_lists(ref, a.numpy(), [EVAL_K])
+    h_g, n_g = om.hits_from_lists(got, a.numpy(), [EVAL_K])
+    same = int((ref == got).all(1).sum())
+    return {"rows": rows, "top20_rows_identical": same, "hr20_cpu": h_c[0] / rows, "hr20_gpu": h_g[0] / rows,
+            "ndcg20_cpu": round(n_c[0] / rows, 6), "ndcg20_gpu": round(n_g[0] / rows, 6),
+            "note": "reference CPU math on the GPU-trained weights vs the device top-20 (canonical ties)"}
+
+
+# ------------------------------------------------------------ GPU runs -----
 def make_trainer(cfg, args, dev, shard):
     from recommenders.models.BidirGRU4Rec.model import BidirGRU4Rec_trainer
     from recommenders.models.GRU4Rec.model import GRU4Rec_trainer
@@ -100,32 +150,58 @@ def make_trainer(cfg, args, dev, shard):
                   learning_rate=0.01, item_num=N, state_size=L, action_dim=N, device=dev)
     if cfg == "c2":
         return GRU4Rec_trainer(shard_items=shard, matmul_precision=args.precision, **common)
+    if cfg == "c2native":
+        return GRU4Rec_trainer(matmul_precision="f32", **common)
     if cfg == "c2s":   # GRU4Rec at C2 shapes with the sampled head (north-star target step)
         return GRU4Rec_trainer(n_negatives=args.negatives, matmul_precision=args.precision, **common)
     if cfg == "c3":
         return BidirGRU4Rec_trainer(dropout=0.0, n_negatives=args.negatives, matmul_precision=args.precision,
                                     **common)
+    if cfg == "c4":
+        from recommenders.data_utils.synthetic import unpopular_items
+        from recommenders.models.SMORL.smorl_gru import SMORL_trainer
+        common.pop("device")
+        g = torch.Generator().manual_seed(7)
+        div = torch.randn(N + 1, 64, generator=g) * 0.01     # frozen div table
+        return SMORL_trainer(padding_pos="end", gamma=0.5, q_weights=[1.0, 1.0, 1.0], alpha=1.0, div_embedding=div,
+                             unpopular_actions_set=unpopular_items(args.item_counts), topk_div=1, topk_nov=1,
+                             device=dev, shard_items=shard, matmul_precision=args.precision, **common)
     raise ValueError(cfg)
 
 
-def timed_run(tr, batches, warmup, steps, world, kernel_timing):
-    """W untimed steps, then K steps between barrier + synchronize; max over ranks."""
+def step_args(cfg, b):
+    s, a, r, sn, ln, nln, e = b
+    if cfg == "c4":
+        return (s, a, r, sn, ln, nln, e)
+    return (s, a, ln)
+
+
+def timed_run(tr, batches, warmup, steps, world, kernel_timing, cfg):
+    """W untimed steps, then K steps between barrier + synchronize; max over ranks.
+    Batches are host (pinned) tensors: the H2D copy is inside every step."""
     from recommenders.hip.timing import KernelTimer, timing
     for i in range(warmup):
-        tr.train_step(*batches[i])
+        tr.train_step(*step_args(cfg, batches[i]))
     timer = KernelTimer()
     if world > 1:
         torch.distributed.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    losses = []
-    if kernel_timing:
-        with timing(timer):
-            for i in range(warmup, warmup + steps):
-                losses.append(tr.train_step(*batches[i]))
-    else:
+    losses, per_step = [], []
+    ctx = timing(timer) if kernel_timing else None
+    if ctx is not None:
+        ctx.__enter__()
+    try:
+        t_prev = t0
         for i in range(warmup, warmup + steps):
-            losses.append(tr.train_step(*batches[i]))
+            out = tr.train_step(*step_args(cfg, batches[i]))   # ends with .item(): a device sync
+            t_now = time.perf_counter()
+            per_step.append(t_now - t_prev)
+            t_prev = t_now
+            losses.append(out[0] if isinstance(out, tuple) else out)
+    finally:
+        if ctx is not None:
+            ctx.__exit__(None, None, None)
     torch.cuda.synchronize()
     if world > 1:
         torch.distributed.barrier()
@@ -139,7 +215,20 @@ def timed_run(tr, batches, warmup, steps, world, kernel_timing):
     kern = {}
     if kernel_timing:
         kern = {k: round(float(np.mean(v)), 4) for k, v in timer.elapsed_ms().items()}
-    return dt, losses, kern
+    return dt, losses, kern, per_step
+
+
+def device_eval(net, ev):
+    """Device top-20 and HR@20 / NDCG@20 of the trained model on the held-out batch."""
+    from recommenders.hip.evalpath import eval_batch
+    s, a, ln = ev
+    net.eval()
+    r = eval_batch(net, s, ln, a, K=EVAL_K, ks=[EVAL_K], want_loss=True)
+    out = {"rows": int(len(a)), "hr20": float(r.hits[0].item()) / len(a), "ndcg20": float(r.ndcg[0].item()) / len(a),
+           "ce": round(float(r.loss.item()), 5)}
+    idx = r.idx.cpu().numpy()
+    net.train()
+    return out, idx
 
 
 def gather_bytes(T, E):
@@ -148,25 +237,63 @@ def gather_bytes(T, E):
 
 
 def sampled_fwd_bytes(B, S, HF):
-    # h read, negative ids, gathered W rows + bias read, Zᵀ write, (max, Σexp) partials, Wg/bg write
-    nT = (S + 127) // 128
-    return B * HF * 4 + S * 4 + 2 * S * (HF + 1) * 4 + B * S * 4 + nT * B * 8
+    # h, targets, negative ids, target + negative W rows and biases, logits B·(S+1)
+    return B * HF * 4 + B * 4 + S * 4 + (B + S) * (HF + 1) * 4 + B * (S + 1) * 4
 
 
-def target_step(kern, T, B, S, E, HF, n_gather):
+def target_step(kern, T, B, S, E, HF, n_gather, terms):
     """North-star target: embedding gather + sampled logits (fwd) against the
-    HBM roofline, with the logits' flop rate beside it."""
+    HBM roofline, with the logits' MFMA rate beside it."""
     if "gather" not in kern or "sampled_fwd" not in kern:
         return None
     tg, ts = kern["gather"] * n_gather, kern["sampled_fwd"]
     by = n_gather * gather_bytes(T, E) + sampled_fwd_bytes(B, S, HF)
     gbs = by / ((tg + ts) * 1e-3) / 1e9
     fl = 2.0 * B * S * HF
-    return {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(gbs / HBM_PEAK_GBS, 4), "bytes_per_step": int(by), "ms": round(tg + ts, 4),
-            "gather_ms": round(tg, 4), "gather_GBs": round(n_gather * gather_bytes(T, E) / (tg * 1e-3) / 1e9, 1),
-            "sampled_fwd_ms": round(ts, 4), "sampled_fwd_TFLOPs": round(fl / (ts * 1e-3) / 1e12, 2),
-            "sampled_fwd_mfma_frac": round(fl / (ts * 1e-3) / 1e12 / FP32_MFMA_PEAK_TFLOPS, 4)}
+    out = {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+           "frac": round(gbs / HBM_PEAK_GBS, 4), "bytes_per_step": int(by), "ms": round(tg + ts, 4),
+           "gather_ms": round(tg, 4), "gather_GBs": round(n_gather * gather_bytes(T, E) / (tg * 1e-3) / 1e9, 1),
+           "sampled_fwd_ms": round(ts, 4), "sampled_fwd_alg_TFLOPs": round(fl / (ts * 1e-3) / 1e12, 2)}
+    if terms:
+        out["sampled_fwd_mfma_frac"] = round(terms * fl / (ts * 1e-3) / 1e12 / BF16_MFMA_PEAK_TFLOPS, 4)
+        out["mfma"] = f"bf16 MFMA, {terms} plane products per fp32 product"
+    else:
+        out["sampled_fwd_mfma_frac"] = round(fl / (ts * 1e-3) / 1e12 / FP32_MFMA_PEAK_TFLOPS, 4)
+    return out
+
+
+def head_roofline(kern, precision, B, N, E):
+    flops_head = 2.0 * B * N * E  # one (B × E)·(E × A) contraction
+    terms = {"f32x9": 9, "f32x6": 6}.get(precision, 0)
+    heads = {k: kern[k] for k in ("head_fwd", "head_dh", "head_dw_adam") if k in kern}
+    if not heads:
+        return None
+    dom = max(heads, key=heads.get)
+    t = heads[dom] * 1e-3
+    traffic = None
+    pmc = os.path.join(HERE, "profiles", "pmc_traffic.json")
+    if os.path.exists(pmc):
+        traffic = json.load(open(pmc)).get(f"{dom}:{precision}" if terms else dom)
+    if terms:
+        # fused split-bf16 head (csrc/head_flash.hip): pass 1 (head_fwd: Z and the softmax half of
+        # dh) and pass 2 (head_dw_adam: Z recomputed, dW) each run two contractions, every fp32
+        # product as `terms` exact bf16 plane products on v_mfma_f32_32x32x16_bf16
+        ex = 2 * terms * flops_head if dom in ("head_fwd", "head_dw_adam") else 0.0
+        alg = {"head_fwd": 2, "head_dw_adam": 1}.get(dom, 0) * flops_head
+        ach = ex / t / 1e12
+        return {"bound": "mfma", "kernel": dom, "achieved": round(ach, 2), "peak": BF16_MFMA_PEAK_TFLOPS,
+                "unit": "TFLOP/s", "frac": round(ach / BF16_MFMA_PEAK_TFLOPS, 4), "traffic": traffic,
+                "flops_per_launch": ex,
+                "mfma": f"bf16 MFMA, fp32 operands split exactly into 3 bf16 planes, {terms} plane products",
+                "algorithmic_fp32_TFLOPs": round(alg / t / 1e12, 2)}
+    ach = flops_head / t / 1e12
+    return {"bound": "mfma", "kernel": dom, "achieved": round(ach, 2), "peak": FP32_MFMA_PEAK_TFLOPS,
+            "unit": "TFLOP/s", "frac": round(ach / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": traffic,
+            "flops_per_launch": flops_head}
+
+
+def pinned(b):
+    return tuple(x.pin_memory() for x in b)
 
 
 def main():
@@ -174,30 +301,38 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    shard = (world > 1 or args.force_shard) and args.config == "c2"
+    shard = (world > 1 or args.force_shard) and args.config in ("c2", "c4")
     if world > 1 or args.force_shard:
         import torch.distributed as dist
         torch.cuda.set_device(local)
         dist.init_process_group("nccl")
-    if world > 1 and args.config != "c2":
-        raise SystemExit("multi-GPU bench runs the C2 headline workload only")
+    if world > 1 and args.config == "c3":
+        raise SystemExit("multi-GPU bench runs the C2 / C4 workloads")
     from recommenders.data_utils.synthetic import SessionStream
 
     dev = torch.device("cuda", local)
     B, L, N, E = args.batch, args.seq, args.items, args.dim
     nsteps = args.warmup + args.steps
-    # synthetic session stream (seeded per rank: each rank owns its batch shard)
-    st = SessionStream(N, L, B * nsteps, seed=2 + rank)
-    batches = []
-    tok = []
+    # synthetic session stream (seeded per rank: each rank owns its batch shard);
+    # one extra batch is held out for evaluation
+    st = SessionStream(N, L, B * (nsteps + 1), seed=2 + rank)
+    args.item_counts = st.item_counts()
+    batches, tok = [], []
     for i in range(nsteps):
-        s, a, r, sn, ln, nln, e = st.batch(i, B)
-        batches.append((s.to(dev), a.to(dev), ln.to(dev)))
-        tok.append(int(ln.sum()))
+        b = st.batch(i, B)
+        batches.append(pinned(b))
+        tok.append(int(b[4].sum()))
+    hb = st.batch(nsteps, B)
+    held = (hb[0], hb[1], hb[4])
     T = float(np.mean(tok[args.warmup:]))
     tr = make_trainer(args.config, args, dev, shard)
     tr.set_train()
-    dt, losses, kern = timed_run(tr, batches, args.warmup, args.steps, world, not args.no_kernel_timing)
+    dt, losses, kern, per_step = timed_run(tr, batches, args.warmup, args.steps, world, not args.no_kernel_timing,
+                                           args.config)
+    ev, dev_idx = None, None
+    net = getattr(tr, "gru_model", None)
+    if not args.no_eval and not shard and net is not None:
+        ev, dev_idx = device_eval(net, held)
     if rank != 0:
         if torch.distributed.is_initialized():
             torch.distributed.destroy_process_group()
@@ -206,53 +341,48 @@ def main():
     value = B * args.steps * world / dt
     roof = None
     target = None
+    native = None
     HF = E * (2 if args.config == "c3" else 1)
-    if args.config == "c2":
-        flops_head = 2.0 * B * N * E  # one (B × E)·(E × A) contraction
-        terms = {"f32x9": 9, "f32x6": 6}.get(args.precision, 0)
+    terms = {"f32x9": 9, "f32x6": 6}.get(args.precision, 0)
+    if args.config in ("c2", "c4"):
         if kern:
-            heads = {k: kern[k] for k in ("head_fwd", "head_dh", "head_dw_adam") if k in kern}
-            dom = max(heads, key=heads.get)
-            t = heads[dom] * 1e-3
-            traffic = None
-            pmc = os.path.join(HERE, "profiles", "pmc_traffic.json")
-            if os.path.exists(pmc):
-                traffic = json.load(open(pmc)).get(f"{dom}:{args.precision}" if terms else dom)
-            if terms:
-                # fused split-bf16 head (csrc/head_flash.hip): pass 1 (head_fwd: Z and the softmax half of
-                # dh) and pass 2 (head_dw_adam: Z recomputed, dW) each run two contractions, every fp32
-                # product as `terms` exact bf16 plane products on v_mfma_f32_32x32x16_bf16
-                ex = 2 * terms * flops_head if dom in ("head_fwd", "head_dw_adam") else 0.0
-                alg = {"head_fwd": 2, "head_dw_adam": 1}.get(dom, 0) * flops_head
-                ach = ex / t / 1e12
-                roof = {"bound": "mfma", "kernel": dom, "achieved": round(ach, 2), "peak": BF16_MFMA_PEAK_TFLOPS,
-                        "unit": "TFLOP/s", "frac": round(ach / BF16_MFMA_PEAK_TFLOPS, 4), "traffic": traffic,
-                        "flops_per_launch": ex,
-                        "mfma": f"bf16 MFMA, fp32 operands split exactly into 3 bf16 planes, {terms} plane products",
-                        "algorithmic_fp32_TFLOPs": round(alg / t / 1e12, 2)}
+            sup = net.heads["output"] if net is not None else tr.SMORL_1.sup_head_output
+            prec = args.precision if sup.flash_terms(B * world) else "f32"
+            roof = head_roofline(kern, prec, B * world, N // world, E)
+        if args.config == "c2" and world == 1:
+            parity_net = None
+            if not args.no_cpu_baseline and not args.no_eval and net is not None:
+                parity_net = net
             else:
-                ach = flops_head / t / 1e12
-                roof = {"bound": "mfma", "kernel": dom, "achieved": round(ach, 2), "peak": FP32_MFMA_PEAK_TFLOPS,
-                        "unit": "TFLOP/s", "frac": round(ach / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": traffic,
-                        "flops_per_launch": flops_head}
-        if world == 1 and not args.no_target and kern:
-            # north-star target step measured on GRU4Rec at C2
-            # shapes with the sampled head: a short side run, own trainer
+                del net
             del tr
             torch.cuda.empty_cache()
-            tr2 = make_trainer("c2s", args, dev, False)
-            tr2.set_train()
-            _, _, k2 = timed_run(tr2, batches, min(2, args.warmup), min(5, args.steps), 1, True)
-            target = target_step(k2, T, B, args.negatives, E, E, 1)
-            if target is not None:
-                target["workload"] = f"GRU4Rec {N} items dim{E} batch {B}, {args.negatives} sampled negatives"
-            del tr2
+            if not args.no_native_side and args.precision != "f32":
+                # the trainers' default arithmetic (native fp32 MFMA head), short side run
+                trn = make_trainer("c2native", args, dev, False)
+                trn.set_train()
+                dtn, _, _, psn = timed_run(trn, batches, 2, min(10, args.steps), 1, False, "c2")
+                native = {"value": round(B * min(10, args.steps) / dtn, 2),
+                          "ms_per_step": round(dtn / min(10, args.steps) * 1e3, 3), "matmul_precision": "f32",
+                          "note": "trainer default arithmetic (native fp32 MFMA head), 10 steps"}
+                del trn
+                torch.cuda.empty_cache()
+            if not args.no_target and kern:
+                # north-star target step measured on GRU4Rec at C2
+                # shapes with the sampled head: a short side run, own trainer
+                tr2 = make_trainer("c2s", args, dev, False)
+                tr2.set_train()
+                _, _, k2, _ = timed_run(tr2, batches, min(2, args.warmup), min(10, args.steps), 1, True, "c2")
+                target = target_step(k2, T, B, args.negatives, E, E, 1, terms)
+                if target is not None:
+                    target["workload"] = f"GRU4Rec {N} items dim{E} batch {B}, {args.negatives} sampled negatives"
+                    target["kernel_ms"] = k2
+                del tr2
     else:
-        target = target_step(kern, T, B, args.negatives, E, HF, 2)
+        target = target_step(kern, T, B, args.negatives, E, HF, 2, terms)
         roof = dict(target) if target else None
         if roof:
             roof["kernel"] = "gather + sampled_fwd"
-            # PMC HBM bytes of the same kernels per step (tools/pmc_c3.sh), committed under profiles/
             pmc = os.path.join(HERE, "profiles", "pmc_traffic.json")
             roof["traffic"] = None
             if os.path.exists(pmc) and (B, args.negatives, HF, args.precision) == (4096, 2048, 256, "f32x6"):
@@ -260,13 +390,20 @@ def main():
     cpu = None
     if world == 1 and not args.no_cpu_baseline and args.config == "c2":
         cpu = cpu_baseline(args)
+        if ev is not None and dev_idx is not None and parity_net is not None:
+            cpu["hr_ndcg_parity"] = cpu_eval_parity(parity_net, held, dev_idx)
     if args.config == "c2":
         metric = "session-steps/sec at 1M items, dim128, batch 4096; HR@20/NDCG@20 parity"
         workload = f"GRU4Rec {N} items, dim{E}, seq_len<={L}, batch {B}/GPU, full-softmax logits"
-    else:
+    elif args.config == "c3":
         metric = "session-steps/sec, BidirGRU4Rec 1M items, dim128, batch 4096, 2048 sampled negatives"
         workload = (f"BidirGRU4Rec {N} items, dim{E}, seq_len<={L}, batch {B}, {args.negatives} shared uniform "
                     f"negatives (sampled softmax), dropout 0")
+    else:
+        metric = "session-steps/sec, SMORL (SQN double-Q, 3 rewards) 1M items, dim128, batch 4096"
+        workload = (f"SMORL_trainer {N} items, dim{E}, seq_len<={L}, batch {B}/GPU, sup head + Q heads acc/div/nov, "
+                    f"topk_div=topk_nov=1, q_weights [1,1,1], gamma 0.5, alpha 1")
+    ps = np.array(per_step) * 1e3
     line = {
         "metric": metric,
         "value": round(value, 2), "unit": "session-steps/sec", "n_gpus": world, "steps": args.steps,
@@ -275,10 +412,13 @@ def main():
         "data": "synthetic (seeded Zipf session stream, random-init weights)",
         "config": {"workload": workload,
                    "global_batch": B * world, "seq_len": L, "items": N, "dim": E,
-                   "parallelism": (f"dp{world} trunk + {world}-way item-sharded head (RCCL)" if world > 1
+                   "parallelism": (f"dp{world} trunk + {world}-way item-sharded tables (RCCL)" if world > 1
                                    else "single"),
                    "tokens_per_batch": int(T)},
-        "roofline": roof, "cpu_baseline": cpu, "north_star_target": target, "kernel_ms": kern,
+        "step_ms": {"median": round(float(np.median(ps)), 3), "p10": round(float(np.percentile(ps, 10)), 3),
+                    "p90": round(float(np.percentile(ps, 90)), 3), "mean": round(float(ps.mean()), 3)},
+        "roofline": roof, "cpu_baseline": cpu, "north_star_target": target, "eval_heldout": ev,
+        "native_f32": native, "kernel_ms": kern,
         "loss_first_last": [round(losses[0], 5), round(losses[-1], 5)],
     }
     print(json.dumps(line), flush=True)

@@ -252,12 +252,15 @@ __global__ __launch_bounds__(FL_T) void k_flash_fwd(const bf16x8* __restrict__ H
 
 // ------------------------------------------------------------ combine ----
 // lse over the splits (natural units) and, when the target is one of this
-// shard's items [lo, lo + A), its logit z = h·W[t] + b[t] (else 0)
+// shard's items [lo, lo + A), its logit z = h·W[t] + b[t]; 0 for a target
+// held by another shard, NaN for one outside [0, A_full) (CrossEntropyLoss
+// raises there; the native head writes a NaN loss row, head.hip k_lse_combine)
 __global__ __launch_bounds__(256) void k_flash_lse(const float* __restrict__ pm, const float* __restrict__ pl,
                                                    int nsplit, const float* __restrict__ h,
                                                    const float* __restrict__ W, const float* __restrict__ bias,
-                                                   const int64_t* __restrict__ tgt, int64_t lo, int A, int B,
-                                                   int HF, float* __restrict__ lse, float* __restrict__ zt) {
+                                                   const int64_t* __restrict__ tgt, int64_t lo, int A,
+                                                   int64_t A_full, int B, int HF, float* __restrict__ lse,
+                                                   float* __restrict__ zt) {
   const int b = blockIdx.x * 256 + threadIdx.x;
   if (b >= B) return;
   float M = NEG_INF;
@@ -270,7 +273,7 @@ __global__ __launch_bounds__(256) void k_flash_lse(const float* __restrict__ pm,
   lse[b] = (M + log2f(L)) * LN2;
   if (zt) {
     const int64_t t = tgt[b] - lo;
-    float z = 0.f;
+    float z = (tgt[b] >= 0 && tgt[b] < A_full) ? 0.f : __builtin_nanf("");
     if (t >= 0 && t < A) {
       for (int k = 0; k < HF; ++k) z = fmaf(h[(int64_t)b * HF + k], W[t * HF + k], z);
       z += bias[t];
@@ -490,12 +493,12 @@ extern "C" int rg_flash_fwd(const void* Hk, const void* Wk, const void* Wr, cons
 }
 
 extern "C" int rg_flash_lse(const float* pm, const float* pl, int nsplit, const float* h, const float* W,
-                            const float* bias, const int64_t* tgt, int64_t lo, int A, int B, int HF, float* lse,
-                            float* zt, hipStream_t stream) {
+                            const float* bias, const int64_t* tgt, int64_t lo, int A, int64_t A_full, int B, int HF,
+                            float* lse, float* zt, hipStream_t stream) {
   if (B <= 0 || A <= 0 || nsplit <= 0 || !pm || !pl || !lse) return RG_ERR_ARG;
-  if (zt && (!h || !W || !bias || !tgt)) return RG_ERR_ARG;
+  if (zt && (!h || !W || !bias || !tgt || A_full < lo + A)) return RG_ERR_ARG;
   hipLaunchKernelGGL(k_flash_lse, dim3((B + 255) / 256), dim3(256), 0, stream, pm, pl, nsplit, h, W, bias, tgt, lo,
-                     A, B, HF, lse, zt);
+                     A, A_full, B, HF, lse, zt);
   RG_LAUNCH_CHECK();
   return RG_OK;
 }

@@ -71,6 +71,20 @@ def _require_hip(model):
         raise TypeError("evaluate() runs the MI355X device path; pass a recommenders.models.* model")
 
 
+def _check_loss_function(loss_function):
+    """The device path computes mean CE (the trainers' ``cross_entropy_loss``,
+    reference eval_protocol.py:182 calls ``loss_function(preds, a)``); any
+    other loss is refused rather than silently replaced."""
+    if loss_function is None:
+        return
+    ok = (isinstance(loss_function, torch.nn.CrossEntropyLoss) and loss_function.weight is None
+          and loss_function.reduction == "mean" and loss_function.ignore_index == -100
+          and loss_function.label_smoothing == 0.0)
+    if not ok:
+        raise NotImplementedError(f"evaluate(): only CrossEntropyLoss(reduction='mean') runs on the device path, "
+                                  f"got {loss_function!r}")
+
+
 def evaluate(evaluation_data_loader, model, device, loss_function, padding_pos, diversity_embedding,
              unpopular_actions_set, head_idx=0, topk_hr_ndcg=[5, 10, 20], topk_to_consider_div=1,
              topk_to_consider_nov=1, topk_to_consider_cov=[1, 5, 10], novelty_rew_signal=1, input_tokenizer=None,
@@ -78,6 +92,7 @@ def evaluate(evaluation_data_loader, model, device, loss_function, padding_pos, 
     """Same 7-tuple as the reference (eval_protocol.py:123-263):
     (loss, hr, ndcg, coverage_res, avg_diversity_rew, avg_novelty_rew, repetitions)."""
     _require_hip(model)
+    _check_loss_function(loss_function)
     if input_tokenizer is not None or output_tokenizer is not None:
         raise NotImplementedError("tokenizer remap is not on the device path yet")
     model.eval()

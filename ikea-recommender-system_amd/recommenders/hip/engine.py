@@ -215,10 +215,7 @@ class Trunk:
         B, L = s.shape
         w = self.ws(slot, B, L, save)
         st = stream_ptr()
-        if lens.device.type == "cpu":
-            w.lens.copy_(lens, non_blocking=False)
-        else:
-            w.lens.copy_(lens)
+        w.lens.copy_(lens, non_blocking=True)
         if self.stepped:  # host bound of the timestep loop (no device sync)
             w.tmax = max(1, min(L, int(lens.max()))) if self.packed and lens.device.type == "cpu" else L
         with region("pack"):
@@ -466,7 +463,7 @@ class SoftmaxHead:
             call("rg_flash_fwd", w.Hk.data_ptr(), w.Wk.data_ptr(), w.Wr.data_ptr(), w.bias_pad.data_ptr(), B, A, HF,
                  terms, w.nsplit, w.pm.data_ptr(), w.pl.data_ptr(), w.pO.data_ptr(), st)
         call("rg_flash_lse", w.pm.data_ptr(), w.pl.data_ptr(), w.nsplit, h.data_ptr(), W, b, tgt.data_ptr(), self.lo,
-             A, B, HF, w.lse.data_ptr(), w.zt.data_ptr(), st)
+             A, self.A_full, B, HF, w.lse.data_ptr(), w.zt.data_ptr(), st)
         return w
 
     def flash_dh(self, w, tgt, lse, g, dh_out):

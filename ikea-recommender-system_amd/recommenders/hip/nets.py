@@ -59,8 +59,11 @@ class HipNet:
 
     # ------------------------------------------------------- nn.Module-ish --
     def set_matmul_precision(self, precision):
-        """Arithmetic of the head GEMMs ("f32" native, "f32x9" / "f32x6"
-        split-bf16, engine.SPLIT_TERMS); only the sampled head uses it so far."""
+        """Arithmetic of the trained heads' GEMMs ("f32" native fp32 MFMA,
+        "f32x9" / "f32x6" split-bf16, engine.SPLIT_TERMS): the full-softmax
+        head's fused training path (csrc/head_flash.hip) or the sampled
+        head's split forward (csrc/sampled.hip).  Evaluation logits and the
+        Q heads' row gathers stay native fp32."""
         for hd in self.heads.values():
             hd.set_matmul_precision(precision)
         return self

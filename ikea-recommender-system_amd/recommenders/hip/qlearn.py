@@ -56,6 +56,10 @@ class QNet(HipNet):
         self.q_heads = [QHead(n, self.action_dim, self.hf, self.device, shard=self.shard) for n in q_names]
         for q in self.q_heads:
             setattr(self, q.name, q)
+        # SMORL's diversity / novelty rewards read the supervised logits' top-k
+        # after the CE forward: that head keeps the Zᵀ-storing native path
+        if len(self.q_heads) > 1:
+            self.sup_head_output.keep_logits = True
         self._argmax_head = None
         self._buf = {}
 

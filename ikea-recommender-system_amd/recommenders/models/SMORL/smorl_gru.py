@@ -46,7 +46,8 @@ class SMORL_trainer:
                  item_num, state_size, action_dim, gamma, gru_layers, q_weights, alpha, div_embedding,
                  unpopular_actions_set, topk_div, device, input_tokenizer=None, output_tokenizer=None,
                  padding_idx=None, torch_rand_seed=118, python_rand_seed=999, name_1="SMORL_1", name_2="SMORL_2",
-                 topk_nov=1, nov_rew_sig=1, shard_items=False, process_group=None, fp16_embeddings=False):
+                 topk_nov=1, nov_rew_sig=1, shard_items=False, process_group=None, fp16_embeddings=False,
+                 matmul_precision="f32"):
         torch.manual_seed(torch_rand_seed)
         random.seed(python_rand_seed)
         self.device = require_gpu(device)
@@ -61,6 +62,10 @@ class SMORL_trainer:
                                         fp16_embeddings=fp16_embeddings)
         self.SMORL_1 = mk(name_1)
         self.SMORL_2 = mk(name_2)
+        # matmul_precision (build extension): arithmetic of the supervised head
+        # GEMMs, "f32" native fp32 MFMA or split-bf16 "f32x9" / "f32x6"
+        for net in (self.SMORL_1, self.SMORL_2):
+            net.set_matmul_precision(matmul_precision)
         self.gamma = gamma
         self.alpha = alpha
         self.q_weights = q_weights

@@ -42,7 +42,7 @@ class SQN_trainer:
     def __init__(self, hidden_dim, embedding_dim, train_pad_embed, use_packed_seq, learning_rate, item_num,
                  state_size, action_dim, gamma, gru_layers, device, padding_idx=None, torch_rand_seed=118,
                  python_rand_seed=999, name_1="SQN_1", name_2="SQN_2", shard_items=False, process_group=None,
-                 fp16_embeddings=False):
+                 fp16_embeddings=False, matmul_precision="f32"):
         torch.manual_seed(torch_rand_seed)
         random.seed(python_rand_seed)
         self.device = require_gpu(device)
@@ -56,6 +56,10 @@ class SQN_trainer:
                                       device=self.device, comm=self.comm, fp16_embeddings=fp16_embeddings)
         self.DQN_1 = mk(name_1)
         self.DQN_2 = mk(name_2)
+        # matmul_precision (build extension): arithmetic of the supervised head
+        # GEMMs, "f32" native fp32 MFMA or split-bf16 "f32x9" / "f32x6"
+        for net in (self.DQN_1, self.DQN_2):
+            net.set_matmul_precision(matmul_precision)
         self.gamma = gamma
         self.learning_rate = learning_rate
         self.cross_entropy_loss = nn.CrossEntropyLoss(weight=None, reduction="mean")

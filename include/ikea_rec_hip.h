@@ -111,7 +111,8 @@ int rg_head_fwd_x(const float* h, const float* W, const float* bias, int B, int 
  * rg_flash_fwd: pass 1 — per (split, row) running max pm and Σexp pl (log2
  *   units) and O = Σ_j 2^(z_j − m)·W_j (nsplit × HF × B).
  * rg_flash_lse: lse (natural units) over the splits; zt = the target logit
- *   when the target is one of items [lo, lo + A), else 0.
+ *   when the target is one of items [lo, lo + A), 0 when another shard holds
+ *   it, NaN when it lies outside [0, A_full) (CrossEntropyLoss raises there).
  * rg_flash_rows: row records (lse·log2 e, target − lo or -1), B × 8 bytes.
  * rg_flash_dh: dh = gscale·(Σ_s 2^(m_s − lse)·O_s − W[target]) (B × HF).
  * rg_flash_dw_adam: pass 2 — dW = dZᵀ·h, db = Σ_b dZ, then Adam (adam6, host
@@ -122,7 +123,8 @@ int rg_head_planes(const float* X, int rows, int HF, void* planes_k, void* plane
 int rg_flash_fwd(const void* Hk, const void* Wk, const void* Wr, const float* bias_pad, int B, int A, int HF,
                  int terms, int nsplit, float* pm, float* pl, float* pO, rg_stream_t stream);
 int rg_flash_lse(const float* pm, const float* pl, int nsplit, const float* h, const float* W, const float* bias,
-                 const int64_t* tgt, int64_t lo, int A, int B, int HF, float* lse, float* zt, rg_stream_t stream);
+                 const int64_t* tgt, int64_t lo, int A, int64_t A_full, int B, int HF, float* lse, float* zt,
+                 rg_stream_t stream);
 int rg_flash_rows(const float* lse, const int64_t* tgt, int64_t lo, int A, int B, void* rowinfo, rg_stream_t stream);
 int rg_flash_dh(const float* pm, const float* pO, const void* rowinfo, int nsplit, const float* W, float gscale,
                 int B, int HF, float* dh, rg_stream_t stream);

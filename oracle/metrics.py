@@ -76,6 +76,65 @@ def hits_for_batch(preds, true_idx, top_k=(5, 10, 20)):
     return hits, ndcg
 
 
+def canonical_topk_fast(values, k):
+    """canonical_topk for wide rows (A ~ 1M): argpartition down to the
+    candidates >= the k-th largest value (ties at the boundary included),
+    then the (value desc, index asc) order among them."""
+    v = np.asarray(values)
+    part = np.argpartition(-v, k - 1, axis=1)[:, :k]
+    kth = np.take_along_axis(v, part, 1).min(1)
+    out = np.empty((v.shape[0], k), dtype=np.int64)
+    for i in range(v.shape[0]):
+        cand = np.nonzero(v[i] >= kth[i])[0]
+        order = np.lexsort((cand, -v[i, cand]))
+        out[i] = cand[order[:k]]
+    return out
+
+
+def hits_from_lists(idx, true_idx, top_k=(5, 10, 20)):
+    """hits_for_batch on given (B, max_k) top-k index lists (rank = first
+    position of the target among the first k, eval_protocol.py:26-59, 84-98)."""
+    idx = np.asarray(idx)
+    tgt = np.asarray(true_idx).reshape(-1, 1)
+    hits = np.zeros(len(top_k))
+    ndcg = np.zeros(len(top_k))
+    for i, k in enumerate(top_k):
+        eq = idx[:, :k] == tgt
+        found = eq.any(1)
+        rank = np.zeros(len(tgt))
+        rank[found] = np.argmax(eq[found], axis=1) + 1
+        hits[i] = found.sum()
+        ndcg[i] = (1.0 / np.log2(rank[found] + 1)).sum()
+    return hits, ndcg
+
+
+def target_ranks(idx, true_idx):
+    """1-based position of the target in each top-k list, 0 if absent."""
+    eq = np.asarray(idx) == np.asarray(true_idx).reshape(-1, 1)
+    found = eq.any(1)
+    r = np.zeros(len(eq), dtype=np.int64)
+    r[found] = np.argmax(eq[found], axis=1) + 1
+    return r
+
+
+def topk_flip_report(z_ref, idx_got, idx_ref, bound):
+    """Compare two canonical top-k lists of the same rows scored by z_ref (the
+    reference-side logits): wherever the lists differ, the item the checked
+    side put at rank j must score (under z_ref) within ``bound`` of the item
+    the reference put there — a flip is allowed only between items whose
+    reference logits are closer than the logit error bound.
+    Returns (rows that differ, max |gap| over differing positions)."""
+    z = np.asarray(z_ref, dtype=np.float64)
+    vg = np.take_along_axis(z, np.asarray(idx_got, dtype=np.int64), 1)
+    vr = np.take_along_axis(z, np.asarray(idx_ref, dtype=np.int64), 1)
+    diff = np.asarray(idx_got) != np.asarray(idx_ref)
+    gap = np.abs(vg - vr)
+    worst = float(gap[diff].max()) if diff.any() else 0.0
+    if worst > bound:
+        raise AssertionError(f"top-k flip between items {worst:.3g} apart (bound {bound:.3g})")
+    return int(diff.any(1).sum()), worst
+
+
 def canonical_topk(values, k):
     """Top-k indices of each row ordered by (value desc, index asc) — the tie
     policy used when comparing against GPU top-k (SURVEY.md §7 hard parts)."""

@@ -24,7 +24,7 @@ def _u8(n):
     return torch.empty(int(n), dtype=torch.uint8, device=dev)
 
 
-def run_flash(h, W, b, tgt, terms, nsplit, lo=0, lse_global=None):
+def run_flash(h, W, b, tgt, terms, nsplit, lo=0, lse_global=None, A_full=None):
     """Every stage of the fused head through the C ABI; pass 2 in its
     gradient-only mode (dW_out / db_out)."""
     call, st = C().call, C().stream_ptr()
@@ -43,7 +43,7 @@ def run_flash(h, W, b, tgt, terms, nsplit, lo=0, lse_global=None):
     lse = torch.full((B,), float("nan"), device=dev)
     zt = torch.full((B,), float("nan"), device=dev)
     call("rg_flash_lse", pm.data_ptr(), pl.data_ptr(), nsplit, h.data_ptr(), W.data_ptr(), b.data_ptr(),
-         tgt.data_ptr(), lo, A, B, HF, lse.data_ptr(), zt.data_ptr(), st)
+         tgt.data_ptr(), lo, A, lo + A if A_full is None else A_full, B, HF, lse.data_ptr(), zt.data_ptr(), st)
     rows = torch.empty(B, 2, device=dev)
     call("rg_flash_rows", (lse if lse_global is None else lse_global).data_ptr(), tgt.data_ptr(), lo, A, B,
          rows.data_ptr(), st)
@@ -105,7 +105,7 @@ def test_flash_head_item_shard():
     h, W, b, tgt = inputs(B, A, HF, 77)
     r = fp64_reference(h, W, b, tgt)
     o = run_flash(h.to(dev), W[lo:hi].contiguous().to(dev), b[lo:hi].contiguous().to(dev), tgt.to(dev), 6, 8,
-                  lo=lo, lse_global=r["lse"].float().to(dev))
+                  lo=lo, lse_global=r["lse"].float().to(dev), A_full=A)
     torch.testing.assert_close(o["lse"], torch.logsumexp(r["Z"][:, lo:hi], 1), rtol=0, atol=2e-5)
     own = (tgt >= lo) & (tgt < hi)
     assert 0 < int(own.sum()) < B
@@ -116,6 +116,29 @@ def test_flash_head_item_shard():
     torch.testing.assert_close(o["dh"], P[:, lo:hi] @ W[lo:hi].double(), rtol=0, atol=1e-6)
     torch.testing.assert_close(o["dW"], r["dW"][lo:hi], rtol=0, atol=1e-7)
     torch.testing.assert_close(o["db"], r["db"][lo:hi], rtol=0, atol=1e-7)
+
+
+@pytest.mark.parametrize("precision", ["f32x6", "f32x9"])
+def test_flash_invalid_target_gives_nan_row(precision):
+    """A target outside [0, A) gives a NaN loss row on the fused head, as on
+    the native head (CrossEntropyLoss raises there); the trainer's loss is NaN."""
+    B, A, HF = 64, 3000, 64
+    h, W, b, tgt = inputs(B, A, HF, 11)
+    tgt[3], tgt[17] = A, -1
+    o = run_flash(h.to(dev), W.to(dev), b.to(dev), tgt.to(dev), TERMS[precision], 8)
+    ce = o["lse"] - o["zt"]
+    assert torch.isnan(ce[3]) and torch.isnan(ce[17])
+    ok = torch.ones(B, dtype=torch.bool)
+    ok[[3, 17]] = False
+    assert torch.isfinite(ce[ok]).all()
+    from recommenders.data_utils.synthetic import SessionStream
+    from recommenders.models.GRU4Rec.model import GRU4Rec_trainer
+    tr = GRU4Rec_trainer(hidden_dim=32, embedding_dim=32, gru_layers=1, train_pad_embed=True, use_packed_seq=True,
+                         learning_rate=0.01, item_num=500, state_size=6, action_dim=500, device="cuda",
+                         matmul_precision=precision)
+    s, a, r, sn, ln, nln, e = SessionStream(500, 6, 64, seed=3).batch(0, 64)
+    a[5] = 500
+    assert np.isnan(tr.train_step(s, a, ln))
 
 
 @pytest.mark.parametrize("precision", ["f32x9", "f32x6"])

@@ -50,7 +50,7 @@ for terms in a.terms:
         "pass1": lambda: call("rg_flash_fwd", Hk.data_ptr(), Wk.data_ptr(), Wr.data_ptr(), bp.data_ptr(), B, A, H,
                               terms, ns, pm.data_ptr(), pl.data_ptr(), pO.data_ptr(), st),
         "combine": lambda: (call("rg_flash_lse", pm.data_ptr(), pl.data_ptr(), ns, h.data_ptr(), W.data_ptr(),
-                                 bias.data_ptr(), tgt.data_ptr(), 0, A, B, H, lse.data_ptr(), zt.data_ptr(), st),
+                                 bias.data_ptr(), tgt.data_ptr(), 0, A, A, B, H, lse.data_ptr(), zt.data_ptr(), st),
                             call("rg_flash_rows", lse.data_ptr(), tgt.data_ptr(), 0, A, B, rows.data_ptr(), st),
                             call("rg_flash_dh", pm.data_ptr(), pO.data_ptr(), rows.data_ptr(), ns, W.data_ptr(),
                                  gs, B, H, dh.data_ptr(), st)),
