@@ -122,6 +122,10 @@ __global__ void k_pad_bias(const float* __restrict__ bias, int A, int Ap, float*
 }
 
 // ------------------------------------------------------------- pass 1 ----
+// The chunk ring is two SEPARATE LDS arrays per operand and the loop is
+// unrolled by two: the compiler orders LDS reads only behind the DMA into the
+// same array, so chunk c's MFMAs start while chunk c+1's DMA is in flight
+// (with one [2][E] array it waited for the just-issued prefetch every chunk).
 template <int HF, int NT>
 __global__ __launch_bounds__(FL_T) void k_flash_fwd(const bf16x8* __restrict__ Hk, const bf16x8* __restrict__ Wk,
                                                     const bf16x8* __restrict__ Wr,
@@ -131,9 +135,9 @@ __global__ __launch_bounds__(FL_T) void k_flash_fwd(const bf16x8* __restrict__ H
   constexpr int NS = HF / 16, NTL = HF / 32;
   constexpr int EK = NS * 192;        // entries per 32-row block, K-planes
   constexpr int ER = NTL * 2 * 192;   // R-planes (== EK)
-  __shared__ bf16x8 sk[2][EK];
-  __shared__ bf16x8 sr[2][ER];
-  __shared__ __attribute__((aligned(16))) float sb[2][32];
+  __shared__ bf16x8 sk0[EK], sk1[EK];
+  __shared__ bf16x8 sr0[ER], sr1[ER];
+  __shared__ __attribute__((aligned(16))) float sb0[32], sb1[32];
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, hh = lane >> 5, l32 = lane & 31;
   // XCD-aware order: the nrb row blocks of one item split are dispatched to
   // the same XCD (round-robin dispatch), so its W chunks are fetched once
@@ -147,12 +151,14 @@ __global__ __launch_bounds__(FL_T) void k_flash_fwd(const bf16x8* __restrict__ H
   const int nct = (A + 31) / 32;
   const int c0 = split * cps;
   const int nch = max(0, min(nct, c0 + cps) - c0);
-  auto issue = [&](int c, int buf) __attribute__((always_inline)) {
-    stage<EK>(Wk + (int64_t)c * EK, sk[buf], w, lane);
-    stage<ER>(Wr + (int64_t)c * ER, sr[buf], w, lane);
-    if (w == 0 && lane < 8) glds16(bias_pad + 32 * c + 4 * lane, sb[buf]);
-  };
-  if (nch > 0) issue(c0, 0);
+#define FL_ISSUE(C, SK, SR, SB)                                                  \
+  do {                                                                           \
+    stage<EK>(Wk + (int64_t)(C) * EK, SK, w, lane);                              \
+    stage<ER>(Wr + (int64_t)(C) * ER, SR, w, lane);                              \
+    if (w == 0 && lane < 8) glds16(bias_pad + 32 * (C) + 4 * lane, SB);          \
+    __builtin_amdgcn_sched_barrier(0); /* keep the prefetch at the top */ \
+  } while (0)
+  if (nch > 0) FL_ISSUE(c0, sk0, sr0, sb0);
   // this wave's 32 rows of h (B operand of Sᵀ = W_c·hᵀ) for the whole split
   bf16x8 hk[NS][3];
 #pragma unroll
@@ -165,77 +171,66 @@ __global__ __launch_bounds__(FL_T) void k_flash_fwd(const bf16x8* __restrict__ H
   for (int t = 0; t < NTL; ++t) o[t] = f16v{};
   float m = NEG_INF, l = 0.f;
   __syncthreads();
-#ifdef FL_DIAG_PRIO
-  if (w >= 4) __builtin_amdgcn_s_setprio(1);
-#endif
-  for (int c = 0; c < nch; ++c) {
-    const int buf = c & 1;
-    if (c + 1 < nch) issue(c0 + c + 1, buf ^ 1);
-    if (active) {
-#ifndef FL_ACC2
-      f16v sa = {};
+  auto chunk = [&](const bf16x8* sk, const bf16x8* sr, const float* sb) __attribute__((always_inline)) {
+    f16v sa = {};
 #pragma unroll
-      for (int s = 0; s < NS; ++s)
-        sa = mfma_split<NT>(sk[buf][s * 192 + lane], sk[buf][s * 192 + 64 + lane], sk[buf][s * 192 + 128 + lane],
-                            hk[s][0], hk[s][1], hk[s][2], sa);
-#else
-      f16v sa = {}, sb2 = {};
+    for (int s = 0; s < NS; ++s)
+      sa = mfma_split<NT>(sk[s * 192 + lane], sk[s * 192 + 64 + lane], sk[s * 192 + 128 + lane], hk[s][0], hk[s][1],
+                          hk[s][2], sa);
+    // logits in log2 units (item acc32_row(r, hh) of the chunk, row l32)
+    float cm = NEG_INF;
 #pragma unroll
-      for (int s = 0; s < NS; s += 2) {
-        sa = mfma_split<NT>(sk[buf][s * 192 + lane], sk[buf][s * 192 + 64 + lane], sk[buf][s * 192 + 128 + lane],
-                            hk[s][0], hk[s][1], hk[s][2], sa);
-        sb2 = mfma_split<NT>(sk[buf][(s + 1) * 192 + lane], sk[buf][(s + 1) * 192 + 64 + lane],
-                             sk[buf][(s + 1) * 192 + 128 + lane], hk[s + 1][0], hk[s + 1][1], hk[s + 1][2], sb2);
+    for (int q = 0; q < 4; ++q) {
+      const f4 bq = *reinterpret_cast<const f4*>(&sb[8 * q + 4 * hh]);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const float z = (sa[4 * q + u] + bq[u]) * L2E;
+        sa[4 * q + u] = z;
+        cm = fmaxf(cm, z);
       }
-      sa += sb2;
-#endif
-      // logits in log2 units (item acc32_row(r, hh) of the chunk, row l32)
-      float cm = NEG_INF;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const f4 bq = *reinterpret_cast<const f4*>(&sb[buf][8 * q + 4 * hh]);
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const float z = (sa[4 * q + u] + bq[u]) * L2E;
-          sa[4 * q + u] = z;
-          cm = fmaxf(cm, z);
-        }
-      }
-      cm = fmaxf(cm, __shfl_xor(cm, 32));
-      const float mn = fmaxf(m, cm);
-      if (__any(mn > m)) {
-        const float a = mn > m ? __builtin_amdgcn_exp2f(m - mn) : 1.f;
-#pragma unroll
-        for (int t = 0; t < NTL; ++t) o[t] *= a;
-        l *= a;
-        m = mn;
-      }
-      const float mm = m == NEG_INF ? 0.f : m;
-      float ps = 0.f;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const float p = __builtin_amdgcn_exp2f(sa[r] - mm);
-        sa[r] = p;
-        ps += p;
-      }
-      l += ps;
-      bf16x8 q0[2], q1[2], q2[2];
-#pragma unroll
-      for (int s = 0; s < 2; ++s)
-        split3x8(f4{sa[8 * s], sa[8 * s + 1], sa[8 * s + 2], sa[8 * s + 3]},
-                 f4{sa[8 * s + 4], sa[8 * s + 5], sa[8 * s + 6], sa[8 * s + 7]}, q0[s], q1[s], q2[s]);
-#pragma unroll
-      for (int t = 0; t < NTL; ++t)
-#pragma unroll
-        for (int s = 0; s < 2; ++s) {
-          const int e = (t * 2 + s) * 192 + lane;
-          o[t] = mfma_split<NT>(sr[buf][e], sr[buf][e + 64], sr[buf][e + 128], q0[s], q1[s], q2[s], o[t]);
-        }
     }
-#ifndef FL_DIAG_NOSYNC
+    cm = fmaxf(cm, __shfl_xor(cm, 32));
+    const float mn = fmaxf(m, cm);
+    if (__any(mn > m)) {
+      const float a = mn > m ? __builtin_amdgcn_exp2f(m - mn) : 1.f;
+#pragma unroll
+      for (int t = 0; t < NTL; ++t) o[t] *= a;
+      l *= a;
+      m = mn;
+    }
+    const float mm = m == NEG_INF ? 0.f : m;
+    float ps = 0.f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const float p = __builtin_amdgcn_exp2f(sa[r] - mm);
+      sa[r] = p;
+      ps += p;
+    }
+    l += ps;
+    bf16x8 q0[2], q1[2], q2[2];
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+      split3x8(f4{sa[8 * s], sa[8 * s + 1], sa[8 * s + 2], sa[8 * s + 3]},
+               f4{sa[8 * s + 4], sa[8 * s + 5], sa[8 * s + 6], sa[8 * s + 7]}, q0[s], q1[s], q2[s]);
+#pragma unroll
+    for (int t = 0; t < NTL; ++t)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const int e = (t * 2 + s) * 192 + lane;
+        o[t] = mfma_split<NT>(sr[e], sr[e + 64], sr[e + 128], q0[s], q1[s], q2[s], o[t]);
+      }
+  };
+  for (int c = 0; c < nch; c += 2) {
+    if (c + 1 < nch) FL_ISSUE(c0 + c + 1, sk1, sr1, sb1);
+    if (active) chunk(sk0, sr0, sb0);
     __syncthreads();
-#endif
+    if (c + 1 < nch) {
+      if (c + 2 < nch) FL_ISSUE(c0 + c + 2, sk0, sr0, sb0);
+      if (active) chunk(sk1, sr1, sb1);
+      __syncthreads();
+    }
   }
+#undef FL_ISSUE
   if (!active) return;
   l += __shfl_xor(l, 32);
   const int row = r0 + l32;
@@ -310,6 +305,7 @@ __global__ __launch_bounds__(256) void k_flash_dh(const float* __restrict__ pm, 
 }
 
 // ------------------------------------------------------------- pass 2 ----
+// Same two-array ring and two-fold unrolled loop as pass 1.
 template <int HF, int NT>
 __global__ __launch_bounds__(FL_T) void k_flash_dw(const bf16x8* __restrict__ Hk, const bf16x8* __restrict__ Hr,
                                                    const bf16x8* __restrict__ Wk,
@@ -322,20 +318,22 @@ __global__ __launch_bounds__(FL_T) void k_flash_dw(const bf16x8* __restrict__ Hk
   constexpr int NS = HF / 16, NTL = HF / 32;
   constexpr int EK = NS * 192;
   constexpr int ER = NTL * 2 * 192;
-  __shared__ bf16x8 sk[2][EK];
-  __shared__ bf16x8 sr[2][ER];
-  __shared__ __attribute__((aligned(16))) float2 si[2][32];
+  __shared__ bf16x8 sk0[EK], sk1[EK];
+  __shared__ bf16x8 sr0[ER], sr1[ER];
+  __shared__ __attribute__((aligned(16))) float2 si0[32], si1[32];
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, hh = lane >> 5, l32 = lane & 31;
   const int j0 = blockIdx.x * 32 * FL_WAVES + 32 * w;
   const bool active = j0 < A;
   const int item = j0 + l32;
   const int nch = B / 32;
-  auto issue = [&](int c, int buf) __attribute__((always_inline)) {
-    stage<EK>(Hk + (int64_t)c * EK, sk[buf], w, lane);
-    stage<ER>(Hr + (int64_t)c * ER, sr[buf], w, lane);
-    if (w == 0 && lane < 16) glds16(rowinfo + 32 * c + 2 * lane, si[buf]);
-  };
-  issue(0, 0);
+#define FL_ISSUE(C, SK, SR, SI)                                                  \
+  do {                                                                           \
+    stage<EK>(Hk + (int64_t)(C) * EK, SK, w, lane);                              \
+    stage<ER>(Hr + (int64_t)(C) * ER, SR, w, lane);                              \
+    if (w == 0 && lane < 16) glds16(rowinfo + 32 * (C) + 2 * lane, SI);          \
+    __builtin_amdgcn_sched_barrier(0); /* keep the prefetch at the top */ \
+  } while (0)
+  FL_ISSUE(0, sk0, sr0, si0);
   // this wave's 32 items of W (B operand of S = h_c·Wᵀ)
   bf16x8 wk[NS][3];
 #pragma unroll
@@ -349,52 +347,53 @@ __global__ __launch_bounds__(FL_T) void k_flash_dw(const bf16x8* __restrict__ Hk
   for (int t = 0; t < NTL; ++t) dw[t] = f16v{};
   float dbs = 0.f;
   __syncthreads();
-#ifdef FL_DIAG_PRIO
-  if (w >= 4) __builtin_amdgcn_s_setprio(1);
-#endif
-  for (int c = 0; c < nch; ++c) {
-    const int buf = c & 1;
-    if (c + 1 < nch) issue(c + 1, buf ^ 1);
-    if (active) {
-      f16v sa = {};
+  auto chunk = [&](const bf16x8* sk, const bf16x8* sr, const float2* si) __attribute__((always_inline)) {
+    f16v sa = {};
 #pragma unroll
-      for (int s = 0; s < NS; ++s)
-        sa = mfma_split<NT>(sk[buf][s * 192 + lane], sk[buf][s * 192 + 64 + lane], sk[buf][s * 192 + 128 + lane],
-                            wk[s][0], wk[s][1], wk[s][2], sa);
-      // dZ for (row acc32_row(r, hh), item l32); db summed per chunk first
-      float cdb = 0.f;
+    for (int s = 0; s < NS; ++s)
+      sa = mfma_split<NT>(sk[s * 192 + lane], sk[s * 192 + 64 + lane], sk[s * 192 + 128 + lane], wk[s][0], wk[s][1],
+                          wk[s][2], sa);
+    // dZ for (row acc32_row(r, hh), item l32); db summed per chunk first
+    float cdb = 0.f;
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const f4 i0 = *reinterpret_cast<const f4*>(&si[buf][8 * q + 4 * hh]);
-        const f4 i1 = *reinterpret_cast<const f4*>(&si[buf][8 * q + 4 * hh + 2]);
+    for (int q = 0; q < 4; ++q) {
+      const f4 i0 = *reinterpret_cast<const f4*>(&si[8 * q + 4 * hh]);
+      const f4 i1 = *reinterpret_cast<const f4*>(&si[8 * q + 4 * hh + 2]);
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const float lse2 = u < 2 ? i0[2 * u] : i1[2 * (u - 2)];
-          const int tb = __float_as_int(u < 2 ? i0[2 * u + 1] : i1[2 * (u - 2) + 1]);
-          const float e = __builtin_amdgcn_exp2f(fmaf(sa[4 * q + u] + bj, L2E, -lse2));
-          const float p = g * (e - (tb == item ? 1.f : 0.f));
-          sa[4 * q + u] = p;
-          cdb += p;
-        }
+      for (int u = 0; u < 4; ++u) {
+        const float lse2 = u < 2 ? i0[2 * u] : i1[2 * (u - 2)];
+        const int tb = __float_as_int(u < 2 ? i0[2 * u + 1] : i1[2 * (u - 2) + 1]);
+        const float e = __builtin_amdgcn_exp2f(fmaf(sa[4 * q + u] + bj, L2E, -lse2));
+        const float p = g * (e - (tb == item ? 1.f : 0.f));
+        sa[4 * q + u] = p;
+        cdb += p;
       }
-      dbs += cdb;
-      bf16x8 q0[2], q1[2], q2[2];
-#pragma unroll
-      for (int s = 0; s < 2; ++s)
-        split3x8(f4{sa[8 * s], sa[8 * s + 1], sa[8 * s + 2], sa[8 * s + 3]},
-                 f4{sa[8 * s + 4], sa[8 * s + 5], sa[8 * s + 6], sa[8 * s + 7]}, q0[s], q1[s], q2[s]);
-#pragma unroll
-      for (int t = 0; t < NTL; ++t)
-#pragma unroll
-        for (int s = 0; s < 2; ++s) {
-          const int e = (t * 2 + s) * 192 + lane;
-          dw[t] = mfma_split<NT>(q0[s], q1[s], q2[s], sr[buf][e], sr[buf][e + 64], sr[buf][e + 128], dw[t]);
-        }
     }
-#ifndef FL_DIAG_NOSYNC
+    dbs += cdb;
+    bf16x8 q0[2], q1[2], q2[2];
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+      split3x8(f4{sa[8 * s], sa[8 * s + 1], sa[8 * s + 2], sa[8 * s + 3]},
+               f4{sa[8 * s + 4], sa[8 * s + 5], sa[8 * s + 6], sa[8 * s + 7]}, q0[s], q1[s], q2[s]);
+#pragma unroll
+    for (int t = 0; t < NTL; ++t)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const int e = (t * 2 + s) * 192 + lane;
+        dw[t] = mfma_split<NT>(q0[s], q1[s], q2[s], sr[e], sr[e + 64], sr[e + 128], dw[t]);
+      }
+  };
+  for (int c = 0; c < nch; c += 2) {
+    if (c + 1 < nch) FL_ISSUE(c + 1, sk1, sr1, si1);
+    if (active) chunk(sk0, sr0, si0);
     __syncthreads();
-#endif
+    if (c + 1 < nch) {
+      if (c + 2 < nch) FL_ISSUE(c + 2, sk0, sr0, si0);
+      if (active) chunk(sk1, sr1, si1);
+      __syncthreads();
+    }
   }
+#undef FL_ISSUE
   if (!active) return;
   dbs += __shfl_xor(dbs, 32);
   if (hh == 0 && item < A) {

@@ -279,52 +279,264 @@ extern "C" int rg_head_fwd_xp(const void* hplanes, const float* W, const float* 
                               int terms, int rpb, float* ZT, int64_t ldz, float* pmax, float* psum, int32_t* parg,
                               int want_sum, hipStream_t stream);
 
-// bytes of scratch rg_sampled_fwd_x needs (the two plane buffers)
+// --------------------------------------------- split-bf16 logits GEMM ----
+// Zᵀ = Wneg·hᵀ + b from operand planes already in MFMA fragment order
+// ([32-row block][16-deep slice j][plane p][lane] × 16 B, lane (hh, n) holding
+// row n, k = 16j + 8hh .. +8): the negatives' planes Wk (k_sampled_prep, or
+// the trunk gather's fused negative prep rg_gather_neg) and h's planes Hk
+// (k_sampled_prep, or the GRU forward's epilogue).  No VALU besides the
+// epilogue.
+//
+// Workgroup = 512 threads = 8 waves over 256 negatives × 128 rows; grid.x =
+// negative tiles, so the dispatch's XCD round-robin keeps a tile's 32 row
+// tiles on one XCD (its A planes are fetched into one L2).  Wave w holds the
+// planes of negatives 256·bx + 32w in VGPRs (3·HF/16 coalesced 1 KB loads);
+// the four 32-row chunks of h's planes go global → LDS by DMA into four
+// separate arrays (the compiler then orders each chunk's reads after that
+// chunk's DMA only).  Issue order: chunk 0's DMA, the A loads, chunks 1-3's
+// DMA; chunk c is waited for with vmcnt(#younger DMA) + s_barrier, and slice
+// j's MFMAs wait only for slice j's A loads, so the MFMAs start before the A
+// planes have all landed.  Accumulators alternate: chunk c's epilogue (+
+// bias, Zᵀ buffer stores with scalar offsets, max / Σexp per (32-negative
+// block, row)) issues under chunk c+1's MFMAs.
+constexpr int SG_NEG = 256;   // negatives per workgroup (8 waves × 32)
+constexpr int SG_ROWS = 128;  // rows per workgroup (4 chunks of 32)
+
+__device__ __forceinline__ void sg_lds_dma(const void* src, void* lds_wave_base) {
+  __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)const_cast<void*>(src),
+                                   (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0, 0);
+}
+
+// s_waitcnt vmcnt(N) with lgkmcnt / expcnt left free (gfx9 encoding)
+#define SG_VMCNT(N) __builtin_amdgcn_s_waitcnt(((N) & 0xF) | (((N) >> 4) << 14) | (0x7 << 4) | (0xF << 8))
+
+template <int HF, int NT>
+__global__ __launch_bounds__(512) void k_sampled_gemm(const bf16x8* __restrict__ Wk, const float* __restrict__ bg,
+                                                      const bf16x8* __restrict__ Hk, int B, int S,
+                                                      float* __restrict__ ZT, int64_t ldz,
+                                                      float* __restrict__ pmax, float* __restrict__ psum) {
+  constexpr int NS = HF / 16;
+  constexpr int CH = NS * 192;              // 16-B fragments of one 32-row chunk's planes
+  constexpr int NPC = CH / 64;              // 1 KB DMA pieces per chunk
+  constexpr int PPW = (NPC + 7) / 8;        // pieces per wave per chunk (duplicates pad the last round)
+  constexpr float L2E = 1.4426950408889634f;
+  __shared__ bf16x8 hc0[CH], hc1[CH], hc2[CH], hc3[CH];
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, hh = lane >> 5, l32 = lane & 31;
+  const int s0 = blockIdx.x * SG_NEG + 32 * w;
+  const bool nact = s0 < S;                 // S % 32 == 0
+  const int rbase = blockIdx.y * SG_ROWS;
+  const int nch = min(SG_ROWS, B - rbase) / 32;   // B % 32 == 0
+#ifdef SG_STAMP
+  const uint64_t t_start = __builtin_amdgcn_s_memtime();
+#endif
+  const bf16x8* __restrict__ hsrc = Hk + (int64_t)(rbase / 32) * CH;
+  // chunks past nch re-fetch chunk 0 (keeps the per-wave DMA count uniform;
+  // never read).  A macro: the DMA's LDS operand must name its array.
+#define SG_DMA(C, DST)                                                                                     \
+  do {                                                                                                      \
+    const int cs_ = (C) < nch ? (C) : 0;                                                                    \
+    _Pragma("unroll") for (int i = 0; i < PPW; ++i) {                                                       \
+      const int q = (w + 8 * i) % NPC;                                                                      \
+      sg_lds_dma(hsrc + (int64_t)cs_ * CH + 64 * q + lane, &DST[64 * q]);                                   \
+    }                                                                                                       \
+  } while (0)
+  // bias of accumulator row acc32_row(r, hh): four runs of 4 negatives (no
+  // lane shuffles here: an LDS-class instruction would make the compiler wait
+  // for every outstanding DMA)
+  f4 bq[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) bq[q] = *reinterpret_cast<const f4*>(bg + (nact ? s0 : 0) + 8 * q + 4 * hh);
+  // the scheduling barriers pin the vector-memory issue order the vmcnt
+  // waits below count on: bias, chunk 0's DMA, A planes, chunks 1-3's DMA
+  __builtin_amdgcn_sched_barrier(0);
+  SG_DMA(0, hc0);
+  __builtin_amdgcn_sched_barrier(0);
+  bf16x8 a[NS][3];
+  const bf16x8* __restrict__ asrc = Wk + (int64_t)(nact ? s0 / 32 : 0) * CH + lane;
+#pragma unroll
+  for (int j = 0; j < NS; ++j)
+#pragma unroll
+    for (int p = 0; p < 3; ++p) a[j][p] = asrc[j * 192 + p * 64];
+  __builtin_amdgcn_sched_barrier(0);
+  SG_DMA(1, hc1);
+  SG_DMA(2, hc2);
+  SG_DMA(3, hc3);
+  __builtin_amdgcn_sched_barrier(0);
+  float bj[16];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) bj[r] = bq[r >> 2][r & 3];
+  // Zᵀ stores through a buffer descriptor over this wave's 32 negative rows
+  const uint64_t zb = (uint64_t)(ZT + (int64_t)(nact ? s0 : 0) * ldz);
+  const uint32_t zlo = __builtin_amdgcn_readfirstlane((uint32_t)zb);
+  const uint32_t zhi = __builtin_amdgcn_readfirstlane((uint32_t)(zb >> 32));
+  const uint32_t znb = __builtin_amdgcn_readfirstlane(nact ? (uint32_t)(32 * ldz * 4) : 0u);
+  const __amdgpu_buffer_rsrc_t zrs =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)zhi << 32) | zlo), 0, znb, 0x00020000);
+  const int zlane = (4 * hh * (int)ldz + l32) * 4;
+  const int zrow4 = __builtin_amdgcn_readfirstlane((int)ldz * 4);
+  float* __restrict__ pm = pmax + (int64_t)(s0 / 32) * B + rbase + l32;
+  float* __restrict__ ps = psum + (int64_t)(s0 / 32) * B + rbase + l32;
+  // (a macro, not a pointer-taking helper: indexing each chunk's own LDS array
+  // keeps the compiler's per-array DMA ordering)
+#define SG_MMA(HC, ACC)                                                                                  \
+  do {                                                                                                    \
+    ACC = f16v{};                                                                                         \
+    _Pragma("unroll") for (int j = 0; j < NS; ++j) ACC =                                                  \
+        mfma_split<NT>(a[j][0], a[j][1], a[j][2], HC[j * 192 + lane], HC[j * 192 + 64 + lane],            \
+                       HC[j * 192 + 128 + lane], ACC);                                                    \
+  } while (0)
+  auto epi = [&](f16v& acc, int c) __attribute__((always_inline)) {
+    float m = -__builtin_inff();
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const float z = acc[r] + bj[r];
+      acc[r] = z;
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(z), zrs, zlane,
+                                            ((r & 3) + 8 * (r >> 2)) * zrow4 + (rbase + 32 * c) * 4, 0);
+      m = fmaxf(m, z);
+    }
+    m = fmaxf(m, __shfl_xor(m, 32));
+    const float m2 = m * L2E;
+    float sum = 0.f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) sum += __builtin_amdgcn_exp2f(fmaf(acc[r], L2E, -m2));
+    sum += __shfl_xor(sum, 32);
+    if (nact && hh == 0) {
+      pm[32 * c] = m;
+      ps[32 * c] = sum;
+    }
+  };
+  auto sync = [&]() __attribute__((always_inline)) {
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  // chunk 0: wait for its DMA only (the A loads and chunks 1-3 may still fly)
+  SG_VMCNT(3 * NS + 3 * PPW);
+  sync();
+  // Waves without negatives (s0 >= S) run the MFMAs on zero planes and write
+  // nothing (their Zᵀ descriptor has no records, their partials are skipped):
+  // no branch around the MFMA chains, whose operand waits stay per-slice.
+  f16v accA, accB;
+  SG_MMA(hc0, accA);
+#ifdef SG_STAMP
+  const uint64_t t_c0 = __builtin_amdgcn_s_memtime();
+#endif
+  if (nch > 1) {
+    SG_VMCNT(2 * PPW);
+    sync();
+    SG_MMA(hc1, accB);
+    epi(accA, 0);
+  }
+  if (nch > 2) {
+    SG_VMCNT(PPW);
+    sync();
+    SG_MMA(hc2, accA);
+    epi(accB, 1);
+  }
+  if (nch > 3) {
+    SG_VMCNT(0);
+    sync();
+    SG_MMA(hc3, accB);
+    epi(accA, 2);
+    epi(accB, 3);
+  } else {
+    if (nch == 1) epi(accA, 0);
+    if (nch == 2) epi(accB, 1);
+    if (nch == 3) epi(accA, 2);
+  }
+  SG_VMCNT(0);  // no DMA may still target this workgroup's LDS when it retires
+#ifdef SG_STAMP
+  const uint64_t t_end = __builtin_amdgcn_s_memtime();
+  if (lane == 0) {  // diagnostic build only: stamps overwrite pmax (the microbench reads them back)
+    int64_t* out = reinterpret_cast<int64_t*>(pmax) + ((int64_t)(blockIdx.y * gridDim.x + blockIdx.x) * 8 + w) * 4;
+    out[0] = (int64_t)t_start;
+    out[1] = (int64_t)t_c0;
+    out[2] = (int64_t)t_end;
+    out[3] = 0;
+  }
+#endif
+#undef SG_MMA
+#undef SG_DMA
+}
+
+// bytes of scratch rg_sampled_fwd_x needs (the negatives' and h's operand planes)
 extern "C" int64_t rg_sampled_work_bytes(int B, int S, int HF) {
   if (B <= 0 || S <= 0 || HF <= 0) return RG_ERR_ARG;
   return ((int64_t)S + B) * HF * 6;
+}
+
+// The logits GEMM alone, from operand planes (k_sampled_gemm above).
+extern "C" int rg_sampled_gemm(const void* Wk, const float* bg, const void* Hk, int B, int S, int HF, int terms,
+                               float* ZT, int64_t ldz, float* pmax, float* psum, hipStream_t stream) {
+  if (B <= 0 || S <= 0 || (B % 32) || (S % 32) || !Wk || !bg || !Hk || !ZT || !pmax || !psum) return RG_ERR_ARG;
+  if (ldz < B) return RG_ERR_ARG;
+  if (terms != 6 && terms != 9) return RG_ERR_ARG;
+  const dim3 grid((unsigned)((S + SG_NEG - 1) / SG_NEG), (unsigned)((B + SG_ROWS - 1) / SG_ROWS));
+#define SGG(HFV, NTV)                                                                                          \
+  hipLaunchKernelGGL((k_sampled_gemm<HFV, NTV>), grid, dim3(512), 0, stream, (const bf16x8*)Wk, bg,          \
+                     (const bf16x8*)Hk, B, S, ZT, ldz, pmax, psum)
+#define SGT(HFV)  \
+  if (terms == 9) \
+    SGG(HFV, 9);  \
+  else            \
+    SGG(HFV, 6);
+  switch (HF) {
+    case 32: SGT(32); break;
+    case 64: SGT(64); break;
+    case 128: SGT(128); break;
+    default: return RG_ERR_SHAPE;
+  }
+#undef SGT
+#undef SGG
+  RG_LAUNCH_CHECK();
+  return RG_OK;
 }
 
 // Split-bf16 forward (terms = 9: exact products, fp32 accumulation; 6: the
 // three sub-ulp terms dropped).  Same outputs and partial blocking as the fast
 // path of rg_sampled_fwd; needs S % 32 == 0 and B % 32 == 0.  draw = 1: neg
 // is an output, filled with the rg_sample_uniform(seed, counter) draw.
+// Operand prep (draw, negatives' row gather → Wg/bg and planes, h's planes;
+// one launch), then the logits: HF <= 128 on rg_sampled_gemm, HF = 256 on
+// rg_head_fwd_xp (a 32-negative HF-256 plane set, 192 VGPRs, does not fit
+// beside the accumulators at two waves per SIMD).
 extern "C" int rg_sampled_fwd_x(const float* h, const float* W, const float* bias, int32_t* neg, int draw,
                                 uint64_t seed, uint64_t counter, int64_t A, int B, int S, int HF, int terms,
                                 float* ZT, int64_t ldz, float* pmax, float* psum, float* Wg, float* bg, void* work,
                                 hipStream_t stream) {
-  if (B <= 0 || S <= 0 || (B % 32) || (S % 32) || work == nullptr || bg == nullptr || Wg == nullptr)
+  if (B <= 0 || S <= 0 || (B % 32) || (S % 32) || work == nullptr || bg == nullptr || Wg == nullptr ||
+      ZT == nullptr)
     return RG_ERR_ARG;
-  if (ZT && ldz < B) return RG_ERR_ARG;
+  if (ldz < B) return RG_ERR_ARG;
   if (draw && (A <= 0 || A > INT32_MAX)) return RG_ERR_ARG;
   if (terms != 6 && terms != 9) return RG_ERR_ARG;
+  const bool gemm = HF <= 128;
   bf16x8* Wp = reinterpret_cast<bf16x8*>(work);
   bf16x8* Hp = Wp + (int64_t)S * HF / 8 * 3;
   const int64_t items = ((int64_t)S + B) * (HF / 8);
   const dim3 gp((unsigned)((items + 255) / 256));
+#define SXP(HFV)                                                                                            \
+  hipLaunchKernelGGL(k_sampled_prep<HFV>, gp, dim3(256), 0, stream, h, W, bias, neg, draw, seed, counter, \
+                     (uint64_t)A, B, S, Wg, bg, gemm ? Wp : (bf16x8*)nullptr, Hp)
+  switch (HF) {
+    case 32: SXP(32); break;
+    case 64: SXP(64); break;
+    case 128: SXP(128); break;
+    case 256: SXP(256); break;
+    default: return RG_ERR_SHAPE;
+  }
+#undef SXP
+  RG_LAUNCH_CHECK();
+  if (gemm) return rg_sampled_gemm(Wp, bg, Hp, B, S, HF, terms, ZT, ldz, pmax, psum, stream);
   // negatives × rows on k_head_fwd_x (csrc/head_split.hip): each wave holds
   // 32 gathered negatives' planes in VGPRs, h's planes stream through LDS; the
   // rows are split over grid.y so the S/(32·waves) negative groups fill the chip
-  const int nw = HF >= 256 ? 4 : 8;
+  const int nw = 4;
   const int ngx = (S + 32 * nw - 1) / (32 * nw);
   const int ny = max(1, 256 / ngx);
   // rows per workgroup (rows·negatives workgroups ≈ one per CU; the best of
-  // 32..512 swept at B 4096, S 2048: 128 at HF 128, 256 at HF 256)
+  // 32..512 swept at B 4096, S 2048: 256 at HF 256)
   const int rpb = ((B + ny - 1) / ny + 31) / 32 * 32;
-#define SXP(HFV)                                                                                            \
-  hipLaunchKernelGGL(k_sampled_prep<HFV>, gp, dim3(256), 0, stream, h, W, bias, neg, draw, seed, counter, \
-                     (uint64_t)A, B, S, Wg, bg, (bf16x8*)nullptr, Hp)
-#define SXH(HFV) SXP(HFV);
-  switch (HF) {
-    case 32: SXH(32); break;
-    case 64: SXH(64); break;
-    case 128: SXH(128); break;
-    case 256: SXH(256); break;
-    default: return RG_ERR_SHAPE;
-  }
-#undef SXH
-#undef SXP
-  RG_LAUNCH_CHECK();
   return rg_head_fwd_xp(Hp, Wg, bg, B, S, HF, terms, rpb, ZT, ldz, pmax, psum, nullptr, 1, stream);
 }
 

@@ -81,11 +81,17 @@ SIGNATURES = {
     "rg_sampled_nparts": [I, I, I],
     "rg_sampled_work_bytes": [I, I, I],
     "rg_sampled_fwd_x": [P, P, P, P, I, U64, U64, I64, I, I, I, I, P, I64, P, P, P, P, P, P],
+    "rg_sampled_gemm": [P, P, P, I, I, I, I, P, I64, P, P, P],
     "rg_sampled_fwd": [P, P, P, P, I, I, I, P, I64, P, P, P, P, P],
     "rg_sampled_lse": [P, P, P, P, I, I64, I, P, P, I, F, P, P, P, P, P, P, P],
     "rg_sampled_dz": [P, I64, P, I, I, F, P, P],
     "rg_weighted_sum": [P, P, I, I64, P, P],
     "rg_stack_rewards": [P, P, P, I, P, P],
+    "rg_token_ids": [P, I, I, P, P, P, I64, P, P, P],
+    "rg_shard_route": [P, P, I64, I, P, P, P, P],
+    "rg_rows_gather": [P, I, I64, I64, P, I, I, P, P, P],
+    "rg_place_rows": [P, I, P, P, P, I, I, I, P, P],
+    "rg_collect_grads": [P, P, P, P, P, I, I, P, P],
 }
 
 _lib = None

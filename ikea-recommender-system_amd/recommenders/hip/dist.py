@@ -41,6 +41,18 @@ class Comm:
         out.copy_(t.view(-1)[self.rank * n:(self.rank + 1) * n].view(out.shape))
         return out
 
+    def all_to_all(self, out, inp, out_splits, in_splits):
+        """Variable all-to-all along dim 0: rows [Σ in_splits[:q], +in_splits[q])
+        of ``inp`` go to rank q; ``out`` receives out_splits[q] rows from q."""
+        if self.native:
+            self.dist.all_to_all_single(out, inp.contiguous(), list(out_splits), list(in_splits), group=self.group)
+            return out
+        o = torch.empty((out.shape[0],) + tuple(out.shape[1:]), dtype=out.dtype)
+        self.dist.all_to_all_single(o, inp.detach().cpu().contiguous(), list(out_splits), list(in_splits),
+                                    group=self.group)
+        out.copy_(o)
+        return out
+
     def all_reduce(self, t, async_op=False):
         if self.native:
             return self.dist.all_reduce(t, group=self.group, async_op=async_op)

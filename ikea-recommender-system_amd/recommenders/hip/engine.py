@@ -162,7 +162,7 @@ class Trunk:
     unchanged), so they are not computed."""
 
     def __init__(self, gru_attr, item_num, E, H, layers, train_pad_embed, packed, pad_idx, bidir, device,
-                 fp16_embeddings=False):
+                 fp16_embeddings=False, comm=None):
         self.gru_attr = gru_attr
         self.N1 = item_num + 1
         self.E, self.H, self.layers, self.bidir = E, H, layers, bidir
@@ -176,18 +176,30 @@ class Trunk:
         # H <= 128: persistent recurrence with W_hh in VGPRs; H = 256: time-stepped
         # path (W_hh is 768 KB; csrc/gru.hip rg_gru_fwd_steps / rg_gru_bwd_steps)
         self.stepped = H > 128
-        self.emb = Param("embedding.weight", init_embedding(self.N1, E, pad_idx, train_pad_embed), device)
+        # comm (multi-GPU): the table is row-sharded, this rank holds rows
+        # [lo, hi) (full init drawn first: RNG parity with one GPU); the rows a
+        # pass needs are exchanged by all-to-all (csrc/emb_shard.hip)
+        self.comm = comm
+        full = init_embedding(self.N1, E, pad_idx, train_pad_embed)
+        if comm is not None:
+            from .dist import item_shard
+            self.lo, self.hi = item_shard(self.N1, comm.world, comm.rank)
+            full = full[self.lo:self.hi].contiguous()
+        else:
+            self.lo, self.hi = 0, self.N1
+        self.n_local = self.hi - self.lo
+        self.emb = Param("embedding.weight", full, device)
         gru = init_gru(E, H, layers, bidir)
         self.gru_params = [Param(f"{gru_attr}.{n}", t, device) for n, t in gru]
         per = 4
         self.dirs = [self.gru_params[d * per:(d + 1) * per] for d in range(self.ndir)]  # layer 0
         self.G_emb = torch.zeros_like(self.emb.p)
-        self.tags = torch.zeros(self.N1, dtype=torch.int32, device=device)
+        self.tags = torch.zeros(self.n_local, dtype=torch.int32, device=device)
         self.err = torch.zeros(1, dtype=torch.int32, device=device)  # out-of-range item ids seen
         self._ws = {}
         # fp16 embedding storage (config C5): the gather reads this copy, Adam
         # keeps the fp32 master and refreshes it in the same sweep
-        self.emb16 = torch.empty(self.N1, E, dtype=torch.float16, device=device) if fp16_embeddings else None
+        self.emb16 = torch.empty(self.n_local, E, dtype=torch.float16, device=device) if fp16_embeddings else None
         self.refresh_half()
 
     def refresh_half(self):
@@ -222,13 +234,20 @@ class Trunk:
             call("rg_pack", w.lens.data_ptr(), B, L, 0 if self.packed else 1, w.perm.data_ptr(),
                  w.lsort.data_ptr(), w.offs.data_ptr(), st)
         H, E = self.H, self.E
+        if self.comm is not None:
+            with region("gather"):
+                self._exchange_rows(w, s, B, L, st)
         for d in range(self.ndir):
             w_ih, w_hh, b_ih, b_hh = self.dirs[d]
-            with region("gather"):
-                call("rg_gather_h" if self.emb16 is not None else "rg_gather", s.data_ptr(), B, L,
-                     w.perm.data_ptr(), w.lsort.data_ptr(), w.offs.data_ptr(),
-                     (self.emb16 if self.emb16 is not None else self.emb.p).data_ptr(), self.N1, E, d,
-                     w.tok_id[d].data_ptr(), w.X[d].data_ptr(), self.err.data_ptr(), st)
+            if self.comm is None:
+                with region("gather"):
+                    call("rg_gather_h" if self.emb16 is not None else "rg_gather", s.data_ptr(), B, L,
+                         w.perm.data_ptr(), w.lsort.data_ptr(), w.offs.data_ptr(),
+                         (self.emb16 if self.emb16 is not None else self.emb.p).data_ptr(), self.N1, E, d,
+                         w.tok_id[d].data_ptr(), w.X[d].data_ptr(), self.err.data_ptr(), st)
+            else:
+                call("rg_place_rows", w.rows_in.data_ptr(), 1 if self.emb16 is not None else 0, w.slot.data_ptr(),
+                     w.lsort.data_ptr(), w.offs.data_ptr(), B, E, d, w.X[d].data_ptr(), st)
             with region("gemm_ih"):
                 call("rg_gemm_f32", w.X[d].data_ptr(), E, 1, w_ih.p.data_ptr(), 1, E, w.Gi[d].data_ptr(), 3 * H,
                      b_ih.p.data_ptr(), w.TM, w.ntok_ptr, 3 * H, E, None, 1, st)
@@ -273,14 +292,7 @@ class Trunk:
             for prm, sl in ((w_ih, w.sl_ih[d]), (w_hh, w.sl_hh[d]), (b_ih, w.cs_ih[d]), (b_hh, w.cs_hh[d])):
                 call("rg_adam_slabs", prm.p.data_ptr(), prm.m.data_ptr(), prm.v.data_ptr(), sl.data_ptr(), S,
                      prm.numel(), adam6, None, st)
-        with region("adam_emb"):
-            if self.emb16 is not None:
-                call("rg_adam_rows_h", self.emb.p.data_ptr(), self.emb.m.data_ptr(), self.emb.v.data_ptr(),
-                     self.G_emb.data_ptr(), self.tags.data_ptr(), tag, self.N1, self.E, adam6,
-                     self.emb16.data_ptr(), st)
-            else:
-                call("rg_adam_rows", self.emb.p.data_ptr(), self.emb.m.data_ptr(), self.emb.v.data_ptr(),
-                     self.G_emb.data_ptr(), self.tags.data_ptr(), tag, self.N1, self.E, adam6, st)
+        self._adam_emb(adam6, tag)
         self._pending = None
 
     def _grads(self, w, S, tag):
@@ -299,9 +311,13 @@ class Trunk:
                      w.sl_ih[d].data_ptr(), w.cs_ih[d].data_ptr(), st)
                 call("rg_wgrad", w.dGh[d].data_ptr(), 3 * H, w.saved[d].data_ptr(), H, TM, w.ntok_ptr, S,
                      w.sl_hh[d].data_ptr(), w.cs_hh[d].data_ptr(), st)
+            if self.comm is None:
+                with region("scatter"):
+                    call("rg_scatter_add", w.tok_id[d].data_ptr(), w.dX[d].data_ptr(), E, w.ntok_ptr, TM, skip,
+                         self.G_emb.data_ptr(), self.tags.data_ptr(), tag, st)
+        if self.comm is not None:
             with region("scatter"):
-                call("rg_scatter_add", w.tok_id[d].data_ptr(), w.dX[d].data_ptr(), E, w.ntok_ptr, TM, skip,
-                     self.G_emb.data_ptr(), self.tags.data_ptr(), tag, st)
+                self._exchange_grads(w, tag, st)
 
     # ---- data-parallel variant: gradients summed over ranks before Adam ----
     def grads_for_allreduce(self, tag):
@@ -309,6 +325,7 @@ class Trunk:
         embedding: the dense G_emb table) ready for a SUM all-reduce."""
         w, S = self._pending
         self._grads(w, S, tag)
+        self._tag = tag
         if getattr(self, "gflat", None) is None:
             n = sum(p.numel() for p in self.gru_params[:4 * self.ndir])
             self.gflat = torch.zeros(n, device=self.device)
@@ -322,7 +339,9 @@ class Trunk:
                 off += n
 
     def allreduce_start(self, comm):
-        return [comm.all_reduce(self.gflat, async_op=True), comm.all_reduce(self.G_emb, async_op=True)]
+        """SUM all-reduce of the GRU gradients (~0.4 MB; the embedding rows went
+        to their owners by all-to-all in _exchange_grads)."""
+        return [comm.all_reduce(self.gflat, async_op=True)]
 
     def adam_after_allreduce(self, adam6):
         st = stream_ptr()
@@ -333,14 +352,68 @@ class Trunk:
                 call("rg_adam_dense", prm.p.data_ptr(), prm.m.data_ptr(), prm.v.data_ptr(),
                      self.gflat.data_ptr() + 4 * off, n, adam6, 0, st)
                 off += n
-        with region("adam_emb"):
-            if self.emb16 is not None:  # dense all-reduced gradient: every row, table cleared
-                call("rg_adam_rows_h", self.emb.p.data_ptr(), self.emb.m.data_ptr(), self.emb.v.data_ptr(),
-                     self.G_emb.data_ptr(), None, 0, self.N1, self.E, adam6, self.emb16.data_ptr(), st)
-            else:
-                call("rg_adam_dense", self.emb.p.data_ptr(), self.emb.m.data_ptr(), self.emb.v.data_ptr(),
-                     self.G_emb.data_ptr(), self.emb.numel(), adam6, 1, st)
+        self._adam_emb(adam6, self._tag)
         self._pending = None
+
+    def _adam_emb(self, adam6, tag):
+        """Dense-semantics Adam over this rank's rows (all of them on one GPU):
+        row-sparse gradient rows tagged with this step's epoch."""
+        st = stream_ptr()
+        with region("adam_emb"):
+            if self.emb16 is not None:
+                call("rg_adam_rows_h", self.emb.p.data_ptr(), self.emb.m.data_ptr(), self.emb.v.data_ptr(),
+                     self.G_emb.data_ptr(), self.tags.data_ptr(), tag, self.n_local, self.E, adam6,
+                     self.emb16.data_ptr(), st)
+            else:
+                call("rg_adam_rows", self.emb.p.data_ptr(), self.emb.m.data_ptr(), self.emb.v.data_ptr(),
+                     self.G_emb.data_ptr(), self.tags.data_ptr(), tag, self.n_local, self.E, adam6, st)
+
+    # ---- row-sharded table: id / row / gradient exchange (csrc/emb_shard.hip) ----
+    def _exchange_rows(self, w, s, B, L, st):
+        """Rows of every packed token of this rank's batch from their owners:
+        route by owner, all-to-all the ids, owners gather, all-to-all the rows."""
+        comm, W = self.comm, self.comm.world
+        if getattr(w, "slot", None) is None:
+            w.slot = torch.empty(w.TM, dtype=torch.int32, device=self.device)
+            w.send_ids = torch.empty(w.TM, dtype=torch.int32, device=self.device)
+            w.counts = torch.zeros(W, dtype=torch.int32, device=self.device)
+            w.counts_all = torch.zeros(W * W, dtype=torch.int32, device=self.device)
+        call("rg_token_ids", s.data_ptr(), B, L, w.perm.data_ptr(), w.lsort.data_ptr(), w.offs.data_ptr(), self.N1,
+             w.tok_id[0].data_ptr(), self.err.data_ptr(), st)
+        call("rg_shard_route", w.tok_id[0].data_ptr(), w.ntok_ptr, self.N1, W, w.slot.data_ptr(),
+             w.send_ids.data_ptr(), w.counts.data_ptr(), st)
+        comm.all_gather(w.counts_all, w.counts)
+        M = w.counts_all.view(W, W).cpu()            # M[q][r]: tokens of rank q owned by rank r (one sync)
+        w.send_splits = M[comm.rank].tolist()
+        w.recv_splits = M[:, comm.rank].tolist()
+        T, R = sum(w.send_splits), sum(w.recv_splits)
+        w.T, w.R = T, R
+        half = self.emb16 is not None
+        rdt = torch.float16 if half else torch.float32
+        w.recv_ids = torch.empty(max(R, 1), dtype=torch.int32, device=self.device)
+        w.local_ids = torch.empty(max(R, 1), dtype=torch.int32, device=self.device)
+        w.nrecv = torch.tensor([R], dtype=torch.int32, device=self.device)
+        comm.all_to_all(w.recv_ids[:R], w.send_ids[:T], w.recv_splits, w.send_splits)
+        rows_out = torch.empty(max(R, 1), self.E, dtype=rdt, device=self.device)
+        call("rg_rows_gather", w.recv_ids.data_ptr(), R, self.lo, self.n_local,
+             (self.emb16 if half else self.emb.p).data_ptr(), self.E, 1 if half else 0, rows_out.data_ptr(),
+             w.local_ids.data_ptr(), st)
+        w.rows_in = torch.empty(max(T, 1), self.E, dtype=rdt, device=self.device)
+        comm.all_to_all(w.rows_in[:T], rows_out[:R], w.send_splits, w.recv_splits)
+
+    def _exchange_grads(self, w, tag, st):
+        """Row-gradients of this rank's tokens to their owners; the owner adds
+        them into its gradient rows (tagged for the row-sparse Adam)."""
+        comm = self.comm
+        gsend = torch.empty(max(w.T, 1), self.E, device=self.device)
+        call("rg_collect_grads", w.dX[0].data_ptr(), w.dX[1].data_ptr() if self.ndir == 2 else None,
+             w.slot.data_ptr(), w.lsort.data_ptr(), w.offs.data_ptr(), w.B, self.E, gsend.data_ptr(), st)
+        grecv = torch.empty(max(w.R, 1), self.E, device=self.device)
+        comm.all_to_all(grecv[:w.R], gsend[:w.T], w.recv_splits, w.send_splits)
+        pad = self.pad - self.lo
+        skip = -1 if self.train_pad or not (0 <= pad < self.n_local) else pad
+        call("rg_scatter_add", w.local_ids.data_ptr(), grecv.data_ptr(), self.E, w.nrecv.data_ptr(), max(w.R, 1),
+             skip, self.G_emb.data_ptr(), self.tags.data_ptr(), tag, st)
 
 
 # ----------------------------------------------------------------- heads ----

@@ -35,8 +35,11 @@ class HipNet:
         self.padding_idx = self.item_num if padding_idx is None else padding_idx
         self.dropout_p = float(dropout)
         self.training = True
+        # with comm (multi-GPU) the item table is row-sharded across the ranks
+        # (csrc/emb_shard.hip) and every head item-sharded (sharded.py)
         self.trunk = Trunk(trunk_attr, self.item_num, embedding_dim, hidden_dim, gru_layers, train_pad_embed,
-                           use_packed_seq, self.padding_idx, bidir, self.device, fp16_embeddings=fp16_embeddings)
+                           use_packed_seq, self.padding_idx, bidir, self.device, fp16_embeddings=fp16_embeddings,
+                           comm=comm)
         self.hf = hidden_dim * (2 if bidir else 1)
         self.comm = comm
         shard = None
@@ -75,18 +78,39 @@ class HipNet:
         return out
 
     def state_dict(self):
+        """Reference key names.  On an item-sharded (multi-GPU) model the
+        item tables are this rank's rows: ``shard_ranges()`` gives them."""
         return OrderedDict((p.name, p.p.detach()) for p in self.named_param_objs())
 
+    def shard_ranges(self):
+        """name -> (lo, hi) row range this rank holds of every item-indexed
+        parameter (the full range on one GPU)."""
+        out = {"embedding.weight": (self.trunk.lo, self.trunk.hi)}
+        for hd in list(self.heads.values()) + list(getattr(self, "q_heads", [])):
+            out[hd.W.name] = out[hd.b.name] = (hd.lo, hd.hi)
+        return out
+
     def load_state_dict(self, sd, strict=True):
+        """Copies the reference-keyed tensors in; full-size item tables are
+        sliced to this rank's rows on an item-sharded model."""
         objs = {p.name: p for p in self.named_param_objs()}
         missing = [k for k in objs if k not in sd]
         unexpected = [k for k in sd if k not in objs]
         if strict and (missing or unexpected):
             raise RuntimeError(f"state_dict mismatch: missing={missing} unexpected={unexpected}")
+        ranges = self.shard_ranges()
         with torch.no_grad():
             for k, v in sd.items():
-                if k in objs:
-                    objs[k].p.copy_(torch.as_tensor(v).to(objs[k].p.device, torch.float32))
+                if k not in objs:
+                    continue
+                t = torch.as_tensor(v)
+                dst = objs[k].p
+                if tuple(t.shape) != tuple(dst.shape) and k in ranges:
+                    lo, hi = ranges[k]
+                    t = t[lo:hi]
+                if tuple(t.shape) != tuple(dst.shape):
+                    raise RuntimeError(f"size mismatch for {k}: got {tuple(t.shape)}, model {tuple(dst.shape)}")
+                dst.copy_(t.to(dst.device, torch.float32))
         self.trunk.refresh_half()
         return self
 

@@ -273,6 +273,11 @@ int64_t rg_sampled_work_bytes(int B, int S, int HF);
 int rg_sampled_fwd_x(const float* h, const float* W, const float* bias, int32_t* neg, int draw, uint64_t seed,
                      uint64_t counter, int64_t A, int B, int S, int HF, int terms, float* ZT, int64_t ldz,
                      float* pmax, float* psum, float* Wg, float* bg, void* work, rg_stream_t stream);
+/* The logits GEMM of rg_sampled_fwd_x alone, from operand planes already in MFMA fragment
+ * order ([32-row block][16-deep slice][plane][lane] × 16 B): Wk the negatives' planes, Hk h's.
+ * HF in {32, 64, 128}; B % 32 == 0, S % 32 == 0; partials as rg_sampled_nparts(B, S, terms). */
+int rg_sampled_gemm(const void* Wk, const float* bg, const void* Hk, int B, int S, int HF, int terms, float* ZT,
+                    int64_t ldz, float* pmax, float* psum, rg_stream_t stream);
 /* per row: z_pos = h_b·W[a_b] + bias[a_b]; lse over {z_pos} ∪ partials; loss_row = lse − z_pos;
  * ids[b] = a_b; dzpos = (exp(z_pos − lse) − 1)·g; gpos = dzpos·h_b; dhpos = dzpos·W[a_b] */
 int rg_sampled_lse(const float* h, const float* W, const float* bias, const int64_t* tgt, int B, int64_t A, int HF,
@@ -281,6 +286,29 @@ int rg_sampled_lse(const float* h, const float* W, const float* bias, const int6
 /* in place dZᵀ = exp(Zᵀ − lse)·g; dbg[s] = Σ_b dZᵀ[s][b] */
 int rg_sampled_dz(float* ZT, int64_t ldz, const float* lse, int B, int S, float gscale, float* dbg,
                   rg_stream_t stream);
+
+/* ---- §8e row-sharded item-embedding table (csrc/emb_shard.hip): the multi-GPU form of
+ * self.embedding(s) and its dense gradient + Adam (GRU4Rec/model.py:35-47, 69, 150-153).  Rank r
+ * holds rows [⌊r·n_rows/world⌋, ⌊(r+1)·n_rows/world⌋).  Per trunk pass:
+ * rg_token_ids: tok_id[t] = item id of packed token t (forward time order; -1 + err if invalid).
+ * rg_shard_route: stable partition of the T = *ntok_ptr tokens by owner rank: slot[t] (send
+ *   position), send_ids[slot[t]] = tok_id[t], counts[world] (world <= 8).
+ * rg_rows_gather: owner side, rows of n received global ids from the local shard [lo, lo + n_local)
+ *   (fp32, or fp16 when half = 1) and local_ids (id − lo, or -1 with a zero row).
+ * rg_place_rows: X[t] = rows_in[slot[t]] widened to fp32; reverse = 1: each row's valid prefix
+ *   reversed (the backward direction of BidirGRU4Rec).
+ * rg_collect_grads: gsend[slot[t]] = dX0[t] + dX1[rev t] (dX1 optional) — the row-gradients each
+ *   owner adds into its rows (rg_scatter_add with local_ids) before rg_adam_rows on its shard. */
+int rg_token_ids(const int64_t* s, int B, int L, const int32_t* perm, const int32_t* lsort, const int32_t* offs,
+                 int64_t n_rows, int32_t* tok_id, int32_t* err, rg_stream_t stream);
+int rg_shard_route(const int32_t* tok_id, const int32_t* ntok_ptr, int64_t n_rows, int world, int32_t* slot,
+                   int32_t* send_ids, int32_t* counts, rg_stream_t stream);
+int rg_rows_gather(const int32_t* ids, int n, int64_t lo, int64_t n_local, const void* table, int E, int half,
+                   void* rows, int32_t* local_ids, rg_stream_t stream);
+int rg_place_rows(const void* rows_in, int half, const int32_t* slot, const int32_t* lsort, const int32_t* offs, int B,
+                  int E, int reverse, float* X, rg_stream_t stream);
+int rg_collect_grads(const float* dX0, const float* dX1, const int32_t* slot, const int32_t* lsort,
+                     const int32_t* offs, int B, int E, float* gsend, rg_stream_t stream);
 
 /* items per online-softmax partial block of rg_head_fwd: pmax/psum/parg hold ceil(A/that) x B */
 int rg_partial_block(void);

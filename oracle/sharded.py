@@ -82,3 +82,32 @@ def sharded_topk(scores_local, K, lo, comm):
             out[i, q] = best[1]
             pos[best[2]] += 1
     return out
+
+
+def sharded_embedding(tok_local, table_shard, lo, n_rows, comm, dX_local=None):
+    """Row-sharded nn.Embedding (csrc/emb_shard.hip) restated with plain
+    collectives: every token's row fetched from its owner (route by owner,
+    all-to-all of ids, owner gathers, all-to-all of rows back); with dX_local
+    the row-gradients sent back to the owners and summed into the owner's
+    rows.  Returns (X_local, dtable_shard)."""
+    world, rank = comm.world, comm.rank
+    own = ((tok_local + 1) * world + n_rows - 1) // n_rows - 1
+    order = torch.sort(own, stable=True).indices
+    send_ids = tok_local[order]
+    counts = torch.bincount(own, minlength=world)
+    M = comm.all_gather(torch.empty(world * world, dtype=torch.int64), counts).view(world, world)
+    send, recv = M[rank].tolist(), M[:, rank].tolist()
+    ids_in = torch.empty(sum(recv), dtype=torch.int64)
+    comm.dist.all_to_all_single(ids_in, send_ids, recv, send)
+    rows_out = table_shard[ids_in - lo]
+    rows_in = torch.empty(sum(send), table_shard.shape[1], dtype=table_shard.dtype)
+    comm.dist.all_to_all_single(rows_in, rows_out, send, recv)
+    X = torch.empty_like(rows_in)
+    X[order] = rows_in
+    if dX_local is None:
+        return X, None
+    g_in = torch.empty(sum(recv), table_shard.shape[1], dtype=dX_local.dtype)
+    comm.dist.all_to_all_single(g_in, dX_local[order].contiguous(), recv, send)
+    dtab = torch.zeros_like(table_shard)
+    dtab.index_add_(0, ids_in - lo, g_in)
+    return X, dtab

@@ -67,6 +67,21 @@ def _worker(rank, world, port, q):
         assert torch.equal(sharded_argmax(loc, lo, comm_f), torch.argmax(S, 1))
         for K in (1, 3, 7):
             assert torch.equal(sharded_topk(loc, K, lo, comm_f), canonical_topk(S, K))
+        # row-sharded item table: rows and row-gradients through the all-to-all
+        # exchange equal a full-table gather and the dense embedding gradient
+        from oracle.sharded import sharded_embedding
+        N1, E = 53, 4
+        table = torch.randn(N1, E, generator=gen, dtype=torch.float64)
+        toks = [torch.randint(0, N1, (n,), generator=gen) for n in (17, 23)][:world]
+        toks[0][:3] = N1 - 1                 # the pad row (last rank's shard) from every rank
+        dXs = [torch.randn(len(t), E, generator=gen, dtype=torch.float64) for t in toks]
+        elo, ehi = item_shard(N1, world, rank)
+        X, dtab = sharded_embedding(toks[rank], table[elo:ehi], elo, N1, comm_f, dXs[rank])
+        assert torch.equal(X, table[toks[rank]])
+        full = torch.zeros(N1, E, dtype=torch.float64)
+        for t, d in zip(toks, dXs):
+            full.index_add_(0, t, d)
+        assert torch.allclose(dtab, full[elo:ehi], atol=1e-12)
         q.put((rank, "ok"))
     except Exception as e:  # pragma: no cover - reported to the parent
         q.put((rank, repr(e)))

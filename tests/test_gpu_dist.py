@@ -42,6 +42,7 @@ def _rank(rank, port, out, precision):
     try:
         from recommenders.models.GRU4Rec.model import GRU4Rec_trainer
         tr = GRU4Rec_trainer(device="cuda:0", shard_items=True, matmul_precision=precision, **CFG)
+        assert tr.gru_model.trunk.n_local < CFG["item_num"] + 1   # the item table is row-sharded
         losses = []
         for s, a, r, sn, ln, nln, e in _batches():
             sl = slice(rank * B, (rank + 1) * B)
@@ -76,9 +77,10 @@ def test_item_sharded_step_equals_single_gpu_global_batch(precision):
         g = np.load(os.path.join(out, f"rank{rank}.npz"))
         np.testing.assert_allclose(g["losses"], ref_losses, rtol=0, atol=1e-4)
         lo, hi = item_shard(CFG["action_dim"], WORLD, rank)
+        elo, ehi = item_shard(CFG["item_num"] + 1, WORLD, rank)
         for k, v in sd.items():
             got = g[k]
-            want = v[lo:hi] if k.startswith("output.") else v
+            want = v[lo:hi] if k.startswith("output.") else (v[elo:ehi] if k == "embedding.weight" else v)
             d = np.abs(got - want)
             assert d.max() <= 2 * lr + 1e-5, (rank, k, float(d.max()))
             assert (d > 1e-4).mean() < 1e-3, (rank, k)

@@ -78,6 +78,8 @@ def _rank(rank, port, out, kind, topk):
 
 @pytest.mark.parametrize("kind,topk", [("sqn", None), ("smorl", (1, 1)), ("smorl", (3, 2))])
 def test_item_sharded_double_q_equals_single_gpu_global_batch(kind, topk):
+    """Heads item-sharded and the item table row-sharded (ids / rows /
+    row-gradients exchanged by all-to-all, csrc/emb_shard.hip)."""
     sys.path.insert(0, os.path.join(REPO, "ikea-recommender-system_amd"))
     out = tempfile.mkdtemp()
     ctx = mp.get_context("spawn")
@@ -96,12 +98,15 @@ def test_item_sharded_double_q_equals_single_gpu_global_batch(kind, topk):
         g = np.load(os.path.join(out, f"rank{rank}.npz"))
         np.testing.assert_allclose(g["losses"], ref_losses, rtol=0, atol=1e-4)
         lo, hi = item_shard(N, WORLD, rank)
+        elo, ehi = item_shard(N + 1, WORLD, rank)   # the row-sharded item table (pad row included)
         for i, net in enumerate(_nets(ref)):
             for k, v in net.state_dict().items():
                 got = g[f"n{i}.{k}"]
                 want = v.cpu().numpy()
                 if "head" in k or k.startswith("output."):
                     want = want[lo:hi]
+                elif k == "embedding.weight":
+                    want = want[elo:ehi]
                 d = np.abs(got - want)
                 assert d.max() <= 2 * lr + 1e-5, (rank, i, k, float(d.max()))
                 assert (d > 1e-4).mean() < 1e-3, (rank, i, k)

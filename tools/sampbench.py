@@ -18,6 +18,8 @@ ap.add_argument("--A", type=int, default=1_000_000)
 ap.add_argument("--HF", type=int, nargs="+", default=[128, 256])
 ap.add_argument("--iters", type=int, default=50)
 ap.add_argument("--prec", nargs="+", default=["f32", "f32x9", "f32x6"])
+ap.add_argument("--stamps", action="store_true", help="SL_STAMP build: print per-wave phase cycles")
+ap.add_argument("--parts", action="store_true", help="also time the plane-fed GEMM alone (HF <= 128)")
 a = ap.parse_args()
 dev = "cuda"
 for HF in a.HF:
@@ -38,12 +40,15 @@ for HF in a.HF:
     st = stream_ptr()
     fl = 2.0 * B * S * HF
     for prec in a.prec:
+        it = [0]
+
         def run():
+            it[0] += 1  # a fresh draw every launch: the negatives' rows come from HBM as in a step
             if prec == "f32":
                 call("rg_sampled_fwd", h.data_ptr(), W.data_ptr(), bias.data_ptr(), neg.data_ptr(), B, S, HF,
                      ZT.data_ptr(), ldz, pm.data_ptr(), ps.data_ptr(), Wg.data_ptr(), bg.data_ptr(), st)
             else:
-                call("rg_sampled_fwd_x", h.data_ptr(), W.data_ptr(), bias.data_ptr(), neg.data_ptr(), 1, 7, 0, A, B,
+                call("rg_sampled_fwd_x", h.data_ptr(), W.data_ptr(), bias.data_ptr(), neg.data_ptr(), 1, 7, it[0], A, B,
                      S, HF, 9 if prec == "f32x9" else 6, ZT.data_ptr(), ldz, pm.data_ptr(), ps.data_ptr(),
                      Wg.data_ptr(), bg.data_ptr(), work.data_ptr(), st)
         for _ in range(3):
@@ -58,3 +63,44 @@ for HF in a.HF:
         us = e0.elapsed_time(e1) / a.iters * 1e3
         print(f"HF {HF} {prec:6s} {us:8.2f} us  {fl / us / 1e6:7.1f} TFLOP/s  Z write {B * S * 4 / us / 1e3:6.0f} GB/s",
               flush=True)
+        if a.parts and prec != "f32" and HF <= 128:
+            Wp = work[:S * HF * 6]
+            Hp = work[S * HF * 6:]
+            terms = 9 if prec == "f32x9" else 6
+
+            def gemm():
+                call("rg_sampled_gemm", Wp.data_ptr(), bg.data_ptr(), Hp.data_ptr(), B, S, HF, terms, ZT.data_ptr(),
+                     ldz, pm.data_ptr(), ps.data_ptr(), st)
+            for _ in range(3):
+                gemm()
+            torch.cuda.synchronize()
+            e0.record()
+            for _ in range(a.iters):
+                gemm()
+            e1.record()
+            torch.cuda.synchronize()
+            ug = e0.elapsed_time(e1) / a.iters * 1e3
+            print(f"   gemm alone {ug:8.2f} us  {fl / ug / 1e6:7.1f} TFLOP/s  ({terms * fl / ug / 1e6 / 2500:.3f} of bf16 peak)",
+                  flush=True)
+            if a.stamps:
+                import numpy as np
+                gemm()
+                torch.cuda.synchronize()
+                nwg = (S // 256) * (B // 128)
+                t = pm.reshape(-1).view(torch.int64)[:nwg * 8 * 4].view(nwg * 8, 4).cpu().numpy().astype(np.float64)
+                print(f"   gemm stamps: to end of chunk-0 MFMA issue median {np.median(t[:, 1] - t[:, 0]):.0f} "
+                      f"(p90 {np.percentile(t[:, 1] - t[:, 0], 90):.0f}), rest median {np.median(t[:, 2] - t[:, 1]):.0f}"
+                      f" (p90 {np.percentile(t[:, 2] - t[:, 1], 90):.0f}) cycles")
+        if a.stamps and prec != "f32" and HF > 128:
+            import numpy as np
+            run()
+            torch.cuda.synchronize()
+            nwg = (S // 128) * max(1, 256 // (S // 128))
+            t = Wg.reshape(-1).view(torch.int64)[:nwg * 8 * 4].view(nwg * 8, 4).cpu().numpy().astype(np.float64)
+            t0 = t[:, 0].min()
+            for name, col in (("start", 0), ("prologue", 1), ("end", 2)):
+                v = t[:, col] - t0
+                print(f"  {name:9s} cycles from first start: p10 {np.percentile(v, 10):8.0f} "
+                      f"median {np.median(v):8.0f} p90 {np.percentile(v, 90):8.0f} max {v.max():8.0f}")
+            print(f"  prologue len median {np.median(t[:, 1] - t[:, 0]):.0f}, loop len median "
+                  f"{np.median(t[:, 2] - t[:, 1]):.0f} cycles")
