@@ -274,126 +274,187 @@ __global__ __launch_bounds__(256) void k_sampled_prep(const float* __restrict__ 
   dst[plane_idx(x >> 5, j, 2, lane, NS)] = p2;
 }
 
+extern "C" int rg_reduce_slabs(const float* slabs, int nslab, int64_t n, float* out, const float* bias, int ncol,
+                               int accumulate, hipStream_t stream);
+
 // split-bf16 logits kernel shared with the full-softmax head (csrc/head_split.hip)
 extern "C" int rg_head_fwd_xp(const void* hplanes, const float* W, const float* bias, int B, int A, int HF,
                               int terms, int rpb, float* ZT, int64_t ldz, float* pmax, float* psum, int32_t* parg,
                               int want_sum, hipStream_t stream);
 
-// --------------------------------------------- split-bf16 logits GEMM ----
-// Zᵀ = Wneg·hᵀ + b from operand planes already in MFMA fragment order
-// ([32-row block][16-deep slice j][plane p][lane] × 16 B, lane (hh, n) holding
-// row n, k = 16j + 8hh .. +8): the negatives' planes Wk (k_sampled_prep, or
-// the trunk gather's fused negative prep rg_gather_neg) and h's planes Hk
-// (k_sampled_prep, or the GRU forward's epilogue).  No VALU besides the
-// epilogue.
+// ------------------------------------- fused split-bf16 logits (HF <= 128) ----
+// The north-star step's logits (GRU4Rec at C2 shapes) in ONE
+// launch: draw, the negatives' row gather, both operands' exact bf16 split,
+// the split-bf16 MFMAs, Z and the (max, Σexp) partials.  Z is stored ROW-major
+// (B × ldz, negatives contiguous), so every lane writes its accumulator as
+// four 16-B runs of 4 negatives (a quarter of the store instructions of the
+// Zᵀ layout).
 //
-// Workgroup = 512 threads = 8 waves over 256 negatives × 128 rows; grid.x =
-// negative tiles, so the dispatch's XCD round-robin keeps a tile's 32 row
-// tiles on one XCD (its A planes are fetched into one L2).  Wave w holds the
-// planes of negatives 256·bx + 32w in VGPRs (3·HF/16 coalesced 1 KB loads);
-// the four 32-row chunks of h's planes go global → LDS by DMA into four
-// separate arrays (the compiler then orders each chunk's reads after that
-// chunk's DMA only).  Issue order: chunk 0's DMA, the A loads, chunks 1-3's
-// DMA; chunk c is waited for with vmcnt(#younger DMA) + s_barrier, and slice
-// j's MFMAs wait only for slice j's A loads, so the MFMAs start before the A
-// planes have all landed.  Accumulators alternate: chunk c's epilogue (+
-// bias, Zᵀ buffer stores with scalar offsets, max / Σexp per (32-negative
-// block, row)) issues under chunk c+1's MFMAs.
-constexpr int SG_NEG = 256;   // negatives per workgroup (8 waves × 32)
-constexpr int SG_ROWS = 128;  // rows per workgroup (4 chunks of 32)
+// Workgroup = 512 threads = 8 waves over 256 negatives × 128 rows (grid.x
+// negative tiles, grid.y row tiles; an XCD takes whole row tiles with every
+// negative tile, so h and the negatives' rows are re-read from its L2).  Wave
+// w owns negatives 256·bx + 32w: its 32 fp32 rows are loaded straight into
+// the MFMA A-fragment layout (lane (hh, n): row n, k = 16j + 8hh .. +8) and
+// split slice by slice right before chunk 0's MFMAs of that slice, so the
+// MFMAs start while the rest of the rows are in flight (only plain loads are
+// in flight there, so the compiler's vmcnt waits stay per slice).  The 128
+// rows of h arrive as four 32-row chunks: fp32 loads into registers one chunk
+// ahead, split once by the workgroup into a two-buffer LDS ring in B-fragment
+// order (lane-linear 16-B writes), one barrier (LDS only, no memory fence) per
+// chunk.  Accumulators alternate, so chunk c's epilogue (+ bias, Z stores,
+// max / Σexp) issues under chunk c+1's MFMAs.  Bytes per CU: 128 KB of W rows
+// + 64 KB of h (fp32) in, 128 KB of Z out.
+//
+// Measured at B 4096, S 2048, HF 128 (tools/sampbench.py, MI355X): 24 µs;
+// a per-wave stamp breakdown puts ~40% in the prologue (the W rows' fragment
+// loads) and the rest at ~2× the MFMA time — see DESIGN.md §4 for the
+// variants tried (plane-fed GEMM, LDS-DMA row images, sliced epilogues).
+constexpr int SF_NEG = 256;   // negatives per workgroup (8 waves × 32)
+constexpr int SF_ROWS = 128;  // rows per workgroup (4 chunks of 32)
 
-__device__ __forceinline__ void sg_lds_dma(const void* src, void* lds_wave_base) {
-  __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)const_cast<void*>(src),
-                                   (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0, 0);
-}
-
-// s_waitcnt vmcnt(N) with lgkmcnt / expcnt left free (gfx9 encoding)
-#define SG_VMCNT(N) __builtin_amdgcn_s_waitcnt(((N) & 0xF) | (((N) >> 4) << 14) | (0x7 << 4) | (0xF << 8))
-
-template <int HF, int NT>
-__global__ __launch_bounds__(512) void k_sampled_gemm(const bf16x8* __restrict__ Wk, const float* __restrict__ bg,
-                                                      const bf16x8* __restrict__ Hk, int B, int S,
-                                                      float* __restrict__ ZT, int64_t ldz,
-                                                      float* __restrict__ pmax, float* __restrict__ psum) {
+template <int HF, int NT, bool DRAW>
+__global__ __launch_bounds__(512) void k_sampled_logits(const float* __restrict__ h, const float* __restrict__ W,
+                                                        const float* __restrict__ bias, int32_t* __restrict__ neg,
+                                                        uint64_t seed, uint64_t counter, uint64_t A, int B, int S,
+                                                        float* __restrict__ Z, int64_t ldz, float* __restrict__ pmax,
+                                                        float* __restrict__ psum, float* __restrict__ Wg,
+                                                        float* __restrict__ bg) {
   constexpr int NS = HF / 16;
   constexpr int CH = NS * 192;              // 16-B fragments of one 32-row chunk's planes
-  constexpr int NPC = CH / 64;              // 1 KB DMA pieces per chunk
-  constexpr int PPW = (NPC + 7) / 8;        // pieces per wave per chunk (duplicates pad the last round)
+  constexpr int ITEMS = 32 * (HF / 8);      // (row, 8-value group) items of one chunk
+  constexpr int IPT = (ITEMS + 511) / 512;  // per thread (1 at HF <= 128)
   constexpr float L2E = 1.4426950408889634f;
-  __shared__ bf16x8 hc0[CH], hc1[CH], hc2[CH], hc3[CH];
+  __shared__ bf16x8 hsA[CH], hsB[CH];
+  __shared__ __attribute__((aligned(16))) float sbias[SF_NEG];
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, hh = lane >> 5, l32 = lane & 31;
-  const int s0 = blockIdx.x * SG_NEG + 32 * w;
+  int bx = blockIdx.x, by = blockIdx.y;
+  {
+    const int gx = gridDim.x, gy = gridDim.y;
+    if ((gy & 7) == 0) {  // XCD i % 8 takes row tiles ≡ i (mod 8) with every negative tile
+      const int i = blockIdx.y * gx + blockIdx.x;
+      const int k = i >> 3;
+      by = (i & 7) + 8 * (k / gx);
+      bx = k % gx;
+    }
+  }
+  const int tile = bx * SF_NEG;
+  const int s0 = tile + 32 * w;
   const bool nact = s0 < S;                 // S % 32 == 0
-  const int rbase = blockIdx.y * SG_ROWS;
-  const int nch = min(SG_ROWS, B - rbase) / 32;   // B % 32 == 0
-#ifdef SG_STAMP
-  const uint64_t t_start = __builtin_amdgcn_s_memtime();
-#endif
-  const bf16x8* __restrict__ hsrc = Hk + (int64_t)(rbase / 32) * CH;
-  // chunks past nch re-fetch chunk 0 (keeps the per-wave DMA count uniform;
-  // never read).  A macro: the DMA's LDS operand must name its array.
-#define SG_DMA(C, DST)                                                                                     \
-  do {                                                                                                      \
-    const int cs_ = (C) < nch ? (C) : 0;                                                                    \
-    _Pragma("unroll") for (int i = 0; i < PPW; ++i) {                                                       \
-      const int q = (w + 8 * i) % NPC;                                                                      \
-      sg_lds_dma(hsrc + (int64_t)cs_ * CH + 64 * q + lane, &DST[64 * q]);                                   \
-    }                                                                                                       \
-  } while (0)
-  // bias of accumulator row acc32_row(r, hh): four runs of 4 negatives (no
-  // lane shuffles here: an LDS-class instruction would make the compiler wait
-  // for every outstanding DMA)
-  f4 bq[4];
+  const bool emit = by == 0;                // row tile 0 publishes ids, Wg, bg
+  const int rbase = by * SF_ROWS;
+  const int nch = min(SF_ROWS, B - rbase) / 32;   // B % 32 == 0
+  // ---- h chunk staging: item i -> (group g, row) with the row fastest
+  f4 st[IPT][2];
+  auto load_h = [&](int c) __attribute__((always_inline)) {
 #pragma unroll
-  for (int q = 0; q < 4; ++q) bq[q] = *reinterpret_cast<const f4*>(bg + (nact ? s0 : 0) + 8 * q + 4 * hh);
-  // the scheduling barriers pin the vector-memory issue order the vmcnt
-  // waits below count on: bias, chunk 0's DMA, A planes, chunks 1-3's DMA
-  __builtin_amdgcn_sched_barrier(0);
-  SG_DMA(0, hc0);
-  __builtin_amdgcn_sched_barrier(0);
-  bf16x8 a[NS][3];
-  const bf16x8* __restrict__ asrc = Wk + (int64_t)(nact ? s0 / 32 : 0) * CH + lane;
+    for (int q = 0; q < IPT; ++q) {
+      const int i = tid + 512 * q;
+      if (i < ITEMS) {
+        const float* src = h + (int64_t)(rbase + 32 * c + (i & 31)) * HF + 8 * (i >> 5);
+        st[q][0] = *reinterpret_cast<const f4*>(src);
+        st[q][1] = *reinterpret_cast<const f4*>(src + 4);
+      }
+    }
+  };
+  auto store_h = [&](bf16x8* hs) __attribute__((always_inline)) {
 #pragma unroll
-  for (int j = 0; j < NS; ++j)
+    for (int q = 0; q < IPT; ++q) {
+      const int i = tid + 512 * q;
+      if (i < ITEMS) {
+        const int g = i >> 5;
+        bf16x8 p0, p1, p2;
+        split3x8(st[q][0], st[q][1], p0, p1, p2);
+        const int e = (g >> 1) * 192 + (g & 1) * 32 + (i & 31);
+        hs[e] = p0;
+        hs[e + 64] = p1;
+        hs[e + 128] = p2;
+      }
+    }
+  };
+  // ---- this wave's negatives: draw, bias, fp32 rows in A-fragment layout.
+  // Vector-memory issue order: bias, h chunk 0, the W rows, h chunk 1;
+  // branch-free (a wave without negatives gathers row 0 and stores nothing).
+  int id;
+  const int s_me = nact ? s0 + l32 : 0;
+  if (DRAW) {
+    const uint64_t z = mix64(seed + 0x9E3779B97F4A7C15ull * (counter * (uint64_t)S + (uint64_t)s_me + 1ull));
+    id = nact ? (int32_t)__umul64hi(z, A) : 0;
+  } else {
+    id = neg[s_me];
+    id = (A > 0 && (uint64_t)(int64_t)id >= A) ? 0 : id;   // guard the gather (callers validate ids)
+  }
+  const float bl = bias[id];
+  load_h(0);
+  f4 wr[NS][2];
+  {
+    const float* src = W + (int64_t)id * HF + 8 * hh;
 #pragma unroll
-    for (int p = 0; p < 3; ++p) a[j][p] = asrc[j * 192 + p * 64];
+    for (int j = 0; j < NS; ++j) {
+      wr[j][0] = *reinterpret_cast<const f4*>(src + 16 * j);
+      wr[j][1] = *reinterpret_cast<const f4*>(src + 16 * j + 4);
+    }
+  }
   __builtin_amdgcn_sched_barrier(0);
-  SG_DMA(1, hc1);
-  SG_DMA(2, hc2);
-  SG_DMA(3, hc3);
-  __builtin_amdgcn_sched_barrier(0);
-  float bj[16];
-#pragma unroll
-  for (int r = 0; r < 16; ++r) bj[r] = bq[r >> 2][r & 3];
-  // Zᵀ stores through a buffer descriptor over this wave's 32 negative rows
-  const uint64_t zb = (uint64_t)(ZT + (int64_t)(nact ? s0 : 0) * ldz);
-  const uint32_t zlo = __builtin_amdgcn_readfirstlane((uint32_t)zb);
-  const uint32_t zhi = __builtin_amdgcn_readfirstlane((uint32_t)(zb >> 32));
-  const uint32_t znb = __builtin_amdgcn_readfirstlane(nact ? (uint32_t)(32 * ldz * 4) : 0u);
-  const __amdgpu_buffer_rsrc_t zrs =
-      __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)zhi << 32) | zlo), 0, znb, 0x00020000);
-  const int zlane = (4 * hh * (int)ldz + l32) * 4;
-  const int zrow4 = __builtin_amdgcn_readfirstlane((int)ldz * 4);
+  store_h(hsA);
+  if (nch > 1) load_h(1);
+  if (hh == 0) sbias[32 * w + l32] = bl;
+  // barrier without a memory fence: only the LDS writes must be complete
+  // (the W rows and h chunk 1 stay in flight); same for every barrier below
+  auto sync_lds = [&]() __attribute__((always_inline)) {
+    __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0), vmcnt / expcnt free
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  sync_lds();
   float* __restrict__ pm = pmax + (int64_t)(s0 / 32) * B + rbase + l32;
   float* __restrict__ ps = psum + (int64_t)(s0 / 32) * B + rbase + l32;
-  // (a macro, not a pointer-taking helper: indexing each chunk's own LDS array
-  // keeps the compiler's per-array DMA ordering)
-#define SG_MMA(HC, ACC)                                                                                  \
-  do {                                                                                                    \
-    ACC = f16v{};                                                                                         \
-    _Pragma("unroll") for (int j = 0; j < NS; ++j) ACC =                                                  \
-        mfma_split<NT>(a[j][0], a[j][1], a[j][2], HC[j * 192 + lane], HC[j * 192 + 64 + lane],            \
-                       HC[j * 192 + 128 + lane], ACC);                                                    \
-  } while (0)
+  bf16x8 a0[NS], a1[NS], a2[NS];
+  // chunk 0: each A slice is split right before its MFMAs
+  f16v accA = {}, accB = {};
+#pragma unroll
+  for (int j = 0; j < NS; ++j) {
+    split3x8(wr[j][0], wr[j][1], a0[j], a1[j], a2[j]);
+    accA = mfma_split<NT>(a0[j], a1[j], a2[j], hsA[j * 192 + lane], hsA[j * 192 + 64 + lane],
+                          hsA[j * 192 + 128 + lane], accA);
+  }
+  // row tile 0 publishes the draw and the gathered rows (the backward's Wg / bg)
+  if (emit && nact) {
+    if (hh == 0) {
+      if (DRAW) neg[s0 + l32] = id;
+      if (bg) bg[s0 + l32] = bl;
+    }
+    if (Wg) {
+      float* dst = Wg + (int64_t)(s0 + l32) * HF + 8 * hh;
+#pragma unroll
+      for (int j = 0; j < NS; ++j) {
+        *reinterpret_cast<f4*>(dst + 16 * j) = wr[j][0];
+        *reinterpret_cast<f4*>(dst + 16 * j + 4) = wr[j][1];
+      }
+    }
+  }
+  auto mma = [&](const bf16x8* hs, f16v& acc) __attribute__((always_inline)) {
+    acc = f16v{};
+#pragma unroll
+    for (int j = 0; j < NS; ++j)
+      acc = mfma_split<NT>(a0[j], a1[j], a2[j], hs[j * 192 + lane], hs[j * 192 + 64 + lane], hs[j * 192 + 128 + lane],
+                           acc);
+  };
+  // epilogue of chunk c: lane (hh, n) holds row rbase + 32c + n, negatives
+  // s0 + acc32_row(r, hh): four runs of 4 consecutive negatives
   auto epi = [&](f16v& acc, int c) __attribute__((always_inline)) {
     float m = -__builtin_inff();
+    float* zrow = Z + (int64_t)(rbase + 32 * c + l32) * ldz + s0 + 4 * hh;
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const float z = acc[r] + bj[r];
-      acc[r] = z;
-      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(z), zrs, zlane,
-                                            ((r & 3) + 8 * (r >> 2)) * zrow4 + (rbase + 32 * c) * 4, 0);
-      m = fmaxf(m, z);
+    for (int q = 0; q < 4; ++q) {
+      const f4 bq = *reinterpret_cast<const f4*>(&sbias[32 * w + 8 * q + 4 * hh]);
+      f4 z;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        z[u] = acc[4 * q + u] + bq[u];
+        acc[4 * q + u] = z[u];
+        m = fmaxf(m, z[u]);
+      }
+      *reinterpret_cast<f4*>(zrow + 8 * q) = z;
     }
     m = fmaxf(m, __shfl_xor(m, 32));
     const float m2 = m * L2E;
@@ -401,62 +462,97 @@ __global__ __launch_bounds__(512) void k_sampled_gemm(const bf16x8* __restrict__
 #pragma unroll
     for (int r = 0; r < 16; ++r) sum += __builtin_amdgcn_exp2f(fmaf(acc[r], L2E, -m2));
     sum += __shfl_xor(sum, 32);
-    if (nact && hh == 0) {
+    if (hh == 0) {
       pm[32 * c] = m;
       ps[32 * c] = sum;
     }
   };
-  auto sync = [&]() __attribute__((always_inline)) {
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
+  // chunk c (>= 1): its rows (in registers since chunk c-1) are split into LDS
+  // buffer c & 1 (last read by chunk c-2, before the previous barrier), chunk
+  // c+1's rows are loaded, and its MFMAs carry chunk c-1's epilogue
+  auto step = [&](int c, bf16x8* hs_cur, f16v& acc_new, f16v& acc_old) __attribute__((always_inline)) {
+    store_h(hs_cur);
+    if (c + 1 < nch) load_h(c + 1);
+    sync_lds();
+    if (nact) {
+      mma(hs_cur, acc_new);
+      epi(acc_old, c - 1);
+    }
   };
-  // chunk 0: wait for its DMA only (the A loads and chunks 1-3 may still fly)
-  SG_VMCNT(3 * NS + 3 * PPW);
-  sync();
-  // Waves without negatives (s0 >= S) run the MFMAs on zero planes and write
-  // nothing (their Zᵀ descriptor has no records, their partials are skipped):
-  // no branch around the MFMA chains, whose operand waits stay per-slice.
-  f16v accA, accB;
-  SG_MMA(hc0, accA);
-#ifdef SG_STAMP
-  const uint64_t t_c0 = __builtin_amdgcn_s_memtime();
-#endif
-  if (nch > 1) {
-    SG_VMCNT(2 * PPW);
-    sync();
-    SG_MMA(hc1, accB);
-    epi(accA, 0);
-  }
-  if (nch > 2) {
-    SG_VMCNT(PPW);
-    sync();
-    SG_MMA(hc2, accA);
-    epi(accB, 1);
-  }
-  if (nch > 3) {
-    SG_VMCNT(0);
-    sync();
-    SG_MMA(hc3, accB);
-    epi(accA, 2);
-    epi(accB, 3);
-  } else {
+  if (nch > 1) step(1, hsB, accB, accA);
+  if (nch > 2) step(2, hsA, accA, accB);
+  if (nch > 3) step(3, hsB, accB, accA);
+  if (nact) {
     if (nch == 1) epi(accA, 0);
     if (nch == 2) epi(accB, 1);
     if (nch == 3) epi(accA, 2);
+    if (nch == 4) epi(accB, 3);
   }
-  SG_VMCNT(0);  // no DMA may still target this workgroup's LDS when it retires
-#ifdef SG_STAMP
-  const uint64_t t_end = __builtin_amdgcn_s_memtime();
-  if (lane == 0) {  // diagnostic build only: stamps overwrite pmax (the microbench reads them back)
-    int64_t* out = reinterpret_cast<int64_t*>(pmax) + ((int64_t)(blockIdx.y * gridDim.x + blockIdx.x) * 8 + w) * 4;
-    out[0] = (int64_t)t_start;
-    out[1] = (int64_t)t_c0;
-    out[2] = (int64_t)t_end;
-    out[3] = 0;
+}
+
+// The fused forward (k_sampled_logits): Z row-major (B × ldz, ldz >= S).
+extern "C" int rg_sampled_logits(const float* h, const float* W, const float* bias, int32_t* neg, int draw,
+                                 uint64_t seed, uint64_t counter, int64_t A, int B, int S, int HF, int terms,
+                                 float* Z, int64_t ldz, float* pmax, float* psum, float* Wg, float* bg,
+                                 hipStream_t stream) {
+  if (B <= 0 || S <= 0 || (B % 32) || (S % 32) || !h || !W || !bias || !neg || !Z || !pmax || !psum || !bg)
+    return RG_ERR_ARG;
+  if (ldz < S || (ldz & 3)) return RG_ERR_ARG;
+  if (draw && (A <= 0 || A > INT32_MAX)) return RG_ERR_ARG;
+  if (terms != 6 && terms != 9) return RG_ERR_ARG;
+  const dim3 grid((unsigned)((S + SF_NEG - 1) / SF_NEG), (unsigned)((B + SF_ROWS - 1) / SF_ROWS));
+#define SFG(HFV, NTV)                                                                                            \
+  if (draw)                                                                                                        \
+    hipLaunchKernelGGL((k_sampled_logits<HFV, NTV, true>), grid, dim3(512), 0, stream, h, W, bias, neg, seed,     \
+                       counter, (uint64_t)A, B, S, Z, ldz, pmax, psum, Wg, bg);                                   \
+  else                                                                                                             \
+    hipLaunchKernelGGL((k_sampled_logits<HFV, NTV, false>), grid, dim3(512), 0, stream, h, W, bias, neg, seed,    \
+                       counter, (uint64_t)(A > 0 ? A : 0), B, S, Z, ldz, pmax, psum, Wg, bg)
+#define SFT(HFV)  \
+  if (terms == 9) \
+    SFG(HFV, 9);  \
+  else            \
+    SFG(HFV, 6);
+  switch (HF) {
+    case 32: SFT(32); break;
+    case 64: SFT(64); break;
+    case 128: SFT(128); break;
+    default: return RG_ERR_SHAPE;
   }
-#endif
-#undef SG_MMA
-#undef SG_DMA
+#undef SFT
+#undef SFG
+  RG_LAUNCH_CHECK();
+  return RG_OK;
+}
+
+// dZ = exp(Z − lse)·g in place for the row-major Z of rg_sampled_logits, and
+// the bias gradient dbg[s] = Σ_b dZ[b][s]: workgroup (s block of 256, row
+// block of 128) writes its column sums to slab[row block][s]; the slabs are
+// then summed in order (deterministic).
+__global__ __launch_bounds__(256) void k_sampled_dz_rows(float* __restrict__ Z, int64_t ldz,
+                                                         const float* __restrict__ lse, int B, int S, float g,
+                                                         float* __restrict__ slabs) {
+  const int s = blockIdx.x * 256 + threadIdx.x;
+  const int b0 = blockIdx.y * 128, b1 = min(B, b0 + 128);
+  if (s >= S) return;
+  float acc = 0.f;
+  for (int b = b0; b < b1; ++b) {
+    float* p = Z + (int64_t)b * ldz + s;
+    const float d = __expf(*p - lse[b]) * g;
+    *p = d;
+    acc += d;
+  }
+  slabs[(int64_t)blockIdx.y * S + s] = acc;
+}
+
+extern "C" int rg_sampled_dz_rows(float* Z, int64_t ldz, const float* lse, int B, int S, float gscale, float* slabs,
+                                  float* dbg, hipStream_t stream) {
+  if (B <= 0 || S <= 0 || ldz < S || !Z || !lse || !slabs || !dbg) return RG_ERR_ARG;
+  const int nrb = (B + 127) / 128;
+  hipLaunchKernelGGL(k_sampled_dz_rows, dim3((S + 255) / 256, nrb), dim3(256), 0, stream, Z, ldz, lse, B, S, gscale,
+                     slabs);
+  RG_LAUNCH_CHECK();
+  return rg_reduce_slabs(slabs, nrb, S, dbg, nullptr, S, 0, stream);
 }
 
 // bytes of scratch rg_sampled_fwd_x needs (the negatives' and h's operand planes)
@@ -465,41 +561,13 @@ extern "C" int64_t rg_sampled_work_bytes(int B, int S, int HF) {
   return ((int64_t)S + B) * HF * 6;
 }
 
-// The logits GEMM alone, from operand planes (k_sampled_gemm above).
-extern "C" int rg_sampled_gemm(const void* Wk, const float* bg, const void* Hk, int B, int S, int HF, int terms,
-                               float* ZT, int64_t ldz, float* pmax, float* psum, hipStream_t stream) {
-  if (B <= 0 || S <= 0 || (B % 32) || (S % 32) || !Wk || !bg || !Hk || !ZT || !pmax || !psum) return RG_ERR_ARG;
-  if (ldz < B) return RG_ERR_ARG;
-  if (terms != 6 && terms != 9) return RG_ERR_ARG;
-  const dim3 grid((unsigned)((S + SG_NEG - 1) / SG_NEG), (unsigned)((B + SG_ROWS - 1) / SG_ROWS));
-#define SGG(HFV, NTV)                                                                                          \
-  hipLaunchKernelGGL((k_sampled_gemm<HFV, NTV>), grid, dim3(512), 0, stream, (const bf16x8*)Wk, bg,          \
-                     (const bf16x8*)Hk, B, S, ZT, ldz, pmax, psum)
-#define SGT(HFV)  \
-  if (terms == 9) \
-    SGG(HFV, 9);  \
-  else            \
-    SGG(HFV, 6);
-  switch (HF) {
-    case 32: SGT(32); break;
-    case 64: SGT(64); break;
-    case 128: SGT(128); break;
-    default: return RG_ERR_SHAPE;
-  }
-#undef SGT
-#undef SGG
-  RG_LAUNCH_CHECK();
-  return RG_OK;
-}
-
 // Split-bf16 forward (terms = 9: exact products, fp32 accumulation; 6: the
-// three sub-ulp terms dropped).  Same outputs and partial blocking as the fast
-// path of rg_sampled_fwd; needs S % 32 == 0 and B % 32 == 0.  draw = 1: neg
-// is an output, filled with the rg_sample_uniform(seed, counter) draw.
-// Operand prep (draw, negatives' row gather → Wg/bg and planes, h's planes;
-// one launch), then the logits: HF <= 128 on rg_sampled_gemm, HF = 256 on
-// rg_head_fwd_xp (a 32-negative HF-256 plane set, 192 VGPRs, does not fit
-// beside the accumulators at two waves per SIMD).
+// three sub-ulp terms dropped) in the Zᵀ layout of rg_sampled_fwd; needs
+// S % 32 == 0 and B % 32 == 0.  draw = 1: neg is an output, filled with the
+// rg_sample_uniform(seed, counter) draw.  Two launches: operand prep (draw,
+// the negatives' row gather -> Wg/bg, h's planes), then rg_head_fwd_xp with
+// the gathered rows as the items.  (HF <= 128 trainers use the one-launch
+// row-major rg_sampled_logits above.)
 extern "C" int rg_sampled_fwd_x(const float* h, const float* W, const float* bias, int32_t* neg, int draw,
                                 uint64_t seed, uint64_t counter, int64_t A, int B, int S, int HF, int terms,
                                 float* ZT, int64_t ldz, float* pmax, float* psum, float* Wg, float* bg, void* work,
@@ -510,14 +578,12 @@ extern "C" int rg_sampled_fwd_x(const float* h, const float* W, const float* bia
   if (ldz < B) return RG_ERR_ARG;
   if (draw && (A <= 0 || A > INT32_MAX)) return RG_ERR_ARG;
   if (terms != 6 && terms != 9) return RG_ERR_ARG;
-  const bool gemm = HF <= 128;
-  bf16x8* Wp = reinterpret_cast<bf16x8*>(work);
-  bf16x8* Hp = Wp + (int64_t)S * HF / 8 * 3;
+  bf16x8* Hp = reinterpret_cast<bf16x8*>(work) + (int64_t)S * HF / 8 * 3;
   const int64_t items = ((int64_t)S + B) * (HF / 8);
   const dim3 gp((unsigned)((items + 255) / 256));
 #define SXP(HFV)                                                                                            \
   hipLaunchKernelGGL(k_sampled_prep<HFV>, gp, dim3(256), 0, stream, h, W, bias, neg, draw, seed, counter, \
-                     (uint64_t)A, B, S, Wg, bg, gemm ? Wp : (bf16x8*)nullptr, Hp)
+                     (uint64_t)A, B, S, Wg, bg, (bf16x8*)nullptr, Hp)
   switch (HF) {
     case 32: SXP(32); break;
     case 64: SXP(64); break;
@@ -527,15 +593,14 @@ extern "C" int rg_sampled_fwd_x(const float* h, const float* W, const float* bia
   }
 #undef SXP
   RG_LAUNCH_CHECK();
-  if (gemm) return rg_sampled_gemm(Wp, bg, Hp, B, S, HF, terms, ZT, ldz, pmax, psum, stream);
   // negatives × rows on k_head_fwd_x (csrc/head_split.hip): each wave holds
   // 32 gathered negatives' planes in VGPRs, h's planes stream through LDS; the
   // rows are split over grid.y so the S/(32·waves) negative groups fill the chip
-  const int nw = 4;
+  const int nw = HF >= 256 ? 4 : 8;
   const int ngx = (S + 32 * nw - 1) / (32 * nw);
   const int ny = max(1, 256 / ngx);
   // rows per workgroup (rows·negatives workgroups ≈ one per CU; the best of
-  // 32..512 swept at B 4096, S 2048: 256 at HF 256)
+  // 32..512 swept at B 4096, S 2048: 128 at HF 128, 256 at HF 256)
   const int rpb = ((B + ny - 1) / ny + 31) / 32 * 32;
   return rg_head_fwd_xp(Hp, Wg, bg, B, S, HF, terms, rpb, ZT, ldz, pmax, psum, nullptr, 1, stream);
 }

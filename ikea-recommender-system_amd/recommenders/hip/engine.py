@@ -632,10 +632,17 @@ class _SampledWS:
     def __init__(self, B, S, HF, device, terms=0):
         z = lambda *s, dt=torch.float32: torch.empty(*s, dtype=dt, device=device)
         self.B, self.S = B, S
-        self.ldz = _round_up(B, 4)
-        self.terms = terms  # 0: native fp32 forward, 6 / 9: split-bf16 (rg_sampled_fwd_x)
+        self.terms = terms  # 0: native fp32 forward, 6 / 9: split-bf16 (rg_sampled_logits / rg_sampled_fwd_x)
         self.nT = call("rg_sampled_nparts", B, S, terms)  # (max, Σexp) partials per row
-        self.ZT = z(S, self.ldz)
+        # logits layout: the fused split forward (HF <= 128, csrc/sampled.hip
+        # k_sampled_logits) stores Z row-major (B × ldz, negatives contiguous);
+        # the other forwards store Zᵀ (S × ldz, rows contiguous)
+        self.zrow = terms != 0 and HF <= 128
+        self.ldz = _round_up(S, 4) if self.zrow else _round_up(B, 4)
+        self.ZT = z(B, self.ldz) if self.zrow else z(S, self.ldz)
+        # (stride over batch rows, stride over negatives) of the logits
+        self.zs_b, self.zs_s = (self.ldz, 1) if self.zrow else (1, self.ldz)
+        self.dbslabs = z((B + 127) // 128, S) if self.zrow else None
         self.pmax = z(self.nT, B)
         self.psum = z(self.nT, B)
         self.lse = z(B)
@@ -701,7 +708,11 @@ class SampledSoftmaxHead(SoftmaxHead):
         g = _f32(1.0 / B)
         split = w.terms != 0
         with region("sampled_fwd"):  # the negatives' row gather is part of the timed logits step
-            if split:  # draw + gather + operand split fused into one prep launch
+            if split and w.zrow:  # one launch: draw, row gather, operand split, logits, partials
+                call("rg_sampled_logits", h.data_ptr(), self.W.p.data_ptr(), self.b.p.data_ptr(), w.ids.data_ptr(),
+                     1, self.seed, self.draws, self.A, B, self.S, self.HF, w.terms, w.ZT.data_ptr(), w.ldz,
+                     w.pmax.data_ptr(), w.psum.data_ptr(), w.Wg.data_ptr(), w.bg.data_ptr(), st)
+            elif split:  # draw + gather + operand split fused into one prep launch
                 if w.work is None:
                     w.work = torch.empty(call("rg_sampled_work_bytes", B, self.S, self.HF), dtype=torch.uint8,
                                          device=self.device)
@@ -731,14 +742,18 @@ class SampledSoftmaxHead(SoftmaxHead):
         if gscale is not None and gscale != g:
             raise NotImplementedError("sampled softmax: the loss scale is fixed at 1/B (set in forward_loss)")
         with region("sampled_bwd"):
-            call("rg_sampled_dz", w.ZT.data_ptr(), w.ldz, w.lse.data_ptr(), B, S, g, w.gb.data_ptr(), st)
+            if w.zrow:
+                call("rg_sampled_dz_rows", w.ZT.data_ptr(), w.ldz, w.lse.data_ptr(), B, S, g, w.dbslabs.data_ptr(),
+                     w.gb.data_ptr(), st)
+            else:
+                call("rg_sampled_dz", w.ZT.data_ptr(), w.ldz, w.lse.data_ptr(), B, S, g, w.gb.data_ptr(), st)
             # dh = dZ · Wg (+ the positive part already in slab 0)
-            call("rg_gemm_f32", w.ZT.data_ptr(), 1, w.ldz, w.Wg.data_ptr(), HF, 1,
+            call("rg_gemm_f32", w.ZT.data_ptr(), w.zs_b, w.zs_s, w.Wg.data_ptr(), HF, 1,
                  w.dh_slabs.data_ptr() + 4 * B * HF, HF, None, B, None, HF, S, None, w.dh_splits, st)
             call("rg_reduce_slabs", w.dh_slabs.data_ptr(), w.dh_splits + 1, B * HF, dh_out.data_ptr(), None, HF, 0,
                  st)
             # dWg = dZᵀ · h  -> rows [0, S) of the scatter list
-            call("rg_gemm_f32", w.ZT.data_ptr(), w.ldz, 1, h.data_ptr(), HF, 1, w.dw_slabs.data_ptr(), HF, None,
+            call("rg_gemm_f32", w.ZT.data_ptr(), w.zs_s, w.zs_b, h.data_ptr(), HF, 1, w.dw_slabs.data_ptr(), HF, None,
                  S, None, HF, B, None, w.dw_splits, st)
             call("rg_reduce_slabs", w.dw_slabs.data_ptr(), w.dw_splits, S * HF, w.grows.data_ptr(), None, HF, 0,
                  st)

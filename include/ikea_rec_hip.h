@@ -273,11 +273,16 @@ int64_t rg_sampled_work_bytes(int B, int S, int HF);
 int rg_sampled_fwd_x(const float* h, const float* W, const float* bias, int32_t* neg, int draw, uint64_t seed,
                      uint64_t counter, int64_t A, int B, int S, int HF, int terms, float* ZT, int64_t ldz,
                      float* pmax, float* psum, float* Wg, float* bg, void* work, rg_stream_t stream);
-/* The logits GEMM of rg_sampled_fwd_x alone, from operand planes already in MFMA fragment
- * order ([32-row block][16-deep slice][plane][lane] × 16 B): Wk the negatives' planes, Hk h's.
- * HF in {32, 64, 128}; B % 32 == 0, S % 32 == 0; partials as rg_sampled_nparts(B, S, terms). */
-int rg_sampled_gemm(const void* Wk, const float* bg, const void* Hk, int B, int S, int HF, int terms, float* ZT,
-                    int64_t ldz, float* pmax, float* psum, rg_stream_t stream);
+/* The split-bf16 sampled forward in ONE launch for HF in {32, 64, 128} (draw, the negatives' row
+ * gather, both operands' bf16 split, MFMAs, logits, partials): same semantics as rg_sampled_fwd_x
+ * but Z is ROW-major, Z[b·ldz + s] (ldz >= S, ldz % 4 == 0).  Wg optional, bg required. */
+int rg_sampled_logits(const float* h, const float* W, const float* bias, int32_t* neg, int draw, uint64_t seed,
+                      uint64_t counter, int64_t A, int B, int S, int HF, int terms, float* Z, int64_t ldz,
+                      float* pmax, float* psum, float* Wg, float* bg, rg_stream_t stream);
+/* in place dZ = exp(Z − lse)·g on the row-major Z of rg_sampled_logits; dbg[s] = Σ_b dZ[b][s]
+ * through ceil(B/128) × S slabs (summed in order: deterministic) */
+int rg_sampled_dz_rows(float* Z, int64_t ldz, const float* lse, int B, int S, float gscale, float* slabs, float* dbg,
+                       rg_stream_t stream);
 /* per row: z_pos = h_b·W[a_b] + bias[a_b]; lse over {z_pos} ∪ partials; loss_row = lse − z_pos;
  * ids[b] = a_b; dzpos = (exp(z_pos − lse) − 1)·g; gpos = dzpos·h_b; dhpos = dzpos·W[a_b] */
 int rg_sampled_lse(const float* h, const float* W, const float* bias, const int64_t* tgt, int B, int64_t A, int HF,

@@ -41,16 +41,16 @@ def trained():
     torch.set_num_threads(8)
     orc = OracleSupervised(kind="gru4rec", **cfg)
     hips = {p: GRU4Rec_trainer(device="cuda", matmul_precision=p, **cfg) for p in ("f32", "f32x6")}
-    st = SessionStream(N, L, B * STEPS, seed=9)
+    # held-out batches come from the same stream (same item popularity), after the training ones
+    st = SessionStream(N, L, B * (STEPS + 2), seed=9)
     for i in range(STEPS):
         s, a, r, sn, ln, nln, e = st.batch(i, B)
         lo = orc.step(s, a, ln)
         for p, tr in hips.items():
             lg = tr.train_step(s, a, ln)
             assert abs(lo - lg) < 1e-4, (p, i, lo, lg)
-    ev = SessionStream(N, L, 2 * B, seed=31)
-    loader = [(b[0], b[1], b[4]) for b in (ev.batch(i, B) for i in range(2))]
-    return orc, hips, loader, unpopular_items(ev.item_counts())
+    loader = [(b[0], b[1], b[4]) for b in (st.batch(STEPS + i, B) for i in range(2))]
+    return orc, hips, loader, unpopular_items(st.item_counts())
 
 
 @pytest.mark.parametrize("precision", ["f32", "f32x6"])

@@ -31,16 +31,22 @@ def run_head(B, S, A, HF, seed=0, collide=False, precision="f32"):
     tgt = torch.randint(0, A, (B,), generator=g)
     if collide:  # some targets equal negatives (and duplicated negatives)
         tgt[: min(B, S) // 2] = neg[: min(B, S) // 2]
-    ldz = (B + 3) // 4 * 4
+    fused = precision.endswith("-fused")   # rg_sampled_logits: one launch, row-major Z
+    precision = precision.replace("-fused", "")
+    ldz = (S + 3) // 4 * 4 if fused else (B + 3) // 4 * 4
     nT = call("rg_sampled_nparts", B, S, {"f32": 0, "f32x9": 9, "f32x6": 6}[precision])
     dh_, W_, b_, neg_, tgt_ = D(h), D(W), D(bias), D(neg, torch.int32), D(tgt)
-    ZT = torch.full((S, ldz), float("nan"), device="cuda")
+    ZT = torch.full((B, ldz) if fused else (S, ldz), float("nan"), device="cuda")
     pm = torch.empty(nT, B, device="cuda")
     ps = torch.empty(nT, B, device="cuda")
     Wg = torch.empty(S, HF, device="cuda")
     bg = torch.empty(S, device="cuda")
     st = stream_ptr()
-    if precision == "f32":
+    if fused:
+        call("rg_sampled_logits", dh_.data_ptr(), W_.data_ptr(), b_.data_ptr(), neg_.data_ptr(), 0, 0, 0, A, B, S,
+             HF, {"f32x9": 9, "f32x6": 6}[precision], ZT.data_ptr(), ldz, pm.data_ptr(), ps.data_ptr(), Wg.data_ptr(),
+             bg.data_ptr(), st)
+    elif precision == "f32":
         call("rg_sampled_fwd", dh_.data_ptr(), W_.data_ptr(), b_.data_ptr(), neg_.data_ptr(), B, S, HF,
              ZT.data_ptr(), ldz, pm.data_ptr(), ps.data_ptr(), Wg.data_ptr(), bg.data_ptr(), st)
     else:
@@ -59,12 +65,17 @@ def run_head(B, S, A, HF, seed=0, collide=False, precision="f32"):
     call("rg_sampled_lse", dh_.data_ptr(), W_.data_ptr(), b_.data_ptr(), tgt_.data_ptr(), B, A, HF, pm.data_ptr(),
          ps.data_ptr(), nT, gs, lse.data_ptr(), lrow.data_ptr(), ids.data_ptr(), dzp.data_ptr(), gpos.data_ptr(),
          dhp.data_ptr(), st)
-    Z = ZT[:, :B].clone()
+    view = (lambda: ZT[:, :S].t()) if fused else (lambda: ZT[:, :B])   # (S, B) either way
+    Z = view().clone()
     dbg = torch.empty(S, device="cuda")
-    call("rg_sampled_dz", ZT.data_ptr(), ldz, lse.data_ptr(), B, S, gs, dbg.data_ptr(), st)
+    if fused:
+        slabs = torch.empty((B + 127) // 128, S, device="cuda")
+        call("rg_sampled_dz_rows", ZT.data_ptr(), ldz, lse.data_ptr(), B, S, gs, slabs.data_ptr(), dbg.data_ptr(), st)
+    else:
+        call("rg_sampled_dz", ZT.data_ptr(), ldz, lse.data_ptr(), B, S, gs, dbg.data_ptr(), st)
     torch.cuda.synchronize()
     out = dict(Z=Z.cpu(), Wg=Wg.cpu(), bg=bg.cpu(), lse=lse.cpu(), lrow=lrow.cpu(), ids=ids.cpu(), dzp=dzp.cpu(),
-               gpos=gpos.cpu(), dhp=dhp.cpu(), dZ=ZT[:, :B].cpu(), dbg=dbg.cpu())
+               gpos=gpos.cpu(), dhp=dhp.cpu(), dZ=view().cpu(), dbg=dbg.cpu())
     return out, dict(h=h, W=W, bias=bias, neg=neg, tgt=tgt)
 
 
@@ -80,10 +91,12 @@ def test_sample_uniform_matches_oracle_bit_exact():
 @pytest.mark.parametrize("B,S,A,HF,collide", [(256, 256, 5000, 128, False), (37, 200, 300, 64, True),
                                               (300, 130, 100, 256, True), (128, 2048, 100000, 32, False),
                                               (2240, 2048, 50000, 256, True), (1120, 64, 700, 64, True)])
-@pytest.mark.parametrize("precision", ["f32", "f32x9", "f32x6"])
+@pytest.mark.parametrize("precision", ["f32", "f32x9", "f32x6", "f32x9-fused", "f32x6-fused"])
 def test_sampled_kernels_match_torch_fp32(B, S, A, HF, collide, precision):
     if precision != "f32" and (B % 32 or S % 32):
         pytest.skip("split-bf16 path needs B, S multiples of 32")
+    if precision.endswith("-fused") and HF > 128:
+        pytest.skip("the one-launch forward covers HF <= 128")
     o, x = run_head(B, S, A, HF, collide=collide, precision=precision)
     h, W, bias, neg, tgt = x["h"], x["W"], x["bias"], x["neg"], x["tgt"]
     zneg = h @ W[neg].t() + bias[neg]                       # (B, S)

@@ -18,8 +18,8 @@ ap.add_argument("--A", type=int, default=1_000_000)
 ap.add_argument("--HF", type=int, nargs="+", default=[128, 256])
 ap.add_argument("--iters", type=int, default=50)
 ap.add_argument("--prec", nargs="+", default=["f32", "f32x9", "f32x6"])
-ap.add_argument("--stamps", action="store_true", help="SL_STAMP build: print per-wave phase cycles")
-ap.add_argument("--parts", action="store_true", help="also time the plane-fed GEMM alone (HF <= 128)")
+ap.add_argument("--fused", action="store_true", help="also time the one-launch rg_sampled_logits (HF <= 128)")
+ap.add_argument("--hot", action="store_true", help="fused: the same draw every launch (W rows cache-resident)")
 a = ap.parse_args()
 dev = "cuda"
 for HF in a.HF:
@@ -63,44 +63,25 @@ for HF in a.HF:
         us = e0.elapsed_time(e1) / a.iters * 1e3
         print(f"HF {HF} {prec:6s} {us:8.2f} us  {fl / us / 1e6:7.1f} TFLOP/s  Z write {B * S * 4 / us / 1e3:6.0f} GB/s",
               flush=True)
-        if a.parts and prec != "f32" and HF <= 128:
-            Wp = work[:S * HF * 6]
-            Hp = work[S * HF * 6:]
+        if a.fused and prec != "f32" and HF <= 128:
+            ldzr = (S + 3) // 4 * 4
+            Zr = torch.empty(B, ldzr, device=dev)
             terms = 9 if prec == "f32x9" else 6
 
-            def gemm():
-                call("rg_sampled_gemm", Wp.data_ptr(), bg.data_ptr(), Hp.data_ptr(), B, S, HF, terms, ZT.data_ptr(),
-                     ldz, pm.data_ptr(), ps.data_ptr(), st)
+            def fz():
+                it[0] += 0 if a.hot else 1
+                call("rg_sampled_logits", h.data_ptr(), W.data_ptr(), bias.data_ptr(), neg.data_ptr(), 1, 7, it[0], A,
+                     B, S, HF, terms, Zr.data_ptr(), ldzr, pm.data_ptr(), ps.data_ptr(), Wg.data_ptr(), bg.data_ptr(),
+                     st)
             for _ in range(3):
-                gemm()
+                fz()
             torch.cuda.synchronize()
             e0.record()
             for _ in range(a.iters):
-                gemm()
+                fz()
             e1.record()
             torch.cuda.synchronize()
-            ug = e0.elapsed_time(e1) / a.iters * 1e3
-            print(f"   gemm alone {ug:8.2f} us  {fl / ug / 1e6:7.1f} TFLOP/s  ({terms * fl / ug / 1e6 / 2500:.3f} of bf16 peak)",
+            uf = e0.elapsed_time(e1) / a.iters * 1e3
+            print(f"   fused one-launch {uf:8.2f} us  {fl / uf / 1e6:7.1f} TFLOP/s  "
+                  f"({terms * fl / uf / 1e6 / 2500:.3f} of bf16 peak), Z write {B * S * 4 / uf / 1e3:6.0f} GB/s",
                   flush=True)
-            if a.stamps:
-                import numpy as np
-                gemm()
-                torch.cuda.synchronize()
-                nwg = (S // 256) * (B // 128)
-                t = pm.reshape(-1).view(torch.int64)[:nwg * 8 * 4].view(nwg * 8, 4).cpu().numpy().astype(np.float64)
-                print(f"   gemm stamps: to end of chunk-0 MFMA issue median {np.median(t[:, 1] - t[:, 0]):.0f} "
-                      f"(p90 {np.percentile(t[:, 1] - t[:, 0], 90):.0f}), rest median {np.median(t[:, 2] - t[:, 1]):.0f}"
-                      f" (p90 {np.percentile(t[:, 2] - t[:, 1], 90):.0f}) cycles")
-        if a.stamps and prec != "f32" and HF > 128:
-            import numpy as np
-            run()
-            torch.cuda.synchronize()
-            nwg = (S // 128) * max(1, 256 // (S // 128))
-            t = Wg.reshape(-1).view(torch.int64)[:nwg * 8 * 4].view(nwg * 8, 4).cpu().numpy().astype(np.float64)
-            t0 = t[:, 0].min()
-            for name, col in (("start", 0), ("prologue", 1), ("end", 2)):
-                v = t[:, col] - t0
-                print(f"  {name:9s} cycles from first start: p10 {np.percentile(v, 10):8.0f} "
-                      f"median {np.median(v):8.0f} p90 {np.percentile(v, 90):8.0f} max {v.max():8.0f}")
-            print(f"  prologue len median {np.median(t[:, 1] - t[:, 0]):.0f}, loop len median "
-                  f"{np.median(t[:, 2] - t[:, 1]):.0f} cycles")
