@@ -45,8 +45,10 @@ namespace {
 
 constexpr float L2E = 1.4426950408889634f;
 constexpr float LN2 = 0.6931471805599453f;
-constexpr int FL_WAVES = 8;   // waves per workgroup (2 per SIMD)
-constexpr int FL_T = 64 * FL_WAVES;
+// waves per workgroup: 8 (2 per SIMD) up to HF 128; at HF 256 a wave's
+// operand planes (192 VGPRs) and O / dW accumulators (128) need the whole
+// 512-register file, so 4 (1 per SIMD)
+constexpr int fl_waves(int HF) { return HF >= 256 ? 4 : 8; }
 
 // element i of lane half hh inside a 16-deep k slice -> row offset
 __device__ __forceinline__ int kperm(int hh, int i) { return (i & 3) + 8 * (i >> 2) + 4 * hh; }
@@ -57,12 +59,12 @@ __device__ __forceinline__ void glds16(const void* src, void* lds_wave_base) {
                                    (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0, 0);
 }
 
-// copy E 16-B entries (E % 64 == 0) from global to LDS, wave-sliced
-template <int E>
+// copy E 16-B entries (E % 64 == 0) from global to LDS, sliced over NW waves
+template <int E, int NW>
 __device__ __forceinline__ void stage(const bf16x8* __restrict__ src, bf16x8* dst, int w, int lane) {
 #pragma unroll
-  for (int q = 0; q < (E + FL_T - 1) / FL_T; ++q) {
-    const int e0 = FL_T * q + 64 * w;  // wave-uniform
+  for (int q = 0; q < (E + 64 * NW - 1) / (64 * NW); ++q) {
+    const int e0 = 64 * NW * q + 64 * w;  // wave-uniform
     if (e0 < E) glds16(src + e0 + lane, dst + e0);
   }
 }
@@ -122,21 +124,27 @@ __global__ void k_pad_bias(const float* __restrict__ bias, int A, int Ap, float*
 }
 
 // ------------------------------------------------------------- pass 1 ----
-// The chunk ring is two SEPARATE LDS arrays per operand and the loop is
-// unrolled by two: the compiler orders LDS reads only behind the DMA into the
-// same array, so chunk c's MFMAs start while chunk c+1's DMA is in flight
-// (with one [2][E] array it waited for the just-issued prefetch every chunk).
-template <int HF, int NT>
-__global__ __launch_bounds__(FL_T) void k_flash_fwd(const bf16x8* __restrict__ Hk, const bf16x8* __restrict__ Wk,
-                                                    const bf16x8* __restrict__ Wr,
-                                                    const float* __restrict__ bias_pad, int B, int A, int nrb,
-                                                    int nsplit, int cps, float* __restrict__ pm,
-                                                    float* __restrict__ pl, float* __restrict__ pO) {
+// The chunk ring is SEPARATE LDS arrays per slot and the loop is unrolled by
+// two: the compiler orders LDS reads only behind the DMA into the same array,
+// so chunk c's MFMAs start while chunk c+1's DMA is in flight (with one [2][E]
+// array it waited for the just-issued prefetch every chunk).  HF 256: the
+// R-planes (48 KB per chunk) are single-buffered: chunk c+1's R DMA is issued
+// after chunk c's O-MFMAs and lands under chunk c+1's S-MFMAs and softmax.
+// ARG: also the row's top-1 (value, item) per split and, with cmax, every
+// chunk's row maximum — the inputs of the fused top-k (SMORL's rewards).
+template <int HF, int NT, bool ARG>
+__global__ __launch_bounds__(64 * fl_waves(HF)) void k_flash_fwd(
+    const bf16x8* __restrict__ Hk, const bf16x8* __restrict__ Wk, const bf16x8* __restrict__ Wr,
+    const float* __restrict__ bias_pad, int B, int A, int nrb, int nsplit, int cps, float* __restrict__ pm,
+    float* __restrict__ pl, float* __restrict__ pO, float* __restrict__ pbest, int32_t* __restrict__ parg,
+    float* __restrict__ cmax) {
+  constexpr int NW = fl_waves(HF);
+  constexpr bool DR = HF <= 128;      // double-buffered R-planes
   constexpr int NS = HF / 16, NTL = HF / 32;
   constexpr int EK = NS * 192;        // entries per 32-row block, K-planes
   constexpr int ER = NTL * 2 * 192;   // R-planes (== EK)
   __shared__ bf16x8 sk0[EK], sk1[EK];
-  __shared__ bf16x8 sr0[ER], sr1[ER];
+  __shared__ bf16x8 sr0[ER], sr1[DR ? ER : 1];
   __shared__ __attribute__((aligned(16))) float sb0[32], sb1[32];
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, hh = lane >> 5, l32 = lane & 31;
   // XCD-aware order: the nrb row blocks of one item split are dispatched to
@@ -146,19 +154,21 @@ __global__ __launch_bounds__(FL_T) void k_flash_fwd(const bf16x8* __restrict__ H
   const int total = nrb * nsplit;
   if ((total & 7) == 0) bid = (bid & 7) * (total >> 3) + (bid >> 3);
   const int split = bid / nrb, rb = bid % nrb;
-  const int r0 = rb * 32 * FL_WAVES + 32 * w;
+  const int r0 = rb * 32 * NW + 32 * w;
   const bool active = r0 < B;
   const int nct = (A + 31) / 32;
   const int c0 = split * cps;
   const int nch = max(0, min(nct, c0 + cps) - c0);
-#define FL_ISSUE(C, SK, SR, SB)                                                  \
-  do {                                                                           \
-    stage<EK>(Wk + (int64_t)(C) * EK, SK, w, lane);                              \
-    stage<ER>(Wr + (int64_t)(C) * ER, SR, w, lane);                              \
-    if (w == 0 && lane < 8) glds16(bias_pad + 32 * (C) + 4 * lane, SB);          \
-    __builtin_amdgcn_sched_barrier(0); /* keep the prefetch at the top */ \
+#define FL_ISSUE_K(C, SK, SB)                                                  \
+  do {                                                                         \
+    stage<EK, NW>(Wk + (int64_t)(C) * EK, SK, w, lane);                        \
+    if (w == 0 && lane < 8) glds16(bias_pad + 32 * (C) + 4 * lane, SB);        \
   } while (0)
-  if (nch > 0) FL_ISSUE(c0, sk0, sr0, sb0);
+#define FL_ISSUE_R(C, SR) stage<ER, NW>(Wr + (int64_t)(C) * ER, SR, w, lane)
+  if (nch > 0) {
+    FL_ISSUE_K(c0, sk0, sb0);
+    FL_ISSUE_R(c0, sr0);
+  }
   // this wave's 32 rows of h (B operand of Sᵀ = W_c·hᵀ) for the whole split
   bf16x8 hk[NS][3];
 #pragma unroll
@@ -170,26 +180,36 @@ __global__ __launch_bounds__(FL_T) void k_flash_fwd(const bf16x8* __restrict__ H
 #pragma unroll
   for (int t = 0; t < NTL; ++t) o[t] = f16v{};
   float m = NEG_INF, l = 0.f;
+  float bv = NEG_INF;   // ARG: this lane's best logit (natural units) and item
+  int bi = INT32_MAX;
   __syncthreads();
-  auto chunk = [&](const bf16x8* sk, const bf16x8* sr, const float* sb) __attribute__((always_inline)) {
+  // S-part of chunk c: Sᵀ, (ARG) top-1 / chunk max, online max / Σexp, P planes
+  auto spart = [&](const bf16x8* sk, const float* sb, int c, bf16x8 (&q0)[2], bf16x8 (&q1)[2], bf16x8 (&q2)[2])
+      __attribute__((always_inline)) {
     f16v sa = {};
 #pragma unroll
     for (int s = 0; s < NS; ++s)
       sa = mfma_split<NT>(sk[s * 192 + lane], sk[s * 192 + 64 + lane], sk[s * 192 + 128 + lane], hk[s][0], hk[s][1],
                           hk[s][2], sa);
-    // logits in log2 units (item acc32_row(r, hh) of the chunk, row l32)
+    // logits (item acc32_row(r, hh) of the chunk, row l32)
     float cm = NEG_INF;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const f4 bq = *reinterpret_cast<const f4*>(&sb[8 * q + 4 * hh]);
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
-        const float z = (sa[4 * q + u] + bq[u]) * L2E;
-        sa[4 * q + u] = z;
+        const float z = sa[4 * q + u] + bq[u];
+        if (ARG && z > bv) {  // items increase with r: strict > keeps the first maximum
+          bv = z;
+          bi = 32 * (c0 + c) + 8 * q + 4 * hh + u;
+        }
+        sa[4 * q + u] = z * L2E;
         cm = fmaxf(cm, z);
       }
     }
     cm = fmaxf(cm, __shfl_xor(cm, 32));
+    if (ARG && cmax != nullptr && hh == 0) cmax[(int64_t)(c0 + c) * B + r0 + l32] = cm;
+    cm *= L2E;
     const float mn = fmaxf(m, cm);
     if (__any(mn > m)) {
       const float a = mn > m ? __builtin_amdgcn_exp2f(m - mn) : 1.f;
@@ -207,11 +227,14 @@ __global__ __launch_bounds__(FL_T) void k_flash_fwd(const bf16x8* __restrict__ H
       ps += p;
     }
     l += ps;
-    bf16x8 q0[2], q1[2], q2[2];
 #pragma unroll
     for (int s = 0; s < 2; ++s)
       split3x8(f4{sa[8 * s], sa[8 * s + 1], sa[8 * s + 2], sa[8 * s + 3]},
                f4{sa[8 * s + 4], sa[8 * s + 5], sa[8 * s + 6], sa[8 * s + 7]}, q0[s], q1[s], q2[s]);
+  };
+  // O-part: Oᵀ += W_cᵀ·Pᵀ
+  auto opart = [&](const bf16x8* sr, const bf16x8 (&q0)[2], const bf16x8 (&q1)[2], const bf16x8 (&q2)[2])
+      __attribute__((always_inline)) {
 #pragma unroll
     for (int t = 0; t < NTL; ++t)
 #pragma unroll
@@ -221,22 +244,70 @@ __global__ __launch_bounds__(FL_T) void k_flash_fwd(const bf16x8* __restrict__ H
       }
   };
   for (int c = 0; c < nch; c += 2) {
-    if (c + 1 < nch) FL_ISSUE(c0 + c + 1, sk1, sr1, sb1);
-    if (active) chunk(sk0, sr0, sb0);
-    __syncthreads();
-    if (c + 1 < nch) {
-      if (c + 2 < nch) FL_ISSUE(c0 + c + 2, sk0, sr0, sb0);
-      if (active) chunk(sk1, sr1, sb1);
+    bf16x8 q0[2], q1[2], q2[2];
+    if (DR) {
+      if (c + 1 < nch) {
+        FL_ISSUE_K(c0 + c + 1, sk1, sb1);
+        FL_ISSUE_R(c0 + c + 1, sr1);
+      }
+      __builtin_amdgcn_sched_barrier(0);   // keep the prefetch at the top
+      if (active) {
+        spart(sk0, sb0, c, q0, q1, q2);
+        opart(sr0, q0, q1, q2);
+      }
       __syncthreads();
+      if (c + 1 < nch) {
+        if (c + 2 < nch) {
+          FL_ISSUE_K(c0 + c + 2, sk0, sb0);
+          FL_ISSUE_R(c0 + c + 2, sr0);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        if (active) {
+          spart(sk1, sb1, c + 1, q0, q1, q2);
+          opart(sr1, q0, q1, q2);
+        }
+        __syncthreads();
+      }
+    } else {
+      // single R buffer: R(c) was issued after the previous chunk's O-part
+      if (c + 1 < nch) FL_ISSUE_K(c0 + c + 1, sk1, sb1);
+      __builtin_amdgcn_sched_barrier(0);
+      if (active) spart(sk0, sb0, c, q0, q1, q2);
+      __syncthreads();   // R(c) and K(c+1) landed for every wave
+      if (active) opart(sr0, q0, q1, q2);
+      __syncthreads();   // every wave is done with sr0 and sk0
+      if (c + 1 < nch) {
+        FL_ISSUE_R(c0 + c + 1, sr0);
+        if (c + 2 < nch) FL_ISSUE_K(c0 + c + 2, sk0, sb0);
+        __builtin_amdgcn_sched_barrier(0);
+        if (active) spart(sk1, sb1, c + 1, q0, q1, q2);
+        __syncthreads();
+        if (active) opart(sr0, q0, q1, q2);
+        __syncthreads();
+        if (c + 2 < nch) FL_ISSUE_R(c0 + c + 2, sr0);
+      }
     }
   }
-#undef FL_ISSUE
+#undef FL_ISSUE_K
+#undef FL_ISSUE_R
   if (!active) return;
   l += __shfl_xor(l, 32);
   const int row = r0 + l32;
+  if (ARG) {  // merge the lane halves: larger value, ties to the smaller item
+    const float v2 = __shfl_xor(bv, 32);
+    const int i2 = __shfl_xor(bi, 32);
+    if (v2 > bv || (v2 == bv && i2 < bi)) {
+      bv = v2;
+      bi = i2;
+    }
+  }
   if (hh == 0) {
     pm[(int64_t)split * B + row] = m;
     pl[(int64_t)split * B + row] = l;
+    if (ARG) {
+      pbest[(int64_t)split * B + row] = bv;
+      parg[(int64_t)split * B + row] = bi;
+    }
   }
 #pragma unroll
   for (int t = 0; t < NTL; ++t)
@@ -305,35 +376,35 @@ __global__ __launch_bounds__(256) void k_flash_dh(const float* __restrict__ pm, 
 }
 
 // ------------------------------------------------------------- pass 2 ----
-// Same two-array ring and two-fold unrolled loop as pass 1.
+// Same ring scheme as pass 1 (HF 256: single-buffered R-planes of h).
 template <int HF, int NT>
-__global__ __launch_bounds__(FL_T) void k_flash_dw(const bf16x8* __restrict__ Hk, const bf16x8* __restrict__ Hr,
-                                                   const bf16x8* __restrict__ Wk,
-                                                   const float* __restrict__ bias_pad,
-                                                   const float2* __restrict__ rowinfo, float g, int B, int A,
-                                                   float* __restrict__ W, float* __restrict__ mW,
-                                                   float* __restrict__ vW, float* __restrict__ bias,
-                                                   float* __restrict__ mb, float* __restrict__ vb, AdamArgs args,
-                                                   float* __restrict__ dW_out, float* __restrict__ db_out) {
+__global__ __launch_bounds__(64 * fl_waves(HF)) void k_flash_dw(
+    const bf16x8* __restrict__ Hk, const bf16x8* __restrict__ Hr, const bf16x8* __restrict__ Wk,
+    const float* __restrict__ bias_pad, const float2* __restrict__ rowinfo, float g, int B, int A,
+    float* __restrict__ W, float* __restrict__ mW, float* __restrict__ vW, float* __restrict__ bias,
+    float* __restrict__ mb, float* __restrict__ vb, AdamArgs args, float* __restrict__ dW_out,
+    float* __restrict__ db_out) {
+  constexpr int NW = fl_waves(HF);
+  constexpr bool DR = HF <= 128;
   constexpr int NS = HF / 16, NTL = HF / 32;
   constexpr int EK = NS * 192;
   constexpr int ER = NTL * 2 * 192;
   __shared__ bf16x8 sk0[EK], sk1[EK];
-  __shared__ bf16x8 sr0[ER], sr1[ER];
+  __shared__ bf16x8 sr0[ER], sr1[DR ? ER : 1];
   __shared__ __attribute__((aligned(16))) float2 si0[32], si1[32];
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, hh = lane >> 5, l32 = lane & 31;
-  const int j0 = blockIdx.x * 32 * FL_WAVES + 32 * w;
+  const int j0 = blockIdx.x * 32 * NW + 32 * w;
   const bool active = j0 < A;
   const int item = j0 + l32;
   const int nch = B / 32;
-#define FL_ISSUE(C, SK, SR, SI)                                                  \
-  do {                                                                           \
-    stage<EK>(Hk + (int64_t)(C) * EK, SK, w, lane);                              \
-    stage<ER>(Hr + (int64_t)(C) * ER, SR, w, lane);                              \
-    if (w == 0 && lane < 16) glds16(rowinfo + 32 * (C) + 2 * lane, SI);          \
-    __builtin_amdgcn_sched_barrier(0); /* keep the prefetch at the top */ \
+#define FL_ISSUE_K(C, SK, SI)                                                  \
+  do {                                                                         \
+    stage<EK, NW>(Hk + (int64_t)(C) * EK, SK, w, lane);                        \
+    if (w == 0 && lane < 16) glds16(rowinfo + 32 * (C) + 2 * lane, SI);        \
   } while (0)
-  FL_ISSUE(0, sk0, sr0, si0);
+#define FL_ISSUE_R(C, SR) stage<ER, NW>(Hr + (int64_t)(C) * ER, SR, w, lane)
+  FL_ISSUE_K(0, sk0, si0);
+  FL_ISSUE_R(0, sr0);
   // this wave's 32 items of W (B operand of S = h_c·Wᵀ)
   bf16x8 wk[NS][3];
 #pragma unroll
@@ -347,7 +418,9 @@ __global__ __launch_bounds__(FL_T) void k_flash_dw(const bf16x8* __restrict__ Hk
   for (int t = 0; t < NTL; ++t) dw[t] = f16v{};
   float dbs = 0.f;
   __syncthreads();
-  auto chunk = [&](const bf16x8* sk, const bf16x8* sr, const float2* si) __attribute__((always_inline)) {
+  // S = h_c·Wᵀ recomputed, dZ = g·(2^(S−lse) − onehot), db; P planes
+  auto spart = [&](const bf16x8* sk, const float2* si, bf16x8 (&q0)[2], bf16x8 (&q1)[2], bf16x8 (&q2)[2])
+      __attribute__((always_inline)) {
     f16v sa = {};
 #pragma unroll
     for (int s = 0; s < NS; ++s)
@@ -370,11 +443,14 @@ __global__ __launch_bounds__(FL_T) void k_flash_dw(const bf16x8* __restrict__ Hk
       }
     }
     dbs += cdb;
-    bf16x8 q0[2], q1[2], q2[2];
 #pragma unroll
     for (int s = 0; s < 2; ++s)
       split3x8(f4{sa[8 * s], sa[8 * s + 1], sa[8 * s + 2], sa[8 * s + 3]},
                f4{sa[8 * s + 4], sa[8 * s + 5], sa[8 * s + 6], sa[8 * s + 7]}, q0[s], q1[s], q2[s]);
+  };
+  // dW += dZᵀ·h_c
+  auto wpart = [&](const bf16x8* sr, const bf16x8 (&q0)[2], const bf16x8 (&q1)[2], const bf16x8 (&q2)[2])
+      __attribute__((always_inline)) {
 #pragma unroll
     for (int t = 0; t < NTL; ++t)
 #pragma unroll
@@ -384,16 +460,51 @@ __global__ __launch_bounds__(FL_T) void k_flash_dw(const bf16x8* __restrict__ Hk
       }
   };
   for (int c = 0; c < nch; c += 2) {
-    if (c + 1 < nch) FL_ISSUE(c + 1, sk1, sr1, si1);
-    if (active) chunk(sk0, sr0, si0);
-    __syncthreads();
-    if (c + 1 < nch) {
-      if (c + 2 < nch) FL_ISSUE(c + 2, sk0, sr0, si0);
-      if (active) chunk(sk1, sr1, si1);
+    bf16x8 q0[2], q1[2], q2[2];
+    if (DR) {
+      if (c + 1 < nch) {
+        FL_ISSUE_K(c + 1, sk1, si1);
+        FL_ISSUE_R(c + 1, sr1);
+      }
+      __builtin_amdgcn_sched_barrier(0);   // keep the prefetch at the top
+      if (active) {
+        spart(sk0, si0, q0, q1, q2);
+        wpart(sr0, q0, q1, q2);
+      }
       __syncthreads();
+      if (c + 1 < nch) {
+        if (c + 2 < nch) {
+          FL_ISSUE_K(c + 2, sk0, si0);
+          FL_ISSUE_R(c + 2, sr0);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        if (active) {
+          spart(sk1, si1, q0, q1, q2);
+          wpart(sr1, q0, q1, q2);
+        }
+        __syncthreads();
+      }
+    } else {
+      if (c + 1 < nch) FL_ISSUE_K(c + 1, sk1, si1);
+      __builtin_amdgcn_sched_barrier(0);
+      if (active) spart(sk0, si0, q0, q1, q2);
+      __syncthreads();
+      if (active) wpart(sr0, q0, q1, q2);
+      __syncthreads();
+      if (c + 1 < nch) {
+        FL_ISSUE_R(c + 1, sr0);
+        if (c + 2 < nch) FL_ISSUE_K(c + 2, sk0, si0);
+        __builtin_amdgcn_sched_barrier(0);
+        if (active) spart(sk1, si1, q0, q1, q2);
+        __syncthreads();
+        if (active) wpart(sr0, q0, q1, q2);
+        __syncthreads();
+        if (c + 2 < nch) FL_ISSUE_R(c + 2, sr0);
+      }
     }
   }
-#undef FL_ISSUE
+#undef FL_ISSUE_K
+#undef FL_ISSUE_R
   if (!active) return;
   dbs += __shfl_xor(dbs, 32);
   if (hh == 0 && item < A) {
@@ -428,7 +539,183 @@ __global__ __launch_bounds__(FL_T) void k_flash_dw(const bf16x8* __restrict__ Hk
   }
 }
 
-inline bool flash_hf_ok(int HF) { return HF == 32 || HF == 64 || HF == 128; }
+// -------------------------------------------------------- fused top-k ----
+// Top-1: merge the per-split (best, item) of pass 1 (splits ascend in item
+// order, so keeping the earlier split on a tie keeps the first maximum).
+__global__ void k_flash_argmax(const float* __restrict__ pbest, const int32_t* __restrict__ parg, int nsplit, int B,
+                               int32_t* __restrict__ out, float* __restrict__ out_max) {
+  const int row = blockIdx.x * blockDim.x + threadIdx.x;
+  if (row >= B) return;
+  float bv = NEG_INF;
+  int bi = INT32_MAX;
+  for (int s = 0; s < nsplit; ++s) {
+    const float v = pbest[(int64_t)s * B + row];
+    const int i = parg[(int64_t)s * B + row];
+    if (i != INT32_MAX && (v > bv || bi == INT32_MAX)) {
+      bv = v;
+      bi = i;
+    }
+  }
+  out[row] = bi == INT32_MAX ? -1 : bi;
+  if (out_max) out_max[row] = bv;
+}
+
+// Top-K (K <= TK_MAX): the K largest 32-item chunk maxima of a row bound its
+// K-th largest logit from below (they hold K distinct items), so every top-K
+// item lies in a chunk whose maximum is >= that bound tau.  Chunks with
+// cmax >= tau - tol (tol covers the split-bf16 error of cmax) are the
+// candidates; their items are rescored in plain fp32 and ranked in the
+// canonical (value desc, index asc) order.
+constexpr int TK_MAX = 32;
+constexpr int TK_CAP = 64;   // candidate chunks per row (2048 items)
+
+__device__ __forceinline__ void tk_insert(float (&t)[TK_MAX], float v) {
+#pragma unroll
+  for (int i = 0; i < TK_MAX; ++i) {
+    const float hi = fmaxf(t[i], v);
+    v = fminf(t[i], v);
+    t[i] = hi;
+  }
+}
+
+// 64 rows per workgroup (lane = row), the 4 waves split the chunk range
+__global__ __launch_bounds__(256) void k_flash_topk_cand(const float* __restrict__ cmax, int nct, int B, int K,
+                                                         float tol_abs, float tol_rel, int32_t* __restrict__ cand,
+                                                         int32_t* __restrict__ ncand, int32_t* __restrict__ err) {
+  __shared__ float st[4][TK_MAX][64];
+  __shared__ int cnt[64];
+  __shared__ float tau_s[64];
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 64 + lane;
+  const bool ok = row < B;
+  float t[TK_MAX];
+#pragma unroll
+  for (int i = 0; i < TK_MAX; ++i) t[i] = NEG_INF;
+  float thr = NEG_INF;   // t[K-1]
+  for (int c = w; c < nct; c += 4) {
+    const float v = ok ? cmax[(int64_t)c * B + row] : NEG_INF;
+    if (v > thr) {
+      tk_insert(t, v);
+#pragma unroll
+      for (int i = 0; i < TK_MAX; ++i)
+        if (i == K - 1) thr = t[i];
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < TK_MAX; ++i) st[w][i][lane] = t[i];
+  if (w == 0) cnt[lane] = 0;
+  __syncthreads();
+  if (w == 0) {
+    for (int q = 1; q < 4; ++q)
+      for (int i = 0; i < K; ++i) {
+        const float v = st[q][i][lane];
+        if (v > thr) {
+          tk_insert(t, v);
+#pragma unroll
+          for (int j = 0; j < TK_MAX; ++j)
+            if (j == K - 1) thr = t[j];
+        }
+      }
+    tau_s[lane] = thr;
+  }
+  __syncthreads();
+  const float tau = tau_s[lane];
+  const float lim = tau > NEG_INF ? tau - (tol_abs + tol_rel * fabsf(tau)) : NEG_INF;
+  for (int c = w; c < nct; c += 4) {
+    const float v = ok ? cmax[(int64_t)c * B + row] : NEG_INF;
+    if (ok && v >= lim) {
+      const int p = atomicAdd(&cnt[lane], 1);
+      if (p < TK_CAP) cand[(int64_t)row * TK_CAP + p] = c;
+    }
+  }
+  __syncthreads();
+  if (w == 0 && ok) {
+    const int n = cnt[lane];
+    // a tie run past the cap, or more than TK_CAP chunks with fewer than K
+    // finite maxima (tau = -inf: every chunk is a candidate)
+    if (n > TK_CAP) atomicOr(err, 1);
+    ncand[row] = min(n, TK_CAP);
+  }
+}
+
+// one workgroup (256 threads) per row: fp32 logits of the candidate items
+// (fmaf chain over k, then + bias), canonical top-K
+__global__ __launch_bounds__(256) void k_flash_topk_eval(const float* __restrict__ h, const float* __restrict__ W,
+                                                         const float* __restrict__ bias, const int32_t* __restrict__ cand,
+                                                         const int32_t* __restrict__ ncand, int A, int HF, int K,
+                                                         int32_t* __restrict__ out_idx, float* __restrict__ out_val) {
+  __shared__ __attribute__((aligned(16))) float hs[256];
+  __shared__ float cv[TK_CAP * 32];
+  __shared__ int ci[TK_CAP * 32];
+  __shared__ float rv[4];
+  __shared__ int ri[4], rs[4];
+  const int row = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  for (int k = tid; k < HF; k += 256) hs[k] = h[(int64_t)row * HF + k];
+  const int n = ncand[row] * 32;
+  __syncthreads();
+  for (int e = tid; e < n; e += 256) {
+    const int item = cand[(int64_t)row * TK_CAP + (e >> 5)] * 32 + (e & 31);
+    float z = NEG_INF;
+    if (item < A) {
+      const f4* wr = reinterpret_cast<const f4*>(W + (int64_t)item * HF);
+      float acc = 0.f;
+      for (int k4 = 0; k4 < HF / 4; ++k4) {
+        const f4 x = wr[k4];
+        acc = fmaf(hs[4 * k4], x[0], acc);
+        acc = fmaf(hs[4 * k4 + 1], x[1], acc);
+        acc = fmaf(hs[4 * k4 + 2], x[2], acc);
+        acc = fmaf(hs[4 * k4 + 3], x[3], acc);
+      }
+      z = acc + bias[item];
+    }
+    cv[e] = z;
+    ci[e] = item < A ? item : INT32_MAX;
+  }
+  __syncthreads();
+  for (int k = 0; k < K; ++k) {
+    float bv = NEG_INF;
+    int bi = INT32_MAX, bs = -1;
+    for (int e = tid; e < n; e += 256) {
+      const float v = cv[e];
+      const int i = ci[e];
+      if (i != INT32_MAX && (v > bv || (v == bv && i < bi) || bs < 0)) {
+        bv = v;
+        bi = i;
+        bs = e;
+      }
+    }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+      const float v2 = __shfl_xor(bv, o);
+      const int i2 = __shfl_xor(bi, o), s2 = __shfl_xor(bs, o);
+      if (s2 >= 0 && (bs < 0 || v2 > bv || (v2 == bv && i2 < bi))) {
+        bv = v2;
+        bi = i2;
+        bs = s2;
+      }
+    }
+    if (lane == 0) {
+      rv[w] = bv;
+      ri[w] = bi;
+      rs[w] = bs;
+    }
+    __syncthreads();
+    if (tid == 0) {
+      for (int q = 1; q < 4; ++q)
+        if (rs[q] >= 0 && (rs[0] < 0 || rv[q] > rv[0] || (rv[q] == rv[0] && ri[q] < ri[0]))) {
+          rv[0] = rv[q];
+          ri[0] = ri[q];
+          rs[0] = rs[q];
+        }
+      out_idx[(int64_t)row * K + k] = rs[0] >= 0 ? ri[0] : -1;
+      if (out_val) out_val[(int64_t)row * K + k] = rv[0];
+      if (rs[0] >= 0) ci[rs[0]] = INT32_MAX;   // taken
+    }
+    __syncthreads();
+  }
+}
+
+inline bool flash_hf_ok(int HF) { return HF == 32 || HF == 64 || HF == 128 || HF == 256; }
 
 }  // namespace
 
@@ -453,6 +740,7 @@ extern "C" int rg_head_planes(const float* X, int rows, int HF, void* planes_k, 
     case 32: PL(32); break;
     case 64: PL(64); break;
     case 128: PL(128); break;
+    case 256: PL(256); break;
   }
 #undef PL
   if (bias && bias_pad)
@@ -461,32 +749,78 @@ extern "C" int rg_head_planes(const float* X, int rows, int HF, void* planes_k, 
   return RG_OK;
 }
 
-extern "C" int rg_flash_fwd(const void* Hk, const void* Wk, const void* Wr, const float* bias_pad, int B, int A,
-                            int HF, int terms, int nsplit, float* pm, float* pl, float* pO, hipStream_t stream) {
+extern "C" int rg_flash_rows_per_block(int HF) { return flash_hf_ok(HF) ? 32 * fl_waves(HF) : RG_ERR_SHAPE; }
+
+extern "C" int rg_flash_fwd_top(const void* Hk, const void* Wk, const void* Wr, const float* bias_pad, int B, int A,
+                                int HF, int terms, int nsplit, float* pm, float* pl, float* pO, float* pbest,
+                                int32_t* parg, float* cmax, hipStream_t stream) {
   if (B <= 0 || A <= 0 || (B % 32) || nsplit <= 0 || !Hk || !Wk || !Wr || !bias_pad || !pm || !pl || !pO)
     return RG_ERR_ARG;
   if (terms != 6 && terms != 9) return RG_ERR_ARG;
   if (!flash_hf_ok(HF)) return RG_ERR_SHAPE;
+  const bool arg = pbest != nullptr;
+  if (arg != (parg != nullptr) || (cmax && !arg)) return RG_ERR_ARG;
   const int nct = (A + 31) / 32;
   const int cps = (nct + nsplit - 1) / nsplit;
-  const int nrb = (B + 32 * FL_WAVES - 1) / (32 * FL_WAVES);
+  const int rpb = 32 * fl_waves(HF);
+  const int nrb = (B + rpb - 1) / rpb;
   const dim3 grid((unsigned)(nrb * nsplit));
-#define FF(HFV, NTV)                                                                                          \
-  hipLaunchKernelGGL((k_flash_fwd<HFV, NTV>), grid, dim3(FL_T), 0, stream, (const bf16x8*)Hk, (const bf16x8*)Wk, \
-                     (const bf16x8*)Wr, bias_pad, B, A, nrb, nsplit, cps, pm, pl, pO)
+#define FF(HFV, NTV, ARGV)                                                                                   \
+  hipLaunchKernelGGL((k_flash_fwd<HFV, NTV, ARGV>), grid, dim3(64 * fl_waves(HFV)), 0, stream,                \
+                     (const bf16x8*)Hk, (const bf16x8*)Wk, (const bf16x8*)Wr, bias_pad, B, A, nrb, nsplit, cps, pm, \
+                     pl, pO, pbest, parg, cmax)
+#define FA(HFV, NTV)     \
+  if (arg) {             \
+    FF(HFV, NTV, true);  \
+  } else {               \
+    FF(HFV, NTV, false); \
+  }
 #define FT(HFV)          \
   if (terms == 9) {      \
-    FF(HFV, 9);          \
+    FA(HFV, 9);          \
   } else {               \
-    FF(HFV, 6);          \
+    FA(HFV, 6);          \
   }
   switch (HF) {
     case 32: FT(32); break;
     case 64: FT(64); break;
     case 128: FT(128); break;
+    case 256: FT(256); break;
   }
 #undef FT
+#undef FA
 #undef FF
+  RG_LAUNCH_CHECK();
+  return RG_OK;
+}
+
+extern "C" int rg_flash_fwd(const void* Hk, const void* Wk, const void* Wr, const float* bias_pad, int B, int A,
+                            int HF, int terms, int nsplit, float* pm, float* pl, float* pO, hipStream_t stream) {
+  return rg_flash_fwd_top(Hk, Wk, Wr, bias_pad, B, A, HF, terms, nsplit, pm, pl, pO, nullptr, nullptr, nullptr,
+                          stream);
+}
+
+extern "C" int rg_flash_argmax(const float* pbest, const int32_t* parg, int nsplit, int B, int32_t* out,
+                               float* out_max, hipStream_t stream) {
+  if (B <= 0 || nsplit <= 0 || !pbest || !parg || !out) return RG_ERR_ARG;
+  hipLaunchKernelGGL(k_flash_argmax, dim3((B + 255) / 256), dim3(256), 0, stream, pbest, parg, nsplit, B, out,
+                     out_max);
+  RG_LAUNCH_CHECK();
+  return RG_OK;
+}
+
+extern "C" int rg_flash_topk_cap(void) { return TK_CAP; }
+
+extern "C" int rg_flash_topk(const float* cmax, int B, int A, int K, float tol_abs, float tol_rel, const float* h,
+                             const float* W, const float* bias, int HF, int32_t* cand, int32_t* ncand, int32_t* out_idx,
+                             float* out_val, int32_t* err, hipStream_t stream) {
+  if (B <= 0 || A <= 0 || K <= 0 || K > TK_MAX || K > A || HF <= 0 || HF > 256 || (HF % 4)) return RG_ERR_ARG;
+  if (!cmax || !h || !W || !bias || !cand || !ncand || !out_idx || !err) return RG_ERR_ARG;
+  const int nct = (A + 31) / 32;
+  hipLaunchKernelGGL(k_flash_topk_cand, dim3((B + 63) / 64), dim3(256), 0, stream, cmax, nct, B, K, tol_abs, tol_rel,
+                     cand, ncand, err);
+  hipLaunchKernelGGL(k_flash_topk_eval, dim3(B), dim3(256), 0, stream, h, W, bias, cand, ncand, A, HF, K, out_idx,
+                     out_val);
   RG_LAUNCH_CHECK();
   return RG_OK;
 }
@@ -530,9 +864,10 @@ extern "C" int rg_flash_dw_adam(const void* Hk, const void* Hr, const void* Wk, 
   if (dW_out ? !db_out : (!adam6 || !W || !mW || !vW || !bias || !mb || !vb)) return RG_ERR_ARG;
   AdamArgs a{};
   if (adam6) a = AdamArgs{adam6[0], adam6[1], adam6[2], adam6[3], adam6[4], adam6[5]};
-  const dim3 grid((unsigned)((A + 32 * FL_WAVES - 1) / (32 * FL_WAVES)));
+  const int rpb = 32 * fl_waves(HF);
+  const dim3 grid((unsigned)((A + rpb - 1) / rpb));
 #define FW(HFV, NTV)                                                                                          \
-  hipLaunchKernelGGL((k_flash_dw<HFV, NTV>), grid, dim3(FL_T), 0, stream, (const bf16x8*)Hk, (const bf16x8*)Hr, \
+  hipLaunchKernelGGL((k_flash_dw<HFV, NTV>), grid, dim3(64 * fl_waves(HFV)), 0, stream, (const bf16x8*)Hk, (const bf16x8*)Hr, \
                      (const bf16x8*)Wk, bias_pad, (const float2*)rowinfo, gscale, B, A, W, mW, vW, bias, mb, vb, \
                      a, dW_out, db_out)
 #define FT(HFV)          \
@@ -545,6 +880,7 @@ extern "C" int rg_flash_dw_adam(const void* Hk, const void* Hr, const void* Wk, 
     case 32: FT(32); break;
     case 64: FT(64); break;
     case 128: FT(128); break;
+    case 256: FT(256); break;
   }
 #undef FT
 #undef FW

@@ -45,6 +45,11 @@ SIGNATURES = {
     "rg_head_plane_bytes": [I, I],
     "rg_head_planes": [P, I, I, P, P, P, P, P],
     "rg_flash_fwd": [P, P, P, P, I, I, I, I, I, P, P, P, P],
+    "rg_flash_rows_per_block": [I],
+    "rg_flash_fwd_top": [P, P, P, P, I, I, I, I, I, P, P, P, P, P, P, P],
+    "rg_flash_argmax": [P, P, I, I, P, P, P],
+    "rg_flash_topk_cap": [],
+    "rg_flash_topk": [P, I, I, I, F, F, P, P, P, I, P, P, P, P, P, P],
     "rg_flash_lse": [P, P, I, P, P, P, P, I64, I, I64, I, I, P, P, P],
     "rg_flash_rows": [P, P, I64, I, I, P, P],
     "rg_flash_dh": [P, P, P, I, P, F, I, I, P, P],

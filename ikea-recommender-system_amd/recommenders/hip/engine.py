@@ -444,14 +444,17 @@ class _FlashWS:
     """Workspace of the fused split-bf16 training head (csrc/head_flash.hip):
     bf16 operand planes of h and W (K- and R-layouts), the bias padded with
     -inf to whole 32-item chunks, per-(split, row) softmax partials and the
-    unnormalised dh partials O (nsplit × HF × B).  No logits are stored."""
+    unnormalised dh partials O (nsplit × HF × B).  No logits are stored.
+    With top_k >= 1 pass 1 also leaves every split's (best logit, item) and,
+    for top_k > 1, every 32-item chunk's row maximum (the fused top-k)."""
 
-    def __init__(self, B, A, HF, device):
+    def __init__(self, B, A, HF, device, top_k=0):
         u8 = lambda n: torch.empty(int(n), dtype=torch.uint8, device=device)  # noqa: E731
-        z = lambda *s: torch.empty(*s, dtype=torch.float32, device=device)  # noqa: E731
-        self.B = B
+        z = lambda *s, dt=torch.float32: torch.empty(*s, dtype=dt, device=device)  # noqa: E731
+        self.B, self.top_k = B, top_k
         self.terms = 0
-        nrb = -(-B // 256)  # 256-row workgroups of pass 1
+        self.h = None
+        nrb = -(-B // call("rg_flash_rows_per_block", HF))  # row blocks of pass 1
         # about one pass-1 workgroup per CU; a multiple of 8 for the XCD order
         self.nsplit = _round_up(min(max(1, 256 // nrb), -(-A // 32)), 8)
         hb, wb = call("rg_head_plane_bytes", B, HF), call("rg_head_plane_bytes", A, HF)
@@ -462,6 +465,14 @@ class _FlashWS:
         self.rows = z(B, 2)
         self.lse, self.zt, self.loss_row = z(B), z(B), z(B)
         self.loss = torch.zeros(1, device=device)
+        self.pbest = self.parg = self.cmax = self.cand = self.ncand = None
+        if top_k >= 1:
+            self.pbest, self.parg = z(self.nsplit, B), z(self.nsplit, B, dt=torch.int32)
+            self.top_idx, self.top_val = z(B, top_k, dt=torch.int32), z(B, top_k)
+        if top_k > 1:
+            self.cmax = z(-(-A // 32), B)
+            self.cand = z(B, call("rg_flash_topk_cap"), dt=torch.int32)
+            self.ncand = z(B, dt=torch.int32)
 
 
 # Head-GEMM arithmetic (build extension; the reference computes in fp32):
@@ -496,9 +507,10 @@ class SoftmaxHead:
         self.b = Param(f"{name}.bias", b, device)
         self._ws = {}
         self._fws = {}
-        # callers that read the stored logits after forward_loss (SMORL's
-        # top-k rewards) keep the native path
-        self.keep_logits = False
+        # entries of the row top-k a caller reads after forward_loss (SMORL's
+        # rewards, ``top_entries``); the fused head computes them in pass 1
+        self.top_k = 0
+        self.top_err = torch.zeros(1, dtype=torch.int32, device=device)
 
     def named_params(self):
         return [self.W, self.b]
@@ -510,15 +522,15 @@ class SoftmaxHead:
     def flash_terms(self, B):
         """bf16 terms of the fused training head for a batch of B rows; 0
         selects the native fp32 path that stores Zᵀ."""
-        if self.precision == "f32" or self.keep_logits or self.HF not in (32, 64, 128) or B % 32:
+        if self.precision == "f32" or self.HF not in (32, 64, 128, 256) or B % 32:
             return 0
         return SPLIT_TERMS[self.precision]
 
     def fws(self, slot, B):
         w = self._fws.get(slot)
-        if w is None or w.B != B:
+        if w is None or w.B != B or w.top_k != self.top_k:
             self._fws.pop(slot, None)
-            w = _FlashWS(B, self.A, self.HF, self.device)
+            w = _FlashWS(B, self.A, self.HF, self.device, self.top_k)
             self._fws[slot] = w
         return w
 
@@ -528,16 +540,56 @@ class SoftmaxHead:
         B, A, HF = h.shape[0], self.A, self.HF
         w = self.fws(slot, B)
         w.terms = terms
+        w.h = h
         st = stream_ptr()
         W, b = self.W.p.data_ptr(), self.b.p.data_ptr()
+        ptr = lambda t: None if t is None else t.data_ptr()  # noqa: E731
         with region("head_fwd"):
             call("rg_head_planes", h.data_ptr(), B, HF, w.Hk.data_ptr(), w.Hr.data_ptr(), None, None, st)
             call("rg_head_planes", W, A, HF, w.Wk.data_ptr(), w.Wr.data_ptr(), b, w.bias_pad.data_ptr(), st)
-            call("rg_flash_fwd", w.Hk.data_ptr(), w.Wk.data_ptr(), w.Wr.data_ptr(), w.bias_pad.data_ptr(), B, A, HF,
-                 terms, w.nsplit, w.pm.data_ptr(), w.pl.data_ptr(), w.pO.data_ptr(), st)
+            call("rg_flash_fwd_top", w.Hk.data_ptr(), w.Wk.data_ptr(), w.Wr.data_ptr(), w.bias_pad.data_ptr(), B, A,
+                 HF, terms, w.nsplit, w.pm.data_ptr(), w.pl.data_ptr(), w.pO.data_ptr(), ptr(w.pbest), ptr(w.parg),
+                 ptr(w.cmax), st)
         call("rg_flash_lse", w.pm.data_ptr(), w.pl.data_ptr(), w.nsplit, h.data_ptr(), W, b, tgt.data_ptr(), self.lo,
              A, self.A_full, B, HF, w.lse.data_ptr(), w.zt.data_ptr(), st)
         return w
+
+    # split-bf16 error allowance of the chunk maxima that select the top-k
+    # candidates (|f32x6 - fp32| is ~1e-7 relative to sum |h||w|)
+    TOP_TOL_ABS, TOP_TOL_REL = 1e-4, 1e-4
+
+    def top_entries(self, w):
+        """(idx (B, K) int32 local item ids, values (B, K)) of every row's top-K
+        logits in the canonical (value desc, index asc) order, after
+        forward_loss with ``top_k = K``.  Fused head: K = 1 merges pass 1's
+        per-split first maxima (split-bf16 logits); K > 1 rescores the items
+        of the candidate chunks in fp32 (rg_flash_topk; a candidate overflow
+        is flagged in ``top_err``, see check_top_err).  Native head: rg_topk
+        over the stored Zᵀ."""
+        K, B = self.top_k, w.B
+        st = stream_ptr()
+        if isinstance(w, _FlashWS):
+            if K == 1:
+                call("rg_flash_argmax", w.pbest.data_ptr(), w.parg.data_ptr(), w.nsplit, B, w.top_idx.data_ptr(),
+                     w.top_val.data_ptr(), st)
+            else:
+                call("rg_flash_topk", w.cmax.data_ptr(), B, self.A, K, _f32(self.TOP_TOL_ABS),
+                     _f32(self.TOP_TOL_REL), w.h.data_ptr(), self.W.p.data_ptr(), self.b.p.data_ptr(), self.HF,
+                     w.cand.data_ptr(), w.ncand.data_ptr(), w.top_idx.data_ptr(), w.top_val.data_ptr(),
+                     self.top_err.data_ptr(), st)
+            return w.top_idx, w.top_val
+        idx = torch.empty(B, K, dtype=torch.int32, device=self.device)
+        vals = torch.empty(B, K, device=self.device)
+        call("rg_topk", w.ZT.data_ptr(), w.ldz, w.pmax.data_ptr(), B, self.A, K, idx.data_ptr(), vals.data_ptr(),
+             self.top_err.data_ptr(), st)
+        return idx, vals
+
+    def check_top_err(self):
+        """Raise if a fused or stored-logit top-k of this head overflowed its
+        candidate buffer since the last check (massive exact ties)."""
+        if int(self.top_err.item()):
+            self.top_err.zero_()
+            raise RuntimeError(f"{self.name}: top-k candidate overflow (massive ties in the logits)")
 
     def flash_dh(self, w, tgt, lse, g, dh_out):
         """dh_out := this head's ∂loss/∂h given the (all-rank) lse."""

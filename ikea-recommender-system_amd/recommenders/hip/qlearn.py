@@ -56,10 +56,6 @@ class QNet(HipNet):
         self.q_heads = [QHead(n, self.action_dim, self.hf, self.device, shard=self.shard) for n in q_names]
         for q in self.q_heads:
             setattr(self, q.name, q)
-        # SMORL's diversity / novelty rewards read the supervised logits' top-k
-        # after the CE forward: that head keeps the Zᵀ-storing native path
-        if len(self.q_heads) > 1:
-            self.sup_head_output.keep_logits = True
         self._argmax_head = None
         self._buf = {}
 
@@ -181,14 +177,18 @@ def smorl_rewards(main, smorl, s, a, r_acc, true_next_len, B):
     dev = main.device
     st = stream_ptr()
     head = main.sup_head_output
-    w = head.ws("main", B, True)
     k_div, k_nov = smorl["topk_div"], smorl["topk_nov"]
     K = max(k_div, k_nov)
-    if K == 1:
+    if head.flash_terms(B):   # fused head: top-K from pass 1, no logits stored
+        idx, _ = head.top_entries(head.fws("main", B))
+    elif K == 1:
+        w = head.ws("main", B, True)
         idx = w.amax  # argmax of the supervised logits = topk(sup, 1)
     else:
+        w = head.ws("main", B, True)
         idx = main.buf("topk_idx", (B, K), torch.int32)
-        call("rg_topk", w.ZT.data_ptr(), w.ldz, w.pmax.data_ptr(), B, head.A, K, idx.data_ptr(), None, None, st)
+        call("rg_topk", w.ZT.data_ptr(), w.ldz, w.pmax.data_ptr(), B, head.A, K, idx.data_ptr(), None,
+             head.top_err.data_ptr(), st)
     r_div = main.buf("r_div", (B,))
     lens = _dev(true_next_len, dev, torch.int64)   # quirk: diversity uses true_next_len
     call("rg_diversity", s.data_ptr(), s.shape[1], lens.data_ptr(), 1 if smorl["pad_end"] else 0, idx.data_ptr(),

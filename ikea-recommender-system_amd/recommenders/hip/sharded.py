@@ -43,11 +43,13 @@ def _sharded_ce_forward(net, head, H_all, a_all, st, want_argmax=False):
     """CE(mean over world·B rows) of the item-sharded head: local logits over
     items [lo, hi) for every gathered row, per-rank LSE merged across ranks,
     target logit summed from its owner.  Keeps Zᵀ/lse for the backward.  With
-    want_argmax the local (row max, argmax) are left in w.mx / w.amax."""
+    want_argmax the native head leaves the local (row max, argmax) in
+    w.mx / w.amax; the fused head computes its top entries in pass 1
+    (head.top_k, read with head.top_entries)."""
     comm = net.comm
     W_, HF = comm.world, net.hf
     Bg = H_all.shape[0]
-    terms = 0 if want_argmax else head.flash_terms(Bg)
+    terms = head.flash_terms(Bg)
     if terms:
         # fused split-bf16 head (csrc/head_flash.hip): local lse and the
         # owner's target logit, no logits stored; targets stay global ids
@@ -180,10 +182,13 @@ def _global_topk(net, head, w, K, name):
     comm = net.comm
     Bg = w.B
     st = stream_ptr()
-    vals = _buf(net, name + "_v", (Bg, K))
-    idx = _buf(net, name + "_i", (Bg, K), torch.int32)
-    call("rg_topk", w.ZT.data_ptr(), w.ldz, w.pmax.data_ptr(), Bg, head.A, K, idx.data_ptr(), vals.data_ptr(),
-         None, st)
+    if getattr(w, "terms", 0):   # fused head: local top-K from pass 1's chunk maxima
+        idx, vals = head.top_entries(w)
+    else:
+        vals = _buf(net, name + "_v", (Bg, K))
+        idx = _buf(net, name + "_i", (Bg, K), torch.int32)
+        call("rg_topk", w.ZT.data_ptr(), w.ldz, w.pmax.data_ptr(), Bg, head.A, K, idx.data_ptr(), vals.data_ptr(),
+             head.top_err.data_ptr(), st)
     v_r = _gather_rows(comm, net, name + "_vr", vals)
     i_r = _gather_rows(comm, net, name + "_ir", idx)
     out = _buf(net, name, (Bg, K), torch.int32)
@@ -253,7 +258,10 @@ def sharded_double_q_step(nets, clocks, k, s, a, r, s_next, true_len, true_next_
              sq.data_ptr(), dq.data_ptr(), st)
         call("rg_sum64", sq.data_ptr(), B, 1.0 / Bg, q_loss.data_ptr(), None, st)
     else:
-        if want_top1:
+        if want_top1 and getattr(w, "terms", 0):
+            am1, mx1 = sup.top_entries(w)
+            top = _global_argmax(main, mx1.view(Bg), am1.view(Bg), A, "sup_top1").view(Bg, 1)
+        elif want_top1:
             top = _global_argmax(main, w.mx, w.amax, A, "sup_top1").view(Bg, 1)
         else:
             top = _global_topk(main, sup, w, max(smorl["topk_div"], smorl["topk_nov"]), "sup_topk")

@@ -66,6 +66,8 @@ class SMORL_trainer:
         # GEMMs, "f32" native fp32 MFMA or split-bf16 "f32x9" / "f32x6"
         for net in (self.SMORL_1, self.SMORL_2):
             net.set_matmul_precision(matmul_precision)
+            # the rewards read the supervised logits' top-k after the CE forward
+            net.sup_head_output.top_k = max(int(topk_div), int(topk_nov))
         self.gamma = gamma
         self.alpha = alpha
         self.q_weights = q_weights
@@ -107,7 +109,10 @@ class SMORL_trainer:
 
     def train_step(self, s, a, r_acc, s_next, true_len, true_next_len, is_end):
         sup, q = self.train_step_async(s, a, r_acc, s_next, true_len, true_next_len, is_end)
-        return sup.item(), q.item()
+        out = sup.item(), q.item()
+        for net in (self.SMORL_1, self.SMORL_2):
+            net.sup_head_output.check_top_err()
+        return out
 
     @property
     def last_rewards(self):

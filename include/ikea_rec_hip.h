@@ -103,7 +103,7 @@ int rg_head_fwd_x(const float* h, const float* W, const float* bias, int B, int 
  * Linear + CrossEntropyLoss(mean) + Adam step of GRU4Rec/model.py:58-60, 80,
  * 121, 146, 149-153 without materialising the (B × A) logits, on split-bf16
  * MFMAs (terms 9: exact products, 6: sub-ulp terms dropped).  HF in {32, 64,
- * 128}; B % 32 == 0.  Multi-GPU item shards pass their first item `lo` and
+ * 128, 256}; B % 32 == 0.  Multi-GPU item shards pass their first item `lo` and
  * merge lse over ranks between rg_flash_lse and rg_flash_rows.
  * rg_head_plane_bytes: bytes of one operand-plane buffer for `rows` rows.
  * rg_head_planes: X (rows × HF) -> K-planes / R-planes (either optional);
@@ -122,6 +122,30 @@ int rg_head_planes(const float* X, int rows, int HF, void* planes_k, void* plane
                    float* bias_pad, rg_stream_t stream);
 int rg_flash_fwd(const void* Hk, const void* Wk, const void* Wr, const float* bias_pad, int B, int A, int HF,
                  int terms, int nsplit, float* pm, float* pl, float* pO, rg_stream_t stream);
+/* ---- fused top-k of the training head's logits (SMORL's diversity / novelty
+ * rewards, smorl_gru.py:298-308 -> diversity.py:15-73 / novelty.py:12-47:
+ * torch.topk(sup, k) of the supervised logits), no logits stored.
+ * rg_flash_rows_per_block: rows of one pass-1 workgroup (row-block size).
+ * rg_flash_fwd_top: rg_flash_fwd plus (optional) per-split first maximum
+ *   pbest/parg (nsplit × B, item local to the head) and, with cmax, every
+ *   32-item chunk's row maximum (ceil(A/32) × B).
+ * rg_flash_argmax: top-1 over the splits (first maximum), out = -1 for a row
+ *   with no finite logit; out_max optional.
+ * rg_flash_topk: canonical top-K (value desc, index asc; K <= 32) from cmax:
+ *   candidate chunks are those whose maximum is >= tau - (tol_abs +
+ *   tol_rel·|tau|), tau = the K-th largest chunk maximum; their items are
+ *   rescored in fp32 (fmaf chain over HF, + bias).  cand: B × rg_flash_topk_cap()
+ *   int32, ncand: B int32; err |= 1 on a candidate overflow. */
+int rg_flash_rows_per_block(int HF);
+int rg_flash_fwd_top(const void* Hk, const void* Wk, const void* Wr, const float* bias_pad, int B, int A, int HF,
+                     int terms, int nsplit, float* pm, float* pl, float* pO, float* pbest, int32_t* parg, float* cmax,
+                     rg_stream_t stream);
+int rg_flash_argmax(const float* pbest, const int32_t* parg, int nsplit, int B, int32_t* out, float* out_max,
+                    rg_stream_t stream);
+int rg_flash_topk_cap(void);
+int rg_flash_topk(const float* cmax, int B, int A, int K, float tol_abs, float tol_rel, const float* h, const float* W,
+                  const float* bias, int HF, int32_t* cand, int32_t* ncand, int32_t* out_idx, float* out_val,
+                  int32_t* err, rg_stream_t stream);
 int rg_flash_lse(const float* pm, const float* pl, int nsplit, const float* h, const float* W, const float* bias,
                  const int64_t* tgt, int64_t lo, int A, int64_t A_full, int B, int HF, float* lse, float* zt,
                  rg_stream_t stream);

@@ -236,11 +236,11 @@ class OracleSMORL:
                  use_packed_seq, learning_rate, item_num, state_size, action_dim, gamma,
                  gru_layers, q_weights, alpha, div_embedding, unpopular_actions_set,
                  topk_div, topk_nov=1, nov_rew_sig=1.0, padding_idx=None,
-                 torch_rand_seed=118, python_rand_seed=999):
+                 torch_rand_seed=118, python_rand_seed=999, fp16_embeddings=False):
         torch.manual_seed(torch_rand_seed)
         random.seed(python_rand_seed)
         mk = lambda: Net("smorl", item_num, action_dim, embedding_dim, hidden_dim, gru_layers,
-                         train_pad_embed, use_packed_seq, padding_idx)
+                         train_pad_embed, use_packed_seq, padding_idx, emb_fp16=fp16_embeddings)
         self.nets = [mk(), mk()]
         self.opts = [make_adam(n, learning_rate) for n in self.nets]
         self.gamma, self.alpha = gamma, alpha

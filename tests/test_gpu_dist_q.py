@@ -56,13 +56,13 @@ def _nets(tr):
     return (tr.DQN_1, tr.DQN_2) if hasattr(tr, "DQN_1") else (tr.SMORL_1, tr.SMORL_2)
 
 
-def _rank(rank, port, out, kind, topk):
+def _rank(rank, port, out, kind, topk, extra):
     sys.path.insert(0, REPO)
     sys.path.insert(0, os.path.join(REPO, "ikea-recommender-system_amd"))
     import torch.distributed as dist
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=WORLD)
     try:
-        tr = _make(kind, topk, device="cuda:0", shard_items=True)
+        tr = _make(kind, topk, device="cuda:0", shard_items=True, **extra)
         losses = []
         for s, a, r, sn, ln, nln, e in _batches():
             sl = slice(rank * B, (rank + 1) * B)
@@ -76,21 +76,29 @@ def _rank(rank, port, out, kind, topk):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("kind,topk", [("sqn", None), ("smorl", (1, 1)), ("smorl", (3, 2))])
-def test_item_sharded_double_q_equals_single_gpu_global_batch(kind, topk):
+F16 = {"fp16_embeddings": True}
+X6 = {"matmul_precision": "f32x6"}
+
+
+@pytest.mark.parametrize("kind,topk,extra", [("sqn", None, {}), ("smorl", (1, 1), {}), ("smorl", (3, 2), {}),
+                                             ("sqn", None, F16), ("smorl", (3, 2), F16),
+                                             ("smorl", (1, 1), {**F16, **X6}), ("smorl", (3, 2), {**F16, **X6})])
+def test_item_sharded_double_q_equals_single_gpu_global_batch(kind, topk, extra):
     """Heads item-sharded and the item table row-sharded (ids / rows /
-    row-gradients exchanged by all-to-all, csrc/emb_shard.hip)."""
+    row-gradients exchanged by all-to-all, csrc/emb_shard.hip); fp16 item
+    table (C5); f32x6: the supervised head on the fused path, its SMORL top-k
+    from pass 1 merged across ranks."""
     sys.path.insert(0, os.path.join(REPO, "ikea-recommender-system_amd"))
     out = tempfile.mkdtemp()
     ctx = mp.get_context("spawn")
     port = _port()
-    procs = [ctx.Process(target=_rank, args=(r, port, out, kind, topk)) for r in range(WORLD)]
+    procs = [ctx.Process(target=_rank, args=(r, port, out, kind, topk, extra)) for r in range(WORLD)]
     for p in procs:
         p.start()
     for p in procs:
         p.join(timeout=300)
         assert p.exitcode == 0
-    ref = _make(kind, topk, device="cuda")
+    ref = _make(kind, topk, device="cuda", **extra)
     ref_losses = np.array([ref.train_step(s, a, r, sn, ln, nln, e) for s, a, r, sn, ln, nln, e in _batches()])
     from recommenders.hip.dist import item_shard
     lr = 0.005

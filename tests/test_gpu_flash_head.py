@@ -79,12 +79,13 @@ def inputs(B, A, HF, seed):
     return h, W, b, tgt
 
 
-# (B, A, HF, nsplit): partial 256-row workgroups (96, 288), ragged last item
+# (B, A, HF, nsplit): partial 256-row (HF 256: 128-row) workgroups, ragged last item
 # chunk (A % 32 != 0), empty splits (512 × 2077 with 64 splits), split counts
 # with and without the XCD reorder (total workgroups % 8)
 @pytest.mark.parametrize("precision", ["f32x9", "f32x6"])
 @pytest.mark.parametrize("B,A,HF,nsplit", [(64, 1000, 32, 8), (128, 3001, 64, 16), (256, 4133, 128, 8),
-                                           (512, 2077, 128, 64), (96, 777, 128, 3), (288, 50000, 128, 16)])
+                                           (512, 2077, 128, 64), (96, 777, 128, 3), (288, 50000, 128, 16),
+                                           (256, 3001, 256, 8), (96, 2077, 256, 24), (160, 777, 256, 3)])
 def test_flash_head_matches_fp64(precision, B, A, HF, nsplit):
     h, W, b, tgt = inputs(B, A, HF, B + A + HF)
     o = run_flash(h.to(dev), W.to(dev), b.to(dev), tgt.to(dev), TERMS[precision], nsplit)
@@ -220,3 +221,83 @@ def test_flash_error_is_fp32_class():
         floor = 8 * 2.0 ** -24 * float(r[k].abs().max())
         for p in ("f32x9", "f32x6"):
             assert table[p][k] <= max(4 * table["f32"][k], floor), (p, k, table)
+
+
+# ------------------------------------------------------------- fused top-k --
+def run_top(h, W, b, terms, nsplit, K):
+    """Pass 1 with the top-k outputs, then rg_flash_argmax (K = 1) or
+    rg_flash_topk: (idx (B, K) int64, vals (B, K) f64, err)."""
+    call, st = C().call, C().stream_ptr()
+    B, HF = h.shape
+    A = W.shape[0]
+    hb, wb = call("rg_head_plane_bytes", B, HF), call("rg_head_plane_bytes", A, HF)
+    Hk, Hr, Wk, Wr = _u8(hb), _u8(hb), _u8(wb), _u8(wb)
+    bp = torch.empty((A + 31) // 32 * 32, device=dev)
+    call("rg_head_planes", h.data_ptr(), B, HF, Hk.data_ptr(), Hr.data_ptr(), None, None, st)
+    call("rg_head_planes", W.data_ptr(), A, HF, Wk.data_ptr(), Wr.data_ptr(), b.data_ptr(), bp.data_ptr(), st)
+    z = lambda *s, dt=torch.float32: torch.full(s, -7, dtype=dt, device=dev)  # noqa: E731
+    pm, pl, pO = z(nsplit, B), z(nsplit, B), z(nsplit, HF, B)
+    pbest, parg = z(nsplit, B), z(nsplit, B, dt=torch.int32)
+    cmax = z((A + 31) // 32, B) if K > 1 else None
+    call("rg_flash_fwd_top", Hk.data_ptr(), Wk.data_ptr(), Wr.data_ptr(), bp.data_ptr(), B, A, HF, terms, nsplit,
+         pm.data_ptr(), pl.data_ptr(), pO.data_ptr(), pbest.data_ptr(), parg.data_ptr(),
+         None if cmax is None else cmax.data_ptr(), st)
+    idx, vals = z(B, K, dt=torch.int32), z(B, K)
+    err = torch.zeros(1, dtype=torch.int32, device=dev)
+    if K == 1:
+        call("rg_flash_argmax", pbest.data_ptr(), parg.data_ptr(), nsplit, B, idx.data_ptr(), vals.data_ptr(), st)
+    else:
+        cap = call("rg_flash_topk_cap")
+        cand, ncand = z(B, cap, dt=torch.int32), z(B, dt=torch.int32)
+        call("rg_flash_topk", cmax.data_ptr(), B, A, K, 1e-4, 1e-4, h.data_ptr(), W.data_ptr(), b.data_ptr(), HF,
+             cand.data_ptr(), ncand.data_ptr(), idx.data_ptr(), vals.data_ptr(), err.data_ptr(), st)
+    torch.cuda.synchronize()
+    return idx.cpu().long(), vals.cpu().double(), int(err.item()), (None if cmax is None else cmax.cpu().double())
+
+
+@pytest.mark.parametrize("precision", ["f32x6", "f32x9"])
+@pytest.mark.parametrize("B,A,HF,nsplit,K", [(128, 3001, 64, 8, 1), (96, 20011, 128, 16, 1), (256, 5000, 256, 8, 1),
+                                             (128, 3001, 64, 8, 12), (96, 20011, 128, 16, 20),
+                                             (160, 5003, 256, 8, 12), (64, 777, 32, 3, 32)])
+def test_fused_topk_matches_canonical_fp64(precision, B, A, HF, nsplit, K):
+    """torch.topk(sup, K) of SMORL's rewards (diversity.py:15-73, novelty.py:12-47)
+    from pass 1 without logits: index lists equal the canonical (value desc,
+    index asc) top-K of the fp64 logits except where two logits lie within the
+    arithmetic's error bound; values within fp32 rounding of fp64; chunk maxima
+    exact to the split-bf16 bound."""
+    from oracle import metrics as om
+    h, W, b, _ = inputs(B, A, HF, 3 * B + A + K)
+    idx, vals, err, cmax = run_top(h.to(dev), W.to(dev), b.to(dev), TERMS[precision], nsplit, K)
+    assert err == 0
+    Z = (h.double() @ W.double().t() + b.double()).numpy()
+    ref = om.canonical_topk_fast(Z, K)
+    got = idx.numpy()
+    tol = 2e-5
+    flips, gap = om.topk_flip_report(Z, got, ref, tol)
+    assert flips <= max(1, B // 50), (flips, gap)
+    np.testing.assert_allclose(vals.numpy(), np.take_along_axis(Z, got, 1), rtol=0, atol=tol)
+    # the device list is canonical in its own values
+    v = vals.numpy()
+    assert ((v[:, :-1] > v[:, 1:]) | ((v[:, :-1] == v[:, 1:]) & (got[:, :-1] < got[:, 1:]))).all()
+    if cmax is not None:
+        nct = (A + 31) // 32
+        Zp = np.full((B, nct * 32), -np.inf)
+        Zp[:, :A] = Z
+        np.testing.assert_allclose(cmax.numpy().T, Zp.reshape(B, nct, 32).max(2), rtol=0, atol=tol)
+
+
+def test_fused_topk_exact_ties_keep_lowest_index():
+    """Exact ties (duplicated W rows and biases): lowest item first, as the
+    canonical order and torch.argmax's first maximum."""
+    B, A, HF, K = 64, 4000, 64, 5
+    h, W, b, _ = inputs(B, A, HF, 21)
+    for j, src in ((3999, 17), (2500, 17), (1234, 17), (60, 800)):
+        W[j], b[j] = W[src], b[src]
+    # make item 17 every row's maximum
+    b[17] = b[3999] = b[2500] = b[1234] = 50.0
+    for K_ in (1, K):
+        idx, vals, err, _ = run_top(h.to(dev), W.to(dev), b.to(dev), 6, 8, K_)
+        assert err == 0
+        assert (idx[:, 0] == 17).all()
+        if K_ > 1:
+            assert (idx[:, 1:4] == torch.tensor([1234, 2500, 3999])).all()

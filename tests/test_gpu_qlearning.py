@@ -88,3 +88,48 @@ def test_sqn_matches_oracle_medium(N, L, B, H):
         rs_t = random.getstate()
         assert orc.last_main == tr.last_main
         assert abs(so - sg) < 1e-4 and abs(qo - qg) < 1e-5, (i, so, sg, qo, qg)
+
+
+@pytest.mark.parametrize("precision", ["f32", "f32x6"])
+def test_smorl_c5_shape_matches_oracle(precision):
+    """Config C5's model shape on one GPU, scaled down in items and batch:
+    SMORL 3-reward at d256 (E = H = 256: the time-stepped GRU), fp16 item
+    table (fp32 master + Adam), seq_len 100, top-k rewards with k > 1, against
+    the oracle's restatement of the same storage.  f32x6: the supervised head
+    on the fused split-bf16 path with its top-k recomputed for the rewards."""
+    from oracle.models import OracleSMORL
+    from recommenders.data_utils.synthetic import SessionStream, unpopular_items
+    from recommenders.models.SMORL.smorl_gru import SMORL_trainer
+    N, L, B, E = 4000, 100, 128, 256
+    st = SessionStream(N, L, B * 4, seed=17)
+    g = torch.Generator().manual_seed(7)
+    table = torch.randn(N + 1, 32, generator=g) * 0.01
+    unpop = unpopular_items(st.item_counts())
+    cfg = dict(hidden_dim=E, embedding_dim=E, padding_pos="end", train_pad_embed=True, use_packed_seq=True,
+               learning_rate=0.005, item_num=N, state_size=L, action_dim=N, gamma=0.5, gru_layers=1,
+               q_weights=[1.0, 0.5, 2.0], alpha=1.0, div_embedding=table, unpopular_actions_set=unpop, topk_div=3,
+               topk_nov=2, nov_rew_sig=1.0, fp16_embeddings=True)
+    torch.set_num_threads(8)
+    orc = OracleSMORL(**cfg)
+    rs_o = random.getstate()
+    tr = SMORL_trainer(device="cuda", matmul_precision=precision, **cfg)
+    rs_t = random.getstate()
+    for i in range(4):
+        b = st.batch(i, B)
+        random.setstate(rs_o)
+        so, qo = orc.step(*b)
+        rs_o = random.getstate()
+        random.setstate(rs_t)
+        sg, qg = tr.train_step(*b)
+        rs_t = random.getstate()
+        assert orc.last_main == tr.last_main
+        np.testing.assert_allclose(tr.last_rewards.cpu().numpy(), orc.last_rewards.numpy(), rtol=0, atol=1e-5)
+        assert abs(so - sg) < 1e-4 and abs(qo - qg) < 1e-5, (i, so, sg, qo, qg)
+    lr = cfg["learning_rate"]
+    for mine, ref in ((tr.SMORL_1, orc.nets[0]), (tr.SMORL_2, orc.nets[1])):
+        sd_o = ref.state_dict()
+        for k, v in mine.state_dict().items():
+            d = (v.cpu() - sd_o[k]).abs()
+            assert float(d.max()) <= 2 * lr + 1e-5, k
+            assert float((d > 1e-4).float().mean()) < 1e-3, k
+        assert torch.equal(mine.trunk.emb16.cpu(), mine.trunk.emb.p.cpu().half())
