@@ -249,142 +249,238 @@ extern "C" int rg_gru_bwd(const float* saved, int64_t plane, const float* Whh, c
   }
 }
 
-// ------------------------------------------------ time-stepped path -------
-// For hidden sizes whose recurrent matrix cannot stay register-resident
-// (H = 256, config C5: W_hh is 768 KB), the recurrence runs one timestep per
-// pair of launches from a native loop: Gh = h·W_hhᵀ + b_hh for the rows still
-// active at step t (an MFMA GEMM, rg_gemm_f32, whose row count nact[t] is read
-// on the device), then one fused gate kernel.  Rows are length-sorted
-// descending, so the rows active at t are the prefix [0, nact[t]).  Same
-// formulas, token layout and saved planes as k_gru_fwd / k_gru_bwd.
-extern "C" int rg_gemm_f32(const float* A, int64_t sam, int64_t sak, const float* B, int64_t sbk, int64_t sbn,
-                           float* C, int64_t ldc, const float* bias, int M, const int32_t* Mptr, int N, int K,
-                           const int32_t* Kptr, int splits, hipStream_t stream);
+// ------------------------------------------- persistent wide path (H 256) --
+// One launch for the whole sequence at H = 256 (config C5), where W_hh
+// (768 KB fp32) fits neither one CU's VGPRs nor its LDS: each workgroup owns
+// 32 length-sorted batch rows for all timesteps and streams W_hh from L2
+// (which holds it: 768 KB of each XCD's 4 MB) every step, as MFMA-fragment
+// ordered 16-B loads; h (fwd) / dG (BPTT) of the 32 rows is the A operand
+// from LDS.  v_mfma_f32_32x32x2_f32 (exact fp32): lane l feeds A[l%32][k] /
+// B[k][l%32] with k = 2q + l/32 of each 8-wide k block, and holds
+// C[acc32_row(r, l/32)][l%32] — one unit (column) × 16 rows per lane, so the
+// gate math stays lane-local.  Per step and wave: 3 gates × H/2 MFMAs.
+//
+// Fragment layout (k_gru_wfrag): frag[(nb·K/8 + kk)·64 + lane] (16 B) holds
+// M[kk·8 + 2q + lane/32][nb·32 + lane%32], q = 0..3, for the K × N operand
+// M[k][n] = src[k·sk + n·sn].  LDS rows store k at position
+// (k & ~7) + (k & 1)·4 + ((k >> 1) & 3), so a lane's four k values of one
+// block are one ds_read_b128.
+__device__ __forceinline__ int wide_pos(int k) { return (k & ~7) + (k & 1) * 4 + ((k >> 1) & 3); }
 
-// nact[t] = #rows with length > t, t ≤ tmax (nact[tmax] = 0)
-__global__ void k_gru_counts(const int32_t* __restrict__ lsort, int B, int tmax, int32_t* __restrict__ nact) {
-  const int t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t > tmax) return;
-  int lo = 0, hi = B;  // first row with lsort <= t (lsort descending)
-  while (lo < hi) {
-    const int mid = (lo + hi) >> 1;
-    if (lsort[mid] > t) lo = mid + 1;
-    else hi = mid;
+__global__ void k_gru_wfrag(const float* __restrict__ src, int64_t sk, int64_t sn, int K, int N, f4* __restrict__ frag) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int KK = K / 8;
+  if (e >= (int64_t)(N / 32) * KK * 64) return;
+  const int lane = (int)(e & 63);
+  const int64_t blk = e >> 6;
+  const int kk = (int)(blk % KK), nb = (int)(blk / KK);
+  const int n = nb * 32 + (lane & 31), k0 = kk * 8 + (lane >> 5);
+  f4 v;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) v[q] = src[(int64_t)(k0 + 2 * q) * sk + (int64_t)n * sn];
+  frag[e] = v;
+}
+
+template <int H>
+__global__ __launch_bounds__(2 * H) void k_gru_fwd_wide(const float* __restrict__ Gi, const f4* __restrict__ WF,
+                                                        const float* __restrict__ bhh, const int32_t* __restrict__ perm,
+                                                        const int32_t* __restrict__ lsort,
+                                                        const int32_t* __restrict__ offs, int B,
+                                                        float* __restrict__ hout, int ldh, int hoff,
+                                                        float* __restrict__ saved, int64_t plane) {
+  constexpr int NW = H / 32, KK = H / 8, LDX = H + 4;
+  __shared__ __attribute__((aligned(16))) float xs[2][32][LDX];
+  __shared__ int len_s[32], tok_s[32];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, hh = lane >> 5, j = lane & 31;
+  const int u = 32 * w + j;  // this lane's unit
+  const int r0 = blockIdx.x * 32;
+  if (tid < 32) {
+    const bool v = r0 + tid < B;
+    len_s[tid] = v ? lsort[r0 + tid] : 0;
+    tok_s[tid] = v ? offs[r0 + tid] : 0;
   }
-  nact[t] = lo;
-}
-
-__global__ void k_gru_step_fwd(int t, const float* __restrict__ Gi, const float* __restrict__ Gh,
-                               const int32_t* __restrict__ nact, const int32_t* __restrict__ offs, int H,
-                               float* __restrict__ hs, float* __restrict__ saved, int64_t plane) {
-  const int r = blockIdx.x;
-  if (r >= nact[t]) return;
-  const int64_t tok = offs[r] + t;
-  const float* gi = Gi + tok * 3 * H;
-  const float* gh = Gh + (int64_t)r * 3 * H;
-  for (int u = threadIdx.x; u < H; u += blockDim.x) {
-    const float hp = hs[(int64_t)r * H + u];
-    const float rr = sigmoidf_ref(gi[u] + gh[u]);
-    const float zz = sigmoidf_ref(gi[H + u] + gh[H + u]);
-    const float an = gh[2 * H + u];
-    const float nn = tanhf(gi[2 * H + u] + rr * an);
-    hs[(int64_t)r * H + u] = (hp - nn) * zz + nn;
-    if (saved) {
-      const int64_t o = tok * H + u;
-      saved[0 * plane + o] = hp;
-      saved[1 * plane + o] = rr;
-      saved[2 * plane + o] = zz;
-      saved[3 * plane + o] = nn;
-      saved[4 * plane + o] = an;
-    }
-  }
-}
-
-__global__ void k_gru_rows_out(const float* __restrict__ hs, const int32_t* __restrict__ perm, int B, int H,
-                               float* __restrict__ hout, int ldh, int hoff) {
-  const int r = blockIdx.x;
-  for (int u = threadIdx.x; u < H; u += blockDim.x) hout[(int64_t)perm[r] * ldh + hoff + u] = hs[(int64_t)r * H + u];
-}
-
-// dh entering step t: rows continuing from t+1 sum the direct and recurrent
-// terms left by step t+1; rows whose last token is t start from dh_final.
-__global__ void k_gru_step_bwd(int t, const float* __restrict__ saved, int64_t plane,
-                               const int32_t* __restrict__ nact, const int32_t* __restrict__ offs,
-                               const int32_t* __restrict__ perm, int H, const float* __restrict__ dhout, int lddh,
-                               int dhoff, float* __restrict__ dh_dir, const float* __restrict__ dh_mat,
-                               float* __restrict__ dGi, float* __restrict__ dGh, float* __restrict__ dGs) {
-  const int r = blockIdx.x;
-  if (r >= nact[t]) return;
-  const bool cont = r < nact[t + 1];
-  const int64_t tok = offs[r] + t;
-  const int G = 3 * H;
-  for (int u = threadIdx.x; u < H; u += blockDim.x) {
-    const int64_t ri = (int64_t)r * H + u;
-    const float dh = cont ? dh_dir[ri] + dh_mat[ri] : dhout[(int64_t)perm[r] * lddh + dhoff + u];
-    const int64_t o = tok * H + u;
-    const float hp = saved[0 * plane + o], rr = saved[1 * plane + o], zz = saved[2 * plane + o];
-    const float nn = saved[3 * plane + o], gh = saved[4 * plane + o];
-    const float dn = dh * (1.0f - zz);
-    const float dz = dh * (hp - nn);
-    const float dan = dn * (1.0f - nn * nn);
-    const float daz = dz * (zz * (1.0f - zz));
-    const float dar = (dan * gh) * (rr * (1.0f - rr));
-    const float dghn = dan * rr;
-    dh_dir[ri] = dh * zz;
-    float* gi = dGi + tok * G;
-    float* g2 = dGh + tok * G;
-    float* gs = dGs + (int64_t)r * G;
-    gi[u] = dar;
-    gi[H + u] = daz;
-    gi[2 * H + u] = dan;
-    g2[u] = dar;
-    g2[H + u] = daz;
-    g2[2 * H + u] = dghn;
-    gs[u] = dar;
-    gs[H + u] = daz;
-    gs[2 * H + u] = dghn;
-  }
-}
-
-extern "C" int rg_gru_fwd_steps(const float* Gi, const float* Whh, const float* bhh, const int32_t* perm,
-                                const int32_t* lsort, const int32_t* offs, int B, int H, int tmax, float* hout,
-                                int ldh, int hoff, float* saved, int64_t plane, float* work, hipStream_t stream) {
-  if (B <= 0 || H <= 0 || H % 4 || tmax <= 0) return RG_ERR_ARG;
-  float* hs = work;                                               // B × H
-  float* Gh = hs + (int64_t)B * H;                                // B × 3H
-  int32_t* nact = reinterpret_cast<int32_t*>(Gh + (int64_t)B * 3 * H);  // tmax + 1
-  hipLaunchKernelGGL(k_gru_counts, dim3((tmax + 256) / 256), dim3(256), 0, stream, lsort, B, tmax, nact);
-  if (hipMemsetAsync(hs, 0, sizeof(float) * (size_t)B * H, stream) != hipSuccess) return RG_ERR_LAUNCH;
-  const int thr = H < 256 ? H : 256;
+  for (int e = tid; e < 32 * LDX; e += 2 * H) xs[0][e / LDX][e % LDX] = 0.f;
+  const float br = bhh[u], bz = bhh[H + u], bn = bhh[2 * H + u];
+  const int tmax = lsort[r0];
+  const int pu = wide_pos(u);
+  const f4* wr_p = WF + (int64_t)(0 * NW + w) * KK * 64 + lane;
+  const f4* wz_p = WF + (int64_t)(1 * NW + w) * KK * 64 + lane;
+  const f4* wn_p = WF + (int64_t)(2 * NW + w) * KK * 64 + lane;
+  float h[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) h[i] = 0.f;
+  __syncthreads();
+  int cur = 0;
   for (int t = 0; t < tmax; ++t) {
-    int rc = rg_gemm_f32(hs, H, 1, Whh, 1, H, Gh, 3 * H, bhh, B, nact + t, 3 * H, H, nullptr, 1, stream);
-    if (rc != RG_OK) return rc;
-    hipLaunchKernelGGL(k_gru_step_fwd, dim3(B), dim3(thr), 0, stream, t, Gi, Gh, nact, offs, H, hs, saved, plane);
+    // this step's input-gate terms (issued ahead of the MFMAs)
+    float gr[16], gz[16], gn[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int row = acc32_row(i, hh);
+      gr[i] = gz[i] = gn[i] = 0.f;
+      if (t < len_s[row]) {
+        const float* g = Gi + (int64_t)(tok_s[row] + t) * (3 * H);
+        gr[i] = g[u];
+        gz[i] = g[H + u];
+        gn[i] = g[2 * H + u];
+      }
+    }
+    f16v ar, az, an;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      ar[i] = br;
+      az[i] = bz;
+      an[i] = bn;
+    }
+    const float* xa = &xs[cur][j][hh * 4];
+#pragma unroll 4
+    for (int kk = 0; kk < KK; ++kk) {
+      const f4 a = *reinterpret_cast<const f4*>(xa + kk * 8);
+      const f4 vr = wr_p[kk * 64], vz = wz_p[kk * 64], vn = wn_p[kk * 64];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        ar = mfma32(a[q], vr[q], ar);
+        az = mfma32(a[q], vz[q], az);
+        an = mfma32(a[q], vn[q], an);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int row = acc32_row(i, hh);
+      if (t < len_s[row]) {
+        const float rr = sigmoidf_ref(gr[i] + ar[i]);
+        const float zz = sigmoidf_ref(gz[i] + az[i]);
+        const float nn = tanhf(gn[i] + rr * an[i]);
+        const float hn = (h[i] - nn) * zz + nn;
+        if (saved) {
+          const int64_t o = (int64_t)(tok_s[row] + t) * H + u;
+          saved[0 * plane + o] = h[i];
+          saved[1 * plane + o] = rr;
+          saved[2 * plane + o] = zz;
+          saved[3 * plane + o] = nn;
+          saved[4 * plane + o] = an[i];
+        }
+        h[i] = hn;
+      }
+      xs[cur ^ 1][row][pu] = h[i];
+    }
+    __syncthreads();
+    cur ^= 1;
   }
-  hipLaunchKernelGGL(k_gru_rows_out, dim3(B), dim3(thr), 0, stream, hs, perm, B, H, hout, ldh, hoff);
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int row = r0 + acc32_row(i, hh);
+    if (row < B) hout[(int64_t)perm[row] * ldh + hoff + u] = h[i];
+  }
+}
+
+template <int H>
+__global__ __launch_bounds__(2 * H) void k_gru_bwd_wide(const float* __restrict__ saved, int64_t plane,
+                                                        const f4* __restrict__ WB, const int32_t* __restrict__ perm,
+                                                        const int32_t* __restrict__ lsort,
+                                                        const int32_t* __restrict__ offs, int B,
+                                                        const float* __restrict__ dhout, int lddh, int dhoff,
+                                                        float* __restrict__ dGi, float* __restrict__ dGh) {
+  constexpr int G = 3 * H, KK = G / 8, LDG = G + 4;
+  __shared__ __attribute__((aligned(16))) float gs[32][LDG];
+  __shared__ int len_s[32], tok_s[32];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, hh = lane >> 5, j = lane & 31;
+  const int u = 32 * w + j;
+  const int r0 = blockIdx.x * 32;
+  if (tid < 32) {
+    const bool v = r0 + tid < B;
+    len_s[tid] = v ? lsort[r0 + tid] : 0;
+    tok_s[tid] = v ? offs[r0 + tid] : 0;
+  }
+  const int tmax = lsort[r0];
+  const int p0 = wide_pos(u), p1 = wide_pos(H + u), p2 = wide_pos(2 * H + u);
+  const f4* wb_p = WB + (int64_t)w * KK * 64 + lane;
+  float dh[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int row = r0 + acc32_row(i, hh);
+    dh[i] = row < B ? dhout[(int64_t)perm[row] * lddh + dhoff + u] : 0.f;
+  }
+  __syncthreads();
+  for (int t = tmax - 1; t >= 0; --t) {
+    float dhd[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int row = acc32_row(i, hh);
+      float dar = 0.f, daz = 0.f, dghn = 0.f;
+      dhd[i] = dh[i];
+      if (t < len_s[row]) {
+        const int64_t tok = tok_s[row] + t;
+        const int64_t o = tok * H + u;
+        const float hp = saved[0 * plane + o], rr = saved[1 * plane + o], zz = saved[2 * plane + o];
+        const float nn = saved[3 * plane + o], gh = saved[4 * plane + o];
+        const float dn = dh[i] * (1.0f - zz);
+        const float dz = dh[i] * (hp - nn);
+        dhd[i] = dh[i] * zz;
+        const float dan = dn * (1.0f - nn * nn);
+        daz = dz * (zz * (1.0f - zz));
+        dar = (dan * gh) * (rr * (1.0f - rr));
+        dghn = dan * rr;
+        float* gi = dGi + tok * G;
+        float* g2 = dGh + tok * G;
+        gi[u] = dar;
+        gi[H + u] = daz;
+        gi[2 * H + u] = dan;
+        g2[u] = dar;
+        g2[H + u] = daz;
+        g2[2 * H + u] = dghn;
+      }
+      gs[row][p0] = dar;
+      gs[row][p1] = daz;
+      gs[row][p2] = dghn;
+    }
+    __syncthreads();
+    if (t > 0) {  // recurrent term of step t-1: W_hhᵀ · dG
+      f16v acc = {};
+      const float* ga = &gs[j][hh * 4];
+#pragma unroll 4
+      for (int kk = 0; kk < KK; ++kk) {
+        const f4 a = *reinterpret_cast<const f4*>(ga + kk * 8);
+        const f4 v = wb_p[kk * 64];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) acc = mfma32(a[q], v[q], acc);
+      }
+#pragma unroll
+      for (int i = 0; i < 16; ++i)
+        if (t < len_s[acc32_row(i, hh)]) dh[i] = dhd[i] + acc[i];
+    }
+    __syncthreads();
+  }
+}
+
+extern "C" int64_t rg_gru_wide_work_bytes(int H) { return H == 256 ? (int64_t)3 * H * H * 4 : RG_ERR_SHAPE; }
+
+extern "C" int rg_gru_fwd_wide(const float* Gi, const float* Whh, const float* bhh, const int32_t* perm,
+                               const int32_t* lsort, const int32_t* offs, int B, int H, float* hout, int ldh, int hoff,
+                               float* saved, int64_t plane, void* wfrag, hipStream_t stream) {
+  if (B <= 0 || !Gi || !Whh || !bhh || !perm || !lsort || !offs || !hout || !wfrag) return RG_ERR_ARG;
+  if (H != 256) return RG_ERR_SHAPE;
+  const int64_t nf = (int64_t)3 * H / 32 * (H / 8) * 64;
+  // operand M[k][n] = W_hh[n][k]: K = H, N = 3H
+  hipLaunchKernelGGL(k_gru_wfrag, dim3((unsigned)((nf + 255) / 256)), dim3(256), 0, stream, Whh, (int64_t)1,
+                     (int64_t)H, H, 3 * H, (f4*)wfrag);
+  hipLaunchKernelGGL(k_gru_fwd_wide<256>, dim3((B + 31) / 32), dim3(2 * 256), 0, stream, Gi, (const f4*)wfrag, bhh,
+                     perm, lsort, offs, B, hout, ldh, hoff, saved, plane);
   RG_LAUNCH_CHECK();
   return RG_OK;
 }
 
-extern "C" int rg_gru_bwd_steps(const float* saved, int64_t plane, const float* Whh, const int32_t* perm,
-                                const int32_t* lsort, const int32_t* offs, int B, int H, int tmax,
-                                const float* dhout, int lddh, int dhoff, float* dGi, float* dGh, float* work,
-                                hipStream_t stream) {
-  if (B <= 0 || H <= 0 || H % 4 || tmax <= 0) return RG_ERR_ARG;
-  float* dh_dir = work;                                            // B × H
-  float* dh_mat = dh_dir + (int64_t)B * H;                         // B × H
-  float* dGs = dh_mat + (int64_t)B * H;                            // B × 3H
-  int32_t* nact = reinterpret_cast<int32_t*>(dGs + (int64_t)B * 3 * H);  // tmax + 1
-  hipLaunchKernelGGL(k_gru_counts, dim3((tmax + 256) / 256), dim3(256), 0, stream, lsort, B, tmax, nact);
-  const int thr = H < 256 ? H : 256;
-  for (int t = tmax - 1; t >= 0; --t) {
-    hipLaunchKernelGGL(k_gru_step_bwd, dim3(B), dim3(thr), 0, stream, t, saved, plane, nact, offs, perm, H, dhout,
-                       lddh, dhoff, dh_dir, dh_mat, dGi, dGh, dGs);
-    if (t > 0) {  // recurrent term for step t−1: dGs · W_hh over the active rows
-      int rc = rg_gemm_f32(dGs, 3 * H, 1, Whh, H, 1, dh_mat, H, nullptr, B, nact + t, H, 3 * H, nullptr, 1, stream);
-      if (rc != RG_OK) return rc;
-    }
-  }
+extern "C" int rg_gru_bwd_wide(const float* saved, int64_t plane, const float* Whh, const int32_t* perm,
+                               const int32_t* lsort, const int32_t* offs, int B, int H, const float* dhout, int lddh,
+                               int dhoff, float* dGi, float* dGh, void* wfrag, hipStream_t stream) {
+  if (B <= 0 || !saved || !Whh || !perm || !lsort || !offs || !dhout || !dGi || !dGh || !wfrag) return RG_ERR_ARG;
+  if (H != 256) return RG_ERR_SHAPE;
+  const int64_t nf = (int64_t)H / 32 * (3 * H / 8) * 64;
+  // operand M[k][n] = W_hh[k][n]: K = 3H, N = H
+  hipLaunchKernelGGL(k_gru_wfrag, dim3((unsigned)((nf + 255) / 256)), dim3(256), 0, stream, Whh, (int64_t)H,
+                     (int64_t)1, 3 * H, H, (f4*)wfrag);
+  hipLaunchKernelGGL(k_gru_bwd_wide<256>, dim3((B + 31) / 32), dim3(2 * 256), 0, stream, saved, plane,
+                     (const f4*)wfrag, perm, lsort, offs, B, dhout, lddh, dhoff, dGi, dGh);
   RG_LAUNCH_CHECK();
   return RG_OK;
 }

@@ -23,7 +23,7 @@ I32 = C.c_int32
 U64 = C.c_uint64
 
 # entry points returning int64_t (all others return int)
-RESTYPE_I64 = {"rg_sampled_work_bytes", "rg_head_work_bytes", "rg_head_plane_bytes"}
+RESTYPE_I64 = {"rg_sampled_work_bytes", "rg_head_work_bytes", "rg_head_plane_bytes", "rg_gru_wide_work_bytes"}
 
 # name -> argtypes
 SIGNATURES = {
@@ -77,8 +77,9 @@ SIGNATURES = {
     "rg_topk": [P, I64, P, I, I, I, P, P, P, P],
     "rg_hits_ndcg": [P, I, P, I, P, I, P, P],
     "rg_mask_scale": [P, P, F, I64, P, P],
-    "rg_gru_fwd_steps": [P, P, P, P, P, P, I, I, I, P, I, I, P, I64, P, P],
-    "rg_gru_bwd_steps": [P, I64, P, P, P, P, I, I, I, P, I, I, P, P, P, P],
+    "rg_gru_wide_work_bytes": [I],
+    "rg_gru_fwd_wide": [P, P, P, P, P, P, I, I, P, I, I, P, I64, P, P],
+    "rg_gru_bwd_wide": [P, I64, P, P, P, P, I, I, P, I, I, P, P, P, P],
     "rg_gather_h": [P, I, I, P, P, P, P, I64, I, I, P, P, P, P],
     "rg_adam_rows_h": [P, P, P, P, P, I32, I64, I, P, P, P],
     "rg_f32_to_f16": [P, I64, P, P],

@@ -136,8 +136,8 @@ class _TrunkWS:
         self.Gi = [z(TM, 3 * H) for _ in range(ndir)]
         self.h = torch.zeros(B, ndir * H, device=device)
         self.plane = TM * H
-        self.step_work = z(5 * B * H + L + 8) if H > 128 else None
-        self.tmax = L
+        # H = 256: W_hh's MFMA fragments for the persistent wide GRU (csrc/gru.hip)
+        self.wfrag = z(call("rg_gru_wide_work_bytes", H) // 4) if H > 128 else None
         self.saved = [z(5, TM, H) for _ in range(ndir)] if save else None
         if save:
             self.dGi = [z(TM, 3 * H) for _ in range(ndir)]
@@ -173,9 +173,10 @@ class Trunk:
         self.device = device
         if E not in _WIDTHS or H not in _WIDTHS:
             raise RuntimeError(f"unsupported trunk shape E={E} H={H} (E, H in {_WIDTHS})")
-        # H <= 128: persistent recurrence with W_hh in VGPRs; H = 256: time-stepped
-        # path (W_hh is 768 KB; csrc/gru.hip rg_gru_fwd_steps / rg_gru_bwd_steps)
-        self.stepped = H > 128
+        # H <= 128: persistent recurrence with W_hh in VGPRs; H = 256: persistent
+        # wide recurrence streaming W_hh (768 KB) from L2 (csrc/gru.hip
+        # rg_gru_fwd_wide / rg_gru_bwd_wide)
+        self.wide = H > 128
         # comm (multi-GPU): the table is row-sharded, this rank holds rows
         # [lo, hi) (full init drawn first: RNG parity with one GPU); the rows a
         # pass needs are exchanged by all-to-all (csrc/emb_shard.hip)
@@ -228,8 +229,6 @@ class Trunk:
         w = self.ws(slot, B, L, save)
         st = stream_ptr()
         w.lens.copy_(lens, non_blocking=True)
-        if self.stepped:  # host bound of the timestep loop (no device sync)
-            w.tmax = max(1, min(L, int(lens.max()))) if self.packed and lens.device.type == "cpu" else L
         with region("pack"):
             call("rg_pack", w.lens.data_ptr(), B, L, 0 if self.packed else 1, w.perm.data_ptr(),
                  w.lsort.data_ptr(), w.offs.data_ptr(), st)
@@ -252,11 +251,11 @@ class Trunk:
                 call("rg_gemm_f32", w.X[d].data_ptr(), E, 1, w_ih.p.data_ptr(), 1, E, w.Gi[d].data_ptr(), 3 * H,
                      b_ih.p.data_ptr(), w.TM, w.ntok_ptr, 3 * H, E, None, 1, st)
             with region("gru_fwd"):
-                if self.stepped:
-                    call("rg_gru_fwd_steps", w.Gi[d].data_ptr(), w_hh.p.data_ptr(), b_hh.p.data_ptr(),
-                         w.perm.data_ptr(), w.lsort.data_ptr(), w.offs.data_ptr(), B, H, w.tmax, w.h.data_ptr(),
+                if self.wide:
+                    call("rg_gru_fwd_wide", w.Gi[d].data_ptr(), w_hh.p.data_ptr(), b_hh.p.data_ptr(),
+                         w.perm.data_ptr(), w.lsort.data_ptr(), w.offs.data_ptr(), B, H, w.h.data_ptr(),
                          self.ndir * H, d * H, w.saved[d].data_ptr() if save else None, w.plane,
-                         w.step_work.data_ptr(), st)
+                         w.wfrag.data_ptr(), st)
                 else:
                     call("rg_gru_fwd", w.Gi[d].data_ptr(), w_hh.p.data_ptr(), b_hh.p.data_ptr(),
                          w.perm.data_ptr(), w.lsort.data_ptr(), w.offs.data_ptr(), B, H, w.h.data_ptr(),
@@ -272,10 +271,10 @@ class Trunk:
         for d in range(self.ndir):
             w_ih, w_hh, _, _ = self.dirs[d]
             with region("gru_bwd"):
-                if self.stepped:
-                    call("rg_gru_bwd_steps", w.saved[d].data_ptr(), w.plane, w_hh.p.data_ptr(), w.perm.data_ptr(),
-                         w.lsort.data_ptr(), w.offs.data_ptr(), B, H, w.tmax, dh.data_ptr(), self.ndir * H,
-                         d * H, w.dGi[d].data_ptr(), w.dGh[d].data_ptr(), w.step_work.data_ptr(), st)
+                if self.wide:
+                    call("rg_gru_bwd_wide", w.saved[d].data_ptr(), w.plane, w_hh.p.data_ptr(), w.perm.data_ptr(),
+                         w.lsort.data_ptr(), w.offs.data_ptr(), B, H, dh.data_ptr(), self.ndir * H, d * H,
+                         w.dGi[d].data_ptr(), w.dGh[d].data_ptr(), w.wfrag.data_ptr(), st)
                 else:
                     call("rg_gru_bwd", w.saved[d].data_ptr(), w.plane, w_hh.p.data_ptr(), w.perm.data_ptr(),
                          w.lsort.data_ptr(), w.offs.data_ptr(), B, H, dh.data_ptr(), self.ndir * H, d * H,

@@ -251,16 +251,18 @@ int rg_weighted_sum(const float* const* X, const float* w, int nh, int64_t n, fl
 /* SMORL reward matrix r (B, 3) f32 = stack([r_acc f64, r_div, r_nov]) (SMORL/smorl_gru.py:311-314, 3 rewards) */
 int rg_stack_rewards(const double* r_acc, const float* r_div, const float* r_nov, int B, float* r, rg_stream_t stream);
 
-/* Time-stepped GRU for hidden sizes whose W_hh cannot stay register-resident (H = 256, config C5;
- * any H % 4 == 0): same contract as rg_gru_fwd / rg_gru_bwd plus tmax (the longest row, host value)
- * and a workspace of 5*B*H + tmax + 1 floats; the timestep loop runs natively, one MFMA GEMM
- * (rg_gemm_f32, device-side active-row count) + one fused gate kernel per step. */
-int rg_gru_fwd_steps(const float* Gi, const float* Whh, const float* bhh, const int32_t* perm, const int32_t* lsort,
-                     const int32_t* offs, int B, int H, int tmax, float* hout, int ldh, int hoff, float* saved,
-                     int64_t plane, float* work, rg_stream_t stream);
-int rg_gru_bwd_steps(const float* saved, int64_t plane, const float* Whh, const int32_t* perm, const int32_t* lsort,
-                     const int32_t* offs, int B, int H, int tmax, const float* dhout, int lddh, int dhoff,
-                     float* dGi, float* dGh, float* work, rg_stream_t stream);
+/* Persistent wide GRU for H = 256 (config C5), whose W_hh (768 KB) fits neither one CU's VGPRs nor
+ * its LDS: same contract as rg_gru_fwd / rg_gru_bwd (GRU4Rec/model.py:49-55, 76-77; one launch for
+ * the whole sequence, 32 rows per workgroup, W_hh streamed from L2 as MFMA fragments every step)
+ * plus wfrag, rg_gru_wide_work_bytes(H) bytes of device scratch (the fragment copy of W_hh, rebuilt
+ * by each call). */
+int64_t rg_gru_wide_work_bytes(int H);
+int rg_gru_fwd_wide(const float* Gi, const float* Whh, const float* bhh, const int32_t* perm, const int32_t* lsort,
+                    const int32_t* offs, int B, int H, float* hout, int ldh, int hoff, float* saved, int64_t plane,
+                    void* wfrag, rg_stream_t stream);
+int rg_gru_bwd_wide(const float* saved, int64_t plane, const float* Whh, const int32_t* perm, const int32_t* lsort,
+                    const int32_t* offs, int B, int H, const float* dhout, int lddh, int dhoff, float* dGi,
+                    float* dGh, void* wfrag, rg_stream_t stream);
 
 /* ---- fp16 embedding storage (config C5: the gather reads an fp16 copy of the table, Adam keeps the
  * fp32 master and moments; fp16 = IEEE binary16 bits, round to nearest even) ---- */

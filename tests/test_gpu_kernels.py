@@ -108,12 +108,14 @@ def gru_ref(X_rows, lens, perm_order, Wih, Whh, bih, bhh, H):
     return hs
 
 
-@pytest.mark.parametrize("H,stepped", [(16, False), (32, False), (64, False), (128, False), (64, True),
-                                       (256, True)])
-def test_gru_forward_backward(H, stepped):
-    """stepped: the time-stepped path (per-step MFMA GEMM + gate kernel) used for H = 256."""
-    g = torch.Generator().manual_seed(3)
-    B, L, E = 37, 7, H
+@pytest.mark.parametrize("H,B,L", [(16, 37, 7), (32, 37, 7), (64, 37, 7), (128, 37, 7), (256, 37, 7),
+                                   (256, 77, 23)])
+def test_gru_forward_backward(H, B, L):
+    """H = 256: the persistent wide path (W_hh streamed from L2 as MFMA
+    fragments, 32 rows per workgroup; partial last workgroup at B = 37, 77)."""
+    wide = H == 256
+    g = torch.Generator().manual_seed(3 + L)
+    E = H
     lens = torch.randint(1, L + 1, (B,), generator=g)
     X = torch.randn(B, L, E, generator=g) * 0.5
     k = 1 / H ** 0.5
@@ -128,10 +130,10 @@ def test_gru_forward_backward(H, stepped):
     Gi = (packed.double() @ Wih.double().t() + bih.double()).float().to(dev)
     hout = torch.zeros(B, H, device=dev)
     saved = torch.zeros(5, T, H, device=dev)
-    work = torch.zeros(5 * B * H + L + 8, device=dev)
-    if stepped:
-        C().call("rg_gru_fwd_steps", Gi.data_ptr(), D(Whh).data_ptr(), D(bhh).data_ptr(), perm.data_ptr(),
-                 ls.data_ptr(), offs.data_ptr(), B, H, L, hout.data_ptr(), H, 0, saved.data_ptr(), T * H,
+    work = torch.zeros(C().call("rg_gru_wide_work_bytes", H) // 4 if wide else 1, device=dev)
+    if wide:
+        C().call("rg_gru_fwd_wide", Gi.data_ptr(), D(Whh).data_ptr(), D(bhh).data_ptr(), perm.data_ptr(),
+                 ls.data_ptr(), offs.data_ptr(), B, H, hout.data_ptr(), H, 0, saved.data_ptr(), T * H,
                  work.data_ptr(), st())
     else:
         C().call("rg_gru_fwd", Gi.data_ptr(), D(Whh).data_ptr(), D(bhh).data_ptr(), perm.data_ptr(),
@@ -156,9 +158,9 @@ def test_gru_forward_backward(H, stepped):
     (href * dh.double()).sum().backward()
     dGi = torch.zeros(T, 3 * H, device=dev)
     dGh = torch.zeros(T, 3 * H, device=dev)
-    if stepped:
-        C().call("rg_gru_bwd_steps", saved.data_ptr(), T * H, D(Whh).data_ptr(), perm.data_ptr(), ls.data_ptr(),
-                 offs.data_ptr(), B, H, L, D(dh).data_ptr(), H, 0, dGi.data_ptr(), dGh.data_ptr(), work.data_ptr(),
+    if wide:
+        C().call("rg_gru_bwd_wide", saved.data_ptr(), T * H, D(Whh).data_ptr(), perm.data_ptr(), ls.data_ptr(),
+                 offs.data_ptr(), B, H, D(dh).data_ptr(), H, 0, dGi.data_ptr(), dGh.data_ptr(), work.data_ptr(),
                  st())
     else:
         C().call("rg_gru_bwd", saved.data_ptr(), T * H, D(Whh).data_ptr(), perm.data_ptr(), ls.data_ptr(),
