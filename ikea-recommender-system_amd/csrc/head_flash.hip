@@ -48,24 +48,41 @@ constexpr float LN2 = 0.6931471805599453f;
 // waves per workgroup: 8 (2 per SIMD) up to HF 128; at HF 256 a wave's
 // operand planes (192 VGPRs) and O / dW accumulators (128) need the whole
 // 512-register file, so 4 (1 per SIMD)
-constexpr int fl_waves(int HF) { return HF >= 256 ? 4 : 8; }
+// Waves per workgroup and 32-row (pass 1) / 32-item (pass 2) blocks per
+// wave.  RB = 2 lets every LDS operand fragment feed two MFMA chains (half
+// the LDS read traffic per MFMA) but needs most of the 512-register file, so
+// one wave per SIMD; measured at C2 (HF 128, f32x6) it lost to two one-block
+// waves per SIMD (pass 2: 10.7 vs 9.7 ms; pass 1 spills), so RB = 1 and eight
+// waves up to HF 128.  HF 256: a block's operand planes alone take 192
+// VGPRs, so four waves (one per SIMD).
+constexpr int fl_rb(int, int) { return 1; }
+constexpr int fl_nw(int HF, int) { return HF <= 128 ? 8 : 4; }
+constexpr int fl_rows(int HF, int pass) { return 32 * fl_rb(HF, pass) * fl_nw(HF, pass); }
 
 // element i of lane half hh inside a 16-deep k slice -> row offset
 __device__ __forceinline__ int kperm(int hh, int i) { return (i & 3) + 8 * (i >> 2) + 4 * hh; }
 
-// 16-byte global -> LDS DMA; LDS address = wave-uniform base + 16·lane
-__device__ __forceinline__ void glds16(const void* src, void* lds_wave_base) {
-  __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)const_cast<void*>(src),
-                                   (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0, 0);
+// raw buffer resource over `base` (SGPRs; num_records = 2^31 - 1 bytes)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_of(const void* base) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, 0x7fffffff, 0x00020000);
+}
+
+// 16-byte buffer -> LDS DMA: lane reads base + voff + soff, LDS address =
+// wave-uniform base + 16·lane.  Addresses cost one VGPR (voff) per wave.
+__device__ __forceinline__ void blds16(__amdgpu_buffer_rsrc_t r, void* lds_wave_base, int voff, int soff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds_wave_base, 16, voff,
+                                           soff, 0, 0);
 }
 
 // copy E 16-B entries (E % 64 == 0) from global to LDS, sliced over NW waves
+// (w wave-uniform, lane16 = 16·lane)
 template <int E, int NW>
-__device__ __forceinline__ void stage(const bf16x8* __restrict__ src, bf16x8* dst, int w, int lane) {
+__device__ __forceinline__ void stage(const bf16x8* __restrict__ src, bf16x8* dst, int w, int lane16) {
+  const __amdgpu_buffer_rsrc_t r = rsrc_of(src);
 #pragma unroll
   for (int q = 0; q < (E + 64 * NW - 1) / (64 * NW); ++q) {
     const int e0 = 64 * NW * q + 64 * w;  // wave-uniform
-    if (e0 < E) glds16(src + e0 + lane, dst + e0);
+    if (e0 < E) blds16(r, dst + e0, lane16, 16 * e0);
   }
 }
 
@@ -133,12 +150,12 @@ __global__ void k_pad_bias(const float* __restrict__ bias, int A, int Ap, float*
 // ARG: also the row's top-1 (value, item) per split and, with cmax, every
 // chunk's row maximum — the inputs of the fused top-k (SMORL's rewards).
 template <int HF, int NT, bool ARG>
-__global__ __launch_bounds__(64 * fl_waves(HF)) void k_flash_fwd(
+__global__ __launch_bounds__(64 * fl_nw(HF, 1)) void k_flash_fwd(
     const bf16x8* __restrict__ Hk, const bf16x8* __restrict__ Wk, const bf16x8* __restrict__ Wr,
     const float* __restrict__ bias_pad, int B, int A, int nrb, int nsplit, int cps, float* __restrict__ pm,
     float* __restrict__ pl, float* __restrict__ pO, float* __restrict__ pbest, int32_t* __restrict__ parg,
     float* __restrict__ cmax) {
-  constexpr int NW = fl_waves(HF);
+  constexpr int NW = fl_nw(HF, 1), RB = fl_rb(HF, 1);
   constexpr bool DR = HF <= 128;      // double-buffered R-planes
   constexpr int NS = HF / 16, NTL = HF / 32;
   constexpr int EK = NS * 192;        // entries per 32-row block, K-planes
@@ -146,105 +163,137 @@ __global__ __launch_bounds__(64 * fl_waves(HF)) void k_flash_fwd(
   __shared__ bf16x8 sk0[EK], sk1[EK];
   __shared__ bf16x8 sr0[ER], sr1[DR ? ER : 1];
   __shared__ __attribute__((aligned(16))) float sb0[32], sb1[32];
-  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, hh = lane >> 5, l32 = lane & 31;
+  const int tid = threadIdx.x, lane = tid & 63, hh = lane >> 5, l32 = lane & 31, lane16 = 16 * lane;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   // XCD-aware order: the nrb row blocks of one item split are dispatched to
   // the same XCD (round-robin dispatch), so its W chunks are fetched once
   // into that XCD's L2 and re-read from there
   int bid = blockIdx.x;
   const int total = nrb * nsplit;
   if ((total & 7) == 0) bid = (bid & 7) * (total >> 3) + (bid >> 3);
-  const int split = bid / nrb, rb = bid % nrb;
-  const int r0 = rb * 32 * NW + 32 * w;
-  const bool active = r0 < B;
+  const int split = bid / nrb, rblk = bid % nrb;
+  const int r0 = rblk * fl_rows(HF, 1) + 32 * RB * w;   // this wave's first row
+  const bool active = r0 < B;                        // any of its RB blocks
   const int nct = (A + 31) / 32;
   const int c0 = split * cps;
   const int nch = max(0, min(nct, c0 + cps) - c0);
 #define FL_ISSUE_K(C, SK, SB)                                                  \
   do {                                                                         \
-    stage<EK, NW>(Wk + (int64_t)(C) * EK, SK, w, lane);                        \
-    if (w == 0 && lane < 8) glds16(bias_pad + 32 * (C) + 4 * lane, SB);        \
+    stage<EK, NW>(Wk + (int64_t)(C) * EK, SK, w, lane16);                      \
+    if (w == 0 && lane < 8) blds16(rsrc_of(bias_pad + 32 * (C)), SB, lane16, 0); \
   } while (0)
-#define FL_ISSUE_R(C, SR) stage<ER, NW>(Wr + (int64_t)(C) * ER, SR, w, lane)
+#define FL_ISSUE_R(C, SR) stage<ER, NW>(Wr + (int64_t)(C) * ER, SR, w, lane16)
   if (nch > 0) {
     FL_ISSUE_K(c0, sk0, sb0);
     FL_ISSUE_R(c0, sr0);
   }
-  // this wave's 32 rows of h (B operand of Sᵀ = W_c·hᵀ) for the whole split
-  bf16x8 hk[NS][3];
+  // this wave's RB × 32 rows of h (B operands of Sᵀ = W_c·hᵀ) for the whole split
+  bf16x8 hk[RB][NS][3];
 #pragma unroll
-  for (int s = 0; s < NS; ++s)
-#pragma unroll
-    for (int p = 0; p < 3; ++p)
-      hk[s][p] = active ? Hk[((int64_t)(r0 >> 5) * NS + s) * 192 + p * 64 + lane] : bf16x8{};
-  f16v o[NTL];
-#pragma unroll
-  for (int t = 0; t < NTL; ++t) o[t] = f16v{};
-  float m = NEG_INF, l = 0.f;
-  float bv = NEG_INF;   // ARG: this lane's best logit (natural units) and item
-  int bi = INT32_MAX;
-  __syncthreads();
-  // S-part of chunk c: Sᵀ, (ARG) top-1 / chunk max, online max / Σexp, P planes
-  auto spart = [&](const bf16x8* sk, const float* sb, int c, bf16x8 (&q0)[2], bf16x8 (&q1)[2], bf16x8 (&q2)[2])
-      __attribute__((always_inline)) {
-    f16v sa = {};
+  for (int j = 0; j < RB; ++j)
 #pragma unroll
     for (int s = 0; s < NS; ++s)
-      sa = mfma_split<NT>(sk[s * 192 + lane], sk[s * 192 + 64 + lane], sk[s * 192 + 128 + lane], hk[s][0], hk[s][1],
-                          hk[s][2], sa);
-    // logits (item acc32_row(r, hh) of the chunk, row l32)
-    float cm = NEG_INF;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const f4 bq = *reinterpret_cast<const f4*>(&sb[8 * q + 4 * hh]);
+      for (int p = 0; p < 3; ++p)
+        hk[j][s][p] = r0 + 32 * j < B ? Hk[((int64_t)((r0 >> 5) + j) * NS + s) * 192 + p * 64 + lane] : bf16x8{};
+  f16v o[RB][NTL];
+  float m[RB], l[RB], bv[RB];  // bv / bi (ARG): this lane's best logit (natural units) and item
+  int bi[RB];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const float z = sa[4 * q + u] + bq[u];
-        if (ARG && z > bv) {  // items increase with r: strict > keeps the first maximum
-          bv = z;
-          bi = 32 * (c0 + c) + 8 * q + 4 * hh + u;
+  for (int j = 0; j < RB; ++j) {
+#pragma unroll
+    for (int t = 0; t < NTL; ++t) o[j][t] = f16v{};
+    m[j] = NEG_INF;
+    l[j] = 0.f;
+    bv[j] = NEG_INF;
+    bi[j] = INT32_MAX;
+  }
+  __syncthreads();
+  // S-part of chunk c for every block: Sᵀ, (ARG) top-1 / chunk max, online
+  // max / Σexp, P planes
+  auto spart = [&](const bf16x8* sk, const float* sb, int c, bf16x8 (&q0)[RB][2], bf16x8 (&q1)[RB][2],
+                   bf16x8 (&q2)[RB][2]) __attribute__((always_inline)) {
+    f16v sa[RB];
+#pragma unroll
+    for (int j = 0; j < RB; ++j) sa[j] = f16v{};
+    // operand fragments software-pipelined one slice ahead; the sched
+    // barriers stop the scheduler from hoisting every slice's LDS reads
+    bf16x8 a0 = sk[lane], a1 = sk[64 + lane], a2 = sk[128 + lane];
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      const int sn = s + 1 < NS ? s + 1 : s;
+      const bf16x8 n0 = sk[sn * 192 + lane], n1 = sk[sn * 192 + 64 + lane], n2 = sk[sn * 192 + 128 + lane];
+#pragma unroll
+      for (int j = 0; j < RB; ++j) sa[j] = mfma_split<NT>(a0, a1, a2, hk[j][s][0], hk[j][s][1], hk[j][s][2], sa[j]);
+      a0 = n0;
+      a1 = n1;
+      a2 = n2;
+      __builtin_amdgcn_sched_barrier(0);
+    }
+#pragma unroll
+    for (int j = 0; j < RB; ++j) {
+      // logits (item acc32_row(r, hh) of the chunk, row l32 of block j)
+      float cm = NEG_INF;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const f4 bq = *reinterpret_cast<const f4*>(&sb[8 * q + 4 * hh]);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const float z = sa[j][4 * q + u] + bq[u];
+          if (ARG && z > bv[j]) {  // items increase with r: strict > keeps the first maximum
+            bv[j] = z;
+            bi[j] = 32 * (c0 + c) + 8 * q + 4 * hh + u;
+          }
+          sa[j][4 * q + u] = z * L2E;
+          cm = fmaxf(cm, z);
         }
-        sa[4 * q + u] = z * L2E;
-        cm = fmaxf(cm, z);
       }
-    }
-    cm = fmaxf(cm, __shfl_xor(cm, 32));
-    if (ARG && cmax != nullptr && hh == 0) cmax[(int64_t)(c0 + c) * B + r0 + l32] = cm;
-    cm *= L2E;
-    const float mn = fmaxf(m, cm);
-    if (__any(mn > m)) {
-      const float a = mn > m ? __builtin_amdgcn_exp2f(m - mn) : 1.f;
+      cm = fmaxf(cm, __shfl_xor(cm, 32));
+      if (ARG && cmax != nullptr && hh == 0 && r0 + 32 * j < B) cmax[(int64_t)(c0 + c) * B + r0 + 32 * j + l32] = cm;
+      cm *= L2E;
+      const float mn = fmaxf(m[j], cm);
+      if (__any(mn > m[j])) {
+        const float a = mn > m[j] ? __builtin_amdgcn_exp2f(m[j] - mn) : 1.f;
 #pragma unroll
-      for (int t = 0; t < NTL; ++t) o[t] *= a;
-      l *= a;
-      m = mn;
-    }
-    const float mm = m == NEG_INF ? 0.f : m;
-    float ps = 0.f;
+        for (int t = 0; t < NTL; ++t) o[j][t] *= a;
+        l[j] *= a;
+        m[j] = mn;
+      }
+      const float mm = m[j] == NEG_INF ? 0.f : m[j];
+      float ps = 0.f;
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const float p = __builtin_amdgcn_exp2f(sa[r] - mm);
-      sa[r] = p;
-      ps += p;
-    }
-    l += ps;
+      for (int r = 0; r < 16; ++r) {
+        const float p = __builtin_amdgcn_exp2f(sa[j][r] - mm);
+        sa[j][r] = p;
+        ps += p;
+      }
+      l[j] += ps;
 #pragma unroll
-    for (int s = 0; s < 2; ++s)
-      split3x8(f4{sa[8 * s], sa[8 * s + 1], sa[8 * s + 2], sa[8 * s + 3]},
-               f4{sa[8 * s + 4], sa[8 * s + 5], sa[8 * s + 6], sa[8 * s + 7]}, q0[s], q1[s], q2[s]);
+      for (int s = 0; s < 2; ++s)
+        split3x8(f4{sa[j][8 * s], sa[j][8 * s + 1], sa[j][8 * s + 2], sa[j][8 * s + 3]},
+                 f4{sa[j][8 * s + 4], sa[j][8 * s + 5], sa[j][8 * s + 6], sa[j][8 * s + 7]}, q0[j][s], q1[j][s],
+                 q2[j][s]);
+    }
   };
-  // O-part: Oᵀ += W_cᵀ·Pᵀ
-  auto opart = [&](const bf16x8* sr, const bf16x8 (&q0)[2], const bf16x8 (&q1)[2], const bf16x8 (&q2)[2])
-      __attribute__((always_inline)) {
+  // O-part: Oᵀ += W_cᵀ·Pᵀ for every block
+  auto opart = [&](const bf16x8* sr, const bf16x8 (&q0)[RB][2], const bf16x8 (&q1)[RB][2],
+                   const bf16x8 (&q2)[RB][2]) __attribute__((always_inline)) {
+    bf16x8 a0 = sr[lane], a1 = sr[64 + lane], a2 = sr[128 + lane];
 #pragma unroll
-    for (int t = 0; t < NTL; ++t)
+    for (int ts = 0; ts < 2 * NTL; ++ts) {
+      const int t = ts >> 1, s = ts & 1;
+      const int en = (ts + 1 < 2 * NTL ? ts + 1 : ts) * 192 + lane;
+      const bf16x8 n0 = sr[en], n1 = sr[en + 64], n2 = sr[en + 128];
 #pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        const int e = (t * 2 + s) * 192 + lane;
-        o[t] = mfma_split<NT>(sr[e], sr[e + 64], sr[e + 128], q0[s], q1[s], q2[s], o[t]);
-      }
+      for (int j = 0; j < RB; ++j) o[j][t] = mfma_split<NT>(a0, a1, a2, q0[j][s], q1[j][s], q2[j][s], o[j][t]);
+      a0 = n0;
+      a1 = n1;
+      a2 = n2;
+      __builtin_amdgcn_sched_barrier(0);
+    }
   };
   for (int c = 0; c < nch; c += 2) {
-    bf16x8 q0[2], q1[2], q2[2];
+    bf16x8 q0[RB][2], q1[RB][2], q2[RB][2];
     if (DR) {
       if (c + 1 < nch) {
         FL_ISSUE_K(c0 + c + 1, sk1, sb1);
@@ -290,30 +339,35 @@ __global__ __launch_bounds__(64 * fl_waves(HF)) void k_flash_fwd(
   }
 #undef FL_ISSUE_K
 #undef FL_ISSUE_R
-  if (!active) return;
-  l += __shfl_xor(l, 32);
-  const int row = r0 + l32;
-  if (ARG) {  // merge the lane halves: larger value, ties to the smaller item
-    const float v2 = __shfl_xor(bv, 32);
-    const int i2 = __shfl_xor(bi, 32);
-    if (v2 > bv || (v2 == bv && i2 < bi)) {
-      bv = v2;
-      bi = i2;
-    }
-  }
-  if (hh == 0) {
-    pm[(int64_t)split * B + row] = m;
-    pl[(int64_t)split * B + row] = l;
-    if (ARG) {
-      pbest[(int64_t)split * B + row] = bv;
-      parg[(int64_t)split * B + row] = bi;
-    }
-  }
 #pragma unroll
-  for (int t = 0; t < NTL; ++t)
+  for (int j = 0; j < RB; ++j) {
+    if (r0 + 32 * j >= B) break;
+    const float lt = l[j] + __shfl_xor(l[j], 32);
+    const int row = r0 + 32 * j + l32;
+    float bvj = bv[j];
+    int bij = bi[j];
+    if (ARG) {  // merge the lane halves: larger value, ties to the smaller item
+      const float v2 = __shfl_xor(bvj, 32);
+      const int i2 = __shfl_xor(bij, 32);
+      if (v2 > bvj || (v2 == bvj && i2 < bij)) {
+        bvj = v2;
+        bij = i2;
+      }
+    }
+    if (hh == 0) {
+      pm[(int64_t)split * B + row] = m[j];
+      pl[(int64_t)split * B + row] = lt;
+      if (ARG) {
+        pbest[(int64_t)split * B + row] = bvj;
+        parg[(int64_t)split * B + row] = bij;
+      }
+    }
 #pragma unroll
-    for (int r = 0; r < 16; ++r)
-      pO[((int64_t)split * HF + 32 * t + acc32_row(r, hh)) * B + row] = o[t][r];
+    for (int t = 0; t < NTL; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r)
+        pO[((int64_t)split * HF + 32 * t + acc32_row(r, hh)) * B + row] = o[j][t][r];
+  }
 }
 
 // ------------------------------------------------------------ combine ----
@@ -376,15 +430,16 @@ __global__ __launch_bounds__(256) void k_flash_dh(const float* __restrict__ pm, 
 }
 
 // ------------------------------------------------------------- pass 2 ----
-// Same ring scheme as pass 1 (HF 256: single-buffered R-planes of h).
+// Same ring scheme as pass 1 (HF 256: single-buffered R-planes of h); a wave
+// owns RB blocks of 32 items.
 template <int HF, int NT>
-__global__ __launch_bounds__(64 * fl_waves(HF)) void k_flash_dw(
+__global__ __launch_bounds__(64 * fl_nw(HF, 2)) void k_flash_dw(
     const bf16x8* __restrict__ Hk, const bf16x8* __restrict__ Hr, const bf16x8* __restrict__ Wk,
     const float* __restrict__ bias_pad, const float2* __restrict__ rowinfo, float g, int B, int A,
     float* __restrict__ W, float* __restrict__ mW, float* __restrict__ vW, float* __restrict__ bias,
     float* __restrict__ mb, float* __restrict__ vb, AdamArgs args, float* __restrict__ dW_out,
     float* __restrict__ db_out) {
-  constexpr int NW = fl_waves(HF);
+  constexpr int NW = fl_nw(HF, 2), RB = fl_rb(HF, 2);
   constexpr bool DR = HF <= 128;
   constexpr int NS = HF / 16, NTL = HF / 32;
   constexpr int EK = NS * 192;
@@ -392,75 +447,107 @@ __global__ __launch_bounds__(64 * fl_waves(HF)) void k_flash_dw(
   __shared__ bf16x8 sk0[EK], sk1[EK];
   __shared__ bf16x8 sr0[ER], sr1[DR ? ER : 1];
   __shared__ __attribute__((aligned(16))) float2 si0[32], si1[32];
-  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, hh = lane >> 5, l32 = lane & 31;
-  const int j0 = blockIdx.x * 32 * NW + 32 * w;
+  const int tid = threadIdx.x, lane = tid & 63, hh = lane >> 5, l32 = lane & 31, lane16 = 16 * lane;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int j0 = blockIdx.x * fl_rows(HF, 2) + 32 * RB * w;   // this wave's first item
   const bool active = j0 < A;
-  const int item = j0 + l32;
   const int nch = B / 32;
 #define FL_ISSUE_K(C, SK, SI)                                                  \
   do {                                                                         \
-    stage<EK, NW>(Hk + (int64_t)(C) * EK, SK, w, lane);                        \
-    if (w == 0 && lane < 16) glds16(rowinfo + 32 * (C) + 2 * lane, SI);        \
+    stage<EK, NW>(Hk + (int64_t)(C) * EK, SK, w, lane16);                      \
+    if (w == 0 && lane < 16) blds16(rsrc_of(rowinfo + 32 * (C)), SI, lane16, 0); \
   } while (0)
-#define FL_ISSUE_R(C, SR) stage<ER, NW>(Hr + (int64_t)(C) * ER, SR, w, lane)
+#define FL_ISSUE_R(C, SR) stage<ER, NW>(Hr + (int64_t)(C) * ER, SR, w, lane16)
   FL_ISSUE_K(0, sk0, si0);
   FL_ISSUE_R(0, sr0);
-  // this wave's 32 items of W (B operand of S = h_c·Wᵀ)
-  bf16x8 wk[NS][3];
+  // this wave's RB × 32 items of W (B operands of S = h_c·Wᵀ)
+  bf16x8 wk[RB][NS][3];
+  float bj[RB];
 #pragma unroll
-  for (int s = 0; s < NS; ++s)
-#pragma unroll
-    for (int p = 0; p < 3; ++p)
-      wk[s][p] = active ? Wk[((int64_t)(j0 >> 5) * NS + s) * 192 + p * 64 + lane] : bf16x8{};
-  const float bj = active ? bias_pad[item] : NEG_INF;
-  f16v dw[NTL];
-#pragma unroll
-  for (int t = 0; t < NTL; ++t) dw[t] = f16v{};
-  float dbs = 0.f;
-  __syncthreads();
-  // S = h_c·Wᵀ recomputed, dZ = g·(2^(S−lse) − onehot), db; P planes
-  auto spart = [&](const bf16x8* sk, const float2* si, bf16x8 (&q0)[2], bf16x8 (&q1)[2], bf16x8 (&q2)[2])
-      __attribute__((always_inline)) {
-    f16v sa = {};
+  for (int j = 0; j < RB; ++j) {
+    const bool act = j0 + 32 * j < A;
 #pragma unroll
     for (int s = 0; s < NS; ++s)
-      sa = mfma_split<NT>(sk[s * 192 + lane], sk[s * 192 + 64 + lane], sk[s * 192 + 128 + lane], wk[s][0], wk[s][1],
-                          wk[s][2], sa);
-    // dZ for (row acc32_row(r, hh), item l32); db summed per chunk first
-    float cdb = 0.f;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const f4 i0 = *reinterpret_cast<const f4*>(&si[8 * q + 4 * hh]);
-      const f4 i1 = *reinterpret_cast<const f4*>(&si[8 * q + 4 * hh + 2]);
+      for (int p = 0; p < 3; ++p)
+        wk[j][s][p] = act ? Wk[((int64_t)((j0 >> 5) + j) * NS + s) * 192 + p * 64 + lane] : bf16x8{};
+    bj[j] = act ? bias_pad[j0 + 32 * j + l32] : NEG_INF;
+  }
+  f16v dw[RB][NTL];
+  float dbs[RB];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const float lse2 = u < 2 ? i0[2 * u] : i1[2 * (u - 2)];
-        const int tb = __float_as_int(u < 2 ? i0[2 * u + 1] : i1[2 * (u - 2) + 1]);
-        const float e = __builtin_amdgcn_exp2f(fmaf(sa[4 * q + u] + bj, L2E, -lse2));
-        const float p = g * (e - (tb == item ? 1.f : 0.f));
-        sa[4 * q + u] = p;
-        cdb += p;
-      }
+  for (int j = 0; j < RB; ++j) {
+#pragma unroll
+    for (int t = 0; t < NTL; ++t) dw[j][t] = f16v{};
+    dbs[j] = 0.f;
+  }
+  __syncthreads();
+  // S = h_c·Wᵀ recomputed, dZ = g·(2^(S−lse) − onehot), db; P planes
+  auto spart = [&](const bf16x8* sk, const float2* si, bf16x8 (&q0)[RB][2], bf16x8 (&q1)[RB][2],
+                   bf16x8 (&q2)[RB][2]) __attribute__((always_inline)) {
+    f16v sa[RB];
+#pragma unroll
+    for (int j = 0; j < RB; ++j) sa[j] = f16v{};
+    // operand fragments software-pipelined one slice ahead; the sched
+    // barriers stop the scheduler from hoisting every slice's LDS reads
+    bf16x8 a0 = sk[lane], a1 = sk[64 + lane], a2 = sk[128 + lane];
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      const int sn = s + 1 < NS ? s + 1 : s;
+      const bf16x8 n0 = sk[sn * 192 + lane], n1 = sk[sn * 192 + 64 + lane], n2 = sk[sn * 192 + 128 + lane];
+#pragma unroll
+      for (int j = 0; j < RB; ++j) sa[j] = mfma_split<NT>(a0, a1, a2, wk[j][s][0], wk[j][s][1], wk[j][s][2], sa[j]);
+      a0 = n0;
+      a1 = n1;
+      a2 = n2;
+      __builtin_amdgcn_sched_barrier(0);
     }
-    dbs += cdb;
+    // dZ for (row acc32_row(r, hh), item l32 of block j); db summed per chunk first
 #pragma unroll
-    for (int s = 0; s < 2; ++s)
-      split3x8(f4{sa[8 * s], sa[8 * s + 1], sa[8 * s + 2], sa[8 * s + 3]},
-               f4{sa[8 * s + 4], sa[8 * s + 5], sa[8 * s + 6], sa[8 * s + 7]}, q0[s], q1[s], q2[s]);
-  };
-  // dW += dZᵀ·h_c
-  auto wpart = [&](const bf16x8* sr, const bf16x8 (&q0)[2], const bf16x8 (&q1)[2], const bf16x8 (&q2)[2])
-      __attribute__((always_inline)) {
+    for (int j = 0; j < RB; ++j) {
+      const int item = j0 + 32 * j + l32;
+      float cdb = 0.f;
 #pragma unroll
-    for (int t = 0; t < NTL; ++t)
+      for (int q = 0; q < 4; ++q) {
+        const f4 i0 = *reinterpret_cast<const f4*>(&si[8 * q + 4 * hh]);
+        const f4 i1 = *reinterpret_cast<const f4*>(&si[8 * q + 4 * hh + 2]);
 #pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        const int e = (t * 2 + s) * 192 + lane;
-        dw[t] = mfma_split<NT>(q0[s], q1[s], q2[s], sr[e], sr[e + 64], sr[e + 128], dw[t]);
+        for (int u = 0; u < 4; ++u) {
+          const float lse2 = u < 2 ? i0[2 * u] : i1[2 * (u - 2)];
+          const int tb = __float_as_int(u < 2 ? i0[2 * u + 1] : i1[2 * (u - 2) + 1]);
+          const float e = __builtin_amdgcn_exp2f(fmaf(sa[j][4 * q + u] + bj[j], L2E, -lse2));
+          const float p = g * (e - (tb == item ? 1.f : 0.f));
+          sa[j][4 * q + u] = p;
+          cdb += p;
+        }
       }
+      dbs[j] += cdb;
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+        split3x8(f4{sa[j][8 * s], sa[j][8 * s + 1], sa[j][8 * s + 2], sa[j][8 * s + 3]},
+                 f4{sa[j][8 * s + 4], sa[j][8 * s + 5], sa[j][8 * s + 6], sa[j][8 * s + 7]}, q0[j][s], q1[j][s],
+                 q2[j][s]);
+    }
+  };
+  // dW += dZᵀ·h_c for every block
+  auto wpart = [&](const bf16x8* sr, const bf16x8 (&q0)[RB][2], const bf16x8 (&q1)[RB][2],
+                   const bf16x8 (&q2)[RB][2]) __attribute__((always_inline)) {
+    bf16x8 b0 = sr[lane], b1 = sr[64 + lane], b2 = sr[128 + lane];
+#pragma unroll
+    for (int ts = 0; ts < 2 * NTL; ++ts) {
+      const int t = ts >> 1, s = ts & 1;
+      const int en = (ts + 1 < 2 * NTL ? ts + 1 : ts) * 192 + lane;
+      const bf16x8 n0 = sr[en], n1 = sr[en + 64], n2 = sr[en + 128];
+#pragma unroll
+      for (int j = 0; j < RB; ++j) dw[j][t] = mfma_split<NT>(q0[j][s], q1[j][s], q2[j][s], b0, b1, b2, dw[j][t]);
+      b0 = n0;
+      b1 = n1;
+      b2 = n2;
+      __builtin_amdgcn_sched_barrier(0);
+    }
   };
   for (int c = 0; c < nch; c += 2) {
-    bf16x8 q0[2], q1[2], q2[2];
+    bf16x8 q0[RB][2], q1[RB][2], q2[RB][2];
     if (DR) {
       if (c + 1 < nch) {
         FL_ISSUE_K(c + 1, sk1, si1);
@@ -505,35 +592,40 @@ __global__ __launch_bounds__(64 * fl_waves(HF)) void k_flash_dw(
   }
 #undef FL_ISSUE_K
 #undef FL_ISSUE_R
-  if (!active) return;
-  dbs += __shfl_xor(dbs, 32);
-  if (hh == 0 && item < A) {
-    if (db_out) {
-      db_out[item] = dbs;
-    } else {
-      float p = bias[item], mq = mb[item], v = vb[item];
-      adam_elem(p, mq, v, dbs, args);
-      bias[item] = p;
-      mb[item] = mq;
-      vb[item] = v;
-    }
-  }
 #pragma unroll
-  for (int t = 0; t < NTL; ++t) {
-    const int col = 32 * t + l32;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int j = j0 + acc32_row(r, hh);
-      if (j >= A) continue;
-      const int64_t o = (int64_t)j * HF + col;
-      if (dW_out) {
-        dW_out[o] = dw[t][r];
+  for (int j = 0; j < RB; ++j) {
+    const int jb = j0 + 32 * j;
+    if (jb >= A) break;
+    const int item = jb + l32;
+    const float dbt = dbs[j] + __shfl_xor(dbs[j], 32);
+    if (hh == 0 && item < A) {
+      if (db_out) {
+        db_out[item] = dbt;
       } else {
-        float p = W[o], mq = mW[o], v = vW[o];
-        adam_elem(p, mq, v, dw[t][r], args);
-        W[o] = p;
-        mW[o] = mq;
-        vW[o] = v;
+        float p = bias[item], mq = mb[item], v = vb[item];
+        adam_elem(p, mq, v, dbt, args);
+        bias[item] = p;
+        mb[item] = mq;
+        vb[item] = v;
+      }
+    }
+#pragma unroll
+    for (int t = 0; t < NTL; ++t) {
+      const int col = 32 * t + l32;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int it = jb + acc32_row(r, hh);
+        if (it >= A) continue;
+        const int64_t o = (int64_t)it * HF + col;
+        if (dW_out) {
+          dW_out[o] = dw[j][t][r];
+        } else {
+          float p = W[o], mq = mW[o], v = vW[o];
+          adam_elem(p, mq, v, dw[j][t][r], args);
+          W[o] = p;
+          mW[o] = mq;
+          vW[o] = v;
+        }
       }
     }
   }
@@ -749,7 +841,7 @@ extern "C" int rg_head_planes(const float* X, int rows, int HF, void* planes_k, 
   return RG_OK;
 }
 
-extern "C" int rg_flash_rows_per_block(int HF) { return flash_hf_ok(HF) ? 32 * fl_waves(HF) : RG_ERR_SHAPE; }
+extern "C" int rg_flash_rows_per_block(int HF) { return flash_hf_ok(HF) ? fl_rows(HF, 1) : RG_ERR_SHAPE; }
 
 extern "C" int rg_flash_fwd_top(const void* Hk, const void* Wk, const void* Wr, const float* bias_pad, int B, int A,
                                 int HF, int terms, int nsplit, float* pm, float* pl, float* pO, float* pbest,
@@ -762,11 +854,11 @@ extern "C" int rg_flash_fwd_top(const void* Hk, const void* Wk, const void* Wr, 
   if (arg != (parg != nullptr) || (cmax && !arg)) return RG_ERR_ARG;
   const int nct = (A + 31) / 32;
   const int cps = (nct + nsplit - 1) / nsplit;
-  const int rpb = 32 * fl_waves(HF);
+  const int rpb = fl_rows(HF, 1);
   const int nrb = (B + rpb - 1) / rpb;
   const dim3 grid((unsigned)(nrb * nsplit));
 #define FF(HFV, NTV, ARGV)                                                                                   \
-  hipLaunchKernelGGL((k_flash_fwd<HFV, NTV, ARGV>), grid, dim3(64 * fl_waves(HFV)), 0, stream,                \
+  hipLaunchKernelGGL((k_flash_fwd<HFV, NTV, ARGV>), grid, dim3(64 * fl_nw(HFV, 1)), 0, stream,                \
                      (const bf16x8*)Hk, (const bf16x8*)Wk, (const bf16x8*)Wr, bias_pad, B, A, nrb, nsplit, cps, pm, \
                      pl, pO, pbest, parg, cmax)
 #define FA(HFV, NTV)     \
@@ -864,10 +956,10 @@ extern "C" int rg_flash_dw_adam(const void* Hk, const void* Hr, const void* Wk, 
   if (dW_out ? !db_out : (!adam6 || !W || !mW || !vW || !bias || !mb || !vb)) return RG_ERR_ARG;
   AdamArgs a{};
   if (adam6) a = AdamArgs{adam6[0], adam6[1], adam6[2], adam6[3], adam6[4], adam6[5]};
-  const int rpb = 32 * fl_waves(HF);
+  const int rpb = fl_rows(HF, 2);
   const dim3 grid((unsigned)((A + rpb - 1) / rpb));
 #define FW(HFV, NTV)                                                                                          \
-  hipLaunchKernelGGL((k_flash_dw<HFV, NTV>), grid, dim3(64 * fl_waves(HFV)), 0, stream, (const bf16x8*)Hk, (const bf16x8*)Hr, \
+  hipLaunchKernelGGL((k_flash_dw<HFV, NTV>), grid, dim3(64 * fl_nw(HFV, 2)), 0, stream, (const bf16x8*)Hk, (const bf16x8*)Hr, \
                      (const bf16x8*)Wk, bias_pad, (const float2*)rowinfo, gscale, B, A, W, mW, vW, bias, mb, vb, \
                      a, dW_out, db_out)
 #define FT(HFV)          \

@@ -31,7 +31,7 @@ u8 = lambda n: torch.empty(int(n), dtype=torch.uint8, device=dev)  # noqa: E731
 hb, wb = call("rg_head_plane_bytes", B, H), call("rg_head_plane_bytes", A, H)
 Hk, Hr, Wk, Wr = u8(hb), u8(hb), u8(wb), u8(wb)
 bp = torch.empty((A + 31) // 32 * 32, device=dev)
-nrb = -(-B // 256)
+nrb = -(-B // call("rg_flash_rows_per_block", H))
 ns = -(-min(max(1, 256 // nrb), -(-A // 32)) // 8) * 8
 pm, pl = torch.empty(ns, B, device=dev), torch.empty(ns, B, device=dev)
 pO = torch.empty(ns, H, B, device=dev)
