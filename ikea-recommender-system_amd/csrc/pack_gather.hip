@@ -147,12 +147,18 @@ __global__ __launch_bounds__(256) void k_gather(const int64_t* __restrict__ s, i
   }
 }
 
-// Compile-time-E variant (E ∈ {32, 64, 128, 256}): V4 = E/4 lanes per token
-// row, 256/V4 tokens per pass, and U passes' loads issued before any store so
-// each lane keeps U independent row reads in flight (the table rows are
-// random: latency, not bandwidth, is what a lane waits on).
+// Compile-time-E variant (E ∈ {32, 64, 128, 256}, L <= GW_MAXL): a workgroup
+// takes GW_ROWS consecutive sorted rows, whose tokens are one contiguous
+// packed range [offs[r0], offs[r0 + GW_ROWS]).  Three dependent memory steps
+// per workgroup: the rows' (perm, length, offset), their item ids (into LDS),
+// then every table row of the range — a lane issues all of its (up to U) row
+// loads before any store, so ~GW_ROWS·22 random 512-B rows are in flight per
+// workgroup (the table rows are random: latency, not bandwidth, is what a
+// lane waits on).  V4 = E/4 lanes per token row.
+constexpr int GW_ROWS = 4;
+constexpr int GW_MAXL = 64;
 template <typename TE, int E>
-__global__ __launch_bounds__(256) void k_gather_e(const int64_t* __restrict__ s, int L,
+__global__ __launch_bounds__(256) void k_gather_e(const int64_t* __restrict__ s, int B, int L,
                                                   const int32_t* __restrict__ perm,
                                                   const int32_t* __restrict__ lsort,
                                                   const int32_t* __restrict__ offs,
@@ -160,39 +166,48 @@ __global__ __launch_bounds__(256) void k_gather_e(const int64_t* __restrict__ s,
                                                   int32_t* __restrict__ tok_id, float* __restrict__ X,
                                                   int32_t* __restrict__ err) {
   constexpr int V4 = E / 4;
-  constexpr int TPP = 256 / V4;
-  constexpr int U = TPP >= 16 ? 2 : 4;
-  const int r = blockIdx.x;
-  const int b = perm[r];
-  const int len = lsort[r];
-  const int base = offs[r];
-  const int c = threadIdx.x % V4, t0 = threadIdx.x / V4;
-  const int64_t* srow = s + (int64_t)b * L;
-  for (int tb = t0; tb < len; tb += TPP * U) {
+  constexpr int TPP = 256 / V4;                       // tokens per pass of the workgroup
+  constexpr int U = 64 / TPP;                         // passes whose loads issue together (64 tokens)
+  __shared__ int ids[GW_ROWS * GW_MAXL];
+  __shared__ int rb[GW_ROWS], rl[GW_ROWS], ro[GW_ROWS + 1];
+  const int tid = threadIdx.x;
+  const int r0 = blockIdx.x * GW_ROWS;
+  const int nr = min(GW_ROWS, B - r0);
+  if (tid < nr) {
+    rb[tid] = perm[r0 + tid];
+    rl[tid] = lsort[r0 + tid];
+    ro[tid] = offs[r0 + tid];
+  }
+  if (tid == 0) ro[nr] = offs[r0 + nr];
+  __syncthreads();
+  // item ids of every (row, t), stored at the token's packed position
+  const int tok0 = ro[0], ntok = ro[nr] - tok0;
+  for (int i = tid; i < ntok; i += 256) {
+    int j = 0;
+#pragma unroll
+    for (int q = 1; q < GW_ROWS; ++q) j += (q < nr && i >= ro[q] - tok0);
+    const int t = i - (ro[j] - tok0), len = rl[j];
+    const int64_t id = s[(int64_t)rb[j] * L + (reverse ? len - 1 - t : t)];
+    ids[i] = (id >= 0 && id < n_rows) ? (int32_t)id : -1;   // nn.Embedding raises on such ids
+  }
+  __syncthreads();
+  const int c = tid % V4, t0 = tid / V4;
+  for (int i0 = t0; i0 < ntok; i0 += 64) {
     f4 v[U];
-    int32_t idv[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const int t = tb + TPP * u;
+      const int i = i0 + TPP * u;
       v[u] = f4{0.f, 0.f, 0.f, 0.f};
-      idv[u] = -1;
-      if (t < len) {
-        const int64_t id = srow[reverse ? len - 1 - t : t];
-        if (id >= 0 && id < n_rows) {  // nn.Embedding raises on such ids
-          idv[u] = (int32_t)id;
-          v[u] = load4(emb + id * E, c);
-        }
-      }
+      if (i < ntok && ids[i] >= 0) v[u] = load4(emb + (int64_t)ids[i] * E, c);
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const int t = tb + TPP * u;
-      if (t < len) {
-        const int tok = base + t;
-        reinterpret_cast<f4*>(X + (int64_t)tok * E)[c] = v[u];
+      const int i = i0 + TPP * u;
+      if (i < ntok) {
+        reinterpret_cast<f4*>(X + (int64_t)(tok0 + i) * E)[c] = v[u];
         if (c == 0) {
-          tok_id[tok] = idv[u];
-          if (idv[u] < 0 && err) atomicOr(err, 1);
+          tok_id[tok0 + i] = ids[i];
+          if (ids[i] < 0 && err) atomicOr(err, 1);
         }
       }
     }
@@ -203,9 +218,10 @@ template <typename TE>
 static bool launch_gather_e(const int64_t* s, int B, int L, const int32_t* perm, const int32_t* lsort,
                             const int32_t* offs, const TE* emb, int64_t n_rows, int E, int reverse,
                             int32_t* tok_id, float* X, int32_t* err, hipStream_t stream) {
-#define GE(EV)                                                                                                   \
-  hipLaunchKernelGGL((k_gather_e<TE, EV>), dim3(B), dim3(256), 0, stream, s, L, perm, lsort, offs, emb, n_rows, \
-                     reverse, tok_id, X, err)
+  if (L > GW_MAXL) return false;
+#define GE(EV)                                                                                              \
+  hipLaunchKernelGGL((k_gather_e<TE, EV>), dim3((B + GW_ROWS - 1) / GW_ROWS), dim3(256), 0, stream, s, B, L, \
+                     perm, lsort, offs, emb, n_rows, reverse, tok_id, X, err)
   switch (E) {
     case 32: GE(32); return true;
     case 64: GE(64); return true;
