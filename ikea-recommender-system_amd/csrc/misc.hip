@@ -68,6 +68,30 @@ extern "C" int rg_stack_rewards(const double* r_acc, const float* r_div, const f
   return RG_OK;
 }
 
+// Tokenizer remap of predicted ids (output vocabulary -> input vocabulary,
+// diversity.py:55-60, repetitiveness.py:42-47): out[i] = lut[idx[i]] with
+// lut[j] = input_tokenizer.stoi(output_tokenizer.itos(j)) built once on the
+// host.  An id outside the table or mapped to -1 (no such string, no <unk>:
+// the reference raises there) gives -1 and sets err.
+__global__ void k_remap_ids(const int32_t* __restrict__ idx, int64_t n, const int32_t* __restrict__ lut,
+                            int64_t lut_n, int32_t* __restrict__ out, int32_t* __restrict__ err) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int32_t j = idx[i];
+  const int32_t v = (j >= 0 && j < lut_n) ? lut[j] : -1;
+  out[i] = v;
+  if (v < 0 && err) atomicOr(err, 1);
+}
+
+extern "C" int rg_remap_ids(const int32_t* idx, int64_t n, const int32_t* lut, int64_t lut_n, int32_t* out,
+                            int32_t* err, hipStream_t stream) {
+  if (n <= 0 || lut_n <= 0 || !idx || !lut || !out) return RG_ERR_ARG;
+  hipLaunchKernelGGL(k_remap_ids, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, idx, n, lut, lut_n, out,
+                     err);
+  RG_LAUNCH_CHECK();
+  return RG_OK;
+}
+
 // items per online-softmax partial block of rg_head_fwd (pmax/psum/parg are
 // ceil(A / rg_partial_block()) × B)
 extern "C" int rg_partial_block(void) { return RG_PBLK; }

@@ -262,40 +262,3 @@ extern "C" int rg_gather_h(const int64_t* s, int B, int L, const int32_t* perm, 
   RG_LAUNCH_CHECK();
   return RG_OK;
 }
-
-// ------------------------------------------------------- scatter-add ----
-// dEmb[tok_id[t]] += dX[t] into a dense gradient table that is kept at zero
-// between steps, and tag touched rows with this step's epoch (the row-sparse
-// Adam sweep reads and clears the gradient of tagged rows).  skip_id (>= 0) is the non-trainable padding row (nn.Embedding
-// padding_idx: its gradient is identically zero).
-__global__ __launch_bounds__(256) void k_scatter_add(const int32_t* __restrict__ tok_id,
-                                                     const float* __restrict__ dX, int E,
-                                                     const int32_t* __restrict__ ntok_ptr,
-                                                     int skip_id, float* __restrict__ G,
-                                                     int32_t* __restrict__ tags, int32_t tag) {
-  // one wave per token; consecutive lanes add consecutive floats (256-B
-  // contiguous atomic wave-instructions, the full-rate shape)
-  const int T = *ntok_ptr;
-  const int lane = threadIdx.x & 63;
-  for (int t = blockIdx.x * 4 + (threadIdx.x >> 6); t < T; t += gridDim.x * 4) {
-    const int id = tok_id[t];
-    if (id == skip_id || id < 0) continue;
-    const float* src = dX + (int64_t)t * E;
-    float* dst = G + (int64_t)id * E;
-    for (int c = lane; c < E; c += 64) atomicAdd(dst + c, src[c]);
-    if (lane == 0) tags[id] = tag;
-  }
-}
-
-extern "C" int rg_scatter_add(const int32_t* tok_id, const float* dX, int E, const int32_t* ntok_ptr,
-                              int max_tokens, int skip_id, float* G, int32_t* tags, int32_t tag,
-                              hipStream_t stream) {
-  if (E <= 0) return RG_ERR_ARG;
-  int blocks = (max_tokens + 3) / 4;
-  if (blocks > 8192) blocks = 8192;
-  if (blocks < 1) blocks = 1;
-  hipLaunchKernelGGL(k_scatter_add, dim3(blocks), dim3(256), 0, stream, tok_id, dX, E, ntok_ptr, skip_id,
-                     G, tags, tag);
-  RG_LAUNCH_CHECK();
-  return RG_OK;
-}

@@ -6,6 +6,14 @@ API for callers that hold (B, A) predictions."""
 import torch
 
 
+def map_ids_host(idx, input_tokenizer, output_tokenizer):
+    """input_tokenizer.stoi(output_tokenizer.itos(x)) for every element (the
+    reference's apply_ branch), through one table lookup."""
+    n = len(output_tokenizer)
+    lut = torch.tensor([input_tokenizer.stoi(output_tokenizer.itos(j)) for j in range(n)], dtype=torch.int64)
+    return lut[idx.cpu().long()].to(idx.device)
+
+
 def get_last_action(s, padding_pos, s_len=None, device="cuda"):
     if padding_pos == "end":
         idx = s_len.to(s.device) - 1
@@ -16,10 +24,10 @@ def get_last_action(s, padding_pos, s_len=None, device="cuda"):
 def get_batch_diversity_rewards(s, predictions, len_states, padding_pos, topk_to_consider, embedding_layer,
                                 device="cuda", input_tokenizer=None, output_tokenizer=None):
     """1 - mean_k cos(E[last action], E[top-k prediction]) per row (eps 1e-6)."""
-    if input_tokenizer is not None:
-        raise NotImplementedError("tokenizer remap is not on the device path yet")
     last = get_last_action(s, padding_pos, len_states, device)
     _, idx = torch.topk(predictions, k=topk_to_consider)
+    if input_tokenizer is not None:   # output -> input vocabulary (tabulated, recommenders/hip/remap.py)
+        idx = map_ids_host(idx, input_tokenizer, output_tokenizer)
     e_last = embedding_layer(last.to(idx.device)).unsqueeze(1)
     e_pred = embedding_layer(idx)
     sim = torch.nn.functional.cosine_similarity(e_last, e_pred, dim=2, eps=1e-6)

@@ -66,6 +66,12 @@ def _div_table(diversity_embedding, device):
     return t.detach().to(device, torch.float32).contiguous()
 
 
+def _lut(input_tokenizer, output_tokenizer, device):
+    from recommenders.hip.remap import remap_table, tokenizers
+    return remap_table(input_tokenizer, output_tokenizer, device) if tokenizers(input_tokenizer,
+                                                                                output_tokenizer) else None
+
+
 def _require_hip(model):
     if not isinstance(model, HipNet):
         raise TypeError("evaluate() runs the MI355X device path; pass a recommenders.models.* model")
@@ -93,10 +99,9 @@ def evaluate(evaluation_data_loader, model, device, loss_function, padding_pos, 
     (loss, hr, ndcg, coverage_res, avg_diversity_rew, avg_novelty_rew, repetitions)."""
     _require_hip(model)
     _check_loss_function(loss_function)
-    if input_tokenizer is not None or output_tokenizer is not None:
-        raise NotImplementedError("tokenizer remap is not on the device path yet")
     model.eval()
     dev = model.device
+    lut = _lut(input_tokenizer, output_tokenizer, dev)
     table = _div_table(diversity_embedding, dev)
     bitmap = unpopular_bitmap(unpopular_actions_set, model.action_dim, dev)
     K = max(max(topk_hr_ndcg), topk_to_consider_div, topk_to_consider_nov, max(topk_to_consider_cov))
@@ -113,7 +118,7 @@ def evaluate(evaluation_data_loader, model, device, loss_function, padding_pos, 
         for s, a, s_len in evaluation_data_loader:
             r = eval_batch(model, s, s_len, a, head_idx=head_idx, K=K, ks=topk_hr_ndcg, padding_pos=padding_pos,
                            div_table=table, k_div=topk_to_consider_div, bitmap=bitmap, k_nov=topk_to_consider_nov,
-                           nov_reward=novelty_rew_signal)
+                           nov_reward=novelty_rew_signal, lut=lut)
             idx = r.idx.cpu().numpy()
             loss += float(r.loss.item())
             hr += r.hits.cpu().numpy()
@@ -121,7 +126,7 @@ def evaluate(evaluation_data_loader, model, device, loss_function, padding_pos, 
             tot_div += float(r.div.double().sum().item()) if r.div is not None else 0.0
             tot_nov += float(r.nov.double().sum().item())
             covered = update_coverage_from_indices(idx, covered, topk_to_consider_cov)
-            reps += repetitions_from_indices(s.cpu().numpy(), idx, topk_hr_ndcg)
+            reps += repetitions_from_indices(s.cpu().numpy(), r.idx_in.cpu().numpy(), topk_hr_ndcg)
             n += len(a)
             nb += 1
     coverage_res = get_coverage(covered, set(unpopular_actions_set), model.action_dim, topk_to_consider_cov)
@@ -142,9 +147,10 @@ def update_train_metrics(s, a, s_len, model, device, padding_pos, diversity_embe
         r = eval_batch(model, s, s_len, a, head_idx=head_idx, K=K, ks=topk_hr_ndcg, padding_pos=padding_pos,
                        div_table=_div_table(diversity_embedding, dev), k_div=topk_to_consider_div,
                        bitmap=unpopular_bitmap(unpopular_actions_set, model.action_dim, dev),
-                       k_nov=topk_to_consider_nov, nov_reward=novelty_rew_signal, want_loss=False)
+                       k_nov=topk_to_consider_nov, nov_reward=novelty_rew_signal, want_loss=False,
+                       lut=_lut(input_tokenizer, output_tokenizer, dev))
         idx = r.idx.cpu().numpy()
         covered = update_coverage_from_indices(idx, actions_covered_topk_dict, topk_to_consider_cov)
-        reps = repetitions_from_indices(s.cpu().numpy(), idx, topk_hr_ndcg)
+        reps = repetitions_from_indices(s.cpu().numpy(), r.idx_in.cpu().numpy(), topk_hr_ndcg)
         return (r.hits.cpu().numpy(), r.ndcg.cpu().numpy(), covered, r.div.sum(), float(r.nov.double().sum()),
                 reps)

@@ -16,4 +16,7 @@ def repetitions_from_indices(s, idx, topk):
 
 def get_batch_repetitions(s, preds, topk=[1], input_tokenizer=None, output_tokenizer=None):
     _, idx = torch.topk(preds, k=max(topk))
+    if input_tokenizer is not None:   # predicted ids back to the input vocabulary
+        from recommenders.evaluate.diversity import map_ids_host
+        idx = map_ids_host(idx, input_tokenizer, output_tokenizer)
     return repetitions_from_indices(s.cpu().numpy(), idx.cpu().numpy(), topk)

@@ -23,7 +23,7 @@ I32 = C.c_int32
 U64 = C.c_uint64
 
 # entry points returning int64_t (all others return int)
-RESTYPE_I64 = {"rg_sampled_work_bytes", "rg_head_work_bytes", "rg_head_plane_bytes", "rg_gru_wide_work_bytes"}
+RESTYPE_I64 = {"rg_sampled_work_bytes", "rg_head_work_bytes", "rg_head_plane_bytes", "rg_gru_wide_work_bytes", "rg_scatter_rows_work_bytes"}
 
 # name -> argtypes
 SIGNATURES = {
@@ -31,7 +31,8 @@ SIGNATURES = {
     "rg_partial_block": [],
     "rg_pack": [P, I, I, I, P, P, P, P],
     "rg_gather": [P, I, I, P, P, P, P, I64, I, I, P, P, P, P],
-    "rg_scatter_add": [P, P, I, P, I, I, P, P, I32, P],
+    "rg_scatter_rows_work_bytes": [I, I, I64],
+    "rg_scatter_rows": [P, P, I, P, I, I, P, I64, P, I32, P, I64, P],
     "rg_gemm_f32": [P, I64, I64, P, I64, I64, P, I64, P, I, P, I, I, P, I, P],
     "rg_reduce_slabs": [P, I, I64, P, P, I, I, P],
     "rg_colsum": [P, I, I, P, I, P, P],
@@ -46,6 +47,7 @@ SIGNATURES = {
     "rg_head_planes": [P, I, I, P, P, P, P, P],
     "rg_flash_fwd": [P, P, P, P, I, I, I, I, I, P, P, P, P],
     "rg_flash_rows_per_block": [I],
+    "rg_remap_ids": [P, I64, P, I64, P, P, P],
     "rg_flash_fwd_top": [P, P, P, P, I, I, I, I, I, P, P, P, P, P, P, P],
     "rg_flash_argmax": [P, P, I, I, P, P, P],
     "rg_flash_topk_cap": [],

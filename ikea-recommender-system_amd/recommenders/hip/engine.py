@@ -120,6 +120,26 @@ def _round_up(x, m):
 
 
 # ---------------------------------------------------------------- trunk ----
+class SegScatter:
+    """Deterministic row scatter-add (csrc/segsum.hip rg_scatter_rows: sort by
+    id, ordered per-row sums, no float atomics) with a workspace that grows to
+    the largest row count seen."""
+
+    def __init__(self, device):
+        self.device = device
+        self.work = None
+        self.key = None
+
+    def __call__(self, ids, src, E, n_ptr, n_max, skip, G, n_rows, tags, tag, st):
+        key = (n_max, E, n_rows)
+        if self.key is None or any(a > b for a, b in zip(key, self.key)):
+            self.key = tuple(max(a, b) for a, b in zip(key, self.key or key))
+            nb = call("rg_scatter_rows_work_bytes", *self.key)
+            self.work = torch.empty(int(nb), dtype=torch.uint8, device=self.device)
+        nb = call("rg_scatter_rows_work_bytes", n_max, E, n_rows)
+        call("rg_scatter_rows", ids, src, E, n_ptr, n_max, skip, G, n_rows, tags, tag, self.work.data_ptr(), nb, st)
+
+
 class _TrunkWS:
     """Workspace of one trunk pass for a (B, L) batch shape."""
 
@@ -197,6 +217,7 @@ class Trunk:
         self.G_emb = torch.zeros_like(self.emb.p)
         self.tags = torch.zeros(self.n_local, dtype=torch.int32, device=device)
         self.err = torch.zeros(1, dtype=torch.int32, device=device)  # out-of-range item ids seen
+        self.scatter = SegScatter(device)
         self._ws = {}
         # fp16 embedding storage (config C5): the gather reads this copy, Adam
         # keeps the fp32 master and refreshes it in the same sweep
@@ -312,8 +333,8 @@ class Trunk:
                      w.sl_hh[d].data_ptr(), w.cs_hh[d].data_ptr(), st)
             if self.comm is None:
                 with region("scatter"):
-                    call("rg_scatter_add", w.tok_id[d].data_ptr(), w.dX[d].data_ptr(), E, w.ntok_ptr, TM, skip,
-                         self.G_emb.data_ptr(), self.tags.data_ptr(), tag, st)
+                    self.scatter(w.tok_id[d].data_ptr(), w.dX[d].data_ptr(), E, w.ntok_ptr, TM, skip,
+                                 self.G_emb.data_ptr(), self.n_local, self.tags.data_ptr(), tag, st)
         if self.comm is not None:
             with region("scatter"):
                 self._exchange_grads(w, tag, st)
@@ -411,8 +432,8 @@ class Trunk:
         comm.all_to_all(grecv[:w.R], gsend[:w.T], w.recv_splits, w.send_splits)
         pad = self.pad - self.lo
         skip = -1 if self.train_pad or not (0 <= pad < self.n_local) else pad
-        call("rg_scatter_add", w.local_ids.data_ptr(), grecv.data_ptr(), self.E, w.nrecv.data_ptr(), max(w.R, 1),
-             skip, self.G_emb.data_ptr(), self.tags.data_ptr(), tag, st)
+        self.scatter(w.local_ids.data_ptr(), grecv.data_ptr(), self.E, w.nrecv.data_ptr(), max(w.R, 1), skip,
+                     self.G_emb.data_ptr(), self.n_local, self.tags.data_ptr(), tag, st)
 
 
 # ----------------------------------------------------------------- heads ----
@@ -736,6 +757,7 @@ class SampledSoftmaxHead(SoftmaxHead):
         self.Gb = torch.zeros_like(self.b.p)
         self.tags = torch.zeros(A, dtype=torch.int32, device=device)
         self.tag = 0
+        self.scatter = SegScatter(device)
         self._sws = {}
 
     def split_terms(self, B):
@@ -809,10 +831,10 @@ class SampledSoftmaxHead(SoftmaxHead):
             call("rg_reduce_slabs", w.dw_slabs.data_ptr(), w.dw_splits, S * HF, w.grows.data_ptr(), None, HF, 0,
                  st)
             self.tag += 1
-            call("rg_scatter_add", w.ids.data_ptr(), w.grows.data_ptr(), HF, w.nrows.data_ptr(), S + B, -1,
-                 self.G.data_ptr(), self.tags.data_ptr(), self.tag, st)
-            call("rg_scatter_add", w.ids.data_ptr(), w.gb.data_ptr(), 1, w.nrows.data_ptr(), S + B, -1,
-                 self.Gb.data_ptr(), self.tags.data_ptr(), self.tag, st)
+            self.scatter(w.ids.data_ptr(), w.grows.data_ptr(), HF, w.nrows.data_ptr(), S + B, -1, self.G.data_ptr(),
+                         self.A, self.tags.data_ptr(), self.tag, st)
+            self.scatter(w.ids.data_ptr(), w.gb.data_ptr(), 1, w.nrows.data_ptr(), S + B, -1, self.Gb.data_ptr(),
+                         self.A, self.tags.data_ptr(), self.tag, st)
         with region("sampled_adam"):
             call("rg_adam_rows", self.W.p.data_ptr(), self.W.m.data_ptr(), self.W.v.data_ptr(), self.G.data_ptr(),
                  self.tags.data_ptr(), self.tag, self.A, HF, adam6, st)

@@ -16,7 +16,7 @@ from .engine import _f32
 
 
 class EvalBatch:
-    __slots__ = ("idx", "vals", "loss", "div", "nov", "hits", "ndcg")
+    __slots__ = ("idx", "idx_in", "vals", "loss", "div", "nov", "hits", "ndcg")
 
 
 def head_for(model, head_idx):
@@ -39,8 +39,11 @@ def topk_device(head, ws, B, K):
 
 
 def eval_batch(model, s, s_len, a, *, head_idx=0, K=20, ks=(20,), padding_pos="end", div_table=None, k_div=1,
-               bitmap=None, k_nov=1, nov_reward=1.0, want_loss=True):
-    """Logits, CE loss, top-K and reward sums of one batch, on the device."""
+               bitmap=None, k_nov=1, nov_reward=1.0, want_loss=True, lut=None):
+    """Logits, CE loss, top-K and reward sums of one batch, on the device.
+    ``lut`` (recommenders/hip/remap.py): the top-K ids are mapped to the input
+    vocabulary for the diversity reward and returned as ``idx_in`` (for the
+    host repetition count), as the reference's tokenizer branch does."""
     dev = model.device
     s = s.to(dev)
     a = a.to(dev)
@@ -59,6 +62,10 @@ def eval_batch(model, s, s_len, a, *, head_idx=0, K=20, ks=(20,), padding_pos="e
         out.loss = loss
     idx, vals, err = topk_device(head, ws, B, K)
     out.idx, out.vals = idx, vals
+    out.idx_in = idx
+    if lut is not None:
+        from .remap import remap_ids
+        out.idx_in = remap_ids(idx, lut, err)
     sums = torch.zeros(2 * len(ks), dtype=torch.float64, device=dev)
     ks_host = (ctypes.c_int * len(ks))(*[int(k) for k in ks])
     call("rg_hits_ndcg", idx.data_ptr(), K, a.data_ptr(), B, ks_host, len(ks), sums.data_ptr(), st)
@@ -68,12 +75,17 @@ def eval_batch(model, s, s_len, a, *, head_idx=0, K=20, ks=(20,), padding_pos="e
         lens = torch.as_tensor(s_len).to(dev, torch.int64)
         div = torch.empty(B, device=dev)
         call("rg_diversity", s.data_ptr(), s.shape[1], lens.data_ptr(), 1 if padding_pos == "end" else 0,
-             idx.data_ptr(), k_div, K, div_table.data_ptr(), div_table.shape[1], _f32(1e-6), B, div.data_ptr(), st)
+             out.idx_in.data_ptr(), k_div, K, div_table.data_ptr(), div_table.shape[1], _f32(1e-6), B, div.data_ptr(),
+             st)
         out.div = div
     if bitmap is not None:
         nov = torch.empty(B, device=dev)
         call("rg_novelty", idx.data_ptr(), k_nov, K, bitmap.data_ptr(), _f32(nov_reward), B, nov.data_ptr(), st)
         out.nov = nov
-    if int(err.item()) != 0:
+    e = int(err.item())
+    if e & 2:
         raise RuntimeError("rg_topk candidate overflow (massive exact ties in the logits)")
+    if e & 1:
+        from .remap import RemapError
+        raise RemapError("a predicted id has no input-vocabulary token (input_tokenizer.stoi(output_tokenizer.itos(id)))")
     return out

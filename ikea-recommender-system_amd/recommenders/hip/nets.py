@@ -90,6 +90,38 @@ class HipNet:
             out[hd.W.name] = out[hd.b.name] = (hd.lo, hd.hi)
         return out
 
+    def full_size(self, name):
+        """Rows of the whole item-indexed parameter ``name`` (None if not item-indexed)."""
+        if name == self.trunk.emb.name:
+            return self.trunk.N1
+        for hd in list(self.heads.values()) + list(getattr(self, "q_heads", [])):
+            if name in (hd.W.name, hd.b.name):
+                return hd.A_full
+        return None
+
+    def gather_rows(self, name, local):
+        """The whole tensor of item-indexed parameter ``name`` from every rank's
+        rows (collective on an item-sharded model; ``local`` itself on one GPU)."""
+        if self.comm is None or self.full_size(name) is None:
+            return local
+        from .dist import item_shard
+        comm, n = self.comm, self.full_size(name)
+        rows = max(item_shard(n, comm.world, q)[1] - item_shard(n, comm.world, q)[0] for q in range(comm.world))
+        pad = torch.zeros((rows,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
+        pad[:local.shape[0]] = local
+        allr = torch.empty((comm.world * rows,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
+        comm.all_gather(allr, pad)
+        parts = []
+        for q in range(comm.world):
+            lo, hi = item_shard(n, comm.world, q)
+            parts.append(allr[q * rows:q * rows + hi - lo])
+        return torch.cat(parts)
+
+    def full_state_dict(self):
+        """``state_dict()`` with every item table whole: on an item-sharded
+        (multi-GPU) model an all-gather of the row shards, on every rank."""
+        return OrderedDict((k, self.gather_rows(k, v)) for k, v in self.state_dict().items())
+
     def load_state_dict(self, sd, strict=True):
         """Copies the reference-keyed tensors in; full-size item tables are
         sliced to this rank's rows on an item-sharded model."""

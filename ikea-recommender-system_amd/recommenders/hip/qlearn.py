@@ -20,6 +20,7 @@ import torch
 from . import call, host_floats, host_ptr_array, stream_ptr
 from .engine import SoftmaxHead, _f32
 from .nets import HipNet
+from .remap import remap_ids
 from .timing import region
 
 
@@ -191,8 +192,10 @@ def smorl_rewards(main, smorl, s, a, r_acc, true_next_len, B):
              head.top_err.data_ptr(), st)
     r_div = main.buf("r_div", (B,))
     lens = _dev(true_next_len, dev, torch.int64)   # quirk: diversity uses true_next_len
-    call("rg_diversity", s.data_ptr(), s.shape[1], lens.data_ptr(), 1 if smorl["pad_end"] else 0, idx.data_ptr(),
-         k_div, K, smorl["div_table"].data_ptr(), smorl["div_table"].shape[1], _f32(1e-6), B, r_div.data_ptr(), st)
+    idx_div = idx if smorl.get("lut") is None else remap_ids(idx, smorl["lut"], smorl["remap_err"])
+    call("rg_diversity", s.data_ptr(), s.shape[1], lens.data_ptr(), 1 if smorl["pad_end"] else 0,
+         idx_div.data_ptr(), k_div, K, smorl["div_table"].data_ptr(), smorl["div_table"].shape[1], _f32(1e-6), B,
+         r_div.data_ptr(), st)
     r_nov = main.buf("r_nov", (B,))
     call("rg_novelty", idx.data_ptr(), k_nov, K, smorl["bitmap"].data_ptr(), _f32(smorl["nov_rew_sig"]), B,
          r_nov.data_ptr(), st)

@@ -26,6 +26,7 @@ import torch
 
 from . import call, host_ptr_array, stream_ptr
 from .engine import _f32
+from .remap import remap_ids
 from .timing import region
 
 
@@ -309,9 +310,10 @@ def _smorl_rewards_rows(main, smorl, s, r_acc, true_next_len, idx, B):
     K = idx.shape[1]
     r_div = _buf(main, "r_div", (B,))
     lens = _dev(true_next_len, dev, torch.int64)   # quirk: diversity uses true_next_len
-    call("rg_diversity", s.data_ptr(), s.shape[1], lens.data_ptr(), 1 if smorl["pad_end"] else 0, idx.data_ptr(),
-         smorl["topk_div"], K, smorl["div_table"].data_ptr(), smorl["div_table"].shape[1], _f32(1e-6), B,
-         r_div.data_ptr(), st)
+    idx_div = idx if smorl.get("lut") is None else remap_ids(idx, smorl["lut"], smorl["remap_err"])
+    call("rg_diversity", s.data_ptr(), s.shape[1], lens.data_ptr(), 1 if smorl["pad_end"] else 0,
+         idx_div.data_ptr(), smorl["topk_div"], K, smorl["div_table"].data_ptr(), smorl["div_table"].shape[1],
+         _f32(1e-6), B, r_div.data_ptr(), st)
     r_nov = _buf(main, "r_nov", (B,))
     call("rg_novelty", idx.data_ptr(), smorl["topk_nov"], K, smorl["bitmap"].data_ptr(), _f32(smorl["nov_rew_sig"]),
          B, r_nov.data_ptr(), st)

@@ -32,22 +32,72 @@ class GRU4Rec(SupervisedNet):
 
 
 class _AdamFacade:
-    """Stands where the reference keeps its torch.optim.Adam (``:124-127``)."""
+    """Stands where the reference keeps its torch.optim.Adam (``:124-127``).
+    ``state_dict()`` / ``load_state_dict()`` use torch.optim.Adam's format
+    (parameters indexed in registration order, per-parameter step / exp_avg /
+    exp_avg_sq), so a reference optimizer loads the state of a HIP trainer and
+    vice versa (true resume); item tables are whole (rows
+    all-gathered on an item-sharded model)."""
 
     def __init__(self, clock, nets):
         self.clock = clock
         self.nets = nets
-        self.param_groups = [{"lr": clock.lr, "betas": (clock.b1, clock.b2), "eps": clock.eps}]
+
+    @property
+    def param_groups(self):
+        c = self.clock
+        return [{"lr": c.lr, "betas": (c.b1, c.b2), "eps": c.eps, "weight_decay": 0, "amsgrad": False}]
 
     def zero_grad(self, set_to_none=True):
         pass  # gradients never persist between steps on the HIP path
 
+    def _params(self):
+        return [(net, p) for net in self.nets for p in net.named_param_objs()]
+
     def state_dict(self):
-        st = {}
-        for net in self.nets:
-            for p in net.named_param_objs():
-                st[p.name] = {"step": self.clock.t, "exp_avg": p.m.detach(), "exp_avg_sq": p.v.detach()}
-        return {"state": st, "param_groups": self.param_groups}
+        c = self.clock
+        ps = self._params()
+        # this torch's own Adam defaults, so torch.optim.Adam.load_state_dict accepts the groups
+        group = torch.optim.Adam([torch.zeros(1, requires_grad=True)], lr=c.lr, betas=(c.b1, c.b2),
+                                 eps=c.eps).state_dict()["param_groups"][0]
+        group["params"] = list(range(len(ps)))
+        state = {}
+        if c.t > 0:
+            for i, (net, p) in enumerate(ps):
+                state[i] = {"step": torch.tensor(float(c.t)), "exp_avg": net.gather_rows(p.name, p.m.detach()),
+                            "exp_avg_sq": net.gather_rows(p.name, p.v.detach())}
+        return {"state": state, "param_groups": [group]}
+
+    def load_state_dict(self, sd):
+        ps = self._params()
+        groups = sd["param_groups"]
+        if len(groups) != 1 or len(groups[0]["params"]) != len(ps):
+            raise ValueError("loaded state dict has a different number of parameter groups / parameters")
+        g = groups[0]
+        if g.get("weight_decay", 0) or g.get("amsgrad", False) or g.get("maximize", False):
+            raise NotImplementedError("only plain Adam (no weight decay / amsgrad / maximize) is on the HIP path")
+        c = self.clock
+        c.lr, (c.b1, c.b2), c.eps = float(g["lr"]), tuple(g["betas"]), float(g["eps"])
+        steps = set()
+        with torch.no_grad():
+            for key, (net, p) in zip(g["params"], ps):
+                st = sd["state"].get(key)
+                if st is None:
+                    p.m.zero_()
+                    p.v.zero_()
+                    continue
+                steps.add(int(float(st["step"])))
+                for dst, src in ((p.m, st["exp_avg"]), (p.v, st["exp_avg_sq"])):
+                    t = torch.as_tensor(src)
+                    if tuple(t.shape) != tuple(dst.shape):
+                        lo, hi = net.shard_ranges().get(p.name, (0, t.shape[0]))
+                        t = t[lo:hi]
+                    if tuple(t.shape) != tuple(dst.shape):
+                        raise RuntimeError(f"optimizer state size mismatch for {p.name}")
+                    dst.copy_(t.to(dst.device, torch.float32))
+        if len(steps) > 1:
+            raise NotImplementedError("per-parameter Adam step counts differ; the HIP path keeps one clock")
+        c.t = steps.pop() if steps else 0
 
 
 class GRU4Rec_trainer:

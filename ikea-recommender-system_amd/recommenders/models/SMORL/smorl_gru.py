@@ -20,6 +20,7 @@ from recommenders.hip.engine import AdamClock
 from recommenders.hip.dist import Comm
 from recommenders.hip.qlearn import QNet, double_q_step, unpopular_bitmap
 from recommenders.hip.sharded import sharded_double_q_step
+from recommenders.hip.remap import RemapError, remap_table, tokenizers
 from recommenders.models.GRU4Rec.model import _AdamFacade
 
 
@@ -52,8 +53,6 @@ class SMORL_trainer:
         random.seed(python_rand_seed)
         self.device = require_gpu(device)
         self.comm = Comm(process_group) if shard_items else None   # item-sharded heads (multi-GPU)
-        if input_tokenizer is not None or output_tokenizer is not None:
-            raise NotImplementedError("tokenizer remap (SURVEY §8f rank 4) is not on the device path yet")
         mk = lambda name: SMORL_GRU_Net(hidden_dim=hidden_dim, item_num=item_num, state_size=state_size,
                                         action_dim=action_dim, gru_layers=gru_layers, gamma=gamma,
                                         q_weights=q_weights, embedding_dim=embedding_dim,
@@ -93,6 +92,11 @@ class SMORL_trainer:
             "pad_end": padding_pos == "end",
             "div_table": table.detach().to(self.device, torch.float32).contiguous(),
             "bitmap": unpopular_bitmap(unpopular_actions_set, action_dim, self.device),
+            # tokenizer remap of the predicted ids for the diversity reward
+            # (diversity.py:55-60), tabulated once (recommenders/hip/remap.py)
+            "lut": (remap_table(input_tokenizer, output_tokenizer, self.device)
+                    if tokenizers(input_tokenizer, output_tokenizer) else None),
+            "remap_err": torch.zeros(1, dtype=torch.int32, device=self.device),
         }
         self.clock_1 = AdamClock(learning_rate)
         self.clock_2 = AdamClock(learning_rate)
@@ -112,6 +116,9 @@ class SMORL_trainer:
         out = sup.item(), q.item()
         for net in (self.SMORL_1, self.SMORL_2):
             net.sup_head_output.check_top_err()
+        if self._smorl["lut"] is not None and int(self._smorl["remap_err"].item()):
+            self._smorl["remap_err"].zero_()
+            raise RemapError("a predicted id has no input-vocabulary token")
         return out
 
     @property

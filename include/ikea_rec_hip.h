@@ -45,10 +45,15 @@ int rg_gather(const int64_t* s, int B, int L, const int32_t* perm, const int32_t
 
 /* ---- A3 embedding backward: replaces embedding_dense_backward (autograd of
  * nn.Embedding, incl. padding_idx masking when train_pad_embed=False,
- * GRU4Rec/model.py:36-47).  Atomic scatter-add of dX rows into a kept-zero
- * (N+1, E) table; touched rows tagged with `tag` for rg_adam_rows. */
-int rg_scatter_add(const int32_t* tok_id, const float* dX, int E, const int32_t* ntok_ptr, int max_tokens,
-                   int skip_id, float* G, int32_t* tags, int32_t tag, rg_stream_t stream);
+ * GRU4Rec/model.py:36-47).  Deterministic, atomic-free scatter-add (csrc/segsum.hip): rows
+ * i < *n_ptr (n_max the host bound) with a valid id != skip_id are added into a kept-zero
+ * (n_rows, E) table G — keys sorted (stable radix sort), each row's contributions summed in
+ * row order, so the result does not depend on scheduling — and tagged with `tag` for
+ * rg_adam_rows.  Also the sampled head's row gradients.  work: rg_scatter_rows_work_bytes. */
+int64_t rg_scatter_rows_work_bytes(int n_max, int E, int64_t n_rows);
+int rg_scatter_rows(const int32_t* ids, const float* src, int E, const int32_t* n_ptr, int n_max, int skip_id,
+                    float* G, int64_t n_rows, int32_t* tags, int32_t tag, void* work, int64_t work_bytes,
+                    rg_stream_t stream);
 
 /* ---- A5 dense contractions of the GRU (input projection W_ih x + b_ih, its
  * input gradient, and the weight gradients of nn.GRU's backward).
@@ -248,6 +253,11 @@ int rg_hits_ndcg(const int32_t* idx, int K, const int64_t* tgt, int B, const int
 int rg_mask_scale(const float* x, const float* mask, float scale, int64_t n, float* y, rg_stream_t stream);
 /* W_comb = sum_i w_i W_i (SMORL target weights, tensor_operations.py:50-70) */
 int rg_weighted_sum(const float* const* X, const float* w, int nh, int64_t n, float* out, rg_stream_t stream);
+/* tokenizer remap of predicted ids, output -> input vocabulary (diversity.py:55-60,
+ * repetitiveness.py:42-47): out[i] = lut[idx[i]]; an id outside [0, lut_n) or mapped to -1 gives -1
+ * and err |= 1 (the reference raises on such an id) */
+int rg_remap_ids(const int32_t* idx, int64_t n, const int32_t* lut, int64_t lut_n, int32_t* out, int32_t* err,
+                 rg_stream_t stream);
 /* SMORL reward matrix r (B, 3) f32 = stack([r_acc f64, r_div, r_nov]) (SMORL/smorl_gru.py:311-314, 3 rewards) */
 int rg_stack_rewards(const double* r_acc, const float* r_div, const float* r_nov, int B, float* r, rg_stream_t stream);
 
@@ -329,7 +339,7 @@ int rg_sampled_dz(float* ZT, int64_t ldz, const float* lse, int B, int S, float 
  * rg_place_rows: X[t] = rows_in[slot[t]] widened to fp32; reverse = 1: each row's valid prefix
  *   reversed (the backward direction of BidirGRU4Rec).
  * rg_collect_grads: gsend[slot[t]] = dX0[t] + dX1[rev t] (dX1 optional) — the row-gradients each
- *   owner adds into its rows (rg_scatter_add with local_ids) before rg_adam_rows on its shard. */
+ *   owner adds into its rows (rg_scatter_rows with local_ids) before rg_adam_rows on its shard. */
 int rg_token_ids(const int64_t* s, int B, int L, const int32_t* perm, const int32_t* lsort, const int32_t* offs,
                  int64_t n_rows, int32_t* tok_id, int32_t* err, rg_stream_t stream);
 int rg_shard_route(const int32_t* tok_id, const int32_t* ntok_ptr, int64_t n_rows, int world, int32_t* slot,

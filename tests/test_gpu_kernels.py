@@ -307,3 +307,47 @@ def test_wgrad_fused_bias(M, N, T, splits):
     ref = G[:T].double().t() @ X[:T].double()
     torch.testing.assert_close(dw.sum(0).cpu().double(), ref, rtol=0, atol=2e-6 * T)
     torch.testing.assert_close(db.sum(0).cpu().double(), G[:T].double().sum(0), rtol=0, atol=2e-6 * T)
+
+
+@pytest.mark.parametrize("E,n_rows,n,n_max", [(128, 1000, 20000, 24000), (32, 50, 3000, 3000), (256, 7000, 5000, 6400),
+                                              (1, 300, 777, 1000)])
+def test_scatter_rows_deterministic(E, n_rows, n, n_max):
+    """rg_scatter_rows (csrc/segsum.hip): G[id] += src rows for the first n of
+    n_max rows, skipping skip_id / invalid ids — one heavy id whose run spans
+    many 64-position blocks, runs ending exactly on block edges, -1 and
+    out-of-range ids; equals an fp64 index_add within fp32 rounding, tags the
+    touched rows, and two runs are bitwise identical."""
+    g = torch.Generator().manual_seed(E + n)
+    ids = torch.randint(0, n_rows, (n_max,), generator=g, dtype=torch.int32)
+    ids[: n // 4] = 7                                   # heavy hitter: a long run across blocks
+    ids[n // 4: n // 4 + 64] = 3                        # a run of exactly one block
+    ids[5] = -1
+    ids[6] = n_rows + 5
+    skip = 11 % n_rows
+    ids[n // 2: n // 2 + 10] = skip
+    ids = ids[torch.randperm(n_max, generator=g)]
+    src = torch.randn(n_max, E, generator=g)
+    n_t = torch.tensor([n], dtype=torch.int32, device=dev)
+    nb = C().call("rg_scatter_rows_work_bytes", n_max, E, n_rows)
+    work = torch.empty(nb, dtype=torch.uint8, device=dev)
+    outs = []
+    for rep in range(2):
+        G = torch.zeros(n_rows, E, device=dev)
+        G[0] = 1.0                                      # adds, not overwrites
+        tags = torch.zeros(n_rows, dtype=torch.int32, device=dev)
+        C().call("rg_scatter_rows", D(ids).data_ptr(), D(src).data_ptr(), E, n_t.data_ptr(), n_max, skip,
+                 G.data_ptr(), n_rows, tags.data_ptr(), 9, work.data_ptr(), nb, st())
+        torch.cuda.synchronize()
+        outs.append((G.cpu(), tags.cpu()))
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+    ref = torch.zeros(n_rows, E, dtype=torch.float64)
+    ref[0] = 1.0
+    use = ids[:n].long()
+    ok = (use >= 0) & (use < n_rows) & (use != skip)
+    ref.index_add_(0, use[ok], src[:n][ok].double())
+    G, tags = outs[0]
+    scale = 1 + torch.zeros(n_rows, E, dtype=torch.float64).index_add_(0, use[ok], src[:n][ok].double().abs())
+    assert float(((G.double() - ref).abs() / scale).max()) < 1e-6
+    touched = torch.zeros(n_rows, dtype=torch.bool)
+    touched[use[ok]] = True
+    assert torch.equal(tags == 9, touched)
