@@ -48,6 +48,7 @@ SIGNATURES = {
     "rg_flash_fwd": [P, P, P, P, I, I, I, I, I, P, P, P, P],
     "rg_flash_rows_per_block": [I],
     "rg_remap_ids": [P, I64, P, I64, P, P, P],
+    "rg_build_transitions": [P, P, P, P, P, I, I, I64, I, P, P, P, P, P, P, P, P],
     "rg_flash_fwd_top": [P, P, P, P, I, I, I, I, I, P, P, P, P, P, P, P],
     "rg_flash_argmax": [P, P, I, I, P, P, P],
     "rg_flash_topk_cap": [],

@@ -253,6 +253,16 @@ int rg_hits_ndcg(const int32_t* idx, int K, const int64_t* tgt, int B, const int
 int rg_mask_scale(const float* x, const float* mask, float scale, int64_t n, float* y, rg_stream_t stream);
 /* W_comb = sum_i w_i W_i (SMORL target weights, tensor_operations.py:50-70) */
 int rg_weighted_sum(const float* const* X, const float* w, int nh, int64_t n, float* out, rg_stream_t stream);
+/* replay-buffer transitions from a device session store (csrc/replay.hip; SURVEY §8f rank 2,
+ * rules of preprocessing.py:5-29, 143-170, 426-464): sessions as CSR — items (int32) and rewards
+ * (f64) per event, ev_sess (int32) the event's session, sess_off (int64, n_sess + 1) — and B event
+ * indices ev -> the trainers' batch: s / s_next (B × L int64, pad_id padded at the end when
+ * pad_end else at the beginning), a, r, true_len = clamp(n_bef, 1, L), true_next_len =
+ * min(n_bef + 1, L), is_end (uint8) */
+int rg_build_transitions(const int32_t* items, const double* rew, const int32_t* ev_sess, const int64_t* sess_off,
+                         const int64_t* ev, int B, int L, int64_t pad_id, int pad_end, int64_t* s, int64_t* a,
+                         double* r, int64_t* s_next, int64_t* len, int64_t* next_len, uint8_t* is_end,
+                         rg_stream_t stream);
 /* tokenizer remap of predicted ids, output -> input vocabulary (diversity.py:55-60,
  * repetitiveness.py:42-47): out[i] = lut[idx[i]]; an id outside [0, lut_n) or mapped to -1 gives -1
  * and err |= 1 (the reference raises on such an id) */
