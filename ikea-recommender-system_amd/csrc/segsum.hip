@@ -9,8 +9,12 @@
 //
 // 1. keys: id, or a sentinel above every id for skipped / invalid / padding
 //    rows; values: the row index.
-// 2. stable radix sort of (key, row) — hipCUB over rocPRIM — so equal ids
-//    are consecutive and in row order.
+// 2. stable sort of (key, row) — hipCUB's radix sort over rocPRIM (below 1M
+//    items it runs rocPRIM's block sort + merge passes; forcing the onesweep
+//    radix passes measured slower at these sizes) — so equal ids are
+//    consecutive and in row order.  With reuse_sort the previous call's sorted
+//    order (same ids, same n_max) is used again: the sampled head scatters its
+//    row gradients and its bias gradients over one sort.
 // 3. one wave per 64-position block of the sorted array walks its block in
 //    order, summing each maximal run of one id; a run wholly inside the block
 //    is added to G here, the (at most two) runs crossing a block edge leave
@@ -48,75 +52,78 @@ __global__ void k_seg_keys(const int32_t* __restrict__ ids, const int32_t* __res
   vals[i] = i;
 }
 
-// E / 64 (rounded up) floats per lane; lane c holds columns c, c + 64, ...
-template <int EPL>
+// One wave per 64-position block of the sorted array, lane q = position q:
+// each lane streams its own row in V-float chunks and a segmented inclusive
+// scan across the lanes (fixed shuffle tree, so a fixed summation order) sums
+// every run of equal ids at once; the lane ending a run adds the sum into G
+// (all run ends of the block in parallel).  A run crossing a block edge
+// leaves its block-local sum as a partial (first / last run of the block).
+template <int V>
+struct vec_t;
+template <>
+struct vec_t<1> {
+  using T = float;
+};
+template <>
+struct vec_t<4> {
+  using T = f4;
+};
+
+template <int V>
 __global__ __launch_bounds__(256) void k_seg_blocks(const uint32_t* __restrict__ keys, const int32_t* __restrict__ rows,
                                                     int n_max, const float* __restrict__ src, int E,
                                                     float* __restrict__ G, int32_t* __restrict__ tags, int32_t tag,
                                                     float* __restrict__ part_first, float* __restrict__ part_last) {
+  using T = typename vec_t<V>::T;
   const int lane = threadIdx.x & 63;
   const int blk = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int p0 = blk * SB;
   if (p0 >= n_max) return;
-  const int p1 = min(p0 + SB, n_max);
-  const uint32_t before = p0 > 0 ? keys[p0 - 1] : SENT - 1;   // any value != keys[p0] when p0 == 0
-  const uint32_t after = p1 < n_max ? keys[p1] : SENT;
-  int p = p0;
-  bool first = true;
-  while (p < p1) {
-    const uint32_t k = keys[p];
-    if (k == SENT) break;   // sentinels sort last: the rest of the array is skipped rows
-    int q = p + 1;
-    while (q < p1 && keys[q] == k) ++q;
-    // rows p .. q-1 in order, eight rows' loads in flight at a time
-    float acc[EPL];
+  const int pos = p0 + lane;
+  const uint32_t key = pos < n_max ? keys[pos] : SENT;
+  const int row = pos < n_max ? rows[pos] : 0;
+  const uint32_t before = p0 > 0 ? keys[p0 - 1] : SENT - 1;          // != keys[p0] when p0 == 0
+  const uint32_t after = p0 + SB < n_max ? keys[p0 + SB] : SENT;
+  uint32_t prev = __shfl_up(key, 1);
+  if (lane == 0) prev = before;
+  uint32_t next = __shfl_down(key, 1);
+  if (lane == 63) next = after;
+  const bool valid = key != SENT;
+  const bool start = valid && key != prev;
+  const bool end = valid && (key != next || lane == 63);
+  const int first_end = __builtin_ctzll(__ballot(end) | (1ull << 63));
+  const bool open_left = valid && key == before && lane <= first_end;  // run continued from the previous block
+  const bool open_right = valid && lane == 63 && key == after;          // run continues into the next block
+  const bool closed = end && !open_right && !(open_left && lane == first_end);
+  if (__ballot(valid) == 0) return;   // a block of skipped rows only
+  const T* r = reinterpret_cast<const T*>(src + (int64_t)row * E);
+  T* g = reinterpret_cast<T*>(G + (int64_t)key * E);
+  const int nv = E / V;
+  for (int c = 0; c < nv; ++c) {
+    T x = valid ? r[c] : T{};
+    bool hd = start || lane == 0;
 #pragma unroll
-    for (int e = 0; e < EPL; ++e) acc[e] = 0.f;
-    for (int r = p; r < q; r += 8) {
-      float v[8][EPL];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const bool ok = r + u < q;
-        const float* s = src + (int64_t)(ok ? rows[r + u] : 0) * E;
-#pragma unroll
-        for (int e = 0; e < EPL; ++e) {
-          const int c = lane + 64 * e;
-          v[u][e] = (ok && c < E) ? s[c] : 0.f;
-        }
+    for (int d = 1; d < 64; d <<= 1) {
+      T y;
+      if constexpr (V == 4) {
+        y = f4{__shfl_up(x[0], d), __shfl_up(x[1], d), __shfl_up(x[2], d), __shfl_up(x[3], d)};
+      } else {
+        y = __shfl_up(x, d);
       }
-#pragma unroll
-      for (int u = 0; u < 8; ++u)
-#pragma unroll
-        for (int e = 0; e < EPL; ++e)
-          if (r + u < q) acc[e] += v[u][e];
+      const bool hy = __shfl_up((int)hd, d);
+      if (lane >= d && !hd) x += y;
+      if (lane >= d) hd = hd || hy;
     }
-    const bool open_left = first && k == before;   // run continues from the previous block
-    const bool open_right = q == p1 && k == after;  // run continues into the next block
-    if (!open_left && !open_right) {
-      float* g = G + (int64_t)k * E;
-#pragma unroll
-      for (int e = 0; e < EPL; ++e) {
-        const int c = lane + 64 * e;
-        if (c < E) g[c] += acc[e];
-      }
-      if (lane == 0) tags[k] = tag;
-    } else {
-      // open_left: this is the block's first run; open_right: its last run
-      // (both for a run covering the whole block)
-#pragma unroll
-      for (int e = 0; e < EPL; ++e) {
-        const int c = lane + 64 * e;
-        if (c < E) {
-          if (open_left) part_first[(int64_t)blk * E + c] = acc[e];
-          if (open_right) part_last[(int64_t)blk * E + c] = acc[e];
-        }
-      }
-    }
-    first = false;
-    p = q;
+    if (closed) g[c] += x;
+    if (end && open_left && lane == first_end) reinterpret_cast<T*>(part_first + (int64_t)blk * E)[c] = x;
+    if (open_right) reinterpret_cast<T*>(part_last + (int64_t)blk * E)[c] = x;
   }
+  if (closed) tags[key] = tag;
 }
 
+// A run crossing block edges: the block where it starts adds its last-run
+// partial and the first-run partials of the following blocks that continue
+// it (their first keys equal the run's id), in block order.
 template <int EPL>
 __global__ __launch_bounds__(256) void k_seg_cross(const uint32_t* __restrict__ keys, int n_max, int E,
                                                    float* __restrict__ G, int32_t* __restrict__ tags, int32_t tag,
@@ -132,24 +139,38 @@ __global__ __launch_bounds__(256) void k_seg_cross(const uint32_t* __restrict__ 
   if (p0 > 0 && keys[p0] == k && keys[p0 - 1] == k) return;
   float acc[EPL];
 #pragma unroll
-  for (int e = 0; e < EPL; ++e) {
-    const int c = lane + 64 * e;
-    acc[e] = c < E ? part_last[(int64_t)blk * E + c] : 0.f;
+  for (int x = 0; x < EPL; ++x) {
+    const int c = lane + 64 * x;
+    acc[x] = c < E ? part_last[(int64_t)blk * E + c] : 0.f;
   }
-  for (int b = blk + 1; b * SB < n_max && keys[b * SB] == k; ++b) {
+  const int nb = (n_max + SB - 1) / SB;
+  for (int b0 = blk + 1; b0 < nb; b0 += 64) {
+    // blocks b0 .. b0+63 that continue the run form a prefix (the keys are sorted)
+    const int b = b0 + lane;
+    const uint64_t cont = __ballot(b < nb && keys[(int64_t)b * SB] == k);
+    const int cnt = (~cont) ? __builtin_ctzll(~cont) : 64;
+    for (int i = 0; i < cnt; i += 8) {
+      float v[8][EPL];
 #pragma unroll
-    for (int e = 0; e < EPL; ++e) {
-      const int c = lane + 64 * e;
-      if (c < E) acc[e] += part_first[(int64_t)b * E + c];
+      for (int u = 0; u < 8; ++u)
+#pragma unroll
+        for (int x = 0; x < EPL; ++x) {
+          const int c = lane + 64 * x;
+          v[u][x] = (i + u < cnt && c < E) ? part_first[(int64_t)(b0 + i + u) * E + c] : 0.f;
+        }
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+#pragma unroll
+        for (int x = 0; x < EPL; ++x)
+          if (i + u < cnt) acc[x] += v[u][x];
     }
-    const int q1 = min((b + 1) * SB, n_max);
-    if (keys[q1 - 1] != k || (q1 < n_max && keys[q1] != k) || q1 == n_max) break;
+    if (cnt < 64) break;
   }
   float* g = G + (int64_t)k * E;
 #pragma unroll
-  for (int e = 0; e < EPL; ++e) {
-    const int c = lane + 64 * e;
-    if (c < E) g[c] += acc[e];
+  for (int x = 0; x < EPL; ++x) {
+    const int c = lane + 64 * x;
+    if (c < E) g[c] += acc[x];
   }
   if (lane == 0) tags[k] = tag;
 }
@@ -158,7 +179,30 @@ struct SegLayout {
   size_t keys_in, keys_out, vals_in, vals_out, part_first, part_last, sort_tmp, total, sort_bytes;
 };
 
+// layouts are cached per (n_max, E, key bits): the hipCUB size query costs
+// host time every call
+struct SegKey {
+  int n_max, E, bits;
+};
+constexpr int SEG_CACHE = 16;
+thread_local SegKey seg_keys_[SEG_CACHE];
+thread_local SegLayout seg_vals_[SEG_CACHE];
+thread_local int seg_n_ = 0;
+
+SegLayout seg_layout_uncached(int n_max, int E, int64_t n_rows);
+
 SegLayout seg_layout(int n_max, int E, int64_t n_rows) {
+  const int bits = key_bits(n_rows);
+  for (int i = 0; i < seg_n_; ++i)
+    if (seg_keys_[i].n_max == n_max && seg_keys_[i].E == E && seg_keys_[i].bits == bits) return seg_vals_[i];
+  const SegLayout L = seg_layout_uncached(n_max, E, n_rows);
+  const int slot = seg_n_ < SEG_CACHE ? seg_n_++ : (n_max + E) % SEG_CACHE;
+  seg_keys_[slot] = SegKey{n_max, E, bits};
+  seg_vals_[slot] = L;
+  return L;
+}
+
+SegLayout seg_layout_uncached(int n_max, int E, int64_t n_rows) {
   SegLayout L{};
   const size_t nb = (size_t)(n_max + SB - 1) / SB;
   auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
@@ -186,8 +230,8 @@ extern "C" int64_t rg_scatter_rows_work_bytes(int n_max, int E, int64_t n_rows) 
 }
 
 extern "C" int rg_scatter_rows(const int32_t* ids, const float* src, int E, const int32_t* n_ptr, int n_max,
-                               int skip_id, float* G, int64_t n_rows, int32_t* tags, int32_t tag, void* work,
-                               int64_t work_bytes, hipStream_t stream) {
+                               int skip_id, float* G, int64_t n_rows, int32_t* tags, int32_t tag, int reuse_sort,
+                               void* work, int64_t work_bytes, hipStream_t stream) {
   if (n_max <= 0 || E <= 0 || E > 512 || n_rows <= 0 || !ids || !src || !n_ptr || !G || !tags || !work)
     return RG_ERR_ARG;
   const SegLayout L = seg_layout(n_max, E, n_rows);
@@ -199,17 +243,21 @@ extern "C" int rg_scatter_rows(const int32_t* ids, const float* src, int E, cons
   int32_t* vout = (int32_t*)(w + L.vals_out);
   float* pf = (float*)(w + L.part_first);
   float* pl = (float*)(w + L.part_last);
-  hipLaunchKernelGGL(k_seg_keys, dim3((n_max + 255) / 256), dim3(256), 0, stream, ids, n_ptr, n_max, n_rows, skip_id,
-                     kin, vin);
   size_t tmp = L.sort_bytes;
-  if (hipcub::DeviceRadixSort::SortPairs(w + L.sort_tmp, tmp, kin, kout, vin, vout, n_max, 0, key_bits(n_rows),
-                                         stream) != hipSuccess)
-    return RG_ERR_LAUNCH;
+  if (!reuse_sort) {
+    hipLaunchKernelGGL(k_seg_keys, dim3((n_max + 255) / 256), dim3(256), 0, stream, ids, n_ptr, n_max, n_rows,
+                       skip_id, kin, vin);
+    if (hipcub::DeviceRadixSort::SortPairs(w + L.sort_tmp, tmp, kin, kout, vin, vout, n_max, 0, key_bits(n_rows),
+                                           stream) != hipSuccess)
+      return RG_ERR_LAUNCH;
+  }
   const int nb = (n_max + SB - 1) / SB;
   const dim3 grid((unsigned)((nb + 3) / 4));
-#define SEG(EPLV)                                                                                              \
-  hipLaunchKernelGGL(k_seg_blocks<EPLV>, grid, dim3(256), 0, stream, kout, vout, n_max, src, E, G, tags, tag,  \
-                     pf, pl);                                                                                  \
+  if (E % 4 == 0)
+    hipLaunchKernelGGL(k_seg_blocks<4>, grid, dim3(256), 0, stream, kout, vout, n_max, src, E, G, tags, tag, pf, pl);
+  else
+    hipLaunchKernelGGL(k_seg_blocks<1>, grid, dim3(256), 0, stream, kout, vout, n_max, src, E, G, tags, tag, pf, pl);
+#define SEG(EPLV) \
   hipLaunchKernelGGL(k_seg_cross<EPLV>, grid, dim3(256), 0, stream, kout, n_max, E, G, tags, tag, pf, pl)
   if (E <= 64) {
     SEG(1);

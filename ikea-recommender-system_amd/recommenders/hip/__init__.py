@@ -32,7 +32,7 @@ SIGNATURES = {
     "rg_pack": [P, I, I, I, P, P, P, P],
     "rg_gather": [P, I, I, P, P, P, P, I64, I, I, P, P, P, P],
     "rg_scatter_rows_work_bytes": [I, I, I64],
-    "rg_scatter_rows": [P, P, I, P, I, I, P, I64, P, I32, P, I64, P],
+    "rg_scatter_rows": [P, P, I, P, I, I, P, I64, P, I32, I, P, I64, P],
     "rg_gemm_f32": [P, I64, I64, P, I64, I64, P, I64, P, I, P, I, I, P, I, P],
     "rg_reduce_slabs": [P, I, I64, P, P, I, I, P],
     "rg_colsum": [P, I, I, P, I, P, P],

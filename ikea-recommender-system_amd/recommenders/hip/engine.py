@@ -128,16 +128,16 @@ class SegScatter:
     def __init__(self, device):
         self.device = device
         self.work = None
-        self.key = None
+        self.sizes = {}
 
-    def __call__(self, ids, src, E, n_ptr, n_max, skip, G, n_rows, tags, tag, st):
-        key = (n_max, E, n_rows)
-        if self.key is None or any(a > b for a, b in zip(key, self.key)):
-            self.key = tuple(max(a, b) for a, b in zip(key, self.key or key))
-            nb = call("rg_scatter_rows_work_bytes", *self.key)
-            self.work = torch.empty(int(nb), dtype=torch.uint8, device=self.device)
-        nb = call("rg_scatter_rows_work_bytes", n_max, E, n_rows)
-        call("rg_scatter_rows", ids, src, E, n_ptr, n_max, skip, G, n_rows, tags, tag, self.work.data_ptr(), nb, st)
+    def __call__(self, ids, src, E, n_ptr, n_max, skip, G, n_rows, tags, tag, st, reuse_sort=False):
+        need = self.sizes.get((n_max, E, n_rows))
+        if need is None:
+            need = self.sizes[(n_max, E, n_rows)] = int(call("rg_scatter_rows_work_bytes", n_max, E, n_rows))
+        if self.work is None or self.work.numel() < need:
+            self.work = torch.empty(need, dtype=torch.uint8, device=self.device)
+        call("rg_scatter_rows", ids, src, E, n_ptr, n_max, skip, G, n_rows, tags, tag, 1 if reuse_sort else 0,
+             self.work.data_ptr(), self.work.numel(), st)
 
 
 class _TrunkWS:
@@ -250,6 +250,9 @@ class Trunk:
         w = self.ws(slot, B, L, save)
         st = stream_ptr()
         w.lens.copy_(lens, non_blocking=True)
+        # host bound of the packed token count (the scatter sorts this many keys)
+        lt = torch.as_tensor(lens)
+        w.T_host = int(lt.clamp(1, L).sum()) if self.packed and lt.device.type == "cpu" else B * L
         with region("pack"):
             call("rg_pack", w.lens.data_ptr(), B, L, 0 if self.packed else 1, w.perm.data_ptr(),
                  w.lsort.data_ptr(), w.offs.data_ptr(), st)
@@ -333,7 +336,7 @@ class Trunk:
                      w.sl_hh[d].data_ptr(), w.cs_hh[d].data_ptr(), st)
             if self.comm is None:
                 with region("scatter"):
-                    self.scatter(w.tok_id[d].data_ptr(), w.dX[d].data_ptr(), E, w.ntok_ptr, TM, skip,
+                    self.scatter(w.tok_id[d].data_ptr(), w.dX[d].data_ptr(), E, w.ntok_ptr, w.T_host, skip,
                                  self.G_emb.data_ptr(), self.n_local, self.tags.data_ptr(), tag, st)
         if self.comm is not None:
             with region("scatter"):
@@ -834,7 +837,7 @@ class SampledSoftmaxHead(SoftmaxHead):
             self.scatter(w.ids.data_ptr(), w.grows.data_ptr(), HF, w.nrows.data_ptr(), S + B, -1, self.G.data_ptr(),
                          self.A, self.tags.data_ptr(), self.tag, st)
             self.scatter(w.ids.data_ptr(), w.gb.data_ptr(), 1, w.nrows.data_ptr(), S + B, -1, self.Gb.data_ptr(),
-                         self.A, self.tags.data_ptr(), self.tag, st)
+                         self.A, self.tags.data_ptr(), self.tag, st, reuse_sort=True)
         with region("sampled_adam"):
             call("rg_adam_rows", self.W.p.data_ptr(), self.W.m.data_ptr(), self.W.v.data_ptr(), self.G.data_ptr(),
                  self.tags.data_ptr(), self.tag, self.A, HF, adam6, st)

@@ -49,11 +49,13 @@ int rg_gather(const int64_t* s, int B, int L, const int32_t* perm, const int32_t
  * i < *n_ptr (n_max the host bound) with a valid id != skip_id are added into a kept-zero
  * (n_rows, E) table G — keys sorted (stable radix sort), each row's contributions summed in
  * row order, so the result does not depend on scheduling — and tagged with `tag` for
- * rg_adam_rows.  Also the sampled head's row gradients.  work: rg_scatter_rows_work_bytes. */
+ * rg_adam_rows.  Also the sampled head's row gradients.  work: rg_scatter_rows_work_bytes;
+ * reuse_sort = 1 reuses the sorted order of the previous call on the same work buffer (same ids,
+ * n_ptr, n_max, skip_id, n_rows): a second source over the same rows (the sampled head's bias). */
 int64_t rg_scatter_rows_work_bytes(int n_max, int E, int64_t n_rows);
 int rg_scatter_rows(const int32_t* ids, const float* src, int E, const int32_t* n_ptr, int n_max, int skip_id,
-                    float* G, int64_t n_rows, int32_t* tags, int32_t tag, void* work, int64_t work_bytes,
-                    rg_stream_t stream);
+                    float* G, int64_t n_rows, int32_t* tags, int32_t tag, int reuse_sort, void* work,
+                    int64_t work_bytes, rg_stream_t stream);
 
 /* ---- A5 dense contractions of the GRU (input projection W_ih x + b_ih, its
  * input gradient, and the weight gradients of nn.GRU's backward).

@@ -336,16 +336,22 @@ def test_scatter_rows_deterministic(E, n_rows, n, n_max):
         G[0] = 1.0                                      # adds, not overwrites
         tags = torch.zeros(n_rows, dtype=torch.int32, device=dev)
         C().call("rg_scatter_rows", D(ids).data_ptr(), D(src).data_ptr(), E, n_t.data_ptr(), n_max, skip,
-                 G.data_ptr(), n_rows, tags.data_ptr(), 9, work.data_ptr(), nb, st())
+                 G.data_ptr(), n_rows, tags.data_ptr(), 9, 0, work.data_ptr(), nb, st())
+        # a second source over the same rows reuses the sort (the sampled head's bias)
+        G1 = torch.zeros(n_rows, 1, device=dev)
+        C().call("rg_scatter_rows", D(ids).data_ptr(), D(src[:, :1].contiguous()).data_ptr(), 1, n_t.data_ptr(),
+                 n_max, skip, G1.data_ptr(), n_rows, tags.data_ptr(), 9, 1, work.data_ptr(), nb, st())
         torch.cuda.synchronize()
-        outs.append((G.cpu(), tags.cpu()))
-    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+        outs.append((G.cpu(), tags.cpu(), G1.cpu()))
+    assert all(torch.equal(x, y) for x, y in zip(outs[0], outs[1]))
     ref = torch.zeros(n_rows, E, dtype=torch.float64)
     ref[0] = 1.0
     use = ids[:n].long()
     ok = (use >= 0) & (use < n_rows) & (use != skip)
     ref.index_add_(0, use[ok], src[:n][ok].double())
-    G, tags = outs[0]
+    G, tags, G1 = outs[0]
+    ref1 = torch.zeros(n_rows, 1, dtype=torch.float64).index_add_(0, use[ok], src[:n][ok][:, :1].double())
+    assert float((G1.double() - ref1).abs().max()) < 1e-4
     scale = 1 + torch.zeros(n_rows, E, dtype=torch.float64).index_add_(0, use[ok], src[:n][ok].double().abs())
     assert float(((G.double() - ref).abs() / scale).max()) < 1e-6
     touched = torch.zeros(n_rows, dtype=torch.bool)
