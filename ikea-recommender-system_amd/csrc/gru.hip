@@ -22,12 +22,32 @@
 // ghn = W_hn h + b_hn.
 #include "common.h"
 
+// Per-direction operands: BidirGRU4Rec runs both directions in one launch
+// (blockIdx.y = direction), sharing the packing (perm / lsort / offs).
+struct GruDirs {
+  const float* Gi[2];
+  const float* Whh[2];
+  const float* bhh[2];
+  float* saved[2];
+};
+struct GruBwdDirs {
+  const float* saved[2];
+  const float* Whh[2];
+  float* dGi[2];
+  float* dGh[2];
+};
+
 template <int H>
-__global__ __launch_bounds__(H * 4) void k_gru_fwd(const float* __restrict__ Gi, const float* __restrict__ Whh,
-                                                   const float* __restrict__ bhh, const int32_t* __restrict__ perm,
+__global__ __launch_bounds__(H * 4) void k_gru_fwd(GruDirs dirs, const int32_t* __restrict__ perm,
                                                    const int32_t* __restrict__ lsort,
                                                    const int32_t* __restrict__ offs, int B, float* __restrict__ hout,
-                                                   int ldh, int hoff, float* __restrict__ saved, int64_t plane) {
+                                                   int ldh, int hoff0, int64_t plane) {
+  const int dir = blockIdx.y;
+  const float* __restrict__ Gi = dirs.Gi[dir];
+  const float* __restrict__ Whh = dirs.Whh[dir];
+  const float* __restrict__ bhh = dirs.bhh[dir];
+  float* __restrict__ saved = dirs.saved[dir];
+  const int hoff = hoff0 + dir * H;
   constexpr int KQ = H / 4;  // reduction quarter owned by lane>>4
   constexpr int LDH = H + 4;
   __shared__ __attribute__((aligned(16))) float hbuf[2][16][LDH];
@@ -121,12 +141,16 @@ __global__ __launch_bounds__(H * 4) void k_gru_fwd(const float* __restrict__ Gi,
 // over all 3H gate rows, so W_hhᵀ for those units is held in VGPRs
 // (3H/4 registers per lane) and the 16 × 3H dGh tile is shared through LDS.
 template <int H>
-__global__ __launch_bounds__(H * 4) void k_gru_bwd(const float* __restrict__ saved, int64_t plane,
-                                                   const float* __restrict__ Whh, const int32_t* __restrict__ perm,
+__global__ __launch_bounds__(H * 4) void k_gru_bwd(GruBwdDirs dirs, int64_t plane, const int32_t* __restrict__ perm,
                                                    const int32_t* __restrict__ lsort,
                                                    const int32_t* __restrict__ offs, int B,
-                                                   const float* __restrict__ dhout, int lddh, int dhoff,
-                                                   float* __restrict__ dGi, float* __restrict__ dGh) {
+                                                   const float* __restrict__ dhout, int lddh, int dhoff0) {
+  const int dir = blockIdx.y;
+  const float* __restrict__ saved = dirs.saved[dir];
+  const float* __restrict__ Whh = dirs.Whh[dir];
+  float* __restrict__ dGi = dirs.dGi[dir];
+  float* __restrict__ dGh = dirs.dGh[dir];
+  const int dhoff = dhoff0 + dir * H;
   constexpr int G = 3 * H;
   constexpr int KQ = G / 4;
   constexpr int LDG = G + 4;
@@ -203,21 +227,44 @@ __global__ __launch_bounds__(H * 4) void k_gru_bwd(const float* __restrict__ sav
 }
 
 template <int H>
-static int launch_fwd(const float* Gi, const float* Whh, const float* bhh, const int32_t* perm,
-                      const int32_t* lsort, const int32_t* offs, int B, float* hout, int ldh, int hoff,
-                      float* saved, int64_t plane, hipStream_t stream) {
-  hipLaunchKernelGGL(k_gru_fwd<H>, dim3((B + 15) / 16), dim3(H * 4), 0, stream, Gi, Whh, bhh, perm, lsort, offs,
-                     B, hout, ldh, hoff, saved, plane);
+static void launch_fwd(const GruDirs& d, int ndir, const int32_t* perm, const int32_t* lsort, const int32_t* offs,
+                       int B, float* hout, int ldh, int hoff, int64_t plane, hipStream_t stream) {
+  hipLaunchKernelGGL(k_gru_fwd<H>, dim3((B + 15) / 16, ndir), dim3(H * 4), 0, stream, d, perm, lsort, offs, B, hout,
+                     ldh, hoff, plane);
+}
+
+template <int H>
+static void launch_bwd(const GruBwdDirs& d, int ndir, int64_t plane, const int32_t* perm, const int32_t* lsort,
+                       const int32_t* offs, int B, const float* dhout, int lddh, int dhoff, hipStream_t stream) {
+  hipLaunchKernelGGL(k_gru_bwd<H>, dim3((B + 15) / 16, ndir), dim3(H * 4), 0, stream, d, plane, perm, lsort, offs,
+                     B, dhout, lddh, dhoff);
+}
+
+static int gru_fwd_dirs(const GruDirs& d, int ndir, const int32_t* perm, const int32_t* lsort, const int32_t* offs,
+                        int B, int H, float* hout, int ldh, int hoff, int64_t plane, hipStream_t stream) {
+  if (B <= 0 || ndir < 1 || ndir > 2) return RG_ERR_ARG;
+  switch (H) {
+    case 16: launch_fwd<16>(d, ndir, perm, lsort, offs, B, hout, ldh, hoff, plane, stream); break;
+    case 32: launch_fwd<32>(d, ndir, perm, lsort, offs, B, hout, ldh, hoff, plane, stream); break;
+    case 64: launch_fwd<64>(d, ndir, perm, lsort, offs, B, hout, ldh, hoff, plane, stream); break;
+    case 128: launch_fwd<128>(d, ndir, perm, lsort, offs, B, hout, ldh, hoff, plane, stream); break;
+    default: return RG_ERR_SHAPE;
+  }
   RG_LAUNCH_CHECK();
   return RG_OK;
 }
 
-template <int H>
-static int launch_bwd(const float* saved, int64_t plane, const float* Whh, const int32_t* perm,
-                      const int32_t* lsort, const int32_t* offs, int B, const float* dhout, int lddh, int dhoff,
-                      float* dGi, float* dGh, hipStream_t stream) {
-  hipLaunchKernelGGL(k_gru_bwd<H>, dim3((B + 15) / 16), dim3(H * 4), 0, stream, saved, plane, Whh, perm, lsort,
-                     offs, B, dhout, lddh, dhoff, dGi, dGh);
+static int gru_bwd_dirs(const GruBwdDirs& d, int ndir, int64_t plane, const int32_t* perm, const int32_t* lsort,
+                        const int32_t* offs, int B, int H, const float* dhout, int lddh, int dhoff,
+                        hipStream_t stream) {
+  if (B <= 0 || ndir < 1 || ndir > 2) return RG_ERR_ARG;
+  switch (H) {
+    case 16: launch_bwd<16>(d, ndir, plane, perm, lsort, offs, B, dhout, lddh, dhoff, stream); break;
+    case 32: launch_bwd<32>(d, ndir, plane, perm, lsort, offs, B, dhout, lddh, dhoff, stream); break;
+    case 64: launch_bwd<64>(d, ndir, plane, perm, lsort, offs, B, dhout, lddh, dhoff, stream); break;
+    case 128: launch_bwd<128>(d, ndir, plane, perm, lsort, offs, B, dhout, lddh, dhoff, stream); break;
+    default: return RG_ERR_SHAPE;
+  }
   RG_LAUNCH_CHECK();
   return RG_OK;
 }
@@ -225,28 +272,49 @@ static int launch_bwd(const float* saved, int64_t plane, const float* Whh, const
 extern "C" int rg_gru_fwd(const float* Gi, const float* Whh, const float* bhh, const int32_t* perm,
                           const int32_t* lsort, const int32_t* offs, int B, int H, float* hout, int ldh, int hoff,
                           float* saved, int64_t plane, hipStream_t stream) {
-  if (B <= 0) return RG_ERR_ARG;
-  switch (H) {
-    case 16: return launch_fwd<16>(Gi, Whh, bhh, perm, lsort, offs, B, hout, ldh, hoff, saved, plane, stream);
-    case 32: return launch_fwd<32>(Gi, Whh, bhh, perm, lsort, offs, B, hout, ldh, hoff, saved, plane, stream);
-    case 64: return launch_fwd<64>(Gi, Whh, bhh, perm, lsort, offs, B, hout, ldh, hoff, saved, plane, stream);
-    case 128: return launch_fwd<128>(Gi, Whh, bhh, perm, lsort, offs, B, hout, ldh, hoff, saved, plane, stream);
-    default: return RG_ERR_SHAPE;
-  }
+  const GruDirs d{{Gi, Gi}, {Whh, Whh}, {bhh, bhh}, {saved, saved}};
+  return gru_fwd_dirs(d, 1, perm, lsort, offs, B, H, hout, ldh, hoff, plane, stream);
 }
 
 extern "C" int rg_gru_bwd(const float* saved, int64_t plane, const float* Whh, const int32_t* perm,
                           const int32_t* lsort, const int32_t* offs, int B, int H, const float* dhout, int lddh,
                           int dhoff, float* dGi, float* dGh, hipStream_t stream) {
-  if (B <= 0) return RG_ERR_ARG;
-  switch (H) {
-    case 16: return launch_bwd<16>(saved, plane, Whh, perm, lsort, offs, B, dhout, lddh, dhoff, dGi, dGh, stream);
-    case 32: return launch_bwd<32>(saved, plane, Whh, perm, lsort, offs, B, dhout, lddh, dhoff, dGi, dGh, stream);
-    case 64: return launch_bwd<64>(saved, plane, Whh, perm, lsort, offs, B, dhout, lddh, dhoff, dGi, dGh, stream);
-    case 128:
-      return launch_bwd<128>(saved, plane, Whh, perm, lsort, offs, B, dhout, lddh, dhoff, dGi, dGh, stream);
-    default: return RG_ERR_SHAPE;
+  const GruBwdDirs d{{saved, saved}, {Whh, Whh}, {dGi, dGi}, {dGh, dGh}};
+  return gru_bwd_dirs(d, 1, plane, perm, lsort, offs, B, H, dhout, lddh, dhoff, stream);
+}
+
+// Both directions of a bidirectional layer in one launch (host arrays of
+// ndir pointers; direction d writes / reads columns hoff + d·H of hout / dhout).
+extern "C" int rg_gru_fwd_dirs(const float* const* Gi, const float* const* Whh, const float* const* bhh,
+                               float* const* saved, int ndir, const int32_t* perm, const int32_t* lsort,
+                               const int32_t* offs, int B, int H, float* hout, int ldh, int hoff, int64_t plane,
+                               hipStream_t stream) {
+  if (!Gi || !Whh || !bhh || !saved || ndir < 1 || ndir > 2) return RG_ERR_ARG;
+  GruDirs d{};
+  for (int i = 0; i < 2; ++i) {
+    const int j = i < ndir ? i : 0;
+    d.Gi[i] = Gi[j];
+    d.Whh[i] = Whh[j];
+    d.bhh[i] = bhh[j];
+    d.saved[i] = saved[j];
   }
+  return gru_fwd_dirs(d, ndir, perm, lsort, offs, B, H, hout, ldh, hoff, plane, stream);
+}
+
+extern "C" int rg_gru_bwd_dirs(float* const* saved, const float* const* Whh, float* const* dGi, float* const* dGh,
+                               int ndir, int64_t plane, const int32_t* perm, const int32_t* lsort,
+                               const int32_t* offs, int B, int H, const float* dhout, int lddh, int dhoff,
+                               hipStream_t stream) {
+  if (!saved || !Whh || !dGi || !dGh || ndir < 1 || ndir > 2) return RG_ERR_ARG;
+  GruBwdDirs d{};
+  for (int i = 0; i < 2; ++i) {
+    const int j = i < ndir ? i : 0;
+    d.saved[i] = saved[j];
+    d.Whh[i] = Whh[j];
+    d.dGi[i] = dGi[j];
+    d.dGh[i] = dGh[j];
+  }
+  return gru_bwd_dirs(d, ndir, plane, perm, lsort, offs, B, H, dhout, lddh, dhoff, stream);
 }
 
 // ------------------------------------------- persistent wide path (H 256) --

@@ -92,11 +92,90 @@ __global__ __launch_bounds__(PACK_THREADS) void k_pack(const int64_t* __restrict
   if (tid == 0) offs[B] = carry;
 }
 
+// B <= PACK_SORT_MAX: the same permutation from one LDS bitonic sort of the
+// unique keys (L - len)·B + row (length descending, row ascending = stable),
+// then a block scan of the sorted lengths.  No serial per-thread loops: the
+// general kernel above spends ~0.1 ms at B 4096 in its O(block) rank scans.
+#define PACK_SORT_MAX 8192
+__global__ __launch_bounds__(PACK_THREADS) void k_pack_sort(const int64_t* __restrict__ lens, int B, int L,
+                                                            int unpacked, int n2, int32_t* __restrict__ perm,
+                                                            int32_t* __restrict__ lsort, int32_t* __restrict__ offs) {
+  __shared__ uint32_t key[PACK_SORT_MAX];
+  __shared__ int wsum[PACK_THREADS / 64];
+  const int tid = threadIdx.x;
+  for (int i = tid; i < n2; i += PACK_THREADS) {
+    uint32_t k = 0xFFFFFFFFu;
+    if (i < B) {
+      int l = unpacked ? L : (int)lens[i];
+      l = l < 1 ? 1 : (l > L ? L : l);
+      k = (uint32_t)(L - l) * (uint32_t)B + (uint32_t)i;
+    }
+    key[i] = k;
+  }
+  __syncthreads();
+  for (int size = 2; size <= n2; size <<= 1)
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      for (int i = tid; i < n2 / 2; i += PACK_THREADS) {
+        const int lo = 2 * i - (i & (stride - 1));
+        const int hi = lo + stride;
+        const bool up = (lo & size) == 0;
+        const uint32_t a = key[lo], b = key[hi];
+        if ((a > b) == up) {
+          key[lo] = b;
+          key[hi] = a;
+        }
+      }
+      __syncthreads();
+    }
+  // rows r of the sorted order; offs = exclusive scan of the lengths
+  constexpr int PER = PACK_SORT_MAX / PACK_THREADS;
+  const int r0 = tid * PER;
+  int lv[PER], run = 0;
+#pragma unroll
+  for (int q = 0; q < PER; ++q) {
+    const int r = r0 + q;
+    lv[q] = 0;
+    if (r < B) {
+      const uint32_t k = key[r];
+      lv[q] = L - (int)(k / (uint32_t)B);
+      perm[r] = (int32_t)(k % (uint32_t)B);
+      lsort[r] = lv[q];
+    }
+    run += lv[q];
+  }
+  // block exclusive scan of the per-thread sums (wave scan + wave totals)
+  const int lane = tid & 63, w = tid >> 6;
+  int inc = run;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const int y = __shfl_up(inc, d);
+    if (lane >= d) inc += y;
+  }
+  if (lane == 63) wsum[w] = inc;
+  __syncthreads();
+  int base = 0;
+  for (int q = 0; q < w; ++q) base += wsum[q];
+  int acc = base + inc - run;
+#pragma unroll
+  for (int q = 0; q < PER; ++q) {
+    const int r = r0 + q;
+    if (r < B) offs[r] = acc;
+    acc += lv[q];
+  }
+  if (tid == PACK_THREADS - 1) offs[B] = acc;
+}
+
 extern "C" int rg_pack(const int64_t* lens, int B, int L, int unpacked, int32_t* perm, int32_t* lsort,
                        int32_t* offs, hipStream_t stream) {
   if (B <= 0 || L <= 0 || L > PACK_MAXL) return RG_ERR_ARG;
-  hipLaunchKernelGGL(k_pack, dim3(1), dim3(PACK_THREADS), 0, stream, lens, B, L, unpacked, perm, lsort,
-                     offs);
+  if (B <= PACK_SORT_MAX) {
+    int n2 = 2;
+    while (n2 < B) n2 <<= 1;
+    hipLaunchKernelGGL(k_pack_sort, dim3(1), dim3(PACK_THREADS), 0, stream, lens, B, L, unpacked, n2, perm, lsort,
+                       offs);
+  } else {
+    hipLaunchKernelGGL(k_pack, dim3(1), dim3(PACK_THREADS), 0, stream, lens, B, L, unpacked, perm, lsort, offs);
+  }
   RG_LAUNCH_CHECK();
   return RG_OK;
 }

@@ -81,6 +81,8 @@ SIGNATURES = {
     "rg_hits_ndcg": [P, I, P, I, P, I, P, P],
     "rg_mask_scale": [P, P, F, I64, P, P],
     "rg_gru_wide_work_bytes": [I],
+    "rg_gru_fwd_dirs": [P, P, P, P, I, P, P, P, I, I, P, I, I, I64, P],
+    "rg_gru_bwd_dirs": [P, P, P, P, I, I64, P, P, P, I, I, P, I, I, P],
     "rg_gru_fwd_wide": [P, P, P, P, P, P, I, I, P, I, I, P, I64, P, P],
     "rg_gru_bwd_wide": [P, I64, P, P, P, P, I, I, P, I, I, P, P, P, P],
     "rg_gather_h": [P, I, I, P, P, P, P, I64, I, I, P, P, P, P],
@@ -152,7 +154,7 @@ def call(name: str, *args) -> int:
 
 def host_ptr_array(tensors):
     """HOST array of device pointers (for the multi-head entry points)."""
-    arr = (C.c_void_p * len(tensors))(*[t.data_ptr() for t in tensors])
+    arr = (C.c_void_p * len(tensors))(*[None if t is None else t.data_ptr() for t in tensors])
     return arr
 
 

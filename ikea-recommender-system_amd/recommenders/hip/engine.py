@@ -274,16 +274,19 @@ class Trunk:
             with region("gemm_ih"):
                 call("rg_gemm_f32", w.X[d].data_ptr(), E, 1, w_ih.p.data_ptr(), 1, E, w.Gi[d].data_ptr(), 3 * H,
                      b_ih.p.data_ptr(), w.TM, w.ntok_ptr, 3 * H, E, None, 1, st)
-            with region("gru_fwd"):
-                if self.wide:
+            if self.wide:
+                with region("gru_fwd"):
                     call("rg_gru_fwd_wide", w.Gi[d].data_ptr(), w_hh.p.data_ptr(), b_hh.p.data_ptr(),
                          w.perm.data_ptr(), w.lsort.data_ptr(), w.offs.data_ptr(), B, H, w.h.data_ptr(),
                          self.ndir * H, d * H, w.saved[d].data_ptr() if save else None, w.plane,
                          w.wfrag.data_ptr(), st)
-                else:
-                    call("rg_gru_fwd", w.Gi[d].data_ptr(), w_hh.p.data_ptr(), b_hh.p.data_ptr(),
-                         w.perm.data_ptr(), w.lsort.data_ptr(), w.offs.data_ptr(), B, H, w.h.data_ptr(),
-                         self.ndir * H, d * H, w.saved[d].data_ptr() if save else None, w.plane, st)
+        if not self.wide:   # every direction in one launch (grid.y = direction)
+            with region("gru_fwd"):
+                nd = range(self.ndir)
+                call("rg_gru_fwd_dirs", host_ptr_array([w.Gi[d] for d in nd]),
+                     host_ptr_array([self.dirs[d][1].p for d in nd]), host_ptr_array([self.dirs[d][3].p for d in nd]),
+                     host_ptr_array([w.saved[d] if save else None for d in nd]), self.ndir, w.perm.data_ptr(),
+                     w.lsort.data_ptr(), w.offs.data_ptr(), B, H, w.h.data_ptr(), self.ndir * H, 0, w.plane, st)
         return w.h
 
     def backward(self, dh, slot="main"):
@@ -292,17 +295,18 @@ class Trunk:
         w = next(v for k, v in self._ws.items() if k[0] == slot and k[3])
         st = stream_ptr()
         H, E, B, TM, S = self.H, self.E, w.B, w.TM, w.splits
-        for d in range(self.ndir):
-            w_ih, w_hh, _, _ = self.dirs[d]
-            with region("gru_bwd"):
-                if self.wide:
-                    call("rg_gru_bwd_wide", w.saved[d].data_ptr(), w.plane, w_hh.p.data_ptr(), w.perm.data_ptr(),
-                         w.lsort.data_ptr(), w.offs.data_ptr(), B, H, dh.data_ptr(), self.ndir * H, d * H,
-                         w.dGi[d].data_ptr(), w.dGh[d].data_ptr(), w.wfrag.data_ptr(), st)
-                else:
-                    call("rg_gru_bwd", w.saved[d].data_ptr(), w.plane, w_hh.p.data_ptr(), w.perm.data_ptr(),
-                         w.lsort.data_ptr(), w.offs.data_ptr(), B, H, dh.data_ptr(), self.ndir * H, d * H,
-                         w.dGi[d].data_ptr(), w.dGh[d].data_ptr(), st)
+        with region("gru_bwd"):
+            if self.wide:
+                for d in range(self.ndir):
+                    call("rg_gru_bwd_wide", w.saved[d].data_ptr(), w.plane, self.dirs[d][1].p.data_ptr(),
+                         w.perm.data_ptr(), w.lsort.data_ptr(), w.offs.data_ptr(), B, H, dh.data_ptr(),
+                         self.ndir * H, d * H, w.dGi[d].data_ptr(), w.dGh[d].data_ptr(), w.wfrag.data_ptr(), st)
+            else:   # every direction in one launch
+                nd = range(self.ndir)
+                call("rg_gru_bwd_dirs", host_ptr_array([w.saved[d] for d in nd]),
+                     host_ptr_array([self.dirs[d][1].p for d in nd]), host_ptr_array([w.dGi[d] for d in nd]),
+                     host_ptr_array([w.dGh[d] for d in nd]), self.ndir, w.plane, w.perm.data_ptr(),
+                     w.lsort.data_ptr(), w.offs.data_ptr(), B, H, dh.data_ptr(), self.ndir * H, 0, st)
         self._pending = (w, S)
 
     def step(self, adam6, tag):

@@ -90,6 +90,16 @@ int rg_gru_fwd(const float* Gi, const float* Whh, const float* bhh, const int32_
 int rg_gru_bwd(const float* saved, int64_t plane, const float* Whh, const int32_t* perm, const int32_t* lsort,
                const int32_t* offs, int B, int H, const float* dhout, int lddh, int dhoff, float* dGi, float* dGh,
                rg_stream_t stream);
+/* every direction of a bidirectional layer (BidirGRU4Rec/model.py:51-58, 86-90) in ONE launch
+ * (grid.y = direction): host arrays of ndir (1 or 2) device pointers; direction d reads / writes
+ * columns hoff + d·H of hout (dhoff + d·H of dhout); the packing (perm / lsort / offs) is shared
+ * (the backward direction's gather stored its rows time-reversed).  H in {16, 32, 64, 128}. */
+int rg_gru_fwd_dirs(const float* const* Gi, const float* const* Whh, const float* const* bhh, float* const* saved,
+                    int ndir, const int32_t* perm, const int32_t* lsort, const int32_t* offs, int B, int H,
+                    float* hout, int ldh, int hoff, int64_t plane, rg_stream_t stream);
+int rg_gru_bwd_dirs(float* const* saved, const float* const* Whh, float* const* dGi, float* const* dGh, int ndir,
+                    int64_t plane, const int32_t* perm, const int32_t* lsort, const int32_t* offs, int B, int H,
+                    const float* dhout, int lddh, int dhoff, rg_stream_t stream);
 
 /* ---- A6/A7 full-softmax head: replaces self.output(h) (nn.Linear,
  * GRU4Rec/model.py:58-60,80) + nn.CrossEntropyLoss(mean) (:121,146).

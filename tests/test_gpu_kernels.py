@@ -41,13 +41,17 @@ def pack(lens, L, unpacked=0):
 
 def test_pack_stable_descending():
     g = torch.Generator().manual_seed(0)
-    for B, L in [(7, 5), (1000, 20), (4096, 50), (3000, 3)]:
+    # B <= 8192: the bitonic-sort kernel; 9000: the general one; lengths outside [1, L] clamp
+    for B, L in [(7, 5), (1000, 20), (4096, 50), (3000, 3), (8192, 100), (9000, 30), (1, 4), (4096, 512)]:
         lens = torch.randint(1, L + 1, (B,), generator=g)
+        if B > 1:
+            lens[0], lens[-1] = 0, L + 7
         perm, ls, offs = pack(lens, L)
-        order = np.argsort(-lens.numpy(), kind="stable")
+        lc = lens.clamp(1, L).numpy()
+        order = np.argsort(-lc, kind="stable")
         assert np.array_equal(perm.cpu().numpy(), order)
-        assert np.array_equal(ls.cpu().numpy(), lens.numpy()[order])
-        assert np.array_equal(offs.cpu().numpy(), np.concatenate([[0], np.cumsum(lens.numpy()[order])]))
+        assert np.array_equal(ls.cpu().numpy(), lc[order])
+        assert np.array_equal(offs.cpu().numpy(), np.concatenate([[0], np.cumsum(lc[order])]))
         perm, ls, offs = pack(lens, L, unpacked=1)
         assert int(offs[-1]) == B * L
 
