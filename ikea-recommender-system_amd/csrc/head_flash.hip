@@ -370,6 +370,100 @@ __global__ __launch_bounds__(64 * fl_nw(HF, 1)) void k_flash_fwd(
   }
 }
 
+// --------------------------------------------------------- argmax only ----
+// argmax_j (h·Wᵀ + b)[row, j] on split-bf16 MFMAs without storing logits: the
+// S-part of pass 1 alone (no softmax, no O) with the first-maximum tracking —
+// the double-Q target a* = argmax_a Q(s', a) of SQN / SMORL (sqn_gru.py:
+// 222-226, tensor_operations.py:50-70 via the combined head).  Same
+// workgroup / split / XCD layout and K-plane DMA ring as pass 1; per split the
+// row's best logit and item go to pbest / parg (merged by rg_flash_argmax).
+template <int HF, int NT>
+__global__ __launch_bounds__(64 * fl_nw(HF, 1)) void k_flash_amax(
+    const bf16x8* __restrict__ Hk, const bf16x8* __restrict__ Wk, const float* __restrict__ bias_pad, int B, int A,
+    int nrb, int nsplit, int cps, float* __restrict__ pbest, int32_t* __restrict__ parg) {
+  constexpr int NW = fl_nw(HF, 1);
+  constexpr int NS = HF / 16;
+  constexpr int EK = NS * 192;
+  __shared__ bf16x8 sk0[EK], sk1[EK];
+  __shared__ __attribute__((aligned(16))) float sb0[32], sb1[32];
+  const int tid = threadIdx.x, lane = tid & 63, hh = lane >> 5, l32 = lane & 31, lane16 = 16 * lane;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  int bid = blockIdx.x;
+  const int total = nrb * nsplit;
+  if ((total & 7) == 0) bid = (bid & 7) * (total >> 3) + (bid >> 3);
+  const int split = bid / nrb, rblk = bid % nrb;
+  const int r0 = rblk * 32 * NW + 32 * w;
+  const bool active = r0 < B;
+  const int nct = (A + 31) / 32;
+  const int c0 = split * cps;
+  const int nch = max(0, min(nct, c0 + cps) - c0);
+#define FA_ISSUE(C, SK, SB)                                                    \
+  do {                                                                         \
+    stage<EK, NW>(Wk + (int64_t)(C) * EK, SK, w, lane16);                      \
+    if (w == 0 && lane < 8) blds16(rsrc_of(bias_pad + 32 * (C)), SB, lane16, 0); \
+  } while (0)
+  if (nch > 0) FA_ISSUE(c0, sk0, sb0);
+  bf16x8 hk[NS][3];
+#pragma unroll
+  for (int s = 0; s < NS; ++s)
+#pragma unroll
+    for (int p = 0; p < 3; ++p)
+      hk[s][p] = active ? Hk[((int64_t)(r0 >> 5) * NS + s) * 192 + p * 64 + lane] : bf16x8{};
+  float bv = NEG_INF;
+  int bi = INT32_MAX;
+  __syncthreads();
+  auto chunk = [&](const bf16x8* sk, const float* sb, int c) __attribute__((always_inline)) {
+    f16v sa = {};
+    bf16x8 a0 = sk[lane], a1 = sk[64 + lane], a2 = sk[128 + lane];
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      const int sn = s + 1 < NS ? s + 1 : s;
+      const bf16x8 n0 = sk[sn * 192 + lane], n1 = sk[sn * 192 + 64 + lane], n2 = sk[sn * 192 + 128 + lane];
+      sa = mfma_split<NT>(a0, a1, a2, hk[s][0], hk[s][1], hk[s][2], sa);
+      a0 = n0;
+      a1 = n1;
+      a2 = n2;
+      __builtin_amdgcn_sched_barrier(0);
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const f4 bq = *reinterpret_cast<const f4*>(&sb[8 * q + 4 * hh]);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const float z = sa[4 * q + u] + bq[u];
+        if (z > bv) {  // items increase with r: strict > keeps the first maximum
+          bv = z;
+          bi = 32 * (c0 + c) + 8 * q + 4 * hh + u;
+        }
+      }
+    }
+  };
+  for (int c = 0; c < nch; c += 2) {
+    if (c + 1 < nch) FA_ISSUE(c0 + c + 1, sk1, sb1);
+    __builtin_amdgcn_sched_barrier(0);
+    if (active) chunk(sk0, sb0, c);
+    __syncthreads();
+    if (c + 1 < nch) {
+      if (c + 2 < nch) FA_ISSUE(c0 + c + 2, sk0, sb0);
+      __builtin_amdgcn_sched_barrier(0);
+      if (active) chunk(sk1, sb1, c + 1);
+      __syncthreads();
+    }
+  }
+#undef FA_ISSUE
+  if (!active) return;
+  const float v2 = __shfl_xor(bv, 32);
+  const int i2 = __shfl_xor(bi, 32);
+  if (v2 > bv || (v2 == bv && i2 < bi)) {
+    bv = v2;
+    bi = i2;
+  }
+  if (hh == 0) {
+    pbest[(int64_t)split * B + r0 + l32] = bv;
+    parg[(int64_t)split * B + r0 + l32] = bi;
+  }
+}
+
 // ------------------------------------------------------------ combine ----
 // lse over the splits (natural units) and, when the target is one of this
 // shard's items [lo, lo + A), its logit z = h·W[t] + b[t]; 0 for a target
@@ -890,6 +984,37 @@ extern "C" int rg_flash_fwd(const void* Hk, const void* Wk, const void* Wr, cons
                             int HF, int terms, int nsplit, float* pm, float* pl, float* pO, hipStream_t stream) {
   return rg_flash_fwd_top(Hk, Wk, Wr, bias_pad, B, A, HF, terms, nsplit, pm, pl, pO, nullptr, nullptr, nullptr,
                           stream);
+}
+
+extern "C" int rg_flash_amax_fwd(const void* Hk, const void* Wk, const float* bias_pad, int B, int A, int HF,
+                                 int terms, int nsplit, float* pbest, int32_t* parg, hipStream_t stream) {
+  if (B <= 0 || A <= 0 || (B % 32) || nsplit <= 0 || !Hk || !Wk || !bias_pad || !pbest || !parg) return RG_ERR_ARG;
+  if (terms != 6 && terms != 9) return RG_ERR_ARG;
+  if (!flash_hf_ok(HF)) return RG_ERR_SHAPE;
+  const int nct = (A + 31) / 32;
+  const int cps = (nct + nsplit - 1) / nsplit;
+  const int rpb = fl_rows(HF, 1);
+  const int nrb = (B + rpb - 1) / rpb;
+  const dim3 grid((unsigned)(nrb * nsplit));
+#define FM(HFV, NTV)                                                                                            \
+  hipLaunchKernelGGL((k_flash_amax<HFV, NTV>), grid, dim3(64 * fl_nw(HFV, 1)), 0, stream, (const bf16x8*)Hk,    \
+                     (const bf16x8*)Wk, bias_pad, B, A, nrb, nsplit, cps, pbest, parg)
+#define FT(HFV)          \
+  if (terms == 9) {      \
+    FM(HFV, 9);          \
+  } else {               \
+    FM(HFV, 6);          \
+  }
+  switch (HF) {
+    case 32: FT(32); break;
+    case 64: FT(64); break;
+    case 128: FT(128); break;
+    case 256: FT(256); break;
+  }
+#undef FT
+#undef FM
+  RG_LAUNCH_CHECK();
+  return RG_OK;
 }
 
 extern "C" int rg_flash_argmax(const float* pbest, const int32_t* parg, int nsplit, int B, int32_t* out,

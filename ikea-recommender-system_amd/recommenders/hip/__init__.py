@@ -51,6 +51,7 @@ SIGNATURES = {
     "rg_build_transitions": [P, P, P, P, P, I, I, I64, I, P, P, P, P, P, P, P, P],
     "rg_flash_fwd_top": [P, P, P, P, I, I, I, I, I, P, P, P, P, P, P, P],
     "rg_flash_argmax": [P, P, I, I, P, P, P],
+    "rg_flash_amax_fwd": [P, P, P, I, I, I, I, I, P, P, P],
     "rg_flash_topk_cap": [],
     "rg_flash_topk": [P, I, I, I, F, F, P, P, P, I, P, P, P, P, P, P],
     "rg_flash_lse": [P, P, I, P, P, P, P, I64, I, I64, I, I, P, P, P],

@@ -502,6 +502,22 @@ class _FlashWS:
             self.ncand = z(B, dt=torch.int32)
 
 
+class _AmaxWS:
+    """Workspace of the split-bf16 argmax (K-planes of h and W, per-split bests)."""
+
+    def __init__(self, B, A, HF, device):
+        u8 = lambda n: torch.empty(int(n), dtype=torch.uint8, device=device)  # noqa: E731
+        z = lambda *s, dt=torch.float32: torch.empty(*s, dtype=dt, device=device)  # noqa: E731
+        self.B = B
+        nrb = -(-B // call("rg_flash_rows_per_block", HF))
+        self.nsplit = _round_up(min(max(1, 256 // nrb), -(-A // 32)), 8)
+        self.Hk = u8(call("rg_head_plane_bytes", B, HF))
+        self.Wk = u8(call("rg_head_plane_bytes", A, HF))
+        self.bias_pad = z(_round_up(A, 32))
+        self.pbest, self.parg = z(self.nsplit, B), z(self.nsplit, B, dt=torch.int32)
+        self.amax, self.mx = z(B, dt=torch.int32), z(B)
+
+
 # Head-GEMM arithmetic (build extension; the reference computes in fp32):
 #   "f32"   native fp32 MFMA (v_mfma_f32_32x32x2_f32: bitwise an fmaf chain)
 #   "f32x9" fp32 operands split exactly into three bf16 planes, all nine
@@ -695,10 +711,29 @@ class SoftmaxHead:
 
     def argmax(self, h, slot="argmax"):
         """argmax_j (h·Wᵀ + b)[b, j] without storing Z (first maximum); the
-        row maxima are left in ``self.ws(slot, B, False).mx``."""
+        row maxima are left in ``self.argmax_mx``.  With a split-bf16
+        precision the contraction runs on bf16 MFMAs (csrc/head_flash.hip
+        k_flash_amax: pass 1's S-part with first-maximum tracking)."""
         B = h.shape[0]
-        w = self.ws(slot, B, False)
         st = stream_ptr()
+        terms = self.flash_terms(B)
+        if terms:
+            w = self._aws.get(slot) if hasattr(self, "_aws") else None
+            if w is None or w.B != B:
+                if not hasattr(self, "_aws"):
+                    self._aws = {}
+                w = self._aws[slot] = _AmaxWS(B, self.A, self.HF, self.device)
+            call("rg_head_planes", h.data_ptr(), B, self.HF, w.Hk.data_ptr(), None, None, None, st)
+            call("rg_head_planes", self.W.p.data_ptr(), self.A, self.HF, w.Wk.data_ptr(), None, self.b.p.data_ptr(),
+                 w.bias_pad.data_ptr(), st)
+            call("rg_flash_amax_fwd", w.Hk.data_ptr(), w.Wk.data_ptr(), w.bias_pad.data_ptr(), B, self.A, self.HF,
+                 terms, w.nsplit, w.pbest.data_ptr(), w.parg.data_ptr(), st)
+            call("rg_flash_argmax", w.pbest.data_ptr(), w.parg.data_ptr(), w.nsplit, B, w.amax.data_ptr(),
+                 w.mx.data_ptr(), st)
+            self.argmax_mx = w.mx
+            return w.amax
+        w = self.ws(slot, B, False)
+        self.argmax_mx = w.mx
         call("rg_head_fwd", h.data_ptr(), self.W.p.data_ptr(), self.b.p.data_ptr(), B, self.A, self.HF, None, 0,
              w.pmax.data_ptr(), w.psum.data_ptr(), w.parg.data_ptr(), 0, st)
         call("rg_lse_combine", w.pmax.data_ptr(), w.psum.data_ptr(), w.parg.data_ptr(), B, w.nJ, w.work.data_ptr(),

@@ -60,6 +60,16 @@ class QNet(HipNet):
         self._argmax_head = None
         self._buf = {}
 
+    def set_matmul_precision(self, precision):
+        """Also the Q heads' argmax contraction (the double-Q target a*): on
+        split-bf16 MFMAs with f32x6 / f32x9; their row gathers stay fp32."""
+        super().set_matmul_precision(precision)
+        for q in self.q_heads:
+            q.set_matmul_precision(precision)
+        if self._argmax_head is not None:
+            self._argmax_head.precision = precision
+        return self
+
     def named_param_objs(self):
         out = list(self.trunk.named_params()) + self.sup_head_output.named_params()
         for q in self.q_heads:
@@ -93,6 +103,7 @@ class QNet(HipNet):
         if self._argmax_head is None:
             hd = SoftmaxHead.__new__(SoftmaxHead)
             hd.name, hd.A, hd.HF, hd.device, hd._ws = "qcomb", self.q_heads[0].A, self.hf, self.device, {}
+            hd.precision = self.q_heads[0].precision
             hd.W = _T(torch.empty_like(self.q_heads[0].W.p))
             hd.b = _T(torch.empty_like(self.q_heads[0].b.p))
             self._argmax_head = hd

@@ -244,7 +244,7 @@ def sharded_double_q_step(nets, clocks, k, s, a, r, s_next, true_len, true_next_
         Hn_all = _gather_rows(comm, main, "Hn_all", h_n)
         am = main.argmax_q(Hn_all, None if smorl is None else smorl["w"])
         head_am = main.q_heads[0] if len(main.q_heads) == 1 else main._argmax_head
-        a_star = _global_argmax(main, head_am.ws("argmax", Bg, False).mx, am, A, "a_star")
+        a_star = _global_argmax(main, head_am.argmax_mx, am, A, "a_star")
         h_b = boot.trunk.forward(s_next, true_len, slot="boot", save=False)   # quirk: true_len
         Hb_all = _gather_rows(comm, main, "Hb_all", h_b)
         qn_all, _ = _owner_q(boot, main, Hb_all, "qn", idx32=a_star)

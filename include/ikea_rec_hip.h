@@ -157,6 +157,10 @@ int rg_flash_rows_per_block(int HF);
 int rg_flash_fwd_top(const void* Hk, const void* Wk, const void* Wr, const float* bias_pad, int B, int A, int HF,
                      int terms, int nsplit, float* pm, float* pl, float* pO, float* pbest, int32_t* parg, float* cmax,
                      rg_stream_t stream);
+/* rg_flash_amax_fwd: argmax only (the double-Q target, sqn_gru.py:222-226) — pass 1's S-part on the
+ *   K-planes of h and W with per-split first maximum (pbest / parg as rg_flash_fwd_top), no softmax. */
+int rg_flash_amax_fwd(const void* Hk, const void* Wk, const float* bias_pad, int B, int A, int HF, int terms,
+                      int nsplit, float* pbest, int32_t* parg, rg_stream_t stream);
 int rg_flash_argmax(const float* pbest, const int32_t* parg, int nsplit, int B, int32_t* out, float* out_max,
                     rg_stream_t stream);
 int rg_flash_topk_cap(void);

@@ -301,3 +301,37 @@ def test_fused_topk_exact_ties_keep_lowest_index():
         assert (idx[:, 0] == 17).all()
         if K_ > 1:
             assert (idx[:, 1:4] == torch.tensor([1234, 2500, 3999])).all()
+
+
+@pytest.mark.parametrize("precision", ["f32x6", "f32x9"])
+@pytest.mark.parametrize("B,A,HF,nsplit", [(128, 3001, 64, 8), (96, 20011, 128, 16), (160, 5003, 256, 8),
+                                           (64, 777, 32, 3)])
+def test_fused_argmax_only(precision, B, A, HF, nsplit):
+    """rg_flash_amax_fwd (the double-Q target's argmax on split-bf16 MFMAs,
+    sqn_gru.py:222-226): the first maximum of the fp64 logits except where the
+    top two lie within the arithmetic's error bound; the returned maxima
+    within fp32 rounding; exact duplicates resolve to the lowest index."""
+    call, st = C().call, C().stream_ptr()
+    h, W, b, _ = inputs(B, A, HF, 7 * B + A)
+    W[A - 5], b[A - 5] = W[11], b[11]          # an exact duplicate of item 11 later in the table
+    hd, Wd, bd = h.to(dev), W.to(dev), b.to(dev)
+    Hk, Wk = _u8(call("rg_head_plane_bytes", B, HF)), _u8(call("rg_head_plane_bytes", A, HF))
+    bp = torch.empty((A + 31) // 32 * 32, device=dev)
+    call("rg_head_planes", hd.data_ptr(), B, HF, Hk.data_ptr(), None, None, None, st)
+    call("rg_head_planes", Wd.data_ptr(), A, HF, Wk.data_ptr(), None, bd.data_ptr(), bp.data_ptr(), st)
+    pbest = torch.full((nsplit, B), -7.0, device=dev)
+    parg = torch.full((nsplit, B), -7, dtype=torch.int32, device=dev)
+    call("rg_flash_amax_fwd", Hk.data_ptr(), Wk.data_ptr(), bp.data_ptr(), B, A, HF, TERMS[precision], nsplit,
+         pbest.data_ptr(), parg.data_ptr(), st)
+    idx = torch.empty(B, dtype=torch.int32, device=dev)
+    mx = torch.empty(B, device=dev)
+    call("rg_flash_argmax", pbest.data_ptr(), parg.data_ptr(), nsplit, B, idx.data_ptr(), mx.data_ptr(), st)
+    torch.cuda.synchronize()
+    Z = (h.double() @ W.double().t() + b.double()).numpy()
+    got = idx.cpu().long().numpy()
+    ref = Z.argmax(1)
+    gap = np.abs(Z[np.arange(B), got] - Z[np.arange(B), ref])
+    assert (gap[got != ref] < 2e-5).all()
+    assert (got != ref).sum() <= max(1, B // 50)
+    np.testing.assert_allclose(mx.cpu().double().numpy(), Z[np.arange(B), got], rtol=0, atol=2e-5)
+    assert not (got == A - 5).any()            # never the later duplicate of 11
