@@ -2,7 +2,7 @@
 """Headline benchmark: GRU4Rec training steps at 1M items, dim 128,
 seq_len <= 50, batch 4096, full-softmax logits (BASELINE.json configs[1]).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c4]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c4|c5]
 
 metric: session-steps/sec (= batch rows × train_step calls per second, whole
 job).  One step = one ``GRU4Rec_trainer.train_step(s, a, true_len)`` on the
@@ -19,7 +19,9 @@ reference CPU math on the GPU-trained weights: its canonical top-20 lists and
 HR@20 / NDCG@20 next to the device's ("hr_ndcg_parity").
 
 Configs: c2 (headline), c3 (BidirGRU4Rec, 2048 sampled negatives),
-c4 (SMORL: GRU4Rec trunk + supervised head + 3 Q heads, 3-reward double-Q).
+c4 (SMORL: GRU4Rec trunk + supervised head + 3 Q heads, 3-reward double-Q),
+c5 (IKEA scale: SMORL at 5M items, d256, seq_len <= 100, global batch 8192
+split over the ranks, fp16 item table; fits one MI355X at ~279 GiB peak).
 Multi-GPU (torch.distributed.run, one rank per GPU, RCCL): weak scaling, each
 rank trains its own 4096-row batch shard, item tables sharded over the ranks
 (DESIGN.md §5).
@@ -62,9 +64,10 @@ def parse():
     ap.add_argument("--no-kernel-timing", action="store_true")
     ap.add_argument("--no-eval", action="store_true")
     ap.add_argument("--force-shard", action="store_true", help="item-sharded path even at world 1 (test)")
-    ap.add_argument("--config", choices=["c2", "c3", "c4"], default="c2",
+    ap.add_argument("--config", choices=["c2", "c3", "c4", "c5"], default="c2",
                     help="c2: headline GRU4Rec full softmax; c3: BidirGRU4Rec with sampled softmax; "
-                         "c4: SMORL 3-reward double-Q")
+                         "c4: SMORL 3-reward double-Q; c5: IKEA-scale SMORL (5M items, d256, L<=100, global "
+                         "batch 8192, fp16 item table)")
     ap.add_argument("--negatives", type=int, default=2048)
     # f32x6 (default): fp32 operands split exactly into three bf16 planes, the six
     # plane products above 2^-24 relative on bf16 MFMAs, fp32 accumulation;
@@ -157,7 +160,7 @@ def make_trainer(cfg, args, dev, shard):
     if cfg == "c3":
         return BidirGRU4Rec_trainer(dropout=0.0, n_negatives=args.negatives, matmul_precision=args.precision,
                                     **common)
-    if cfg == "c4":
+    if cfg in ("c4", "c5"):
         from recommenders.data_utils.synthetic import unpopular_items
         from recommenders.models.SMORL.smorl_gru import SMORL_trainer
         common.pop("device")
@@ -165,13 +168,14 @@ def make_trainer(cfg, args, dev, shard):
         div = torch.randn(N + 1, 64, generator=g) * 0.01     # frozen div table
         return SMORL_trainer(padding_pos="end", gamma=0.5, q_weights=[1.0, 1.0, 1.0], alpha=1.0, div_embedding=div,
                              unpopular_actions_set=unpopular_items(args.item_counts), topk_div=1, topk_nov=1,
-                             device=dev, shard_items=shard, matmul_precision=args.precision, **common)
+                             device=dev, shard_items=shard, matmul_precision=args.precision,
+                             fp16_embeddings=(cfg == "c5"), **common)
     raise ValueError(cfg)
 
 
 def step_args(cfg, b):
     s, a, r, sn, ln, nln, e = b
-    if cfg == "c4":
+    if cfg in ("c4", "c5"):
         return (s, a, r, sn, ln, nln, e)
     return (s, a, ln)
 
@@ -272,7 +276,7 @@ def head_roofline(kern, precision, B, N, E):
     t = heads[dom] * 1e-3
     traffic = None
     pmc = os.path.join(HERE, "profiles", "pmc_traffic.json")
-    if os.path.exists(pmc):
+    if os.path.exists(pmc) and (B, N, E) == (BATCH, ITEMS, DIM):   # the PMC passes ran at the C2 shapes
         traffic = json.load(open(pmc)).get(f"{dom}:{precision}" if terms else dom)
     if terms:
         # fused split-bf16 head (csrc/head_flash.hip): pass 1 (head_fwd: Z and the softmax half of
@@ -301,7 +305,18 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    shard = (world > 1 or args.force_shard) and args.config in ("c2", "c4")
+    if args.config == "c5":
+        # BASELINE configs[4]: 5M items, d256, seq_len <= 100, batch 8192 (global:
+        # each of the N ranks trains 8192 / N rows), fp16 item table; flags that
+        # were left at the C2 defaults take the C5 values
+        for k, c2v, c5v in (("items", ITEMS, 5_000_000), ("dim", DIM, 256), ("seq", SEQ, 100),
+                            ("batch", BATCH, 8192)):
+            if getattr(args, k) == c2v:
+                setattr(args, k, c5v)
+        if args.batch % (32 * world):
+            raise SystemExit("c5: the global batch must split into multiples of 32 rows per rank")
+        args.batch //= world
+    shard = (world > 1 or args.force_shard) and args.config in ("c2", "c4", "c5")
     if world > 1 or args.force_shard:
         import torch.distributed as dist
         torch.cuda.set_device(local)
@@ -325,10 +340,15 @@ def main():
     hb = st.batch(nsteps, B)
     held = (hb[0], hb[1], hb[4])
     T = float(np.mean(tok[args.warmup:]))
+    t_init = time.perf_counter()
     tr = make_trainer(args.config, args, dev, shard)
     tr.set_train()
+    print(f"bench: trainer built in {time.perf_counter() - t_init:.1f} s, "
+          f"{torch.cuda.memory_allocated(dev) / 2**30:.1f} GiB on the device", file=sys.stderr, flush=True)
     dt, losses, kern, per_step = timed_run(tr, batches, args.warmup, args.steps, world, not args.no_kernel_timing,
                                            args.config)
+    print(f"bench: peak device memory {torch.cuda.max_memory_allocated(dev) / 2**30:.1f} GiB", file=sys.stderr,
+          flush=True)
     ev, dev_idx = None, None
     net = getattr(tr, "gru_model", None)
     if not args.no_eval and not shard and net is not None:
@@ -344,7 +364,7 @@ def main():
     native = None
     HF = E * (2 if args.config == "c3" else 1)
     terms = {"f32x9": 9, "f32x6": 6}.get(args.precision, 0)
-    if args.config in ("c2", "c4"):
+    if args.config in ("c2", "c4", "c5"):
         if kern:
             sup = net.heads["output"] if net is not None else tr.SMORL_1.sup_head_output
             prec = args.precision if sup.flash_terms(B * world) else "f32"
@@ -399,15 +419,21 @@ def main():
         metric = "session-steps/sec, BidirGRU4Rec 1M items, dim128, batch 4096, 2048 sampled negatives"
         workload = (f"BidirGRU4Rec {N} items, dim{E}, seq_len<={L}, batch {B}, {args.negatives} shared uniform "
                     f"negatives (sampled softmax), dropout 0")
-    else:
+    elif args.config == "c4":
         metric = "session-steps/sec, SMORL (SQN double-Q, 3 rewards) 1M items, dim128, batch 4096"
         workload = (f"SMORL_trainer {N} items, dim{E}, seq_len<={L}, batch {B}/GPU, sup head + Q heads acc/div/nov, "
                     f"topk_div=topk_nov=1, q_weights [1,1,1], gamma 0.5, alpha 1")
+    else:
+        metric = "session-steps/sec, IKEA-scale SMORL (SQN double-Q, 3 rewards) 5M items, dim256, batch 8192"
+        workload = (f"SMORL_trainer {N} items, dim{E}, seq_len<={L}, global batch {B * world} ({B}/GPU), fp16 item "
+                    f"table (fp32 master + Adam), sup head + Q heads acc/div/nov, topk_div=topk_nov=1, "
+                    f"q_weights [1,1,1], gamma 0.5, alpha 1")
     ps = np.array(per_step) * 1e3
     line = {
         "metric": metric,
         "value": round(value, 2), "unit": "session-steps/sec", "n_gpus": world, "steps": args.steps,
-        "warmup": args.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak",
+        "warmup": args.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True,
+        "scaling": "strong" if args.config == "c5" else "weak",
         "vs_baseline": None, "dtype": "f32", "matmul_precision": args.precision,
         "data": "synthetic (seeded Zipf session stream, random-init weights)",
         "config": {"workload": workload,
