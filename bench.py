@@ -211,7 +211,8 @@ def timed_run(tr, batches, warmup, steps, world, kernel_timing, cfg):
         torch.distributed.barrier()
     dt = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([dt], device=torch.cuda.current_device())
+        native = torch.distributed.get_backend() == "nccl"
+        t = torch.tensor([dt], device=torch.cuda.current_device() if native else "cpu")
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         dt = float(t)
     if not all(np.isfinite(losses)):
@@ -319,8 +320,13 @@ def main():
     shard = (world > 1 or args.force_shard) and args.config in ("c2", "c4", "c5")
     if world > 1 or args.force_shard:
         import torch.distributed as dist
+        # RCCL in production; RG_BENCH_BACKEND=gloo rehearses the N-rank path with
+        # several ranks on one GPU (host-staged collectives, hip/dist.py)
+        backend = os.environ.get("RG_BENCH_BACKEND", "nccl")
+        if backend != "nccl":
+            local %= torch.cuda.device_count()
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl")
+        dist.init_process_group(backend)
     if world > 1 and args.config == "c3":
         raise SystemExit("multi-GPU bench runs the C2 / C4 workloads")
     from recommenders.data_utils.synthetic import SessionStream
