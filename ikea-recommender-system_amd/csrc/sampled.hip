@@ -754,3 +754,129 @@ extern "C" int rg_sampled_dz(float* ZT, int64_t ldz, const float* lse, int B, in
   RG_LAUNCH_CHECK();
   return RG_OK;
 }
+
+// ------------------------------------------------------------------ BPR ----
+// Sampled BPR (Rendle et al. 2009; the GRU4Rec paper's pairwise loss) over the
+// same logits — build-defined like the sampled softmax (SURVEY §8 A7 ext.,
+// north_star "sampled-softmax/BPR logits"):
+//   loss = mean_b (1/S) Σ_s −log σ(z_b,pos − z_b,s) = mean_b (1/S) Σ_s softplus(z_b,s − z_b,pos)
+//   ∂loss/∂z_b,s = g·σ(z_b,s − z_b,pos)/S,   ∂loss/∂z_b,pos = −Σ_s ∂loss/∂z_b,s      (g = 1/B)
+// Z element (b, s) lives at Z[b·zsb + s·zss]: row-major Z of rg_sampled_logits
+// (zsb = ldz, zss = 1) or the Zᵀ of rg_sampled_fwd / rg_sampled_fwd_x (zsb = 1,
+// zss = ldz).  k_bpr_rows: one wave per row — the positive logit (fp32 dot),
+// Σ softplus and Σ σ over the row's S logits, loss row (NaN for a target
+// outside [0, A)), zpos, and the positive's gradient rows as k_sampled_lse.
+__device__ __forceinline__ float softplusf_acc(float x) { return fmaxf(x, 0.f) + log1pf(expf(-fabsf(x))); }
+__device__ __forceinline__ float sigmoidf_acc(float x) {
+  if (x >= 0.f) return 1.f / (1.f + expf(-x));
+  const float e = expf(x);
+  return e / (1.f + e);
+}
+
+template <int HF>
+__global__ __launch_bounds__(256) void k_bpr_rows(const float* __restrict__ h, const float* __restrict__ W,
+                                                  const float* __restrict__ bias, const int64_t* __restrict__ tgt,
+                                                  int B, int64_t A, const float* __restrict__ Z, int64_t zsb,
+                                                  int64_t zss, int S, float gscale, float* __restrict__ zpos,
+                                                  float* __restrict__ loss_row, int32_t* __restrict__ ids,
+                                                  float* __restrict__ dzpos, float* __restrict__ gpos,
+                                                  float* __restrict__ dhpos) {
+  constexpr int PER = HF >= 64 ? HF / 64 : 1;
+  const int lane = threadIdx.x & 63;
+  const int b = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (b >= B) return;  // whole wave
+  const int64_t t = tgt[b];
+  const bool ok = t >= 0 && t < A;
+  const int64_t tt = ok ? t : 0;
+  float hv[PER], wv[PER];
+  float dot = 0.f;
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    const int c = lane + 64 * i;
+    const bool cv = c < HF;
+    hv[i] = cv ? h[(int64_t)b * HF + c] : 0.f;
+    wv[i] = cv ? W[tt * HF + c] : 0.f;
+    dot = fmaf(hv[i], wv[i], dot);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) dot += __shfl_xor(dot, o);
+  const float zp = dot + bias[tt];
+  float sp = 0.f, sg = 0.f;
+  const float* zr = Z + (int64_t)b * zsb;
+  for (int s = lane; s < S; s += 64) {
+    const float x = zr[(int64_t)s * zss] - zp;
+    sp += softplusf_acc(x);
+    sg += sigmoidf_acc(x);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    sp += __shfl_xor(sp, o);
+    sg += __shfl_xor(sg, o);
+  }
+  const float inv_s = 1.f / (float)S;
+  const float dp = -gscale * sg * inv_s;
+  if (lane == 0) {
+    zpos[b] = zp;
+    loss_row[b] = ok ? sp * inv_s : __builtin_nanf("");
+    ids[b] = ok ? (int32_t)t : -1;
+    dzpos[b] = ok ? dp : 0.f;
+  }
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    const int c = lane + 64 * i;
+    if (c < HF) {
+      gpos[(int64_t)b * HF + c] = ok ? dp * hv[i] : 0.f;
+      dhpos[(int64_t)b * HF + c] = ok ? dp * wv[i] : 0.f;
+    }
+  }
+}
+
+extern "C" int rg_bpr_rows(const float* h, const float* W, const float* bias, const int64_t* tgt, int B, int64_t A,
+                           int HF, const float* Z, int64_t zsb, int64_t zss, int S, float gscale, float* zpos,
+                           float* loss_row, int32_t* ids, float* dzpos, float* gpos, float* dhpos,
+                           hipStream_t stream) {
+  if (B <= 0 || A <= 0 || S <= 0 || !Z || zsb <= 0 || zss <= 0) return RG_ERR_ARG;
+  dim3 grid((B + 3) / 4);
+#define BPR(HFV)                                                                                            \
+  hipLaunchKernelGGL(k_bpr_rows<HFV>, grid, dim3(256), 0, stream, h, W, bias, tgt, B, A, Z, zsb, zss, S, \
+                     gscale, zpos, loss_row, ids, dzpos, gpos, dhpos)
+  switch (HF) {
+    case 32: BPR(32); break;
+    case 64: BPR(64); break;
+    case 128: BPR(128); break;
+    case 256: BPR(256); break;
+    default: return RG_ERR_SHAPE;
+  }
+#undef BPR
+  RG_LAUNCH_CHECK();
+  return RG_OK;
+}
+
+// dZ(b, s) = g·σ(Z(b, s) − zpos[b])/S in place; workgroup (256 negatives,
+// 128 rows) writes its column sums to slab[row block][s], summed in order
+// (deterministic) into dbg[s] = Σ_b dZ(b, s).
+__global__ __launch_bounds__(256) void k_bpr_dz(float* __restrict__ Z, int64_t zsb, int64_t zss,
+                                                const float* __restrict__ zpos, int B, int S, float gs,
+                                                float* __restrict__ slabs) {
+  const int s = blockIdx.x * 256 + threadIdx.x;
+  const int b0 = blockIdx.y * 128, b1 = min(B, b0 + 128);
+  if (s >= S) return;
+  float acc = 0.f;
+  for (int b = b0; b < b1; ++b) {
+    float* p = Z + (int64_t)b * zsb + (int64_t)s * zss;
+    const float d = sigmoidf_acc(*p - zpos[b]) * gs;
+    *p = d;
+    acc += d;
+  }
+  slabs[(int64_t)blockIdx.y * S + s] = acc;
+}
+
+extern "C" int rg_bpr_dz(float* Z, int64_t zsb, int64_t zss, const float* zpos, int B, int S, float gscale,
+                         float* slabs, float* dbg, hipStream_t stream) {
+  if (B <= 0 || S <= 0 || !Z || zsb <= 0 || zss <= 0 || !zpos || !slabs || !dbg) return RG_ERR_ARG;
+  const int nrb = (B + 127) / 128;
+  hipLaunchKernelGGL(k_bpr_dz, dim3((S + 255) / 256, nrb), dim3(256), 0, stream, Z, zsb, zss, zpos, B, S,
+                     gscale / (float)S, slabs);
+  RG_LAUNCH_CHECK();
+  return rg_reduce_slabs(slabs, nrb, S, dbg, nullptr, S, 0, stream);
+}

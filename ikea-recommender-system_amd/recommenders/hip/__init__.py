@@ -98,6 +98,8 @@ SIGNATURES = {
     "rg_sampled_fwd": [P, P, P, P, I, I, I, P, I64, P, P, P, P, P],
     "rg_sampled_lse": [P, P, P, P, I, I64, I, P, P, I, F, P, P, P, P, P, P, P],
     "rg_sampled_dz": [P, I64, P, I, I, F, P, P],
+    "rg_bpr_rows": [P, P, P, P, I, I64, I, P, I64, I64, I, F, P, P, P, P, P, P, P],
+    "rg_bpr_dz": [P, I64, I64, P, I, I, F, P, P, P],
     "rg_weighted_sum": [P, P, I, I64, P, P],
     "rg_stack_rewards": [P, P, P, I, P, P],
     "rg_token_ids": [P, I, I, P, P, P, I64, P, P, P],

@@ -756,7 +756,7 @@ class _SampledWS:
         self.ZT = z(B, self.ldz) if self.zrow else z(S, self.ldz)
         # (stride over batch rows, stride over negatives) of the logits
         self.zs_b, self.zs_s = (self.ldz, 1) if self.zrow else (1, self.ldz)
-        self.dbslabs = z((B + 127) // 128, S) if self.zrow else None
+        self.dbslabs = z((B + 127) // 128, S)
         self.pmax = z(self.nT, B)
         self.psum = z(self.nT, B)
         self.lse = z(B)
@@ -786,12 +786,18 @@ class SampledSoftmaxHead(SoftmaxHead):
     state_dict keys as SoftmaxHead; Adam stays dense (rows the step did not
     touch see g = 0, as torch.optim.Adam would)."""
 
-    def __init__(self, name, A, HF, device, n_neg, seed=0):
+    LOSSES = ("ce", "bpr")
+
+    def __init__(self, name, A, HF, device, n_neg, seed=0, loss="ce"):
         if HF % 32 or HF > 256:
             raise ValueError(f"sampled softmax needs head width in {{32, 64, 128, 256}}, got {HF}")
         if n_neg <= 0:
             raise ValueError("n_negatives must be positive")
+        if loss not in self.LOSSES:
+            raise ValueError(f"sampled loss must be one of {self.LOSSES}, got {loss!r}")
         super().__init__(name, A, HF, device)
+        # "ce": CE over [target ‖ negatives]; "bpr": mean_s −log σ(z_pos − z_neg_s)
+        self.loss = loss
         self.S = int(n_neg)
         self.seed = int(seed) & (2**64 - 1)
         self.draws = 0
@@ -841,10 +847,16 @@ class SampledSoftmaxHead(SoftmaxHead):
                      B, self.S, self.HF, w.ZT.data_ptr(), w.ldz, w.pmax.data_ptr(), w.psum.data_ptr(),
                      w.Wg.data_ptr(), w.bg.data_ptr(), st)
         self.draws += 1
-        call("rg_sampled_lse", h.data_ptr(), self.W.p.data_ptr(), self.b.p.data_ptr(), tgt.data_ptr(), B, self.A,
-             self.HF, w.pmax.data_ptr(), w.psum.data_ptr(), w.nT, g, w.lse.data_ptr(), w.loss_row.data_ptr(),
-             w.ids.data_ptr() + 4 * self.S, w.gb.data_ptr() + 4 * self.S,
-             w.grows.data_ptr() + 4 * self.S * self.HF, w.dh_slabs.data_ptr(), st)
+        if self.loss == "bpr":   # w.lse holds z_pos for the backward
+            call("rg_bpr_rows", h.data_ptr(), self.W.p.data_ptr(), self.b.p.data_ptr(), tgt.data_ptr(), B, self.A,
+                 self.HF, w.ZT.data_ptr(), w.zs_b, w.zs_s, self.S, g, w.lse.data_ptr(), w.loss_row.data_ptr(),
+                 w.ids.data_ptr() + 4 * self.S, w.gb.data_ptr() + 4 * self.S,
+                 w.grows.data_ptr() + 4 * self.S * self.HF, w.dh_slabs.data_ptr(), st)
+        else:
+            call("rg_sampled_lse", h.data_ptr(), self.W.p.data_ptr(), self.b.p.data_ptr(), tgt.data_ptr(), B,
+                 self.A, self.HF, w.pmax.data_ptr(), w.psum.data_ptr(), w.nT, g, w.lse.data_ptr(),
+                 w.loss_row.data_ptr(), w.ids.data_ptr() + 4 * self.S, w.gb.data_ptr() + 4 * self.S,
+                 w.grows.data_ptr() + 4 * self.S * self.HF, w.dh_slabs.data_ptr(), st)
         call("rg_sum_scale", w.loss_row.data_ptr(), B, g, w.loss.data_ptr(), None, st)
         return w.loss, w
 
@@ -857,7 +869,10 @@ class SampledSoftmaxHead(SoftmaxHead):
         if gscale is not None and gscale != g:
             raise NotImplementedError("sampled softmax: the loss scale is fixed at 1/B (set in forward_loss)")
         with region("sampled_bwd"):
-            if w.zrow:
+            if self.loss == "bpr":
+                call("rg_bpr_dz", w.ZT.data_ptr(), w.zs_b, w.zs_s, w.lse.data_ptr(), B, S, g, w.dbslabs.data_ptr(),
+                     w.gb.data_ptr(), st)
+            elif w.zrow:
                 call("rg_sampled_dz_rows", w.ZT.data_ptr(), w.ldz, w.lse.data_ptr(), B, S, g, w.dbslabs.data_ptr(),
                      w.gb.data_ptr(), st)
             else:

@@ -22,7 +22,7 @@ class HipNet:
 
     def __init__(self, *, trunk_attr, head_names, hidden_dim, embedding_dim, item_num, state_size, action_dim,
                  gru_layers, use_packed_seq, train_pad_embed, padding_idx, bidir, device, dropout=0.0,
-                 comm=None, n_negatives=None, neg_seed=0, fp16_embeddings=False):
+                 comm=None, n_negatives=None, neg_seed=0, fp16_embeddings=False, sampled_loss="ce"):
         self.hidden_dim = hidden_dim
         self.embedding_dim = embedding_dim
         self.item_num = int(item_num)
@@ -51,7 +51,7 @@ class HipNet:
             if comm is not None:
                 raise NotImplementedError("sampled softmax with item sharding")
             self.heads = OrderedDict((n, SampledSoftmaxHead(n, action_dim, self.hf, self.device, n_negatives,
-                                                            neg_seed)) for n in head_names)
+                                                            neg_seed, loss=sampled_loss)) for n in head_names)
         else:
             self.heads = OrderedDict((n, SoftmaxHead(n, action_dim, self.hf, self.device, shard=shard))
                                      for n in head_names)

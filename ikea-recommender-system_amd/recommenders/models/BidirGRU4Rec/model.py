@@ -21,20 +21,20 @@ from recommenders.models.GRU4Rec.model import _AdamFacade
 class BidirGRU4Rec(SupervisedNet):
     def __init__(self, hidden_size, embedding_dim, item_num, state_size, action_dim, gru_layers=1, dropout=0,
                  use_packed_seq=True, train_pad_embed=True, padding_idx=None, device="cuda", n_negatives=None,
-                 neg_seed=0, fp16_embeddings=False):
+                 neg_seed=0, fp16_embeddings=False, sampled_loss="ce"):
         super().__init__(trunk_attr="gru", head_names=["output"], hidden_dim=hidden_size,
                          embedding_dim=embedding_dim, item_num=item_num, state_size=state_size,
                          action_dim=action_dim, gru_layers=gru_layers, use_packed_seq=use_packed_seq,
                          train_pad_embed=train_pad_embed, padding_idx=padding_idx, bidir=True, device=device,
                          dropout=dropout, n_negatives=n_negatives, neg_seed=neg_seed,
-                         fp16_embeddings=fp16_embeddings)
+                         fp16_embeddings=fp16_embeddings, sampled_loss=sampled_loss)
 
 
 class BidirGRU4Rec_trainer:
     def __init__(self, hidden_dim, embedding_dim, gru_layers, dropout, train_pad_embed, use_packed_seq,
                  learning_rate, item_num, state_size, action_dim, device, padding_idx=None, torch_rand_seed=118,
                  python_rand_seed=999, n_negatives=None, neg_seed=0, fp16_embeddings=False,
-                 matmul_precision="f32"):
+                 matmul_precision="f32", sampled_loss="ce"):
         torch.manual_seed(torch_rand_seed)
         random.seed(python_rand_seed)
         self.device = require_gpu(device)
@@ -43,7 +43,7 @@ class BidirGRU4Rec_trainer:
                                       dropout=dropout, use_packed_seq=use_packed_seq,
                                       train_pad_embed=train_pad_embed, padding_idx=padding_idx,
                                       device=self.device, n_negatives=n_negatives, neg_seed=neg_seed,
-                                      fp16_embeddings=fp16_embeddings)
+                                      fp16_embeddings=fp16_embeddings, sampled_loss=sampled_loss)
         self.gru_model.set_matmul_precision(matmul_precision)
         self.learning_rate = learning_rate
         self.cross_entropy_loss = nn.CrossEntropyLoss(weight=None, reduction="mean")

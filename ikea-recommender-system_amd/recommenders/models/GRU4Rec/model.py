@@ -23,12 +23,13 @@ class GRU4Rec(SupervisedNet):
 
     def __init__(self, hidden_size, embedding_dim, item_num, state_size, action_dim, gru_layers=1,
                  use_packed_seq=True, train_pad_embed=True, padding_idx=None, device="cuda", comm=None,
-                 n_negatives=None, neg_seed=0, fp16_embeddings=False):
+                 n_negatives=None, neg_seed=0, fp16_embeddings=False, sampled_loss="ce"):
         super().__init__(trunk_attr="gru", head_names=["output"], hidden_dim=hidden_size,
                          embedding_dim=embedding_dim, item_num=item_num, state_size=state_size,
                          action_dim=action_dim, gru_layers=gru_layers, use_packed_seq=use_packed_seq,
                          train_pad_embed=train_pad_embed, padding_idx=padding_idx, bidir=False, device=device,
-                         comm=comm, n_negatives=n_negatives, neg_seed=neg_seed, fp16_embeddings=fp16_embeddings)
+                         comm=comm, n_negatives=n_negatives, neg_seed=neg_seed, fp16_embeddings=fp16_embeddings,
+                         sampled_loss=sampled_loss)
 
 
 class _AdamFacade:
@@ -104,7 +105,7 @@ class GRU4Rec_trainer:
     def __init__(self, hidden_dim, embedding_dim, gru_layers, train_pad_embed, use_packed_seq, learning_rate,
                  item_num, state_size, action_dim, device, padding_idx=None, torch_rand_seed=118,
                  python_rand_seed=999, shard_items=False, process_group=None, n_negatives=None, neg_seed=0,
-                 fp16_embeddings=False, matmul_precision="f32"):
+                 fp16_embeddings=False, matmul_precision="f32", sampled_loss="ce"):
         torch.manual_seed(torch_rand_seed)
         random.seed(python_rand_seed)
         self.device = require_gpu(device)
@@ -114,14 +115,16 @@ class GRU4Rec_trainer:
         self.comm = Comm(process_group) if shard_items else None
         # n_negatives (build extension, off by default): sampled softmax over the
         # target and n_negatives shared uniform negatives instead of the full
-        # softmax (config C3; recommenders/hip/engine.py:SampledSoftmaxHead).
+        # softmax (config C3; recommenders/hip/engine.py:SampledSoftmaxHead);
+        # sampled_loss "bpr" trains the same logits with the pairwise BPR loss.
         # fp16_embeddings (build extension, off by default): the gather reads an
         # fp16 copy of the item table, Adam keeps the fp32 master (config C5).
         self.gru_model = GRU4Rec(hidden_size=hidden_dim, embedding_dim=embedding_dim, item_num=item_num,
                                  state_size=state_size, action_dim=action_dim, gru_layers=gru_layers,
                                  use_packed_seq=use_packed_seq, train_pad_embed=train_pad_embed,
                                  padding_idx=padding_idx, device=self.device, comm=self.comm,
-                                 n_negatives=n_negatives, neg_seed=neg_seed, fp16_embeddings=fp16_embeddings)
+                                 n_negatives=n_negatives, neg_seed=neg_seed, fp16_embeddings=fp16_embeddings,
+                                 sampled_loss=sampled_loss)
         # matmul_precision (build extension): "f32" (default, native fp32 MFMA)
         # or the split-bf16 "f32x9" / "f32x6" head GEMMs (hip/engine.py)
         self.gru_model.set_matmul_precision(matmul_precision)

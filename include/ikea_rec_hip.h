@@ -353,6 +353,18 @@ int rg_sampled_lse(const float* h, const float* W, const float* bias, const int6
 /* in place dZᵀ = exp(Zᵀ − lse)·g; dbg[s] = Σ_b dZᵀ[s][b] */
 int rg_sampled_dz(float* ZT, int64_t ldz, const float* lse, int B, int S, float gscale, float* dbg,
                   rg_stream_t stream);
+/* Sampled BPR over the same logits (build-defined; north_star "sampled-softmax/BPR"; the
+ * reference's trainers have CE only, GRU4Rec/model.py:121):
+ * loss = mean_b (1/S) Σ_s softplus(z_b,s − z_b,pos).  Z(b, s) at Z[b·zsb + s·zss] (row-major Z of
+ * rg_sampled_logits: zsb = ldz, zss = 1; Zᵀ of rg_sampled_fwd(_x): zsb = 1, zss = ldz).
+ * rg_bpr_rows: per row zpos = h_b·W[a_b] + bias[a_b], loss_row (NaN for a target outside [0, A)),
+ * ids, dzpos = −g·Σ_s σ(z_s − zpos)/S, gpos = dzpos·h_b, dhpos = dzpos·W[a_b].
+ * rg_bpr_dz: in place dZ = g·σ(Z − zpos)/S; dbg[s] = Σ_b dZ(b, s) through ceil(B/128) × S slabs. */
+int rg_bpr_rows(const float* h, const float* W, const float* bias, const int64_t* tgt, int B, int64_t A, int HF,
+                const float* Z, int64_t zsb, int64_t zss, int S, float gscale, float* zpos, float* loss_row,
+                int32_t* ids, float* dzpos, float* gpos, float* dhpos, rg_stream_t stream);
+int rg_bpr_dz(float* Z, int64_t zsb, int64_t zss, const float* zpos, int B, int S, float gscale, float* slabs,
+              float* dbg, rg_stream_t stream);
 
 /* ---- §8e row-sharded item-embedding table (csrc/emb_shard.hip): the multi-GPU form of
  * self.embedding(s) and its dense gradient + Adam (GRU4Rec/model.py:35-47, 69, 150-153).  Rank r

@@ -155,6 +155,15 @@ def sampled_ce(h, weight, bias, a, neg):
     return F.cross_entropy(logits, torch.zeros(h.shape[0], dtype=torch.long))
 
 
+def sampled_bpr(h, weight, bias, a, neg):
+    """Sampled BPR (Rendle et al. 2009; build-defined, no reference counterpart):
+    mean_b (1/S) Σ_s −log σ(z_pos − z_neg_s) over the shared negatives
+    (duplicates and target collisions kept)."""
+    zpos = (h * weight[a]).sum(1) + bias[a]
+    zneg = h @ weight[neg].t() + bias[neg]
+    return -F.logsigmoid(zpos[:, None] - zneg).mean()
+
+
 class OracleSupervised:
     """GRU4Rec / BidirGRU4Rec trainer restatement (``GRU4Rec/model.py:86-155``).
     ``n_negatives``: the build-defined sampled softmax (config C3)."""
@@ -162,9 +171,10 @@ class OracleSupervised:
     def __init__(self, kind, hidden_dim, embedding_dim, gru_layers, train_pad_embed,
                  use_packed_seq, learning_rate, item_num, state_size, action_dim,
                  dropout=0.0, padding_idx=None, torch_rand_seed=118, python_rand_seed=999,
-                 n_negatives=None, neg_seed=0, fp16_embeddings=False):
+                 n_negatives=None, neg_seed=0, fp16_embeddings=False, sampled_loss="ce"):
         torch.manual_seed(torch_rand_seed)
         random.seed(python_rand_seed)
+        self.sampled_loss = {"ce": sampled_ce, "bpr": sampled_bpr}[sampled_loss]
         self.net = Net(kind, item_num, action_dim, embedding_dim, hidden_dim, gru_layers,
                        train_pad_embed, use_packed_seq, padding_idx, dropout, emb_fp16=fp16_embeddings)
         self.opt = make_adam(self.net, learning_rate)
@@ -176,7 +186,7 @@ class OracleSupervised:
                                                   self.net.action_dim))
             self.draws += 1
             head = getattr(self.net, self.net.head_names[0])
-            loss = sampled_ce(self.net.hidden(s, true_len), head.weight, head.bias, a, neg)
+            loss = self.sampled_loss(self.net.hidden(s, true_len), head.weight, head.bias, a, neg)
         else:
             preds = self.net(s, true_len)
             loss = F.cross_entropy(preds, a)  # CrossEntropyLoss(reduction="mean")

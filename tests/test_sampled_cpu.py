@@ -49,3 +49,23 @@ def test_sampled_ce_matches_explicit_formula():
         m = max(zs)
         tot += m + np.log(sum(np.exp(z - m) for z in zs)) - zs[0]
     assert abs(got - tot / B) < 1e-12
+
+
+def test_oracle_bpr_matches_pairwise_formula():
+    """oracle.sampled_bpr against the BPR definition written out in float64
+    numpy: mean over rows and negatives of log(1 + exp(z_neg - z_pos))."""
+    import torch
+    from oracle.models import sampled_bpr
+    g = torch.Generator().manual_seed(3)
+    B, S, A, H = 17, 40, 90, 8
+    h = torch.randn(B, H, generator=g, dtype=torch.float64)
+    W = torch.randn(A, H, generator=g, dtype=torch.float64)
+    b = torch.randn(A, generator=g, dtype=torch.float64)
+    a = torch.randint(0, A, (B,), generator=g)
+    neg = torch.randint(0, A, (S,), generator=g)
+    got = float(sampled_bpr(h, W, b, a, neg))
+    hn, Wn, bn = h.numpy(), W.numpy(), b.numpy()
+    zp = (hn * Wn[a.numpy()]).sum(1) + bn[a.numpy()]
+    zn = hn @ Wn[neg.numpy()].T + bn[neg.numpy()]
+    want = np.log1p(np.exp(zn - zp[:, None])).mean()
+    assert abs(got - want) < 1e-12
