@@ -96,6 +96,26 @@ def test_gemm_layouts(M, N, K, splits):
             torch.testing.assert_close(out.sum(0).cpu(), ref, rtol=1e-5, atol=1e-4 * max(1.0, K / 1000))
 
 
+@pytest.mark.parametrize("M,N,K", [(85003, 384, 128), (300, 128, 384), (129, 768, 256), (7, 256, 32), (4100, 60, 64)])
+def test_gemm_large_tile_path(M, N, K):
+    """k_gemm_nt (rg_gemm_f32 with A k-contiguous, no split-K, K % 32 == 0):
+    both B layouts, bias, the row count read from the device (grid sized
+    for more rows than exist), partial M / N tiles, against fp64."""
+    g = torch.Generator().manual_seed(4)
+    A = torch.randn(M, K, generator=g)
+    W = torch.randn(N, K, generator=g) * 0.1
+    bias = torch.randn(N, generator=g)
+    ref = (A.double() @ W.double().t() + bias.double()).float()
+    Ad, bd = A.to(dev), bias.to(dev)
+    Mdev = torch.tensor([M], dtype=torch.int32, device=dev)
+    for Bd, sbk, sbn in ((W.to(dev), 1, K), (W.t().contiguous().to(dev), N, 1)):
+        out = torch.full((M + 5, N), float("nan"), device=dev)
+        C().call("rg_gemm_f32", Ad.data_ptr(), K, 1, Bd.data_ptr(), sbk, sbn, out.data_ptr(), N, bd.data_ptr(),
+                 M + 200, Mdev.data_ptr(), N, K, None, 1, st())
+        torch.testing.assert_close(out[:M].cpu(), ref, rtol=1e-5, atol=1e-4 * max(1.0, K / 1000))
+        assert torch.isnan(out[M:]).all()   # rows past the device-side count untouched
+
+
 def gru_ref(X_rows, lens, perm_order, Wih, Whh, bih, bhh, H):
     """fp64 GRU over each (unsorted) row; returns final h per original row and saved states."""
     hs = {}
@@ -257,6 +277,34 @@ def test_adam_kernels_match_torch():
                  rows, cols, clock.next_args(), st())
     torch.testing.assert_close(P.cpu(), pt.detach(), rtol=0, atol=2e-6)
     assert float(G.abs().max()) == 0.0
+
+
+@pytest.mark.parametrize("n,nslab", [(49152, 128), (384, 128), (1000, 7), (33, 1)])
+def test_adam_slabs_match_torch(n, nslab):
+    """Split-K slab reduction + Adam (the GRU weights' update): gradient = Σ
+    slabs (fp64 reference), the step as torch.optim.Adam; g_out mode returns
+    the reduced gradient; two launches are bitwise identical."""
+    from recommenders.hip.engine import AdamClock
+    g = torch.Generator().manual_seed(9)
+    p0 = torch.randn(n, generator=g)
+    slabs = [torch.randn(nslab, n, generator=g) * 0.1 for _ in range(2)]
+    pt = p0.clone().requires_grad_(True)
+    opt = torch.optim.Adam([pt], lr=0.01)
+    P, M, V = p0.to(dev), torch.zeros(n, device=dev), torch.zeros(n, device=dev)
+    clock = AdamClock(0.01)
+    for i in range(2):
+        pt.grad = slabs[i].double().sum(0).float()
+        opt.step()
+        C().call("rg_adam_slabs", P.data_ptr(), M.data_ptr(), V.data_ptr(), D(slabs[i]).data_ptr(), nslab, n,
+                 clock.next_args(), None, st())
+    torch.testing.assert_close(P.cpu(), pt.detach(), rtol=0, atol=2e-6)
+    out = [torch.empty(n, device=dev) for _ in range(2)]
+    sd = D(slabs[0])
+    for o in out:
+        C().call("rg_adam_slabs", P.data_ptr(), M.data_ptr(), V.data_ptr(), sd.data_ptr(), nslab, n, None,
+                 o.data_ptr(), st())
+    torch.testing.assert_close(out[0].cpu().double(), slabs[0].double().sum(0), rtol=0, atol=1e-5)
+    assert torch.equal(out[0], out[1])
 
 
 def test_q_kernels_and_rewards():
