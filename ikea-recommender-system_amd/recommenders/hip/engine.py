@@ -546,14 +546,39 @@ class SoftmaxHead:
             w, b = w[self.lo:self.hi].contiguous(), b[self.lo:self.hi].contiguous()
         self.name, self.A, self.HF, self.device = name, self.hi - self.lo, HF, device
         self.precision = "f32"  # see set_matmul_precision
-        self.W = Param(f"{name}.weight", w, device)
-        self.b = Param(f"{name}.bias", b, device)
+        self._Wp = Param(f"{name}.weight", w, device)
+        self._bp = Param(f"{name}.bias", b, device)
+        self._joined = True
         self._ws = {}
         self._fws = {}
         # entries of the row top-k a caller reads after forward_loss (SMORL's
         # rewards, ``top_entries``); the fused head computes them in pass 1
         self.top_k = 0
         self.top_err = torch.zeros(1, dtype=torch.int32, device=device)
+
+    # W / b (and their Adam moments) are only reachable through these
+    # properties, which first order the current stream after an overlapped
+    # pass 2 still running on the side stream (backward_step(overlap=True)):
+    # nothing can read or write the parameters before their update lands.
+    @property
+    def W(self):
+        self.join()
+        return self._Wp
+
+    @W.setter
+    def W(self, v):
+        self.join()
+        self._Wp = v
+
+    @property
+    def b(self):
+        self.join()
+        return self._bp
+
+    @b.setter
+    def b(self, v):
+        self.join()
+        self._bp = v
 
     def named_params(self):
         return [self.W, self.b]
@@ -570,6 +595,7 @@ class SoftmaxHead:
         return SPLIT_TERMS[self.precision]
 
     def fws(self, slot, B):
+        self.join()   # the workspace's h planes / row records are pass 2's inputs
         w = self._fws.get(slot)
         if w is None or w.B != B or w.top_k != self.top_k:
             self._fws.pop(slot, None)
@@ -642,12 +668,19 @@ class SoftmaxHead:
             call("rg_flash_dh", w.pm.data_ptr(), w.pO.data_ptr(), w.rows.data_ptr(), w.nsplit, self.W.p.data_ptr(), g,
                  w.B, self.HF, dh_out.data_ptr(), st)
 
+    def join(self):
+        """Order the current stream after an overlapped pass 2 (backward_step(overlap=True))."""
+        if not self._joined:
+            self._joined = True
+            torch.cuda.current_stream(self.device).wait_stream(self._side)
+
     def flash_dw_adam(self, w, g, adam6):
         """Pass 2: dW, db and the Adam step of W / b (after flash_dh)."""
+        Wp, bp = self._Wp, self._bp   # not the joining properties: this may run on the side stream
         with region("head_dw_adam"):
             call("rg_flash_dw_adam", w.Hk.data_ptr(), w.Hr.data_ptr(), w.Wk.data_ptr(), w.bias_pad.data_ptr(),
-                 w.rows.data_ptr(), g, w.B, self.A, self.HF, w.terms, self.W.p.data_ptr(), self.W.m.data_ptr(),
-                 self.W.v.data_ptr(), self.b.p.data_ptr(), self.b.m.data_ptr(), self.b.v.data_ptr(), adam6, None,
+                 w.rows.data_ptr(), g, w.B, self.A, self.HF, w.terms, Wp.p.data_ptr(), Wp.m.data_ptr(),
+                 Wp.v.data_ptr(), bp.p.data_ptr(), bp.m.data_ptr(), bp.v.data_ptr(), adam6, None,
                  None, stream_ptr())
 
     def ws(self, slot, B, store_z):
@@ -689,14 +722,26 @@ class SoftmaxHead:
         call("rg_sum_scale", w.loss_row.data_ptr(), B, _f32(1.0 / B), w.loss.data_ptr(), None, st)
         return w.loss, w
 
-    def backward_step(self, h, tgt, dh_out, adam6, slot="main", gscale=None):
-        """dh_out (B, HF) := ∂loss/∂h (overwrites); then the fused dW/db + Adam."""
+    def backward_step(self, h, tgt, dh_out, adam6, slot="main", gscale=None, overlap=False):
+        """dh_out (B, HF) := ∂loss/∂h (overwrites); then the fused dW/db + Adam.
+        overlap (fused head): pass 2 runs on a side stream, so the caller's
+        trunk backward (which needs only dh) fills the CUs pass 2's last,
+        partial round of workgroups leaves idle; the caller must ``join()``
+        before anything reads W / b again."""
         B = h.shape[0]
         g = _f32(1.0 / B) if gscale is None else gscale
         if self.flash_terms(B):
             w = self.fws(slot, B)
             self.flash_dh(w, tgt, w.lse, g, dh_out)
-            self.flash_dw_adam(w, g, adam6)
+            if overlap:   # joined lazily: by the next access of W / b or of the workspace
+                if getattr(self, "_side", None) is None:
+                    self._side = torch.cuda.Stream(device=self.device)
+                self._side.wait_stream(torch.cuda.current_stream())
+                with torch.cuda.stream(self._side):
+                    self.flash_dw_adam(w, g, adam6)
+                self._joined = False
+            else:
+                self.flash_dw_adam(w, g, adam6)
             return
         w = self.ws(slot, B, True)
         st = stream_ptr()
@@ -860,8 +905,8 @@ class SampledSoftmaxHead(SoftmaxHead):
         call("rg_sum_scale", w.loss_row.data_ptr(), B, g, w.loss.data_ptr(), None, st)
         return w.loss, w
 
-    def backward_step(self, h, tgt, dh_out, adam6, slot="main", gscale=None):
-        B = h.shape[0]
+    def backward_step(self, h, tgt, dh_out, adam6, slot="main", gscale=None, overlap=False):
+        B = h.shape[0]   # (overlap: no side-stream pass here; the sampled backward is short)
         w = self.sws(slot, B)
         st = stream_ptr()
         S, HF = self.S, self.HF

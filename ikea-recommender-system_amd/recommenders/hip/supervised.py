@@ -8,6 +8,8 @@ body of GRU4Rec_trainer and BidirGRU4Rec_trainer
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from .nets import HipNet
@@ -24,6 +26,10 @@ class SupervisedNet(HipNet):
         head = next(iter(self.heads.values()))
         _, z = head.logits_T(h, slot="eval")
         return z
+
+
+# RG_OVERLAP_HEAD_DW=0 keeps pass 2 on the launch stream (A/B measurement)
+OVERLAP_HEAD_DW = os.environ.get("RG_OVERLAP_HEAD_DW", "1") != "0"
 
 
 def supervised_step(net: SupervisedNet, clock, s, a, true_len):
@@ -48,7 +54,10 @@ def supervised_step(net: SupervisedNet, clock, s, a, true_len):
     adam6 = clock.next_args()
     net.trunk_tag = getattr(net, "trunk_tag", 0) + 1
     dh = net.dh_buffer(B)
-    head.backward_step(h_in, a, dh, adam6, slot="main")
+    # the head's pass 2 (dW + Adam) runs on a side stream under the trunk
+    # backward (which needs only dh) and the next step's trunk forward; the
+    # head joins it on the next access of its parameters or workspace
+    head.backward_step(h_in, a, dh, adam6, slot="main", overlap=OVERLAP_HEAD_DW)
     if mask is not None:
         net.apply_mask(dh, mask, dh)
     net.trunk.backward(dh, slot="main")
