@@ -670,9 +670,19 @@ class SoftmaxHead:
 
     def join(self):
         """Order the current stream after an overlapped pass 2 (backward_step(overlap=True))."""
-        if not self._joined:
+        if not getattr(self, "_joined", True):   # (heads built with __new__ never overlap)
             self._joined = True
             torch.cuda.current_stream(self.device).wait_stream(self._side)
+
+    def flash_dw_adam_async(self, w, g, adam6):
+        """Pass 2 on this head's side stream, ordered after everything issued so
+        far; the head joins it on the next access of W / b or its workspace."""
+        if getattr(self, "_side", None) is None:
+            self._side = torch.cuda.Stream(device=self.device)
+        self._side.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(self._side):
+            self.flash_dw_adam(w, g, adam6)
+        self._joined = False
 
     def flash_dw_adam(self, w, g, adam6):
         """Pass 2: dW, db and the Adam step of W / b (after flash_dh)."""
@@ -734,12 +744,7 @@ class SoftmaxHead:
             w = self.fws(slot, B)
             self.flash_dh(w, tgt, w.lse, g, dh_out)
             if overlap:   # joined lazily: by the next access of W / b or of the workspace
-                if getattr(self, "_side", None) is None:
-                    self._side = torch.cuda.Stream(device=self.device)
-                self._side.wait_stream(torch.cuda.current_stream())
-                with torch.cuda.stream(self._side):
-                    self.flash_dw_adam(w, g, adam6)
-                self._joined = False
+                self.flash_dw_adam_async(w, g, adam6)
             else:
                 self.flash_dw_adam(w, g, adam6)
             return

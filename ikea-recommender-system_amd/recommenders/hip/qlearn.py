@@ -131,6 +131,9 @@ def _dev(x, dev, dtype=None):
     return x if dtype is None else x.to(dtype)
 
 
+from .supervised import OVERLAP_HEAD_DW  # noqa: E402
+
+
 def double_q_step(nets, clocks, k, s, a, r, s_next, true_len, true_next_len, is_end, *, gamma, smorl=None):
     """One SQN (smorl=None) or SMORL step with main = nets[k].  Returns device
     (sup_loss (1,) f32, q_loss (1,) f64 for SQN / f32 for SMORL)."""
@@ -173,7 +176,8 @@ def double_q_step(nets, clocks, k, s, a, r, s_next, true_len, true_next_len, is_
     main.trunk_tag = getattr(main, "trunk_tag", 0) + 1
     tag = main.trunk_tag
     dh = main.dh_buffer(B)
-    main.sup_head_output.backward_step(h, a, dh, adam6, slot="main")
+    # the supervised head's pass 2 overlaps the Q heads' backward / Adam and the trunk
+    main.sup_head_output.backward_step(h, a, dh, adam6, slot="main", overlap=OVERLAP_HEAD_DW)
     call("rg_q_backward", h.data_ptr(), main.hf, host_ptr_array([x.W.p for x in main.q_heads]),
          host_ptr_array([x.G for x in main.q_heads]), host_ptr_array([x.Gb for x in main.q_heads]),
          host_ptr_array([x.tags for x in main.q_heads]), nh, a.data_ptr(), B, dq.data_ptr(), dh.data_ptr(), tag, st)

@@ -90,6 +90,9 @@ def _sharded_ce_dh(net, head, w, lse, tgt_loc, dH_all, st):
     call("rg_reduce_slabs", w.dh_slabs.data_ptr(), n, Bg * net.hf, dH_all.data_ptr(), None, net.hf, 0, st)
 
 
+from .supervised import OVERLAP_HEAD_DW  # noqa: E402
+
+
 def _sharded_ce_dw_adam(net, head, w, lse, tgt_loc, H_all, adam6, st):
     Bg = H_all.shape[0]
     if getattr(w, "terms", 0):
@@ -132,6 +135,9 @@ def sharded_supervised_step(net, clock, s, a, true_len):
     net.trunk_tag = getattr(net, "trunk_tag", 0) + 1
     dH_all = _buf(net, "dH_all", (Bg, HF))
     _sharded_ce_dh(net, head, w, lse, tgt_loc, dH_all, st)
+    fused = bool(getattr(w, "terms", 0)) and OVERLAP_HEAD_DW
+    if fused:   # pass 2 on the head's side stream under the exchanges and the trunk backward
+        head.flash_dw_adam_async(w, _f32(1.0 / Bg), adam6)
     dh = net.dh_buffer(B)
     with region("comm_dh"):
         comm.reduce_scatter(dh, dH_all)
@@ -140,7 +146,8 @@ def sharded_supervised_step(net, clock, s, a, true_len):
     net.trunk.backward(dh, slot="main")
     net.trunk.grads_for_allreduce(net.trunk_tag)
     works = net.trunk.allreduce_start(comm)
-    _sharded_ce_dw_adam(net, head, w, lse, tgt_loc, H_all, adam6, st)
+    if not fused:
+        _sharded_ce_dw_adam(net, head, w, lse, tgt_loc, H_all, adam6, st)
     with region("comm_wait"):
         for wk in works:
             if wk is not None:
@@ -280,6 +287,9 @@ def sharded_double_q_step(nets, clocks, k, s, a, r, s_next, true_len, true_next_
     tag = main.trunk_tag
     dH_all = _buf(main, "dH_all", (Bg, HF))
     _sharded_ce_dh(main, sup, w, lse, tgt_loc, dH_all, st)
+    fused = bool(getattr(w, "terms", 0)) and OVERLAP_HEAD_DW
+    if fused:   # pass 2 on the supervised head's side stream under the rest of the step
+        sup.flash_dw_adam_async(w, _f32(1.0 / Bg), adam6)
     dq_all = _gather_rows(comm, main, "dq_all", dq)
     call("rg_q_backward", H_all.data_ptr(), HF, host_ptr_array([x.W.p for x in main.q_heads]),
          host_ptr_array([x.G for x in main.q_heads]), host_ptr_array([x.Gb for x in main.q_heads]),
@@ -291,7 +301,8 @@ def sharded_double_q_step(nets, clocks, k, s, a, r, s_next, true_len, true_next_
     main.trunk.backward(dh, slot="main")
     main.trunk.grads_for_allreduce(tag)
     works = main.trunk.allreduce_start(comm)
-    _sharded_ce_dw_adam(main, sup, w, lse, tgt_loc, H_all, adam6, st)
+    if not fused:
+        _sharded_ce_dw_adam(main, sup, w, lse, tgt_loc, H_all, adam6, st)
     for qh in main.q_heads:
         qh.adam(adam6, tag)
     with region("comm_wait"):
