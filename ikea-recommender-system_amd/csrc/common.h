@@ -89,6 +89,11 @@ __device__ __forceinline__ void adam_elem(float& p, float& m, float& v, float g,
 // |a2·b2| ≤ 2^-32·|ab|: below fp32's unit roundoff per product).
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
+// `terms` code of the fused head (rg_flash_*) beyond 6 / 9 (every
+// contraction at that many plane products): precision "f32x6d3" — the logits
+// (S = W·hᵀ, both passes) and dW at 6 products, pass 1's O = P·W (→ dh) at 3
+#define RG_TERMS_X6D3 636
+
 __device__ __forceinline__ f16v mfma32bf(bf16x8 a, bf16x8 b, f16v c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
 }
@@ -108,11 +113,18 @@ __device__ __forceinline__ void split3x8(const f4& lo, const f4& hi, bf16x8& p0,
   }
 }
 
-// acc += Σ_terms a_p · b_q over one 16-wide k slice (NT = 6 or 9 terms),
-// smallest terms first
+// acc += Σ_terms a_p · b_q over one 16-wide k slice (NT = 9, 6 or 3 terms),
+// smallest terms first.  NT = 3 keeps a0·b0, a0·b1, a1·b0 (dropped terms
+// ≤ 3·2^-18·|ab|); only the fused head's O = P·W contraction (→ dh) uses it
+// (precision "f32x6d3", RG_TERMS_X6D3), never logits or dW.
 template <int NT>
 __device__ __forceinline__ f16v mfma_split(const bf16x8& a0, const bf16x8& a1, const bf16x8& a2, const bf16x8& b0,
                                            const bf16x8& b1, const bf16x8& b2, f16v acc) {
+  if (NT == 3) {
+    acc = mfma32bf(a0, b1, acc);
+    acc = mfma32bf(a1, b0, acc);
+    return mfma32bf(a0, b0, acc);
+  }
   if (NT == 9) {
     acc = mfma32bf(a2, b2, acc);
     acc = mfma32bf(a1, b2, acc);

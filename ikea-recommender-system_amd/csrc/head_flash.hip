@@ -76,13 +76,15 @@ __device__ __forceinline__ void blds16(__amdgpu_buffer_rsrc_t r, void* lds_wave_
 
 // copy E 16-B entries (E % 64 == 0) from global to LDS, sliced over NW waves
 // (w wave-uniform, lane16 = 16·lane)
-template <int E, int NW>
+// (P2 = false: the third plane of every [p < 3][lane] group is not copied —
+// the 3-term gradient contractions never read it)
+template <int E, int NW, bool P2 = true>
 __device__ __forceinline__ void stage(const bf16x8* __restrict__ src, bf16x8* dst, int w, int lane16) {
   const __amdgpu_buffer_rsrc_t r = rsrc_of(src);
 #pragma unroll
   for (int q = 0; q < (E + 64 * NW - 1) / (64 * NW); ++q) {
     const int e0 = 64 * NW * q + 64 * w;  // wave-uniform
-    if (e0 < E) blds16(r, dst + e0, lane16, 16 * e0);
+    if (e0 < E && (P2 || (e0 >> 6) % 3 != 2)) blds16(r, dst + e0, lane16, 16 * e0);
   }
 }
 
@@ -149,7 +151,7 @@ __global__ void k_pad_bias(const float* __restrict__ bias, int A, int Ap, float*
 // after chunk c's O-MFMAs and lands under chunk c+1's S-MFMAs and softmax.
 // ARG: also the row's top-1 (value, item) per split and, with cmax, every
 // chunk's row maximum — the inputs of the fused top-k (SMORL's rewards).
-template <int HF, int NT, bool ARG>
+template <int HF, int NT, int NG, bool ARG>
 __global__ __launch_bounds__(64 * fl_nw(HF, 1)) void k_flash_fwd(
     const bf16x8* __restrict__ Hk, const bf16x8* __restrict__ Wk, const bf16x8* __restrict__ Wr,
     const float* __restrict__ bias_pad, int B, int A, int nrb, int nsplit, int cps, float* __restrict__ pm,
@@ -182,7 +184,7 @@ __global__ __launch_bounds__(64 * fl_nw(HF, 1)) void k_flash_fwd(
     stage<EK, NW>(Wk + (int64_t)(C) * EK, SK, w, lane16);                      \
     if (w == 0 && lane < 8) blds16(rsrc_of(bias_pad + 32 * (C)), SB, lane16, 0); \
   } while (0)
-#define FL_ISSUE_R(C, SR) stage<ER, NW>(Wr + (int64_t)(C) * ER, SR, w, lane16)
+#define FL_ISSUE_R(C, SR) stage<ER, NW, NG != 3>(Wr + (int64_t)(C) * ER, SR, w, lane16)
   if (nch > 0) {
     FL_ISSUE_K(c0, sk0, sb0);
     FL_ISSUE_R(c0, sr0);
@@ -285,7 +287,7 @@ __global__ __launch_bounds__(64 * fl_nw(HF, 1)) void k_flash_fwd(
       const int en = (ts + 1 < 2 * NTL ? ts + 1 : ts) * 192 + lane;
       const bf16x8 n0 = sr[en], n1 = sr[en + 64], n2 = sr[en + 128];
 #pragma unroll
-      for (int j = 0; j < RB; ++j) o[j][t] = mfma_split<NT>(a0, a1, a2, q0[j][s], q1[j][s], q2[j][s], o[j][t]);
+      for (int j = 0; j < RB; ++j) o[j][t] = mfma_split<NG>(a0, a1, a2, q0[j][s], q1[j][s], q2[j][s], o[j][t]);
       a0 = n0;
       a1 = n1;
       a2 = n2;
@@ -902,6 +904,7 @@ __global__ __launch_bounds__(256) void k_flash_topk_eval(const float* __restrict
 }
 
 inline bool flash_hf_ok(int HF) { return HF == 32 || HF == 64 || HF == 128 || HF == 256; }
+inline bool flash_terms_ok(int t) { return t == 6 || t == 9 || t == RG_TERMS_X6D3; }
 
 }  // namespace
 
@@ -942,7 +945,7 @@ extern "C" int rg_flash_fwd_top(const void* Hk, const void* Wk, const void* Wr, 
                                 int32_t* parg, float* cmax, hipStream_t stream) {
   if (B <= 0 || A <= 0 || (B % 32) || nsplit <= 0 || !Hk || !Wk || !Wr || !bias_pad || !pm || !pl || !pO)
     return RG_ERR_ARG;
-  if (terms != 6 && terms != 9) return RG_ERR_ARG;
+  if (!flash_terms_ok(terms)) return RG_ERR_ARG;
   if (!flash_hf_ok(HF)) return RG_ERR_SHAPE;
   const bool arg = pbest != nullptr;
   if (arg != (parg != nullptr) || (cmax && !arg)) return RG_ERR_ARG;
@@ -951,21 +954,23 @@ extern "C" int rg_flash_fwd_top(const void* Hk, const void* Wk, const void* Wr, 
   const int rpb = fl_rows(HF, 1);
   const int nrb = (B + rpb - 1) / rpb;
   const dim3 grid((unsigned)(nrb * nsplit));
-#define FF(HFV, NTV, ARGV)                                                                                   \
-  hipLaunchKernelGGL((k_flash_fwd<HFV, NTV, ARGV>), grid, dim3(64 * fl_nw(HFV, 1)), 0, stream,                \
+#define FF(HFV, NTV, NGV, ARGV)                                                                              \
+  hipLaunchKernelGGL((k_flash_fwd<HFV, NTV, NGV, ARGV>), grid, dim3(64 * fl_nw(HFV, 1)), 0, stream,                \
                      (const bf16x8*)Hk, (const bf16x8*)Wk, (const bf16x8*)Wr, bias_pad, B, A, nrb, nsplit, cps, pm, \
                      pl, pO, pbest, parg, cmax)
-#define FA(HFV, NTV)     \
-  if (arg) {             \
-    FF(HFV, NTV, true);  \
-  } else {               \
-    FF(HFV, NTV, false); \
+#define FA(HFV, NTV, NGV)     \
+  if (arg) {                  \
+    FF(HFV, NTV, NGV, true);  \
+  } else {                    \
+    FF(HFV, NTV, NGV, false); \
   }
-#define FT(HFV)          \
-  if (terms == 9) {      \
-    FA(HFV, 9);          \
-  } else {               \
-    FA(HFV, 6);          \
+#define FT(HFV)                        \
+  if (terms == 9) {                    \
+    FA(HFV, 9, 9);                     \
+  } else if (terms == RG_TERMS_X6D3) { \
+    FA(HFV, 6, 3);                     \
+  } else {                             \
+    FA(HFV, 6, 6);                     \
   }
   switch (HF) {
     case 32: FT(32); break;
@@ -989,6 +994,7 @@ extern "C" int rg_flash_fwd(const void* Hk, const void* Wk, const void* Wr, cons
 extern "C" int rg_flash_amax_fwd(const void* Hk, const void* Wk, const float* bias_pad, int B, int A, int HF,
                                  int terms, int nsplit, float* pbest, int32_t* parg, hipStream_t stream) {
   if (B <= 0 || A <= 0 || (B % 32) || nsplit <= 0 || !Hk || !Wk || !bias_pad || !pbest || !parg) return RG_ERR_ARG;
+  if (terms == RG_TERMS_X6D3) terms = 6;   // logits only
   if (terms != 6 && terms != 9) return RG_ERR_ARG;
   if (!flash_hf_ok(HF)) return RG_ERR_SHAPE;
   const int nct = (A + 31) / 32;
@@ -1076,7 +1082,7 @@ extern "C" int rg_flash_dw_adam(const void* Hk, const void* Hr, const void* Wk, 
                                 float* mW, float* vW, float* bias, float* mb, float* vb, const float* adam6,
                                 float* dW_out, float* db_out, hipStream_t stream) {
   if (B <= 0 || A <= 0 || (B % 32) || !Hk || !Hr || !Wk || !bias_pad || !rowinfo) return RG_ERR_ARG;
-  if (terms != 6 && terms != 9) return RG_ERR_ARG;
+  if (!flash_terms_ok(terms)) return RG_ERR_ARG;
   if (!flash_hf_ok(HF)) return RG_ERR_SHAPE;
   if (dW_out ? !db_out : (!adam6 || !W || !mW || !vW || !bias || !mb || !vb)) return RG_ERR_ARG;
   AdamArgs a{};

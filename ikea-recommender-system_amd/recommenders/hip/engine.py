@@ -523,12 +523,21 @@ class _AmaxWS:
 #   "f32x9" fp32 operands split exactly into three bf16 planes, all nine
 #           plane products on bf16 MFMAs (exact products, fp32 accumulation)
 #   "f32x6" the same without the three sub-ulp terms (csrc/common.h)
-SPLIT_TERMS = {"f32x9": 9, "f32x6": 6}
+#   "f32x6d3" logits at f32x6; the fused head's O = P·W contraction (→ dh)
+#           at the three leading plane products (its dh error stays at the
+#           reference CPU fp32 path's); dW and every other GEMM
+#           as f32x6
+# SPLIT_TERMS: the fused full-softmax head's `terms` code (csrc/common.h
+# RG_TERMS_*); LOGIT_TERMS: every logits-only split GEMM (sampled head, Q
+# argmax)
+SPLIT_TERMS = {"f32x9": 9, "f32x6": 6, "f32x6d3": 636}
+LOGIT_TERMS = {"f32x9": 9, "f32x6": 6, "f32x6d3": 6}
+PRECISIONS = ("f32",) + tuple(SPLIT_TERMS)
 
 
 def check_precision(precision):
-    if precision not in ("f32", "f32x9", "f32x6"):
-        raise ValueError(f"matmul_precision must be 'f32', 'f32x9' or 'f32x6', got {precision!r}")
+    if precision not in PRECISIONS:
+        raise ValueError(f"matmul_precision must be one of {PRECISIONS}, got {precision!r}")
     return precision
 
 
@@ -862,7 +871,7 @@ class SampledSoftmaxHead(SoftmaxHead):
         """bf16 terms of the forward for batch B (0: native fp32 MFMA)."""
         if self.precision == "f32" or B % 32 or self.S % 32:
             return 0
-        return SPLIT_TERMS[self.precision]
+        return LOGIT_TERMS[self.precision]
 
     def sws(self, slot, B):
         w = self._sws.get(slot)

@@ -119,8 +119,10 @@ int rg_head_fwd_x(const float* h, const float* W, const float* bias, int B, int 
 /* ---- A6/A7/A8 fused training head (csrc/head_flash.hip): the full-softmax
  * Linear + CrossEntropyLoss(mean) + Adam step of GRU4Rec/model.py:58-60, 80,
  * 121, 146, 149-153 without materialising the (B × A) logits, on split-bf16
- * MFMAs (terms 9: exact products, 6: sub-ulp terms dropped).  HF in {32, 64,
- * 128, 256}; B % 32 == 0.  Multi-GPU item shards pass their first item `lo` and
+ * MFMAs (terms 9: exact products, 6: sub-ulp terms dropped; 636 = precision
+ * "f32x6d3": logits at 6 products, pass 1's O = P·W (-> dh) at the 3 leading
+ * ones, dW at 6; rg_flash_amax_fwd reads it as its logits' 6).  HF in
+ * {32, 64, 128, 256}; B % 32 == 0.  Multi-GPU item shards pass their first item `lo` and
  * merge lse over ranks between rg_flash_lse and rg_flash_rows.
  * rg_head_plane_bytes: bytes of one operand-plane buffer for `rows` rows.
  * rg_head_planes: X (rows × HF) -> K-planes / R-planes (either optional);

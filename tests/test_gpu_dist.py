@@ -53,7 +53,7 @@ def _rank(rank, port, out, precision):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("precision", ["f32", "f32x6"])
+@pytest.mark.parametrize("precision", ["f32", "f32x6", "f32x6d3"])
 def test_item_sharded_step_equals_single_gpu_global_batch(precision):
     """f32x6: every rank runs the fused split-bf16 head on its item shard
     (recommenders/hip/sharded.py); compared with the single-GPU fused head."""

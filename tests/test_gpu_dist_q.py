@@ -78,11 +78,13 @@ def _rank(rank, port, out, kind, topk, extra):
 
 F16 = {"fp16_embeddings": True}
 X6 = {"matmul_precision": "f32x6"}
+X6D3 = {"matmul_precision": "f32x6d3"}
 
 
 @pytest.mark.parametrize("kind,topk,extra", [("sqn", None, {}), ("smorl", (1, 1), {}), ("smorl", (3, 2), {}),
                                              ("sqn", None, F16), ("smorl", (3, 2), F16),
-                                             ("smorl", (1, 1), {**F16, **X6}), ("smorl", (3, 2), {**F16, **X6})])
+                                             ("smorl", (1, 1), {**F16, **X6}), ("smorl", (3, 2), {**F16, **X6}),
+                                             ("sqn", None, X6D3), ("smorl", (3, 2), {**F16, **X6D3})])
 def test_item_sharded_double_q_equals_single_gpu_global_batch(kind, topk, extra):
     """Heads item-sharded and the item table row-sharded (ids / rows /
     row-gradients exchanged by all-to-all, csrc/emb_shard.hip); fp16 item

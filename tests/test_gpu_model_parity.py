@@ -1,7 +1,7 @@
 """Model-level parity of the evaluation metric (BASELINE metric "HR@20/NDCG@20
 parity"; north_star "bit-exact for top-k index lists").
 
-1. The HIP GRU4Rec_trainer (native f32 and fused split-bf16 f32x6 heads) and
+1. The HIP GRU4Rec_trainer (native f32, fused split-bf16 f32x6 / f32x6d3 heads) and
    the CPU oracle (the reference's PyTorch-CPU math, pinned to the reference's
    golden vectors) are trained side by side on the same synthetic stream at
    C2 widths (H 128, L 50, N 50k, B 1024).  Both trained models are then
@@ -40,7 +40,7 @@ def trained():
                learning_rate=LR, item_num=N, state_size=L, action_dim=N)
     torch.set_num_threads(8)
     orc = OracleSupervised(kind="gru4rec", **cfg)
-    hips = {p: GRU4Rec_trainer(device="cuda", matmul_precision=p, **cfg) for p in ("f32", "f32x6")}
+    hips = {p: GRU4Rec_trainer(device="cuda", matmul_precision=p, **cfg) for p in ("f32", "f32x6", "f32x6d3")}
     # held-out batches come from the same stream (same item popularity), after the training ones
     st = SessionStream(N, L, B * (STEPS + 2), seed=9)
     for i in range(STEPS):
@@ -53,7 +53,7 @@ def trained():
     return orc, hips, loader, unpopular_items(st.item_counts())
 
 
-@pytest.mark.parametrize("precision", ["f32", "f32x6"])
+@pytest.mark.parametrize("precision", ["f32", "f32x6", "f32x6d3"])
 def test_trained_model_top20_and_hr_ndcg_match_oracle(trained, precision):
     from recommenders.evaluate.eval_protocol import evaluate
     from recommenders.hip.evalpath import eval_batch
@@ -122,7 +122,7 @@ def _fp64_head(h, W, b, tgt, rows, chunk=131072):
     return lse, lse - zt, dh
 
 
-@pytest.mark.parametrize("precision", ["f32x6", "f32"])
+@pytest.mark.parametrize("precision", ["f32x6", "f32", "f32x6d3"])
 def test_full_c2_step_lse_ce_dh_against_fp64(precision):
     from recommenders.data_utils.synthetic import SessionStream
     from recommenders.models.GRU4Rec.model import GRU4Rec_trainer

@@ -90,7 +90,7 @@ def test_sqn_matches_oracle_medium(N, L, B, H):
         assert abs(so - sg) < 1e-4 and abs(qo - qg) < 1e-5, (i, so, sg, qo, qg)
 
 
-@pytest.mark.parametrize("precision", ["f32", "f32x6"])
+@pytest.mark.parametrize("precision", ["f32", "f32x6", "f32x6d3"])
 def test_smorl_c5_shape_matches_oracle(precision):
     """Config C5's model shape on one GPU, scaled down in items and batch:
     SMORL 3-reward at d256 (E = H = 256: the time-stepped GRU), fp16 item
