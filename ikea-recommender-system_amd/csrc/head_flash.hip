@@ -530,11 +530,10 @@ __global__ __launch_bounds__(256) void k_flash_dh(const float* __restrict__ pm, 
 // owns RB blocks of 32 items.
 template <int HF, int NT>
 __global__ __launch_bounds__(64 * fl_nw(HF, 2)) void k_flash_dw(
-    const bf16x8* __restrict__ Hk, const bf16x8* __restrict__ Hr, const bf16x8* __restrict__ Wk,
-    const float* __restrict__ bias_pad, const float2* __restrict__ rowinfo, float g, int B, int A,
-    float* __restrict__ W, float* __restrict__ mW, float* __restrict__ vW, float* __restrict__ bias,
-    float* __restrict__ mb, float* __restrict__ vb, AdamArgs args, float* __restrict__ dW_out,
-    float* __restrict__ db_out) {
+    const bf16x8* __restrict__ Hk, const bf16x8* __restrict__ Hr, const bf16x8* Wk, const float* bias_pad,
+    const float2* __restrict__ rowinfo, float g, int B, int A, float* __restrict__ W, float* __restrict__ mW,
+    float* __restrict__ vW, float* __restrict__ bias, float* __restrict__ mb, float* __restrict__ vb, AdamArgs args,
+    float* __restrict__ dW_out, float* __restrict__ db_out, bf16x8* Wk_out, bf16x8* Wr_out, float* bias_pad_out) {
   constexpr int NW = fl_nw(HF, 2), RB = fl_rb(HF, 2);
   constexpr bool DR = HF <= 128;
   constexpr int NS = HF / 16, NTL = HF / 32;
@@ -688,6 +687,25 @@ __global__ __launch_bounds__(64 * fl_nw(HF, 2)) void k_flash_dw(
   }
 #undef FL_ISSUE_K
 #undef FL_ISSUE_R
+  // Adam epilogue; with Wk_out / Wr_out (Adam mode) the updated rows also
+  // leave as the next pass 1's operand planes: the accumulator block of a
+  // (t, s) pair already is an R-plane entry (registers 8s..8s+7 = rows
+  // 16s + kperm(hh, i)), the K-planes go through a per-wave LDS transpose
+  // (32 items × 32 columns at a time, rows padded to 33 floats)
+  // (the ring arrays are idle after the main loop's last barrier; HF 32's are
+  // too small, so it has its own)
+  constexpr int TRP = 33, TRW = 32 * TRP;         // floats per wave
+  constexpr int WPA = EK * 16 / (TRW * 4);        // waves per ring array
+  __shared__ float trd[HF == 32 ? NW * TRW : 1];
+  float* tr;
+  if (HF == 32) {
+    tr = trd + w * TRW;
+  } else {
+    const int ai = w / WPA, ao = (w % WPA) * TRW;
+    bf16x8* base = ai == 0 ? sk0 : ai == 1 ? sk1 : ai == 2 ? sr0 : sr1;
+    tr = reinterpret_cast<float*>(base) + ao;
+  }
+  const bool planes = Wk_out != nullptr && dW_out == nullptr;
 #pragma unroll
   for (int j = 0; j < RB; ++j) {
     const int jb = j0 + 32 * j;
@@ -703,6 +721,7 @@ __global__ __launch_bounds__(64 * fl_nw(HF, 2)) void k_flash_dw(
         bias[item] = p;
         mb[item] = mq;
         vb[item] = v;
+        if (planes) bias_pad_out[item] = p;
       }
     }
 #pragma unroll
@@ -711,7 +730,10 @@ __global__ __launch_bounds__(64 * fl_nw(HF, 2)) void k_flash_dw(
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int it = jb + acc32_row(r, hh);
-        if (it >= A) continue;
+        if (it >= A) {
+          dw[j][t][r] = 0.f;   // rows past A: zero planes, as rg_head_planes writes them
+          continue;
+        }
         const int64_t o = (int64_t)it * HF + col;
         if (dW_out) {
           dW_out[o] = dw[j][t][r];
@@ -721,6 +743,36 @@ __global__ __launch_bounds__(64 * fl_nw(HF, 2)) void k_flash_dw(
           W[o] = p;
           mW[o] = mq;
           vW[o] = v;
+          dw[j][t][r] = p;
+        }
+      }
+      if (planes) {
+        const int64_t blk = jb >> 5;
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+          bf16x8 p0, p1, p2;
+          split3x8(f4{dw[j][t][8 * s2], dw[j][t][8 * s2 + 1], dw[j][t][8 * s2 + 2], dw[j][t][8 * s2 + 3]},
+                   f4{dw[j][t][8 * s2 + 4], dw[j][t][8 * s2 + 5], dw[j][t][8 * s2 + 6], dw[j][t][8 * s2 + 7]}, p0, p1,
+                   p2);
+          bf16x8* dst = Wr_out + ((blk * NTL + t) * 2 + s2) * 192 + lane;
+          dst[0] = p0;
+          dst[64] = p1;
+          dst[128] = p2;
+        }
+#pragma unroll
+        for (int r = 0; r < 16; ++r) tr[acc32_row(r, hh) * TRP + l32] = dw[j][t][r];
+        // (item, 8-column group) entries of these 32 columns: 32 items × 4 groups
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          const int e = lane + 64 * q, ii = e & 31, grp = e >> 5;
+          const float* src = tr + ii * TRP + 8 * grp;
+          bf16x8 p0, p1, p2;
+          split3x8(f4{src[0], src[1], src[2], src[3]}, f4{src[4], src[5], src[6], src[7]}, p0, p1, p2);
+          const int sk = 2 * t + (grp >> 1);
+          bf16x8* dst = Wk_out + (blk * NS + sk) * 192 + (grp & 1) * 32 + ii;
+          dst[0] = p0;
+          dst[64] = p1;
+          dst[128] = p2;
         }
       }
     }
@@ -1077,14 +1129,16 @@ extern "C" int rg_flash_dh(const float* pm, const float* pO, const void* rowinfo
   return RG_OK;
 }
 
-extern "C" int rg_flash_dw_adam(const void* Hk, const void* Hr, const void* Wk, const float* bias_pad,
-                                const void* rowinfo, float gscale, int B, int A, int HF, int terms, float* W,
-                                float* mW, float* vW, float* bias, float* mb, float* vb, const float* adam6,
-                                float* dW_out, float* db_out, hipStream_t stream) {
+extern "C" int rg_flash_dw_adam_planes(const void* Hk, const void* Hr, const void* Wk, const float* bias_pad,
+                                       const void* rowinfo, float gscale, int B, int A, int HF, int terms, float* W,
+                                       float* mW, float* vW, float* bias, float* mb, float* vb, const float* adam6,
+                                       float* dW_out, float* db_out, void* Wk_out, void* Wr_out, float* bias_pad_out,
+                                       hipStream_t stream) {
   if (B <= 0 || A <= 0 || (B % 32) || !Hk || !Hr || !Wk || !bias_pad || !rowinfo) return RG_ERR_ARG;
   if (!flash_terms_ok(terms)) return RG_ERR_ARG;
   if (!flash_hf_ok(HF)) return RG_ERR_SHAPE;
   if (dW_out ? !db_out : (!adam6 || !W || !mW || !vW || !bias || !mb || !vb)) return RG_ERR_ARG;
+  if ((Wk_out != nullptr) != (Wr_out != nullptr) || (Wk_out && (dW_out || !bias_pad_out))) return RG_ERR_ARG;
   AdamArgs a{};
   if (adam6) a = AdamArgs{adam6[0], adam6[1], adam6[2], adam6[3], adam6[4], adam6[5]};
   const int rpb = fl_rows(HF, 2);
@@ -1092,7 +1146,7 @@ extern "C" int rg_flash_dw_adam(const void* Hk, const void* Hr, const void* Wk, 
 #define FW(HFV, NTV)                                                                                          \
   hipLaunchKernelGGL((k_flash_dw<HFV, NTV>), grid, dim3(64 * fl_nw(HFV, 2)), 0, stream, (const bf16x8*)Hk, (const bf16x8*)Hr, \
                      (const bf16x8*)Wk, bias_pad, (const float2*)rowinfo, gscale, B, A, W, mW, vW, bias, mb, vb, \
-                     a, dW_out, db_out)
+                     a, dW_out, db_out, (bf16x8*)Wk_out, (bf16x8*)Wr_out, bias_pad_out)
 #define FT(HFV)          \
   if (terms == 9) {      \
     FW(HFV, 9);          \
@@ -1109,4 +1163,12 @@ extern "C" int rg_flash_dw_adam(const void* Hk, const void* Hr, const void* Wk, 
 #undef FW
   RG_LAUNCH_CHECK();
   return RG_OK;
+}
+
+extern "C" int rg_flash_dw_adam(const void* Hk, const void* Hr, const void* Wk, const float* bias_pad,
+                                const void* rowinfo, float gscale, int B, int A, int HF, int terms, float* W,
+                                float* mW, float* vW, float* bias, float* mb, float* vb, const float* adam6,
+                                float* dW_out, float* db_out, hipStream_t stream) {
+  return rg_flash_dw_adam_planes(Hk, Hr, Wk, bias_pad, rowinfo, gscale, B, A, HF, terms, W, mW, vW, bias, mb, vb, adam6,
+                                 dW_out, db_out, nullptr, nullptr, nullptr, stream);
 }

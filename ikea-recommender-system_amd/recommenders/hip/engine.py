@@ -19,6 +19,7 @@ LinearHead   a Linear(H→A) used only through row gathers / argmax (Q heads).
 from __future__ import annotations
 
 import math
+import os
 
 import numpy as np
 import torch
@@ -481,6 +482,7 @@ class _FlashWS:
         self.B, self.top_k = B, top_k
         self.terms = 0
         self.h = None
+        self.wgen = -1   # generation of the head's W / b its W planes hold (SoftmaxHead._wgen)
         nrb = -(-B // call("rg_flash_rows_per_block", HF))  # row blocks of pass 1
         # about one pass-1 workgroup per CU; a multiple of 8 for the XCD order
         self.nsplit = _round_up(min(max(1, 256 // nrb), -(-A // 32)), 8)
@@ -531,6 +533,8 @@ class _AmaxWS:
 # RG_TERMS_*); LOGIT_TERMS: every logits-only split GEMM (sampled head, Q
 # argmax)
 SPLIT_TERMS = {"f32x9": 9, "f32x6": 6, "f32x6d3": 636}
+# RG_PASS2_PLANES=0: pass 2 leaves W's operand planes to the next rg_head_planes (A/B measurement)
+PASS2_PLANES = os.environ.get("RG_PASS2_PLANES", "1") != "0"
 LOGIT_TERMS = {"f32x9": 9, "f32x6": 6, "f32x6d3": 6}
 PRECISIONS = ("f32",) + tuple(SPLIT_TERMS)
 
@@ -547,6 +551,8 @@ class SoftmaxHead:
     sharding); the full init is drawn first so every rank consumes the RNG
     exactly like the single-GPU (and reference) construction."""
 
+    _wgen = 0   # (class default: heads built with __new__, qlearn.py)
+
     def __init__(self, name, A, HF, device, shard=None):
         w, b = init_linear(HF, A)
         self.lo, self.hi = (0, A) if shard is None else shard
@@ -555,6 +561,10 @@ class SoftmaxHead:
             w, b = w[self.lo:self.hi].contiguous(), b[self.lo:self.hi].contiguous()
         self.name, self.A, self.HF, self.device = name, self.hi - self.lo, HF, device
         self.precision = "f32"  # see set_matmul_precision
+        # generation of W / b: bumped by every access through the W / b
+        # properties (any of them may write) and by the fused pass 2; a fused
+        # workspace's operand planes are current while its wgen matches
+        self._wgen = 0
         self._Wp = Param(f"{name}.weight", w, device)
         self._bp = Param(f"{name}.bias", b, device)
         self._joined = True
@@ -572,22 +582,32 @@ class SoftmaxHead:
     @property
     def W(self):
         self.join()
+        self._wgen += 1
         return self._Wp
 
     @W.setter
     def W(self, v):
         self.join()
+        self._wgen += 1
         self._Wp = v
 
     @property
     def b(self):
         self.join()
+        self._wgen += 1
         return self._bp
 
     @b.setter
     def b(self, v):
         self.join()
+        self._wgen += 1
         self._bp = v
+
+    def params_ro(self):
+        """(W, b) for a read-only use on the current stream: joins like the
+        properties but keeps the fused workspaces' operand planes current."""
+        self.join()
+        return self._Wp, self._bp
 
     def named_params(self):
         return [self.W, self.b]
@@ -620,11 +640,14 @@ class SoftmaxHead:
         w.terms = terms
         w.h = h
         st = stream_ptr()
-        W, b = self.W.p.data_ptr(), self.b.p.data_ptr()
+        Wp, bp = self.params_ro()
+        W, b = Wp.p.data_ptr(), bp.p.data_ptr()
         ptr = lambda t: None if t is None else t.data_ptr()  # noqa: E731
         with region("head_fwd"):
             call("rg_head_planes", h.data_ptr(), B, HF, w.Hk.data_ptr(), w.Hr.data_ptr(), None, None, st)
-            call("rg_head_planes", W, A, HF, w.Wk.data_ptr(), w.Wr.data_ptr(), b, w.bias_pad.data_ptr(), st)
+            if w.wgen != self._wgen:   # else the previous pass 2 left this W's planes here
+                call("rg_head_planes", W, A, HF, w.Wk.data_ptr(), w.Wr.data_ptr(), b, w.bias_pad.data_ptr(), st)
+                w.wgen = self._wgen
             call("rg_flash_fwd_top", w.Hk.data_ptr(), w.Wk.data_ptr(), w.Wr.data_ptr(), w.bias_pad.data_ptr(), B, A,
                  HF, terms, w.nsplit, w.pm.data_ptr(), w.pl.data_ptr(), w.pO.data_ptr(), ptr(w.pbest), ptr(w.parg),
                  ptr(w.cmax), st)
@@ -652,7 +675,7 @@ class SoftmaxHead:
                      w.top_val.data_ptr(), st)
             else:
                 call("rg_flash_topk", w.cmax.data_ptr(), B, self.A, K, _f32(self.TOP_TOL_ABS),
-                     _f32(self.TOP_TOL_REL), w.h.data_ptr(), self.W.p.data_ptr(), self.b.p.data_ptr(), self.HF,
+                     _f32(self.TOP_TOL_REL), w.h.data_ptr(), self._Wp.p.data_ptr(), self._bp.p.data_ptr(), self.HF,
                      w.cand.data_ptr(), w.ncand.data_ptr(), w.top_idx.data_ptr(), w.top_val.data_ptr(),
                      self.top_err.data_ptr(), st)
             return w.top_idx, w.top_val
@@ -674,8 +697,8 @@ class SoftmaxHead:
         st = stream_ptr()
         call("rg_flash_rows", lse.data_ptr(), tgt.data_ptr(), self.lo, self.A, w.B, w.rows.data_ptr(), st)
         with region("head_dh"):
-            call("rg_flash_dh", w.pm.data_ptr(), w.pO.data_ptr(), w.rows.data_ptr(), w.nsplit, self.W.p.data_ptr(), g,
-                 w.B, self.HF, dh_out.data_ptr(), st)
+            call("rg_flash_dh", w.pm.data_ptr(), w.pO.data_ptr(), w.rows.data_ptr(), w.nsplit,
+                 self.params_ro()[0].p.data_ptr(), g, w.B, self.HF, dh_out.data_ptr(), st)
 
     def join(self):
         """Order the current stream after an overlapped pass 2 (backward_step(overlap=True))."""
@@ -694,13 +717,25 @@ class SoftmaxHead:
         self._joined = False
 
     def flash_dw_adam(self, w, g, adam6):
-        """Pass 2: dW, db and the Adam step of W / b (after flash_dh)."""
+        """Pass 2: dW, db and the Adam step of W / b (after flash_dh); the
+        updated W / b also leave as this workspace's operand planes and padded
+        bias (the next flash_forward on it skips rg_head_planes for W)."""
         Wp, bp = self._Wp, self._bp   # not the joining properties: this may run on the side stream
+        if not PASS2_PLANES:
+            with region("head_dw_adam"):
+                call("rg_flash_dw_adam", w.Hk.data_ptr(), w.Hr.data_ptr(), w.Wk.data_ptr(), w.bias_pad.data_ptr(),
+                     w.rows.data_ptr(), g, w.B, self.A, self.HF, w.terms, Wp.p.data_ptr(), Wp.m.data_ptr(),
+                     Wp.v.data_ptr(), bp.p.data_ptr(), bp.m.data_ptr(), bp.v.data_ptr(), adam6, None, None,
+                     stream_ptr())
+            self._wgen += 1
+            return
         with region("head_dw_adam"):
-            call("rg_flash_dw_adam", w.Hk.data_ptr(), w.Hr.data_ptr(), w.Wk.data_ptr(), w.bias_pad.data_ptr(),
-                 w.rows.data_ptr(), g, w.B, self.A, self.HF, w.terms, Wp.p.data_ptr(), Wp.m.data_ptr(),
-                 Wp.v.data_ptr(), bp.p.data_ptr(), bp.m.data_ptr(), bp.v.data_ptr(), adam6, None,
-                 None, stream_ptr())
+            call("rg_flash_dw_adam_planes", w.Hk.data_ptr(), w.Hr.data_ptr(), w.Wk.data_ptr(),
+                 w.bias_pad.data_ptr(), w.rows.data_ptr(), g, w.B, self.A, self.HF, w.terms, Wp.p.data_ptr(),
+                 Wp.m.data_ptr(), Wp.v.data_ptr(), bp.p.data_ptr(), bp.m.data_ptr(), bp.v.data_ptr(), adam6, None,
+                 None, w.Wk.data_ptr(), w.Wr.data_ptr(), w.bias_pad.data_ptr(), stream_ptr())
+        self._wgen += 1
+        w.wgen = self._wgen
 
     def ws(self, slot, B, store_z):
         key = (slot, B, store_z)

@@ -59,6 +59,57 @@ def run_flash(h, W, b, tgt, terms, nsplit, lo=0, lse_global=None, A_full=None):
     return {k: v.cpu().double() for k, v in dict(lse=lse, zt=zt, dh=dh, dW=dW, db=db).items()}
 
 
+@pytest.mark.parametrize("B,A,HF", [(64, 1000, 32), (96, 3001, 64), (128, 4133, 128), (64, 2077, 256)])
+def test_pass2_writes_next_planes(B, A, HF):
+    """rg_flash_dw_adam_planes: the updated W / b leave as operand planes and
+    padded bias bit-identical to rg_head_planes of the updated tensors (what
+    the next pass 1 reads), incl. a ragged last item block; W / b / moments
+    equal plain rg_flash_dw_adam's."""
+    call, st = C().call, C().stream_ptr()
+    h, W, b, tgt = inputs(B, A, HF, 3 + HF)
+    h, W, b, tgt = h.to(dev), W.to(dev), b.to(dev), tgt.to(dev)
+    hb, wb = call("rg_head_plane_bytes", B, HF), call("rg_head_plane_bytes", A, HF)
+    Hk, Hr, Wk, Wr = _u8(hb), _u8(hb), _u8(wb), _u8(wb)
+    bp = torch.empty((A + 31) // 32 * 32, device=dev)
+    call("rg_head_planes", h.data_ptr(), B, HF, Hk.data_ptr(), Hr.data_ptr(), None, None, st)
+    call("rg_head_planes", W.data_ptr(), A, HF, Wk.data_ptr(), Wr.data_ptr(), b.data_ptr(), bp.data_ptr(), st)
+    ns = 8
+    pm, pl, pO = torch.empty(ns, B, device=dev), torch.empty(ns, B, device=dev), torch.empty(ns, HF, B, device=dev)
+    call("rg_flash_fwd", Hk.data_ptr(), Wk.data_ptr(), Wr.data_ptr(), bp.data_ptr(), B, A, HF, 6, ns, pm.data_ptr(),
+         pl.data_ptr(), pO.data_ptr(), st)
+    lse, zt, rows = torch.empty(B, device=dev), torch.empty(B, device=dev), torch.empty(B, 2, device=dev)
+    call("rg_flash_lse", pm.data_ptr(), pl.data_ptr(), ns, h.data_ptr(), W.data_ptr(), b.data_ptr(), tgt.data_ptr(),
+         0, A, A, B, HF, lse.data_ptr(), zt.data_ptr(), st)
+    call("rg_flash_rows", lse.data_ptr(), tgt.data_ptr(), 0, A, B, rows.data_ptr(), st)
+    adam6 = C().host_floats([0.1, 0.999, 0.001, 0.0316, 1e-8, -0.01])
+    g = float(np.float32(1.0 / B))
+    outs = []
+    for planes in (False, True):
+        Wx, bx = W.clone(), b.clone()
+        mW, vW = torch.full_like(W, 0.01), torch.full_like(W, 0.02)
+        mb, vb = torch.full_like(b, 0.01), torch.full_like(b, 0.02)
+        Wk2, Wr2, bp2 = Wk.clone(), Wr.clone(), bp.clone()
+        args = [Hk.data_ptr(), Hr.data_ptr(), Wk2.data_ptr(), bp2.data_ptr(), rows.data_ptr(), g, B, A, HF, 6,
+                Wx.data_ptr(), mW.data_ptr(), vW.data_ptr(), bx.data_ptr(), mb.data_ptr(), vb.data_ptr(), adam6,
+                None, None]
+        if planes:
+            call("rg_flash_dw_adam_planes", *args, Wk2.data_ptr(), Wr2.data_ptr(), bp2.data_ptr(), st)
+        else:
+            call("rg_flash_dw_adam", *args, st)
+        torch.cuda.synchronize()
+        outs.append((Wx, bx, mW, vW, mb, vb, Wk2, Wr2, bp2))
+    for x, y in zip(outs[0][:6], outs[1][:6]):
+        assert torch.equal(x, y)
+    Wx, bx = outs[1][0], outs[1][1]
+    Wk3, Wr3, bp3 = _u8(wb), _u8(wb), torch.empty_like(bp)
+    call("rg_head_planes", Wx.data_ptr(), A, HF, Wk3.data_ptr(), Wr3.data_ptr(), bx.data_ptr(), bp3.data_ptr(), st)
+    torch.cuda.synchronize()
+    assert not torch.equal(Wk3, Wk)   # W moved
+    assert torch.equal(outs[1][6], Wk3)
+    assert torch.equal(outs[1][7], Wr3)
+    assert torch.equal(outs[1][8], bp3)
+
+
 def fp64_reference(h, W, b, tgt):
     Wr = W.double().requires_grad_(True)
     br = b.double().requires_grad_(True)
