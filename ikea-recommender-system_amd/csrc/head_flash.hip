@@ -471,13 +471,15 @@ __global__ __launch_bounds__(64 * fl_nw(HF, 1)) void k_flash_amax(
 // shard's items [lo, lo + A), its logit z = h·W[t] + b[t]; 0 for a target
 // held by another shard, NaN for one outside [0, A_full) (CrossEntropyLoss
 // raises there; the native head writes a NaN loss row, head.hip k_lse_combine)
-__global__ __launch_bounds__(256) void k_flash_lse(const float* __restrict__ pm, const float* __restrict__ pl,
-                                                   int nsplit, const float* __restrict__ h,
-                                                   const float* __restrict__ W, const float* __restrict__ bias,
-                                                   const int64_t* __restrict__ tgt, int64_t lo, int A,
-                                                   int64_t A_full, int B, int HF, float* __restrict__ lse,
-                                                   float* __restrict__ zt) {
-  const int b = blockIdx.x * 256 + threadIdx.x;
+// (HF a template parameter: the row's h and W[t] arrive as 16-B loads issued
+// up front; the dot is the same sequential fmaf chain over k; 64-row blocks)
+template <int HF>
+__global__ __launch_bounds__(64) void k_flash_lse(const float* __restrict__ pm, const float* __restrict__ pl,
+                                                  int nsplit, const float* __restrict__ h,
+                                                  const float* __restrict__ W, const float* __restrict__ bias,
+                                                  const int64_t* __restrict__ tgt, int64_t lo, int A, int64_t A_full,
+                                                  int B, float* __restrict__ lse, float* __restrict__ zt) {
+  const int b = blockIdx.x * 64 + threadIdx.x;
   if (b >= B) return;
   float M = NEG_INF;
   for (int s = 0; s < nsplit; ++s) M = fmaxf(M, pm[(int64_t)s * B + b]);
@@ -491,7 +493,18 @@ __global__ __launch_bounds__(256) void k_flash_lse(const float* __restrict__ pm,
     const int64_t t = tgt[b] - lo;
     float z = (tgt[b] >= 0 && tgt[b] < A_full) ? 0.f : __builtin_nanf("");
     if (t >= 0 && t < A) {
-      for (int k = 0; k < HF; ++k) z = fmaf(h[(int64_t)b * HF + k], W[t * HF + k], z);
+      const f4* hr = reinterpret_cast<const f4*>(h + (int64_t)b * HF);
+      const f4* wr = reinterpret_cast<const f4*>(W + t * HF);
+      f4 hv[HF / 4], wv[HF / 4];
+#pragma unroll
+      for (int k = 0; k < HF / 4; ++k) {
+        hv[k] = hr[k];
+        wv[k] = wr[k];
+      }
+#pragma unroll
+      for (int k = 0; k < HF / 4; ++k)
+#pragma unroll
+        for (int u = 0; u < 4; ++u) z = fmaf(hv[k][u], wv[k][u], z);
       z += bias[t];
     }
     zt[b] = z;
@@ -1105,8 +1118,17 @@ extern "C" int rg_flash_lse(const float* pm, const float* pl, int nsplit, const 
                             float* lse, float* zt, hipStream_t stream) {
   if (B <= 0 || A <= 0 || nsplit <= 0 || !pm || !pl || !lse) return RG_ERR_ARG;
   if (zt && (!h || !W || !bias || !tgt || A_full < lo + A)) return RG_ERR_ARG;
-  hipLaunchKernelGGL(k_flash_lse, dim3((B + 255) / 256), dim3(256), 0, stream, pm, pl, nsplit, h, W, bias, tgt, lo,
-                     A, A_full, B, HF, lse, zt);
+  if (zt && !flash_hf_ok(HF)) return RG_ERR_SHAPE;
+#define FLS(HFV)                                                                                                 \
+  hipLaunchKernelGGL(k_flash_lse<HFV>, dim3((B + 63) / 64), dim3(64), 0, stream, pm, pl, nsplit, h, W, bias, tgt, lo, \
+                     A, A_full, B, lse, zt)
+  switch (zt ? HF : 32) {
+    case 32: FLS(32); break;
+    case 64: FLS(64); break;
+    case 128: FLS(128); break;
+    case 256: FLS(256); break;
+  }
+#undef FLS
   RG_LAUNCH_CHECK();
   return RG_OK;
 }

@@ -54,9 +54,11 @@ for terms in a.terms:
                             call("rg_flash_rows", lse.data_ptr(), tgt.data_ptr(), 0, A, B, rows.data_ptr(), st),
                             call("rg_flash_dh", pm.data_ptr(), pO.data_ptr(), rows.data_ptr(), ns, W.data_ptr(),
                                  gs, B, H, dh.data_ptr(), st)),
-        "pass2": lambda: call("rg_flash_dw_adam", Hk.data_ptr(), Hr.data_ptr(), Wk.data_ptr(), bp.data_ptr(),
+        # as the trainers run it: the updated W also leaves as the next pass 1's planes
+        "pass2": lambda: call("rg_flash_dw_adam_planes", Hk.data_ptr(), Hr.data_ptr(), Wk.data_ptr(), bp.data_ptr(),
                               rows.data_ptr(), gs, B, A, H, terms, W.data_ptr(), mW.data_ptr(), vW.data_ptr(),
-                              bias.data_ptr(), mb.data_ptr(), vb.data_ptr(), adam6, None, None, st),
+                              bias.data_ptr(), mb.data_ptr(), vb.data_ptr(), adam6, None, None, Wk.data_ptr(),
+                              Wr.data_ptr(), bp.data_ptr(), st),
     }
     for name, fn in stages.items():
         fn()
@@ -70,5 +72,6 @@ for terms in a.terms:
         ms = e0.elapsed_time(e1) / a.iters
         extra = ""
         if name in ("pass1", "pass2"):
-            extra = f"  {2 * terms * fl / ms / 1e9:7.1f} TFLOP/s bf16 MFMA ({2 * terms * fl / ms / 1e9 / 2500:.3f} of peak)"
+            nprod = {6: 12, 9: 18, 636: 9 if name == "pass1" else 12}[terms]   # plane products per pass
+            extra = f"  {nprod * fl / ms / 1e9:7.1f} TFLOP/s bf16 MFMA ({nprod * fl / ms / 1e9 / 2500:.3f} of peak)"
         print(f"terms {terms} {name:8s} {ms:8.3f} ms{extra}", flush=True)
