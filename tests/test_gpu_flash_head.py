@@ -59,7 +59,8 @@ def run_flash(h, W, b, tgt, terms, nsplit, lo=0, lse_global=None, A_full=None):
     return {k: v.cpu().double() for k, v in dict(lse=lse, zt=zt, dh=dh, dW=dW, db=db).items()}
 
 
-@pytest.mark.parametrize("B,A,HF", [(64, 1000, 32), (96, 3001, 64), (128, 4133, 128), (64, 2077, 256)])
+@pytest.mark.parametrize("B,A,HF", [(64, 1000, 32), (96, 3001, 64), (128, 4133, 128), (64, 2077, 256),
+                                    (64, 20011, 64), (96, 40009, 128)])
 def test_pass2_writes_next_planes(B, A, HF):
     """rg_flash_dw_adam_planes: the updated W / b leave as operand planes and
     padded bias bit-identical to rg_head_planes of the updated tensors (what
