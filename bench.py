@@ -311,6 +311,12 @@ def pinned(b):
 
 def main():
     args = parse()
+    # the ONE JSON line goes to the real stdout; everything else that writes to
+    # fd 1 while the job runs (RCCL's version banner at init, library logs)
+    # is sent to stderr
+    sys.stdout.flush()
+    json_fd = os.dup(1)
+    os.dup2(2, 1)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -452,8 +458,9 @@ def main():
         "data": "synthetic (seeded Zipf session stream, random-init weights)",
         "config": {"workload": workload,
                    "global_batch": B * world, "seq_len": L, "items": N, "dim": E,
-                   "parallelism": (f"dp{world} trunk + {world}-way item-sharded tables (RCCL)" if world > 1
-                                   else "single"),
+                   "parallelism": (f"dp{world} trunk + {world}-way item-sharded tables "
+                                   f"({torch.distributed.get_backend() if torch.distributed.is_initialized() else ''})"
+                                   if shard else "single"),
                    "tokens_per_batch": int(T)},
         "step_ms": {"median": round(float(np.median(ps)), 3), "p10": round(float(np.percentile(ps, 10)), 3),
                     "p90": round(float(np.percentile(ps, 90)), 3), "mean": round(float(ps.mean()), 3)},
@@ -461,7 +468,7 @@ def main():
         "native_f32": native, "kernel_ms": kern,
         "loss_first_last": [round(losses[0], 5), round(losses[-1], 5)],
     }
-    print(json.dumps(line), flush=True)
+    os.write(json_fd, (json.dumps(line) + "\n").encode())
     if torch.distributed.is_initialized():
         torch.distributed.destroy_process_group()
 
