@@ -379,10 +379,13 @@ __global__ __launch_bounds__(64 * fl_nw(HF, 1)) void k_flash_fwd(
 // 222-226, tensor_operations.py:50-70 via the combined head).  Same
 // workgroup / split / XCD layout and K-plane DMA ring as pass 1; per split the
 // row's best logit and item go to pbest / parg (merged by rg_flash_argmax).
-template <int HF, int NT>
+// CM (screening, NT = 3): also every 32-item chunk's row maximum (cmax,
+// ceil(A/32) × B) for the exact re-scoring of rg_flash_argmax_exact; plane 2
+// of the operands is then never read (not even DMA'd).
+template <int HF, int NT, bool CM>
 __global__ __launch_bounds__(64 * fl_nw(HF, 1)) void k_flash_amax(
     const bf16x8* __restrict__ Hk, const bf16x8* __restrict__ Wk, const float* __restrict__ bias_pad, int B, int A,
-    int nrb, int nsplit, int cps, float* __restrict__ pbest, int32_t* __restrict__ parg) {
+    int nrb, int nsplit, int cps, float* __restrict__ pbest, int32_t* __restrict__ parg, float* __restrict__ cmax) {
   constexpr int NW = fl_nw(HF, 1);
   constexpr int NS = HF / 16;
   constexpr int EK = NS * 192;
@@ -401,7 +404,7 @@ __global__ __launch_bounds__(64 * fl_nw(HF, 1)) void k_flash_amax(
   const int nch = max(0, min(nct, c0 + cps) - c0);
 #define FA_ISSUE(C, SK, SB)                                                    \
   do {                                                                         \
-    stage<EK, NW>(Wk + (int64_t)(C) * EK, SK, w, lane16);                      \
+    stage<EK, NW, NT != 3>(Wk + (int64_t)(C) * EK, SK, w, lane16);             \
     if (w == 0 && lane < 8) blds16(rsrc_of(bias_pad + 32 * (C)), SB, lane16, 0); \
   } while (0)
   if (nch > 0) FA_ISSUE(c0, sk0, sb0);
@@ -427,17 +430,23 @@ __global__ __launch_bounds__(64 * fl_nw(HF, 1)) void k_flash_amax(
       a2 = n2;
       __builtin_amdgcn_sched_barrier(0);
     }
+    float cm = NEG_INF;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const f4 bq = *reinterpret_cast<const f4*>(&sb[8 * q + 4 * hh]);
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         const float z = sa[4 * q + u] + bq[u];
+        cm = fmaxf(cm, z);
         if (z > bv) {  // items increase with r: strict > keeps the first maximum
           bv = z;
           bi = 32 * (c0 + c) + 8 * q + 4 * hh + u;
         }
       }
+    }
+    if (CM) {
+      cm = fmaxf(cm, __shfl_xor(cm, 32));
+      if (hh == 0) cmax[(int64_t)(c0 + c) * B + r0 + l32] = cm;
     }
   };
   for (int c = 0; c < nch; c += 2) {
@@ -903,6 +912,7 @@ __global__ __launch_bounds__(256) void k_flash_topk_eval(const float* __restrict
   __shared__ float rv[4];
   __shared__ int ri[4], rs[4];
   const int row = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  if (ncand[row] < 0 || ncand[row] > TK_CAP) return;   // overflowed screening: the caller's result stays
   for (int k = tid; k < HF; k += 256) hs[k] = h[(int64_t)row * HF + k];
   const int n = ncand[row] * 32;
   __syncthreads();
@@ -965,6 +975,58 @@ __global__ __launch_bounds__(256) void k_flash_topk_eval(const float* __restrict
       if (rs[0] >= 0) ci[rs[0]] = INT32_MAX;   // taken
     }
     __syncthreads();
+  }
+}
+
+// out[0] = max_a ||W_a||_2 (float bits ordered as uint: max is order-independent);
+// out[0] must be 0 on entry.  32 lanes per row, HF / 4 <= 64 float4s per row.
+__global__ __launch_bounds__(256) void k_row_norm_max(const float* __restrict__ W, int64_t A, int HF,
+                                                      float* __restrict__ out) {
+  const int lane = threadIdx.x & 31, n4 = HF / 4;
+  float best = 0.f;
+  for (int64_t a = (blockIdx.x * 256 + threadIdx.x) / 32; a < A; a += (int64_t)gridDim.x * 8) {
+    const f4* wr = reinterpret_cast<const f4*>(W + a * HF);
+    float s = 0.f;
+    for (int k = lane; k < n4; k += 32) {
+      const f4 x = wr[k];
+      s = fmaf(x[0], x[0], fmaf(x[1], x[1], fmaf(x[2], x[2], fmaf(x[3], x[3], s))));
+    }
+#pragma unroll
+    for (int o = 16; o >= 1; o >>= 1) s += __shfl_xor(s, o);
+    best = fmaxf(best, sqrtf(s));
+  }
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) best = fmaxf(best, __shfl_xor(best, o));
+  if ((threadIdx.x & 63) == 0) atomicMax(reinterpret_cast<unsigned int*>(out), __float_as_uint(best));
+}
+
+// per row: lim = tau − (tol·||h_b||_2·wnorm[0] + 1e-6·|tau|), tau = the screening's best (value)
+__global__ void k_amax_lim(const float* __restrict__ best, const float* __restrict__ h, int B, int HF,
+                           const float* __restrict__ wnorm, float tol, float* __restrict__ lim) {
+  const int row = blockIdx.x * blockDim.x + threadIdx.x;
+  if (row >= B) return;
+  float hn = 0.f;
+  for (int k = 0; k < HF; ++k) hn = fmaf(h[(int64_t)row * HF + k], h[(int64_t)row * HF + k], hn);
+  const float tau = best[row];
+  lim[row] = tau > NEG_INF ? tau - (tol * sqrtf(hn) * wnorm[0] + 1e-6f * fabsf(tau)) : NEG_INF;
+}
+
+// candidate chunks (cmax >= lim) of every row, chunk range split over grid.y;
+// appended in any order through a per-row counter (the re-scoring keeps the
+// first maximum by (value, item), so the order does not matter)
+__global__ __launch_bounds__(256) void k_amax_cand(const float* __restrict__ cmax, int nct, int B,
+                                                   const float* __restrict__ lim, int32_t* __restrict__ cand,
+                                                   int32_t* __restrict__ ncand) {
+  const int row = blockIdx.x * 256 + threadIdx.x;
+  if (row >= B) return;
+  const int per = (nct + gridDim.y - 1) / gridDim.y;
+  const int c0 = blockIdx.y * per, c1 = min(nct, c0 + per);
+  const float l = lim[row];
+  for (int c = c0; c < c1; ++c) {
+    if (cmax[(int64_t)c * B + row] >= l) {
+      const int p = atomicAdd(&ncand[row], 1);
+      if (p < TK_CAP) cand[(int64_t)row * TK_CAP + p] = c;
+    }
   }
 }
 
@@ -1068,8 +1130,8 @@ extern "C" int rg_flash_amax_fwd(const void* Hk, const void* Wk, const float* bi
   const int nrb = (B + rpb - 1) / rpb;
   const dim3 grid((unsigned)(nrb * nsplit));
 #define FM(HFV, NTV)                                                                                            \
-  hipLaunchKernelGGL((k_flash_amax<HFV, NTV>), grid, dim3(64 * fl_nw(HFV, 1)), 0, stream, (const bf16x8*)Hk,    \
-                     (const bf16x8*)Wk, bias_pad, B, A, nrb, nsplit, cps, pbest, parg)
+  hipLaunchKernelGGL((k_flash_amax<HFV, NTV, false>), grid, dim3(64 * fl_nw(HFV, 1)), 0, stream, (const bf16x8*)Hk, \
+                     (const bf16x8*)Wk, bias_pad, B, A, nrb, nsplit, cps, pbest, parg, (float*)nullptr)
 #define FT(HFV)          \
   if (terms == 9) {      \
     FM(HFV, 9);          \
@@ -1193,4 +1255,61 @@ extern "C" int rg_flash_dw_adam(const void* Hk, const void* Hr, const void* Wk, 
                                 float* dW_out, float* db_out, hipStream_t stream) {
   return rg_flash_dw_adam_planes(Hk, Hr, Wk, bias_pad, rowinfo, gscale, B, A, HF, terms, W, mW, vW, bias, mb, vb, adam6,
                                  dW_out, db_out, nullptr, nullptr, nullptr, stream);
+}
+
+// Exact argmax through screening (the double-Q target of SQN / SMORL at the
+// cost of 3 plane products instead of 6): k_flash_amax<NT = 3> leaves the
+// per-split first maximum and every chunk's row maximum of the 3-term logits;
+// the caller merges the former (rg_flash_argmax) and then
+// rg_flash_argmax_exact re-scores, in fp32 (fmaf chain over k, + bias), every
+// item of every chunk whose 3-term maximum lies within the error bound
+// tol·||h_b||_2·max_a||W_a||_2 of the row's best, and keeps the first maximum.
+extern "C" int rg_flash_amax_screen(const void* Hk, const void* Wk, const float* bias_pad, int B, int A, int HF,
+                                    int nsplit, float* pbest, int32_t* parg, float* cmax, hipStream_t stream) {
+  if (B <= 0 || A <= 0 || (B % 32) || nsplit <= 0 || !Hk || !Wk || !bias_pad || !pbest || !parg || !cmax)
+    return RG_ERR_ARG;
+  if (!flash_hf_ok(HF)) return RG_ERR_SHAPE;
+  const int nct = (A + 31) / 32;
+  const int cps = (nct + nsplit - 1) / nsplit;
+  const int rpb = fl_rows(HF, 1);
+  const int nrb = (B + rpb - 1) / rpb;
+  const dim3 grid((unsigned)(nrb * nsplit));
+#define FS(HFV)                                                                                                   \
+  hipLaunchKernelGGL((k_flash_amax<HFV, 3, true>), grid, dim3(64 * fl_nw(HFV, 1)), 0, stream, (const bf16x8*)Hk,  \
+                     (const bf16x8*)Wk, bias_pad, B, A, nrb, nsplit, cps, pbest, parg, cmax)
+  switch (HF) {
+    case 32: FS(32); break;
+    case 64: FS(64); break;
+    case 128: FS(128); break;
+    case 256: FS(256); break;
+  }
+#undef FS
+  RG_LAUNCH_CHECK();
+  return RG_OK;
+}
+
+extern "C" int rg_row_norm_max(const float* W, int64_t A, int HF, float* out, hipStream_t stream) {
+  if (A <= 0 || HF <= 0 || HF > 256 || (HF % 4) || !W || !out) return RG_ERR_ARG;
+  if (hipMemsetAsync(out, 0, sizeof(float), stream) != hipSuccess) return RG_ERR_LAUNCH;
+  const int64_t blocks = (A + 7) / 8;
+  hipLaunchKernelGGL(k_row_norm_max, dim3((unsigned)(blocks < 4096 ? blocks : 4096)), dim3(256), 0, stream, W, A, HF,
+                     out);
+  RG_LAUNCH_CHECK();
+  return RG_OK;
+}
+
+extern "C" int rg_flash_argmax_exact(const float* cmax, int B, int A, const float* h, const float* W, const float* bias,
+                                     int HF, const float* wnorm, float tol, float* lim, int32_t* cand, int32_t* ncand,
+                                     int32_t* out_idx, float* out_val, hipStream_t stream) {
+  if (B <= 0 || A <= 0 || HF <= 0 || HF > 256 || (HF % 4)) return RG_ERR_ARG;
+  if (!cmax || !h || !W || !bias || !wnorm || !lim || !cand || !ncand || !out_idx || !out_val) return RG_ERR_ARG;
+  const int nct = (A + 31) / 32;
+  if (hipMemsetAsync(ncand, 0, sizeof(int32_t) * B, stream) != hipSuccess) return RG_ERR_LAUNCH;
+  hipLaunchKernelGGL(k_amax_lim, dim3((B + 255) / 256), dim3(256), 0, stream, out_val, h, B, HF, wnorm, tol, lim);
+  const int ys = max(1, min(256, 2048 / ((B + 255) / 256)));   // ~2048 workgroups
+  hipLaunchKernelGGL(k_amax_cand, dim3((B + 255) / 256, ys), dim3(256), 0, stream, cmax, nct, B, lim, cand, ncand);
+  hipLaunchKernelGGL(k_flash_topk_eval, dim3(B), dim3(256), 0, stream, h, W, bias, cand, ncand, A, HF, 1, out_idx,
+                     out_val);
+  RG_LAUNCH_CHECK();
+  return RG_OK;
 }

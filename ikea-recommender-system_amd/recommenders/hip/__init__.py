@@ -52,6 +52,9 @@ SIGNATURES = {
     "rg_flash_fwd_top": [P, P, P, P, I, I, I, I, I, P, P, P, P, P, P, P],
     "rg_flash_argmax": [P, P, I, I, P, P, P],
     "rg_flash_amax_fwd": [P, P, P, I, I, I, I, I, P, P, P],
+    "rg_flash_amax_screen": [P, P, P, I, I, I, I, P, P, P, P],
+    "rg_row_norm_max": [P, I64, I, P, P],
+    "rg_flash_argmax_exact": [P, I, I, P, P, P, I, P, F, P, P, P, P, P, P],
     "rg_flash_topk_cap": [],
     "rg_flash_topk": [P, I, I, I, F, F, P, P, P, I, P, P, P, P, P, P],
     "rg_flash_lse": [P, P, I, P, P, P, P, I64, I, I64, I, I, P, P, P],

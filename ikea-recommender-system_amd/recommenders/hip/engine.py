@@ -505,12 +505,14 @@ class _FlashWS:
 
 
 class _AmaxWS:
-    """Workspace of the split-bf16 argmax (K-planes of h and W, per-split bests)."""
+    """Workspace of the split-bf16 argmax (K-planes of h and W, per-split bests;
+    with ``screen`` the chunk maxima, candidates and max row norm of the
+    screening argmax)."""
 
-    def __init__(self, B, A, HF, device):
+    def __init__(self, B, A, HF, device, screen=False):
         u8 = lambda n: torch.empty(int(n), dtype=torch.uint8, device=device)  # noqa: E731
         z = lambda *s, dt=torch.float32: torch.empty(*s, dtype=dt, device=device)  # noqa: E731
-        self.B = B
+        self.B, self.screen = B, screen
         nrb = -(-B // call("rg_flash_rows_per_block", HF))
         self.nsplit = _round_up(min(max(1, 256 // nrb), -(-A // 32)), 8)
         self.Hk = u8(call("rg_head_plane_bytes", B, HF))
@@ -518,6 +520,11 @@ class _AmaxWS:
         self.bias_pad = z(_round_up(A, 32))
         self.pbest, self.parg = z(self.nsplit, B), z(self.nsplit, B, dt=torch.int32)
         self.amax, self.mx = z(B, dt=torch.int32), z(B)
+        if screen:
+            self.cmax = z(-(-A // 32), B)
+            self.cand = z(B, call("rg_flash_topk_cap"), dt=torch.int32)
+            self.ncand = z(B, dt=torch.int32)
+            self.wnorm, self.lim = z(1), z(B)
 
 
 # Head-GEMM arithmetic (build extension; the reference computes in fp32):
@@ -535,6 +542,15 @@ class _AmaxWS:
 SPLIT_TERMS = {"f32x9": 9, "f32x6": 6, "f32x6d3": 636}
 # RG_PASS2_PLANES=0: pass 2 leaves W's operand planes to the next rg_head_planes (A/B measurement)
 PASS2_PLANES = os.environ.get("RG_PASS2_PLANES", "1") != "0"
+# split-bf16 argmax (SQN / SMORL double-Q target): screening on 3 plane products, then every item
+# of every 32-item chunk whose screened maximum lies within SCREEN_TOL·||h_b||·max_a||W_a|| of the
+# row's best is re-scored in fp32 (first maximum).  The bound covers the dropped plane products
+# (3·2^-18), fp32 accumulation of both sums (384 + 128 terms at 2^-24) on both sides, with margin
+# (DESIGN §4a).  Needs ceil(A/32)·B floats of chunk maxima; above SCREEN_CMAX_BYTES (or with
+# RG_SCREEN_ARGMAX=0) the 6-product argmax runs instead.
+SCREEN_ARGMAX = os.environ.get("RG_SCREEN_ARGMAX", "1") != "0"
+SCREEN_TOL = 1e-4
+SCREEN_CMAX_BYTES = 2 << 30
 LOGIT_TERMS = {"f32x9": 9, "f32x6": 6, "f32x6d3": 6}
 PRECISIONS = ("f32",) + tuple(SPLIT_TERMS)
 
@@ -812,18 +828,31 @@ class SoftmaxHead:
         st = stream_ptr()
         terms = self.flash_terms(B)
         if terms:
+            # screening (3 plane products + exact fp32 re-scoring of the chunks
+            # within the error bound) unless its chunk maxima would not fit
+            screen = SCREEN_ARGMAX and -(-self.A // 32) * B * 4 <= SCREEN_CMAX_BYTES
             w = self._aws.get(slot) if hasattr(self, "_aws") else None
-            if w is None or w.B != B:
+            if w is None or w.B != B or w.screen != screen:
                 if not hasattr(self, "_aws"):
                     self._aws = {}
-                w = self._aws[slot] = _AmaxWS(B, self.A, self.HF, self.device)
+                self._aws.pop(slot, None)
+                w = self._aws[slot] = _AmaxWS(B, self.A, self.HF, self.device, screen)
+            W, b = self.W.p.data_ptr(), self.b.p.data_ptr()
             call("rg_head_planes", h.data_ptr(), B, self.HF, w.Hk.data_ptr(), None, None, None, st)
-            call("rg_head_planes", self.W.p.data_ptr(), self.A, self.HF, w.Wk.data_ptr(), None, self.b.p.data_ptr(),
-                 w.bias_pad.data_ptr(), st)
-            call("rg_flash_amax_fwd", w.Hk.data_ptr(), w.Wk.data_ptr(), w.bias_pad.data_ptr(), B, self.A, self.HF,
-                 terms, w.nsplit, w.pbest.data_ptr(), w.parg.data_ptr(), st)
+            call("rg_head_planes", W, self.A, self.HF, w.Wk.data_ptr(), None, b, w.bias_pad.data_ptr(), st)
+            if screen:
+                call("rg_flash_amax_screen", w.Hk.data_ptr(), w.Wk.data_ptr(), w.bias_pad.data_ptr(), B, self.A,
+                     self.HF, w.nsplit, w.pbest.data_ptr(), w.parg.data_ptr(), w.cmax.data_ptr(), st)
+            else:
+                call("rg_flash_amax_fwd", w.Hk.data_ptr(), w.Wk.data_ptr(), w.bias_pad.data_ptr(), B, self.A, self.HF,
+                     terms, w.nsplit, w.pbest.data_ptr(), w.parg.data_ptr(), st)
             call("rg_flash_argmax", w.pbest.data_ptr(), w.parg.data_ptr(), w.nsplit, B, w.amax.data_ptr(),
                  w.mx.data_ptr(), st)
+            if screen:
+                call("rg_row_norm_max", W, self.A, self.HF, w.wnorm.data_ptr(), st)
+                call("rg_flash_argmax_exact", w.cmax.data_ptr(), B, self.A, h.data_ptr(), W, b, self.HF,
+                     w.wnorm.data_ptr(), _f32(SCREEN_TOL), w.lim.data_ptr(), w.cand.data_ptr(), w.ncand.data_ptr(),
+                     w.amax.data_ptr(), w.mx.data_ptr(), st)
             self.argmax_mx = w.mx
             return w.amax
         w = self.ws(slot, B, False)

@@ -165,6 +165,21 @@ int rg_flash_amax_fwd(const void* Hk, const void* Wk, const float* bias_pad, int
                       int nsplit, float* pbest, int32_t* parg, rg_stream_t stream);
 int rg_flash_argmax(const float* pbest, const int32_t* parg, int nsplit, int B, int32_t* out, float* out_max,
                     rg_stream_t stream);
+/* Exact argmax by screening (the same double-Q target at half the MFMA work):
+ * rg_flash_amax_screen: rg_flash_amax_fwd on 3 plane products (planes 0-1 only) that also writes
+ *   every 32-item chunk's row maximum cmax (ceil(A/32) × B); merge pbest/parg with rg_flash_argmax.
+ * rg_row_norm_max: out[0] = max_a ||W_a||_2 (A × HF rows, HF % 4 == 0).
+ * rg_flash_argmax_exact: re-scores in fp32 (fmaf chain over k, + bias) every item of every chunk whose
+ *   screened maximum is >= tau − (tol·||h_b||_2·wnorm[0] + 1e-6·|tau|), tau = out_val (rg_flash_argmax's
+ *   screening maximum), and writes the first maximum into out_idx / out_val (in place over the
+ *   screening result); a row with more than rg_flash_topk_cap() candidate chunks keeps the screening
+ *   result.  lim: B floats, cand: B × rg_flash_topk_cap() int32, ncand: B int32 (work). */
+int rg_flash_amax_screen(const void* Hk, const void* Wk, const float* bias_pad, int B, int A, int HF, int nsplit,
+                         float* pbest, int32_t* parg, float* cmax, rg_stream_t stream);
+int rg_row_norm_max(const float* W, int64_t A, int HF, float* out, rg_stream_t stream);
+int rg_flash_argmax_exact(const float* cmax, int B, int A, const float* h, const float* W, const float* bias, int HF,
+                          const float* wnorm, float tol, float* lim, int32_t* cand, int32_t* ncand, int32_t* out_idx,
+                          float* out_val, rg_stream_t stream);
 int rg_flash_topk_cap(void);
 int rg_flash_topk(const float* cmax, int B, int A, int K, float tol_abs, float tol_rel, const float* h, const float* W,
                   const float* bias, int HF, int32_t* cand, int32_t* ncand, int32_t* out_idx, float* out_val,

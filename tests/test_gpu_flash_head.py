@@ -407,3 +407,114 @@ def test_fused_argmax_only(precision, B, A, HF, nsplit):
     assert (got != ref).sum() <= max(1, B // 50)
     np.testing.assert_allclose(mx.cpu().double().numpy(), Z[np.arange(B), got], rtol=0, atol=2e-5)
     assert not (got == A - 5).any()            # never the later duplicate of 11
+
+
+@pytest.mark.parametrize("B,A,HF,nsplit", [(256, 50000, 128, 8), (96, 20011, 64, 16), (64, 5003, 256, 8),
+                                           (64, 777, 32, 3)])
+def test_screening_argmax_is_exact(B, A, HF, nsplit):
+    """rg_flash_amax_screen + rg_flash_argmax_exact (the SQN / SMORL double-Q
+    target, sqn_gru.py:222-226): the first maximum of the fp32 logits, also
+    where the 3-term screening alone would pick a different item — planted
+    exact ties (duplicate rows: lowest index) and near-ties (1e-6 apart, far
+    below the screening error) — and a row with h = 0 (logits = bias)."""
+    call, st = C().call, C().stream_ptr()
+    g = torch.Generator().manual_seed(A + HF)
+    h = torch.tanh(torch.randn(B, HF, generator=g) * 2)
+    W = torch.randn(A, HF, generator=g) * 0.3
+    b = torch.randn(A, generator=g) * 0.3
+    Z = h.double() @ W.double().t() + b.double()
+    top = Z.argmax(1)
+    for r in range(0, B, 3):        # exact tie: a copy of the winner at a higher index
+        j = int(top[r])
+        k = (j * 7919 + 13) % A
+        if k > j:
+            W[k], b[k] = W[j], b[j]
+    for r in range(1, B, 3):        # near tie: a slightly better copy at a lower index
+        j = int(top[r])
+        k = (j * 104729 + 7) % A
+        if k < j:
+            W[k], b[k] = W[j], b[j] + 1e-6
+    h[B - 1] = 0.0                  # every logit of this row = its bias
+    b_eq = b.clone()
+    hd, Wd, bd = h.to(dev), W.to(dev), b.to(dev)
+    rows_eq = B - 1
+    Z = h.double() @ W.double().t() + b.double()
+    hb, wb = call("rg_head_plane_bytes", B, HF), call("rg_head_plane_bytes", A, HF)
+    Hk, Wk = _u8(hb), _u8(wb)
+    bp = torch.empty((A + 31) // 32 * 32, device=dev)
+    call("rg_head_planes", hd.data_ptr(), B, HF, Hk.data_ptr(), None, None, None, st)
+    call("rg_head_planes", Wd.data_ptr(), A, HF, Wk.data_ptr(), None, bd.data_ptr(), bp.data_ptr(), st)
+    pbest = torch.empty(nsplit, B, device=dev)
+    parg = torch.empty(nsplit, B, dtype=torch.int32, device=dev)
+    cmax = torch.empty((A + 31) // 32, B, device=dev)
+    call("rg_flash_amax_screen", Hk.data_ptr(), Wk.data_ptr(), bp.data_ptr(), B, A, HF, nsplit, pbest.data_ptr(),
+         parg.data_ptr(), cmax.data_ptr(), st)
+    idx = torch.empty(B, dtype=torch.int32, device=dev)
+    val = torch.empty(B, device=dev)
+    call("rg_flash_argmax", pbest.data_ptr(), parg.data_ptr(), nsplit, B, idx.data_ptr(), val.data_ptr(), st)
+    wn = torch.empty(1, device=dev)
+    call("rg_row_norm_max", Wd.data_ptr(), A, HF, wn.data_ptr(), st)
+    cap = call("rg_flash_topk_cap")
+    cand = torch.empty(B, cap, dtype=torch.int32, device=dev)
+    ncand = torch.empty(B, dtype=torch.int32, device=dev)
+    lim = torch.empty(B, device=dev)
+    call("rg_flash_argmax_exact", cmax.data_ptr(), B, A, hd.data_ptr(), Wd.data_ptr(), bd.data_ptr(), HF,
+         wn.data_ptr(), 1e-4, lim.data_ptr(), cand.data_ptr(), ncand.data_ptr(),
+         idx.data_ptr(), val.data_ptr(), st)
+    torch.cuda.synchronize()
+    assert abs(float(wn) - float(W.norm(dim=1).max())) <= 1e-5 * float(W.norm(dim=1).max())
+    idx, val = idx.cpu().long(), val.cpu().double()
+    # canonical: the first maximum of the fp64 logits (fp32 re-scoring only differs below its own rounding)
+    zmax = Z.max(1).values
+    first = (Z >= zmax[:, None]).double().argmax(1)
+    sl = (h.abs().double() @ W.abs().double().t()).max(1).values   # scale of the row's sums
+    for r in range(B):
+        if r == rows_eq:
+            continue
+        if int(idx[r]) != int(first[r]):
+            # only within the fp32 re-scoring's own rounding of the two items
+            assert float(zmax[r] - Z[r, idx[r]]) <= 200 * 2.0 ** -24 * float(sl[r]), (r, int(idx[r]), int(first[r]))
+        assert abs(float(val[r]) - float(Z[r, idx[r]])) <= 200 * 2.0 ** -24 * float(sl[r])
+    # exact ties resolve to the lowest index; near ties 1e-6 apart to the better item
+    for r in range(0, B - 1, 3):
+        assert int(idx[r]) == int(first[r])
+    for r in range(1, B - 1, 3):
+        assert int(idx[r]) == int(first[r])
+    assert int(idx[rows_eq]) == int(torch.argmax(b_eq.double()))
+
+
+def test_screening_argmax_overflow_keeps_first():
+    """Every logit of a row equal (h = 0, bias 0): more candidate chunks than
+    rg_flash_topk_cap(), so the row keeps the screening's first maximum (item
+    0); the other rows are still re-scored."""
+    call, st = C().call, C().stream_ptr()
+    B, A, HF, nsplit = 64, 5003, 64, 8
+    g = torch.Generator().manual_seed(5)
+    h = torch.tanh(torch.randn(B, HF, generator=g))
+    h[7] = 0.0
+    W = torch.randn(A, HF, generator=g) * 0.3
+    b = torch.zeros(A)
+    hd, Wd, bd = h.to(dev), W.to(dev), b.to(dev)
+    hb, wb = call("rg_head_plane_bytes", B, HF), call("rg_head_plane_bytes", A, HF)
+    Hk, Wk = _u8(hb), _u8(wb)
+    bp = torch.empty((A + 31) // 32 * 32, device=dev)
+    call("rg_head_planes", hd.data_ptr(), B, HF, Hk.data_ptr(), None, None, None, st)
+    call("rg_head_planes", Wd.data_ptr(), A, HF, Wk.data_ptr(), None, bd.data_ptr(), bp.data_ptr(), st)
+    pbest, parg = torch.empty(nsplit, B, device=dev), torch.empty(nsplit, B, dtype=torch.int32, device=dev)
+    cmax = torch.empty((A + 31) // 32, B, device=dev)
+    call("rg_flash_amax_screen", Hk.data_ptr(), Wk.data_ptr(), bp.data_ptr(), B, A, HF, nsplit, pbest.data_ptr(),
+         parg.data_ptr(), cmax.data_ptr(), st)
+    idx, val = torch.empty(B, dtype=torch.int32, device=dev), torch.empty(B, device=dev)
+    call("rg_flash_argmax", pbest.data_ptr(), parg.data_ptr(), nsplit, B, idx.data_ptr(), val.data_ptr(), st)
+    wn = torch.empty(1, device=dev)
+    call("rg_row_norm_max", Wd.data_ptr(), A, HF, wn.data_ptr(), st)
+    cap = call("rg_flash_topk_cap")
+    cand, ncand = torch.empty(B, cap, dtype=torch.int32, device=dev), torch.empty(B, dtype=torch.int32, device=dev)
+    lim = torch.empty(B, device=dev)
+    call("rg_flash_argmax_exact", cmax.data_ptr(), B, A, hd.data_ptr(), Wd.data_ptr(), bd.data_ptr(), HF,
+         wn.data_ptr(), 1e-4, lim.data_ptr(), cand.data_ptr(), ncand.data_ptr(), idx.data_ptr(), val.data_ptr(), st)
+    torch.cuda.synchronize()
+    assert int(ncand[7]) > cap and int(idx[7]) == 0
+    Z = h.double() @ W.double().t()
+    ok = torch.arange(B) != 7
+    assert torch.equal(idx.cpu().long()[ok], Z.argmax(1)[ok])
