@@ -551,11 +551,20 @@ __global__ __launch_bounds__(256) void k_flash_dh(const float* __restrict__ pm, 
 // Same ring scheme as pass 1 (HF 256: single-buffered R-planes of h); a wave
 // owns RB blocks of 32 items.
 template <int HF, int NT>
+//
+// Tail: the item blocks past the last whole round of workgroups (nfull
+// blocks) are split over tsplit workgroups each, every one taking a
+// contiguous range of the row chunks; they write partial dW / db (tail_dw:
+// tsplit × ntail × HF, tail_db: tsplit × ntail, ntail = A − 256·nfull) and
+// k_flash_tail sums them in order and finishes (Adam, planes).  At C2 the
+// 67 leftover blocks of 3907 would otherwise run as a 16th round on 26% of
+// the CUs.
 __global__ __launch_bounds__(64 * fl_nw(HF, 2)) void k_flash_dw(
-    const bf16x8* __restrict__ Hk, const bf16x8* __restrict__ Hr, const bf16x8* Wk, const float* bias_pad,
-    const float2* __restrict__ rowinfo, float g, int B, int A, float* __restrict__ W, float* __restrict__ mW,
+    const bf16x8* __restrict__ Hk0, const bf16x8* __restrict__ Hr0, const bf16x8* Wk, const float* bias_pad,
+    const float2* __restrict__ rowinfo0, float g, int B, int A, float* __restrict__ W, float* __restrict__ mW,
     float* __restrict__ vW, float* __restrict__ bias, float* __restrict__ mb, float* __restrict__ vb, AdamArgs args,
-    float* __restrict__ dW_out, float* __restrict__ db_out, bf16x8* Wk_out, bf16x8* Wr_out, float* bias_pad_out) {
+    float* __restrict__ dW_out, float* __restrict__ db_out, bf16x8* Wk_out, bf16x8* Wr_out, float* bias_pad_out,
+    int nfull, int tsplit, float* __restrict__ tail_dw, float* __restrict__ tail_db) {
   constexpr int NW = fl_nw(HF, 2), RB = fl_rb(HF, 2);
   constexpr bool DR = HF <= 128;
   constexpr int NS = HF / 16, NTL = HF / 32;
@@ -566,9 +575,17 @@ __global__ __launch_bounds__(64 * fl_nw(HF, 2)) void k_flash_dw(
   __shared__ __attribute__((aligned(16))) float2 si0[32], si1[32];
   const int tid = threadIdx.x, lane = tid & 63, hh = lane >> 5, l32 = lane & 31, lane16 = 16 * lane;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int j0 = blockIdx.x * fl_rows(HF, 2) + 32 * RB * w;   // this wave's first item
+  const int bx = blockIdx.x;
+  const bool tail = bx >= nfull;
+  const int blk = tail ? nfull + (bx - nfull) / tsplit : bx;
+  const int j0 = blk * fl_rows(HF, 2) + 32 * RB * w;   // this wave's first item
   const bool active = j0 < A;
-  const int nch = B / 32;
+  const int nct = B / 32, cper = (nct + tsplit - 1) / tsplit;
+  const int cb = tail ? (bx - nfull) % tsplit * cper : 0;
+  const int nch = tail ? max(0, min(nct, cb + cper) - cb) : nct;
+  const bf16x8* __restrict__ Hk = Hk0 + (int64_t)cb * EK;
+  const bf16x8* __restrict__ Hr = Hr0 + (int64_t)cb * ER;
+  const float2* __restrict__ rowinfo = rowinfo0 + 32 * cb;
 #define FL_ISSUE_K(C, SK, SI)                                                  \
   do {                                                                         \
     stage<EK, NW>(Hk + (int64_t)(C) * EK, SK, w, lane16);                      \
@@ -728,6 +745,25 @@ __global__ __launch_bounds__(64 * fl_nw(HF, 2)) void k_flash_dw(
     tr = reinterpret_cast<float*>(base) + ao;
   }
   const bool planes = Wk_out != nullptr && dW_out == nullptr;
+  if (tail) {
+    const int i0 = nfull * fl_rows(HF, 2), ntail = A - i0, part = (bx - nfull) % tsplit;
+#pragma unroll
+    for (int j = 0; j < RB; ++j) {
+      const int jb = j0 + 32 * j;
+      if (jb >= A) break;
+      const int item = jb + l32;
+      const float dbt = dbs[j] + __shfl_xor(dbs[j], 32);
+      if (hh == 0 && item < A) tail_db[(int64_t)part * ntail + item - i0] = dbt;
+#pragma unroll
+      for (int t = 0; t < NTL; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int it = jb + acc32_row(r, hh);
+          if (it < A) tail_dw[((int64_t)part * ntail + it - i0) * HF + 32 * t + l32] = dw[j][t][r];
+        }
+    }
+    return;
+  }
 #pragma unroll
   for (int j = 0; j < RB; ++j) {
     const int jb = j0 + 32 * j;
@@ -1030,6 +1066,59 @@ __global__ __launch_bounds__(256) void k_amax_cand(const float* __restrict__ cma
   }
 }
 
+// pass 2's tail: sum the tsplit partials of every leftover item in part
+// order, then the raw gradient (dW_out / db_out) or Adam on W / b
+__global__ __launch_bounds__(256) void k_flash_tail(const float* __restrict__ tail_dw, const float* __restrict__ tail_db,
+                                                    int tsplit, int i0, int ntail, int HF, float* __restrict__ W,
+                                                    float* __restrict__ mW, float* __restrict__ vW,
+                                                    float* __restrict__ bias, float* __restrict__ mb,
+                                                    float* __restrict__ vb, AdamArgs args, float* __restrict__ dW_out,
+                                                    float* __restrict__ db_out) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t n = (int64_t)ntail * HF;
+  if (i < n) {
+    float gs = 0.f;
+    for (int p = 0; p < tsplit; ++p) gs += tail_dw[(int64_t)p * n + i];
+    const int64_t o = (int64_t)i0 * HF + i;
+    if (dW_out) {
+      dW_out[o] = gs;
+    } else {
+      float pw = W[o], mq = mW[o], v = vW[o];
+      adam_elem(pw, mq, v, gs, args);
+      W[o] = pw;
+      mW[o] = mq;
+      vW[o] = v;
+    }
+  }
+  if (i < ntail) {
+    float gs = 0.f;
+    for (int p = 0; p < tsplit; ++p) gs += tail_db[(int64_t)p * ntail + i];
+    if (db_out) {
+      db_out[i0 + i] = gs;
+    } else {
+      float pb = bias[i0 + i], mq = mb[i0 + i], v = vb[i0 + i];
+      adam_elem(pb, mq, v, gs, args);
+      bias[i0 + i] = pb;
+      mb[i0 + i] = mq;
+      vb[i0 + i] = v;
+    }
+  }
+}
+
+// pass 2's grid: nfull whole item blocks, then the leftover blocks split tsplit
+// ways over the row chunks when they would fill less than ~3/4 of a round
+struct FlTail {
+  int nfull, tsplit, ntail;
+};
+inline FlTail fl_tail(int B, int A, int HF) {
+  const int rpb = fl_rows(HF, 2), nblk = (A + rpb - 1) / rpb, nct = B / 32;
+  const int nfull = nblk / 256 * 256, left = nblk - nfull;
+  if (nfull == 0 || left == 0 || left > 192) return FlTail{nblk, 1, 0};
+  const int ts = min(min(8, 256 / left), nct);
+  if (ts < 2) return FlTail{nblk, 1, 0};
+  return FlTail{nfull, ts, A - nfull * rpb};
+}
+
 inline bool flash_hf_ok(int HF) { return HF == 32 || HF == 64 || HF == 128 || HF == 256; }
 inline bool flash_terms_ok(int t) { return t == 6 || t == 9 || t == RG_TERMS_X6D3; }
 
@@ -1217,7 +1306,7 @@ extern "C" int rg_flash_dw_adam_planes(const void* Hk, const void* Hr, const voi
                                        const void* rowinfo, float gscale, int B, int A, int HF, int terms, float* W,
                                        float* mW, float* vW, float* bias, float* mb, float* vb, const float* adam6,
                                        float* dW_out, float* db_out, void* Wk_out, void* Wr_out, float* bias_pad_out,
-                                       hipStream_t stream) {
+                                       void* work, int64_t work_bytes, hipStream_t stream) {
   if (B <= 0 || A <= 0 || (B % 32) || !Hk || !Hr || !Wk || !bias_pad || !rowinfo) return RG_ERR_ARG;
   if (!flash_terms_ok(terms)) return RG_ERR_ARG;
   if (!flash_hf_ok(HF)) return RG_ERR_SHAPE;
@@ -1226,11 +1315,17 @@ extern "C" int rg_flash_dw_adam_planes(const void* Hk, const void* Hr, const voi
   AdamArgs a{};
   if (adam6) a = AdamArgs{adam6[0], adam6[1], adam6[2], adam6[3], adam6[4], adam6[5]};
   const int rpb = fl_rows(HF, 2);
-  const dim3 grid((unsigned)((A + rpb - 1) / rpb));
+  FlTail tl = fl_tail(B, A, HF);
+  if (tl.ntail && (int64_t)tl.tsplit * tl.ntail * (HF + 1) * 4 > (work ? work_bytes : 0)) tl = FlTail{(A + rpb - 1) / rpb, 1, 0};
+  float* tail_dw = (float*)work;
+  float* tail_db = tl.ntail ? tail_dw + (int64_t)tl.tsplit * tl.ntail * HF : nullptr;
+  const int nblk = (A + rpb - 1) / rpb;
+  const dim3 grid((unsigned)(tl.nfull + (nblk - tl.nfull) * tl.tsplit));
 #define FW(HFV, NTV)                                                                                          \
   hipLaunchKernelGGL((k_flash_dw<HFV, NTV>), grid, dim3(64 * fl_nw(HFV, 2)), 0, stream, (const bf16x8*)Hk, (const bf16x8*)Hr, \
                      (const bf16x8*)Wk, bias_pad, (const float2*)rowinfo, gscale, B, A, W, mW, vW, bias, mb, vb, \
-                     a, dW_out, db_out, (bf16x8*)Wk_out, (bf16x8*)Wr_out, bias_pad_out)
+                     a, dW_out, db_out, (bf16x8*)Wk_out, (bf16x8*)Wr_out, bias_pad_out, tl.nfull, tl.tsplit, tail_dw, \
+                     tail_db)
 #define FT(HFV)          \
   if (terms == 9) {      \
     FW(HFV, 9);          \
@@ -1245,8 +1340,40 @@ extern "C" int rg_flash_dw_adam_planes(const void* Hk, const void* Hr, const voi
   }
 #undef FT
 #undef FW
+  if (tl.ntail) {
+    const int i0 = tl.nfull * rpb;
+    hipLaunchKernelGGL(k_flash_tail, dim3((unsigned)(((int64_t)tl.ntail * HF + 255) / 256)), dim3(256), 0, stream,
+                       tail_dw, tail_db, tl.tsplit, i0, tl.ntail, HF, W, mW, vW, bias, mb, vb, a, dW_out, db_out);
+    if (Wk_out && !dW_out) {   // the leftover rows' planes and padded bias, from the updated W / b
+      const int ap = (A + 31) / 32 * 32;
+      const float* Xs = W + (int64_t)i0 * HF;
+      bf16x8* Pk = (bf16x8*)Wk_out + (int64_t)(i0 / 32) * (HF / 16) * 192;
+      bf16x8* Pr = (bf16x8*)Wr_out + (int64_t)(i0 / 32) * (HF / 32) * 2 * 192;
+      const int rows = A - i0, rp = ap - i0;
+      const unsigned gk = (unsigned)(((int64_t)rp * (HF / 8) + 255) / 256);
+      const unsigned gr = (unsigned)(((int64_t)(rp / 32) * (HF / 32) * 2 * 64 + 255) / 256);
+#define PLT(HFV)                                                                                   \
+  hipLaunchKernelGGL(k_planes_k<HFV>, dim3(gk), dim3(256), 0, stream, Xs, rows, rp, Pk);          \
+  hipLaunchKernelGGL(k_planes_r<HFV>, dim3(gr), dim3(256), 0, stream, Xs, rows, rp, Pr)
+      switch (HF) {
+        case 32: PLT(32); break;
+        case 64: PLT(64); break;
+        case 128: PLT(128); break;
+        case 256: PLT(256); break;
+      }
+#undef PLT
+      hipLaunchKernelGGL(k_pad_bias, dim3((rp + 255) / 256), dim3(256), 0, stream, bias + i0, rows, rp,
+                         bias_pad_out + i0);
+    }
+  }
   RG_LAUNCH_CHECK();
   return RG_OK;
+}
+
+extern "C" int64_t rg_flash_dw_work_bytes(int B, int A, int HF) {
+  if (B <= 0 || A <= 0 || (B % 32) || !flash_hf_ok(HF)) return RG_ERR_ARG;
+  const FlTail tl = fl_tail(B, A, HF);
+  return (int64_t)tl.tsplit * tl.ntail * (HF + 1) * 4;
 }
 
 extern "C" int rg_flash_dw_adam(const void* Hk, const void* Hr, const void* Wk, const float* bias_pad,
@@ -1254,7 +1381,7 @@ extern "C" int rg_flash_dw_adam(const void* Hk, const void* Hr, const void* Wk, 
                                 float* mW, float* vW, float* bias, float* mb, float* vb, const float* adam6,
                                 float* dW_out, float* db_out, hipStream_t stream) {
   return rg_flash_dw_adam_planes(Hk, Hr, Wk, bias_pad, rowinfo, gscale, B, A, HF, terms, W, mW, vW, bias, mb, vb, adam6,
-                                 dW_out, db_out, nullptr, nullptr, nullptr, stream);
+                                 dW_out, db_out, nullptr, nullptr, nullptr, nullptr, 0, stream);
 }
 
 // Exact argmax through screening (the double-Q target of SQN / SMORL at the

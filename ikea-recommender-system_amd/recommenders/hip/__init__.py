@@ -23,7 +23,8 @@ I32 = C.c_int32
 U64 = C.c_uint64
 
 # entry points returning int64_t (all others return int)
-RESTYPE_I64 = {"rg_sampled_work_bytes", "rg_head_work_bytes", "rg_head_plane_bytes", "rg_gru_wide_work_bytes", "rg_scatter_rows_work_bytes"}
+RESTYPE_I64 = {"rg_sampled_work_bytes", "rg_head_work_bytes", "rg_head_plane_bytes", "rg_gru_wide_work_bytes",
+               "rg_scatter_rows_work_bytes", "rg_flash_dw_work_bytes"}
 
 # name -> argtypes
 SIGNATURES = {
@@ -61,7 +62,8 @@ SIGNATURES = {
     "rg_flash_rows": [P, P, I64, I, I, P, P],
     "rg_flash_dh": [P, P, P, I, P, F, I, I, P, P],
     "rg_flash_dw_adam": [P, P, P, P, P, F, I, I, I, I, P, P, P, P, P, P, P, P, P, P],
-    "rg_flash_dw_adam_planes": [P, P, P, P, P, F, I, I, I, I, P, P, P, P, P, P, P, P, P, P, P, P, P],
+    "rg_flash_dw_adam_planes": [P, P, P, P, P, F, I, I, I, I, P, P, P, P, P, P, P, P, P, P, P, P, P, I64, P],
+    "rg_flash_dw_work_bytes": [I, I, I],
     "rg_lse_combine": [P, P, P, I, I, P, P, I64, P, I, P, P, P, P, P],
     "rg_sum_scale": [P, I, F, P, P, P],
     "rg_lse_merge_ranks": [P, I, I, P, P],

@@ -492,6 +492,9 @@ class _FlashWS:
         self.pm, self.pl = z(self.nsplit, B), z(self.nsplit, B)
         self.pO = z(self.nsplit, HF, B)
         self.rows = z(B, 2)
+        # pass 2's split-tail partials (rg_flash_dw_work_bytes; 0 when the grid has no tail to split)
+        self.dw_work_bytes = int(call("rg_flash_dw_work_bytes", B, A, HF)) if PASS2_TAIL_SPLIT else 0
+        self.dw_work = u8(max(self.dw_work_bytes, 16))
         self.lse, self.zt, self.loss_row = z(B), z(B), z(B)
         self.loss = torch.zeros(1, device=device)
         self.pbest = self.parg = self.cmax = self.cand = self.ncand = None
@@ -542,6 +545,8 @@ class _AmaxWS:
 SPLIT_TERMS = {"f32x9": 9, "f32x6": 6, "f32x6d3": 636}
 # RG_PASS2_PLANES=0: pass 2 leaves W's operand planes to the next rg_head_planes (A/B measurement)
 PASS2_PLANES = os.environ.get("RG_PASS2_PLANES", "1") != "0"
+# RG_PASS2_TAIL=0: pass 2's leftover item blocks run as a partial last round (A/B measurement)
+PASS2_TAIL_SPLIT = os.environ.get("RG_PASS2_TAIL", "1") != "0"
 # split-bf16 argmax (SQN / SMORL double-Q target): screening on 3 plane products, then every item
 # of every 32-item chunk whose screened maximum lies within SCREEN_TOL·||h_b||·max_a||W_a|| of the
 # row's best is re-scored in fp32 (first maximum).  The bound covers the dropped plane products
@@ -749,7 +754,8 @@ class SoftmaxHead:
             call("rg_flash_dw_adam_planes", w.Hk.data_ptr(), w.Hr.data_ptr(), w.Wk.data_ptr(),
                  w.bias_pad.data_ptr(), w.rows.data_ptr(), g, w.B, self.A, self.HF, w.terms, Wp.p.data_ptr(),
                  Wp.m.data_ptr(), Wp.v.data_ptr(), bp.p.data_ptr(), bp.m.data_ptr(), bp.v.data_ptr(), adam6, None,
-                 None, w.Wk.data_ptr(), w.Wr.data_ptr(), w.bias_pad.data_ptr(), stream_ptr())
+                 None, w.Wk.data_ptr(), w.Wr.data_ptr(), w.bias_pad.data_ptr(), w.dw_work.data_ptr(),
+                 w.dw_work_bytes, stream_ptr())
         self._wgen += 1
         w.wgen = self._wgen
 

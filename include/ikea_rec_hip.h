@@ -197,11 +197,15 @@ int rg_flash_dw_adam(const void* Hk, const void* Hr, const void* Wk, const float
  * planes (Wk_out / Wr_out, rg_head_planes layout; Wk_out may be Wk — a workgroup reads and
  * rewrites only its own items) and the updated bias into bias_pad_out (pad entries untouched):
  * rg_head_planes of the new W is then not needed before the next rg_flash_fwd.  Wk_out, Wr_out
- * and bias_pad_out together or all NULL; not with dW_out. */
+ * and bias_pad_out together or all NULL; not with dW_out.  work (rg_flash_dw_work_bytes(B, A, HF)
+ * bytes; optional): the item blocks past the last whole round of 256 workgroups are then split
+ * over the row chunks (partial dW / db summed in order by a finishing kernel). */
 int rg_flash_dw_adam_planes(const void* Hk, const void* Hr, const void* Wk, const float* bias_pad,
                             const void* rowinfo, float gscale, int B, int A, int HF, int terms, float* W, float* mW,
                             float* vW, float* bias, float* mb, float* vb, const float* adam6, float* dW_out,
-                            float* db_out, void* Wk_out, void* Wr_out, float* bias_pad_out, rg_stream_t stream);
+                            float* db_out, void* Wk_out, void* Wr_out, float* bias_pad_out, void* work,
+                            int64_t work_bytes, rg_stream_t stream);
+int64_t rg_flash_dw_work_bytes(int B, int A, int HF);
 /* rg_head_fwd_x from h's planes (rg_head_work_bytes layout) with the rows split
  * over workgroups: rpb rows per workgroup (multiple of 32), parg optional.
  * The sampled softmax's split forward (rg_sampled_fwd_x) runs on it with the

@@ -60,7 +60,7 @@ def run_flash(h, W, b, tgt, terms, nsplit, lo=0, lse_global=None, A_full=None):
 
 
 @pytest.mark.parametrize("B,A,HF", [(64, 1000, 32), (96, 3001, 64), (128, 4133, 128), (64, 2077, 256),
-                                    (64, 20011, 64), (96, 40009, 128)])
+                                    (64, 20011, 64), (96, 40009, 128), (96, 78341, 64)])
 def test_pass2_writes_next_planes(B, A, HF):
     """rg_flash_dw_adam_planes: the updated W / b leave as operand planes and
     padded bias bit-identical to rg_head_planes of the updated tensors (what
@@ -94,13 +94,16 @@ def test_pass2_writes_next_planes(B, A, HF):
                 Wx.data_ptr(), mW.data_ptr(), vW.data_ptr(), bx.data_ptr(), mb.data_ptr(), vb.data_ptr(), adam6,
                 None, None]
         if planes:
-            call("rg_flash_dw_adam_planes", *args, Wk2.data_ptr(), Wr2.data_ptr(), bp2.data_ptr(), st)
+            nb = call("rg_flash_dw_work_bytes", B, A, HF)
+            work = _u8(max(nb, 16))
+            call("rg_flash_dw_adam_planes", *args, Wk2.data_ptr(), Wr2.data_ptr(), bp2.data_ptr(), work.data_ptr(),
+                 nb, st)
         else:
             call("rg_flash_dw_adam", *args, st)
         torch.cuda.synchronize()
         outs.append((Wx, bx, mW, vW, mb, vb, Wk2, Wr2, bp2))
-    for x, y in zip(outs[0][:6], outs[1][:6]):
-        assert torch.equal(x, y)
+    for x, y in zip(outs[0][:6], outs[1][:6]):   # (the tail split sums in another order: allclose)
+        torch.testing.assert_close(x, y, rtol=1e-5, atol=1e-6)
     Wx, bx = outs[1][0], outs[1][1]
     Wk3, Wr3, bp3 = _u8(wb), _u8(wb), torch.empty_like(bp)
     call("rg_head_planes", Wx.data_ptr(), A, HF, Wk3.data_ptr(), Wr3.data_ptr(), bx.data_ptr(), bp3.data_ptr(), st)
@@ -109,6 +112,38 @@ def test_pass2_writes_next_planes(B, A, HF):
     assert torch.equal(outs[1][6], Wk3)
     assert torch.equal(outs[1][7], Wr3)
     assert torch.equal(outs[1][8], bp3)
+
+
+@pytest.mark.parametrize("B,A,HF", [(96, 78341, 64), (128, 78341, 64), (64, 70000, 128)])
+def test_pass2_tail_split_matches_fp64(B, A, HF):
+    """Pass 2 with its leftover item blocks split over the row chunks
+    (rg_flash_dw_adam_planes with work; 306 blocks of 256 = 256 whole + 50
+    split 3 / 4 ways, HF 64; 274 = 256 + 18 at HF 128): raw dW / db against
+    fp64 at the fused head's tolerances, and nonzero split work."""
+    call, st = C().call, C().stream_ptr()
+    nb = call("rg_flash_dw_work_bytes", B, A, HF)
+    assert nb > 0
+    h, W, b, tgt = inputs(B, A, HF, 17)
+    r = fp64_reference(h, W, b, tgt)
+    h, W, b, tgt = h.to(dev), W.to(dev), b.to(dev), tgt.to(dev)
+    o = run_flash(h, W, b, tgt, 6, 8)   # dh, lse via the plain path (no tail split)
+    hb, wb = call("rg_head_plane_bytes", B, HF), call("rg_head_plane_bytes", A, HF)
+    Hk, Hr, Wk, Wr = _u8(hb), _u8(hb), _u8(wb), _u8(wb)
+    bp = torch.empty((A + 31) // 32 * 32, device=dev)
+    call("rg_head_planes", h.data_ptr(), B, HF, Hk.data_ptr(), Hr.data_ptr(), None, None, st)
+    call("rg_head_planes", W.data_ptr(), A, HF, Wk.data_ptr(), Wr.data_ptr(), b.data_ptr(), bp.data_ptr(), st)
+    rows = torch.empty(B, 2, device=dev)
+    call("rg_flash_rows", o["lse"].float().to(dev).data_ptr(), tgt.data_ptr(), 0, A, B, rows.data_ptr(), st)
+    dW = torch.full((A, HF), float("nan"), device=dev)
+    db = torch.full((A,), float("nan"), device=dev)
+    work = _u8(nb)
+    g = float(np.float32(1.0 / B))
+    call("rg_flash_dw_adam_planes", Hk.data_ptr(), Hr.data_ptr(), Wk.data_ptr(), bp.data_ptr(), rows.data_ptr(), g, B,
+         A, HF, 6, None, None, None, None, None, None, None, dW.data_ptr(), db.data_ptr(), None, None, None,
+         work.data_ptr(), nb, st)
+    torch.cuda.synchronize()
+    torch.testing.assert_close(dW.cpu().double(), r["dW"], rtol=0, atol=1e-7)
+    torch.testing.assert_close(db.cpu().double(), r["db"], rtol=0, atol=1e-7)
 
 
 def fp64_reference(h, W, b, tgt):

@@ -41,6 +41,8 @@ dh = torch.empty(B, H, device=dev)
 adam6 = host_floats([0.1, 0.999, 0.001, 0.0316, 1e-8, -1e-9])  # tiny step: W stays put
 st = stream_ptr()
 gs = 1.0 / B
+dwb = call("rg_flash_dw_work_bytes", B, A, H)
+dww = u8(max(dwb, 16))
 call("rg_head_planes", h.data_ptr(), B, H, Hk.data_ptr(), Hr.data_ptr(), None, None, st)
 fl = 2.0 * B * A * H
 for terms in a.terms:
@@ -58,7 +60,7 @@ for terms in a.terms:
         "pass2": lambda: call("rg_flash_dw_adam_planes", Hk.data_ptr(), Hr.data_ptr(), Wk.data_ptr(), bp.data_ptr(),
                               rows.data_ptr(), gs, B, A, H, terms, W.data_ptr(), mW.data_ptr(), vW.data_ptr(),
                               bias.data_ptr(), mb.data_ptr(), vb.data_ptr(), adam6, None, None, Wk.data_ptr(),
-                              Wr.data_ptr(), bp.data_ptr(), st),
+                              Wr.data_ptr(), bp.data_ptr(), dww.data_ptr(), dwb, st),
     }
     for name, fn in stages.items():
         fn()
