@@ -516,15 +516,22 @@ class _AmaxWS:
         u8 = lambda n: torch.empty(int(n), dtype=torch.uint8, device=device)  # noqa: E731
         z = lambda *s, dt=torch.float32: torch.empty(*s, dtype=dt, device=device)  # noqa: E731
         self.B, self.screen = B, screen
-        nrb = -(-B // call("rg_flash_rows_per_block", HF))
-        self.nsplit = _round_up(min(max(1, 256 // nrb), -(-A // 32)), 8)
+        rpb = call("rg_flash_rows_per_block", HF)
+        nct = -(-A // 32)
+        # screening runs over row chunks of Bc rows (all B when the chunk maxima fit
+        # SCREEN_CMAX_BYTES; else 2048-row chunks, 16 row blocks × 16 splits at HF 128)
+        self.Bc = B
+        if screen and nct * B * 4 > SCREEN_CMAX_BYTES:
+            self.Bc = min(B, SCREEN_ROW_CHUNK)
+        nrb = -(-self.Bc // rpb)
+        self.nsplit = _round_up(min(max(1, 256 // nrb), nct), 8)
         self.Hk = u8(call("rg_head_plane_bytes", B, HF))
         self.Wk = u8(call("rg_head_plane_bytes", A, HF))
         self.bias_pad = z(_round_up(A, 32))
-        self.pbest, self.parg = z(self.nsplit, B), z(self.nsplit, B, dt=torch.int32)
+        self.pbest, self.parg = z(self.nsplit, self.Bc), z(self.nsplit, self.Bc, dt=torch.int32)
         self.amax, self.mx = z(B, dt=torch.int32), z(B)
         if screen:
-            self.cmax = z(-(-A // 32), B)
+            self.cmax = z(nct, self.Bc)
             self.cand = z(B, call("rg_flash_topk_cap"), dt=torch.int32)
             self.ncand = z(B, dt=torch.int32)
             self.wnorm, self.lim = z(1), z(B)
@@ -551,11 +558,12 @@ PASS2_TAIL_SPLIT = os.environ.get("RG_PASS2_TAIL", "1") != "0"
 # of every 32-item chunk whose screened maximum lies within SCREEN_TOL·||h_b||·max_a||W_a|| of the
 # row's best is re-scored in fp32 (first maximum).  The bound covers the dropped plane products
 # (3·2^-18), fp32 accumulation of both sums (384 + 128 terms at 2^-24) on both sides, with margin
-# (DESIGN §4a).  Needs ceil(A/32)·B floats of chunk maxima; above SCREEN_CMAX_BYTES (or with
-# RG_SCREEN_ARGMAX=0) the 6-product argmax runs instead.
+# (DESIGN §4a).  Needs ceil(A/32)·B floats of chunk maxima; above SCREEN_CMAX_BYTES the rows
+# are screened in 2048-row chunks (C5 at one GPU); RG_SCREEN_ARGMAX=0 runs the 6-product argmax.
 SCREEN_ARGMAX = os.environ.get("RG_SCREEN_ARGMAX", "1") != "0"
 SCREEN_TOL = 1e-4
 SCREEN_CMAX_BYTES = 2 << 30
+SCREEN_ROW_CHUNK = 2048
 LOGIT_TERMS = {"f32x9": 9, "f32x6": 6, "f32x6d3": 6}
 PRECISIONS = ("f32",) + tuple(SPLIT_TERMS)
 
@@ -836,7 +844,7 @@ class SoftmaxHead:
         if terms:
             # screening (3 plane products + exact fp32 re-scoring of the chunks
             # within the error bound) unless its chunk maxima would not fit
-            screen = SCREEN_ARGMAX and -(-self.A // 32) * B * 4 <= SCREEN_CMAX_BYTES
+            screen = SCREEN_ARGMAX
             w = self._aws.get(slot) if hasattr(self, "_aws") else None
             if w is None or w.B != B or w.screen != screen:
                 if not hasattr(self, "_aws"):
@@ -846,19 +854,25 @@ class SoftmaxHead:
             W, b = self.W.p.data_ptr(), self.b.p.data_ptr()
             call("rg_head_planes", h.data_ptr(), B, self.HF, w.Hk.data_ptr(), None, None, None, st)
             call("rg_head_planes", W, self.A, self.HF, w.Wk.data_ptr(), None, b, w.bias_pad.data_ptr(), st)
-            if screen:
-                call("rg_flash_amax_screen", w.Hk.data_ptr(), w.Wk.data_ptr(), w.bias_pad.data_ptr(), B, self.A,
-                     self.HF, w.nsplit, w.pbest.data_ptr(), w.parg.data_ptr(), w.cmax.data_ptr(), st)
-            else:
+            if not screen:
                 call("rg_flash_amax_fwd", w.Hk.data_ptr(), w.Wk.data_ptr(), w.bias_pad.data_ptr(), B, self.A, self.HF,
                      terms, w.nsplit, w.pbest.data_ptr(), w.parg.data_ptr(), st)
-            call("rg_flash_argmax", w.pbest.data_ptr(), w.parg.data_ptr(), w.nsplit, B, w.amax.data_ptr(),
-                 w.mx.data_ptr(), st)
-            if screen:
+                call("rg_flash_argmax", w.pbest.data_ptr(), w.parg.data_ptr(), w.nsplit, B, w.amax.data_ptr(),
+                     w.mx.data_ptr(), st)
+            else:
                 call("rg_row_norm_max", W, self.A, self.HF, w.wnorm.data_ptr(), st)
-                call("rg_flash_argmax_exact", w.cmax.data_ptr(), B, self.A, h.data_ptr(), W, b, self.HF,
-                     w.wnorm.data_ptr(), _f32(SCREEN_TOL), w.lim.data_ptr(), w.cand.data_ptr(), w.ncand.data_ptr(),
-                     w.amax.data_ptr(), w.mx.data_ptr(), st)
+                hk_row = self.HF * 6   # K-plane bytes per row
+                for r0 in range(0, B, w.Bc):
+                    bc = min(w.Bc, B - r0)
+                    call("rg_flash_amax_screen", w.Hk.data_ptr() + r0 * hk_row, w.Wk.data_ptr(),
+                         w.bias_pad.data_ptr(), bc, self.A, self.HF, w.nsplit, w.pbest.data_ptr(),
+                         w.parg.data_ptr(), w.cmax.data_ptr(), st)
+                    call("rg_flash_argmax", w.pbest.data_ptr(), w.parg.data_ptr(), w.nsplit, bc,
+                         w.amax.data_ptr() + 4 * r0, w.mx.data_ptr() + 4 * r0, st)
+                    call("rg_flash_argmax_exact", w.cmax.data_ptr(), bc, self.A, h.data_ptr() + 4 * r0 * self.HF, W, b,
+                         self.HF, w.wnorm.data_ptr(), _f32(SCREEN_TOL), w.lim.data_ptr() + 4 * r0,
+                         w.cand.data_ptr() + 4 * r0 * call("rg_flash_topk_cap"), w.ncand.data_ptr() + 4 * r0,
+                         w.amax.data_ptr() + 4 * r0, w.mx.data_ptr() + 4 * r0, st)
             self.argmax_mx = w.mx
             return w.amax
         w = self.ws(slot, B, False)

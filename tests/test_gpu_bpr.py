@@ -110,7 +110,8 @@ def test_bpr_invalid_target_gives_nan_row():
 @pytest.mark.parametrize("kind,precision,E,N,L,B,S", [("gru4rec", "f32", 32, 3000, 10, 256, 512),
                                                       ("gru4rec", "f32x6", 128, 50000, 50, 1024, 2048),
                                                       ("bidir", "f32", 32, 5000, 12, 200, 256),
-                                                      ("bidir", "f32x6", 64, 20000, 20, 512, 1024)])
+                                                      ("bidir", "f32x6", 64, 20000, 20, 512, 1024),
+                                                      ("bidir", "f32x6d3", 64, 20000, 20, 512, 1024)])
 def test_bpr_trainer_matches_oracle(kind, precision, E, N, L, B, S):
     from oracle.models import OracleSupervised
     from recommenders.data_utils.synthetic import SessionStream

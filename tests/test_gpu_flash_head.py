@@ -553,3 +553,28 @@ def test_screening_argmax_overflow_keeps_first():
     Z = h.double() @ W.double().t()
     ok = torch.arange(B) != 7
     assert torch.equal(idx.cpu().long()[ok], Z.argmax(1)[ok])
+
+
+def test_screening_argmax_row_chunks_match(monkeypatch):
+    """SoftmaxHead.argmax on the split path: screening in row chunks (what C5
+    at one GPU does when the chunk maxima would exceed SCREEN_CMAX_BYTES)
+    gives the same items and values as one whole-batch screening, and both
+    equal the fp64 first maximum away from fp32 rounding ties."""
+    from recommenders.hip import engine
+    B, A, HF = 1024, 20000, 128
+    hd = engine.SoftmaxHead("x", A, HF, dev)
+    hd.set_matmul_precision("f32x6")
+    g = torch.Generator().manual_seed(3)
+    h = torch.tanh(torch.randn(B, HF, generator=g)).to(dev)
+    i1 = hd.argmax(h, slot="a").clone()
+    v1 = hd.argmax_mx.clone()
+    monkeypatch.setattr(engine, "SCREEN_CMAX_BYTES", 1)
+    monkeypatch.setattr(engine, "SCREEN_ROW_CHUNK", 256)
+    i2 = hd.argmax(h, slot="b").clone()
+    v2 = hd.argmax_mx.clone()
+    assert hd._aws["b"].Bc == 256
+    assert torch.equal(i1, i2) and torch.equal(v1, v2)
+    Z = h.double().cpu() @ hd.W.p.double().cpu().t() + hd.b.p.double().cpu()
+    zmax = Z.max(1).values
+    gap = zmax - Z[torch.arange(B), i1.cpu().long()]
+    assert float(gap.max()) <= 1e-5

@@ -162,7 +162,7 @@ def test_split_precision_error_is_fp32_class():
     assert errs["f32x6"] <= 3.0 * errs["f32"] + 1e-9, errs
 
 
-@pytest.mark.parametrize("precision", ["f32x9", "f32x6"])
+@pytest.mark.parametrize("precision", ["f32x9", "f32x6", "f32x6d3"])
 def test_split_precision_trainer_matches_oracle(precision):
     """GRU4Rec at C2 shapes (scaled down) with the sampled head on the split
     GEMM: same loss / weight tolerances as the native path."""
