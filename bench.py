@@ -398,13 +398,13 @@ def main():
             del tr
             torch.cuda.empty_cache()
             if not args.no_native_side and args.precision != "f32":
-                # the trainers' default arithmetic (native fp32 MFMA head), short side run
+                # the native fp32 MFMA head (precision "f32"), short side run
                 trn = make_trainer("c2native", args, dev, False)
                 trn.set_train()
                 dtn, _, _, psn = timed_run(trn, batches, 2, min(10, args.steps), 1, False, "c2")
                 native = {"value": round(B * min(10, args.steps) / dtn, 2),
                           "ms_per_step": round(dtn / min(10, args.steps) * 1e3, 3), "matmul_precision": "f32",
-                          "note": "trainer default arithmetic (native fp32 MFMA head), 10 steps"}
+                          "note": "native fp32 MFMA head (matmul_precision f32), 10 steps"}
                 del trn
                 torch.cuda.empty_cache()
             if not args.no_target and kern:

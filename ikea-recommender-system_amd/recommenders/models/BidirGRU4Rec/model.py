@@ -34,7 +34,7 @@ class BidirGRU4Rec_trainer:
     def __init__(self, hidden_dim, embedding_dim, gru_layers, dropout, train_pad_embed, use_packed_seq,
                  learning_rate, item_num, state_size, action_dim, device, padding_idx=None, torch_rand_seed=118,
                  python_rand_seed=999, n_negatives=None, neg_seed=0, fp16_embeddings=False,
-                 matmul_precision="f32", sampled_loss="ce"):
+                 matmul_precision="f32x6d3", sampled_loss="ce"):
         torch.manual_seed(torch_rand_seed)
         random.seed(python_rand_seed)
         self.device = require_gpu(device)

@@ -105,7 +105,7 @@ class GRU4Rec_trainer:
     def __init__(self, hidden_dim, embedding_dim, gru_layers, train_pad_embed, use_packed_seq, learning_rate,
                  item_num, state_size, action_dim, device, padding_idx=None, torch_rand_seed=118,
                  python_rand_seed=999, shard_items=False, process_group=None, n_negatives=None, neg_seed=0,
-                 fp16_embeddings=False, matmul_precision="f32", sampled_loss="ce"):
+                 fp16_embeddings=False, matmul_precision="f32x6d3", sampled_loss="ce"):
         torch.manual_seed(torch_rand_seed)
         random.seed(python_rand_seed)
         self.device = require_gpu(device)
@@ -125,8 +125,10 @@ class GRU4Rec_trainer:
                                  padding_idx=padding_idx, device=self.device, comm=self.comm,
                                  n_negatives=n_negatives, neg_seed=neg_seed, fp16_embeddings=fp16_embeddings,
                                  sampled_loss=sampled_loss)
-        # matmul_precision (build extension): "f32" (default, native fp32 MFMA)
-        # or the split-bf16 "f32x9" / "f32x6" head GEMMs (hip/engine.py)
+        # matmul_precision (build extension): "f32x6d3" (default: the fused
+        # split-bf16 head, fp32-class — every output within 2x of the reference
+        # CPU fp32 path's error against fp64), "f32x6" / "f32x9", or
+        # "f32" (native fp32 MFMA, logits stored) (hip/engine.py)
         self.gru_model.set_matmul_precision(matmul_precision)
         self.learning_rate = learning_rate
         self.cross_entropy_loss = nn.CrossEntropyLoss(weight=None, reduction="mean")

@@ -48,7 +48,7 @@ class SMORL_trainer:
                  unpopular_actions_set, topk_div, device, input_tokenizer=None, output_tokenizer=None,
                  padding_idx=None, torch_rand_seed=118, python_rand_seed=999, name_1="SMORL_1", name_2="SMORL_2",
                  topk_nov=1, nov_rew_sig=1, shard_items=False, process_group=None, fp16_embeddings=False,
-                 matmul_precision="f32"):
+                 matmul_precision="f32x6d3"):
         torch.manual_seed(torch_rand_seed)
         random.seed(python_rand_seed)
         self.device = require_gpu(device)
@@ -62,7 +62,8 @@ class SMORL_trainer:
         self.SMORL_1 = mk(name_1)
         self.SMORL_2 = mk(name_2)
         # matmul_precision (build extension): arithmetic of the supervised head
-        # GEMMs, "f32" native fp32 MFMA or split-bf16 "f32x9" / "f32x6"
+        # and the Q argmax, split-bf16 "f32x6d3" (default, fp32-class) / "f32x6" /
+        # "f32x9", or "f32" native fp32 MFMA (GRU4Rec/model.py)
         for net in (self.SMORL_1, self.SMORL_2):
             net.set_matmul_precision(matmul_precision)
             # the rewards read the supervised logits' top-k after the CE forward

@@ -42,7 +42,7 @@ class SQN_trainer:
     def __init__(self, hidden_dim, embedding_dim, train_pad_embed, use_packed_seq, learning_rate, item_num,
                  state_size, action_dim, gamma, gru_layers, device, padding_idx=None, torch_rand_seed=118,
                  python_rand_seed=999, name_1="SQN_1", name_2="SQN_2", shard_items=False, process_group=None,
-                 fp16_embeddings=False, matmul_precision="f32"):
+                 fp16_embeddings=False, matmul_precision="f32x6d3"):
         torch.manual_seed(torch_rand_seed)
         random.seed(python_rand_seed)
         self.device = require_gpu(device)
@@ -57,7 +57,8 @@ class SQN_trainer:
         self.DQN_1 = mk(name_1)
         self.DQN_2 = mk(name_2)
         # matmul_precision (build extension): arithmetic of the supervised head
-        # GEMMs, "f32" native fp32 MFMA or split-bf16 "f32x9" / "f32x6"
+        # and the Q argmax, split-bf16 "f32x6d3" (default, fp32-class) / "f32x6" /
+        # "f32x9", or "f32" native fp32 MFMA (GRU4Rec/model.py)
         for net in (self.DQN_1, self.DQN_2):
             net.set_matmul_precision(matmul_precision)
         self.gamma = gamma
