@@ -97,9 +97,6 @@ __global__ __launch_bounds__(64 * HX_WAVES_OF(HF)) void k_head_fwd_x(const bf16x
   // to itself the compiler sinks it next to its LDS commit, which exposes
   // the full L2 latency every chunk)
   auto load_chunk = [&](int c) __attribute__((always_inline)) {
-#ifdef HX_DIAG_NOLOAD
-    if (c > 1) return;
-#endif
 #pragma unroll
     for (int q = 0; q < EPT; ++q) {
       const int e = tid + 64 * NW * q;
@@ -108,9 +105,6 @@ __global__ __launch_bounds__(64 * HX_WAVES_OF(HF)) void k_head_fwd_x(const bf16x
     __builtin_amdgcn_sched_barrier(0);
   };
   auto store_chunk = [&](int buf) __attribute__((always_inline)) {
-#ifdef HX_DIAG_NOLOAD
-    if (nch < 0) return;
-#endif
 #pragma unroll
     for (int q = 0; q < EPT; ++q) {
       const int e = tid + 64 * NW * q;
@@ -173,11 +167,9 @@ __global__ __launch_bounds__(64 * HX_WAVES_OF(HF)) void k_head_fwd_x(const bf16x
         if (r < 16) {
           const float z = acc[r] + bj[r];
           acc[r] = z;
-#ifndef HX_DIAG_NOSTORE
           if (SZ)
             __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(z), zrs, zlane,
                                                   ((r & 3) + 8 * (r >> 2)) * zrow4 + (rbase + 32 * cc) * 4, 0);
-#endif
           const bool gt = z > em;
           em = gt ? z : em;
           ea = gt ? jw + acc32_row(r, half) : ea;
@@ -212,30 +204,9 @@ __global__ __launch_bounds__(64 * HX_WAVES_OF(HF)) void k_head_fwd_x(const bf16x
       const bf16x8 b0 = hs[buf][0][j][half][l32];
       const bf16x8 b1 = hs[buf][1][j][half][l32];
       const bf16x8 b2 = hs[buf][2][j][half][l32];
-#ifndef HX_DIAG_NOMFMA
       acc = mfma_split<NT>(a0[j], a1[j], a2[j], b0, b1, b2, acc);
-#else
-      acc[0] += (float)b0[0] + (float)b1[1] + (float)b2[2];
-#endif
-#ifndef HX_DIAG_NOEPI
       if (epi) epi_slice(prev, cprev, j);
-#else
-      if (epi && j == 0) em += prev[0];  // keeps the MFMA chain live
-#endif
-#if defined(HX_SGB)
-      // one MFMA, then up to four VALU, repeated: the epilogue's vector work
-      // issues in the MFMAs' shadow instead of as a burst after them
-      __builtin_amdgcn_sched_group_barrier(0x100, 3, 0);
-#pragma unroll
-      for (int t = 0; t < NT; ++t) {
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-        __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);
-      }
-      __builtin_amdgcn_sched_group_barrier(0x040, 2, 0);
       __builtin_amdgcn_sched_barrier(0);
-#elif !defined(HX_NO_SLICE_SB)
-      __builtin_amdgcn_sched_barrier(0);
-#endif
     }
   };
   f16v accA = {}, accB = {};

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Build an A/B variant library with one csrc file recompiled under extra
-# flags (e.g. -DSX_DIAG_NOSTORE).  Usage:
+# flags (e.g. -DADAM_U=2).  Usage:
 #   tools/build_variant.sh NAME FILE.hip [extra hipcc flags]
 # -> variants/lib_NAME.so (select at run time with IKEA_REC_HIP_LIB=...)
 set -e
