@@ -2,8 +2,24 @@
 // SQN / SMORL training path.  Wave64 everywhere; fp32 data; exact-f32 MFMA
 // (v_mfma_f32_32x32x2_f32 / v_mfma_f32_16x16x4_f32, bitwise an fmaf chain).
 #pragma once
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+
+// Kernel-exact timing (bench.py's single-kernel regions, rg_timing_events):
+// when armed, the next RG_TLAUNCH launch records the two events at its
+// dispatch packet's start / end (hipExtLaunchKernelGGL) and disarms them, so
+// the measured duration excludes the event-record commands around it.
+extern hipEvent_t rg_tev0, rg_tev1;
+#define RG_TLAUNCH(K, G, BK, SH, ST, ...)                                                \
+  do {                                                                                   \
+    if (rg_tev0 != nullptr) {                                                            \
+      hipExtLaunchKernelGGL(K, G, BK, SH, ST, rg_tev0, rg_tev1, 0u, __VA_ARGS__);        \
+      rg_tev0 = rg_tev1 = nullptr;                                                       \
+    } else {                                                                             \
+      hipLaunchKernelGGL(K, G, BK, SH, ST, __VA_ARGS__);                                 \
+    }                                                                                    \
+  } while (0)
 
 typedef float f4 __attribute__((ext_vector_type(4)));
 typedef float f16v __attribute__((ext_vector_type(16)));

@@ -95,3 +95,16 @@ extern "C" int rg_remap_ids(const int32_t* idx, int64_t n, const int32_t* lut, i
 // items per online-softmax partial block of rg_head_fwd (pmax/psum/parg are
 // ceil(A / rg_partial_block()) × B)
 extern "C" int rg_partial_block(void) { return RG_PBLK; }
+
+hipEvent_t rg_tev0 = nullptr, rg_tev1 = nullptr;
+
+// arm (or, with NULLs, disarm) kernel-exact timing for the next RG_TLAUNCH
+// launch; returns 1 when the previous arming was still pending (no RG_TLAUNCH
+// launch consumed it), else 0
+extern "C" int rg_timing_events(void* start, void* stop) {
+  if ((start == nullptr) != (stop == nullptr)) return RG_ERR_ARG;
+  const int pending = rg_tev0 != nullptr ? 1 : 0;
+  rg_tev0 = (hipEvent_t)start;
+  rg_tev1 = (hipEvent_t)stop;
+  return pending;
+}

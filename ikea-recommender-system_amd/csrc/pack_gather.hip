@@ -299,8 +299,8 @@ static bool launch_gather_e(const int64_t* s, int B, int L, const int32_t* perm,
                             int32_t* tok_id, float* X, int32_t* err, hipStream_t stream) {
   if (L > GW_MAXL) return false;
 #define GE(EV)                                                                                              \
-  hipLaunchKernelGGL((k_gather_e<TE, EV>), dim3((B + GW_ROWS - 1) / GW_ROWS), dim3(256), 0, stream, s, B, L, \
-                     perm, lsort, offs, emb, n_rows, reverse, tok_id, X, err)
+  RG_TLAUNCH((k_gather_e<TE, EV>), dim3((B + GW_ROWS - 1) / GW_ROWS), dim3(256), 0, stream, s, B, L, perm, lsort, \
+             offs, emb, n_rows, reverse, tok_id, X, err)
   switch (E) {
     case 32: GE(32); return true;
     case 64: GE(64); return true;

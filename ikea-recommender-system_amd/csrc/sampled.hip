@@ -503,10 +503,10 @@ extern "C" int rg_sampled_logits(const float* h, const float* W, const float* bi
   const dim3 grid((unsigned)((S + SF_NEG - 1) / SF_NEG), (unsigned)((B + SF_ROWS - 1) / SF_ROWS));
 #define SFG(HFV, NTV)                                                                                            \
   if (draw)                                                                                                        \
-    hipLaunchKernelGGL((k_sampled_logits<HFV, NTV, true>), grid, dim3(512), 0, stream, h, W, bias, neg, seed,     \
+    RG_TLAUNCH((k_sampled_logits<HFV, NTV, true>), grid, dim3(512), 0, stream, h, W, bias, neg, seed,             \
                        counter, (uint64_t)A, B, S, Z, ldz, pmax, psum, Wg, bg);                                   \
   else                                                                                                             \
-    hipLaunchKernelGGL((k_sampled_logits<HFV, NTV, false>), grid, dim3(512), 0, stream, h, W, bias, neg, seed,    \
+    RG_TLAUNCH((k_sampled_logits<HFV, NTV, false>), grid, dim3(512), 0, stream, h, W, bias, neg, seed,            \
                        counter, (uint64_t)(A > 0 ? A : 0), B, S, Z, ldz, pmax, psum, Wg, bg)
 #define SFT(HFV)  \
   if (terms == 9) \

@@ -64,6 +64,7 @@ SIGNATURES = {
     "rg_flash_dw_adam": [P, P, P, P, P, F, I, I, I, I, P, P, P, P, P, P, P, P, P, P],
     "rg_flash_dw_adam_planes": [P, P, P, P, P, F, I, I, I, I, P, P, P, P, P, P, P, P, P, P, P, P, P, I64, P],
     "rg_flash_dw_work_bytes": [I, I, I],
+    "rg_timing_events": [P, P],
     "rg_lse_combine": [P, P, P, I, I, P, P, I64, P, I, P, P, P, P, P],
     "rg_sum_scale": [P, I, F, P, P, P],
     "rg_lse_merge_ranks": [P, I, I, P, P],

@@ -264,7 +264,7 @@ class Trunk:
         for d in range(self.ndir):
             w_ih, w_hh, b_ih, b_hh = self.dirs[d]
             if self.comm is None:
-                with region("gather"):
+                with region("gather", exact=True):
                     call("rg_gather_h" if self.emb16 is not None else "rg_gather", s.data_ptr(), B, L,
                          w.perm.data_ptr(), w.lsort.data_ptr(), w.offs.data_ptr(),
                          (self.emb16 if self.emb16 is not None else self.emb.p).data_ptr(), self.N1, E, d,
@@ -971,7 +971,9 @@ class SampledSoftmaxHead(SoftmaxHead):
         st = stream_ptr()
         g = _f32(1.0 / B)
         split = w.terms != 0
-        with region("sampled_fwd"):  # the negatives' row gather is part of the timed logits step
+        # the negatives' row gather is part of the timed logits step; with the
+        # one-launch kernel the region is kernel-exact
+        with region("sampled_fwd", exact=bool(split and w.zrow)):
             if split and w.zrow:  # one launch: draw, row gather, operand split, logits, partials
                 call("rg_sampled_logits", h.data_ptr(), self.W.p.data_ptr(), self.b.p.data_ptr(), w.ids.data_ptr(),
                      1, self.seed, self.draws, self.A, B, self.S, self.HF, w.terms, w.ZT.data_ptr(), w.ldz,

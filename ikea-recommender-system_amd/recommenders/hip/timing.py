@@ -31,15 +31,30 @@ def timing(timer):
 
 
 @contextlib.contextmanager
-def region(name):
+def region(name, exact=False):
+    """Time the enclosed launches with a pair of events on the current
+    stream.  exact=True (a region of ONE library kernel launched through
+    RG_TLAUNCH, csrc/common.h): the library stamps the events at that
+    kernel's own start / end (hipExtLaunchKernelGGL), so the duration excludes
+    the event-record commands around it (which add microseconds to a
+    microseconds-long kernel); if no such launch happened, the region falls
+    back to the stream events."""
     if _active is None:
         yield
         return
+    from . import call
     a = torch.cuda.Event(enable_timing=True)
     b = torch.cuda.Event(enable_timing=True)
     a.record()
+    if exact:
+        b.record()   # (creates the event; the launch re-records both)
+        call("rg_timing_events", a.cuda_event, b.cuda_event)
     try:
         yield
     finally:
-        b.record()
+        if exact:
+            if call("rg_timing_events", None, None):   # not consumed: plain stream events
+                b.record()
+        else:
+            b.record()
         _active.pairs.setdefault(name, []).append((a, b))

@@ -422,6 +422,11 @@ int rg_collect_grads(const float* dX0, const float* dX1, const int32_t* slot, co
 /* items per online-softmax partial block of rg_head_fwd: pmax/psum/parg hold ceil(A/that) x B */
 int rg_partial_block(void);
 int rg_abi_version(void);
+/* Kernel-exact timing (bench.py): arm two hipEvent_t (created, timing-enabled) so the next
+ * gather / one-launch sampled-logits kernel stamps them at its own start / end
+ * (hipExtLaunchKernelGGL) and disarms them; NULL, NULL disarms.  Returns 1 when the previous
+ * arming was still pending, else 0.  Not thread-safe (one host thread drives the library). */
+int rg_timing_events(void* start, void* stop);
 
 #ifdef __cplusplus
 }
