@@ -133,6 +133,9 @@ def _dev(x, dev, dtype=None):
 
 from .supervised import OVERLAP_HEAD_DW  # noqa: E402
 
+# RG_TARGET_FIRST=0 issues the double-Q target after the supervised head's forward (A/B measurement)
+TARGET_FIRST = __import__("os").environ.get("RG_TARGET_FIRST", "1") != "0"
+
 
 def double_q_step(nets, clocks, k, s, a, r, s_next, true_len, true_next_len, is_end, *, gamma, smorl=None):
     """One SQN (smorl=None) or SMORL step with main = nets[k].  Returns device
@@ -148,13 +151,23 @@ def double_q_step(nets, clocks, k, s, a, r, s_next, true_len, true_next_len, is_
     st = stream_ptr()
     with region("sqn_trunk_main"):
         h = main.trunk.forward(s, true_len, slot="main", save=True)
+
+    def target():
+        with region("sqn_target"):
+            h_n = main.trunk.forward(s_next, true_next_len, slot="next", save=False)
+            a_star = main.argmax_q(h_n, None if smorl is None else smorl["w"])
+            h_b = boot.trunk.forward(s_next, true_len, slot="boot", save=False)   # quirk: true_len
+            return boot.gather_q(h_b, idx32=a_star, out=main.buf("qn", (B, nh)))
+
+    # the double-Q target needs neither the supervised head nor its workspace,
+    # so it is issued before forward_loss, whose access of the head waits for
+    # the previous step's overlapped pass 2: target and pass 2 share the GPU
+    if TARGET_FIRST:
+        qn = target()
     sup_loss, _ = main.sup_head_output.forward_loss(h, a, slot="main")
     q = main.gather_q(h, idx64=a, out=main.buf("q", (B, nh)))
-    with region("sqn_target"):
-        h_n = main.trunk.forward(s_next, true_next_len, slot="next", save=False)
-        a_star = main.argmax_q(h_n, None if smorl is None else smorl["w"])
-        h_b = boot.trunk.forward(s_next, true_len, slot="boot", save=False)   # quirk: true_len
-        qn = boot.gather_q(h_b, idx32=a_star, out=main.buf("qn", (B, nh)))
+    if not TARGET_FIRST:
+        qn = target()
     dq = main.buf("dq", (B, nh))
     if smorl is None:
         r64 = _dev(r, dev, torch.float64)
