@@ -63,8 +63,14 @@ def parse():
     ap.add_argument("--dim", type=int, default=DIM)
     ap.add_argument("--seq", type=int, default=SEQ)
     ap.add_argument("--batch", type=int, default=BATCH)
-    ap.add_argument("--cpu-batch", type=int, default=512)
-    ap.add_argument("--cpu-steps", type=int, default=6)
+    # CPU leg: batch 4096 when the host has >= 96 GiB of RAM (the
+    # reference materialises the 16.4 GB logits, their log_softmax and grads),
+    # else 512; plus the C1 line (BASELINE configs[0], 100 steps)
+    ap.add_argument("--cpu-batch", type=int, default=0, help="0: 4096 if host RAM >= 96 GiB else 512")
+    ap.add_argument("--cpu-steps", type=int, default=0, help="timed CPU steps (0: 2 at batch 4096, 6 below)")
+    ap.add_argument("--c1-steps", type=int, default=100)
+    ap.add_argument("--harness-steps", type=int, default=10,
+                    help="C2: per-batch train_step + update_train_metrics as trainGRU.py:195-224 runs them")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-timing", action="store_true")
     ap.add_argument("--no-eval", action="store_true")
@@ -88,6 +94,17 @@ def parse():
     return ap.parse_args()
 
 
+def host_ram_gib():
+    try:
+        with open("/proc/meminfo") as f:
+            for line in f:
+                if line.startswith("MemTotal:"):
+                    return round(int(line.split()[1]) / 2**20, 1)
+    except OSError:
+        pass
+    return None
+
+
 def cpu_model():
     try:
         with open("/proc/cpuinfo") as f:
@@ -100,33 +117,50 @@ def cpu_model():
 
 
 # ------------------------------------------------------------ CPU leg ------
-def cpu_baseline(args):
-    """The reference's per-step math on PyTorch-CPU (oracle/, restatement pinned
-    to the reference's golden vectors) on a bounded sample: same item count,
-    dims and seq_len, batch reduced to --cpu-batch rows."""
+def _cpu_run(items, dim, seq, B, steps, seed):
+    """Oracle GRU4Rec steps on the host: (per-step seconds after 1 warm-up)."""
     from oracle.models import OracleSupervised
     from recommenders.data_utils.synthetic import SessionStream
-    threads = torch.get_num_threads()
-    B = args.cpu_batch
-    orc = OracleSupervised(kind="gru4rec", hidden_dim=args.dim, embedding_dim=args.dim, gru_layers=1,
-                           train_pad_embed=True, use_packed_seq=True, learning_rate=0.01, item_num=args.items,
-                           state_size=args.seq, action_dim=args.items)
-    st = SessionStream(args.items, args.seq, B * (args.cpu_steps + 1), seed=2)
+    orc = OracleSupervised(kind="gru4rec", hidden_dim=dim, embedding_dim=dim, gru_layers=1, train_pad_embed=True,
+                           use_packed_seq=True, learning_rate=0.01, item_num=items, state_size=seq, action_dim=items)
+    st = SessionStream(items, seq, B * (steps + 1), seed=seed)
     b = st.batch(0, B)
     orc.step(b[0], b[1], b[4])  # warm-up
     times = []
-    for i in range(1, args.cpu_steps + 1):
+    for i in range(1, steps + 1):
         b = st.batch(i, B)
         t0 = time.perf_counter()
         orc.step(b[0], b[1], b[4])
         times.append(time.perf_counter() - t0)
+    return times
+
+
+def cpu_baseline(args):
+    """The reference's per-step math on PyTorch-CPU (oracle/, restatement pinned
+    to the reference's golden vectors), timed on this host: the C2 workload
+    (same items, dims, seq_len; batch 4096 when the host RAM allows it, SURVEY
+    §8d) and the C1 line (BASELINE configs[0]: 10k items, dim32, L<=20,
+    batch 64, --c1-steps steps)."""
+    threads = torch.get_num_threads()
+    ram = host_ram_gib()
+    B = args.cpu_batch or (4096 if ram is not None and ram >= 96 else 512)
+    steps = args.cpu_steps or (2 if B >= 4096 else 6)
+    times = _cpu_run(args.items, args.dim, args.seq, B, steps, 2)
     dt = float(np.sum(times))
-    return {"value": round(B * args.cpu_steps / dt, 2), "unit": "session-steps/sec", "cores": threads,
-            "cpu_model": cpu_model(), "kind": "port",
-            "median_ms_per_step": round(float(np.median(times)) * 1e3, 1),
-            "sample": (f"oracle (reference PyTorch-CPU math) GRU4Rec {args.items} items dim{args.dim} "
-                       f"L<={args.seq}, batch {B}, {args.cpu_steps} timed steps after 1 warm-up, "
-                       f"{threads} threads, {dt:.1f} s")}
+    out = {"value": round(B * steps / dt, 2), "unit": "session-steps/sec", "cores": threads,
+           "cpu_model": cpu_model(), "host_ram_gib": ram, "kind": "port",
+           "median_ms_per_step": round(float(np.median(times)) * 1e3, 1),
+           "sample": (f"oracle (reference PyTorch-CPU math) GRU4Rec {args.items} items dim{args.dim} "
+                      f"L<={args.seq}, batch {B}, {steps} timed steps after 1 warm-up, "
+                      f"{threads} threads, {dt:.1f} s")}
+    if args.c1_steps > 0:
+        t1 = _cpu_run(10_000, 32, 20, 64, args.c1_steps, 1)
+        d1 = float(np.sum(t1))
+        out["c1"] = {"value": round(64 * args.c1_steps / d1, 2), "unit": "session-steps/sec",
+                     "ms_per_step": round(d1 / args.c1_steps * 1e3, 3), "steps": args.c1_steps,
+                     "workload": "GRU4Rec 10k items, dim32, seq_len<=20, batch 64 (BASELINE configs[0]), "
+                                 f"{threads} threads"}
+    return out
 
 
 def cpu_eval_parity(net, ev, dev_idx, rows=256):
@@ -309,8 +343,118 @@ def pinned(b):
     return tuple(x.pin_memory() for x in b)
 
 
+# ------------------------------------------------------ multi-rank launch ---
+def free_port():
+    import socket
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+def launch_cmd(nproc, argv, port):
+    """torch.distributed.run command starting one rank per GPU of this node."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
+            "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__), *argv]
+
+
+def relay_json(stdout_text):
+    """The one JSON result line among the ranks' merged stdout (rank 0's)."""
+    found = None
+    for line in stdout_text.splitlines():
+        line = line.strip()
+        if line.startswith("{"):
+            try:
+                d = json.loads(line)
+            except ValueError:
+                continue
+            if isinstance(d, dict) and "metric" in d:
+                found = line
+    return found
+
+
+def launch_ranks(args, argv, runner=None):
+    """``bench.py --gpus N`` without a torch.distributed launcher: start the N
+    ranks as child processes (torch.distributed.run, before this process
+    touches any GPU) and relay rank 0's JSON line.  Returns the exit code."""
+    import subprocess
+    runner = runner or subprocess.run
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    r = runner(launch_cmd(args.gpus, argv, free_port()), stdout=subprocess.PIPE, env=env, text=True)
+    line = relay_json(r.stdout or "")
+    if r.returncode != 0 or line is None:
+        sys.stderr.write(r.stdout or "")
+        return r.returncode or 1
+    sys.stdout.write(line + "\n")
+    sys.stdout.flush()
+    return 0
+
+
+def check_world(args):
+    """None when this process is a rank of the right world size; otherwise the
+    action: ("launch", N) or ("error", message)."""
+    ws = os.environ.get("WORLD_SIZE")
+    if ws is None:
+        return ("launch", args.gpus) if args.gpus > 1 else None
+    if int(ws) != args.gpus:
+        return ("error", f"bench.py: WORLD_SIZE={ws} but --gpus {args.gpus}")
+    return None
+
+
+def max_over_ranks(vals, op="max"):
+    """Element-wise max (or sum) of a list of floats over the ranks."""
+    if not torch.distributed.is_initialized():
+        return list(vals)
+    native = torch.distributed.get_backend() == "nccl"
+    t = torch.tensor(vals, dtype=torch.float64, device=torch.cuda.current_device() if native else "cpu")
+    torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX if op == "max" else torch.distributed.ReduceOp.SUM)
+    return [float(x) for x in t.cpu()]
+
+
+def harness_run(tr, batches, n, args, item_counts):
+    """The reference training loop's per-batch pair (trainGRU.py:195-224):
+    ``train_step`` then ``update_train_metrics`` on the same batch (top-k
+    [10, 20] HR / NDCG, coverage [1, 5, 10], diversity + novelty top-1 with a
+    frozen 64-wide div table).  Returns per-batch ms statistics."""
+    from recommenders.data_utils.synthetic import unpopular_items
+    from recommenders.evaluate.eval_protocol import update_train_metrics
+    g = torch.Generator().manual_seed(7)
+    div = torch.nn.Embedding.from_pretrained(torch.randn(args.items + 1, 64, generator=g) * 0.01, freeze=True)
+    unpop = unpopular_items(item_counts)
+    cov = {k: set() for k in (1, 5, 10)}
+    t_all, t_met = [], []
+    for i in range(n):
+        s, a, _, _, ln, _, _ = batches[i % len(batches)]
+        t0 = time.perf_counter()
+        tr.set_train()
+        tr.train_step(s, a, ln)
+        t1 = time.perf_counter()
+        hr, nd, cov, dv, nv, reps = update_train_metrics(
+            s=s, a=a, s_len=ln, model=tr.gru_model, device=tr.device, padding_pos="end", diversity_embedding=div,
+            unpopular_actions_set=unpop, actions_covered_topk_dict=cov, head_idx=0, topk_hr_ndcg=[10, 20],
+            topk_to_consider_cov=[1, 5, 10], topk_to_consider_div=1, topk_to_consider_nov=1, novelty_rew_signal=1)
+        float(dv)   # the harness accumulates it on the host
+        t2 = time.perf_counter()
+        t_all.append(t2 - t0)
+        t_met.append(t2 - t1)
+    tr.set_train()
+    B = batches[0][0].shape[0]
+    ta, tm = np.array(t_all[1:]) * 1e3, np.array(t_met[1:]) * 1e3
+    return {"harness_ms_per_step": round(float(np.median(ta)), 3),
+            "update_train_metrics_ms": round(float(np.median(tm)), 3),
+            "value": round(B / (float(np.median(ta)) * 1e-3), 2), "unit": "session-steps/sec", "batches": n - 1,
+            "note": "median per batch of train_step + update_train_metrics (trainGRU.py:195-224), after 1 untimed "
+                    "batch; metrics: HR/NDCG@[10,20], coverage [1,5,10], div/nov top-1"}
+
+
 def main():
     args = parse()
+    act = check_world(args)
+    if act is not None:
+        if act[0] == "error":
+            raise SystemExit(act[1])
+        # no torch.distributed launcher around us: start the ranks as children
+        sys.exit(launch_ranks(args, sys.argv[1:]))
     # the ONE JSON line goes to the real stdout; everything else that writes to
     # fd 1 while the job runs (RCCL's version banner at init, library logs)
     # is sent to stderr
@@ -342,7 +486,7 @@ def main():
         torch.cuda.set_device(local)
         dist.init_process_group(backend)
     if world > 1 and args.config == "c3":
-        raise SystemExit("multi-GPU bench runs the C2 / C4 workloads")
+        raise SystemExit("multi-GPU bench runs the C2 / C4 / C5 workloads")
     from recommenders.data_utils.synthetic import SessionStream
 
     dev = torch.device("cuda", local)
@@ -369,19 +513,19 @@ def main():
                                            args.config)
     print(f"bench: peak device memory {torch.cuda.max_memory_allocated(dev) / 2**30:.1f} GiB", file=sys.stderr,
           flush=True)
-    ev, dev_idx = None, None
     net = getattr(tr, "gru_model", None)
+    harness = None
+    if args.config == "c2" and not shard and args.harness_steps > 1 and not args.no_eval:
+        harness = harness_run(tr, batches, args.harness_steps, args, args.item_counts)
+    ev, dev_idx = None, None
     if not args.no_eval and not shard and net is not None:
         ev, dev_idx = device_eval(net, held)
-    if rank != 0:
-        if torch.distributed.is_initialized():
-            torch.distributed.destroy_process_group()
-        return
     ms = dt / args.steps * 1e3
     value = B * args.steps * world / dt
     roof = None
     target = None
     native = None
+    parity_net = None
     HF = E * (2 if args.config == "c3" else 1)
     terms = LOGIT_TERMS.get(args.precision, 0)
     if args.config in ("c2", "c4", "c5"):
@@ -389,15 +533,14 @@ def main():
             sup = net.heads["output"] if net is not None else tr.SMORL_1.sup_head_output
             prec = args.precision if sup.flash_terms(B * world) else "f32"
             roof = head_roofline(kern, prec, B * world, N // world, E)
-        if args.config == "c2" and world == 1:
-            parity_net = None
-            if not args.no_cpu_baseline and not args.no_eval and net is not None:
+        if args.config == "c2":
+            if world == 1 and not args.no_cpu_baseline and not args.no_eval and net is not None:
                 parity_net = net
             else:
                 del net
             del tr
             torch.cuda.empty_cache()
-            if not args.no_native_side and args.precision != "f32":
+            if world == 1 and not args.no_native_side and args.precision != "f32":
                 # the native fp32 MFMA head (precision "f32"), short side run
                 trn = make_trainer("c2native", args, dev, False)
                 trn.set_train()
@@ -409,13 +552,26 @@ def main():
                 torch.cuda.empty_cache()
             if not args.no_target and kern:
                 # north-star target step measured on GRU4Rec at C2
-                # shapes with the sampled head: a short side run, own trainer
+                # shapes with the sampled head: a short side run, own trainer, on
+                # every rank (its own batch shard; the sampled head keeps the
+                # whole table: it is not item-sharded)
                 tr2 = make_trainer("c2s", args, dev, False)
                 tr2.set_train()
-                _, _, k2, _ = timed_run(tr2, batches, min(2, args.warmup), min(10, args.steps), 1, True, "c2")
+                _, _, k2, _ = timed_run(tr2, batches, min(2, args.warmup), min(10, args.steps), world, True, "c2")
                 target = target_step(k2, T, B, args.negatives, E, E, 1, terms)
+                if target is not None and world > 1:
+                    by_sum, = max_over_ranks([float(target["bytes_per_step"])], op="sum")
+                    tg, ts = max_over_ranks([k2["gather"], k2["sampled_fwd"]])
+                    gbs = by_sum / ((tg + ts) * 1e-3) / 1e9
+                    target.update({"achieved": round(gbs, 1), "peak": HBM_PEAK_GBS * world,
+                                   "frac": round(gbs / (HBM_PEAK_GBS * world), 4), "bytes_per_step": int(by_sum),
+                                   "ms": round(tg + ts, 4), "gather_ms": round(tg, 4), "sampled_fwd_ms": round(ts, 4),
+                                   "ranks": world,
+                                   "note": "every rank's gather + sampled logits over its own batch shard (local "
+                                           "whole table); bytes summed over ranks, kernel times max over ranks, "
+                                           "peak = ranks x 8 TB/s"})
                 if target is not None:
-                    target["workload"] = f"GRU4Rec {N} items dim{E} batch {B}, {args.negatives} sampled negatives"
+                    target["workload"] = f"GRU4Rec {N} items dim{E} batch {B}/GPU, {args.negatives} sampled negatives"
                     target["kernel_ms"] = k2
                 del tr2
     else:
@@ -427,6 +583,10 @@ def main():
             roof["traffic"] = None
             if os.path.exists(pmc) and (B, args.negatives, HF, args.precision) == (4096, 2048, 256, "f32x6"):
                 roof["traffic"] = json.load(open(pmc)).get("c3:gather+sampled_fwd")
+    if rank != 0:
+        if torch.distributed.is_initialized():
+            torch.distributed.destroy_process_group()
+        return
     cpu = None
     if world == 1 and not args.no_cpu_baseline and args.config == "c2":
         cpu = cpu_baseline(args)
@@ -465,7 +625,7 @@ def main():
         "step_ms": {"median": round(float(np.median(ps)), 3), "p10": round(float(np.percentile(ps, 10)), 3),
                     "p90": round(float(np.percentile(ps, 90)), 3), "mean": round(float(ps.mean()), 3)},
         "roofline": roof, "cpu_baseline": cpu, "north_star_target": target, "eval_heldout": ev,
-        "native_f32": native, "kernel_ms": kern,
+        "harness": harness, "native_f32": native, "kernel_ms": kern,
         "loss_first_last": [round(losses[0], 5), round(losses[-1], 5)],
     }
     os.write(json_fd, (json.dumps(line) + "\n").encode())

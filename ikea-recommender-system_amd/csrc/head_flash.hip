@@ -151,6 +151,8 @@ __global__ void k_pad_bias(const float* __restrict__ bias, int A, int Ap, float*
 // after chunk c's O-MFMAs and lands under chunk c+1's S-MFMAs and softmax.
 // ARG: also the row's top-1 (value, item) per split and, with cmax, every
 // chunk's row maximum — the inputs of the fused top-k (SMORL's rewards).
+// NG = 0 (rg_flash_score, evaluation): the S-part alone — lse partials,
+// per-split top-1 and chunk maxima, no O contraction, no R-planes read.
 template <int HF, int NT, int NG, bool ARG>
 __global__ __launch_bounds__(64 * fl_nw(HF, 1)) void k_flash_fwd(
     const bf16x8* __restrict__ Hk, const bf16x8* __restrict__ Wk, const bf16x8* __restrict__ Wr,
@@ -163,7 +165,7 @@ __global__ __launch_bounds__(64 * fl_nw(HF, 1)) void k_flash_fwd(
   constexpr int EK = NS * 192;        // entries per 32-row block, K-planes
   constexpr int ER = NTL * 2 * 192;   // R-planes (== EK)
   __shared__ bf16x8 sk0[EK], sk1[EK];
-  __shared__ bf16x8 sr0[ER], sr1[DR ? ER : 1];
+  __shared__ bf16x8 sr0[NG ? ER : 1], sr1[(DR && NG) ? ER : 1];
   __shared__ __attribute__((aligned(16))) float sb0[32], sb1[32];
   const int tid = threadIdx.x, lane = tid & 63, hh = lane >> 5, l32 = lane & 31, lane16 = 16 * lane;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -184,7 +186,10 @@ __global__ __launch_bounds__(64 * fl_nw(HF, 1)) void k_flash_fwd(
     stage<EK, NW>(Wk + (int64_t)(C) * EK, SK, w, lane16);                      \
     if (w == 0 && lane < 8) blds16(rsrc_of(bias_pad + 32 * (C)), SB, lane16, 0); \
   } while (0)
-#define FL_ISSUE_R(C, SR) stage<ER, NW, NG != 3>(Wr + (int64_t)(C) * ER, SR, w, lane16)
+#define FL_ISSUE_R(C, SR)                                                                \
+  do {                                                                                   \
+    if constexpr (NG > 0) stage<ER, NW, NG != 3>(Wr + (int64_t)(C) * ER, SR, w, lane16); \
+  } while (0)
   if (nch > 0) {
     FL_ISSUE_K(c0, sk0, sb0);
     FL_ISSUE_R(c0, sr0);
@@ -280,6 +285,7 @@ __global__ __launch_bounds__(64 * fl_nw(HF, 1)) void k_flash_fwd(
   // O-part: Oᵀ += W_cᵀ·Pᵀ for every block
   auto opart = [&](const bf16x8* sr, const bf16x8 (&q0)[RB][2], const bf16x8 (&q1)[RB][2],
                    const bf16x8 (&q2)[RB][2]) __attribute__((always_inline)) {
+    if constexpr (NG > 0) {
     bf16x8 a0 = sr[lane], a1 = sr[64 + lane], a2 = sr[128 + lane];
 #pragma unroll
     for (int ts = 0; ts < 2 * NTL; ++ts) {
@@ -293,10 +299,11 @@ __global__ __launch_bounds__(64 * fl_nw(HF, 1)) void k_flash_fwd(
       a2 = n2;
       __builtin_amdgcn_sched_barrier(0);
     }
+    }
   };
   for (int c = 0; c < nch; c += 2) {
     bf16x8 q0[RB][2], q1[RB][2], q2[RB][2];
-    if (DR) {
+    if (DR || NG == 0) {
       if (c + 1 < nch) {
         FL_ISSUE_K(c0 + c + 1, sk1, sb1);
         FL_ISSUE_R(c0 + c + 1, sr1);
@@ -364,11 +371,13 @@ __global__ __launch_bounds__(64 * fl_nw(HF, 1)) void k_flash_fwd(
         parg[(int64_t)split * B + row] = bij;
       }
     }
+    if constexpr (NG > 0) {
 #pragma unroll
-    for (int t = 0; t < NTL; ++t)
+      for (int t = 0; t < NTL; ++t)
 #pragma unroll
-      for (int r = 0; r < 16; ++r)
-        pO[((int64_t)split * HF + 32 * t + acc32_row(r, hh)) * B + row] = o[j][t][r];
+        for (int r = 0; r < 16; ++r)
+          pO[((int64_t)split * HF + 32 * t + acc32_row(r, hh)) * B + row] = o[j][t][r];
+    }
   }
 }
 
@@ -936,8 +945,12 @@ __global__ __launch_bounds__(256) void k_flash_topk_cand(const float* __restrict
   }
 }
 
-// one workgroup (256 threads) per row: fp32 logits of the candidate items
-// (fmaf chain over k, then + bias), canonical top-K
+// one workgroup (256 threads) per row: fp32 logits of the candidate items,
+// canonical top-K.  The dot is the native fp32 head's own chain (csrc/head.hip
+// k_head_fwd*: v_mfma_f32_32x32x2_f32 with k = s from lane half 0 and k =
+// HF/2 + s from half 1, i.e. fmaf over s of (h[s]·w[s], then h[HF/2+s]·w[HF/2+s]),
+// then + bias), so a re-scored logit is bitwise the one the model's forward()
+// stores and the top-K equals the canonical top-K of those logits.
 __global__ __launch_bounds__(256) void k_flash_topk_eval(const float* __restrict__ h, const float* __restrict__ W,
                                                          const float* __restrict__ bias, const int32_t* __restrict__ cand,
                                                          const int32_t* __restrict__ ncand, int A, int HF, int K,
@@ -957,13 +970,19 @@ __global__ __launch_bounds__(256) void k_flash_topk_eval(const float* __restrict
     float z = NEG_INF;
     if (item < A) {
       const f4* wr = reinterpret_cast<const f4*>(W + (int64_t)item * HF);
+      const int kh4 = HF / 8;   // float4s per half
       float acc = 0.f;
-      for (int k4 = 0; k4 < HF / 4; ++k4) {
-        const f4 x = wr[k4];
-        acc = fmaf(hs[4 * k4], x[0], acc);
-        acc = fmaf(hs[4 * k4 + 1], x[1], acc);
-        acc = fmaf(hs[4 * k4 + 2], x[2], acc);
-        acc = fmaf(hs[4 * k4 + 3], x[3], acc);
+      for (int s4 = 0; s4 < kh4; ++s4) {
+        const f4 xa = wr[s4], xb = wr[kh4 + s4];
+        const int ka = 4 * s4, kb = HF / 2 + 4 * s4;
+        acc = fmaf(hs[ka], xa[0], acc);
+        acc = fmaf(hs[kb], xb[0], acc);
+        acc = fmaf(hs[ka + 1], xa[1], acc);
+        acc = fmaf(hs[kb + 1], xb[1], acc);
+        acc = fmaf(hs[ka + 2], xa[2], acc);
+        acc = fmaf(hs[kb + 2], xb[2], acc);
+        acc = fmaf(hs[ka + 3], xa[3], acc);
+        acc = fmaf(hs[kb + 3], xb[3], acc);
       }
       z = acc + bias[item];
     }
@@ -1207,6 +1226,46 @@ extern "C" int rg_flash_fwd(const void* Hk, const void* Wk, const void* Wr, cons
                           stream);
 }
 
+// Evaluation scoring (no O contraction): pass 1's S-part over the fp32
+// logits at `terms` plane products — per-(split, row) max / Σexp (-> lse via
+// rg_flash_lse), per-split first maximum and every 32-item chunk's row
+// maximum (-> exact canonical top-K via rg_flash_topk).
+extern "C" int rg_flash_score(const void* Hk, const void* Wk, const float* bias_pad, int B, int A, int HF, int terms,
+                              int nsplit, float* pm, float* pl, float* pbest, int32_t* parg, float* cmax,
+                              hipStream_t stream) {
+  if (B <= 0 || A <= 0 || (B % 32) || nsplit <= 0 || !Hk || !Wk || !bias_pad || !pm || !pl || !pbest || !parg ||
+      !cmax)
+    return RG_ERR_ARG;
+  if (terms == RG_TERMS_X6D3) terms = 6;   // logits only
+  if (terms != 6 && terms != 9) return RG_ERR_ARG;
+  if (!flash_hf_ok(HF)) return RG_ERR_SHAPE;
+  const int nct = (A + 31) / 32;
+  const int cps = (nct + nsplit - 1) / nsplit;
+  const int rpb = fl_rows(HF, 1);
+  const int nrb = (B + rpb - 1) / rpb;
+  const dim3 grid((unsigned)(nrb * nsplit));
+#define FSC(HFV, NTV)                                                                                             \
+  hipLaunchKernelGGL((k_flash_fwd<HFV, NTV, 0, true>), grid, dim3(64 * fl_nw(HFV, 1)), 0, stream, (const bf16x8*)Hk, \
+                     (const bf16x8*)Wk, (const bf16x8*)nullptr, bias_pad, B, A, nrb, nsplit, cps, pm, pl,         \
+                     (float*)nullptr, pbest, parg, cmax)
+#define FT(HFV)          \
+  if (terms == 9) {      \
+    FSC(HFV, 9);         \
+  } else {               \
+    FSC(HFV, 6);         \
+  }
+  switch (HF) {
+    case 32: FT(32); break;
+    case 64: FT(64); break;
+    case 128: FT(128); break;
+    case 256: FT(256); break;
+  }
+#undef FT
+#undef FSC
+  RG_LAUNCH_CHECK();
+  return RG_OK;
+}
+
 extern "C" int rg_flash_amax_fwd(const void* Hk, const void* Wk, const float* bias_pad, int B, int A, int HF,
                                  int terms, int nsplit, float* pbest, int32_t* parg, hipStream_t stream) {
   if (B <= 0 || A <= 0 || (B % 32) || nsplit <= 0 || !Hk || !Wk || !bias_pad || !pbest || !parg) return RG_ERR_ARG;
@@ -1253,7 +1312,7 @@ extern "C" int rg_flash_topk_cap(void) { return TK_CAP; }
 extern "C" int rg_flash_topk(const float* cmax, int B, int A, int K, float tol_abs, float tol_rel, const float* h,
                              const float* W, const float* bias, int HF, int32_t* cand, int32_t* ncand, int32_t* out_idx,
                              float* out_val, int32_t* err, hipStream_t stream) {
-  if (B <= 0 || A <= 0 || K <= 0 || K > TK_MAX || K > A || HF <= 0 || HF > 256 || (HF % 4)) return RG_ERR_ARG;
+  if (B <= 0 || A <= 0 || K <= 0 || K > TK_MAX || K > A || HF <= 0 || HF > 256 || (HF % 8)) return RG_ERR_ARG;
   if (!cmax || !h || !W || !bias || !cand || !ncand || !out_idx || !err) return RG_ERR_ARG;
   const int nct = (A + 31) / 32;
   hipLaunchKernelGGL(k_flash_topk_cand, dim3((B + 63) / 64), dim3(256), 0, stream, cmax, nct, B, K, tol_abs, tol_rel,
@@ -1428,7 +1487,7 @@ extern "C" int rg_row_norm_max(const float* W, int64_t A, int HF, float* out, hi
 extern "C" int rg_flash_argmax_exact(const float* cmax, int B, int A, const float* h, const float* W, const float* bias,
                                      int HF, const float* wnorm, float tol, float* lim, int32_t* cand, int32_t* ncand,
                                      int32_t* out_idx, float* out_val, hipStream_t stream) {
-  if (B <= 0 || A <= 0 || HF <= 0 || HF > 256 || (HF % 4)) return RG_ERR_ARG;
+  if (B <= 0 || A <= 0 || HF <= 0 || HF > 256 || (HF % 8)) return RG_ERR_ARG;
   if (!cmax || !h || !W || !bias || !wnorm || !lim || !cand || !ncand || !out_idx || !out_val) return RG_ERR_ARG;
   const int nct = (A + 31) / 32;
   if (hipMemsetAsync(ncand, 0, sizeof(int32_t) * B, stream) != hipSuccess) return RG_ERR_LAUNCH;

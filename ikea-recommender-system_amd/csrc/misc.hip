@@ -92,6 +92,56 @@ extern "C" int rg_remap_ids(const int32_t* idx, int64_t n, const int32_t* lut, i
   return RG_OK;
 }
 
+// Repetition counts (repetitiveness.py:21-57): for every k of ks, the number
+// of (state slot, top-k prediction) pairs with s[b, t] == idx[b, j], j < k,
+// summed over the batch.  One wave per row, lanes over the L slots; integer
+// counts (order-free atomics on 64-bit integers: deterministic).
+constexpr int REP_MAXK = 16;
+struct RepKs {
+  int k[REP_MAXK];
+};
+__global__ __launch_bounds__(256) void k_repetitions(const int64_t* __restrict__ s, int L,
+                                                     const int32_t* __restrict__ idx, int K, int B, RepKs ks, int nk,
+                                                     unsigned long long* __restrict__ out) {
+  const int b = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (b >= B) return;
+  unsigned cnt[REP_MAXK];
+#pragma unroll
+  for (int q = 0; q < REP_MAXK; ++q) cnt[q] = 0;
+  for (int t = lane; t < L; t += 64) {
+    const int64_t v = s[(int64_t)b * L + t];
+    for (int j = 0; j < K; ++j) {
+      if (v == (int64_t)idx[(int64_t)b * K + j]) {
+#pragma unroll
+        for (int q = 0; q < REP_MAXK; ++q)
+          if (q < nk && j < ks.k[q]) ++cnt[q];
+      }
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < REP_MAXK; ++q) {
+    if (q >= nk) break;
+    unsigned c = cnt[q];
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) c += __shfl_xor(c, o);
+    if (lane == 0 && c) atomicAdd(&out[q], (unsigned long long)c);
+  }
+}
+
+extern "C" int rg_repetitions(const int64_t* s, int L, const int32_t* idx, int K, int B, const int* ks, int nk,
+                              unsigned long long* out, hipStream_t stream) {
+  if (B <= 0 || L <= 0 || K <= 0 || nk <= 0 || nk > REP_MAXK || !s || !idx || !ks || !out) return RG_ERR_ARG;
+  RepKs kk{};
+  for (int q = 0; q < nk; ++q) {
+    if (ks[q] <= 0 || ks[q] > K) return RG_ERR_ARG;
+    kk.k[q] = ks[q];
+  }
+  hipLaunchKernelGGL(k_repetitions, dim3((B + 3) / 4), dim3(256), 0, stream, s, L, idx, K, B, kk, nk, out);
+  RG_LAUNCH_CHECK();
+  return RG_OK;
+}
+
 // items per online-softmax partial block of rg_head_fwd (pmax/psum/parg are
 // ceil(A / rg_partial_block()) × B)
 extern "C" int rg_partial_block(void) { return RG_PBLK; }

@@ -187,15 +187,28 @@ extern "C" int rg_sum64(const double* x, int n, double scale, double* out64, flo
 // Diversity reward (diversity.py:4-73): last = s[b, len_b−1] (end padding)
 // or s[b, L−1] (beg); r = 1 − mean_k cos(D[last], D[idx_bk]), cos with
 // per-vector norms clamped at eps (torch cosine_similarity).  One wave per row.
+// An id outside the table's Drows rows (e.g. -1 from an unmapped tokenizer
+// remap, where the reference's stoi raises KeyError) gives a NaN reward and
+// is never dereferenced.
 __global__ __launch_bounds__(256) void k_diversity(const int64_t* __restrict__ s, int L,
                                                    const int64_t* __restrict__ lens, int pad_end,
                                                    const int32_t* __restrict__ idx, int k, int ldi,
-                                                   const float* __restrict__ D, int Ed, float eps, int B,
-                                                   float* __restrict__ out) {
+                                                   const float* __restrict__ D, int64_t Drows, int Ed, float eps,
+                                                   int B, float* __restrict__ out) {
   const int b = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (b >= B) return;
-  const int64_t last = pad_end ? s[(int64_t)b * L + (lens[b] - 1)] : s[(int64_t)b * L + (L - 1)];
+  const int64_t li = pad_end ? lens[b] - 1 : L - 1;
+  const int64_t last = (li >= 0 && li < L) ? s[(int64_t)b * L + li] : -1;
+  bool bad = last < 0 || last >= Drows;
+  for (int q = 0; q < k; ++q) {
+    const int64_t j = idx[(int64_t)b * ldi + q];
+    bad |= j < 0 || j >= Drows;
+  }
+  if (bad) {   // wave-uniform (every lane read the same ids)
+    if (lane == 0) out[b] = __builtin_nanf("");
+    return;
+  }
   const float* x1 = D + last * Ed;
   float n1 = 0.f;
   for (int c = lane; c < Ed; c += 64) n1 += x1[c] * x1[c];
@@ -214,10 +227,11 @@ __global__ __launch_bounds__(256) void k_diversity(const int64_t* __restrict__ s
 }
 
 extern "C" int rg_diversity(const int64_t* s, int L, const int64_t* lens, int pad_end, const int32_t* idx, int k,
-                            int ldi, const float* D, int Ed, float eps, int B, float* out, hipStream_t stream) {
-  if (B <= 0 || k <= 0 || ldi < k) return RG_ERR_ARG;
-  hipLaunchKernelGGL(k_diversity, dim3((B + 3) / 4), dim3(256), 0, stream, s, L, lens, pad_end, idx, k, ldi, D, Ed,
-                     eps, B, out);
+                            int ldi, const float* D, int64_t Drows, int Ed, float eps, int B, float* out,
+                            hipStream_t stream) {
+  if (B <= 0 || k <= 0 || ldi < k || Drows <= 0 || L <= 0) return RG_ERR_ARG;
+  hipLaunchKernelGGL(k_diversity, dim3((B + 3) / 4), dim3(256), 0, stream, s, L, lens, pad_end, idx, k, ldi, D, Drows,
+                     Ed, eps, B, out);
   RG_LAUNCH_CHECK();
   return RG_OK;
 }

@@ -11,9 +11,19 @@ def get_coverage_k(unique_topk_actions, unpopular_items, num_actions):
 
 
 def update_coverage_from_indices(idx, actions_covered_topk_dict, top_k):
+    """Add every row's first k ids to the covered set of each k (reference
+    update_actions_covered_topk_dict, coverage.py:24-53).  The batch's ids are
+    de-duplicated first and the covered set is grown in place (O(batch)
+    instead of the reference's O(|covered|) ``union`` copy per batch; the
+    dict ends up holding the same sets)."""
     idx = np.asarray(idx)
     for k in top_k:
-        actions_covered_topk_dict[k] = actions_covered_topk_dict[k].union(idx[:, :k].ravel().tolist())
+        new = np.unique(idx[:, :k]).tolist()
+        cur = actions_covered_topk_dict[k]
+        if isinstance(cur, set):
+            cur.update(new)
+        else:
+            actions_covered_topk_dict[k] = set(cur).union(new)
     return actions_covered_topk_dict
 
 

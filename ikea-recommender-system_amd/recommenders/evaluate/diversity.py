@@ -8,10 +8,18 @@ import torch
 
 def map_ids_host(idx, input_tokenizer, output_tokenizer):
     """input_tokenizer.stoi(output_tokenizer.itos(x)) for every element (the
-    reference's apply_ branch), through one table lookup."""
-    n = len(output_tokenizer)
-    lut = torch.tensor([input_tokenizer.stoi(output_tokenizer.itos(j)) for j in range(n)], dtype=torch.int64)
-    return lut[idx.cpu().long()].to(idx.device)
+    reference's apply_ branch) through the pair's cached lookup table
+    (recommenders/hip/remap.py host_table); an id with no input token raises
+    KeyError (RemapError) as the reference's stoi does."""
+    from recommenders.hip.remap import RemapError, host_table
+    lut = host_table(input_tokenizer, output_tokenizer)
+    i = idx.cpu().long()
+    if bool(((i < 0) | (i >= len(lut))).any()):
+        raise IndexError("predicted id outside the output vocabulary")
+    out = lut[i].long()
+    if bool((out < 0).any()):
+        raise RemapError("a predicted id has no input-vocabulary token (input_tokenizer.stoi(output_tokenizer.itos(id)))")
+    return out.to(idx.device)
 
 
 def get_last_action(s, padding_pos, s_len=None, device="cuda"):

@@ -15,7 +15,6 @@ import numpy as np
 import torch
 
 from recommenders.evaluate.coverage import get_coverage, update_coverage_from_indices
-from recommenders.evaluate.repetitiveness import repetitions_from_indices
 from recommenders.hip.evalpath import eval_batch
 from recommenders.hip.nets import HipNet
 from recommenders.hip.qlearn import unpopular_bitmap
@@ -59,11 +58,24 @@ def get_preds(states, true_len, model, head_idx):
     return out[head_idx] if isinstance(out, tuple) else out
 
 
+_DIV = {}
+
+
 def _div_table(diversity_embedding, device):
+    """The frozen diversity table on the device, cached per (tensor, in-place
+    version, device): the harness passes the same embedding every batch
+    (trainGRU.py:199-224), a 1M x 64 table is 256 MB of H2D per call."""
     if diversity_embedding is None:
         return None
     t = diversity_embedding.weight if hasattr(diversity_embedding, "weight") else diversity_embedding
-    return t.detach().to(device, torch.float32).contiguous()
+    key = (id(t), t._version, str(device))
+    hit = _DIV.get(key)
+    if hit is not None and hit[0] is t:
+        return hit[1]
+    d = t.detach().to(device, torch.float32).contiguous()
+    _DIV.clear()
+    _DIV[key] = (t, d)
+    return d
 
 
 def _lut(input_tokenizer, output_tokenizer, device):
@@ -118,7 +130,7 @@ def evaluate(evaluation_data_loader, model, device, loss_function, padding_pos, 
         for s, a, s_len in evaluation_data_loader:
             r = eval_batch(model, s, s_len, a, head_idx=head_idx, K=K, ks=topk_hr_ndcg, padding_pos=padding_pos,
                            div_table=table, k_div=topk_to_consider_div, bitmap=bitmap, k_nov=topk_to_consider_nov,
-                           nov_reward=novelty_rew_signal, lut=lut)
+                           nov_reward=novelty_rew_signal, lut=lut, rep_ks=topk_hr_ndcg)
             idx = r.idx.cpu().numpy()
             loss += float(r.loss.item())
             hr += r.hits.cpu().numpy()
@@ -126,7 +138,7 @@ def evaluate(evaluation_data_loader, model, device, loss_function, padding_pos, 
             tot_div += float(r.div.double().sum().item()) if r.div is not None else 0.0
             tot_nov += float(r.nov.double().sum().item())
             covered = update_coverage_from_indices(idx, covered, topk_to_consider_cov)
-            reps += repetitions_from_indices(s.cpu().numpy(), r.idx_in.cpu().numpy(), topk_hr_ndcg)
+            reps += r.reps.cpu().numpy()
             n += len(a)
             nb += 1
     coverage_res = get_coverage(covered, set(unpopular_actions_set), model.action_dim, topk_to_consider_cov)
@@ -148,9 +160,9 @@ def update_train_metrics(s, a, s_len, model, device, padding_pos, diversity_embe
                        div_table=_div_table(diversity_embedding, dev), k_div=topk_to_consider_div,
                        bitmap=unpopular_bitmap(unpopular_actions_set, model.action_dim, dev),
                        k_nov=topk_to_consider_nov, nov_reward=novelty_rew_signal, want_loss=False,
-                       lut=_lut(input_tokenizer, output_tokenizer, dev))
+                       lut=_lut(input_tokenizer, output_tokenizer, dev), rep_ks=topk_hr_ndcg)
         idx = r.idx.cpu().numpy()
         covered = update_coverage_from_indices(idx, actions_covered_topk_dict, topk_to_consider_cov)
-        reps = repetitions_from_indices(s.cpu().numpy(), r.idx_in.cpu().numpy(), topk_hr_ndcg)
+        reps = r.reps.cpu().numpy().astype(np.float64)
         return (r.hits.cpu().numpy(), r.ndcg.cpu().numpy(), covered, r.div.sum(), float(r.nov.double().sum()),
                 reps)

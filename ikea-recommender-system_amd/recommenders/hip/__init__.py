@@ -53,6 +53,7 @@ SIGNATURES = {
     "rg_flash_fwd_top": [P, P, P, P, I, I, I, I, I, P, P, P, P, P, P, P],
     "rg_flash_argmax": [P, P, I, I, P, P, P],
     "rg_flash_amax_fwd": [P, P, P, I, I, I, I, I, P, P, P],
+    "rg_flash_score": [P, P, P, I, I, I, I, I, P, P, P, P, P, P],
     "rg_flash_amax_screen": [P, P, P, I, I, I, I, P, P, P, P],
     "rg_row_norm_max": [P, I64, I, P, P],
     "rg_flash_argmax_exact": [P, I, I, P, P, P, I, P, F, P, P, P, P, P, P],
@@ -83,10 +84,11 @@ SIGNATURES = {
     "rg_sqn_td": [P, P, P, P, F, I, D, P, P, P],
     "rg_smorl_td": [P, P, P, P, P, I, F, F, I, P, P, P],
     "rg_sum64": [P, I, D, P, P, P],
-    "rg_diversity": [P, I, P, I, P, I, I, P, I, F, I, P, P],
+    "rg_diversity": [P, I, P, I, P, I, I, P, I64, I, F, I, P, P],
     "rg_novelty": [P, I, I, P, F, I, P, P],
     "rg_topk": [P, I64, P, I, I, I, P, P, P, P],
     "rg_hits_ndcg": [P, I, P, I, P, I, P, P],
+    "rg_repetitions": [P, I, P, I, I, P, I, P, P],
     "rg_mask_scale": [P, P, F, I64, P, P],
     "rg_gru_wide_work_bytes": [I],
     "rg_gru_fwd_dirs": [P, P, P, P, I, P, P, P, I, I, P, I, I, I64, P],

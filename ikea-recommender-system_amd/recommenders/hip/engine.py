@@ -501,10 +501,52 @@ class _FlashWS:
         if top_k >= 1:
             self.pbest, self.parg = z(self.nsplit, B), z(self.nsplit, B, dt=torch.int32)
             self.top_idx, self.top_val = z(B, top_k, dt=torch.int32), z(B, top_k)
-        if top_k > 1:
+        # chunk maxima for the exact top-K (K = 1 too, while they fit
+        # SCREEN_CMAX_BYTES; else K = 1 merges the per-split first maxima)
+        if top_k > 1 or (top_k == 1 and -(-A // 32) * B * 4 <= SCREEN_CMAX_BYTES):
             self.cmax = z(-(-A // 32), B)
             self.cand = z(B, call("rg_flash_topk_cap"), dt=torch.int32)
             self.ncand = z(B, dt=torch.int32)
+
+
+# evaluation scoring (SoftmaxHead.score_topk): rows per chunk such that the
+# chunk maxima (ceil(A/32) x rows floats) stay within this many bytes
+EVAL_CMAX_BYTES = 1 << 30
+
+
+class _ScoreWS:
+    """Workspace of SoftmaxHead.score_topk for B rows and top-K: one row
+    chunk's operands (R rows, R % 32 == 0) and the whole batch's outputs."""
+
+    @staticmethod
+    def get(head, slot, B, K):
+        d = head.__dict__.setdefault("_sws_eval", {})
+        w = d.get(slot)
+        if w is None or w.B != B or w.K != K:
+            d.pop(slot, None)
+            w = d[slot] = _ScoreWS(B, K, head.A, head.HF, head.device)
+        return w
+
+    def __init__(self, B, K, A, HF, device):
+        z = lambda *s, dt=torch.float32: torch.empty(*s, dtype=dt, device=device)  # noqa: E731
+        nct = -(-A // 32)
+        self.B, self.K = B, K
+        rmax = max(32, EVAL_CMAX_BYTES // (4 * nct) // 32 * 32)
+        self.R = R = min(_round_up(B, 32), rmax)
+        nrb = -(-R // call("rg_flash_rows_per_block", HF))
+        self.nsplit = _round_up(min(max(1, 256 // nrb), nct), 8)
+        self.h = torch.zeros(R, HF, device=device)
+        self.t = torch.zeros(R, dtype=torch.int64, device=device)
+        self.Hk = torch.empty(call("rg_head_plane_bytes", R, HF), dtype=torch.uint8, device=device)
+        self.pm, self.pl, self.pbest = z(self.nsplit, R), z(self.nsplit, R), z(self.nsplit, R)
+        self.parg = z(self.nsplit, R, dt=torch.int32)
+        self.cmax = z(nct, R)
+        self.lse, self.zt = z(R), z(R)
+        self.cand = z(R, call("rg_flash_topk_cap"), dt=torch.int32)
+        self.ncand = z(R, dt=torch.int32)
+        Bp = _round_up(B, R)
+        self.idx, self.vals = z(Bp, K, dt=torch.int32), z(Bp, K)
+        self.loss_row = z(Bp)
 
 
 class _AmaxWS:
@@ -691,15 +733,18 @@ class SoftmaxHead:
     def top_entries(self, w):
         """(idx (B, K) int32 local item ids, values (B, K)) of every row's top-K
         logits in the canonical (value desc, index asc) order, after
-        forward_loss with ``top_k = K``.  Fused head: K = 1 merges pass 1's
-        per-split first maxima (split-bf16 logits); K > 1 rescores the items
-        of the candidate chunks in fp32 (rg_flash_topk; a candidate overflow
-        is flagged in ``top_err``, see check_top_err).  Native head: rg_topk
-        over the stored Zᵀ."""
+        forward_loss with ``top_k = K``.  Fused head: the items of the
+        candidate chunks (chunk maximum within the split-bf16 error of the
+        K-th largest) are re-scored in fp32 (rg_flash_topk; a candidate
+        overflow is flagged in ``top_err``, see check_top_err) — also for
+        K = 1 unless the chunk maxima exceed SCREEN_CMAX_BYTES (C5 on one GPU:
+        then pass 1's per-split first maxima of the split-bf16 logits are
+        merged, so a near-tie within ~2^-24·Σ|h||w| may pick the other item).
+        Native head: rg_topk over the stored Zᵀ."""
         K, B = self.top_k, w.B
         st = stream_ptr()
         if isinstance(w, _FlashWS):
-            if K == 1:
+            if K == 1 and w.cmax is None:
                 call("rg_flash_argmax", w.pbest.data_ptr(), w.parg.data_ptr(), w.nsplit, B, w.top_idx.data_ptr(),
                      w.top_val.data_ptr(), st)
             else:
@@ -713,6 +758,70 @@ class SoftmaxHead:
         call("rg_topk", w.ZT.data_ptr(), w.ldz, w.pmax.data_ptr(), B, self.A, K, idx.data_ptr(), vals.data_ptr(),
              self.top_err.data_ptr(), st)
         return idx, vals
+
+    # ---- evaluation scoring without logits (evaluate / update_train_metrics) ----
+    def score_topk(self, h, K, tgt=None, slot="eval"):
+        """Canonical top-K (value desc, index asc) of the fp32 logits h·Wᵀ + b
+        of every row and, with ``tgt``, the per-row CE (lse − z_target),
+        without a (B, A) logit buffer (reference eval_protocol.py:123-359
+        scores the full (B, A) predictions).  Rows run in chunks of R (cmax
+        ≤ EVAL_CMAX_BYTES): rg_flash_score (pass 1's S-part at 6 plane
+        products: lse partials + chunk maxima), rg_flash_lse (lse, fp32
+        target logit), rg_flash_topk (every item of the candidate chunks
+        re-scored in fp32, fmaf chain + bias).  Returns (idx (B, K) int32,
+        vals (B, K), loss_row (B,) or None); a candidate overflow (massive
+        exact ties) sets ``top_err``.  HF must be in {32, 64, 128, 256}, K <= 32."""
+        B, A, HF = h.shape[0], self.A, self.HF
+        if K > min(32, A) or HF not in (32, 64, 128, 256):
+            raise ValueError(f"score_topk: K={K} (<= 32 and <= A) and HF={HF} in {{32, 64, 128, 256}}")
+        w = _ScoreWS.get(self, slot, B, K)
+        st = stream_ptr()
+        Wp, bp = self.params_ro()
+        Wk, bias_pad = self._eval_planes(Wp, bp, st)
+        R = w.R
+        for r0 in range(0, B, R):
+            n = min(R, B - r0)
+            hs = w.h if n < R else h[r0:r0 + R]
+            if n < R:   # ragged tail: zero-padded rows (scored, never read back)
+                w.h.zero_()
+                w.h[:n].copy_(h[r0:r0 + n])
+            call("rg_head_planes", hs.data_ptr(), R, HF, w.Hk.data_ptr(), None, None, None, st)
+            call("rg_flash_score", w.Hk.data_ptr(), Wk.data_ptr(), bias_pad.data_ptr(), R, A, HF, 6, w.nsplit,
+                 w.pm.data_ptr(), w.pl.data_ptr(), w.pbest.data_ptr(), w.parg.data_ptr(), w.cmax.data_ptr(), st)
+            if tgt is not None:
+                ts = w.t if n < R else tgt[r0:r0 + R]
+                if n < R:
+                    w.t.zero_()
+                    w.t[:n].copy_(tgt[r0:r0 + n])
+                call("rg_flash_lse", w.pm.data_ptr(), w.pl.data_ptr(), w.nsplit, hs.data_ptr(), Wp.p.data_ptr(),
+                     bp.p.data_ptr(), ts.data_ptr(), 0, A, A, R, HF, w.lse.data_ptr(), w.zt.data_ptr(), st)
+                call("rg_sub", w.lse.data_ptr(), w.zt.data_ptr(), n, w.loss_row.data_ptr() + 4 * r0, st)
+            call("rg_flash_topk", w.cmax.data_ptr(), R, A, K, _f32(self.TOP_TOL_ABS), _f32(self.TOP_TOL_REL),
+                 hs.data_ptr(), Wp.p.data_ptr(), bp.p.data_ptr(), HF, w.cand.data_ptr(), w.ncand.data_ptr(),
+                 w.idx.data_ptr() + 4 * r0 * K, w.vals.data_ptr() + 4 * r0 * K, self.top_err.data_ptr(), st)
+        return w.idx[:B], w.vals[:B], (w.loss_row[:B] if tgt is not None else None)
+
+    def _eval_planes(self, Wp, bp, st):
+        """W's K-planes and padded bias for the current W: a training
+        workspace's (pass 2 left them current) when one matches, else the
+        head's own evaluation copy, rebuilt when W changed."""
+        for fw in self._fws.values():
+            if fw.wgen == self._wgen:
+                return fw.Wk, fw.bias_pad
+        ep = getattr(self, "_eplanes", None)
+        if ep is None or ep[0] != self._wgen:
+            Wk = ep[1] if ep is not None else torch.empty(call("rg_head_plane_bytes", self.A, self.HF),
+                                                           dtype=torch.uint8, device=self.device)
+            bias_pad = ep[2] if ep is not None else torch.empty(_round_up(self.A, 32), device=self.device)
+            call("rg_head_planes", Wp.p.data_ptr(), self.A, self.HF, Wk.data_ptr(), None, bp.p.data_ptr(),
+                 bias_pad.data_ptr(), st)
+            ep = self._eplanes = (self._wgen, Wk, bias_pad)
+        return ep[1], ep[2]
+
+    def release_eval(self):
+        """Drop the evaluation workspaces (row-chunk buffers, W planes copy)."""
+        self._eplanes = None
+        getattr(self, "_sws_eval", {}).clear()
 
     def check_top_err(self):
         """Raise if a fused or stored-logit top-k of this head overflowed its
@@ -777,11 +886,15 @@ class SoftmaxHead:
             self._ws[key] = w
         return w
 
-    def logits_T(self, h, slot="eval"):
-        """Zᵀ (A × ldz) for h; returns the (B, A) logical view (no copy)."""
+    def logits_T(self, h, slot=None):
+        """Zᵀ (A × ldz) for h; returns (workspace, the (B, A) logical view, no
+        copy).  slot=None: a fresh buffer owned by the returned tensors (the
+        model's forward(), for callers that index the logits — freed when they
+        drop it); a named slot keeps it cached in the head."""
         B = h.shape[0]
-        w = self.ws(slot, B, True)
-        call("rg_head_fwd", h.data_ptr(), self.W.p.data_ptr(), self.b.p.data_ptr(), B, self.A, self.HF,
+        w = self.ws(slot, B, True) if slot is not None else _HeadWS(B, self.A, self.HF, True, self.device)
+        Wp, bp = self.params_ro()
+        call("rg_head_fwd", h.data_ptr(), Wp.p.data_ptr(), bp.p.data_ptr(), B, self.A, self.HF,
              w.ZT.data_ptr(), w.ldz, w.pmax.data_ptr(), w.psum.data_ptr(), w.parg.data_ptr(), 1, stream_ptr())
         return w, w.ZT[:, :B].t()
 

@@ -20,7 +20,7 @@ import torch
 from . import call, host_floats, host_ptr_array, stream_ptr
 from .engine import SoftmaxHead, _f32
 from .nets import HipNet
-from .remap import remap_ids
+from .remap import raise_if_unmapped, remap_ids
 from .timing import region
 
 
@@ -89,8 +89,8 @@ class QNet(HipNet):
         if self.comm is not None:
             raise NotImplementedError("forward() of an item-sharded model: each rank holds a slice of the items")
         h = self.hidden(s, lengths, slot="eval", save=False)
-        _, sup = self.sup_head_output.logits_T(h, slot="eval")
-        outs = [q.logits_T(h, slot="eval")[1] for q in self.q_heads]
+        _, sup = self.sup_head_output.logits_T(h)
+        outs = [q.logits_T(h)[1] for q in self.q_heads]
         if len(outs) == 1:
             return sup, outs[0]
         return sup, torch.stack(outs, dim=1)
@@ -178,6 +178,8 @@ def double_q_step(nets, clocks, k, s, a, r, s_next, true_len, true_next_len, is_
         call("rg_sum64", sq.data_ptr(), B, 1.0 / B, q_loss.data_ptr(), None, st)
     else:
         rr = smorl_rewards(main, smorl, s, a, r, true_next_len, B)
+        if smorl.get("lut") is not None:   # the reference raises in the reward, before any update
+            raise_if_unmapped(smorl["remap_err"])
         row = main.buf("qrow", (B,))
         q_loss = main.buf("qloss32", (1,))
         grad_row = _f32(np.float32(smorl["alpha"]) / np.float32(B))
@@ -222,7 +224,8 @@ def smorl_rewards(main, smorl, s, a, r_acc, true_next_len, B):
     lens = _dev(true_next_len, dev, torch.int64)   # quirk: diversity uses true_next_len
     idx_div = idx if smorl.get("lut") is None else remap_ids(idx, smorl["lut"], smorl["remap_err"])
     call("rg_diversity", s.data_ptr(), s.shape[1], lens.data_ptr(), 1 if smorl["pad_end"] else 0,
-         idx_div.data_ptr(), k_div, K, smorl["div_table"].data_ptr(), smorl["div_table"].shape[1], _f32(1e-6), B,
+         idx_div.data_ptr(), k_div, K, smorl["div_table"].data_ptr(), smorl["div_table"].shape[0],
+         smorl["div_table"].shape[1], _f32(1e-6), B,
          r_div.data_ptr(), st)
     r_nov = main.buf("r_nov", (B,))
     call("rg_novelty", idx.data_ptr(), k_nov, K, smorl["bitmap"].data_ptr(), _f32(smorl["nov_rew_sig"]), B,
@@ -234,10 +237,23 @@ def smorl_rewards(main, smorl, s, a, r_acc, true_next_len, B):
     return rr
 
 
+_BITMAPS = {}
+
+
 def unpopular_bitmap(unpopular, n_actions, device):
+    """The unpopular set (novelty.py:12-47, item_frequency.py:8-24) as a device
+    bitmap over the actions; cached per (set object, size, n_actions, device)
+    — the harness passes the same set every batch."""
+    key = (id(unpopular), len(unpopular), int(n_actions), str(device))
+    hit = _BITMAPS.get(key)
+    if hit is not None and hit[0] is unpopular:
+        return hit[1]
+    j = np.fromiter((int(x) for x in unpopular), dtype=np.int64, count=len(unpopular))
+    j = j[(j >= 0) & (j < n_actions)]
     bm = np.zeros((n_actions + 31) // 32, dtype=np.uint32)
-    for j in unpopular:
-        j = int(j)
-        if 0 <= j < n_actions:
-            bm[j >> 5] |= np.uint32(1) << np.uint32(j & 31)
-    return torch.from_numpy(bm.view(np.int32)).to(device)
+    np.bitwise_or.at(bm, j >> 5, (np.uint32(1) << (j & 31).astype(np.uint32)))
+    t = torch.from_numpy(bm.view(np.int32)).to(device)
+    if len(_BITMAPS) > 8:
+        _BITMAPS.clear()
+    _BITMAPS[key] = (unpopular, t)
+    return t

@@ -13,9 +13,10 @@ from . import call, stream_ptr
 _CACHE = {}
 
 
-def remap_table(input_tokenizer, output_tokenizer, device):
-    """int32 device table over the output vocabulary, cached per (pair, device)."""
-    key = (id(input_tokenizer), id(output_tokenizer), str(device))
+def host_table(input_tokenizer, output_tokenizer):
+    """int32 host table lut[j] = stoi(itos(j)) over the output vocabulary (-1
+    where the reference's stoi raises), built once per tokenizer pair."""
+    key = (id(input_tokenizer), id(output_tokenizer), "host")
     hit = _CACHE.get(key)
     if hit is not None and hit[0] is input_tokenizer and hit[1] is output_tokenizer:
         return hit[2]
@@ -25,13 +26,38 @@ def remap_table(input_tokenizer, output_tokenizer, device):
             lut.append(int(input_tokenizer.stoi(output_tokenizer.itos(j))))
         except (KeyError, IndexError):
             lut.append(-1)
-    t = torch.tensor(lut, dtype=torch.int32).to(device)
+    t = torch.tensor(lut, dtype=torch.int32)
+    _CACHE[key] = (input_tokenizer, output_tokenizer, t)
+    return t
+
+
+def remap_table(input_tokenizer, output_tokenizer, device):
+    """The host table on ``device``, cached per (pair, device)."""
+    key = (id(input_tokenizer), id(output_tokenizer), str(device))
+    hit = _CACHE.get(key)
+    if hit is not None and hit[0] is input_tokenizer and hit[1] is output_tokenizer:
+        return hit[2]
+    t = host_table(input_tokenizer, output_tokenizer).to(device)
     _CACHE[key] = (input_tokenizer, output_tokenizer, t)
     return t
 
 
 class RemapError(KeyError):
     pass
+
+
+def raise_if_unmapped(err, comm=None):
+    """Raise RemapError if a remapped id had no input-vocabulary token, where
+    the reference's ``stoi`` raises KeyError inside the reward (diversity.py:
+    55-60) — i.e. before its backward / optimizer step.  Called between the
+    rewards and the first parameter update (one host sync, tokenizer runs
+    only); on an item-sharded step the flag is summed over the ranks first so
+    every rank raises together."""
+    if comm is not None:
+        comm.all_reduce(err)
+    if int(err.item()):
+        err.zero_()
+        raise RemapError("a predicted id has no input-vocabulary token (input_tokenizer.stoi(output_tokenizer.itos(id)))")
 
 
 def remap_ids(idx, lut, err=None):

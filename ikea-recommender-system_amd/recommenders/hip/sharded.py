@@ -26,7 +26,7 @@ import torch
 
 from . import call, host_ptr_array, stream_ptr
 from .engine import _f32
-from .remap import remap_ids
+from .remap import raise_if_unmapped, remap_ids
 from .timing import region
 
 
@@ -274,6 +274,8 @@ def sharded_double_q_step(nets, clocks, k, s, a, r, s_next, true_len, true_next_
         else:
             top = _global_topk(main, sup, w, max(smorl["topk_div"], smorl["topk_nov"]), "sup_topk")
         rr = _smorl_rewards_rows(main, smorl, s, r, true_next_len, top[rows].contiguous(), B)
+        if smorl.get("lut") is not None:   # every rank raises together, before any update
+            raise_if_unmapped(smorl["remap_err"], comm)
         row = _buf(main, "qrow", (B,))
         q_loss = _buf(main, "qloss32", (1,))
         grad_row = _f32(np.float32(smorl["alpha"]) / np.float32(Bg))
@@ -323,7 +325,8 @@ def _smorl_rewards_rows(main, smorl, s, r_acc, true_next_len, idx, B):
     lens = _dev(true_next_len, dev, torch.int64)   # quirk: diversity uses true_next_len
     idx_div = idx if smorl.get("lut") is None else remap_ids(idx, smorl["lut"], smorl["remap_err"])
     call("rg_diversity", s.data_ptr(), s.shape[1], lens.data_ptr(), 1 if smorl["pad_end"] else 0,
-         idx_div.data_ptr(), smorl["topk_div"], K, smorl["div_table"].data_ptr(), smorl["div_table"].shape[1],
+         idx_div.data_ptr(), smorl["topk_div"], K, smorl["div_table"].data_ptr(), smorl["div_table"].shape[0],
+         smorl["div_table"].shape[1],
          _f32(1e-6), B, r_div.data_ptr(), st)
     r_nov = _buf(main, "r_nov", (B,))
     call("rg_novelty", idx.data_ptr(), smorl["topk_nov"], K, smorl["bitmap"].data_ptr(), _f32(smorl["nov_rew_sig"]),

@@ -24,7 +24,7 @@ class SupervisedNet(HipNet):
             mask = self.dropout_mask(h.shape[0])
             h = self.apply_mask(h, mask, torch.empty_like(h))
         head = next(iter(self.heads.values()))
-        _, z = head.logits_T(h, slot="eval")
+        _, z = head.logits_T(h)
         return z
 
 

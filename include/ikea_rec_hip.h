@@ -159,6 +159,12 @@ int rg_flash_rows_per_block(int HF);
 int rg_flash_fwd_top(const void* Hk, const void* Wk, const void* Wr, const float* bias_pad, int B, int A, int HF,
                      int terms, int nsplit, float* pm, float* pl, float* pO, float* pbest, int32_t* parg, float* cmax,
                      rg_stream_t stream);
+/* rg_flash_score: evaluation scoring (evaluate / update_train_metrics, eval_protocol.py:123-359)
+ *   — pass 1's S-part without the O contraction: pm / pl (-> rg_flash_lse), per-split first maximum
+ *   (pbest / parg) and every 32-item chunk's row maximum cmax (ceil(A/32) x B, -> rg_flash_topk for
+ *   the exact canonical top-K); no (B x A) logits.  terms 6 / 9 (636 reads as 6). */
+int rg_flash_score(const void* Hk, const void* Wk, const float* bias_pad, int B, int A, int HF, int terms, int nsplit,
+                   float* pm, float* pl, float* pbest, int32_t* parg, float* cmax, rg_stream_t stream);
 /* rg_flash_amax_fwd: argmax only (the double-Q target, sqn_gru.py:222-226) — pass 1's S-part on the
  *   K-planes of h and W with per-split first maximum (pbest / parg as rg_flash_fwd_top), no softmax. */
 int rg_flash_amax_fwd(const void* Hk, const void* Wk, const float* bias_pad, int B, int A, int HF, int terms,
@@ -276,9 +282,12 @@ int rg_sqn_td(const float* q, float* qn, const double* r, const uint8_t* is_end,
 int rg_smorl_td(const float* q, float* qn, const float* r, const uint8_t* is_end, const float* w, int nh,
                 float gamma, float grad_row, int B, float* row_loss, float* dq, rg_stream_t stream);
 int rg_sum64(const double* x, int n, double scale, double* out64, float* out32, rg_stream_t stream);
-/* A12 diversity reward: recommenders/evaluate/diversity.py:15-73. */
+/* A12 diversity reward: recommenders/evaluate/diversity.py:15-73.  D has Drows
+ * rows; a row whose last action or predicted id lies outside [0, Drows) (an
+ * unmapped tokenizer id, where the reference's stoi raises KeyError) gets NaN
+ * and no table read. */
 int rg_diversity(const int64_t* s, int L, const int64_t* lens, int pad_end, const int32_t* idx, int k, int ldi,
-                 const float* D, int Ed, float eps, int B, float* out, rg_stream_t stream);
+                 const float* D, int64_t Drows, int Ed, float eps, int B, float* out, rg_stream_t stream);
 /* A13 novelty reward: recommenders/evaluate/novelty.py:12-47 (U as bitmap). */
 int rg_novelty(const int32_t* idx, int k, int ldi, const uint32_t* bitmap, float reward, int B, float* out,
                rg_stream_t stream);
@@ -290,6 +299,11 @@ int rg_novelty(const int32_t* idx, int k, int ldi, const uint32_t* bitmap, float
  * out_val (B, k) optional; *err |= 2 on candidate overflow (massive ties). */
 int rg_topk(const float* ZT, int64_t ldz, const float* pmax, int B, int A, int k, int32_t* out_idx, float* out_val,
             int32_t* err, rg_stream_t stream);
+/* repetition counts (recommenders/evaluate/repetitiveness.py:21-57): out[q] += number of
+ * (b, t, j) with s[b, t] == idx[b, j] and j < ks[q] (ks: HOST int array, nk <= 16, k <= K;
+ * integer counts, deterministic).  idx: (B, K) predicted ids in the input vocabulary. */
+int rg_repetitions(const int64_t* s, int L, const int32_t* idx, int K, int B, const int* ks, int nk,
+                   unsigned long long* out, rg_stream_t stream);
 /* HR@k / NDCG@k sums (eval_protocol.py:26-100) accumulated into out
  * (2*nk doubles: hits..., ndcg...); ks: HOST int array, k <= K. */
 int rg_hits_ndcg(const int32_t* idx, int K, const int64_t* tgt, int B, const int* ks, int nk, double* out,

@@ -1,0 +1,74 @@
+"""bench.py's multi-rank contract on CPU (no GPU touched): ``--gpus N``
+without a torch.distributed launcher starts N ranks as child processes and
+relays rank 0's JSON line; WORLD_SIZE != --gpus is an error."""
+import importlib.util
+import os
+import subprocess
+import sys
+import types
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _bench():
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(ROOT, "bench.py"))
+    m = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(m)
+    return m
+
+
+def test_check_world(monkeypatch):
+    b = _bench()
+    args = types.SimpleNamespace(gpus=1)
+    monkeypatch.delenv("WORLD_SIZE", raising=False)
+    assert b.check_world(args) is None
+    args.gpus = 4
+    assert b.check_world(args) == ("launch", 4)
+    monkeypatch.setenv("WORLD_SIZE", "4")
+    assert b.check_world(args) is None
+    monkeypatch.setenv("WORLD_SIZE", "2")
+    assert b.check_world(args)[0] == "error"
+
+
+def test_relay_picks_the_result_line():
+    b = _bench()
+    out = "RCCL version 2.x\n{\"not\": 1}\nnoise {\n{\"metric\": \"m\", \"value\": 3, \"n_gpus\": 2}\ntrailer\n"
+    assert b.relay_json(out) == "{\"metric\": \"m\", \"value\": 3, \"n_gpus\": 2}"
+    assert b.relay_json("nothing here") is None
+
+
+def test_launch_ranks_runs_torch_distributed_and_relays(capsys):
+    b = _bench()
+    seen = {}
+
+    def runner(cmd, stdout=None, env=None, text=None):
+        seen["cmd"], seen["env"] = cmd, env
+        return types.SimpleNamespace(returncode=0, stdout="banner\n{\"metric\": \"x\", \"n_gpus\": 2}\n")
+
+    args = types.SimpleNamespace(gpus=2)
+    rc = b.launch_ranks(args, ["--gpus", "2", "--steps", "3"], runner=runner)
+    assert rc == 0
+    cmd = seen["cmd"]
+    assert cmd[1:3] == ["-m", "torch.distributed.run"]
+    assert "--nproc-per-node=2" in cmd and "--master-addr=127.0.0.1" in cmd and "--nnodes=1" in cmd
+    assert cmd[-4:] == ["--gpus", "2", "--steps", "3"] and cmd[-5].endswith("bench.py")
+    assert seen["env"]["HSA_ENABLE_IPC_MODE_LEGACY"] == "0"
+    assert capsys.readouterr().out.strip() == "{\"metric\": \"x\", \"n_gpus\": 2}"
+
+
+def test_launch_ranks_failure_is_nonzero():
+    b = _bench()
+    runner = lambda cmd, **kw: types.SimpleNamespace(returncode=3, stdout="boom")  # noqa: E731
+    assert b.launch_ranks(types.SimpleNamespace(gpus=2), [], runner=runner) == 3
+    runner = lambda cmd, **kw: types.SimpleNamespace(returncode=0, stdout="no json")  # noqa: E731
+    assert b.launch_ranks(types.SimpleNamespace(gpus=2), [], runner=runner) == 1
+
+
+def test_world_size_mismatch_exits_nonzero():
+    env = dict(os.environ, WORLD_SIZE="2")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "1"], env=env,
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode != 0
+    assert "WORLD_SIZE=2" in r.stderr

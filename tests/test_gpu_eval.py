@@ -96,3 +96,97 @@ def test_evaluate_matches_oracle():
     np.testing.assert_allclose(reps, R_ / n, atol=0)
     for k in (1, 5):
         assert cov[k][1] == len(covs[k]) / N
+
+
+@pytest.mark.parametrize("N,B,H,K", [(3000, 100, 32, 20), (70000, 256, 64, 10), (20011, 96, 128, 32),
+                                     (5003, 65, 256, 1)])
+def test_score_topk_equals_native_logits_topk(N, B, H, K):
+    """Evaluation scoring without a (B, A) buffer (SoftmaxHead.score_topk:
+    rg_flash_score + rg_flash_lse + rg_flash_topk) against the native head's
+    stored logits of the same h: the canonical top-K index lists AND values
+    bitwise equal (the re-scoring repeats the native MFMA's fmaf chain), the
+    per-row CE within fp32 rounding of rg_lse_combine's; ragged B."""
+    from recommenders.data_utils.synthetic import SessionStream
+    from recommenders.hip.evalpath import head_for
+    from recommenders.models.GRU4Rec.model import GRU4Rec
+    torch.manual_seed(5)
+    m = GRU4Rec(hidden_size=H, embedding_dim=H, item_num=N, state_size=8, action_dim=N, device="cuda")
+    m.eval()
+    s, a, r, sn, ln, nln, e = SessionStream(N, 8, B, seed=11).batch(0, B)
+    h = m.hidden(s.cuda(), ln, slot="eval")
+    head = head_for(m, 0)
+    idx, vals, loss_row = head.score_topk(h, K, a.cuda())
+    ws, z = head.logits_T(h)
+    zc = z.cpu().numpy()
+    ref = om.canonical_topk(zc, K)
+    assert int(head.top_err.item()) == 0
+    np.testing.assert_array_equal(idx.cpu().numpy(), ref)
+    np.testing.assert_array_equal(vals.cpu().numpy(), np.take_along_axis(zc, ref, 1))
+    ce = torch.nn.functional.cross_entropy(torch.from_numpy(zc).double(), a, reduction="none").numpy()
+    np.testing.assert_allclose(loss_row.cpu().double().numpy(), ce, rtol=0, atol=2e-5)
+
+
+def test_score_topk_row_chunks(monkeypatch):
+    """Row-chunked scoring (chunk maxima capped, several chunks plus a ragged
+    tail) gives the same lists and values as one chunk; the CE rows agree to
+    fp32 rounding (the lse merges a different number of item splits)."""
+    from recommenders.data_utils.synthetic import SessionStream
+    from recommenders.hip import engine
+    from recommenders.hip.evalpath import head_for
+    N, B, K = 40000, 300, 20
+    m = _model(N=N)
+    m.eval()
+    s, a, r, sn, ln, nln, e = SessionStream(N, 8, B, seed=12).batch(0, B)
+    h = m.hidden(s.cuda(), ln, slot="eval")
+    head = head_for(m, 0)
+    i1, v1, l1 = (x.clone() for x in head.score_topk(h, K, a.cuda()))
+    head.release_eval()
+    monkeypatch.setattr(engine, "EVAL_CMAX_BYTES", 64 * 4 * ((N + 31) // 32))   # 64 rows per chunk
+    i2, v2, l2 = head.score_topk(h, K, a.cuda(), slot="eval2")
+    assert head._sws_eval["eval2"].R == 64
+    np.testing.assert_array_equal(i1.cpu().numpy(), i2.cpu().numpy())
+    np.testing.assert_array_equal(v1.cpu().numpy(), v2.cpu().numpy())
+    np.testing.assert_allclose(l1.cpu().numpy(), l2.cpu().numpy(), rtol=4e-7, atol=0)
+
+
+def test_eval_allocates_no_logits():
+    """evaluate()'s per-batch scoring leaves no (B, A) buffer behind and
+    allocates far less than one (C2-like width, A = 200k)."""
+    from recommenders.data_utils.synthetic import SessionStream, unpopular_items
+    from recommenders.evaluate.eval_protocol import evaluate
+    from recommenders.models.GRU4Rec.model import GRU4Rec
+    N, L, B = 200_000, 20, 1024
+    m = GRU4Rec(hidden_size=128, embedding_dim=128, item_num=N, state_size=L, action_dim=N, device="cuda")
+    st = SessionStream(N, L, 2 * B, seed=13)
+    loader = [(b[0], b[1], b[4]) for b in (st.batch(i, B) for i in range(2))]
+    torch.cuda.synchronize()
+    base = torch.cuda.memory_allocated()
+    torch.cuda.reset_peak_memory_stats()
+    evaluate(loader, m, "cuda", None, "end", None, unpopular_items(st.item_counts()), topk_hr_ndcg=[20])
+    torch.cuda.synchronize()
+    zt_bytes = 4 * B * N
+    assert torch.cuda.max_memory_allocated() - base < zt_bytes // 2
+    assert not any(k[0] == "eval" for k in m.heads["output"]._ws)
+
+
+def test_evaluate_unmapped_token_raises():
+    """A predicted id with no input-vocabulary token: the reference's stoi
+    raises KeyError inside evaluate(); here RemapError (a KeyError), and the
+    diversity kernel never reads the table at row -1."""
+    from recommenders.data_utils.synthetic import SessionStream, unpopular_items
+    from recommenders.evaluate.eval_protocol import evaluate
+    from recommenders.hip.remap import RemapError
+    from recommenders.utils.tokenizer import Tokenizer
+    N, L, B = 3000, 8, 64
+    m = _model(N=N, L=L)
+    st = SessionStream(N, L, B, seed=14)
+    b = st.batch(0, B)
+    loader = [(b[0], b[1], b[4])]
+    names = [f"item{j}" for j in range(N)]
+    tout = Tokenizer(names)
+    tin = Tokenizer(names[: N // 2])        # no <unk>: half of the output ids cannot be mapped
+    table = torch.randn(N // 2 + 2, 8)
+    with pytest.raises(RemapError):
+        evaluate(loader, m, "cuda", None, "end", torch.nn.Embedding.from_pretrained(table), unpopular_items(
+            st.item_counts()), topk_hr_ndcg=[20], topk_to_consider_div=20, input_tokenizer=tin, output_tokenizer=tout)
+    torch.cuda.synchronize()     # the device is healthy afterwards

@@ -331,9 +331,10 @@ def test_flash_error_is_fp32_class(case):
 
 
 # ------------------------------------------------------------- fused top-k --
-def run_top(h, W, b, terms, nsplit, K):
-    """Pass 1 with the top-k outputs, then rg_flash_argmax (K = 1) or
-    rg_flash_topk: (idx (B, K) int64, vals (B, K) f64, err)."""
+def run_top(h, W, b, terms, nsplit, K, exact1=False):
+    """Pass 1 with the top-k outputs, then rg_flash_argmax (K = 1, unless
+    exact1: the trainers' K = 1 re-scoring) or rg_flash_topk:
+    (idx (B, K) int64, vals (B, K) f64, err)."""
     call, st = C().call, C().stream_ptr()
     B, HF = h.shape
     A = W.shape[0]
@@ -345,13 +346,13 @@ def run_top(h, W, b, terms, nsplit, K):
     z = lambda *s, dt=torch.float32: torch.full(s, -7, dtype=dt, device=dev)  # noqa: E731
     pm, pl, pO = z(nsplit, B), z(nsplit, B), z(nsplit, HF, B)
     pbest, parg = z(nsplit, B), z(nsplit, B, dt=torch.int32)
-    cmax = z((A + 31) // 32, B) if K > 1 else None
+    cmax = z((A + 31) // 32, B) if K > 1 or exact1 else None
     call("rg_flash_fwd_top", Hk.data_ptr(), Wk.data_ptr(), Wr.data_ptr(), bp.data_ptr(), B, A, HF, terms, nsplit,
          pm.data_ptr(), pl.data_ptr(), pO.data_ptr(), pbest.data_ptr(), parg.data_ptr(),
          None if cmax is None else cmax.data_ptr(), st)
     idx, vals = z(B, K, dt=torch.int32), z(B, K)
     err = torch.zeros(1, dtype=torch.int32, device=dev)
-    if K == 1:
+    if K == 1 and not exact1:
         call("rg_flash_argmax", pbest.data_ptr(), parg.data_ptr(), nsplit, B, idx.data_ptr(), vals.data_ptr(), st)
     else:
         cap = call("rg_flash_topk_cap")
@@ -362,7 +363,7 @@ def run_top(h, W, b, terms, nsplit, K):
     return idx.cpu().long(), vals.cpu().double(), int(err.item()), (None if cmax is None else cmax.cpu().double())
 
 
-@pytest.mark.parametrize("precision", ["f32x6", "f32x9"])
+@pytest.mark.parametrize("precision", ["f32x6", "f32x9", "f32x6d3"])
 @pytest.mark.parametrize("B,A,HF,nsplit,K", [(128, 3001, 64, 8, 1), (96, 20011, 128, 16, 1), (256, 5000, 256, 8, 1),
                                              (128, 3001, 64, 8, 12), (96, 20011, 128, 16, 20),
                                              (160, 5003, 256, 8, 12), (64, 777, 32, 3, 32)])
@@ -393,6 +394,42 @@ def test_fused_topk_matches_canonical_fp64(precision, B, A, HF, nsplit, K):
         np.testing.assert_allclose(cmax.numpy().T, Zp.reshape(B, nct, 32).max(2), rtol=0, atol=tol)
 
 
+@pytest.mark.parametrize("precision", ["f32x6", "f32x6d3"])
+@pytest.mark.parametrize("B,A,HF,nsplit", [(128, 50000, 128, 16), (64, 5003, 256, 8), (96, 3001, 64, 8)])
+def test_fused_top1_rescored_is_first_fp32_maximum(precision, B, A, HF, nsplit):
+    """SMORL's top-1 reward item (topk_div = topk_nov = 1, the C4 bench
+    setting) through the trainers' path: pass 1's chunk maxima + rg_flash_topk
+    with K = 1, i.e. the fp32 re-scoring — the first maximum of the fp32
+    logits also where the split-bf16 logits alone could pick another item:
+    planted exact duplicates (lowest index wins) and near-ties 1e-6 apart."""
+    h, W, b, _ = inputs(B, A, HF, 5 * B + A)
+    Z = h.double() @ W.double().t() + b.double()
+    top = Z.argmax(1)
+    for r in range(0, B, 3):            # exact tie: a copy of the winner at a higher index
+        j = int(top[r])
+        k = (j * 7919 + 13) % A
+        if k > j:
+            W[k], b[k] = W[j], b[j]
+    for r in range(1, B, 3):            # near tie: a slightly better copy at a lower index
+        j = int(top[r])
+        k = (j * 104729 + 7) % A
+        if k < j:
+            W[k], b[k] = W[j], b[j] + 1e-6
+    Z = h.double() @ W.double().t() + b.double()
+    idx, vals, err, _ = run_top(h.to(dev), W.to(dev), b.to(dev), TERMS[precision], nsplit, 1, exact1=True)
+    assert err == 0
+    zmax = Z.max(1).values
+    first = (Z >= zmax[:, None]).double().argmax(1)
+    sl = (h.abs().double() @ W.abs().double().t()).max(1).values
+    for r in range(B):
+        if int(idx[r, 0]) != int(first[r]):
+            assert float(zmax[r] - Z[r, idx[r, 0]]) <= 200 * 2.0 ** -24 * float(sl[r]), r
+    for r in range(0, B, 3):
+        assert int(idx[r, 0]) == int(first[r])
+    for r in range(1, B, 3):
+        assert int(idx[r, 0]) == int(first[r])
+
+
 def test_fused_topk_exact_ties_keep_lowest_index():
     """Exact ties (duplicated W rows and biases): lowest item first, as the
     canonical order and torch.argmax's first maximum."""
@@ -410,7 +447,7 @@ def test_fused_topk_exact_ties_keep_lowest_index():
             assert (idx[:, 1:4] == torch.tensor([1234, 2500, 3999])).all()
 
 
-@pytest.mark.parametrize("precision", ["f32x6", "f32x9"])
+@pytest.mark.parametrize("precision", ["f32x6", "f32x9", "f32x6d3"])
 @pytest.mark.parametrize("B,A,HF,nsplit", [(128, 3001, 64, 8), (96, 20011, 128, 16), (160, 5003, 256, 8),
                                            (64, 777, 32, 3)])
 def test_fused_argmax_only(precision, B, A, HF, nsplit):

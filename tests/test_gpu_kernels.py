@@ -333,7 +333,7 @@ def test_q_kernels_and_rewards():
     top = torch.topk(preds, 3).indices.to(torch.int32)
     out = torch.zeros(B, device=dev)
     hip.call("rg_diversity", D(s).data_ptr(), L, D(lens).data_ptr(), 1, D(top).data_ptr(), 3, 3,
-             D(table).data_ptr(), Ed, 1e-6, B, out.data_ptr(), st())
+             D(table).data_ptr(), table.shape[0], Ed, 1e-6, B, out.data_ptr(), st())
     torch.testing.assert_close(out.cpu(), om.batch_diversity_rewards(s, preds, lens, "end", 3, table), rtol=0,
                                atol=1e-6)
     unpop = set(range(0, A, 3))

@@ -122,6 +122,18 @@ def _fp64_head(h, W, b, tgt, rows, chunk=131072):
     return lse, lse - zt, dh
 
 
+def _cpu_fp32_dh(h, W, b, tgt, rows, B):
+    """The reference's own CPU fp32 path on the same rows: nn.Linear logits,
+    CrossEntropyLoss(mean over the B-row batch) and autograd
+    (GRU4Rec/model.py:80, 121, 146-150) -> dh of those rows."""
+    torch.set_num_threads(max(8, min(16, torch.get_num_threads())))
+    hr = h[rows].cpu().float().requires_grad_(True)
+    z = hr @ W.cpu().float().t() + b.cpu().float()
+    loss = torch.nn.functional.cross_entropy(z, tgt[rows].cpu(), reduction="sum") / B
+    loss.backward()
+    return hr.grad.double().to(h.device)
+
+
 @pytest.mark.parametrize("precision", ["f32x6", "f32", "f32x6d3"])
 def test_full_c2_step_lse_ce_dh_against_fp64(precision):
     from recommenders.data_utils.synthetic import SessionStream
@@ -145,9 +157,17 @@ def test_full_c2_step_lse_ce_dh_against_fp64(precision):
     e_ce = float((w.loss_row[rows].double() - ce64).abs().max())
     e_dh = float((dh[rows].double() - dh64).abs().max())
     scale = float(dh64.abs().max())
-    print(f"{precision}: |lse err| {e_lse:.3g}, |CE err| {e_ce:.3g}, |dh err| {e_dh:.3g} (|dh| max {scale:.3g})")
+    # the reference CPU fp32 path's own dh error on the same rows (the bar of
+    # test_flash_error_is_fp32_class, here at the benched width A = 1M)
+    e_cpu = float((_cpu_fp32_dh(h, W0, b0, tgt, rows, BF) - dh64).abs().max())
+    floor = 8 * 2.0 ** -24 * scale
+    print(f"{precision}: |lse err| {e_lse:.3g}, |CE err| {e_ce:.3g}, |dh err| {e_dh:.3g} "
+          f"(reference CPU fp32 {e_cpu:.3g}, |dh| max {scale:.3g})")
     assert e_lse < 1e-4 and e_ce < 1e-4
-    assert e_dh <= 1e-4 * scale
+    # split-bf16 precisions (the bench / trainer default f32x6d3 included):
+    # within 2x of the reference CPU fp32 path; the native fp32-MFMA side path
+    # ("f32": dh = dZ·W summed over 1M items in split-K slabs) within 4x
+    assert e_dh <= max((4 if precision == "f32" else 2) * e_cpu, floor), (precision, e_dh, e_cpu)
     assert abs(loss - float(w.loss_row.double().mean())) < 1e-5
     assert np.isfinite(loss)
 

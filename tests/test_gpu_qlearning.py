@@ -133,3 +133,81 @@ def test_smorl_c5_shape_matches_oracle(precision):
             assert float(d.max()) <= 2 * lr + 1e-5, k
             assert float((d > 1e-4).float().mean()) < 1e-3, k
         assert torch.equal(mine.trunk.emb16.cpu(), mine.trunk.emb.p.cpu().half())
+
+
+def test_smorl_c4_bench_path_matches_oracle():
+    """The benched C4 instantiation (bench.py --config c4) at an oracle-sized
+    item count: SMORL 3-reward, H = E = 128, B % 32 == 0, L 50, precision
+    f32x6d3 (fused supervised head k_flash_fwd<128, 6, 3, true>: pass 1's
+    top-1 for the rewards re-scored in fp32, rg_flash_topk K = 1), screening
+    argmax for the double-Q target, q_weights [1, 1, 1], topk_div = topk_nov
+    = 1 — against OracleSMORL (the reference's helpers composed,
+    smorl_gru.py:233-334)."""
+    from oracle.models import OracleSMORL
+    from recommenders.data_utils.synthetic import SessionStream, unpopular_items
+    from recommenders.models.SMORL.smorl_gru import SMORL_trainer
+    N, L, B, E = 30000, 50, 256, 128
+    st = SessionStream(N, L, B * 4, seed=21)
+    g = torch.Generator().manual_seed(7)
+    table = torch.randn(N + 1, 64, generator=g) * 0.01
+    unpop = unpopular_items(st.item_counts())
+    cfg = dict(hidden_dim=E, embedding_dim=E, padding_pos="end", train_pad_embed=True, use_packed_seq=True,
+               learning_rate=0.01, item_num=N, state_size=L, action_dim=N, gamma=0.5, gru_layers=1,
+               q_weights=[1.0, 1.0, 1.0], alpha=1.0, div_embedding=table, unpopular_actions_set=unpop, topk_div=1,
+               topk_nov=1, nov_rew_sig=1.0)
+    torch.set_num_threads(8)
+    orc = OracleSMORL(**cfg)
+    rs_o = random.getstate()
+    tr = SMORL_trainer(device="cuda", matmul_precision="f32x6d3", **cfg)
+    rs_t = random.getstate()
+    assert tr.SMORL_1.sup_head_output.flash_terms(B) == 636
+    for i in range(4):
+        b = st.batch(i, B)
+        random.setstate(rs_o)
+        so, qo = orc.step(*b)
+        rs_o = random.getstate()
+        random.setstate(rs_t)
+        sg, qg = tr.train_step(*b)
+        rs_t = random.getstate()
+        assert orc.last_main == tr.last_main
+        np.testing.assert_allclose(tr.last_rewards.cpu().numpy(), orc.last_rewards.numpy(), rtol=0, atol=1e-5)
+        assert abs(so - sg) < 1e-4 and abs(qo - qg) < 1e-5, (i, so, sg, qo, qg)
+    lr = cfg["learning_rate"]
+    for mine, ref in ((tr.SMORL_1, orc.nets[0]), (tr.SMORL_2, orc.nets[1])):
+        sd_o = ref.state_dict()
+        for k, v in mine.state_dict().items():
+            d = (v.cpu() - sd_o[k]).abs()
+            assert float(d.max()) <= 2 * lr + 1e-5, k
+            assert float((d > 1e-4).float().mean()) < 1e-3, k
+
+
+def test_smorl_unmapped_token_raises_before_update():
+    """Tokenizer pair where a predicted output id has no input token: the
+    reference's stoi raises KeyError inside the diversity reward, before its
+    backward; here RemapError is raised before any parameter update (weights,
+    Adam moments and clocks unchanged), on train_step and train_step_async."""
+    from recommenders.data_utils.synthetic import SessionStream, unpopular_items
+    from recommenders.hip.remap import RemapError
+    from recommenders.models.SMORL.smorl_gru import SMORL_trainer
+    from recommenders.utils.tokenizer import Tokenizer
+    N, L, B, E = 2000, 10, 64, 32
+    st = SessionStream(N, L, B, seed=5)
+    names = [f"item{j}" for j in range(N)]
+    tout = Tokenizer(names)
+    tin = Tokenizer(names[: N // 4])     # no <unk>: three quarters of the ids cannot be mapped
+    table = torch.randn(N // 4 + 2, 16)
+    tr = SMORL_trainer(hidden_dim=E, embedding_dim=E, padding_pos="end", train_pad_embed=True, use_packed_seq=True,
+                       learning_rate=0.01, item_num=N, state_size=L, action_dim=N, gamma=0.5, gru_layers=1,
+                       q_weights=[1.0, 1.0, 1.0], alpha=1.0, div_embedding=table,
+                       unpopular_actions_set=unpopular_items(st.item_counts()), topk_div=8, topk_nov=1,
+                       device="cuda", input_tokenizer=tin, output_tokenizer=tout)
+    before = [{k: v.clone() for k, v in net.state_dict().items()} for net in (tr.SMORL_1, tr.SMORL_2)]
+    clocks = (tr.clock_1.t, tr.clock_2.t)
+    for fn in (tr.train_step, tr.train_step_async):
+        with pytest.raises(RemapError):
+            fn(*st.batch(0, B))
+    torch.cuda.synchronize()
+    assert (tr.clock_1.t, tr.clock_2.t) == clocks
+    for net, sd in zip((tr.SMORL_1, tr.SMORL_2), before):
+        for k, v in net.state_dict().items():
+            assert torch.equal(v, sd[k]), k
