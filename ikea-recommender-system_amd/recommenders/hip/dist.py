@@ -6,6 +6,7 @@ host memory — used to run several ranks on one GPU in tests and on CPU.
 """
 from __future__ import annotations
 
+import numpy as np
 import torch
 
 
@@ -19,6 +20,17 @@ class Comm:
         self.rank = dist.get_rank(group)
         self.world = dist.get_world_size(group)
         self.native = dist.get_backend(group) == "nccl"
+        # host-side group for the small per-step routing counts (computed on
+        # the host from the host batch): a gloo group next to RCCL, so the
+        # count exchange never waits on the device stream
+        self.host_group = dist.new_group(backend="gloo") if self.native else group
+
+    def host_all_gather(self, t):
+        """(world, *t.shape) CPU tensor of every rank's CPU tensor ``t`` (no device sync)."""
+        t = t.contiguous()
+        parts = [torch.empty_like(t) for _ in range(self.world)]
+        self.dist.all_gather(parts, t, group=self.host_group)
+        return torch.stack(parts)
 
     def all_gather(self, out, inp):
         """out (world·n) ← concat over ranks of inp (n), rank-major."""
@@ -65,3 +77,33 @@ class Comm:
 def item_shard(A, world, rank):
     """Contiguous, balanced item range [lo, hi) owned by `rank`."""
     return (rank * A) // world, ((rank + 1) * A) // world
+
+
+def owner_counts(s, lens, L, packed, n_rows, world):
+    """Per owner rank, the number of this batch's packed tokens whose table row
+    it holds (host restatement of csrc/emb_shard.hip k_token_ids +
+    k_shard_route: tokens t < clamp(len, 1, L) of every row, all L when
+    unpacked; owner ⌈(id+1)·W/N1⌉ − 1; ids outside [0, N1) go to rank 0)."""
+    s = np.asarray(s)
+    B = s.shape[0]
+    ln = np.clip(np.asarray(lens, dtype=np.int64), 1, L) if packed else np.full(B, L, dtype=np.int64)
+    ids = s[np.arange(L)[None, :] < ln[:, None]]
+    ok = (ids >= 0) & (ids < n_rows)
+    own = np.where(ok, ((ids + 1) * world + n_rows - 1) // n_rows - 1, 0)
+    return np.bincount(own, minlength=world).astype(np.int64)
+
+
+def host_routes(comm, trunk, passes):
+    """Send / receive splits of every trunk pass's id / row exchange, from
+    the host batch: owner counts per pass, one host all-gather over the gloo
+    group (W × passes × W ints).  passes: [(s, lens)] host tensors; returns
+    [(send_splits, recv_splits)] or None when a batch is already on the device
+    (then the exchange routes on the device and reads the counts back)."""
+    for s, ln in passes:
+        if torch.as_tensor(s).device.type != "cpu" or torch.as_tensor(ln).device.type != "cpu":
+            return None
+    mine = np.stack([owner_counts(torch.as_tensor(s).numpy(), torch.as_tensor(ln).numpy(), torch.as_tensor(s).shape[1],
+                                  trunk.packed, trunk.N1, comm.world) for s, ln in passes])
+    allc = comm.host_all_gather(torch.from_numpy(mine)).numpy()   # (W, P, W): [q, p, r]
+    r = comm.rank
+    return [(allc[r, p, :].tolist(), allc[:, p, r].tolist()) for p in range(len(passes))]

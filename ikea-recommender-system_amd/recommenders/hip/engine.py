@@ -19,7 +19,6 @@ LinearHead   a Linear(H→A) used only through row gathers / argmax (Q heads).
 from __future__ import annotations
 
 import math
-import os
 
 import numpy as np
 import torch
@@ -245,8 +244,11 @@ class Trunk:
             self._ws[key] = w
         return w
 
-    def forward(self, s, lens, slot="main", save=False):
-        """s: int64 (B, L) device; lens: int64 (B,) device or CPU. Returns h (B, ndir*H)."""
+    def forward(self, s, lens, slot="main", save=False, route=None):
+        """s: int64 (B, L) device; lens: int64 (B,) device or CPU. Returns h (B, ndir*H).
+        route (item-sharded table): this pass's (send_splits, recv_splits) from
+        the host batch (dist.host_routes); None routes on the device and reads
+        the counts back (one sync)."""
         B, L = s.shape
         w = self.ws(slot, B, L, save)
         st = stream_ptr()
@@ -260,7 +262,7 @@ class Trunk:
         H, E = self.H, self.E
         if self.comm is not None:
             with region("gather"):
-                self._exchange_rows(w, s, B, L, st)
+                self._exchange_rows(w, s, B, L, st, route)
         for d in range(self.ndir):
             w_ih, w_hh, b_ih, b_hh = self.dirs[d]
             if self.comm is None:
@@ -397,46 +399,62 @@ class Trunk:
                      self.G_emb.data_ptr(), self.tags.data_ptr(), tag, self.n_local, self.E, adam6, st)
 
     # ---- row-sharded table: id / row / gradient exchange (csrc/emb_shard.hip) ----
-    def _exchange_rows(self, w, s, B, L, st):
+    def _xbuf(self, w, name, rows, cols=None, dtype=torch.int32):
+        """Exchange buffer of at least ``rows`` rows, kept on the pass's
+        workspace and grown (×1.25) only when a step needs more."""
+        t = getattr(w, name, None)
+        if t is None or t.shape[0] < rows or t.dtype != dtype:
+            n = max(16, int(rows * 1.25) if t is not None else rows)
+            t = torch.empty((n,) if cols is None else (n, cols), dtype=dtype, device=self.device)
+            setattr(w, name, t)
+        return t
+
+    def _exchange_rows(self, w, s, B, L, st, route=None):
         """Rows of every packed token of this rank's batch from their owners:
-        route by owner, all-to-all the ids, owners gather, all-to-all the rows."""
+        route by owner, all-to-all the ids, owners gather, all-to-all the rows.
+        With ``route`` (splits computed on the host from the host batch) no
+        device value is read back; otherwise the device counts are (one sync)."""
         comm, W = self.comm, self.comm.world
         if getattr(w, "slot", None) is None:
             w.slot = torch.empty(w.TM, dtype=torch.int32, device=self.device)
             w.send_ids = torch.empty(w.TM, dtype=torch.int32, device=self.device)
             w.counts = torch.zeros(W, dtype=torch.int32, device=self.device)
             w.counts_all = torch.zeros(W * W, dtype=torch.int32, device=self.device)
+            w.nrecv = torch.zeros(1, dtype=torch.int32, device=self.device)
         call("rg_token_ids", s.data_ptr(), B, L, w.perm.data_ptr(), w.lsort.data_ptr(), w.offs.data_ptr(), self.N1,
              w.tok_id[0].data_ptr(), self.err.data_ptr(), st)
         call("rg_shard_route", w.tok_id[0].data_ptr(), w.ntok_ptr, self.N1, W, w.slot.data_ptr(),
              w.send_ids.data_ptr(), w.counts.data_ptr(), st)
-        comm.all_gather(w.counts_all, w.counts)
-        M = w.counts_all.view(W, W).cpu()            # M[q][r]: tokens of rank q owned by rank r (one sync)
-        w.send_splits = M[comm.rank].tolist()
-        w.recv_splits = M[:, comm.rank].tolist()
+        if route is not None:
+            w.send_splits, w.recv_splits = list(route[0]), list(route[1])
+        else:
+            comm.all_gather(w.counts_all, w.counts)
+            M = w.counts_all.view(W, W).cpu()            # M[q][r]: tokens of rank q owned by rank r (one sync)
+            w.send_splits = M[comm.rank].tolist()
+            w.recv_splits = M[:, comm.rank].tolist()
         T, R = sum(w.send_splits), sum(w.recv_splits)
         w.T, w.R = T, R
         half = self.emb16 is not None
         rdt = torch.float16 if half else torch.float32
-        w.recv_ids = torch.empty(max(R, 1), dtype=torch.int32, device=self.device)
-        w.local_ids = torch.empty(max(R, 1), dtype=torch.int32, device=self.device)
-        w.nrecv = torch.tensor([R], dtype=torch.int32, device=self.device)
-        comm.all_to_all(w.recv_ids[:R], w.send_ids[:T], w.recv_splits, w.send_splits)
-        rows_out = torch.empty(max(R, 1), self.E, dtype=rdt, device=self.device)
-        call("rg_rows_gather", w.recv_ids.data_ptr(), R, self.lo, self.n_local,
+        recv_ids = self._xbuf(w, "recv_ids", max(R, 1))
+        w.local_ids = self._xbuf(w, "local_ids_buf", max(R, 1))
+        w.nrecv.fill_(R)
+        comm.all_to_all(recv_ids[:R], w.send_ids[:T], w.recv_splits, w.send_splits)
+        rows_out = self._xbuf(w, "rows_out", max(R, 1), self.E, rdt)
+        call("rg_rows_gather", recv_ids.data_ptr(), R, self.lo, self.n_local,
              (self.emb16 if half else self.emb.p).data_ptr(), self.E, 1 if half else 0, rows_out.data_ptr(),
              w.local_ids.data_ptr(), st)
-        w.rows_in = torch.empty(max(T, 1), self.E, dtype=rdt, device=self.device)
+        w.rows_in = self._xbuf(w, "rows_in_buf", max(T, 1), self.E, rdt)
         comm.all_to_all(w.rows_in[:T], rows_out[:R], w.send_splits, w.recv_splits)
 
     def _exchange_grads(self, w, tag, st):
         """Row-gradients of this rank's tokens to their owners; the owner adds
         them into its gradient rows (tagged for the row-sparse Adam)."""
         comm = self.comm
-        gsend = torch.empty(max(w.T, 1), self.E, device=self.device)
+        gsend = self._xbuf(w, "gsend", max(w.T, 1), self.E, torch.float32)
         call("rg_collect_grads", w.dX[0].data_ptr(), w.dX[1].data_ptr() if self.ndir == 2 else None,
              w.slot.data_ptr(), w.lsort.data_ptr(), w.offs.data_ptr(), w.B, self.E, gsend.data_ptr(), st)
-        grecv = torch.empty(max(w.R, 1), self.E, device=self.device)
+        grecv = self._xbuf(w, "grecv", max(w.R, 1), self.E, torch.float32)
         comm.all_to_all(grecv[:w.R], gsend[:w.T], w.recv_splits, w.send_splits)
         pad = self.pad - self.lo
         skip = -1 if self.train_pad or not (0 <= pad < self.n_local) else pad
@@ -493,7 +511,7 @@ class _FlashWS:
         self.pO = z(self.nsplit, HF, B)
         self.rows = z(B, 2)
         # pass 2's split-tail partials (rg_flash_dw_work_bytes; 0 when the grid has no tail to split)
-        self.dw_work_bytes = int(call("rg_flash_dw_work_bytes", B, A, HF)) if PASS2_TAIL_SPLIT else 0
+        self.dw_work_bytes = int(call("rg_flash_dw_work_bytes", B, A, HF))
         self.dw_work = u8(max(self.dw_work_bytes, 16))
         self.lse, self.zt, self.loss_row = z(B), z(B), z(B)
         self.loss = torch.zeros(1, device=device)
@@ -592,17 +610,12 @@ class _AmaxWS:
 # RG_TERMS_*); LOGIT_TERMS: every logits-only split GEMM (sampled head, Q
 # argmax)
 SPLIT_TERMS = {"f32x9": 9, "f32x6": 6, "f32x6d3": 636}
-# RG_PASS2_PLANES=0: pass 2 leaves W's operand planes to the next rg_head_planes (A/B measurement)
-PASS2_PLANES = os.environ.get("RG_PASS2_PLANES", "1") != "0"
-# RG_PASS2_TAIL=0: pass 2's leftover item blocks run as a partial last round (A/B measurement)
-PASS2_TAIL_SPLIT = os.environ.get("RG_PASS2_TAIL", "1") != "0"
 # split-bf16 argmax (SQN / SMORL double-Q target): screening on 3 plane products, then every item
 # of every 32-item chunk whose screened maximum lies within SCREEN_TOL·||h_b||·max_a||W_a|| of the
 # row's best is re-scored in fp32 (first maximum).  The bound covers the dropped plane products
 # (3·2^-18), fp32 accumulation of both sums (384 + 128 terms at 2^-24) on both sides, with margin
 # (DESIGN §4a).  Needs ceil(A/32)·B floats of chunk maxima; above SCREEN_CMAX_BYTES the rows
-# are screened in 2048-row chunks (C5 at one GPU); RG_SCREEN_ARGMAX=0 runs the 6-product argmax.
-SCREEN_ARGMAX = os.environ.get("RG_SCREEN_ARGMAX", "1") != "0"
+# are screened in 2048-row chunks (C5 at one GPU).
 SCREEN_TOL = 1e-4
 SCREEN_CMAX_BYTES = 2 << 30
 SCREEN_ROW_CHUNK = 2048
@@ -859,14 +872,6 @@ class SoftmaxHead:
         updated W / b also leave as this workspace's operand planes and padded
         bias (the next flash_forward on it skips rg_head_planes for W)."""
         Wp, bp = self._Wp, self._bp   # not the joining properties: this may run on the side stream
-        if not PASS2_PLANES:
-            with region("head_dw_adam"):
-                call("rg_flash_dw_adam", w.Hk.data_ptr(), w.Hr.data_ptr(), w.Wk.data_ptr(), w.bias_pad.data_ptr(),
-                     w.rows.data_ptr(), g, w.B, self.A, self.HF, w.terms, Wp.p.data_ptr(), Wp.m.data_ptr(),
-                     Wp.v.data_ptr(), bp.p.data_ptr(), bp.m.data_ptr(), bp.v.data_ptr(), adam6, None, None,
-                     stream_ptr())
-            self._wgen += 1
-            return
         with region("head_dw_adam"):
             call("rg_flash_dw_adam_planes", w.Hk.data_ptr(), w.Hr.data_ptr(), w.Wk.data_ptr(),
                  w.bias_pad.data_ptr(), w.rows.data_ptr(), g, w.B, self.A, self.HF, w.terms, Wp.p.data_ptr(),
@@ -955,37 +960,31 @@ class SoftmaxHead:
         st = stream_ptr()
         terms = self.flash_terms(B)
         if terms:
-            # screening (3 plane products + exact fp32 re-scoring of the chunks
-            # within the error bound) unless its chunk maxima would not fit
-            screen = SCREEN_ARGMAX
+            # screening (3 plane products) + exact fp32 re-scoring of the
+            # chunks within the error bound (rows in chunks when the chunk
+            # maxima would not fit SCREEN_CMAX_BYTES)
             w = self._aws.get(slot) if hasattr(self, "_aws") else None
-            if w is None or w.B != B or w.screen != screen:
+            if w is None or w.B != B:
                 if not hasattr(self, "_aws"):
                     self._aws = {}
                 self._aws.pop(slot, None)
-                w = self._aws[slot] = _AmaxWS(B, self.A, self.HF, self.device, screen)
+                w = self._aws[slot] = _AmaxWS(B, self.A, self.HF, self.device, True)
             W, b = self.W.p.data_ptr(), self.b.p.data_ptr()
             call("rg_head_planes", h.data_ptr(), B, self.HF, w.Hk.data_ptr(), None, None, None, st)
             call("rg_head_planes", W, self.A, self.HF, w.Wk.data_ptr(), None, b, w.bias_pad.data_ptr(), st)
-            if not screen:
-                call("rg_flash_amax_fwd", w.Hk.data_ptr(), w.Wk.data_ptr(), w.bias_pad.data_ptr(), B, self.A, self.HF,
-                     terms, w.nsplit, w.pbest.data_ptr(), w.parg.data_ptr(), st)
-                call("rg_flash_argmax", w.pbest.data_ptr(), w.parg.data_ptr(), w.nsplit, B, w.amax.data_ptr(),
-                     w.mx.data_ptr(), st)
-            else:
-                call("rg_row_norm_max", W, self.A, self.HF, w.wnorm.data_ptr(), st)
-                hk_row = self.HF * 6   # K-plane bytes per row
-                for r0 in range(0, B, w.Bc):
-                    bc = min(w.Bc, B - r0)
-                    call("rg_flash_amax_screen", w.Hk.data_ptr() + r0 * hk_row, w.Wk.data_ptr(),
-                         w.bias_pad.data_ptr(), bc, self.A, self.HF, w.nsplit, w.pbest.data_ptr(),
-                         w.parg.data_ptr(), w.cmax.data_ptr(), st)
-                    call("rg_flash_argmax", w.pbest.data_ptr(), w.parg.data_ptr(), w.nsplit, bc,
-                         w.amax.data_ptr() + 4 * r0, w.mx.data_ptr() + 4 * r0, st)
-                    call("rg_flash_argmax_exact", w.cmax.data_ptr(), bc, self.A, h.data_ptr() + 4 * r0 * self.HF, W, b,
-                         self.HF, w.wnorm.data_ptr(), _f32(SCREEN_TOL), w.lim.data_ptr() + 4 * r0,
-                         w.cand.data_ptr() + 4 * r0 * call("rg_flash_topk_cap"), w.ncand.data_ptr() + 4 * r0,
-                         w.amax.data_ptr() + 4 * r0, w.mx.data_ptr() + 4 * r0, st)
+            call("rg_row_norm_max", W, self.A, self.HF, w.wnorm.data_ptr(), st)
+            hk_row = self.HF * 6   # K-plane bytes per row
+            for r0 in range(0, B, w.Bc):
+                bc = min(w.Bc, B - r0)
+                call("rg_flash_amax_screen", w.Hk.data_ptr() + r0 * hk_row, w.Wk.data_ptr(),
+                     w.bias_pad.data_ptr(), bc, self.A, self.HF, w.nsplit, w.pbest.data_ptr(),
+                     w.parg.data_ptr(), w.cmax.data_ptr(), st)
+                call("rg_flash_argmax", w.pbest.data_ptr(), w.parg.data_ptr(), w.nsplit, bc,
+                     w.amax.data_ptr() + 4 * r0, w.mx.data_ptr() + 4 * r0, st)
+                call("rg_flash_argmax_exact", w.cmax.data_ptr(), bc, self.A, h.data_ptr() + 4 * r0 * self.HF, W, b,
+                     self.HF, w.wnorm.data_ptr(), _f32(SCREEN_TOL), w.lim.data_ptr() + 4 * r0,
+                     w.cand.data_ptr() + 4 * r0 * call("rg_flash_topk_cap"), w.ncand.data_ptr() + 4 * r0,
+                     w.amax.data_ptr() + 4 * r0, w.mx.data_ptr() + 4 * r0, st)
             self.argmax_mx = w.mx
             return w.amax
         w = self.ws(slot, B, False)

@@ -131,10 +131,6 @@ def _dev(x, dev, dtype=None):
     return x if dtype is None else x.to(dtype)
 
 
-from .supervised import OVERLAP_HEAD_DW  # noqa: E402
-
-# RG_TARGET_FIRST=0 issues the double-Q target after the supervised head's forward (A/B measurement)
-TARGET_FIRST = __import__("os").environ.get("RG_TARGET_FIRST", "1") != "0"
 
 
 def double_q_step(nets, clocks, k, s, a, r, s_next, true_len, true_next_len, is_end, *, gamma, smorl=None):
@@ -162,12 +158,9 @@ def double_q_step(nets, clocks, k, s, a, r, s_next, true_len, true_next_len, is_
     # the double-Q target needs neither the supervised head nor its workspace,
     # so it is issued before forward_loss, whose access of the head waits for
     # the previous step's overlapped pass 2: target and pass 2 share the GPU
-    if TARGET_FIRST:
-        qn = target()
+    qn = target()
     sup_loss, _ = main.sup_head_output.forward_loss(h, a, slot="main")
     q = main.gather_q(h, idx64=a, out=main.buf("q", (B, nh)))
-    if not TARGET_FIRST:
-        qn = target()
     dq = main.buf("dq", (B, nh))
     if smorl is None:
         r64 = _dev(r, dev, torch.float64)
@@ -192,7 +185,7 @@ def double_q_step(nets, clocks, k, s, a, r, s_next, true_len, true_next_len, is_
     tag = main.trunk_tag
     dh = main.dh_buffer(B)
     # the supervised head's pass 2 overlaps the Q heads' backward / Adam and the trunk
-    main.sup_head_output.backward_step(h, a, dh, adam6, slot="main", overlap=OVERLAP_HEAD_DW)
+    main.sup_head_output.backward_step(h, a, dh, adam6, slot="main", overlap=True)
     call("rg_q_backward", h.data_ptr(), main.hf, host_ptr_array([x.W.p for x in main.q_heads]),
          host_ptr_array([x.G for x in main.q_heads]), host_ptr_array([x.Gb for x in main.q_heads]),
          host_ptr_array([x.tags for x in main.q_heads]), nh, a.data_ptr(), B, dq.data_ptr(), dh.data_ptr(), tag, st)

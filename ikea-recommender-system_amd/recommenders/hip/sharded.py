@@ -26,6 +26,7 @@ import torch
 
 from . import call, host_ptr_array, stream_ptr
 from .engine import _f32
+from .dist import host_routes
 from .remap import raise_if_unmapped, remap_ids
 from .timing import region
 
@@ -90,7 +91,6 @@ def _sharded_ce_dh(net, head, w, lse, tgt_loc, dH_all, st):
     call("rg_reduce_slabs", w.dh_slabs.data_ptr(), n, Bg * net.hf, dH_all.data_ptr(), None, net.hf, 0, st)
 
 
-from .supervised import OVERLAP_HEAD_DW  # noqa: E402
 
 
 def _sharded_ce_dw_adam(net, head, w, lse, tgt_loc, H_all, adam6, st):
@@ -113,12 +113,14 @@ def _gather_rows(comm, net, name, x):
 def sharded_supervised_step(net, clock, s, a, true_len):
     comm = net.comm
     dev = net.device
+    # the id / row exchange's splits from the host batch (no device read-back)
+    route = host_routes(comm, net.trunk, [(s, true_len)])
     s = s.to(dev, non_blocking=True)
     a = a.to(dev, non_blocking=True).contiguous()
     head = next(iter(net.heads.values()))
     HF = net.hf
     st = stream_ptr()
-    h = net.trunk.forward(s, true_len, slot="main", save=True)
+    h = net.trunk.forward(s, true_len, slot="main", save=True, route=route and route[0])
     B = h.shape[0]
     Bg = comm.world * B
     mask = None
@@ -135,7 +137,7 @@ def sharded_supervised_step(net, clock, s, a, true_len):
     net.trunk_tag = getattr(net, "trunk_tag", 0) + 1
     dH_all = _buf(net, "dH_all", (Bg, HF))
     _sharded_ce_dh(net, head, w, lse, tgt_loc, dH_all, st)
-    fused = bool(getattr(w, "terms", 0)) and OVERLAP_HEAD_DW
+    fused = bool(getattr(w, "terms", 0))
     if fused:   # pass 2 on the head's side stream under the exchanges and the trunk backward
         head.flash_dw_adam_async(w, _f32(1.0 / Bg), adam6)
     dh = net.dh_buffer(B)
@@ -225,6 +227,9 @@ def sharded_double_q_step(nets, clocks, k, s, a, r, s_next, true_len, true_next_
     main, boot = nets[k], nets[1 - k]
     comm = main.comm
     dev = main.device
+    # splits of the three trunk passes' id / row exchanges from the host batch
+    # (one host all-gather over the gloo group; no device read-back)
+    routes = host_routes(comm, main.trunk, [(s, true_len), (s_next, true_next_len), (s_next, true_len)]) or [None] * 3
     s = _dev(s, dev)
     a = _dev(a, dev).contiguous()
     s_next = _dev(s_next, dev)
@@ -238,7 +243,7 @@ def sharded_double_q_step(nets, clocks, k, s, a, r, s_next, true_len, true_next_
     st = stream_ptr()
     sup = main.sup_head_output
     with region("sqn_trunk_main"):
-        h = main.trunk.forward(s, true_len, slot="main", save=True)
+        h = main.trunk.forward(s, true_len, slot="main", save=True, route=routes[0])
     with region("comm_fwd"):
         H_all = _gather_rows(comm, main, "H_all", h)
         a_all = _gather_rows(comm, main, "a_all", a)
@@ -247,12 +252,13 @@ def sharded_double_q_step(nets, clocks, k, s, a, r, s_next, true_len, true_next_
     sup_loss = w.loss
     q_all, a_loc = _owner_q(main, main, H_all, "q", idx64=a_all)
     with region("sqn_target"):
-        h_n = main.trunk.forward(s_next, true_next_len, slot="next", save=False)
+        h_n = main.trunk.forward(s_next, true_next_len, slot="next", save=False, route=routes[1])
         Hn_all = _gather_rows(comm, main, "Hn_all", h_n)
         am = main.argmax_q(Hn_all, None if smorl is None else smorl["w"])
         head_am = main.q_heads[0] if len(main.q_heads) == 1 else main._argmax_head
         a_star = _global_argmax(main, head_am.argmax_mx, am, A, "a_star")
-        h_b = boot.trunk.forward(s_next, true_len, slot="boot", save=False)   # quirk: true_len
+        h_b = boot.trunk.forward(s_next, true_len, slot="boot", save=False,   # quirk: true_len
+                                 route=routes[2])
         Hb_all = _gather_rows(comm, main, "Hb_all", h_b)
         qn_all, _ = _owner_q(boot, main, Hb_all, "qn", idx32=a_star)
     q = q_all[rows]
@@ -289,7 +295,7 @@ def sharded_double_q_step(nets, clocks, k, s, a, r, s_next, true_len, true_next_
     tag = main.trunk_tag
     dH_all = _buf(main, "dH_all", (Bg, HF))
     _sharded_ce_dh(main, sup, w, lse, tgt_loc, dH_all, st)
-    fused = bool(getattr(w, "terms", 0)) and OVERLAP_HEAD_DW
+    fused = bool(getattr(w, "terms", 0))
     if fused:   # pass 2 on the supervised head's side stream under the rest of the step
         sup.flash_dw_adam_async(w, _f32(1.0 / Bg), adam6)
     dq_all = _gather_rows(comm, main, "dq_all", dq)

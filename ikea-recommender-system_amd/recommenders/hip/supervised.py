@@ -8,7 +8,6 @@ body of GRU4Rec_trainer and BidirGRU4Rec_trainer
 """
 from __future__ import annotations
 
-import os
 
 import torch
 
@@ -28,8 +27,6 @@ class SupervisedNet(HipNet):
         return z
 
 
-# RG_OVERLAP_HEAD_DW=0 keeps pass 2 on the launch stream (A/B measurement)
-OVERLAP_HEAD_DW = os.environ.get("RG_OVERLAP_HEAD_DW", "1") != "0"
 
 
 def supervised_step(net: SupervisedNet, clock, s, a, true_len):
@@ -57,7 +54,7 @@ def supervised_step(net: SupervisedNet, clock, s, a, true_len):
     # the head's pass 2 (dW + Adam) runs on a side stream under the trunk
     # backward (which needs only dh) and the next step's trunk forward; the
     # head joins it on the next access of its parameters or workspace
-    head.backward_step(h_in, a, dh, adam6, slot="main", overlap=OVERLAP_HEAD_DW)
+    head.backward_step(h_in, a, dh, adam6, slot="main", overlap=True)
     if mask is not None:
         net.apply_mask(dh, mask, dh)
     net.trunk.backward(dh, slot="main")

@@ -82,6 +82,21 @@ def _worker(rank, world, port, q):
         for t, d in zip(toks, dXs):
             full.index_add_(0, t, d)
         assert torch.allclose(dtab, full[elo:ehi], atol=1e-12)
+        # host routing of the sharded table's exchange (no device read-back):
+        # every rank's send / receive splits from the host batches
+        import types
+        from recommenders.hip.dist import host_routes, owner_counts
+        N1r, L = 101, 6
+        trunk = types.SimpleNamespace(packed=True, N1=N1r)
+        batches = [(torch.randint(0, N1r, (5, L), generator=gen), torch.randint(1, L + 1, (5,), generator=gen))
+                   for _ in range(world)]
+        batches2 = [(torch.randint(0, N1r, (5, L), generator=gen), torch.randint(1, L + 1, (5,), generator=gen))
+                    for _ in range(world)]
+        routes = host_routes(comm_f, trunk, [batches[rank], batches2[rank]])
+        for p_, bs in enumerate((batches, batches2)):
+            M = [owner_counts(x.numpy(), ln.numpy(), L, True, N1r, world) for x, ln in bs]
+            assert routes[p_][0] == list(M[rank])
+            assert routes[p_][1] == [int(M[qq][rank]) for qq in range(world)]
         q.put((rank, "ok"))
     except Exception as e:  # pragma: no cover - reported to the parent
         q.put((rank, repr(e)))
@@ -111,3 +126,26 @@ def test_item_shard_partition():
             assert parts[0][0] == 0 and parts[-1][1] == A
             assert all(parts[i][1] == parts[i + 1][0] for i in range(w - 1))
             assert max(h - l for l, h in parts) - min(h - l for l, h in parts) <= 1
+
+
+def test_owner_counts_match_token_rules():
+    """dist.owner_counts (host routing) = the tokens k_token_ids / k_shard_route
+    send to each owner: t < clamp(len, 1, L) (all L unpacked), owner by
+    item_shard ranges, ids outside [0, N1) to rank 0."""
+    import numpy as np
+    sys.path.insert(0, os.path.join(REPO, "ikea-recommender-system_amd"))
+    from recommenders.hip.dist import item_shard, owner_counts
+    rng = np.random.default_rng(3)
+    for N1, W, L, packed in ((1001, 8, 7, True), (50, 3, 5, False), (9, 2, 4, True)):
+        s = rng.integers(-2, N1 + 3, size=(13, L))
+        lens = rng.integers(0, L + 3, size=13)
+        exp = np.zeros(W, dtype=np.int64)
+        for b in range(13):
+            n = L if not packed else min(max(int(lens[b]), 1), L)
+            for t in range(n):
+                i = int(s[b, t])
+                o = 0
+                if 0 <= i < N1:
+                    o = next(r for r in range(W) if item_shard(N1, W, r)[0] <= i < item_shard(N1, W, r)[1])
+                exp[o] += 1
+        np.testing.assert_array_equal(owner_counts(s, lens, L, packed, N1, W), exp)
