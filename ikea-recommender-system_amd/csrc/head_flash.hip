@@ -885,32 +885,43 @@ __device__ __forceinline__ void tk_insert(float (&t)[TK_MAX], float v) {
   }
 }
 
-// 64 rows per workgroup (lane = row), the 4 waves split the chunk range
-__global__ __launch_bounds__(256) void k_flash_topk_cand(const float* __restrict__ cmax, int nct, int B, int K,
-                                                         float tol_abs, float tol_rel, int32_t* __restrict__ cand,
-                                                         int32_t* __restrict__ ncand, int32_t* __restrict__ err) {
+// tau = the K-th largest chunk maximum of every row, in two stages so the
+// chunk range is read by the whole chip (one workgroup per row block scanning
+// all ceil(A/32) chunks was latency-bound: ~8 ms at C4 for K = 1).
+// Stage 1: grid (row blocks of 64, P parts of the chunk range), lane = row,
+// the 4 waves interleave the part's chunks; each wave keeps its top-K, the
+// part's top-K (merged in LDS) goes to part[p][i][row].
+__global__ __launch_bounds__(256) void k_topk_part(const float* __restrict__ cmax, int nct, int B, int K,
+                                                   float* __restrict__ part) {
   __shared__ float st[4][TK_MAX][64];
-  __shared__ int cnt[64];
-  __shared__ float tau_s[64];
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int row = blockIdx.x * 64 + lane;
   const bool ok = row < B;
+  const int P = gridDim.y, per = (nct + P - 1) / P;
+  const int c0 = blockIdx.y * per, c1 = min(nct, c0 + per);
   float t[TK_MAX];
 #pragma unroll
   for (int i = 0; i < TK_MAX; ++i) t[i] = NEG_INF;
   float thr = NEG_INF;   // t[K-1]
-  for (int c = w; c < nct; c += 4) {
-    const float v = ok ? cmax[(int64_t)c * B + row] : NEG_INF;
-    if (v > thr) {
-      tk_insert(t, v);
+  for (int c = c0 + w; c < c1; c += 16) {
+    float v[4];
 #pragma unroll
-      for (int i = 0; i < TK_MAX; ++i)
-        if (i == K - 1) thr = t[i];
+    for (int u = 0; u < 4; ++u) {   // four independent loads in flight per lane
+      const int cc = c + 4 * u;
+      v[u] = (ok && cc < c1) ? cmax[(int64_t)cc * B + row] : NEG_INF;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (v[u] > thr) {
+        tk_insert(t, v[u]);
+#pragma unroll
+        for (int i = 0; i < TK_MAX; ++i)
+          if (i == K - 1) thr = t[i];
+      }
     }
   }
 #pragma unroll
   for (int i = 0; i < TK_MAX; ++i) st[w][i][lane] = t[i];
-  if (w == 0) cnt[lane] = 0;
   __syncthreads();
   if (w == 0) {
     for (int q = 1; q < 4; ++q)
@@ -923,26 +934,35 @@ __global__ __launch_bounds__(256) void k_flash_topk_cand(const float* __restrict
             if (j == K - 1) thr = t[j];
         }
       }
-    tau_s[lane] = thr;
+    if (ok)
+#pragma unroll
+      for (int i = 0; i < TK_MAX; ++i)
+        if (i < K) part[((int64_t)blockIdx.y * K + i) * B + row] = t[i];
   }
-  __syncthreads();
-  const float tau = tau_s[lane];
-  const float lim = tau > NEG_INF ? tau - (tol_abs + tol_rel * fabsf(tau)) : NEG_INF;
-  for (int c = w; c < nct; c += 4) {
-    const float v = ok ? cmax[(int64_t)c * B + row] : NEG_INF;
-    if (ok && v >= lim) {
-      const int p = atomicAdd(&cnt[lane], 1);
-      if (p < TK_CAP) cand[(int64_t)row * TK_CAP + p] = c;
+}
+
+// Stage 2: per row the K-th largest of the P·K part values -> the candidate
+// limit lim = tau − (tol_abs + tol_rel·|tau|) (−inf while fewer than K finite
+// maxima exist: every chunk is then a candidate); ncand := 0.
+__global__ void k_topk_lim(const float* __restrict__ part, int P, int K, int B, float tol_abs, float tol_rel,
+                           float* __restrict__ lim, int32_t* __restrict__ ncand) {
+  const int row = blockIdx.x * blockDim.x + threadIdx.x;
+  if (row >= B) return;
+  float t[TK_MAX];
+#pragma unroll
+  for (int i = 0; i < TK_MAX; ++i) t[i] = NEG_INF;
+  float thr = NEG_INF;
+  for (int j = 0; j < P * K; ++j) {
+    const float v = part[(int64_t)j * B + row];
+    if (v > thr) {
+      tk_insert(t, v);
+#pragma unroll
+      for (int i = 0; i < TK_MAX; ++i)
+        if (i == K - 1) thr = t[i];
     }
   }
-  __syncthreads();
-  if (w == 0 && ok) {
-    const int n = cnt[lane];
-    // a tie run past the cap, or more than TK_CAP chunks with fewer than K
-    // finite maxima (tau = -inf: every chunk is a candidate)
-    if (n > TK_CAP) atomicOr(err, 1);
-    ncand[row] = min(n, TK_CAP);
-  }
+  lim[row] = thr > NEG_INF ? thr - (tol_abs + tol_rel * fabsf(thr)) : NEG_INF;
+  ncand[row] = 0;
 }
 
 // one workgroup (256 threads) per row: fp32 logits of the candidate items,
@@ -951,17 +971,23 @@ __global__ __launch_bounds__(256) void k_flash_topk_cand(const float* __restrict
 // HF/2 + s from half 1, i.e. fmaf over s of (h[s]·w[s], then h[HF/2+s]·w[HF/2+s]),
 // then + bias), so a re-scored logit is bitwise the one the model's forward()
 // stores and the top-K equals the canonical top-K of those logits.
+// A row with more than TK_CAP candidate chunks (a tie run past the cap) keeps
+// the caller's result and, with err, raises the overflow flag.
 __global__ __launch_bounds__(256) void k_flash_topk_eval(const float* __restrict__ h, const float* __restrict__ W,
                                                          const float* __restrict__ bias, const int32_t* __restrict__ cand,
                                                          const int32_t* __restrict__ ncand, int A, int HF, int K,
-                                                         int32_t* __restrict__ out_idx, float* __restrict__ out_val) {
+                                                         int32_t* __restrict__ out_idx, float* __restrict__ out_val,
+                                                         int32_t* __restrict__ err) {
   __shared__ __attribute__((aligned(16))) float hs[256];
   __shared__ float cv[TK_CAP * 32];
   __shared__ int ci[TK_CAP * 32];
   __shared__ float rv[4];
   __shared__ int ri[4], rs[4];
   const int row = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  if (ncand[row] < 0 || ncand[row] > TK_CAP) return;   // overflowed screening: the caller's result stays
+  if (ncand[row] < 0 || ncand[row] > TK_CAP) {   // overflow: the caller's result stays
+    if (err && threadIdx.x == 0) atomicOr(err, 1);
+    return;
+  }
   for (int k = tid; k < HF; k += 256) hs[k] = h[(int64_t)row * HF + k];
   const int n = ncand[row] * 32;
   __syncthreads();
@@ -1309,16 +1335,30 @@ extern "C" int rg_flash_argmax(const float* pbest, const int32_t* parg, int nspl
 
 extern "C" int rg_flash_topk_cap(void) { return TK_CAP; }
 
+// parts of the chunk range for tau (stage 1): ~2048 workgroups, >= 64 chunks each
+inline int topk_parts(int B, int nct) { return max(1, min(64, min(2048 / ((B + 63) / 64), nct / 64))); }
+
+extern "C" int64_t rg_flash_topk_work_bytes(int B, int A, int K) {
+  if (B <= 0 || A <= 0 || K <= 0 || K > TK_MAX) return RG_ERR_ARG;
+  return ((int64_t)topk_parts(B, (A + 31) / 32) * K * B + B) * 4;
+}
+
 extern "C" int rg_flash_topk(const float* cmax, int B, int A, int K, float tol_abs, float tol_rel, const float* h,
                              const float* W, const float* bias, int HF, int32_t* cand, int32_t* ncand, int32_t* out_idx,
-                             float* out_val, int32_t* err, hipStream_t stream) {
+                             float* out_val, int32_t* err, void* work, hipStream_t stream) {
   if (B <= 0 || A <= 0 || K <= 0 || K > TK_MAX || K > A || HF <= 0 || HF > 256 || (HF % 8)) return RG_ERR_ARG;
-  if (!cmax || !h || !W || !bias || !cand || !ncand || !out_idx || !err) return RG_ERR_ARG;
+  if (!cmax || !h || !W || !bias || !cand || !ncand || !out_idx || !err || !work) return RG_ERR_ARG;
   const int nct = (A + 31) / 32;
-  hipLaunchKernelGGL(k_flash_topk_cand, dim3((B + 63) / 64), dim3(256), 0, stream, cmax, nct, B, K, tol_abs, tol_rel,
-                     cand, ncand, err);
+  const int P = topk_parts(B, nct);
+  float* part = (float*)work;
+  float* lim = part + (int64_t)P * K * B;
+  hipLaunchKernelGGL(k_topk_part, dim3((B + 63) / 64, P), dim3(256), 0, stream, cmax, nct, B, K, part);
+  hipLaunchKernelGGL(k_topk_lim, dim3((B + 255) / 256), dim3(256), 0, stream, part, P, K, B, tol_abs, tol_rel, lim,
+                     ncand);
+  const int ys = max(1, min(256, 2048 / ((B + 255) / 256)));   // ~2048 workgroups over the chunk range
+  hipLaunchKernelGGL(k_amax_cand, dim3((B + 255) / 256, ys), dim3(256), 0, stream, cmax, nct, B, lim, cand, ncand);
   hipLaunchKernelGGL(k_flash_topk_eval, dim3(B), dim3(256), 0, stream, h, W, bias, cand, ncand, A, HF, K, out_idx,
-                     out_val);
+                     out_val, err);
   RG_LAUNCH_CHECK();
   return RG_OK;
 }
@@ -1495,7 +1535,7 @@ extern "C" int rg_flash_argmax_exact(const float* cmax, int B, int A, const floa
   const int ys = max(1, min(256, 2048 / ((B + 255) / 256)));   // ~2048 workgroups
   hipLaunchKernelGGL(k_amax_cand, dim3((B + 255) / 256, ys), dim3(256), 0, stream, cmax, nct, B, lim, cand, ncand);
   hipLaunchKernelGGL(k_flash_topk_eval, dim3(B), dim3(256), 0, stream, h, W, bias, cand, ncand, A, HF, 1, out_idx,
-                     out_val);
+                     out_val, (int32_t*)nullptr);
   RG_LAUNCH_CHECK();
   return RG_OK;
 }

@@ -309,11 +309,15 @@ extern "C" int rg_head_fwd_xp(const void* hplanes, const float* W, const float* 
 // a per-wave stamp breakdown puts ~40% in the prologue (the W rows' fragment
 // loads) and the rest at ~2× the MFMA time — see DESIGN.md §4 for the
 // variants tried (plane-fed GEMM, LDS-DMA row images, sliced epilogues).
-constexpr int SF_NEG = 256;   // negatives per workgroup (8 waves × 32)
+#ifndef SF_NW
+#define SF_NW 8               // waves per workgroup (each 32 negatives)
+#endif
+constexpr int SF_NEG = 32 * SF_NW;   // negatives per workgroup
+constexpr int SF_THR = 64 * SF_NW;   // threads per workgroup
 constexpr int SF_ROWS = 128;  // rows per workgroup (4 chunks of 32)
 
 template <int HF, int NT, bool DRAW>
-__global__ __launch_bounds__(512) void k_sampled_logits(const float* __restrict__ h, const float* __restrict__ W,
+__global__ __launch_bounds__(SF_THR) void k_sampled_logits(const float* __restrict__ h, const float* __restrict__ W,
                                                         const float* __restrict__ bias, int32_t* __restrict__ neg,
                                                         uint64_t seed, uint64_t counter, uint64_t A, int B, int S,
                                                         float* __restrict__ Z, int64_t ldz, float* __restrict__ pmax,
@@ -322,7 +326,7 @@ __global__ __launch_bounds__(512) void k_sampled_logits(const float* __restrict_
   constexpr int NS = HF / 16;
   constexpr int CH = NS * 192;              // 16-B fragments of one 32-row chunk's planes
   constexpr int ITEMS = 32 * (HF / 8);      // (row, 8-value group) items of one chunk
-  constexpr int IPT = (ITEMS + 511) / 512;  // per thread (1 at HF <= 128)
+  constexpr int IPT = (ITEMS + SF_THR - 1) / SF_THR;  // per thread (1 at HF <= 128, 8 waves)
   constexpr float L2E = 1.4426950408889634f;
   __shared__ bf16x8 hsA[CH], hsB[CH];
   __shared__ __attribute__((aligned(16))) float sbias[SF_NEG];
@@ -348,7 +352,7 @@ __global__ __launch_bounds__(512) void k_sampled_logits(const float* __restrict_
   auto load_h = [&](int c) __attribute__((always_inline)) {
 #pragma unroll
     for (int q = 0; q < IPT; ++q) {
-      const int i = tid + 512 * q;
+      const int i = tid + SF_THR * q;
       if (i < ITEMS) {
         const float* src = h + (int64_t)(rbase + 32 * c + (i & 31)) * HF + 8 * (i >> 5);
         st[q][0] = *reinterpret_cast<const f4*>(src);
@@ -359,7 +363,7 @@ __global__ __launch_bounds__(512) void k_sampled_logits(const float* __restrict_
   auto store_h = [&](bf16x8* hs) __attribute__((always_inline)) {
 #pragma unroll
     for (int q = 0; q < IPT; ++q) {
-      const int i = tid + 512 * q;
+      const int i = tid + SF_THR * q;
       if (i < ITEMS) {
         const int g = i >> 5;
         bf16x8 p0, p1, p2;
@@ -503,10 +507,10 @@ extern "C" int rg_sampled_logits(const float* h, const float* W, const float* bi
   const dim3 grid((unsigned)((S + SF_NEG - 1) / SF_NEG), (unsigned)((B + SF_ROWS - 1) / SF_ROWS));
 #define SFG(HFV, NTV)                                                                                            \
   if (draw)                                                                                                        \
-    RG_TLAUNCH((k_sampled_logits<HFV, NTV, true>), grid, dim3(512), 0, stream, h, W, bias, neg, seed,             \
+    RG_TLAUNCH((k_sampled_logits<HFV, NTV, true>), grid, dim3(SF_THR), 0, stream, h, W, bias, neg, seed,             \
                        counter, (uint64_t)A, B, S, Z, ldz, pmax, psum, Wg, bg);                                   \
   else                                                                                                             \
-    RG_TLAUNCH((k_sampled_logits<HFV, NTV, false>), grid, dim3(512), 0, stream, h, W, bias, neg, seed,            \
+    RG_TLAUNCH((k_sampled_logits<HFV, NTV, false>), grid, dim3(SF_THR), 0, stream, h, W, bias, neg, seed,            \
                        counter, (uint64_t)(A > 0 ? A : 0), B, S, Z, ldz, pmax, psum, Wg, bg)
 #define SFT(HFV)  \
   if (terms == 9) \

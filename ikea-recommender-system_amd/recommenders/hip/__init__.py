@@ -24,7 +24,8 @@ U64 = C.c_uint64
 
 # entry points returning int64_t (all others return int)
 RESTYPE_I64 = {"rg_sampled_work_bytes", "rg_head_work_bytes", "rg_head_plane_bytes", "rg_gru_wide_work_bytes",
-               "rg_scatter_rows_work_bytes", "rg_flash_dw_work_bytes"}
+               "rg_scatter_rows_work_bytes", "rg_flash_dw_work_bytes",
+               "rg_flash_topk_work_bytes"}
 
 # name -> argtypes
 SIGNATURES = {
@@ -58,7 +59,8 @@ SIGNATURES = {
     "rg_row_norm_max": [P, I64, I, P, P],
     "rg_flash_argmax_exact": [P, I, I, P, P, P, I, P, F, P, P, P, P, P, P],
     "rg_flash_topk_cap": [],
-    "rg_flash_topk": [P, I, I, I, F, F, P, P, P, I, P, P, P, P, P, P],
+    "rg_flash_topk": [P, I, I, I, F, F, P, P, P, I, P, P, P, P, P, P, P],
+    "rg_flash_topk_work_bytes": [I, I, I],
     "rg_flash_lse": [P, P, I, P, P, P, P, I64, I, I64, I, I, P, P, P],
     "rg_flash_rows": [P, P, I64, I, I, P, P],
     "rg_flash_dh": [P, P, P, I, P, F, I, I, P, P],

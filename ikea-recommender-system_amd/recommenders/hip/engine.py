@@ -525,6 +525,8 @@ class _FlashWS:
             self.cmax = z(-(-A // 32), B)
             self.cand = z(B, call("rg_flash_topk_cap"), dt=torch.int32)
             self.ncand = z(B, dt=torch.int32)
+            self.tk_work = torch.empty(call("rg_flash_topk_work_bytes", B, A, top_k), dtype=torch.uint8,
+                                       device=device)
 
 
 # evaluation scoring (SoftmaxHead.score_topk): rows per chunk such that the
@@ -562,6 +564,7 @@ class _ScoreWS:
         self.lse, self.zt = z(R), z(R)
         self.cand = z(R, call("rg_flash_topk_cap"), dt=torch.int32)
         self.ncand = z(R, dt=torch.int32)
+        self.tk_work = torch.empty(call("rg_flash_topk_work_bytes", R, A, K), dtype=torch.uint8, device=device)
         Bp = _round_up(B, R)
         self.idx, self.vals = z(Bp, K, dt=torch.int32), z(Bp, K)
         self.loss_row = z(Bp)
@@ -764,7 +767,7 @@ class SoftmaxHead:
                 call("rg_flash_topk", w.cmax.data_ptr(), B, self.A, K, _f32(self.TOP_TOL_ABS),
                      _f32(self.TOP_TOL_REL), w.h.data_ptr(), self._Wp.p.data_ptr(), self._bp.p.data_ptr(), self.HF,
                      w.cand.data_ptr(), w.ncand.data_ptr(), w.top_idx.data_ptr(), w.top_val.data_ptr(),
-                     self.top_err.data_ptr(), st)
+                     self.top_err.data_ptr(), w.tk_work.data_ptr(), st)
             return w.top_idx, w.top_val
         idx = torch.empty(B, K, dtype=torch.int32, device=self.device)
         vals = torch.empty(B, K, device=self.device)
@@ -811,7 +814,8 @@ class SoftmaxHead:
                 call("rg_sub", w.lse.data_ptr(), w.zt.data_ptr(), n, w.loss_row.data_ptr() + 4 * r0, st)
             call("rg_flash_topk", w.cmax.data_ptr(), R, A, K, _f32(self.TOP_TOL_ABS), _f32(self.TOP_TOL_REL),
                  hs.data_ptr(), Wp.p.data_ptr(), bp.p.data_ptr(), HF, w.cand.data_ptr(), w.ncand.data_ptr(),
-                 w.idx.data_ptr() + 4 * r0 * K, w.vals.data_ptr() + 4 * r0 * K, self.top_err.data_ptr(), st)
+                 w.idx.data_ptr() + 4 * r0 * K, w.vals.data_ptr() + 4 * r0 * K, self.top_err.data_ptr(),
+                 w.tk_work.data_ptr(), st)
         return w.idx[:B], w.vals[:B], (w.loss_row[:B] if tgt is not None else None)
 
     def _eval_planes(self, Wp, bp, st):

@@ -153,8 +153,11 @@ int rg_flash_fwd(const void* Hk, const void* Wk, const void* Wr, const float* bi
  * rg_flash_topk: canonical top-K (value desc, index asc; K <= 32) from cmax:
  *   candidate chunks are those whose maximum is >= tau - (tol_abs +
  *   tol_rel·|tau|), tau = the K-th largest chunk maximum; their items are
- *   rescored in fp32 (fmaf chain over HF, + bias).  cand: B × rg_flash_topk_cap()
- *   int32, ncand: B int32; err |= 1 on a candidate overflow. */
+ *   rescored in fp32 (the native fp32 head's fmaf chain over HF, + bias: bitwise
+ *   rg_head_fwd's logits).  tau comes from a chip-wide two-stage reduction of
+ *   the chunk maxima.  cand: B × rg_flash_topk_cap() int32, ncand: B int32,
+ *   work: rg_flash_topk_work_bytes(B, A, K) bytes; err |= 1 on a candidate
+ *   overflow (that row's output is left unchanged). */
 int rg_flash_rows_per_block(int HF);
 int rg_flash_fwd_top(const void* Hk, const void* Wk, const void* Wr, const float* bias_pad, int B, int A, int HF,
                      int terms, int nsplit, float* pm, float* pl, float* pO, float* pbest, int32_t* parg, float* cmax,
@@ -187,9 +190,10 @@ int rg_flash_argmax_exact(const float* cmax, int B, int A, const float* h, const
                           const float* wnorm, float tol, float* lim, int32_t* cand, int32_t* ncand, int32_t* out_idx,
                           float* out_val, rg_stream_t stream);
 int rg_flash_topk_cap(void);
+int64_t rg_flash_topk_work_bytes(int B, int A, int K);
 int rg_flash_topk(const float* cmax, int B, int A, int K, float tol_abs, float tol_rel, const float* h, const float* W,
                   const float* bias, int HF, int32_t* cand, int32_t* ncand, int32_t* out_idx, float* out_val,
-                  int32_t* err, rg_stream_t stream);
+                  int32_t* err, void* work, rg_stream_t stream);
 int rg_flash_lse(const float* pm, const float* pl, int nsplit, const float* h, const float* W, const float* bias,
                  const int64_t* tgt, int64_t lo, int A, int64_t A_full, int B, int HF, float* lse, float* zt,
                  rg_stream_t stream);

@@ -357,8 +357,9 @@ def run_top(h, W, b, terms, nsplit, K, exact1=False):
     else:
         cap = call("rg_flash_topk_cap")
         cand, ncand = z(B, cap, dt=torch.int32), z(B, dt=torch.int32)
+        work = _u8(call("rg_flash_topk_work_bytes", B, A, K))
         call("rg_flash_topk", cmax.data_ptr(), B, A, K, 1e-4, 1e-4, h.data_ptr(), W.data_ptr(), b.data_ptr(), HF,
-             cand.data_ptr(), ncand.data_ptr(), idx.data_ptr(), vals.data_ptr(), err.data_ptr(), st)
+             cand.data_ptr(), ncand.data_ptr(), idx.data_ptr(), vals.data_ptr(), err.data_ptr(), work.data_ptr(), st)
     torch.cuda.synchronize()
     return idx.cpu().long(), vals.cpu().double(), int(err.item()), (None if cmax is None else cmax.cpu().double())
 
