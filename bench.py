@@ -320,6 +320,8 @@ def head_roofline(kern, precision, B, N, E):
     pmc = os.path.join(HERE, "profiles", "pmc_traffic.json")
     if os.path.exists(pmc) and (B, N, E) == (BATCH, ITEMS, DIM):   # the PMC passes ran at the C2 shapes
         traffic = json.load(open(pmc)).get(f"{dom}:{precision}" if terms else dom)
+    elif os.path.exists(pmc) and (B, N, E) == (8192, 5_000_000, 256) and terms:   # ... and at C5 (r03g)
+        traffic = json.load(open(pmc)).get(f"c5:{dom}:{precision}")
     if terms:
         # fused split-bf16 head (csrc/head_flash.hip): pass 1 (head_fwd: Z and the softmax half of
         # dh) and pass 2 (head_dw_adam: Z recomputed, dW) each run two contractions, every fp32

@@ -161,15 +161,33 @@ extern "C" int rg_adam_rows_h(float* P, float* M, float* V, float* G, const int3
 }
 
 // out = fp16(x), round to nearest even (initial copy / after load_state_dict)
-__global__ void k_f32_to_f16(const float* __restrict__ x, int64_t n, __half* __restrict__ out) {
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+// 8 values per thread-iteration (two 16-B loads, one 16-B store; the
+// tables are E-wide rows, E % 8 == 0 — a scalar tail covers any n)
+__global__ __launch_bounds__(256) void k_f32_to_f16(const float* __restrict__ x, int64_t n, __half* __restrict__ out) {
+  const int64_t n8 = n / 8;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n8; i += stride) {
+    const f4 a = reinterpret_cast<const f4*>(x)[2 * i], b = reinterpret_cast<const f4*>(x)[2 * i + 1];
+    union {
+      __half h[8];
+      uint4 u;
+    } o;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      o.h[k] = __float2half_rn(a[k]);
+      o.h[4 + k] = __float2half_rn(b[k]);
+    }
+    reinterpret_cast<uint4*>(out)[i] = o.u;
+  }
+  for (int64_t i = 8 * n8 + blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += stride)
     out[i] = __float2half_rn(x[i]);
 }
 
 extern "C" int rg_f32_to_f16(const float* x, int64_t n, uint16_t* out, hipStream_t stream) {
   if (n <= 0) return RG_ERR_ARG;
-  int blocks = (int)((n + 255) / 256);
-  if (blocks > 16384) blocks = 16384;
+  if ((reinterpret_cast<uintptr_t>(x) & 15) || (reinterpret_cast<uintptr_t>(out) & 15)) return RG_ERR_ARG;
+  int blocks = (int)((n / 8 + 255) / 256);
+  blocks = blocks < 1 ? 1 : (blocks > 8192 ? 8192 : blocks);
   hipLaunchKernelGGL(k_f32_to_f16, dim3(blocks), dim3(256), 0, stream, x, n, reinterpret_cast<__half*>(out));
   RG_LAUNCH_CHECK();
   return RG_OK;

@@ -309,6 +309,9 @@ extern "C" int rg_head_fwd_xp(const void* hplanes, const float* W, const float* 
 // a per-wave stamp breakdown puts ~40% in the prologue (the W rows' fragment
 // loads) and the rest at ~2× the MFMA time — see DESIGN.md §4 for the
 // variants tried (plane-fed GEMM, LDS-DMA row images, sliced epilogues).
+#ifndef SF_STAGE_ALL
+#define SF_STAGE_ALL 0        // 1: h chunks 1..3 staged together (2 barriers instead of 4)
+#endif
 #ifndef SF_NW
 #define SF_NW 8               // waves per workgroup (each 32 negatives)
 #endif
@@ -329,6 +332,9 @@ __global__ __launch_bounds__(SF_THR) void k_sampled_logits(const float* __restri
   constexpr int IPT = (ITEMS + SF_THR - 1) / SF_THR;  // per thread (1 at HF <= 128, 8 waves)
   constexpr float L2E = 1.4426950408889634f;
   __shared__ bf16x8 hsA[CH], hsB[CH];
+#if SF_STAGE_ALL
+  __shared__ bf16x8 hsC[CH], hsD[CH];
+#endif
   __shared__ __attribute__((aligned(16))) float sbias[SF_NEG];
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, hh = lane >> 5, l32 = lane & 31;
   int bx = blockIdx.x, by = blockIdx.y;
@@ -349,25 +355,29 @@ __global__ __launch_bounds__(SF_THR) void k_sampled_logits(const float* __restri
   const int nch = min(SF_ROWS, B - rbase) / 32;   // B % 32 == 0
   // ---- h chunk staging: item i -> (group g, row) with the row fastest
   f4 st[IPT][2];
-  auto load_h = [&](int c) __attribute__((always_inline)) {
+#if SF_STAGE_ALL
+  f4 st2[IPT][2], st3[IPT][2];
+#endif
+  auto load_to = [&](f4 (&dst)[IPT][2], int c) __attribute__((always_inline)) {
 #pragma unroll
     for (int q = 0; q < IPT; ++q) {
       const int i = tid + SF_THR * q;
       if (i < ITEMS) {
         const float* src = h + (int64_t)(rbase + 32 * c + (i & 31)) * HF + 8 * (i >> 5);
-        st[q][0] = *reinterpret_cast<const f4*>(src);
-        st[q][1] = *reinterpret_cast<const f4*>(src + 4);
+        dst[q][0] = *reinterpret_cast<const f4*>(src);
+        dst[q][1] = *reinterpret_cast<const f4*>(src + 4);
       }
     }
   };
-  auto store_h = [&](bf16x8* hs) __attribute__((always_inline)) {
+  auto load_h = [&](int c) __attribute__((always_inline)) { load_to(st, c); };
+  auto store_from = [&](const f4 (&src)[IPT][2], bf16x8* hs) __attribute__((always_inline)) {
 #pragma unroll
     for (int q = 0; q < IPT; ++q) {
       const int i = tid + SF_THR * q;
       if (i < ITEMS) {
         const int g = i >> 5;
         bf16x8 p0, p1, p2;
-        split3x8(st[q][0], st[q][1], p0, p1, p2);
+        split3x8(src[q][0], src[q][1], p0, p1, p2);
         const int e = (g >> 1) * 192 + (g & 1) * 32 + (i & 31);
         hs[e] = p0;
         hs[e + 64] = p1;
@@ -375,6 +385,7 @@ __global__ __launch_bounds__(SF_THR) void k_sampled_logits(const float* __restri
       }
     }
   };
+  auto store_h = [&](bf16x8* hs) __attribute__((always_inline)) { store_from(st, hs); };
   // ---- this wave's negatives: draw, bias, fp32 rows in A-fragment layout.
   // Vector-memory issue order: bias, h chunk 0, the W rows, h chunk 1;
   // branch-free (a wave without negatives gathers row 0 and stores nothing).
@@ -401,6 +412,10 @@ __global__ __launch_bounds__(SF_THR) void k_sampled_logits(const float* __restri
   __builtin_amdgcn_sched_barrier(0);
   store_h(hsA);
   if (nch > 1) load_h(1);
+#if SF_STAGE_ALL
+  if (nch > 2) load_to(st2, 2);
+  if (nch > 3) load_to(st3, 3);
+#endif
   if (hh == 0) sbias[32 * w + l32] = bl;
   // barrier without a memory fence: only the LDS writes must be complete
   // (the W rows and h chunk 1 stay in flight); same for every barrier below
@@ -483,6 +498,37 @@ __global__ __launch_bounds__(SF_THR) void k_sampled_logits(const float* __restri
       epi(acc_old, c - 1);
     }
   };
+#if SF_STAGE_ALL
+  // chunks 1..3 (loaded before chunk 0's MFMAs) are split into their own LDS
+  // buffers behind those MFMAs, one more barrier, then the remaining MFMAs
+  // run back to back with the epilogues interleaved: 2 barriers, not 4
+  if (nch > 1) {
+    store_from(st, hsB);
+    if (nch > 2) store_from(st2, hsC);
+    if (nch > 3) store_from(st3, hsD);
+    sync_lds();
+    if (nact) {
+      mma(hsB, accB);
+      epi(accA, 0);
+      if (nch > 2) {
+        mma(hsC, accA);
+        epi(accB, 1);
+        if (nch > 3) {
+          mma(hsD, accB);
+          epi(accA, 2);
+          epi(accB, 3);
+        } else {
+          epi(accA, 2);
+        }
+      } else {
+        epi(accB, 1);
+      }
+    }
+  } else if (nact) {
+    epi(accA, 0);
+  }
+}
+#else
   if (nch > 1) step(1, hsB, accB, accA);
   if (nch > 2) step(2, hsA, accA, accB);
   if (nch > 3) step(3, hsB, accB, accA);
@@ -493,6 +539,7 @@ __global__ __launch_bounds__(SF_THR) void k_sampled_logits(const float* __restri
     if (nch == 4) epi(accB, 3);
   }
 }
+#endif
 
 // The fused forward (k_sampled_logits): Z row-major (B × ldz, ldz >= S).
 extern "C" int rg_sampled_logits(const float* h, const float* W, const float* bias, int32_t* neg, int draw,
