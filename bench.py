@@ -583,8 +583,8 @@ def main():
             roof["kernel"] = "gather + sampled_fwd"
             pmc = os.path.join(HERE, "profiles", "pmc_traffic.json")
             roof["traffic"] = None
-            if os.path.exists(pmc) and (B, args.negatives, HF, args.precision) == (4096, 2048, 256, "f32x6"):
-                roof["traffic"] = json.load(open(pmc)).get("c3:gather+sampled_fwd")
+            if os.path.exists(pmc) and (B, args.negatives, HF) == (4096, 2048, 256) and terms == 6:
+                roof["traffic"] = json.load(open(pmc)).get("c3:gather+sampled_fwd:r03")
     if rank != 0:
         if torch.distributed.is_initialized():
             torch.distributed.destroy_process_group()

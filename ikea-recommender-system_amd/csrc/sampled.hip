@@ -309,18 +309,19 @@ extern "C" int rg_head_fwd_xp(const void* hplanes, const float* W, const float* 
 // a per-wave stamp breakdown puts ~40% in the prologue (the W rows' fragment
 // loads) and the rest at ~2× the MFMA time — see DESIGN.md §4 for the
 // variants tried (plane-fed GEMM, LDS-DMA row images, sliced epilogues).
-#ifndef SF_STAGE_ALL
-#define SF_STAGE_ALL 0        // 1: h chunks 1..3 staged together (2 barriers instead of 4)
-#endif
 #ifndef SF_NW
-#define SF_NW 8               // waves per workgroup (each 32 negatives)
+#define SF_NW 8               // waves per workgroup (each 32 negatives) up to HF 128
 #endif
-constexpr int SF_NEG = 32 * SF_NW;   // negatives per workgroup
-constexpr int SF_THR = 64 * SF_NW;   // threads per workgroup
+// HF 256: a wave's 32 negatives are 192 VGPRs of operand planes plus 128 of
+// fp32 rows in flight, so one wave per SIMD (four per workgroup) and the
+// whole 512-entry register file
+constexpr int sf_nw(int HF) { return HF <= 128 ? SF_NW : 4; }
+constexpr int sf_neg(int HF) { return 32 * sf_nw(HF); }   // negatives per workgroup
+constexpr int sf_thr(int HF) { return 64 * sf_nw(HF); }   // threads per workgroup
 constexpr int SF_ROWS = 128;  // rows per workgroup (4 chunks of 32)
 
 template <int HF, int NT, bool DRAW>
-__global__ __launch_bounds__(SF_THR) void k_sampled_logits(const float* __restrict__ h, const float* __restrict__ W,
+__global__ __launch_bounds__(sf_thr(HF)) void k_sampled_logits(const float* __restrict__ h, const float* __restrict__ W,
                                                         const float* __restrict__ bias, int32_t* __restrict__ neg,
                                                         uint64_t seed, uint64_t counter, uint64_t A, int B, int S,
                                                         float* __restrict__ Z, int64_t ldz, float* __restrict__ pmax,
@@ -329,12 +330,16 @@ __global__ __launch_bounds__(SF_THR) void k_sampled_logits(const float* __restri
   constexpr int NS = HF / 16;
   constexpr int CH = NS * 192;              // 16-B fragments of one 32-row chunk's planes
   constexpr int ITEMS = 32 * (HF / 8);      // (row, 8-value group) items of one chunk
-  constexpr int IPT = (ITEMS + SF_THR - 1) / SF_THR;  // per thread (1 at HF <= 128, 8 waves)
+  constexpr int SF_THR = sf_thr(HF), SF_NEG = sf_neg(HF);
+  constexpr int IPT = (ITEMS + SF_THR - 1) / SF_THR;  // per thread (1 at HF <= 128, 8 waves; 4 at HF 256)
   constexpr float L2E = 1.4426950408889634f;
+  // HF <= 128: all four h chunks get their own LDS buffer (chunks 1..3 are
+  // staged together behind chunk 0's MFMAs: two barriers instead of four,
+  // 25.5 -> 22.8 us at C2 shapes); HF 256 (48 KB per chunk) keeps the
+  // two-buffer ring with a barrier per chunk
+  constexpr bool STAGE = HF <= 128;
   __shared__ bf16x8 hsA[CH], hsB[CH];
-#if SF_STAGE_ALL
-  __shared__ bf16x8 hsC[CH], hsD[CH];
-#endif
+  __shared__ bf16x8 hsC[STAGE ? CH : 1], hsD[STAGE ? CH : 1];
   __shared__ __attribute__((aligned(16))) float sbias[SF_NEG];
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, hh = lane >> 5, l32 = lane & 31;
   int bx = blockIdx.x, by = blockIdx.y;
@@ -355,9 +360,7 @@ __global__ __launch_bounds__(SF_THR) void k_sampled_logits(const float* __restri
   const int nch = min(SF_ROWS, B - rbase) / 32;   // B % 32 == 0
   // ---- h chunk staging: item i -> (group g, row) with the row fastest
   f4 st[IPT][2];
-#if SF_STAGE_ALL
-  f4 st2[IPT][2], st3[IPT][2];
-#endif
+  f4 st2[IPT][2], st3[IPT][2];   // (STAGE: chunks 2, 3)
   auto load_to = [&](f4 (&dst)[IPT][2], int c) __attribute__((always_inline)) {
 #pragma unroll
     for (int q = 0; q < IPT; ++q) {
@@ -412,10 +415,10 @@ __global__ __launch_bounds__(SF_THR) void k_sampled_logits(const float* __restri
   __builtin_amdgcn_sched_barrier(0);
   store_h(hsA);
   if (nch > 1) load_h(1);
-#if SF_STAGE_ALL
-  if (nch > 2) load_to(st2, 2);
-  if (nch > 3) load_to(st3, 3);
-#endif
+  if constexpr (STAGE) {
+    if (nch > 2) load_to(st2, 2);
+    if (nch > 3) load_to(st3, 3);
+  }
   if (hh == 0) sbias[32 * w + l32] = bl;
   // barrier without a memory fence: only the LDS writes must be complete
   // (the W rows and h chunk 1 stay in flight); same for every barrier below
@@ -498,48 +501,47 @@ __global__ __launch_bounds__(SF_THR) void k_sampled_logits(const float* __restri
       epi(acc_old, c - 1);
     }
   };
-#if SF_STAGE_ALL
-  // chunks 1..3 (loaded before chunk 0's MFMAs) are split into their own LDS
-  // buffers behind those MFMAs, one more barrier, then the remaining MFMAs
-  // run back to back with the epilogues interleaved: 2 barriers, not 4
-  if (nch > 1) {
-    store_from(st, hsB);
-    if (nch > 2) store_from(st2, hsC);
-    if (nch > 3) store_from(st3, hsD);
-    sync_lds();
-    if (nact) {
-      mma(hsB, accB);
-      epi(accA, 0);
-      if (nch > 2) {
-        mma(hsC, accA);
-        epi(accB, 1);
-        if (nch > 3) {
-          mma(hsD, accB);
-          epi(accA, 2);
-          epi(accB, 3);
+  if constexpr (STAGE) {
+    // chunks 1..3 (loaded before chunk 0's MFMAs) are split into their own LDS
+    // buffers behind those MFMAs, one more barrier, then the remaining MFMAs
+    // run back to back with the epilogues interleaved: 2 barriers, not 4
+    if (nch > 1) {
+      store_from(st, hsB);
+      if (nch > 2) store_from(st2, hsC);
+      if (nch > 3) store_from(st3, hsD);
+      sync_lds();
+      if (nact) {
+        mma(hsB, accB);
+        epi(accA, 0);
+        if (nch > 2) {
+          mma(hsC, accA);
+          epi(accB, 1);
+          if (nch > 3) {
+            mma(hsD, accB);
+            epi(accA, 2);
+            epi(accB, 3);
+          } else {
+            epi(accA, 2);
+          }
         } else {
-          epi(accA, 2);
+          epi(accB, 1);
         }
-      } else {
-        epi(accB, 1);
       }
+    } else if (nact) {
+      epi(accA, 0);
     }
-  } else if (nact) {
-    epi(accA, 0);
+  } else {
+    if (nch > 1) step(1, hsB, accB, accA);
+    if (nch > 2) step(2, hsA, accA, accB);
+    if (nch > 3) step(3, hsB, accB, accA);
+    if (nact) {
+      if (nch == 1) epi(accA, 0);
+      if (nch == 2) epi(accB, 1);
+      if (nch == 3) epi(accA, 2);
+      if (nch == 4) epi(accB, 3);
+    }
   }
 }
-#else
-  if (nch > 1) step(1, hsB, accB, accA);
-  if (nch > 2) step(2, hsA, accA, accB);
-  if (nch > 3) step(3, hsB, accB, accA);
-  if (nact) {
-    if (nch == 1) epi(accA, 0);
-    if (nch == 2) epi(accB, 1);
-    if (nch == 3) epi(accA, 2);
-    if (nch == 4) epi(accB, 3);
-  }
-}
-#endif
 
 // The fused forward (k_sampled_logits): Z row-major (B × ldz, ldz >= S).
 extern "C" int rg_sampled_logits(const float* h, const float* W, const float* bias, int32_t* neg, int draw,
@@ -551,13 +553,14 @@ extern "C" int rg_sampled_logits(const float* h, const float* W, const float* bi
   if (ldz < S || (ldz & 3)) return RG_ERR_ARG;
   if (draw && (A <= 0 || A > INT32_MAX)) return RG_ERR_ARG;
   if (terms != 6 && terms != 9) return RG_ERR_ARG;
-  const dim3 grid((unsigned)((S + SF_NEG - 1) / SF_NEG), (unsigned)((B + SF_ROWS - 1) / SF_ROWS));
+  const int neg_wg = sf_neg(HF);
+  const dim3 grid((unsigned)((S + neg_wg - 1) / neg_wg), (unsigned)((B + SF_ROWS - 1) / SF_ROWS));
 #define SFG(HFV, NTV)                                                                                            \
   if (draw)                                                                                                        \
-    RG_TLAUNCH((k_sampled_logits<HFV, NTV, true>), grid, dim3(SF_THR), 0, stream, h, W, bias, neg, seed,             \
+    RG_TLAUNCH((k_sampled_logits<HFV, NTV, true>), grid, dim3(sf_thr(HFV)), 0, stream, h, W, bias, neg, seed,             \
                        counter, (uint64_t)A, B, S, Z, ldz, pmax, psum, Wg, bg);                                   \
   else                                                                                                             \
-    RG_TLAUNCH((k_sampled_logits<HFV, NTV, false>), grid, dim3(SF_THR), 0, stream, h, W, bias, neg, seed,            \
+    RG_TLAUNCH((k_sampled_logits<HFV, NTV, false>), grid, dim3(sf_thr(HFV)), 0, stream, h, W, bias, neg, seed,            \
                        counter, (uint64_t)(A > 0 ? A : 0), B, S, Z, ldz, pmax, psum, Wg, bg)
 #define SFT(HFV)  \
   if (terms == 9) \
@@ -568,6 +571,7 @@ extern "C" int rg_sampled_logits(const float* h, const float* W, const float* bi
     case 32: SFT(32); break;
     case 64: SFT(64); break;
     case 128: SFT(128); break;
+    case 256: SFT(256); break;
     default: return RG_ERR_SHAPE;
   }
 #undef SFT

@@ -1007,10 +1007,10 @@ class _SampledWS:
         self.B, self.S = B, S
         self.terms = terms  # 0: native fp32 forward, 6 / 9: split-bf16 (rg_sampled_logits / rg_sampled_fwd_x)
         self.nT = call("rg_sampled_nparts", B, S, terms)  # (max, Σexp) partials per row
-        # logits layout: the fused split forward (HF <= 128, csrc/sampled.hip
-        # k_sampled_logits) stores Z row-major (B × ldz, negatives contiguous);
-        # the other forwards store Zᵀ (S × ldz, rows contiguous)
-        self.zrow = terms != 0 and HF <= 128
+        # logits layout: the fused one-launch split forward (csrc/sampled.hip
+        # k_sampled_logits, HF <= 256) stores Z row-major (B × ldz, negatives
+        # contiguous); the native fp32 forward stores Zᵀ (S × ldz, rows contiguous)
+        self.zrow = terms != 0 and HF <= 256
         self.ldz = _round_up(S, 4) if self.zrow else _round_up(B, 4)
         self.ZT = z(B, self.ldz) if self.zrow else z(S, self.ldz)
         # (stride over batch rows, stride over negatives) of the logits

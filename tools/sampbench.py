@@ -63,7 +63,7 @@ for HF in a.HF:
         us = e0.elapsed_time(e1) / a.iters * 1e3
         print(f"HF {HF} {prec:6s} {us:8.2f} us  {fl / us / 1e6:7.1f} TFLOP/s  Z write {B * S * 4 / us / 1e3:6.0f} GB/s",
               flush=True)
-        if a.fused and prec != "f32" and HF <= 128:
+        if a.fused and prec != "f32" and HF <= 256:
             ldzr = (S + 3) // 4 * 4
             Zr = torch.empty(B, ldzr, device=dev)
             terms = 9 if prec == "f32x9" else 6
