@@ -114,6 +114,17 @@ __device__ __forceinline__ f16v mfma32bf(bf16x8 a, bf16x8 b, f16v c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
 }
 
+// raw buffer resource over `base` (SGPRs; num_records = 2^31 - 1 bytes) and
+// a 16-byte buffer -> LDS DMA: lane reads base + voff + soff, LDS address =
+// wave-uniform base + 16·lane
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rg_rsrc(const void* base) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, 0x7fffffff, 0x00020000);
+}
+__device__ __forceinline__ void rg_blds16(__amdgpu_buffer_rsrc_t r, void* lds_wave_base, int voff, int soff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds_wave_base, 16, voff,
+                                           soff, 0, 0);
+}
+
 // 8 consecutive fp32 values -> their three bf16 planes
 __device__ __forceinline__ void split3x8(const f4& lo, const f4& hi, bf16x8& p0, bf16x8& p1, bf16x8& p2) {
 #pragma unroll

@@ -37,11 +37,15 @@ struct GruBwdDirs {
   float* dGh[2];
 };
 
+// hk (optional): the final h also leaves as the bf16 K-planes of the whole
+// (B × ldh) hidden matrix (csrc/head_flash.hip layout: [row/32][k slice][plane]
+// [lane], 16-B entries of 8 consecutive units) for the sampled head's logits
+// (csrc/sampled.hip k_sampled_logits, HKP) — split here, once, where h is made.
 template <int H>
 __global__ __launch_bounds__(H * 4) void k_gru_fwd(GruDirs dirs, const int32_t* __restrict__ perm,
                                                    const int32_t* __restrict__ lsort,
                                                    const int32_t* __restrict__ offs, int B, float* __restrict__ hout,
-                                                   int ldh, int hoff0, int64_t plane) {
+                                                   int ldh, int hoff0, int64_t plane, bf16x8* __restrict__ hk) {
   const int dir = blockIdx.y;
   const float* __restrict__ Gi = dirs.Gi[dir];
   const float* __restrict__ Whh = dirs.Whh[dir];
@@ -133,6 +137,24 @@ __global__ __launch_bounds__(H * 4) void k_gru_fwd(GruDirs dirs, const int32_t* 
     cur ^= 1;
   }
   if (valid) *reinterpret_cast<f4*>(hout + (int64_t)perm[row] * ldh + hoff + u0) = h;
+  if (hk != nullptr) {   // hbuf[cur] holds the 16 rows' final h (the loop ended on a barrier)
+    constexpr int G = H / 8;   // 8-unit groups of this direction
+    const int nsp = ldh / 16;  // k slices of the whole row
+    for (int i = threadIdx.x; i < 16 * G; i += H * 4) {
+      const int rr = i / G, g = i % G;
+      if (r0 + rr >= B) continue;
+      const f4 lo = *reinterpret_cast<const f4*>(&hbuf[cur][rr][8 * g]);
+      const f4 hi = *reinterpret_cast<const f4*>(&hbuf[cur][rr][8 * g + 4]);
+      bf16x8 p0, p1, p2;
+      split3x8(lo, hi, p0, p1, p2);
+      const int x = perm[r0 + rr];
+      const int gg = hoff / 8 + g;
+      const int64_t e = ((int64_t)(x >> 5) * nsp + (gg >> 1)) * 192 + (gg & 1) * 32 + (x & 31);
+      hk[e] = p0;
+      hk[e + 64] = p1;
+      hk[e + 128] = p2;
+    }
+  }
 }
 
 // BPTT.  dh_final (original row order) -> dGi = [da_r, da_z, da_n],
@@ -228,9 +250,9 @@ __global__ __launch_bounds__(H * 4) void k_gru_bwd(GruBwdDirs dirs, int64_t plan
 
 template <int H>
 static void launch_fwd(const GruDirs& d, int ndir, const int32_t* perm, const int32_t* lsort, const int32_t* offs,
-                       int B, float* hout, int ldh, int hoff, int64_t plane, hipStream_t stream) {
+                       int B, float* hout, int ldh, int hoff, int64_t plane, bf16x8* hk, hipStream_t stream) {
   hipLaunchKernelGGL(k_gru_fwd<H>, dim3((B + 15) / 16, ndir), dim3(H * 4), 0, stream, d, perm, lsort, offs, B, hout,
-                     ldh, hoff, plane);
+                     ldh, hoff, plane, hk);
 }
 
 template <int H>
@@ -241,13 +263,17 @@ static void launch_bwd(const GruBwdDirs& d, int ndir, int64_t plane, const int32
 }
 
 static int gru_fwd_dirs(const GruDirs& d, int ndir, const int32_t* perm, const int32_t* lsort, const int32_t* offs,
-                        int B, int H, float* hout, int ldh, int hoff, int64_t plane, hipStream_t stream) {
+                        int B, int H, float* hout, int ldh, int hoff, int64_t plane, hipStream_t stream,
+                        void* h_planes = nullptr) {
   if (B <= 0 || ndir < 1 || ndir > 2) return RG_ERR_ARG;
+  if (h_planes && (!(ldh == 32 || ldh == 64 || ldh == 128 || ldh == 256) || (hoff % 8) || hoff + ndir * H > ldh))
+    return RG_ERR_ARG;
+  bf16x8* hk = (bf16x8*)h_planes;
   switch (H) {
-    case 16: launch_fwd<16>(d, ndir, perm, lsort, offs, B, hout, ldh, hoff, plane, stream); break;
-    case 32: launch_fwd<32>(d, ndir, perm, lsort, offs, B, hout, ldh, hoff, plane, stream); break;
-    case 64: launch_fwd<64>(d, ndir, perm, lsort, offs, B, hout, ldh, hoff, plane, stream); break;
-    case 128: launch_fwd<128>(d, ndir, perm, lsort, offs, B, hout, ldh, hoff, plane, stream); break;
+    case 16: launch_fwd<16>(d, ndir, perm, lsort, offs, B, hout, ldh, hoff, plane, hk, stream); break;
+    case 32: launch_fwd<32>(d, ndir, perm, lsort, offs, B, hout, ldh, hoff, plane, hk, stream); break;
+    case 64: launch_fwd<64>(d, ndir, perm, lsort, offs, B, hout, ldh, hoff, plane, hk, stream); break;
+    case 128: launch_fwd<128>(d, ndir, perm, lsort, offs, B, hout, ldh, hoff, plane, hk, stream); break;
     default: return RG_ERR_SHAPE;
   }
   RG_LAUNCH_CHECK();
@@ -299,6 +325,25 @@ extern "C" int rg_gru_fwd_dirs(const float* const* Gi, const float* const* Whh, 
     d.saved[i] = saved[j];
   }
   return gru_fwd_dirs(d, ndir, perm, lsort, offs, B, H, hout, ldh, hoff, plane, stream);
+}
+
+// rg_gru_fwd_dirs that also writes the final h as bf16 K-planes (rows padded
+// to 32: rg_head_plane_bytes(B, ldh) bytes; ldh in {32, 64, 128, 256}).
+// Rows past B in the last 32-row block are left as they are.
+extern "C" int rg_gru_fwd_dirs_planes(const float* const* Gi, const float* const* Whh, const float* const* bhh,
+                                      float* const* saved, int ndir, const int32_t* perm, const int32_t* lsort,
+                                      const int32_t* offs, int B, int H, float* hout, int ldh, int hoff,
+                                      int64_t plane, void* h_planes, hipStream_t stream) {
+  if (!Gi || !Whh || !bhh || !saved || !h_planes || ndir < 1 || ndir > 2) return RG_ERR_ARG;
+  GruDirs d{};
+  for (int i = 0; i < 2; ++i) {
+    const int j = i < ndir ? i : 0;
+    d.Gi[i] = Gi[j];
+    d.Whh[i] = Whh[j];
+    d.bhh[i] = bhh[j];
+    d.saved[i] = saved[j];
+  }
+  return gru_fwd_dirs(d, ndir, perm, lsort, offs, B, H, hout, ldh, hoff, plane, stream, h_planes);
 }
 
 extern "C" int rg_gru_bwd_dirs(float* const* saved, const float* const* Whh, float* const* dGi, float* const* dGh,

@@ -320,13 +320,17 @@ constexpr int sf_neg(int HF) { return 32 * sf_nw(HF); }   // negatives per workg
 constexpr int sf_thr(int HF) { return 64 * sf_nw(HF); }   // threads per workgroup
 constexpr int SF_ROWS = 128;  // rows per workgroup (4 chunks of 32)
 
-template <int HF, int NT, bool DRAW>
+// HKP (HF <= 128): h arrives as its bf16 K-planes (hk, written by the GRU
+// forward that produced h, rg_gru_fwd_dirs_planes) and each 32-row chunk
+// moves global -> LDS by 16-B LDS-DMA: no fp32 h loads, no split, no LDS
+// stores in this kernel.
+template <int HF, int NT, bool DRAW, bool HKP>
 __global__ __launch_bounds__(sf_thr(HF)) void k_sampled_logits(const float* __restrict__ h, const float* __restrict__ W,
                                                         const float* __restrict__ bias, int32_t* __restrict__ neg,
                                                         uint64_t seed, uint64_t counter, uint64_t A, int B, int S,
                                                         float* __restrict__ Z, int64_t ldz, float* __restrict__ pmax,
                                                         float* __restrict__ psum, float* __restrict__ Wg,
-                                                        float* __restrict__ bg) {
+                                                        float* __restrict__ bg, const bf16x8* __restrict__ hk) {
   constexpr int NS = HF / 16;
   constexpr int CH = NS * 192;              // 16-B fragments of one 32-row chunk's planes
   constexpr int ITEMS = 32 * (HF / 8);      // (row, 8-value group) items of one chunk
@@ -389,6 +393,15 @@ __global__ __launch_bounds__(sf_thr(HF)) void k_sampled_logits(const float* __re
     }
   };
   auto store_h = [&](bf16x8* hs) __attribute__((always_inline)) { store_from(st, hs); };
+  // chunk c's K-planes (CH contiguous 16-B entries) -> LDS by DMA, sliced over the waves
+  auto dma_chunk = [&](bf16x8* hs, int c) __attribute__((always_inline)) {
+    const __amdgpu_buffer_rsrc_t r = rg_rsrc(hk + (int64_t)((rbase >> 5) + c) * CH);
+#pragma unroll
+    for (int q = 0; q < (CH + SF_THR - 1) / SF_THR; ++q) {
+      const int e0 = SF_THR * q + 64 * __builtin_amdgcn_readfirstlane(w);   // wave-uniform
+      if (e0 < CH) rg_blds16(r, hs + e0, 16 * lane, 16 * e0);
+    }
+  };
   // ---- this wave's negatives: draw, bias, fp32 rows in A-fragment layout.
   // Vector-memory issue order: bias, h chunk 0, the W rows, h chunk 1;
   // branch-free (a wave without negatives gathers row 0 and stores nothing).
@@ -402,7 +415,11 @@ __global__ __launch_bounds__(sf_thr(HF)) void k_sampled_logits(const float* __re
     id = (A > 0 && (uint64_t)(int64_t)id >= A) ? 0 : id;   // guard the gather (callers validate ids)
   }
   const float bl = bias[id];
-  load_h(0);
+  if constexpr (HKP) {
+    dma_chunk(hsA, 0);
+  } else {
+    load_h(0);
+  }
   f4 wr[NS][2];
   {
     const float* src = W + (int64_t)id * HF + 8 * hh;
@@ -413,13 +430,6 @@ __global__ __launch_bounds__(sf_thr(HF)) void k_sampled_logits(const float* __re
     }
   }
   __builtin_amdgcn_sched_barrier(0);
-  store_h(hsA);
-  if (nch > 1) load_h(1);
-  if constexpr (STAGE) {
-    if (nch > 2) load_to(st2, 2);
-    if (nch > 3) load_to(st3, 3);
-  }
-  if (hh == 0) sbias[32 * w + l32] = bl;
   // barrier without a memory fence: only the LDS writes must be complete
   // (the W rows and h chunk 1 stay in flight); same for every barrier below
   auto sync_lds = [&]() __attribute__((always_inline)) {
@@ -427,7 +437,22 @@ __global__ __launch_bounds__(sf_thr(HF)) void k_sampled_logits(const float* __re
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
   };
-  sync_lds();
+  if constexpr (HKP) {
+    if (hh == 0) sbias[32 * w + l32] = bl;
+    __syncthreads();   // chunk 0's DMA and the W rows landed (vmcnt(0)), sbias visible
+    if (nch > 1) dma_chunk(hsB, 1);
+    if (nch > 2) dma_chunk(hsC, 2);
+    if (nch > 3) dma_chunk(hsD, 3);
+  } else {
+    store_h(hsA);
+    if (nch > 1) load_h(1);
+    if constexpr (STAGE) {
+      if (nch > 2) load_to(st2, 2);
+      if (nch > 3) load_to(st3, 3);
+    }
+    if (hh == 0) sbias[32 * w + l32] = bl;
+    sync_lds();
+  }
   float* __restrict__ pm = pmax + (int64_t)(s0 / 32) * B + rbase + l32;
   float* __restrict__ ps = psum + (int64_t)(s0 / 32) * B + rbase + l32;
   bf16x8 a0[NS], a1[NS], a2[NS];
@@ -501,7 +526,31 @@ __global__ __launch_bounds__(sf_thr(HF)) void k_sampled_logits(const float* __re
       epi(acc_old, c - 1);
     }
   };
-  if constexpr (STAGE) {
+  if constexpr (HKP) {
+    // chunks 1..3 were DMA'd behind chunk 0's MFMAs: one full wait + barrier
+    if (nch > 1) {
+      __syncthreads();
+      if (nact) {
+        mma(hsB, accB);
+        epi(accA, 0);
+        if (nch > 2) {
+          mma(hsC, accA);
+          epi(accB, 1);
+          if (nch > 3) {
+            mma(hsD, accB);
+            epi(accA, 2);
+            epi(accB, 3);
+          } else {
+            epi(accA, 2);
+          }
+        } else {
+          epi(accB, 1);
+        }
+      }
+    } else if (nact) {
+      epi(accA, 0);
+    }
+  } else if constexpr (STAGE) {
     // chunks 1..3 (loaded before chunk 0's MFMAs) are split into their own LDS
     // buffers behind those MFMAs, one more barrier, then the remaining MFMAs
     // run back to back with the epilogues interleaved: 2 barriers, not 4
@@ -547,7 +596,7 @@ __global__ __launch_bounds__(sf_thr(HF)) void k_sampled_logits(const float* __re
 extern "C" int rg_sampled_logits(const float* h, const float* W, const float* bias, int32_t* neg, int draw,
                                  uint64_t seed, uint64_t counter, int64_t A, int B, int S, int HF, int terms,
                                  float* Z, int64_t ldz, float* pmax, float* psum, float* Wg, float* bg,
-                                 hipStream_t stream) {
+                                 const void* h_planes, hipStream_t stream) {
   if (B <= 0 || S <= 0 || (B % 32) || (S % 32) || !h || !W || !bias || !neg || !Z || !pmax || !psum || !bg)
     return RG_ERR_ARG;
   if (ldz < S || (ldz & 3)) return RG_ERR_ARG;
@@ -555,18 +604,24 @@ extern "C" int rg_sampled_logits(const float* h, const float* W, const float* bi
   if (terms != 6 && terms != 9) return RG_ERR_ARG;
   const int neg_wg = sf_neg(HF);
   const dim3 grid((unsigned)((S + neg_wg - 1) / neg_wg), (unsigned)((B + SF_ROWS - 1) / SF_ROWS));
-#define SFG(HFV, NTV)                                                                                            \
-  if (draw)                                                                                                        \
-    RG_TLAUNCH((k_sampled_logits<HFV, NTV, true>), grid, dim3(sf_thr(HFV)), 0, stream, h, W, bias, neg, seed,             \
-                       counter, (uint64_t)A, B, S, Z, ldz, pmax, psum, Wg, bg);                                   \
-  else                                                                                                             \
-    RG_TLAUNCH((k_sampled_logits<HFV, NTV, false>), grid, dim3(sf_thr(HFV)), 0, stream, h, W, bias, neg, seed,            \
-                       counter, (uint64_t)(A > 0 ? A : 0), B, S, Z, ldz, pmax, psum, Wg, bg)
-#define SFT(HFV)  \
-  if (terms == 9) \
-    SFG(HFV, 9);  \
-  else            \
-    SFG(HFV, 6);
+  const bf16x8* hk = (const bf16x8*)h_planes;
+#define SFH(HFV, NTV, DRV, HKV)                                                                                    \
+  RG_TLAUNCH((k_sampled_logits<HFV, NTV, DRV, HKV>), grid, dim3(sf_thr(HFV)), 0, stream, h, W, bias, neg, seed,   \
+             counter, (uint64_t)(A > 0 ? A : 0), B, S, Z, ldz, pmax, psum, Wg, bg, hk)
+#define SFG(HFV, NTV)                                 \
+  if (hk && HFV <= 128) {                             \
+    if (draw) SFH(HFV, NTV, true, (HFV <= 128));      \
+    else SFH(HFV, NTV, false, (HFV <= 128));          \
+  } else {                                            \
+    if (draw) SFH(HFV, NTV, true, false);             \
+    else SFH(HFV, NTV, false, false);                 \
+  }
+#define SFT(HFV)    \
+  if (terms == 9) { \
+    SFG(HFV, 9);    \
+  } else {          \
+    SFG(HFV, 6);    \
+  }
   switch (HF) {
     case 32: SFT(32); break;
     case 64: SFT(64); break;
@@ -576,6 +631,7 @@ extern "C" int rg_sampled_logits(const float* h, const float* W, const float* bi
   }
 #undef SFT
 #undef SFG
+#undef SFH
   RG_LAUNCH_CHECK();
   return RG_OK;
 }

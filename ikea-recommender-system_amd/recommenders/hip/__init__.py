@@ -94,6 +94,7 @@ SIGNATURES = {
     "rg_mask_scale": [P, P, F, I64, P, P],
     "rg_gru_wide_work_bytes": [I],
     "rg_gru_fwd_dirs": [P, P, P, P, I, P, P, P, I, I, P, I, I, I64, P],
+    "rg_gru_fwd_dirs_planes": [P, P, P, P, I, P, P, P, I, I, P, I, I, I64, P, P],
     "rg_gru_bwd_dirs": [P, P, P, P, I, I64, P, P, P, I, I, P, I, I, P],
     "rg_gru_fwd_wide": [P, P, P, P, P, P, I, I, P, I, I, P, I64, P, P],
     "rg_gru_bwd_wide": [P, I64, P, P, P, P, I, I, P, I, I, P, P, P, P],
@@ -104,7 +105,7 @@ SIGNATURES = {
     "rg_sampled_nparts": [I, I, I],
     "rg_sampled_work_bytes": [I, I, I],
     "rg_sampled_fwd_x": [P, P, P, P, I, U64, U64, I64, I, I, I, I, P, I64, P, P, P, P, P, P],
-    "rg_sampled_logits": [P, P, P, P, I, U64, U64, I64, I, I, I, I, P, I64, P, P, P, P, P],
+    "rg_sampled_logits": [P, P, P, P, I, U64, U64, I64, I, I, I, I, P, I64, P, P, P, P, P, P],
     "rg_sampled_dz_rows": [P, I64, P, I, I, F, P, P, P],
     "rg_sampled_fwd": [P, P, P, P, I, I, I, P, I64, P, P, P, P, P],
     "rg_sampled_lse": [P, P, P, P, I, I64, I, P, P, I, F, P, P, P, P, P, P, P],

@@ -219,6 +219,11 @@ class Trunk:
         self.err = torch.zeros(1, dtype=torch.int32, device=device)  # out-of-range item ids seen
         self.scatter = SegScatter(device)
         self._ws = {}
+        # emit_planes (set for the sampled head's split logits): the training
+        # forward's GRU launch also writes the final h as bf16 K-planes
+        # (rg_gru_fwd_dirs_planes), left in h_planes for the head
+        self.emit_planes = False
+        self.h_planes = None
         # fp16 embedding storage (config C5): the gather reads this copy, Adam
         # keeps the fp32 master and refreshes it in the same sweep
         self.emb16 = torch.empty(self.n_local, E, dtype=torch.float16, device=device) if fp16_embeddings else None
@@ -283,13 +288,22 @@ class Trunk:
                          w.perm.data_ptr(), w.lsort.data_ptr(), w.offs.data_ptr(), B, H, w.h.data_ptr(),
                          self.ndir * H, d * H, w.saved[d].data_ptr() if save else None, w.plane,
                          w.wfrag.data_ptr(), st)
+        self.h_planes = None
         if not self.wide:   # every direction in one launch (grid.y = direction)
             with region("gru_fwd"):
                 nd = range(self.ndir)
-                call("rg_gru_fwd_dirs", host_ptr_array([w.Gi[d] for d in nd]),
-                     host_ptr_array([self.dirs[d][1].p for d in nd]), host_ptr_array([self.dirs[d][3].p for d in nd]),
-                     host_ptr_array([w.saved[d] if save else None for d in nd]), self.ndir, w.perm.data_ptr(),
-                     w.lsort.data_ptr(), w.offs.data_ptr(), B, H, w.h.data_ptr(), self.ndir * H, 0, w.plane, st)
+                args = (host_ptr_array([w.Gi[d] for d in nd]), host_ptr_array([self.dirs[d][1].p for d in nd]),
+                        host_ptr_array([self.dirs[d][3].p for d in nd]),
+                        host_ptr_array([w.saved[d] if save else None for d in nd]), self.ndir, w.perm.data_ptr(),
+                        w.lsort.data_ptr(), w.offs.data_ptr(), B, H, w.h.data_ptr(), self.ndir * H, 0, w.plane)
+                if self.emit_planes and save and self.ndir * H in (32, 64, 128, 256):
+                    if getattr(w, "hk", None) is None:
+                        w.hk = torch.empty(call("rg_head_plane_bytes", B, self.ndir * H), dtype=torch.uint8,
+                                           device=self.device)
+                    call("rg_gru_fwd_dirs_planes", *args, w.hk.data_ptr(), st)
+                    self.h_planes = w.hk
+                else:
+                    call("rg_gru_fwd_dirs", *args, st)
         return w.h
 
     def backward(self, dh, slot="main"):
@@ -907,9 +921,10 @@ class SoftmaxHead:
              w.ZT.data_ptr(), w.ldz, w.pmax.data_ptr(), w.psum.data_ptr(), w.parg.data_ptr(), 1, stream_ptr())
         return w, w.ZT[:, :B].t()
 
-    def forward_loss(self, h, tgt, slot="main"):
+    def forward_loss(self, h, tgt, slot="main", h_planes=None):
         """CE(mean) of Z = h·Wᵀ + b against tgt; keeps Zᵀ / lse for backward.
-        Returns the device loss tensor (1,) and the workspace."""
+        Returns the device loss tensor (1,) and the workspace.  (h_planes:
+        used by the sampled head only.)"""
         B = h.shape[0]
         st = stream_ptr()
         terms = self.flash_terms(B)
@@ -1081,7 +1096,9 @@ class SampledSoftmaxHead(SoftmaxHead):
             self._sws[slot] = w
         return w
 
-    def forward_loss(self, h, tgt, slot="main"):
+    def forward_loss(self, h, tgt, slot="main", h_planes=None):
+        """h_planes: h's bf16 K-planes from the GRU forward (Trunk.emit_planes),
+        consumed by the one-launch split logits at HF <= 128."""
         B = h.shape[0]
         w = self.sws(slot, B)
         st = stream_ptr()
@@ -1091,9 +1108,10 @@ class SampledSoftmaxHead(SoftmaxHead):
         # one-launch kernel the region is kernel-exact
         with region("sampled_fwd", exact=bool(split and w.zrow)):
             if split and w.zrow:  # one launch: draw, row gather, operand split, logits, partials
+                hp = h_planes.data_ptr() if h_planes is not None and self.HF <= 128 else None
                 call("rg_sampled_logits", h.data_ptr(), self.W.p.data_ptr(), self.b.p.data_ptr(), w.ids.data_ptr(),
                      1, self.seed, self.draws, self.A, B, self.S, self.HF, w.terms, w.ZT.data_ptr(), w.ldz,
-                     w.pmax.data_ptr(), w.psum.data_ptr(), w.Wg.data_ptr(), w.bg.data_ptr(), st)
+                     w.pmax.data_ptr(), w.psum.data_ptr(), w.Wg.data_ptr(), w.bg.data_ptr(), hp, st)
             elif split:  # draw + gather + operand split fused into one prep launch
                 if w.work is None:
                     w.work = torch.empty(call("rg_sampled_work_bytes", B, self.S, self.HF), dtype=torch.uint8,

@@ -47,7 +47,8 @@ def supervised_step(net: SupervisedNet, clock, s, a, true_len):
         h_in = net.apply_mask(h, mask, hd)
     else:
         h_in = h
-    loss, _ = head.forward_loss(h_in, a, slot="main")
+    # the GRU forward's bf16 K-planes of h (sampled head) unless dropout changed h
+    loss, _ = head.forward_loss(h_in, a, slot="main", h_planes=net.trunk.h_planes if mask is None else None)
     adam6 = clock.next_args()
     net.trunk_tag = getattr(net, "trunk_tag", 0) + 1
     dh = net.dh_buffer(B)

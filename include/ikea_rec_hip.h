@@ -97,6 +97,12 @@ int rg_gru_bwd(const float* saved, int64_t plane, const float* Whh, const int32_
 int rg_gru_fwd_dirs(const float* const* Gi, const float* const* Whh, const float* const* bhh, float* const* saved,
                     int ndir, const int32_t* perm, const int32_t* lsort, const int32_t* offs, int B, int H,
                     float* hout, int ldh, int hoff, int64_t plane, rg_stream_t stream);
+/* the same, also writing the final h as bf16 K-planes of the (B × ldh) matrix (rg_head_plane_bytes(B, ldh)
+ * bytes, ldh in {32, 64, 128, 256}) for rg_sampled_logits' h_planes: the split happens once, where h is made. */
+int rg_gru_fwd_dirs_planes(const float* const* Gi, const float* const* Whh, const float* const* bhh,
+                           float* const* saved, int ndir, const int32_t* perm, const int32_t* lsort,
+                           const int32_t* offs, int B, int H, float* hout, int ldh, int hoff, int64_t plane,
+                           void* h_planes, rg_stream_t stream);
 int rg_gru_bwd_dirs(float* const* saved, const float* const* Whh, float* const* dGi, float* const* dGh, int ndir,
                     int64_t plane, const int32_t* perm, const int32_t* lsort, const int32_t* offs, int B, int H,
                     const float* dhout, int lddh, int dhoff, rg_stream_t stream);
@@ -383,12 +389,14 @@ int64_t rg_sampled_work_bytes(int B, int S, int HF);
 int rg_sampled_fwd_x(const float* h, const float* W, const float* bias, int32_t* neg, int draw, uint64_t seed,
                      uint64_t counter, int64_t A, int B, int S, int HF, int terms, float* ZT, int64_t ldz,
                      float* pmax, float* psum, float* Wg, float* bg, void* work, rg_stream_t stream);
-/* The split-bf16 sampled forward in ONE launch for HF in {32, 64, 128} (draw, the negatives' row
+/* The split-bf16 sampled forward in ONE launch for HF in {32, 64, 128, 256} (draw, the negatives' row
  * gather, both operands' bf16 split, MFMAs, logits, partials): same semantics as rg_sampled_fwd_x
- * but Z is ROW-major, Z[b·ldz + s] (ldz >= S, ldz % 4 == 0).  Wg optional, bg required. */
+ * but Z is ROW-major, Z[b·ldz + s] (ldz >= S, ldz % 4 == 0).  Wg optional, bg required.
+ * h_planes (optional, HF <= 128): h's bf16 K-planes (rg_gru_fwd_dirs_planes / rg_head_planes), moved
+ * to LDS by DMA instead of splitting h in the kernel. */
 int rg_sampled_logits(const float* h, const float* W, const float* bias, int32_t* neg, int draw, uint64_t seed,
                       uint64_t counter, int64_t A, int B, int S, int HF, int terms, float* Z, int64_t ldz,
-                      float* pmax, float* psum, float* Wg, float* bg, rg_stream_t stream);
+                      float* pmax, float* psum, float* Wg, float* bg, const void* h_planes, rg_stream_t stream);
 /* in place dZ = exp(Z − lse)·g on the row-major Z of rg_sampled_logits; dbg[s] = Σ_b dZ[b][s]
  * through ceil(B/128) × S slabs (summed in order: deterministic) */
 int rg_sampled_dz_rows(float* Z, int64_t ldz, const float* lse, int B, int S, float gscale, float* slabs, float* dbg,

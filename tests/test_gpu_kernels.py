@@ -409,3 +409,43 @@ def test_scatter_rows_deterministic(E, n_rows, n, n_max):
     touched = torch.zeros(n_rows, dtype=torch.bool)
     touched[use[ok]] = True
     assert torch.equal(tags == 9, touched)
+
+
+@pytest.mark.parametrize("H,ndir,B,L", [(128, 1, 100, 9), (64, 2, 70, 6), (32, 1, 33, 5), (16, 2, 64, 4)])
+def test_gru_forward_emits_h_planes(H, ndir, B, L):
+    """rg_gru_fwd_dirs_planes: the same final h as rg_gru_fwd_dirs, and its
+    bf16 K-planes (the sampled head's operand) bitwise equal to
+    rg_head_planes of that h (ragged rows, both directions of a Bidir layer)."""
+    g = torch.Generator().manual_seed(H + ndir)
+    lens = torch.randint(1, L + 1, (B,), generator=g)
+    perm, ls, offs = pack(lens, L)
+    T = int(lens.sum())
+    k = 1 / H ** 0.5
+    Gi = [(torch.randn(T, 3 * H, generator=g) * 0.5).to(dev) for _ in range(ndir)]
+    Whh = [((torch.rand(3 * H, H, generator=g) * 2 - 1) * k).to(dev) for _ in range(ndir)]
+    bhh = [((torch.rand(3 * H, generator=g) * 2 - 1) * k).to(dev) for _ in range(ndir)]
+    HF = ndir * H
+    outs = []
+    for planes in (False, True):
+        hout = torch.zeros(B, HF, device=dev)
+        saved = [torch.zeros(5, T, H, device=dev) for _ in range(ndir)]
+        args = (C().host_ptr_array(Gi), C().host_ptr_array(Whh), C().host_ptr_array(bhh), C().host_ptr_array(saved),
+                ndir, perm.data_ptr(), ls.data_ptr(), offs.data_ptr(), B, H, hout.data_ptr(), HF, 0, T * H)
+        hk = torch.zeros(C().call("rg_head_plane_bytes", B, HF), dtype=torch.uint8, device=dev)
+        if planes:
+            C().call("rg_gru_fwd_dirs_planes", *args, hk.data_ptr(), st())
+        else:
+            C().call("rg_gru_fwd_dirs", *args, st())
+        outs.append((hout, hk))
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0][0], outs[1][0])
+    ref = torch.zeros_like(outs[1][1])
+    C().call("rg_head_planes", outs[1][0].data_ptr(), B, HF, ref.data_ptr(), None, None, None, st())
+    torch.cuda.synchronize()
+    # rows past B inside the last 32-row block are not written by the GRU: compare the written rows
+    n = B // 32 * 32 * HF * 6
+    assert torch.equal(outs[1][1][:n], ref[:n])
+    if B % 32:
+        blk = outs[1][1][n:].view(HF // 16, 3, 2, 32, 16)[..., :B % 32, :]
+        rblk = ref[n:].view(HF // 16, 3, 2, 32, 16)[..., :B % 32, :]
+        assert torch.equal(blk, rblk)

@@ -31,8 +31,9 @@ def run_head(B, S, A, HF, seed=0, collide=False, precision="f32"):
     tgt = torch.randint(0, A, (B,), generator=g)
     if collide:  # some targets equal negatives (and duplicated negatives)
         tgt[: min(B, S) // 2] = neg[: min(B, S) // 2]
-    fused = precision.endswith("-fused")   # rg_sampled_logits: one launch, row-major Z
-    precision = precision.replace("-fused", "")
+    planes = precision.endswith("-fusedp")   # ... with h as bf16 K-planes (the GRU forward's output)
+    fused = precision.endswith("-fused") or planes   # rg_sampled_logits: one launch, row-major Z
+    precision = precision.replace("-fusedp", "").replace("-fused", "")
     ldz = (S + 3) // 4 * 4 if fused else (B + 3) // 4 * 4
     nT = call("rg_sampled_nparts", B, S, {"f32": 0, "f32x9": 9, "f32x6": 6}[precision])
     dh_, W_, b_, neg_, tgt_ = D(h), D(W), D(bias), D(neg, torch.int32), D(tgt)
@@ -43,9 +44,13 @@ def run_head(B, S, A, HF, seed=0, collide=False, precision="f32"):
     bg = torch.empty(S, device="cuda")
     st = stream_ptr()
     if fused:
+        hk = None
+        if planes:
+            hk = torch.empty(call("rg_head_plane_bytes", B, HF), dtype=torch.uint8, device="cuda")
+            call("rg_head_planes", dh_.data_ptr(), B, HF, hk.data_ptr(), None, None, None, st)
         call("rg_sampled_logits", dh_.data_ptr(), W_.data_ptr(), b_.data_ptr(), neg_.data_ptr(), 0, 0, 0, A, B, S,
              HF, {"f32x9": 9, "f32x6": 6}[precision], ZT.data_ptr(), ldz, pm.data_ptr(), ps.data_ptr(), Wg.data_ptr(),
-             bg.data_ptr(), st)
+             bg.data_ptr(), None if hk is None else hk.data_ptr(), st)
     elif precision == "f32":
         call("rg_sampled_fwd", dh_.data_ptr(), W_.data_ptr(), b_.data_ptr(), neg_.data_ptr(), B, S, HF,
              ZT.data_ptr(), ldz, pm.data_ptr(), ps.data_ptr(), Wg.data_ptr(), bg.data_ptr(), st)
@@ -91,7 +96,7 @@ def test_sample_uniform_matches_oracle_bit_exact():
 @pytest.mark.parametrize("B,S,A,HF,collide", [(256, 256, 5000, 128, False), (37, 200, 300, 64, True),
                                               (300, 130, 100, 256, True), (128, 2048, 100000, 32, False),
                                               (2240, 2048, 50000, 256, True), (1120, 64, 700, 64, True)])
-@pytest.mark.parametrize("precision", ["f32", "f32x9", "f32x6", "f32x9-fused", "f32x6-fused"])
+@pytest.mark.parametrize("precision", ["f32", "f32x9", "f32x6", "f32x9-fused", "f32x6-fused", "f32x6-fusedp"])
 def test_sampled_kernels_match_torch_fp32(B, S, A, HF, collide, precision):
     if precision != "f32" and (B % 32 or S % 32):
         pytest.skip("split-bf16 path needs B, S multiples of 32")

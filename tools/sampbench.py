@@ -20,6 +20,7 @@ ap.add_argument("--iters", type=int, default=50)
 ap.add_argument("--prec", nargs="+", default=["f32", "f32x9", "f32x6"])
 ap.add_argument("--fused", action="store_true", help="also time the one-launch rg_sampled_logits (HF <= 128)")
 ap.add_argument("--hot", action="store_true", help="fused: the same draw every launch (W rows cache-resident)")
+ap.add_argument("--planes", action="store_true", help="fused: h as bf16 K-planes (as the GRU forward leaves them)")
 a = ap.parse_args()
 dev = "cuda"
 for HF in a.HF:
@@ -67,12 +68,16 @@ for HF in a.HF:
             ldzr = (S + 3) // 4 * 4
             Zr = torch.empty(B, ldzr, device=dev)
             terms = 9 if prec == "f32x9" else 6
+            hk = None
+            if a.planes and HF <= 128:
+                hk = torch.empty(call("rg_head_plane_bytes", B, HF), dtype=torch.uint8, device=dev)
+                call("rg_head_planes", h.data_ptr(), B, HF, hk.data_ptr(), None, None, None, st)
 
             def fz():
                 it[0] += 0 if a.hot else 1
                 call("rg_sampled_logits", h.data_ptr(), W.data_ptr(), bias.data_ptr(), neg.data_ptr(), 1, 7, it[0], A,
                      B, S, HF, terms, Zr.data_ptr(), ldzr, pm.data_ptr(), ps.data_ptr(), Wg.data_ptr(), bg.data_ptr(),
-                     st)
+                     None if hk is None else hk.data_ptr(), st)
             for _ in range(3):
                 fz()
             torch.cuda.synchronize()
