@@ -943,11 +943,19 @@ __global__ __launch_bounds__(256) void k_topk_part(const float* __restrict__ cma
 
 // Stage 2: per row the K-th largest of the P·K part values -> the candidate
 // limit lim = tau − (tol_abs + tol_rel·|tau|) (−inf while fewer than K finite
-// maxima exist: every chunk is then a candidate); ncand := 0.
+// maxima exist: every chunk is then a candidate); ncand := 0.  With wnorm
+// (screened chunk maxima, 3 plane products): tol_abs = tol·||h_b||_2·wnorm[0]
+// per row — the screening argmax's bound (rg_flash_argmax_exact).
 __global__ void k_topk_lim(const float* __restrict__ part, int P, int K, int B, float tol_abs, float tol_rel,
-                           float* __restrict__ lim, int32_t* __restrict__ ncand) {
+                           float* __restrict__ lim, int32_t* __restrict__ ncand, const float* __restrict__ h, int HF,
+                           const float* __restrict__ wnorm) {
   const int row = blockIdx.x * blockDim.x + threadIdx.x;
   if (row >= B) return;
+  if (wnorm) {
+    float hn = 0.f;
+    for (int k = 0; k < HF; ++k) hn = fmaf(h[(int64_t)row * HF + k], h[(int64_t)row * HF + k], hn);
+    tol_abs = tol_abs * sqrtf(hn) * wnorm[0];
+  }
   float t[TK_MAX];
 #pragma unroll
   for (int i = 0; i < TK_MAX; ++i) t[i] = NEG_INF;
@@ -1343,9 +1351,9 @@ extern "C" int64_t rg_flash_topk_work_bytes(int B, int A, int K) {
   return ((int64_t)topk_parts(B, (A + 31) / 32) * K * B + B) * 4;
 }
 
-extern "C" int rg_flash_topk(const float* cmax, int B, int A, int K, float tol_abs, float tol_rel, const float* h,
-                             const float* W, const float* bias, int HF, int32_t* cand, int32_t* ncand, int32_t* out_idx,
-                             float* out_val, int32_t* err, void* work, hipStream_t stream) {
+static int flash_topk(const float* cmax, int B, int A, int K, float tol_abs, float tol_rel, const float* wnorm,
+                      const float* h, const float* W, const float* bias, int HF, int32_t* cand, int32_t* ncand,
+                      int32_t* out_idx, float* out_val, int32_t* err, void* work, hipStream_t stream) {
   if (B <= 0 || A <= 0 || K <= 0 || K > TK_MAX || K > A || HF <= 0 || HF > 256 || (HF % 8)) return RG_ERR_ARG;
   if (!cmax || !h || !W || !bias || !cand || !ncand || !out_idx || !err || !work) return RG_ERR_ARG;
   const int nct = (A + 31) / 32;
@@ -1354,13 +1362,33 @@ extern "C" int rg_flash_topk(const float* cmax, int B, int A, int K, float tol_a
   float* lim = part + (int64_t)P * K * B;
   hipLaunchKernelGGL(k_topk_part, dim3((B + 63) / 64, P), dim3(256), 0, stream, cmax, nct, B, K, part);
   hipLaunchKernelGGL(k_topk_lim, dim3((B + 255) / 256), dim3(256), 0, stream, part, P, K, B, tol_abs, tol_rel, lim,
-                     ncand);
+                     ncand, h, HF, wnorm);
   const int ys = max(1, min(256, 2048 / ((B + 255) / 256)));   // ~2048 workgroups over the chunk range
   hipLaunchKernelGGL(k_amax_cand, dim3((B + 255) / 256, ys), dim3(256), 0, stream, cmax, nct, B, lim, cand, ncand);
   hipLaunchKernelGGL(k_flash_topk_eval, dim3(B), dim3(256), 0, stream, h, W, bias, cand, ncand, A, HF, K, out_idx,
                      out_val, err);
   RG_LAUNCH_CHECK();
   return RG_OK;
+}
+
+extern "C" int rg_flash_topk(const float* cmax, int B, int A, int K, float tol_abs, float tol_rel, const float* h,
+                             const float* W, const float* bias, int HF, int32_t* cand, int32_t* ncand, int32_t* out_idx,
+                             float* out_val, int32_t* err, void* work, hipStream_t stream) {
+  return flash_topk(cmax, B, A, K, tol_abs, tol_rel, nullptr, h, W, bias, HF, cand, ncand, out_idx, out_val, err, work,
+                    stream);
+}
+
+// Top-K from SCREENED chunk maxima (rg_flash_amax_screen: 3 plane products):
+// candidates within tol·||h_b||_2·wnorm[0] + 1e-6·|tau| of tau (wnorm from
+// rg_row_norm_max), re-scored exactly as rg_flash_topk; a candidate overflow
+// sets err (the caller re-scores the batch at 6 products).
+extern "C" int rg_flash_topk_screened(const float* cmax, int B, int A, int K, float tol, const float* wnorm,
+                                      const float* h, const float* W, const float* bias, int HF, int32_t* cand,
+                                      int32_t* ncand, int32_t* out_idx, float* out_val, int32_t* err, void* work,
+                                      hipStream_t stream) {
+  if (!wnorm) return RG_ERR_ARG;
+  return flash_topk(cmax, B, A, K, tol, 1e-6f, wnorm, h, W, bias, HF, cand, ncand, out_idx, out_val, err, work,
+                    stream);
 }
 
 extern "C" int rg_flash_lse(const float* pm, const float* pl, int nsplit, const float* h, const float* W,

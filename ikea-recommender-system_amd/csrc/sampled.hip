@@ -439,10 +439,13 @@ __global__ __launch_bounds__(sf_thr(HF)) void k_sampled_logits(const float* __re
   };
   if constexpr (HKP) {
     if (hh == 0) sbias[32 * w + l32] = bl;
-    __syncthreads();   // chunk 0's DMA and the W rows landed (vmcnt(0)), sbias visible
+    // every chunk's DMA is issued up front; one full wait + barrier (the W
+    // rows are needed by chunk 0 anyway), then all MFMAs run barrier-free
+    // (21.7 -> 21.4 us against a second barrier behind chunk 0)
     if (nch > 1) dma_chunk(hsB, 1);
     if (nch > 2) dma_chunk(hsC, 2);
     if (nch > 3) dma_chunk(hsD, 3);
+    __syncthreads();
   } else {
     store_h(hsA);
     if (nch > 1) load_h(1);
@@ -527,9 +530,8 @@ __global__ __launch_bounds__(sf_thr(HF)) void k_sampled_logits(const float* __re
     }
   };
   if constexpr (HKP) {
-    // chunks 1..3 were DMA'd behind chunk 0's MFMAs: one full wait + barrier
+    // chunks 1..3 landed at the first barrier
     if (nch > 1) {
-      __syncthreads();
       if (nact) {
         mma(hsB, accB);
         epi(accA, 0);

@@ -61,6 +61,7 @@ SIGNATURES = {
     "rg_flash_topk_cap": [],
     "rg_flash_topk": [P, I, I, I, F, F, P, P, P, I, P, P, P, P, P, P, P],
     "rg_flash_topk_work_bytes": [I, I, I],
+    "rg_flash_topk_screened": [P, I, I, I, F, P, P, P, P, I, P, P, P, P, P, P, P],
     "rg_flash_lse": [P, P, I, P, P, P, P, I64, I, I64, I, I, P, P, P],
     "rg_flash_rows": [P, P, I64, I, I, P, P],
     "rg_flash_dh": [P, P, P, I, P, F, I, I, P, P],

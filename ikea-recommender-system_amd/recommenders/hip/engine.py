@@ -576,6 +576,7 @@ class _ScoreWS:
         self.parg = z(self.nsplit, R, dt=torch.int32)
         self.cmax = z(nct, R)
         self.lse, self.zt = z(R), z(R)
+        self.wnorm = z(1)
         self.cand = z(R, call("rg_flash_topk_cap"), dt=torch.int32)
         self.ncand = z(R, dt=torch.int32)
         self.tk_work = torch.empty(call("rg_flash_topk_work_bytes", R, A, K), dtype=torch.uint8, device=device)
@@ -790,7 +791,7 @@ class SoftmaxHead:
         return idx, vals
 
     # ---- evaluation scoring without logits (evaluate / update_train_metrics) ----
-    def score_topk(self, h, K, tgt=None, slot="eval"):
+    def score_topk(self, h, K, tgt=None, slot="eval", screen=False):
         """Canonical top-K (value desc, index asc) of the fp32 logits h·Wᵀ + b
         of every row and, with ``tgt``, the per-row CE (lse − z_target),
         without a (B, A) logit buffer (reference eval_protocol.py:123-359
@@ -800,7 +801,11 @@ class SoftmaxHead:
         target logit), rg_flash_topk (every item of the candidate chunks
         re-scored in fp32, fmaf chain + bias).  Returns (idx (B, K) int32,
         vals (B, K), loss_row (B,) or None); a candidate overflow (massive
-        exact ties) sets ``top_err``.  HF must be in {32, 64, 128, 256}, K <= 32."""
+        exact ties) sets ``top_err``.  HF must be in {32, 64, 128, 256}, K <= 32.
+        screen (no tgt): the chunk maxima come from the 3-product screening
+        pass (rg_flash_amax_screen) and the candidates are taken within its
+        error bound (rg_flash_topk_screened) — the same exact lists at half the
+        MFMA work; an overflow there sets ``top_err`` too (re-score without)."""
         B, A, HF = h.shape[0], self.A, self.HF
         if K > min(32, A) or HF not in (32, 64, 128, 256):
             raise ValueError(f"score_topk: K={K} (<= 32 and <= A) and HF={HF} in {{32, 64, 128, 256}}")
@@ -809,6 +814,9 @@ class SoftmaxHead:
         Wp, bp = self.params_ro()
         Wk, bias_pad = self._eval_planes(Wp, bp, st)
         R = w.R
+        screen = screen and tgt is None
+        if screen:
+            call("rg_row_norm_max", Wp.p.data_ptr(), A, HF, w.wnorm.data_ptr(), st)
         for r0 in range(0, B, R):
             n = min(R, B - r0)
             hs = w.h if n < R else h[r0:r0 + R]
@@ -816,6 +824,14 @@ class SoftmaxHead:
                 w.h.zero_()
                 w.h[:n].copy_(h[r0:r0 + n])
             call("rg_head_planes", hs.data_ptr(), R, HF, w.Hk.data_ptr(), None, None, None, st)
+            if screen:
+                call("rg_flash_amax_screen", w.Hk.data_ptr(), Wk.data_ptr(), bias_pad.data_ptr(), R, A, HF, w.nsplit,
+                     w.pbest.data_ptr(), w.parg.data_ptr(), w.cmax.data_ptr(), st)
+                call("rg_flash_topk_screened", w.cmax.data_ptr(), R, A, K, _f32(SCREEN_TOL), w.wnorm.data_ptr(),
+                     hs.data_ptr(), Wp.p.data_ptr(), bp.p.data_ptr(), HF, w.cand.data_ptr(), w.ncand.data_ptr(),
+                     w.idx.data_ptr() + 4 * r0 * K, w.vals.data_ptr() + 4 * r0 * K, self.top_err.data_ptr(),
+                     w.tk_work.data_ptr(), st)
+                continue
             call("rg_flash_score", w.Hk.data_ptr(), Wk.data_ptr(), bias_pad.data_ptr(), R, A, HF, 6, w.nsplit,
                  w.pm.data_ptr(), w.pl.data_ptr(), w.pbest.data_ptr(), w.parg.data_ptr(), w.cmax.data_ptr(), st)
             if tgt is not None:

@@ -55,9 +55,18 @@ def fused_scoring(head, K):
 
 def score_rows(head, h, K, tgt=None):
     """(idx (B, K) int32, vals (B, K), loss_row (B,) or None, err flag tensor):
-    the canonical top-K and per-row CE of h's logits without a (B, A) buffer."""
+    the canonical top-K and per-row CE of h's logits without a (B, A) buffer.
+    Without targets (update_train_metrics) the chunk maxima come from the
+    3-product screening pass; a row whose screening error band holds more
+    candidate chunks than the cap sends the batch back through the exact
+    6-product scoring (one host read of the flag)."""
     B = h.shape[0]
     if fused_scoring(head, K):
+        if tgt is None:
+            idx, vals, _ = head.score_topk(h, K, None, screen=True)
+            if not int(head.top_err.item()):
+                return idx, vals, None, head.top_err
+            head.top_err.zero_()
         idx, vals, loss_row = head.score_topk(h, K, tgt)
         return idx, vals, loss_row, head.top_err
     # stored-logit fallback, row-chunked

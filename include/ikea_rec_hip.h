@@ -197,6 +197,12 @@ int rg_flash_argmax_exact(const float* cmax, int B, int A, const float* h, const
                           float* out_val, rg_stream_t stream);
 int rg_flash_topk_cap(void);
 int64_t rg_flash_topk_work_bytes(int B, int A, int K);
+/* rg_flash_topk on the screened chunk maxima of rg_flash_amax_screen (3 plane products): candidate
+ * chunks within tol·||h_b||_2·wnorm[0] + 1e-6·|tau| of tau (wnorm: rg_row_norm_max), then the same
+ * exact fp32 re-scoring; err |= 1 on a candidate overflow (re-score that batch with rg_flash_score). */
+int rg_flash_topk_screened(const float* cmax, int B, int A, int K, float tol, const float* wnorm, const float* h,
+                           const float* W, const float* bias, int HF, int32_t* cand, int32_t* ncand, int32_t* out_idx,
+                           float* out_val, int32_t* err, void* work, rg_stream_t stream);
 int rg_flash_topk(const float* cmax, int B, int A, int K, float tol_abs, float tol_rel, const float* h, const float* W,
                   const float* bias, int HF, int32_t* cand, int32_t* ncand, int32_t* out_idx, float* out_val,
                   int32_t* err, void* work, rg_stream_t stream);
