@@ -269,9 +269,12 @@ def device_eval(net, ev):
     from recommenders.hip.evalpath import eval_batch
     s, a, ln = ev
     net.eval()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
     r = eval_batch(net, s, ln, a, K=EVAL_K, ks=[EVAL_K], want_loss=True)
     out = {"rows": int(len(a)), "hr20": float(r.hits[0].item()) / len(a), "ndcg20": float(r.ndcg[0].item()) / len(a),
-           "ce": round(float(r.loss.item()), 5)}
+           "ce": round(float(r.loss.item()), 5), "ms": round((time.perf_counter() - t0) * 1e3, 2),
+           "note": "evaluate()'s device path on the held-out batch: no (B, A) logits (DESIGN §4c)"}
     idx = r.idx.cpu().numpy()
     net.train()
     return out, idx
@@ -522,6 +525,15 @@ def main():
     ev, dev_idx = None, None
     if not args.no_eval and not shard and net is not None:
         ev, dev_idx = device_eval(net, held)
+    elif not args.no_eval and not shard and args.config in ("c4", "c5"):
+        # the supervised head of the trained SMORL net (evaluate(head_idx=0));
+        # at C5 (5M items, batch 8192) the held-out evaluation must fit beside
+        # the trainer: the target-side trunk workspaces are dropped first
+        for q in (tr.SMORL_1, tr.SMORL_2):
+            for k in [k for k in q.trunk._ws if k[0] in ("next", "boot")]:
+                del q.trunk._ws[k]
+        torch.cuda.empty_cache()
+        ev, _ = device_eval(tr.SMORL_1, held)
     ms = dt / args.steps * 1e3
     value = B * args.steps * world / dt
     roof = None
