@@ -302,8 +302,11 @@ extern "C" int rg_head_fwd_xp(const void* hplanes, const float* W, const float* 
 // ahead, split once by the workgroup into a two-buffer LDS ring in B-fragment
 // order (lane-linear 16-B writes), one barrier (LDS only, no memory fence) per
 // chunk.  Accumulators alternate, so chunk c's epilogue (+ bias, Z stores,
-// max / Σexp) issues under chunk c+1's MFMAs.  Bytes per CU: 128 KB of W rows
-// + 64 KB of h (fp32) in, 128 KB of Z out.
+// max / Σexp) issues under chunk c+1's MFMAs.  The Z stores go through a
+// per-wave 4 KB LDS tile (XOR-swizzled, conflict-free both ways) so every
+// 16-B store instruction writes eight whole 128-B row segments instead of 32
+// rows × 32 B.  Bytes per CU: 128 KB of W rows + 64 KB of h (fp32) in,
+// 128 KB of Z out.
 //
 // Measured at B 4096, S 2048, HF 128 (tools/sampbench.py, MI355X): 24 µs;
 // a per-wave stamp breakdown puts ~40% in the prologue (the W rows' fragment
@@ -345,6 +348,7 @@ __global__ __launch_bounds__(sf_thr(HF)) void k_sampled_logits(const float* __re
   __shared__ bf16x8 hsA[CH], hsB[CH];
   __shared__ bf16x8 hsC[STAGE ? CH : 1], hsD[STAGE ? CH : 1];
   __shared__ __attribute__((aligned(16))) float sbias[SF_NEG];
+  __shared__ f4 ztile[256 * sf_nw(HF)];
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, hh = lane >> 5, l32 = lane & 31;
   int bx = blockIdx.x, by = blockIdx.y;
   {
@@ -493,7 +497,7 @@ __global__ __launch_bounds__(sf_thr(HF)) void k_sampled_logits(const float* __re
   // s0 + acc32_row(r, hh): four runs of 4 consecutive negatives
   auto epi = [&](f16v& acc, int c) __attribute__((always_inline)) {
     float m = -__builtin_inff();
-    float* zrow = Z + (int64_t)(rbase + 32 * c + l32) * ldz + s0 + 4 * hh;
+    f4* zt = ztile + 256 * w;   // this wave's 32 × 32 tile, 16-B group g of row n at n·8 + (g ^ (n & 7))
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const f4 bq = *reinterpret_cast<const f4*>(&sbias[32 * w + 8 * q + 4 * hh]);
@@ -504,7 +508,15 @@ __global__ __launch_bounds__(sf_thr(HF)) void k_sampled_logits(const float* __re
         acc[4 * q + u] = z[u];
         m = fmaxf(m, z[u]);
       }
-      *reinterpret_cast<f4*>(zrow + 8 * q) = z;
+      zt[8 * l32 + ((2 * q + hh) ^ (l32 & 7))] = z;
+    }
+    // whole 128-B row segments: lane (n8, g) stores row 8q + n8, negatives s0 + 4g .. +3
+    {
+      const int n8 = lane >> 3, g = lane & 7;
+      float* zr = Z + (int64_t)(rbase + 32 * c + n8) * ldz + s0 + 4 * g;
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        *reinterpret_cast<f4*>(zr + (int64_t)(8 * q) * ldz) = zt[8 * (8 * q + n8) + (g ^ n8)];
     }
     m = fmaxf(m, __shfl_xor(m, 32));
     const float m2 = m * L2E;
