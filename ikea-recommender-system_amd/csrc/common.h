@@ -165,3 +165,46 @@ __device__ __forceinline__ f16v mfma_split(const bf16x8& a0, const bf16x8& a1, c
   acc = mfma32bf(a0, b0, acc);
   return acc;
 }
+
+// The same plane products on v_mfma_f32_16x16x32_bf16 (16×16 tile, k 32
+// deep: operand lane l carries row / col l%16, k group l/16 (8 values);
+// accumulator register i of lane l is C[4(l/16) + i][l%16]).  The fused head
+// runs on this shape: in an LDS-fed split-bf16 loop at two waves per SIMD it
+// sustains 0.84 of the bf16 peak against 0.73 for 32x32x16 at equal FLOPs
+// (tools/mfma_shape.hip: the chip holds a higher clock).
+//
+// Operand planes of a matrix X (rows × HF) in that shape, 16-B entries:
+//   K-planes  [x/32][s < HF/32][blk < 2][p < 3][lane]: lane = 16·kg + n holds
+//             X[32(x/32) + 16·blk + n][32s + 8kg + 0..7]        (k over features)
+//   R-planes  [x/32][fb < HF/16][p < 3][lane]: lane = 16·kg + n holds
+//             X[32(x/32) + kperm16(kg, e)][16fb + n], e = 0..7   (k over rows)
+// kperm16: the k order in which an accumulator pair (rows 4kg + i of tile 0,
+// 16 + 4kg + i of tile 1) feeds the next MFMA as its 32-deep operand.
+__device__ __forceinline__ int kperm16(int kg, int e) { return (e & 3) + 4 * kg + 16 * (e >> 2); }
+__device__ __forceinline__ int64_t kplane16(int64_t x, int g8, int HF) {   // entry of (row x, 8-value group g8), plane 0
+  return ((((x >> 5) * (HF / 32) + (g8 >> 2)) * 2 + ((x >> 4) & 1)) * 3) * 64 + 16 * (g8 & 3) + (x & 15);
+}
+__device__ __forceinline__ f4 mfma16bf(bf16x8 a, bf16x8 b, f4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+template <int NT>
+__device__ __forceinline__ f4 mfma16_split(const bf16x8& a0, const bf16x8& a1, const bf16x8& a2, const bf16x8& b0,
+                                          const bf16x8& b1, const bf16x8& b2, f4 acc) {
+  if (NT == 3) {
+    acc = mfma16bf(a0, b1, acc);
+    acc = mfma16bf(a1, b0, acc);
+    return mfma16bf(a0, b0, acc);
+  }
+  if (NT == 9) {
+    acc = mfma16bf(a2, b2, acc);
+    acc = mfma16bf(a1, b2, acc);
+    acc = mfma16bf(a2, b1, acc);
+  }
+  acc = mfma16bf(a0, b2, acc);
+  acc = mfma16bf(a1, b1, acc);
+  acc = mfma16bf(a2, b0, acc);
+  acc = mfma16bf(a0, b1, acc);
+  acc = mfma16bf(a1, b0, acc);
+  acc = mfma16bf(a0, b0, acc);
+  return acc;
+}

@@ -139,7 +139,6 @@ __global__ __launch_bounds__(H * 4) void k_gru_fwd(GruDirs dirs, const int32_t* 
   if (valid) *reinterpret_cast<f4*>(hout + (int64_t)perm[row] * ldh + hoff + u0) = h;
   if (hk != nullptr) {   // hbuf[cur] holds the 16 rows' final h (the loop ended on a barrier)
     constexpr int G = H / 8;   // 8-unit groups of this direction
-    const int nsp = ldh / 16;  // k slices of the whole row
     for (int i = threadIdx.x; i < 16 * G; i += H * 4) {
       const int rr = i / G, g = i % G;
       if (r0 + rr >= B) continue;
@@ -149,7 +148,7 @@ __global__ __launch_bounds__(H * 4) void k_gru_fwd(GruDirs dirs, const int32_t* 
       split3x8(lo, hi, p0, p1, p2);
       const int x = perm[r0 + rr];
       const int gg = hoff / 8 + g;
-      const int64_t e = ((int64_t)(x >> 5) * nsp + (gg >> 1)) * 192 + (gg & 1) * 32 + (x & 31);
+      const int64_t e = kplane16(x, gg, ldh);
       hk[e] = p0;
       hk[e + 64] = p1;
       hk[e + 128] = p2;

@@ -23,20 +23,21 @@
 // ranks between rg_flash_lse and rg_flash_rows; targets outside the shard
 // carry −1 and never match a local item.
 //
-// MFMA 32x32x16 fragment conventions (common.h acc32_row): operand lane l
-// carries row/col l%32 and k group l/32 (8 values); accumulator register r
-// of lane l is C[acc32_row(r, l/32)][l%32].  The k order inside a 16-deep
-// slice is free as long as both operands agree, so a 32-row accumulator
-// block (registers 8s..8s+7 = rows 16s + kperm(l/32, i)) feeds the next
-// MFMA as its k = 32 operand with no data movement.
+// MFMA shape: v_mfma_f32_16x16x32_bf16 (common.h mfma16_split: 0.84 of the
+// bf16 peak in this LDS-fed split loop against 0.73 for 32x32x16).  A wave
+// owns 32 rows (pass 1) / 32 items (pass 2) as two 16-wide tiles; operand
+// lane l carries row / col l%16 and k group l/16 (8 values); accumulator
+// register i of lane l is C[4(l/16) + i][l%16].  The k order inside a
+// 32-deep slice is free as long as both operands agree, so the two 16-row
+// accumulator tiles of a 32-row block (rows 4kg + i and 16 + 4kg + i of lane
+// group kg, common.h kperm16) feed the next MFMA as its 32-deep operand with
+// no data movement.
 //
-// Operand planes (16-B bf16x8 entries, one 32-row block contiguous):
-//   K-planes  [x/32][s < HF/16][p < 3][lane]: lane = hh·32 + x%32 holds
-//             X[x][16s + 8hh + 0..7]                     (k over features)
-//   R-planes  [x/32][t < HF/32][s < 2][p < 3][lane]: lane = hh·32 + n holds
-//             X[32(x/32) + 16s + kperm(hh, i)][32t + n]  (k over rows)
-// Both are lane-linear per wave, so chunks move global → LDS with 16-byte
-// LDS-DMA (global_load_lds_dwordx4) and are read back by ds_read_b128.
+// Operand planes (16-B bf16x8 entries, one 32-row block contiguous; layout
+// in common.h): K-planes (k over features) and R-planes (k over rows, in
+// kperm16 order).  Both are lane-linear per wave, so chunks move global → LDS
+// with 16-byte LDS-DMA (global_load_lds_dwordx4) and are read back by
+// ds_read_b128.
 #include "common.h"
 
 #define NEG_INF (-__builtin_inff())
@@ -47,20 +48,11 @@ constexpr float L2E = 1.4426950408889634f;
 constexpr float LN2 = 0.6931471805599453f;
 // waves per workgroup: 8 (2 per SIMD) up to HF 128; at HF 256 a wave's
 // operand planes (192 VGPRs) and O / dW accumulators (128) need the whole
-// 512-register file, so 4 (1 per SIMD)
-// Waves per workgroup and 32-row (pass 1) / 32-item (pass 2) blocks per
-// wave.  RB = 2 lets every LDS operand fragment feed two MFMA chains (half
-// the LDS read traffic per MFMA) but needs most of the 512-register file, so
-// one wave per SIMD; measured at C2 (HF 128, f32x6) it lost to two one-block
-// waves per SIMD (pass 2: 10.7 vs 9.7 ms; pass 1 spills), so RB = 1 and eight
-// waves up to HF 128.  HF 256: a block's operand planes alone take 192
-// VGPRs, so four waves (one per SIMD).
-constexpr int fl_rb(int, int) { return 1; }
+// 512-register file, so 4 (1 per SIMD).  (Two 32-row blocks per wave at one
+// wave per SIMD, halving the LDS reads per MFMA, lost at C2: pass 2 10.7 vs
+// 9.7 ms, pass 1 spilled.)
 constexpr int fl_nw(int HF, int) { return HF <= 128 ? 8 : 4; }
-constexpr int fl_rows(int HF, int pass) { return 32 * fl_rb(HF, pass) * fl_nw(HF, pass); }
-
-// element i of lane half hh inside a 16-deep k slice -> row offset
-__device__ __forceinline__ int kperm(int hh, int i) { return (i & 3) + 8 * (i >> 2) + 4 * hh; }
+constexpr int fl_rows(int HF, int pass) { return 32 * fl_nw(HF, pass); }
 
 // raw buffer resource over `base` (SGPRs; num_records = 2^31 - 1 bytes)
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_of(const void* base) {
@@ -89,10 +81,11 @@ __device__ __forceinline__ void stage(const bf16x8* __restrict__ src, bf16x8* ds
 }
 
 // ------------------------------------------------------------- planes ----
+// K- / R-planes of the 16x16x32 shape (common.h kplane16 / kperm16)
 template <int HF>
 __global__ __launch_bounds__(256) void k_planes_k(const float* __restrict__ X, int rows, int rows_pad,
                                                   bf16x8* __restrict__ P) {
-  constexpr int G = HF / 8, NS = HF / 16;
+  constexpr int G = HF / 8;
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (i >= (int64_t)rows_pad * G) return;
   const int x = (int)(i / G), g = (int)(i % G);
@@ -103,7 +96,7 @@ __global__ __launch_bounds__(256) void k_planes_k(const float* __restrict__ X, i
   }
   bf16x8 p0, p1, p2;
   split3x8(lo, hi, p0, p1, p2);
-  const int64_t base = ((int64_t)(x >> 5) * NS + (g >> 1)) * 192 + (g & 1) * 32 + (x & 31);
+  const int64_t base = kplane16(x, g, HF);
   P[base] = p0;
   P[base + 64] = p1;
   P[base + 128] = p2;
@@ -112,26 +105,24 @@ __global__ __launch_bounds__(256) void k_planes_k(const float* __restrict__ X, i
 template <int HF>
 __global__ __launch_bounds__(256) void k_planes_r(const float* __restrict__ X, int rows, int rows_pad,
                                                   bf16x8* __restrict__ P) {
-  constexpr int NTL = HF / 32;
+  constexpr int NF = HF / 16;
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (i >= (int64_t)(rows_pad / 32) * NTL * 2 * 64) return;
+  if (i >= (int64_t)(rows_pad / 32) * NF * 64) return;
   const int lane = (int)(i & 63);
-  int64_t q = i >> 6;
-  const int s = (int)(q & 1);
-  q >>= 1;
-  const int t = (int)(q % NTL);
-  const int64_t c = q / NTL;
-  const int hh = lane >> 5, col = 32 * t + (lane & 31);
+  const int64_t q = i >> 6;
+  const int fb = (int)(q % NF);
+  const int64_t c = q / NF;
+  const int kg = lane >> 4, col = 16 * fb + (lane & 15);
   f4 lo, hi;
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
-    const int64_t row = 32 * c + 16 * s + kperm(hh, e);
+    const int64_t row = 32 * c + kperm16(kg, e);
     const float v = row < rows ? X[row * HF + col] : 0.f;
     if (e < 4) lo[e] = v; else hi[e - 4] = v;
   }
   bf16x8 p0, p1, p2;
   split3x8(lo, hi, p0, p1, p2);
-  const int64_t base = ((c * NTL + t) * 2 + s) * 192 + lane;
+  const int64_t base = (c * NF + fb) * 192 + lane;
   P[base] = p0;
   P[base + 64] = p1;
   P[base + 128] = p2;
@@ -159,15 +150,15 @@ __global__ __launch_bounds__(64 * fl_nw(HF, 1)) void k_flash_fwd(
     const float* __restrict__ bias_pad, int B, int A, int nrb, int nsplit, int cps, float* __restrict__ pm,
     float* __restrict__ pl, float* __restrict__ pO, float* __restrict__ pbest, int32_t* __restrict__ parg,
     float* __restrict__ cmax) {
-  constexpr int NW = fl_nw(HF, 1), RB = fl_rb(HF, 1);
+  constexpr int NW = fl_nw(HF, 1);
   constexpr bool DR = HF <= 128;      // double-buffered R-planes
-  constexpr int NS = HF / 16, NTL = HF / 32;
-  constexpr int EK = NS * 192;        // entries per 32-row block, K-planes
-  constexpr int ER = NTL * 2 * 192;   // R-planes (== EK)
+  constexpr int NS = HF / 32, NF = HF / 16;
+  constexpr int EK = NS * 2 * 192;    // entries per 32-row block, K-planes
+  constexpr int ER = NF * 192;        // R-planes (== EK)
   __shared__ bf16x8 sk0[EK], sk1[EK];
   __shared__ bf16x8 sr0[NG ? ER : 1], sr1[(DR && NG) ? ER : 1];
   __shared__ __attribute__((aligned(16))) float sb0[32], sb1[32];
-  const int tid = threadIdx.x, lane = tid & 63, hh = lane >> 5, l32 = lane & 31, lane16 = 16 * lane;
+  const int tid = threadIdx.x, lane = tid & 63, kg = lane >> 4, l16 = lane & 15, lane16 = 16 * lane;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   // XCD-aware order: the nrb row blocks of one item split are dispatched to
   // the same XCD (round-robin dispatch), so its W chunks are fetched once
@@ -176,8 +167,8 @@ __global__ __launch_bounds__(64 * fl_nw(HF, 1)) void k_flash_fwd(
   const int total = nrb * nsplit;
   if ((total & 7) == 0) bid = (bid & 7) * (total >> 3) + (bid >> 3);
   const int split = bid / nrb, rblk = bid % nrb;
-  const int r0 = rblk * fl_rows(HF, 1) + 32 * RB * w;   // this wave's first row
-  const bool active = r0 < B;                        // any of its RB blocks
+  const int r0 = rblk * fl_rows(HF, 1) + 32 * w;   // this wave's first row
+  const bool active = r0 < B;
   const int nct = (A + 31) / 32;
   const int c0 = split * cps;
   const int nch = max(0, min(nct, c0 + cps) - c0);
@@ -194,115 +185,120 @@ __global__ __launch_bounds__(64 * fl_nw(HF, 1)) void k_flash_fwd(
     FL_ISSUE_K(c0, sk0, sb0);
     FL_ISSUE_R(c0, sr0);
   }
-  // this wave's RB × 32 rows of h (B operands of Sᵀ = W_c·hᵀ) for the whole split
-  bf16x8 hk[RB][NS][3];
+  // this wave's 32 rows of h as two 16-row B operands (Sᵀ = W_c·hᵀ), for the whole split
+  bf16x8 hk[NS][2][3];
 #pragma unroll
-  for (int j = 0; j < RB; ++j)
+  for (int s = 0; s < NS; ++s)
 #pragma unroll
-    for (int s = 0; s < NS; ++s)
+    for (int rb = 0; rb < 2; ++rb)
 #pragma unroll
       for (int p = 0; p < 3; ++p)
-        hk[j][s][p] = r0 + 32 * j < B ? Hk[((int64_t)((r0 >> 5) + j) * NS + s) * 192 + p * 64 + lane] : bf16x8{};
-  f16v o[RB][NTL];
-  float m[RB], l[RB], bv[RB];  // bv / bi (ARG): this lane's best logit (natural units) and item
-  int bi[RB];
+        hk[s][rb][p] = active ? Hk[(((int64_t)(r0 >> 5) * NS + s) * 2 + rb) * 192 + p * 64 + lane] : bf16x8{};
+  // Oᵀ tiles (feature block fb, row block rb): lane (kg, n) holds features
+  // 16fb + 4kg + i of row 16rb + n; m / l / best per row block: row 16rb + l16
+  f4 o[NF][2];
+  float m[2], l[2], bv[2];
+  int bi[2];
 #pragma unroll
-  for (int j = 0; j < RB; ++j) {
+  for (int rb = 0; rb < 2; ++rb) {
 #pragma unroll
-    for (int t = 0; t < NTL; ++t) o[j][t] = f16v{};
-    m[j] = NEG_INF;
-    l[j] = 0.f;
-    bv[j] = NEG_INF;
-    bi[j] = INT32_MAX;
+    for (int fb = 0; fb < NF; ++fb) o[fb][rb] = f4{0.f, 0.f, 0.f, 0.f};
+    m[rb] = NEG_INF;
+    l[rb] = 0.f;
+    bv[rb] = NEG_INF;
+    bi[rb] = INT32_MAX;
   }
   __syncthreads();
-  // S-part of chunk c for every block: Sᵀ, (ARG) top-1 / chunk max, online
-  // max / Σexp, P planes
-  auto spart = [&](const bf16x8* sk, const float* sb, int c, bf16x8 (&q0)[RB][2], bf16x8 (&q1)[RB][2],
-                   bf16x8 (&q2)[RB][2]) __attribute__((always_inline)) {
-    f16v sa[RB];
+  // S-part of chunk c: Sᵀ tiles (item block ib, row block rb), (ARG) top-1 /
+  // chunk max, online max / Σexp, P planes (q*[rb]: the B operand of the O-part)
+  auto spart = [&](const bf16x8* sk, const float* sb, int c, bf16x8 (&q0)[2], bf16x8 (&q1)[2], bf16x8 (&q2)[2])
+                   __attribute__((always_inline)) {
+    f4 sa[2][2];
 #pragma unroll
-    for (int j = 0; j < RB; ++j) sa[j] = f16v{};
-    // operand fragments software-pipelined one slice ahead; the sched
-    // barriers stop the scheduler from hoisting every slice's LDS reads
+    for (int ib = 0; ib < 2; ++ib)
+#pragma unroll
+      for (int rb = 0; rb < 2; ++rb) sa[ib][rb] = f4{0.f, 0.f, 0.f, 0.f};
+    // W fragments software-pipelined one (slice, item block) ahead; the sched
+    // barriers stop the scheduler from hoisting every step's LDS reads
     bf16x8 a0 = sk[lane], a1 = sk[64 + lane], a2 = sk[128 + lane];
 #pragma unroll
-    for (int s = 0; s < NS; ++s) {
-      const int sn = s + 1 < NS ? s + 1 : s;
-      const bf16x8 n0 = sk[sn * 192 + lane], n1 = sk[sn * 192 + 64 + lane], n2 = sk[sn * 192 + 128 + lane];
+    for (int t = 0; t < 2 * NS; ++t) {
+      const int s = t >> 1, ib = t & 1;
+      const int en = (t + 1 < 2 * NS ? t + 1 : t) * 192 + lane;
+      const bf16x8 n0 = sk[en], n1 = sk[en + 64], n2 = sk[en + 128];
 #pragma unroll
-      for (int j = 0; j < RB; ++j) sa[j] = mfma_split<NT>(a0, a1, a2, hk[j][s][0], hk[j][s][1], hk[j][s][2], sa[j]);
+      for (int rb = 0; rb < 2; ++rb)
+        sa[ib][rb] = mfma16_split<NT>(a0, a1, a2, hk[s][rb][0], hk[s][rb][1], hk[s][rb][2], sa[ib][rb]);
       a0 = n0;
       a1 = n1;
       a2 = n2;
       __builtin_amdgcn_sched_barrier(0);
     }
 #pragma unroll
-    for (int j = 0; j < RB; ++j) {
-      // logits (item acc32_row(r, hh) of the chunk, row l32 of block j)
+    for (int rb = 0; rb < 2; ++rb) {
+      // logits (items 16ib + 4kg + u of the chunk, row 16rb + l16)
       float cm = NEG_INF;
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const f4 bq = *reinterpret_cast<const f4*>(&sb[8 * q + 4 * hh]);
+      for (int ib = 0; ib < 2; ++ib) {
+        const f4 bq = *reinterpret_cast<const f4*>(&sb[16 * ib + 4 * kg]);
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
-          const float z = sa[j][4 * q + u] + bq[u];
-          if (ARG && z > bv[j]) {  // items increase with r: strict > keeps the first maximum
-            bv[j] = z;
-            bi[j] = 32 * (c0 + c) + 8 * q + 4 * hh + u;
+          const float z = sa[ib][rb][u] + bq[u];
+          if (ARG && z > bv[rb]) {  // items increase with (ib, u): strict > keeps the first maximum
+            bv[rb] = z;
+            bi[rb] = 32 * (c0 + c) + 16 * ib + 4 * kg + u;
           }
-          sa[j][4 * q + u] = z * L2E;
+          sa[ib][rb][u] = z * L2E;
           cm = fmaxf(cm, z);
         }
       }
+      cm = fmaxf(cm, __shfl_xor(cm, 16));
       cm = fmaxf(cm, __shfl_xor(cm, 32));
-      if (ARG && cmax != nullptr && hh == 0 && r0 + 32 * j < B) cmax[(int64_t)(c0 + c) * B + r0 + 32 * j + l32] = cm;
+      if (ARG && cmax != nullptr && kg == 0) cmax[(int64_t)(c0 + c) * B + r0 + 16 * rb + l16] = cm;
       cm *= L2E;
-      const float mn = fmaxf(m[j], cm);
-      if (__any(mn > m[j])) {
-        const float a = mn > m[j] ? __builtin_amdgcn_exp2f(m[j] - mn) : 1.f;
+      const float mn = fmaxf(m[rb], cm);
+      if (__any(mn > m[rb])) {
+        const float a = mn > m[rb] ? __builtin_amdgcn_exp2f(m[rb] - mn) : 1.f;
 #pragma unroll
-        for (int t = 0; t < NTL; ++t) o[j][t] *= a;
-        l[j] *= a;
-        m[j] = mn;
+        for (int fb = 0; fb < NF; ++fb) o[fb][rb] *= a;
+        l[rb] *= a;
+        m[rb] = mn;
       }
-      const float mm = m[j] == NEG_INF ? 0.f : m[j];
+      const float mm = m[rb] == NEG_INF ? 0.f : m[rb];
       float ps = 0.f;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const float p = __builtin_amdgcn_exp2f(sa[j][r] - mm);
-        sa[j][r] = p;
-        ps += p;
-      }
-      l[j] += ps;
+      for (int ib = 0; ib < 2; ++ib)
 #pragma unroll
-      for (int s = 0; s < 2; ++s)
-        split3x8(f4{sa[j][8 * s], sa[j][8 * s + 1], sa[j][8 * s + 2], sa[j][8 * s + 3]},
-                 f4{sa[j][8 * s + 4], sa[j][8 * s + 5], sa[j][8 * s + 6], sa[j][8 * s + 7]}, q0[j][s], q1[j][s],
-                 q2[j][s]);
+        for (int u = 0; u < 4; ++u) {
+          const float p = __builtin_amdgcn_exp2f(sa[ib][rb][u] - mm);
+          sa[ib][rb][u] = p;
+          ps += p;
+        }
+      l[rb] += ps;
+      // k slots of the O-part: items kperm16(kg, e)
+      split3x8(sa[0][rb], sa[1][rb], q0[rb], q1[rb], q2[rb]);
     }
   };
-  // O-part: Oᵀ += W_cᵀ·Pᵀ for every block
-  auto opart = [&](const bf16x8* sr, const bf16x8 (&q0)[RB][2], const bf16x8 (&q1)[RB][2],
-                   const bf16x8 (&q2)[RB][2]) __attribute__((always_inline)) {
+  // O-part: Oᵀ += W_cᵀ·Pᵀ, one R-plane fragment per feature block
+  auto opart = [&](const bf16x8* sr, const bf16x8 (&q0)[2], const bf16x8 (&q1)[2], const bf16x8 (&q2)[2])
+                   __attribute__((always_inline)) {
     if constexpr (NG > 0) {
-    bf16x8 a0 = sr[lane], a1 = sr[64 + lane], a2 = sr[128 + lane];
+      bf16x8 a0 = sr[lane], a1 = sr[64 + lane], a2 = sr[128 + lane];
 #pragma unroll
-    for (int ts = 0; ts < 2 * NTL; ++ts) {
-      const int t = ts >> 1, s = ts & 1;
-      const int en = (ts + 1 < 2 * NTL ? ts + 1 : ts) * 192 + lane;
-      const bf16x8 n0 = sr[en], n1 = sr[en + 64], n2 = sr[en + 128];
+      for (int fb = 0; fb < NF; ++fb) {
+        const int en = (fb + 1 < NF ? fb + 1 : fb) * 192 + lane;
+        const bf16x8 n0 = sr[en], n1 = sr[en + 64], n2 = NG == 3 ? n0 : sr[en + 128];
 #pragma unroll
-      for (int j = 0; j < RB; ++j) o[j][t] = mfma_split<NG>(a0, a1, a2, q0[j][s], q1[j][s], q2[j][s], o[j][t]);
-      a0 = n0;
-      a1 = n1;
-      a2 = n2;
-      __builtin_amdgcn_sched_barrier(0);
-    }
+        for (int rb = 0; rb < 2; ++rb) o[fb][rb] = mfma16_split<NG>(a0, a1, a2, q0[rb], q1[rb], q2[rb], o[fb][rb]);
+        a0 = n0;
+        a1 = n1;
+        a2 = n2;
+        __builtin_amdgcn_sched_barrier(0);
+      }
     }
   };
   for (int c = 0; c < nch; c += 2) {
-    bf16x8 q0[RB][2], q1[RB][2], q2[RB][2];
+    bf16x8 q0[2], q1[2], q2[2];
     if (DR || NG == 0) {
       if (c + 1 < nch) {
         FL_ISSUE_K(c0 + c + 1, sk1, sb1);
@@ -348,23 +344,27 @@ __global__ __launch_bounds__(64 * fl_nw(HF, 1)) void k_flash_fwd(
   }
 #undef FL_ISSUE_K
 #undef FL_ISSUE_R
+  if (!active) return;
 #pragma unroll
-  for (int j = 0; j < RB; ++j) {
-    if (r0 + 32 * j >= B) break;
-    const float lt = l[j] + __shfl_xor(l[j], 32);
-    const int row = r0 + 32 * j + l32;
-    float bvj = bv[j];
-    int bij = bi[j];
-    if (ARG) {  // merge the lane halves: larger value, ties to the smaller item
-      const float v2 = __shfl_xor(bvj, 32);
-      const int i2 = __shfl_xor(bij, 32);
-      if (v2 > bvj || (v2 == bvj && i2 < bij)) {
-        bvj = v2;
-        bij = i2;
+  for (int rb = 0; rb < 2; ++rb) {
+    float lt = l[rb] + __shfl_xor(l[rb], 16);
+    lt += __shfl_xor(lt, 32);
+    const int row = r0 + 16 * rb + l16;
+    float bvj = bv[rb];
+    int bij = bi[rb];
+    if (ARG) {  // merge the four lane groups: larger value, ties to the smaller item
+#pragma unroll
+      for (int d = 16; d <= 32; d *= 2) {
+        const float v2 = __shfl_xor(bvj, d);
+        const int i2 = __shfl_xor(bij, d);
+        if (v2 > bvj || (v2 == bvj && i2 < bij)) {
+          bvj = v2;
+          bij = i2;
+        }
       }
     }
-    if (hh == 0) {
-      pm[(int64_t)split * B + row] = m[j];
+    if (kg == 0) {
+      pm[(int64_t)split * B + row] = m[rb];
       pl[(int64_t)split * B + row] = lt;
       if (ARG) {
         pbest[(int64_t)split * B + row] = bvj;
@@ -373,10 +373,9 @@ __global__ __launch_bounds__(64 * fl_nw(HF, 1)) void k_flash_fwd(
     }
     if constexpr (NG > 0) {
 #pragma unroll
-      for (int t = 0; t < NTL; ++t)
+      for (int fb = 0; fb < NF; ++fb)
 #pragma unroll
-        for (int r = 0; r < 16; ++r)
-          pO[((int64_t)split * HF + 32 * t + acc32_row(r, hh)) * B + row] = o[j][t][r];
+        for (int i = 0; i < 4; ++i) pO[((int64_t)split * HF + 16 * fb + 4 * kg + i) * B + row] = o[fb][rb][i];
     }
   }
 }
@@ -396,11 +395,11 @@ __global__ __launch_bounds__(64 * fl_nw(HF, 1)) void k_flash_amax(
     const bf16x8* __restrict__ Hk, const bf16x8* __restrict__ Wk, const float* __restrict__ bias_pad, int B, int A,
     int nrb, int nsplit, int cps, float* __restrict__ pbest, int32_t* __restrict__ parg, float* __restrict__ cmax) {
   constexpr int NW = fl_nw(HF, 1);
-  constexpr int NS = HF / 16;
-  constexpr int EK = NS * 192;
+  constexpr int NS = HF / 32;
+  constexpr int EK = NS * 2 * 192;
   __shared__ bf16x8 sk0[EK], sk1[EK];
   __shared__ __attribute__((aligned(16))) float sb0[32], sb1[32];
-  const int tid = threadIdx.x, lane = tid & 63, hh = lane >> 5, l32 = lane & 31, lane16 = 16 * lane;
+  const int tid = threadIdx.x, lane = tid & 63, kg = lane >> 4, l16 = lane & 15, lane16 = 16 * lane;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   int bid = blockIdx.x;
   const int total = nrb * nsplit;
@@ -417,45 +416,60 @@ __global__ __launch_bounds__(64 * fl_nw(HF, 1)) void k_flash_amax(
     if (w == 0 && lane < 8) blds16(rsrc_of(bias_pad + 32 * (C)), SB, lane16, 0); \
   } while (0)
   if (nch > 0) FA_ISSUE(c0, sk0, sb0);
-  bf16x8 hk[NS][3];
+  bf16x8 hk[NS][2][3];
 #pragma unroll
   for (int s = 0; s < NS; ++s)
 #pragma unroll
-    for (int p = 0; p < 3; ++p)
-      hk[s][p] = active ? Hk[((int64_t)(r0 >> 5) * NS + s) * 192 + p * 64 + lane] : bf16x8{};
-  float bv = NEG_INF;
-  int bi = INT32_MAX;
+    for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+      for (int p = 0; p < 3; ++p)
+        hk[s][rb][p] = active && (NT != 3 || p < 2)
+                           ? Hk[(((int64_t)(r0 >> 5) * NS + s) * 2 + rb) * 192 + p * 64 + lane]
+                           : bf16x8{};
+  float bv[2] = {NEG_INF, NEG_INF};
+  int bi[2] = {INT32_MAX, INT32_MAX};
   __syncthreads();
   auto chunk = [&](const bf16x8* sk, const float* sb, int c) __attribute__((always_inline)) {
-    f16v sa = {};
-    bf16x8 a0 = sk[lane], a1 = sk[64 + lane], a2 = sk[128 + lane];
+    f4 sa[2][2];
 #pragma unroll
-    for (int s = 0; s < NS; ++s) {
-      const int sn = s + 1 < NS ? s + 1 : s;
-      const bf16x8 n0 = sk[sn * 192 + lane], n1 = sk[sn * 192 + 64 + lane], n2 = sk[sn * 192 + 128 + lane];
-      sa = mfma_split<NT>(a0, a1, a2, hk[s][0], hk[s][1], hk[s][2], sa);
+    for (int ib = 0; ib < 2; ++ib)
+#pragma unroll
+      for (int rb = 0; rb < 2; ++rb) sa[ib][rb] = f4{0.f, 0.f, 0.f, 0.f};
+    bf16x8 a0 = sk[lane], a1 = sk[64 + lane], a2 = NT == 3 ? a0 : sk[128 + lane];
+#pragma unroll
+    for (int t = 0; t < 2 * NS; ++t) {
+      const int s = t >> 1, ib = t & 1;
+      const int en = (t + 1 < 2 * NS ? t + 1 : t) * 192 + lane;
+      const bf16x8 n0 = sk[en], n1 = sk[en + 64], n2 = NT == 3 ? n0 : sk[en + 128];
+#pragma unroll
+      for (int rb = 0; rb < 2; ++rb)
+        sa[ib][rb] = mfma16_split<NT>(a0, a1, a2, hk[s][rb][0], hk[s][rb][1], hk[s][rb][2], sa[ib][rb]);
       a0 = n0;
       a1 = n1;
       a2 = n2;
       __builtin_amdgcn_sched_barrier(0);
     }
-    float cm = NEG_INF;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const f4 bq = *reinterpret_cast<const f4*>(&sb[8 * q + 4 * hh]);
+    for (int rb = 0; rb < 2; ++rb) {
+      float cm = NEG_INF;
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const float z = sa[4 * q + u] + bq[u];
-        cm = fmaxf(cm, z);
-        if (z > bv) {  // items increase with r: strict > keeps the first maximum
-          bv = z;
-          bi = 32 * (c0 + c) + 8 * q + 4 * hh + u;
+      for (int ib = 0; ib < 2; ++ib) {
+        const f4 bq = *reinterpret_cast<const f4*>(&sb[16 * ib + 4 * kg]);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const float z = sa[ib][rb][u] + bq[u];
+          cm = fmaxf(cm, z);
+          if (z > bv[rb]) {  // items increase with (ib, u): strict > keeps the first maximum
+            bv[rb] = z;
+            bi[rb] = 32 * (c0 + c) + 16 * ib + 4 * kg + u;
+          }
         }
       }
-    }
-    if (CM) {
-      cm = fmaxf(cm, __shfl_xor(cm, 32));
-      if (hh == 0) cmax[(int64_t)(c0 + c) * B + r0 + l32] = cm;
+      if (CM) {
+        cm = fmaxf(cm, __shfl_xor(cm, 16));
+        cm = fmaxf(cm, __shfl_xor(cm, 32));
+        if (kg == 0) cmax[(int64_t)(c0 + c) * B + r0 + 16 * rb + l16] = cm;
+      }
     }
   };
   for (int c = 0; c < nch; c += 2) {
@@ -472,15 +486,23 @@ __global__ __launch_bounds__(64 * fl_nw(HF, 1)) void k_flash_amax(
   }
 #undef FA_ISSUE
   if (!active) return;
-  const float v2 = __shfl_xor(bv, 32);
-  const int i2 = __shfl_xor(bi, 32);
-  if (v2 > bv || (v2 == bv && i2 < bi)) {
-    bv = v2;
-    bi = i2;
-  }
-  if (hh == 0) {
-    pbest[(int64_t)split * B + r0 + l32] = bv;
-    parg[(int64_t)split * B + r0 + l32] = bi;
+#pragma unroll
+  for (int rb = 0; rb < 2; ++rb) {
+    float bvj = bv[rb];
+    int bij = bi[rb];
+#pragma unroll
+    for (int d = 16; d <= 32; d *= 2) {
+      const float v2 = __shfl_xor(bvj, d);
+      const int i2 = __shfl_xor(bij, d);
+      if (v2 > bvj || (v2 == bvj && i2 < bij)) {
+        bvj = v2;
+        bij = i2;
+      }
+    }
+    if (kg == 0) {
+      pbest[(int64_t)split * B + r0 + 16 * rb + l16] = bvj;
+      parg[(int64_t)split * B + r0 + 16 * rb + l16] = bij;
+    }
   }
 }
 
@@ -558,8 +580,7 @@ __global__ __launch_bounds__(256) void k_flash_dh(const float* __restrict__ pm, 
 
 // ------------------------------------------------------------- pass 2 ----
 // Same ring scheme as pass 1 (HF 256: single-buffered R-planes of h); a wave
-// owns RB blocks of 32 items.
-template <int HF, int NT>
+// owns 32 items (two 16-item tiles).
 //
 // Tail: the item blocks past the last whole round of workgroups (nfull
 // blocks) are split over tsplit workgroups each, every one taking a
@@ -568,26 +589,27 @@ template <int HF, int NT>
 // k_flash_tail sums them in order and finishes (Adam, planes).  At C2 the
 // 67 leftover blocks of 3907 would otherwise run as a 16th round on 26% of
 // the CUs.
+template <int HF, int NT>
 __global__ __launch_bounds__(64 * fl_nw(HF, 2)) void k_flash_dw(
     const bf16x8* __restrict__ Hk0, const bf16x8* __restrict__ Hr0, const bf16x8* Wk, const float* bias_pad,
     const float2* __restrict__ rowinfo0, float g, int B, int A, float* __restrict__ W, float* __restrict__ mW,
     float* __restrict__ vW, float* __restrict__ bias, float* __restrict__ mb, float* __restrict__ vb, AdamArgs args,
     float* __restrict__ dW_out, float* __restrict__ db_out, bf16x8* Wk_out, bf16x8* Wr_out, float* bias_pad_out,
     int nfull, int tsplit, float* __restrict__ tail_dw, float* __restrict__ tail_db) {
-  constexpr int NW = fl_nw(HF, 2), RB = fl_rb(HF, 2);
+  constexpr int NW = fl_nw(HF, 2);
   constexpr bool DR = HF <= 128;
-  constexpr int NS = HF / 16, NTL = HF / 32;
-  constexpr int EK = NS * 192;
-  constexpr int ER = NTL * 2 * 192;
+  constexpr int NS = HF / 32, NF = HF / 16;
+  constexpr int EK = NS * 2 * 192;
+  constexpr int ER = NF * 192;
   __shared__ bf16x8 sk0[EK], sk1[EK];
   __shared__ bf16x8 sr0[ER], sr1[DR ? ER : 1];
   __shared__ __attribute__((aligned(16))) float2 si0[32], si1[32];
-  const int tid = threadIdx.x, lane = tid & 63, hh = lane >> 5, l32 = lane & 31, lane16 = 16 * lane;
+  const int tid = threadIdx.x, lane = tid & 63, kg = lane >> 4, l16 = lane & 15, lane16 = 16 * lane;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int bx = blockIdx.x;
   const bool tail = bx >= nfull;
   const int blk = tail ? nfull + (bx - nfull) / tsplit : bx;
-  const int j0 = blk * fl_rows(HF, 2) + 32 * RB * w;   // this wave's first item
+  const int j0 = blk * fl_rows(HF, 2) + 32 * w;   // this wave's first item
   const bool active = j0 < A;
   const int nct = B / 32, cper = (nct + tsplit - 1) / tsplit;
   const int cb = tail ? (bx - nfull) % tsplit * cper : 0;
@@ -603,86 +625,82 @@ __global__ __launch_bounds__(64 * fl_nw(HF, 2)) void k_flash_dw(
 #define FL_ISSUE_R(C, SR) stage<ER, NW>(Hr + (int64_t)(C) * ER, SR, w, lane16)
   FL_ISSUE_K(0, sk0, si0);
   FL_ISSUE_R(0, sr0);
-  // this wave's RB × 32 items of W (B operands of S = h_c·Wᵀ)
-  bf16x8 wk[RB][NS][3];
-  float bj[RB];
+  // this wave's 32 items of W as two 16-item B operands of S = h_c·Wᵀ
+  bf16x8 wk[NS][2][3];
+  float bj[2];
 #pragma unroll
-  for (int j = 0; j < RB; ++j) {
-    const bool act = j0 + 32 * j < A;
+  for (int ib = 0; ib < 2; ++ib) {
 #pragma unroll
     for (int s = 0; s < NS; ++s)
 #pragma unroll
       for (int p = 0; p < 3; ++p)
-        wk[j][s][p] = act ? Wk[((int64_t)((j0 >> 5) + j) * NS + s) * 192 + p * 64 + lane] : bf16x8{};
-    bj[j] = act ? bias_pad[j0 + 32 * j + l32] : NEG_INF;
+        wk[s][ib][p] = active ? Wk[(((int64_t)(j0 >> 5) * NS + s) * 2 + ib) * 192 + p * 64 + lane] : bf16x8{};
+    bj[ib] = active ? bias_pad[j0 + 16 * ib + l16] : NEG_INF;
   }
-  f16v dw[RB][NTL];
-  float dbs[RB];
+  // dW tiles (item block ib, feature block fb): lane (kg, n) holds items
+  // 16ib + 4kg + i, feature 16fb + n; db per item block: this lane's item 16ib + l16
+  f4 dw[2][NF];
+  float dbs[2] = {0.f, 0.f};
 #pragma unroll
-  for (int j = 0; j < RB; ++j) {
+  for (int ib = 0; ib < 2; ++ib)
 #pragma unroll
-    for (int t = 0; t < NTL; ++t) dw[j][t] = f16v{};
-    dbs[j] = 0.f;
-  }
+    for (int fb = 0; fb < NF; ++fb) dw[ib][fb] = f4{0.f, 0.f, 0.f, 0.f};
   __syncthreads();
-  // S = h_c·Wᵀ recomputed, dZ = g·(2^(S−lse) − onehot), db; P planes
-  auto spart = [&](const bf16x8* sk, const float2* si, bf16x8 (&q0)[RB][2], bf16x8 (&q1)[RB][2],
-                   bf16x8 (&q2)[RB][2]) __attribute__((always_inline)) {
-    f16v sa[RB];
+  // S = h_c·Wᵀ recomputed, dZ = g·(2^(S−lse) − onehot), db; dZᵀ planes
+  // (q*[ib]: the A operand of dW, k over the chunk's rows in kperm16 order)
+  auto spart = [&](const bf16x8* sk, const float2* si, bf16x8 (&q0)[2], bf16x8 (&q1)[2], bf16x8 (&q2)[2])
+                   __attribute__((always_inline)) {
+    f4 sa[2][2];   // [rb][ib]: lane (kg, n) holds rows 16rb + 4kg + u, item 16ib + n
 #pragma unroll
-    for (int j = 0; j < RB; ++j) sa[j] = f16v{};
-    // operand fragments software-pipelined one slice ahead; the sched
-    // barriers stop the scheduler from hoisting every slice's LDS reads
+    for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+      for (int ib = 0; ib < 2; ++ib) sa[rb][ib] = f4{0.f, 0.f, 0.f, 0.f};
     bf16x8 a0 = sk[lane], a1 = sk[64 + lane], a2 = sk[128 + lane];
 #pragma unroll
-    for (int s = 0; s < NS; ++s) {
-      const int sn = s + 1 < NS ? s + 1 : s;
-      const bf16x8 n0 = sk[sn * 192 + lane], n1 = sk[sn * 192 + 64 + lane], n2 = sk[sn * 192 + 128 + lane];
+    for (int t = 0; t < 2 * NS; ++t) {
+      const int s = t >> 1, rb = t & 1;
+      const int en = (t + 1 < 2 * NS ? t + 1 : t) * 192 + lane;
+      const bf16x8 n0 = sk[en], n1 = sk[en + 64], n2 = sk[en + 128];
 #pragma unroll
-      for (int j = 0; j < RB; ++j) sa[j] = mfma_split<NT>(a0, a1, a2, wk[j][s][0], wk[j][s][1], wk[j][s][2], sa[j]);
+      for (int ib = 0; ib < 2; ++ib)
+        sa[rb][ib] = mfma16_split<NT>(a0, a1, a2, wk[s][ib][0], wk[s][ib][1], wk[s][ib][2], sa[rb][ib]);
       a0 = n0;
       a1 = n1;
       a2 = n2;
       __builtin_amdgcn_sched_barrier(0);
     }
-    // dZ for (row acc32_row(r, hh), item l32 of block j); db summed per chunk first
 #pragma unroll
-    for (int j = 0; j < RB; ++j) {
-      const int item = j0 + 32 * j + l32;
+    for (int ib = 0; ib < 2; ++ib) {
+      const int item = j0 + 16 * ib + l16;
       float cdb = 0.f;
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const f4 i0 = *reinterpret_cast<const f4*>(&si[8 * q + 4 * hh]);
-        const f4 i1 = *reinterpret_cast<const f4*>(&si[8 * q + 4 * hh + 2]);
+      for (int rb = 0; rb < 2; ++rb) {
+        const f4 i0 = *reinterpret_cast<const f4*>(&si[16 * rb + 4 * kg]);
+        const f4 i1 = *reinterpret_cast<const f4*>(&si[16 * rb + 4 * kg + 2]);
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
           const float lse2 = u < 2 ? i0[2 * u] : i1[2 * (u - 2)];
           const int tb = __float_as_int(u < 2 ? i0[2 * u + 1] : i1[2 * (u - 2) + 1]);
-          const float e = __builtin_amdgcn_exp2f(fmaf(sa[j][4 * q + u] + bj[j], L2E, -lse2));
+          const float e = __builtin_amdgcn_exp2f(fmaf(sa[rb][ib][u] + bj[ib], L2E, -lse2));
           const float p = g * (e - (tb == item ? 1.f : 0.f));
-          sa[j][4 * q + u] = p;
+          sa[rb][ib][u] = p;
           cdb += p;
         }
       }
-      dbs[j] += cdb;
-#pragma unroll
-      for (int s = 0; s < 2; ++s)
-        split3x8(f4{sa[j][8 * s], sa[j][8 * s + 1], sa[j][8 * s + 2], sa[j][8 * s + 3]},
-                 f4{sa[j][8 * s + 4], sa[j][8 * s + 5], sa[j][8 * s + 6], sa[j][8 * s + 7]}, q0[j][s], q1[j][s],
-                 q2[j][s]);
+      dbs[ib] += cdb;
+      split3x8(sa[0][ib], sa[1][ib], q0[ib], q1[ib], q2[ib]);
     }
   };
-  // dW += dZᵀ·h_c for every block
-  auto wpart = [&](const bf16x8* sr, const bf16x8 (&q0)[RB][2], const bf16x8 (&q1)[RB][2],
-                   const bf16x8 (&q2)[RB][2]) __attribute__((always_inline)) {
+  // dW += dZᵀ·h_c, one R-plane fragment of h per feature block
+  auto wpart = [&](const bf16x8* sr, const bf16x8 (&q0)[2], const bf16x8 (&q1)[2], const bf16x8 (&q2)[2])
+                   __attribute__((always_inline)) {
     bf16x8 b0 = sr[lane], b1 = sr[64 + lane], b2 = sr[128 + lane];
 #pragma unroll
-    for (int ts = 0; ts < 2 * NTL; ++ts) {
-      const int t = ts >> 1, s = ts & 1;
-      const int en = (ts + 1 < 2 * NTL ? ts + 1 : ts) * 192 + lane;
+    for (int fb = 0; fb < NF; ++fb) {
+      const int en = (fb + 1 < NF ? fb + 1 : fb) * 192 + lane;
       const bf16x8 n0 = sr[en], n1 = sr[en + 64], n2 = sr[en + 128];
 #pragma unroll
-      for (int j = 0; j < RB; ++j) dw[j][t] = mfma_split<NT>(q0[j][s], q1[j][s], q2[j][s], b0, b1, b2, dw[j][t]);
+      for (int ib = 0; ib < 2; ++ib) dw[ib][fb] = mfma16_split<NT>(q0[ib], q1[ib], q2[ib], b0, b1, b2, dw[ib][fb]);
       b0 = n0;
       b1 = n1;
       b2 = n2;
@@ -690,7 +708,7 @@ __global__ __launch_bounds__(64 * fl_nw(HF, 2)) void k_flash_dw(
     }
   };
   for (int c = 0; c < nch; c += 2) {
-    bf16x8 q0[RB][2], q1[RB][2], q2[RB][2];
+    bf16x8 q0[2], q1[2], q2[2];
     if (DR) {
       if (c + 1 < nch) {
         FL_ISSUE_K(c + 1, sk1, si1);
@@ -736,10 +754,10 @@ __global__ __launch_bounds__(64 * fl_nw(HF, 2)) void k_flash_dw(
 #undef FL_ISSUE_K
 #undef FL_ISSUE_R
   // Adam epilogue; with Wk_out / Wr_out (Adam mode) the updated rows also
-  // leave as the next pass 1's operand planes: the accumulator block of a
-  // (t, s) pair already is an R-plane entry (registers 8s..8s+7 = rows
-  // 16s + kperm(hh, i)), the K-planes go through a per-wave LDS transpose
-  // (32 items × 32 columns at a time, rows padded to 33 floats)
+  // leave as the next pass 1's operand planes: the two item tiles of a
+  // feature block already are an R-plane entry (items kperm16(kg, e)), the
+  // K-planes go through a per-wave LDS transpose (32 items × 32 columns at a
+  // time, rows padded to 33 floats)
   // (the ring arrays are idle after the main loop's last barrier; HF 32's are
   // too small, so it has its own)
   constexpr int TRP = 33, TRW = 32 * TRP;         // floats per wave
@@ -753,94 +771,98 @@ __global__ __launch_bounds__(64 * fl_nw(HF, 2)) void k_flash_dw(
     bf16x8* base = ai == 0 ? sk0 : ai == 1 ? sk1 : ai == 2 ? sr0 : sr1;
     tr = reinterpret_cast<float*>(base) + ao;
   }
+  if (!active) return;
   const bool planes = Wk_out != nullptr && dW_out == nullptr;
+  float dbt[2];
+#pragma unroll
+  for (int ib = 0; ib < 2; ++ib) {
+    dbt[ib] = dbs[ib] + __shfl_xor(dbs[ib], 16);
+    dbt[ib] += __shfl_xor(dbt[ib], 32);
+  }
   if (tail) {
     const int i0 = nfull * fl_rows(HF, 2), ntail = A - i0, part = (bx - nfull) % tsplit;
 #pragma unroll
-    for (int j = 0; j < RB; ++j) {
-      const int jb = j0 + 32 * j;
-      if (jb >= A) break;
-      const int item = jb + l32;
-      const float dbt = dbs[j] + __shfl_xor(dbs[j], 32);
-      if (hh == 0 && item < A) tail_db[(int64_t)part * ntail + item - i0] = dbt;
+    for (int ib = 0; ib < 2; ++ib) {
+      const int item = j0 + 16 * ib + l16;
+      if (kg == 0 && item < A) tail_db[(int64_t)part * ntail + item - i0] = dbt[ib];
 #pragma unroll
-      for (int t = 0; t < NTL; ++t)
+      for (int fb = 0; fb < NF; ++fb)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int it = jb + acc32_row(r, hh);
-          if (it < A) tail_dw[((int64_t)part * ntail + it - i0) * HF + 32 * t + l32] = dw[j][t][r];
+        for (int i = 0; i < 4; ++i) {
+          const int it = j0 + 16 * ib + 4 * kg + i;
+          if (it < A) tail_dw[((int64_t)part * ntail + it - i0) * HF + 16 * fb + l16] = dw[ib][fb][i];
         }
     }
     return;
   }
 #pragma unroll
-  for (int j = 0; j < RB; ++j) {
-    const int jb = j0 + 32 * j;
-    if (jb >= A) break;
-    const int item = jb + l32;
-    const float dbt = dbs[j] + __shfl_xor(dbs[j], 32);
-    if (hh == 0 && item < A) {
+  for (int ib = 0; ib < 2; ++ib) {
+    const int item = j0 + 16 * ib + l16;
+    if (kg == 0 && item < A) {
       if (db_out) {
-        db_out[item] = dbt;
+        db_out[item] = dbt[ib];
       } else {
         float p = bias[item], mq = mb[item], v = vb[item];
-        adam_elem(p, mq, v, dbt, args);
+        adam_elem(p, mq, v, dbt[ib], args);
         bias[item] = p;
         mb[item] = mq;
         vb[item] = v;
         if (planes) bias_pad_out[item] = p;
       }
     }
+  }
+  const int64_t blk32 = j0 >> 5;
 #pragma unroll
-    for (int t = 0; t < NTL; ++t) {
-      const int col = 32 * t + l32;
+  for (int s = 0; s < NS; ++s) {
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int it = jb + acc32_row(r, hh);
-        if (it >= A) {
-          dw[j][t][r] = 0.f;   // rows past A: zero planes, as rg_head_planes writes them
-          continue;
+    for (int f2 = 0; f2 < 2; ++f2) {
+      const int fb = 2 * s + f2, col = 16 * fb + l16;
+#pragma unroll
+      for (int ib = 0; ib < 2; ++ib)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int it = j0 + 16 * ib + 4 * kg + i;
+          if (it >= A) {
+            dw[ib][fb][i] = 0.f;   // rows past A: zero planes, as rg_head_planes writes them
+            continue;
+          }
+          const int64_t o = (int64_t)it * HF + col;
+          if (dW_out) {
+            dW_out[o] = dw[ib][fb][i];
+          } else {
+            float p = W[o], mq = mW[o], v = vW[o];
+            adam_elem(p, mq, v, dw[ib][fb][i], args);
+            W[o] = p;
+            mW[o] = mq;
+            vW[o] = v;
+            dw[ib][fb][i] = p;
+          }
         }
-        const int64_t o = (int64_t)it * HF + col;
-        if (dW_out) {
-          dW_out[o] = dw[j][t][r];
-        } else {
-          float p = W[o], mq = mW[o], v = vW[o];
-          adam_elem(p, mq, v, dw[j][t][r], args);
-          W[o] = p;
-          mW[o] = mq;
-          vW[o] = v;
-          dw[j][t][r] = p;
-        }
-      }
       if (planes) {
-        const int64_t blk = jb >> 5;
+        bf16x8 p0, p1, p2;
+        split3x8(dw[0][fb], dw[1][fb], p0, p1, p2);
+        bf16x8* dst = Wr_out + (blk32 * NF + fb) * 192 + lane;
+        dst[0] = p0;
+        dst[64] = p1;
+        dst[128] = p2;
 #pragma unroll
-        for (int s2 = 0; s2 < 2; ++s2) {
-          bf16x8 p0, p1, p2;
-          split3x8(f4{dw[j][t][8 * s2], dw[j][t][8 * s2 + 1], dw[j][t][8 * s2 + 2], dw[j][t][8 * s2 + 3]},
-                   f4{dw[j][t][8 * s2 + 4], dw[j][t][8 * s2 + 5], dw[j][t][8 * s2 + 6], dw[j][t][8 * s2 + 7]}, p0, p1,
-                   p2);
-          bf16x8* dst = Wr_out + ((blk * NTL + t) * 2 + s2) * 192 + lane;
-          dst[0] = p0;
-          dst[64] = p1;
-          dst[128] = p2;
-        }
+        for (int ib = 0; ib < 2; ++ib)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) tr[acc32_row(r, hh) * TRP + l32] = dw[j][t][r];
-        // (item, 8-column group) entries of these 32 columns: 32 items × 4 groups
+          for (int i = 0; i < 4; ++i) tr[(16 * ib + 4 * kg + i) * TRP + 16 * f2 + l16] = dw[ib][fb][i];
+      }
+    }
+    if (planes) {
+      // (item, 8-column group) entries of columns 32s .. 32s + 31: 32 items × 4 groups
 #pragma unroll
-        for (int q = 0; q < 2; ++q) {
-          const int e = lane + 64 * q, ii = e & 31, grp = e >> 5;
-          const float* src = tr + ii * TRP + 8 * grp;
-          bf16x8 p0, p1, p2;
-          split3x8(f4{src[0], src[1], src[2], src[3]}, f4{src[4], src[5], src[6], src[7]}, p0, p1, p2);
-          const int sk = 2 * t + (grp >> 1);
-          bf16x8* dst = Wk_out + (blk * NS + sk) * 192 + (grp & 1) * 32 + ii;
-          dst[0] = p0;
-          dst[64] = p1;
-          dst[128] = p2;
-        }
+      for (int q = 0; q < 2; ++q) {
+        const int e = lane + 64 * q, ii = e & 31, grp = e >> 5;
+        const float* src = tr + ii * TRP + 8 * grp;
+        bf16x8 p0, p1, p2;
+        split3x8(f4{src[0], src[1], src[2], src[3]}, f4{src[4], src[5], src[6], src[7]}, p0, p1, p2);
+        bf16x8* dst = Wk_out + ((blk32 * NS + s) * 2 + (ii >> 4)) * 192 + 16 * grp + (ii & 15);
+        dst[0] = p0;
+        dst[64] = p1;
+        dst[128] = p2;
       }
     }
   }
@@ -1189,7 +1211,7 @@ extern "C" int rg_head_planes(const float* X, int rows, int HF, void* planes_k, 
   if (!flash_hf_ok(HF)) return RG_ERR_SHAPE;
   const int rp = (rows + 31) / 32 * 32;
   const unsigned gk = (unsigned)(((int64_t)rp * (HF / 8) + 255) / 256);
-  const unsigned gr = (unsigned)(((int64_t)(rp / 32) * (HF / 32) * 2 * 64 + 255) / 256);
+  const unsigned gr = (unsigned)(((int64_t)(rp / 32) * (HF / 16) * 64 + 255) / 256);
 #define PL(HFV)                                                                                                \
   if (planes_k)                                                                                                \
     hipLaunchKernelGGL(k_planes_k<HFV>, dim3(gk), dim3(256), 0, stream, X, rows, rp, (bf16x8*)planes_k);     \
@@ -1475,10 +1497,10 @@ extern "C" int rg_flash_dw_adam_planes(const void* Hk, const void* Hr, const voi
       const int ap = (A + 31) / 32 * 32;
       const float* Xs = W + (int64_t)i0 * HF;
       bf16x8* Pk = (bf16x8*)Wk_out + (int64_t)(i0 / 32) * (HF / 16) * 192;
-      bf16x8* Pr = (bf16x8*)Wr_out + (int64_t)(i0 / 32) * (HF / 32) * 2 * 192;
+      bf16x8* Pr = (bf16x8*)Wr_out + (int64_t)(i0 / 32) * (HF / 16) * 192;
       const int rows = A - i0, rp = ap - i0;
       const unsigned gk = (unsigned)(((int64_t)rp * (HF / 8) + 255) / 256);
-      const unsigned gr = (unsigned)(((int64_t)(rp / 32) * (HF / 32) * 2 * 64 + 255) / 256);
+      const unsigned gr = (unsigned)(((int64_t)(rp / 32) * (HF / 16) * 64 + 255) / 256);
 #define PLT(HFV)                                                                                   \
   hipLaunchKernelGGL(k_planes_k<HFV>, dim3(gk), dim3(256), 0, stream, Xs, rows, rp, Pk);          \
   hipLaunchKernelGGL(k_planes_r<HFV>, dim3(gr), dim3(256), 0, stream, Xs, rows, rp, Pr)

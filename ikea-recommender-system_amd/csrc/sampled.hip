@@ -386,10 +386,10 @@ __global__ __launch_bounds__(sf_thr(HF)) void k_sampled_logits(const float* __re
     for (int q = 0; q < IPT; ++q) {
       const int i = tid + SF_THR * q;
       if (i < ITEMS) {
-        const int g = i >> 5;
+        const int g = i >> 5, row = i & 31;
         bf16x8 p0, p1, p2;
         split3x8(src[q][0], src[q][1], p0, p1, p2);
-        const int e = (g >> 1) * 192 + (g & 1) * 32 + (i & 31);
+        const int e = ((g >> 2) * 2 + (row >> 4)) * 192 + 16 * (g & 3) + (row & 15);   // K-planes (common.h)
         hs[e] = p0;
         hs[e + 64] = p1;
         hs[e + 128] = p2;
@@ -462,14 +462,18 @@ __global__ __launch_bounds__(sf_thr(HF)) void k_sampled_logits(const float* __re
   }
   float* __restrict__ pm = pmax + (int64_t)(s0 / 32) * B + rbase + l32;
   float* __restrict__ ps = psum + (int64_t)(s0 / 32) * B + rbase + l32;
+  // B fragment of 16-deep slice j (lane (hh, n): row n, k = 16j + 8hh .. +8)
+  // inside a chunk's K-planes (common.h: [k32 slice][16-row tile][plane][16·kg + n])
+  auto boff = [&](int j) __attribute__((always_inline)) {
+    return ((j >> 1) * 2 + (l32 >> 4)) * 192 + 16 * (2 * (j & 1) + hh) + (l32 & 15);
+  };
   bf16x8 a0[NS], a1[NS], a2[NS];
   // chunk 0: each A slice is split right before its MFMAs
   f16v accA = {}, accB = {};
 #pragma unroll
   for (int j = 0; j < NS; ++j) {
     split3x8(wr[j][0], wr[j][1], a0[j], a1[j], a2[j]);
-    accA = mfma_split<NT>(a0[j], a1[j], a2[j], hsA[j * 192 + lane], hsA[j * 192 + 64 + lane],
-                          hsA[j * 192 + 128 + lane], accA);
+    accA = mfma_split<NT>(a0[j], a1[j], a2[j], hsA[boff(j)], hsA[boff(j) + 64], hsA[boff(j) + 128], accA);
   }
   // row tile 0 publishes the draw and the gathered rows (the backward's Wg / bg)
   if (emit && nact) {
@@ -490,8 +494,7 @@ __global__ __launch_bounds__(sf_thr(HF)) void k_sampled_logits(const float* __re
     acc = f16v{};
 #pragma unroll
     for (int j = 0; j < NS; ++j)
-      acc = mfma_split<NT>(a0[j], a1[j], a2[j], hs[j * 192 + lane], hs[j * 192 + 64 + lane], hs[j * 192 + 128 + lane],
-                           acc);
+      acc = mfma_split<NT>(a0[j], a1[j], a2[j], hs[boff(j)], hs[boff(j) + 64], hs[boff(j) + 128], acc);
   };
   // epilogue of chunk c: lane (hh, n) holds row rbase + 32c + n, negatives
   // s0 + acc32_row(r, hh): four runs of 4 consecutive negatives
