@@ -753,16 +753,19 @@ __global__ __launch_bounds__(64 * fl_nw(HF, 2)) void k_flash_dw(
   }
 #undef FL_ISSUE_K
 #undef FL_ISSUE_R
-  // Adam epilogue; with Wk_out / Wr_out (Adam mode) the updated rows also
-  // leave as the next pass 1's operand planes: the two item tiles of a
-  // feature block already are an R-plane entry (items kperm16(kg, e)), the
-  // K-planes go through a per-wave LDS transpose (32 items × 32 columns at a
-  // time, rows padded to 33 floats)
+  // Epilogue, 32 feature columns (two feature blocks) at a time through a
+  // per-wave LDS tile (32 items × 32 columns, rows padded to 36 floats): the
+  // raw dW tile goes in, every lane then takes four (item, 4-column) pieces —
+  // 16-B loads / stores of W, mW, vW (or dW_out), eight 128-B row segments
+  // per instruction — and writes the updated values back; with Wk_out /
+  // Wr_out (Adam mode) the updated rows also leave as the next pass 1's
+  // operand planes, read from the tile (R-planes: items kperm16(kg, e) of a
+  // column; K-planes: 8 consecutive columns of an item)
   // (the ring arrays are idle after the main loop's last barrier; HF 32's are
   // too small, so it has its own)
-  constexpr int TRP = 33, TRW = 32 * TRP;         // floats per wave
+  constexpr int TRP = 36, TRW = 32 * TRP;         // floats per wave (16-B aligned rows)
   constexpr int WPA = EK * 16 / (TRW * 4);        // waves per ring array
-  __shared__ float trd[HF == 32 ? NW * TRW : 1];
+  __shared__ __attribute__((aligned(16))) float trd[HF == 32 ? NW * TRW : 4];
   float* tr;
   if (HF == 32) {
     tr = trd + w * TRW;
@@ -812,53 +815,68 @@ __global__ __launch_bounds__(64 * fl_nw(HF, 2)) void k_flash_dw(
     }
   }
   const int64_t blk32 = j0 >> 5;
+  const int c4 = lane & 7;
 #pragma unroll
   for (int s = 0; s < NS; ++s) {
 #pragma unroll
-    for (int f2 = 0; f2 < 2; ++f2) {
-      const int fb = 2 * s + f2, col = 16 * fb + l16;
+    for (int f2 = 0; f2 < 2; ++f2)
 #pragma unroll
       for (int ib = 0; ib < 2; ++ib)
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int it = j0 + 16 * ib + 4 * kg + i;
-          if (it >= A) {
-            dw[ib][fb][i] = 0.f;   // rows past A: zero planes, as rg_head_planes writes them
-            continue;
+        for (int i = 0; i < 4; ++i) tr[(16 * ib + 4 * kg + i) * TRP + 16 * f2 + l16] = dw[ib][2 * s + f2][i];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int ii = (lane >> 3) + 8 * q, it = j0 + ii;
+      f4* tp = reinterpret_cast<f4*>(tr + ii * TRP + 4 * c4);
+      f4 gv = *tp;
+      if (it < A) {
+        const int64_t o = (int64_t)it * HF + 32 * s + 4 * c4;
+        if (dW_out) {
+          *reinterpret_cast<f4*>(dW_out + o) = gv;
+        } else {
+          f4 pw = *reinterpret_cast<const f4*>(W + o), mq = *reinterpret_cast<const f4*>(mW + o),
+             v = *reinterpret_cast<const f4*>(vW + o);
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            float pu = pw[u], mu = mq[u], vu = v[u];
+            adam_elem(pu, mu, vu, gv[u], args);
+            pw[u] = pu;
+            mq[u] = mu;
+            v[u] = vu;
           }
-          const int64_t o = (int64_t)it * HF + col;
-          if (dW_out) {
-            dW_out[o] = dw[ib][fb][i];
-          } else {
-            float p = W[o], mq = mW[o], v = vW[o];
-            adam_elem(p, mq, v, dw[ib][fb][i], args);
-            W[o] = p;
-            mW[o] = mq;
-            vW[o] = v;
-            dw[ib][fb][i] = p;
-          }
+          *reinterpret_cast<f4*>(W + o) = pw;
+          *reinterpret_cast<f4*>(mW + o) = mq;
+          *reinterpret_cast<f4*>(vW + o) = v;
+          gv = pw;
         }
-      if (planes) {
+      } else {
+        gv = f4{0.f, 0.f, 0.f, 0.f};   // rows past A: zero planes, as rg_head_planes writes them
+      }
+      if (planes) *tp = gv;
+    }
+    if (planes) {
+#pragma unroll
+      for (int f2 = 0; f2 < 2; ++f2) {
+        f4 lo, hi;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float x = tr[kperm16(kg, e) * TRP + 16 * f2 + l16];
+          if (e < 4) lo[e] = x; else hi[e - 4] = x;
+        }
         bf16x8 p0, p1, p2;
-        split3x8(dw[0][fb], dw[1][fb], p0, p1, p2);
-        bf16x8* dst = Wr_out + (blk32 * NF + fb) * 192 + lane;
+        split3x8(lo, hi, p0, p1, p2);
+        bf16x8* dst = Wr_out + (blk32 * NF + 2 * s + f2) * 192 + lane;
         dst[0] = p0;
         dst[64] = p1;
         dst[128] = p2;
-#pragma unroll
-        for (int ib = 0; ib < 2; ++ib)
-#pragma unroll
-          for (int i = 0; i < 4; ++i) tr[(16 * ib + 4 * kg + i) * TRP + 16 * f2 + l16] = dw[ib][fb][i];
       }
-    }
-    if (planes) {
       // (item, 8-column group) entries of columns 32s .. 32s + 31: 32 items × 4 groups
 #pragma unroll
       for (int q = 0; q < 2; ++q) {
         const int e = lane + 64 * q, ii = e & 31, grp = e >> 5;
-        const float* src = tr + ii * TRP + 8 * grp;
+        const f4* src = reinterpret_cast<const f4*>(tr + ii * TRP + 8 * grp);
         bf16x8 p0, p1, p2;
-        split3x8(f4{src[0], src[1], src[2], src[3]}, f4{src[4], src[5], src[6], src[7]}, p0, p1, p2);
+        split3x8(src[0], src[1], p0, p1, p2);
         bf16x8* dst = Wk_out + ((blk32 * NS + s) * 2 + (ii >> 4)) * 192 + 16 * grp + (ii & 15);
         dst[0] = p0;
         dst[64] = p1;
