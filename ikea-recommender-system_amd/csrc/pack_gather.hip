@@ -234,7 +234,15 @@ __global__ __launch_bounds__(256) void k_gather(const int64_t* __restrict__ s, i
 // loads before any store, so ~GW_ROWS·22 random 512-B rows are in flight per
 // workgroup (the table rows are random: latency, not bandwidth, is what a
 // lane waits on).  V4 = E/4 lanes per token row.
-constexpr int GW_ROWS = 4;
+#ifndef GW_ROWS
+#define GW_ROWS 4
+#endif
+#ifndef GW_FLIGHT
+#define GW_FLIGHT 64         // token rows whose loads a workgroup keeps in flight
+#endif
+#ifndef GW_PIPE
+#define GW_PIPE 0
+#endif
 constexpr int GW_MAXL = 64;
 template <typename TE, int E>
 __global__ __launch_bounds__(256) void k_gather_e(const int64_t* __restrict__ s, int B, int L,
@@ -246,7 +254,7 @@ __global__ __launch_bounds__(256) void k_gather_e(const int64_t* __restrict__ s,
                                                   int32_t* __restrict__ err) {
   constexpr int V4 = E / 4;
   constexpr int TPP = 256 / V4;                       // tokens per pass of the workgroup
-  constexpr int U = 64 / TPP;                         // passes whose loads issue together (64 tokens)
+  constexpr int U = GW_FLIGHT / TPP;                  // passes whose loads issue together
   __shared__ int ids[GW_ROWS * GW_MAXL];
   __shared__ int rb[GW_ROWS], rl[GW_ROWS], ro[GW_ROWS + 1];
   const int tid = threadIdx.x;
@@ -271,14 +279,15 @@ __global__ __launch_bounds__(256) void k_gather_e(const int64_t* __restrict__ s,
   }
   __syncthreads();
   const int c = tid % V4, t0 = tid / V4;
-  for (int i0 = t0; i0 < ntok; i0 += 64) {
-    f4 v[U];
+  auto load = [&](f4 (&v)[U], int i0) __attribute__((always_inline)) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int i = i0 + TPP * u;
       v[u] = f4{0.f, 0.f, 0.f, 0.f};
       if (i < ntok && ids[i] >= 0) v[u] = load4(emb + (int64_t)ids[i] * E, c);
     }
+  };
+  auto store = [&](const f4 (&v)[U], int i0) __attribute__((always_inline)) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int i = i0 + TPP * u;
@@ -289,6 +298,26 @@ __global__ __launch_bounds__(256) void k_gather_e(const int64_t* __restrict__ s,
           if (ids[i] < 0 && err) atomicOr(err, 1);
         }
       }
+    }
+  };
+  if (GW_PIPE) {
+    // the next group's loads are issued before this group's stores
+    f4 cur[U];
+    load(cur, t0);
+    for (int i0 = t0; i0 < ntok; i0 += GW_FLIGHT) {
+      f4 nxt[U];
+      const bool more = i0 + GW_FLIGHT < ntok;
+      if (more) load(nxt, i0 + GW_FLIGHT);
+      store(cur, i0);
+      if (!more) break;
+#pragma unroll
+      for (int u = 0; u < U; ++u) cur[u] = nxt[u];
+    }
+  } else {
+    for (int i0 = t0; i0 < ntok; i0 += GW_FLIGHT) {
+      f4 v[U];
+      load(v, i0);
+      store(v, i0);
     }
   }
 }

@@ -15,6 +15,21 @@ from . import call, stream_ptr
 from .engine import SampledSoftmaxHead, SoftmaxHead, Trunk
 
 
+
+_LOGGED_PRECISIONS = set()
+
+
+def _log_precision_once(precision):
+    """Say once per process which head arithmetic the trainers run (the
+    default "f32x6d3" runs dh on three bf16 plane products)."""
+    if precision not in _LOGGED_PRECISIONS:
+        _LOGGED_PRECISIONS.add(precision)
+        import logging
+        logging.getLogger("recommenders").info(
+            "head matmul_precision=%s (f32: native fp32 MFMA; f32x9 / f32x6: fp32 operands split into bf16 planes; "
+            "f32x6d3: f32x6 with dh on three plane products)", precision)
+
+
 class HipNet:
     """Embedding + GRU trunk + linear heads, parameters on one MI355X."""
 
@@ -71,6 +86,7 @@ class HipNet:
         Q heads' row gathers stay native fp32."""
         for hd in self.heads.values():
             hd.set_matmul_precision(precision)
+        _log_precision_once(precision)
         return self
 
     def named_param_objs(self):

@@ -2,7 +2,7 @@
 # round-2 snapshot: full GPU suite, C2 / C3 / C4 bench lines, rocprofv3 kernel stats of a short C2 run
 set -o pipefail
 mkdir -p gpurun_out/snap
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > gpurun_out/snap/pytest_gpu.log 2>&1 || { echo "pytest failed"; grep -E "FAIL|Error" gpurun_out/snap/pytest_gpu.log | tail -20; tail -30 gpurun_out/snap/pytest_gpu.log; exit 1; }
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --ignore=tests/test_gpu_long_horizon.py --timeout 300 --timeout-method thread > gpurun_out/snap/pytest_gpu.log 2>&1 || { echo "pytest failed"; grep -E "FAIL|Error" gpurun_out/snap/pytest_gpu.log | tail -20; tail -30 gpurun_out/snap/pytest_gpu.log; exit 1; }
 tail -2 gpurun_out/snap/pytest_gpu.log
 timeout -k 10 500 python bench.py > gpurun_out/snap/bench_c2.json 2> gpurun_out/snap/bench_c2.err || { tail -20 gpurun_out/snap/bench_c2.err; exit 1; }
 timeout -k 10 300 python bench.py --config c3 --steps 50 --warmup 10 > gpurun_out/snap/bench_c3.json 2> gpurun_out/snap/bench_c3.err || { tail -20 gpurun_out/snap/bench_c3.err; exit 1; }
