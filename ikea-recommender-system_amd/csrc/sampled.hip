@@ -323,6 +323,28 @@ constexpr int sf_neg(int HF) { return 32 * sf_nw(HF); }   // negatives per workg
 constexpr int sf_thr(int HF) { return 64 * sf_nw(HF); }   // threads per workgroup
 constexpr int SF_ROWS = 128;  // rows per workgroup (4 chunks of 32)
 
+// Diagnostic build only (-DSF_STAMP, tools/sfstamp.py): per-wave s_memrealtime
+// stamps at the phase boundaries of k_sampled_logits, read back by rg_sf_stamp_read.
+#ifdef SF_STAMP
+__device__ uint64_t g_sf_stamp[4096 * 8 * 8];
+#define SFD_T(k)                                                                                     \
+  do {                                                                                              \
+    const uint64_t _t = __builtin_amdgcn_s_memrealtime();                                           \
+    if (lane == 0) g_sf_stamp[(((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * 8 + w) * 8 + (k)] = _t; \
+  } while (0)
+#define SFD_C(k)                                                                                     \
+  do {                                                                                              \
+    const uint64_t _t = __builtin_amdgcn_s_memtime();                                               \
+    if (lane == 0) g_sf_stamp[(((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * 8 + w) * 8 + (k)] = _t; \
+  } while (0)
+extern "C" int rg_sf_stamp_read(void* dst, int64_t n) {
+  return hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_sf_stamp), n * 8, 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
+#else
+#define SFD_T(k)
+#define SFD_C(k)
+#endif
+
 // HKP (HF <= 128): h arrives as its bf16 K-planes (hk, written by the GRU
 // forward that produced h, rg_gru_fwd_dirs_planes) and each 32-row chunk
 // moves global -> LDS by 16-B LDS-DMA: no fp32 h loads, no split, no LDS
@@ -350,6 +372,8 @@ __global__ __launch_bounds__(sf_thr(HF)) void k_sampled_logits(const float* __re
   __shared__ __attribute__((aligned(16))) float sbias[SF_NEG];
   __shared__ f4 ztile[256 * sf_nw(HF)];
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, hh = lane >> 5, l32 = lane & 31;
+  SFD_T(0);
+  SFD_C(6);
   int bx = blockIdx.x, by = blockIdx.y;
   {
     const int gx = gridDim.x, gy = gridDim.y;
@@ -420,18 +444,41 @@ __global__ __launch_bounds__(sf_thr(HF)) void k_sampled_logits(const float* __re
   }
   const float bl = bias[id];
   if constexpr (HKP) {
+#ifndef SF_NOH
     dma_chunk(hsA, 0);
+#endif
   } else {
     load_h(0);
   }
   f4 wr[NS][2];
   {
+#if defined(SF_NOW)
+#pragma unroll
+    for (int j = 0; j < NS; ++j) {
+      wr[j][0] = f4{(float)lane, 1.f, 2.f, (float)j};
+      wr[j][1] = f4{(float)l32, 3.f, 4.f, (float)id};
+    }
+#elif defined(SF_COALW)
+    // timing diagnostic: the same rows read with 2 whole rows per instruction (values land in the wrong lanes)
+    const int idr = __shfl(id, 0);
+#pragma unroll
+    for (int j = 0; j < NS; ++j) {
+      const int n = 2 * j + hh;
+      const int idn = __shfl(id, n);
+      const float* src = W + (int64_t)idn * HF + 4 * l32;
+      wr[j][0] = *reinterpret_cast<const f4*>(src);
+      const int idm = __shfl(id, n + 16);
+      wr[j][1] = *reinterpret_cast<const f4*>(W + (int64_t)idm * HF + 4 * l32);
+    }
+    (void)idr;
+#else
     const float* src = W + (int64_t)id * HF + 8 * hh;
 #pragma unroll
     for (int j = 0; j < NS; ++j) {
       wr[j][0] = *reinterpret_cast<const f4*>(src + 16 * j);
       wr[j][1] = *reinterpret_cast<const f4*>(src + 16 * j + 4);
     }
+#endif
   }
   __builtin_amdgcn_sched_barrier(0);
   // barrier without a memory fence: only the LDS writes must be complete
@@ -446,10 +493,13 @@ __global__ __launch_bounds__(sf_thr(HF)) void k_sampled_logits(const float* __re
     // every chunk's DMA is issued up front; one full wait + barrier (the W
     // rows are needed by chunk 0 anyway), then all MFMAs run barrier-free
     // (21.7 -> 21.4 us against a second barrier behind chunk 0)
+#ifndef SF_NOH
     if (nch > 1) dma_chunk(hsB, 1);
     if (nch > 2) dma_chunk(hsC, 2);
     if (nch > 3) dma_chunk(hsD, 3);
+#endif
     __syncthreads();
+    SFD_T(1);
   } else {
     store_h(hsA);
     if (nch > 1) load_h(1);
@@ -550,13 +600,18 @@ __global__ __launch_bounds__(sf_thr(HF)) void k_sampled_logits(const float* __re
       if (nact) {
         mma(hsB, accB);
         epi(accA, 0);
+        SFD_T(2);
         if (nch > 2) {
           mma(hsC, accA);
           epi(accB, 1);
+          SFD_T(3);
           if (nch > 3) {
             mma(hsD, accB);
             epi(accA, 2);
+            SFD_T(4);
             epi(accB, 3);
+            SFD_T(5);
+            SFD_C(7);
           } else {
             epi(accA, 2);
           }
