@@ -140,6 +140,39 @@ __device__ __forceinline__ void split3x8(const f4& lo, const f4& hi, bf16x8& p0,
   }
 }
 
+// ---- sampled negatives (csrc/sampled.hip, csrc/pack_gather.hip) ----
+// Counter-based uniform draw: negative s of draw `counter` is the high 64 bits
+// of splitmix64(seed + φ·(counter·S + s + 1))·A — reproducible on the host.
+__device__ __forceinline__ uint64_t mix64(uint64_t z) {
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+__device__ __forceinline__ int32_t draw_id(uint64_t seed, uint64_t counter, int S, int s, uint64_t A) {
+  return (int32_t)__umul64hi(mix64(seed + 0x9E3779B97F4A7C15ull * (counter * (uint64_t)S + (uint64_t)s + 1ull)), A);
+}
+// Fragment-order plane buffer of 32-row blocks (the A operand of the sampled
+// logits' v_mfma_f32_32x32x16_bf16): entry (block, 16-deep slice j, plane p,
+// lane), lane (hh, n) = row n, k = 16j + 8hh .. +8, one 16-B bf16x8 each.
+__device__ __forceinline__ int64_t plane_idx(int blk, int j, int p, int lane, int NS) {
+  return (((int64_t)blk * NS + j) * 3 + p) * 64 + lane;
+}
+// The negatives' row gather of a sampled step, done by extra workgroups of the
+// embedding-gather launch (rg_gather_neg): ids, biases, fp32 rows (the
+// backward's operands) and the rows' bf16 planes in fragment order (the
+// logits' A operand, so rg_sampled_logits reads them as whole 1 KB
+// wave-instructions instead of gathering 512-B rows itself).
+struct NegPrep {
+  const float* W;
+  const float* bias;
+  int32_t* ids;
+  float* Wg;
+  float* bg;
+  bf16x8* Wp;
+  uint64_t seed, counter, A;
+  int S, HF, nwg;
+};
+
 // acc += Σ_terms a_p · b_q over one 16-wide k slice (NT = 9, 6 or 3 terms),
 // smallest terms first.  NT = 3 keeps a0·b0, a0·b1, a1·b0 (dropped terms
 // ≤ 3·2^-18·|ab|); only the fused head's O = P·W contraction (→ dh) uses it

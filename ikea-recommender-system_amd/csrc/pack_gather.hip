@@ -231,19 +231,49 @@ __global__ __launch_bounds__(256) void k_gather(const int64_t* __restrict__ s, i
 // packed range [offs[r0], offs[r0 + GW_ROWS]).  Three dependent memory steps
 // per workgroup: the rows' (perm, length, offset), their item ids (into LDS),
 // then every table row of the range — a lane issues all of its (up to U) row
-// loads before any store, so ~GW_ROWS·22 random 512-B rows are in flight per
-// workgroup (the table rows are random: latency, not bandwidth, is what a
-// lane waits on).  V4 = E/4 lanes per token row.
-#ifndef GW_ROWS
-#define GW_ROWS 4
-#endif
-#ifndef GW_FLIGHT
-#define GW_FLIGHT 64         // token rows whose loads a workgroup keeps in flight
-#endif
-#ifndef GW_PIPE
-#define GW_PIPE 0
-#endif
+// loads before any store, so up to GW_FLIGHT random 512-B rows are in flight
+// per workgroup (the table rows are random: latency, not bandwidth, is what a
+// lane waits on; 128 in flight measured 0.3 µs faster than 64 at C2, the next
+// group's loads issued under this group's stores no faster).  V4 = E/4 lanes
+// per token row.
+//
+// Sampled steps (rg_gather_neg) put the negatives' row gather in the same
+// launch: the first np.nwg workgroups draw the S negatives and write their
+// ids, biases, fp32 rows and fragment-order bf16 planes (common.h NegPrep)
+// while the rest gather the embedding rows.
+constexpr int GW_ROWS = 4;
+constexpr int GW_FLIGHT = 128;
 constexpr int GW_MAXL = 64;
+
+// one thread per (negative, 8-value group): a wave covers 32 negatives × 2
+// groups = one 16-deep slice, so each of its three plane stores is one
+// contiguous 1 KB fragment (S % 32 == 0)
+__device__ __forceinline__ void neg_prep(const NegPrep& np, int bid) {
+  const int G = np.HF >> 3, NS = np.HF >> 4;
+  const int64_t i = (int64_t)bid * 256 + threadIdx.x;
+  if (i >= (int64_t)np.S * G) return;
+  const int blk = (int)(i / (32 * G));
+  const int rem = (int)(i - (int64_t)blk * 32 * G);
+  const int x = blk * 32 + (rem & 31), g = rem >> 5;
+  const int id = draw_id(np.seed, np.counter, np.S, x, np.A);
+  const float* src = np.W + (int64_t)id * np.HF + 8 * g;
+  const f4 lo = *reinterpret_cast<const f4*>(src);
+  const f4 hi = *reinterpret_cast<const f4*>(src + 4);
+  float* dst = np.Wg + (int64_t)x * np.HF + 8 * g;
+  *reinterpret_cast<f4*>(dst) = lo;
+  *reinterpret_cast<f4*>(dst + 4) = hi;
+  bf16x8 p0, p1, p2;
+  split3x8(lo, hi, p0, p1, p2);
+  const int lane = (g & 1) * 32 + (x & 31);
+  np.Wp[plane_idx(blk, g >> 1, 0, lane, NS)] = p0;
+  np.Wp[plane_idx(blk, g >> 1, 1, lane, NS)] = p1;
+  np.Wp[plane_idx(blk, g >> 1, 2, lane, NS)] = p2;
+  if (g == 0) {
+    np.ids[x] = id;
+    np.bg[x] = np.bias[id];
+  }
+}
+
 template <typename TE, int E>
 __global__ __launch_bounds__(256) void k_gather_e(const int64_t* __restrict__ s, int B, int L,
                                                   const int32_t* __restrict__ perm,
@@ -251,14 +281,18 @@ __global__ __launch_bounds__(256) void k_gather_e(const int64_t* __restrict__ s,
                                                   const int32_t* __restrict__ offs,
                                                   const TE* __restrict__ emb, int64_t n_rows, int reverse,
                                                   int32_t* __restrict__ tok_id, float* __restrict__ X,
-                                                  int32_t* __restrict__ err) {
+                                                  int32_t* __restrict__ err, NegPrep np) {
   constexpr int V4 = E / 4;
   constexpr int TPP = 256 / V4;                       // tokens per pass of the workgroup
   constexpr int U = GW_FLIGHT / TPP;                  // passes whose loads issue together
   __shared__ int ids[GW_ROWS * GW_MAXL];
   __shared__ int rb[GW_ROWS], rl[GW_ROWS], ro[GW_ROWS + 1];
+  if ((int)blockIdx.x < np.nwg) {
+    neg_prep(np, blockIdx.x);
+    return;
+  }
   const int tid = threadIdx.x;
-  const int r0 = blockIdx.x * GW_ROWS;
+  const int r0 = ((int)blockIdx.x - np.nwg) * GW_ROWS;
   const int nr = min(GW_ROWS, B - r0);
   if (tid < nr) {
     rb[tid] = perm[r0 + tid];
@@ -279,15 +313,14 @@ __global__ __launch_bounds__(256) void k_gather_e(const int64_t* __restrict__ s,
   }
   __syncthreads();
   const int c = tid % V4, t0 = tid / V4;
-  auto load = [&](f4 (&v)[U], int i0) __attribute__((always_inline)) {
+  for (int i0 = t0; i0 < ntok; i0 += GW_FLIGHT) {
+    f4 v[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int i = i0 + TPP * u;
       v[u] = f4{0.f, 0.f, 0.f, 0.f};
       if (i < ntok && ids[i] >= 0) v[u] = load4(emb + (int64_t)ids[i] * E, c);
     }
-  };
-  auto store = [&](const f4 (&v)[U], int i0) __attribute__((always_inline)) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int i = i0 + TPP * u;
@@ -299,37 +332,18 @@ __global__ __launch_bounds__(256) void k_gather_e(const int64_t* __restrict__ s,
         }
       }
     }
-  };
-  if (GW_PIPE) {
-    // the next group's loads are issued before this group's stores
-    f4 cur[U];
-    load(cur, t0);
-    for (int i0 = t0; i0 < ntok; i0 += GW_FLIGHT) {
-      f4 nxt[U];
-      const bool more = i0 + GW_FLIGHT < ntok;
-      if (more) load(nxt, i0 + GW_FLIGHT);
-      store(cur, i0);
-      if (!more) break;
-#pragma unroll
-      for (int u = 0; u < U; ++u) cur[u] = nxt[u];
-    }
-  } else {
-    for (int i0 = t0; i0 < ntok; i0 += GW_FLIGHT) {
-      f4 v[U];
-      load(v, i0);
-      store(v, i0);
-    }
   }
 }
 
 template <typename TE>
 static bool launch_gather_e(const int64_t* s, int B, int L, const int32_t* perm, const int32_t* lsort,
                             const int32_t* offs, const TE* emb, int64_t n_rows, int E, int reverse,
-                            int32_t* tok_id, float* X, int32_t* err, hipStream_t stream) {
+                            int32_t* tok_id, float* X, int32_t* err, const NegPrep& np, hipStream_t stream) {
   if (L > GW_MAXL) return false;
+  const dim3 grid((unsigned)(np.nwg + (B + GW_ROWS - 1) / GW_ROWS));
 #define GE(EV)                                                                                              \
-  RG_TLAUNCH((k_gather_e<TE, EV>), dim3((B + GW_ROWS - 1) / GW_ROWS), dim3(256), 0, stream, s, B, L, perm, lsort, \
-             offs, emb, n_rows, reverse, tok_id, X, err)
+  RG_TLAUNCH((k_gather_e<TE, EV>), grid, dim3(256), 0, stream, s, B, L, perm, lsort, offs, emb, n_rows,       \
+             reverse, tok_id, X, err, np)
   switch (E) {
     case 32: GE(32); return true;
     case 64: GE(64); return true;
@@ -344,7 +358,7 @@ extern "C" int rg_gather(const int64_t* s, int B, int L, const int32_t* perm, co
                          const int32_t* offs, const float* emb, int64_t n_rows, int E, int reverse,
                          int32_t* tok_id, float* X, int32_t* err, hipStream_t stream) {
   if (B <= 0 || (E & 3)) return RG_ERR_ARG;
-  if (launch_gather_e(s, B, L, perm, lsort, offs, emb, n_rows, E, reverse, tok_id, X, err, stream)) {
+  if (launch_gather_e(s, B, L, perm, lsort, offs, emb, n_rows, E, reverse, tok_id, X, err, NegPrep{}, stream)) {
     RG_LAUNCH_CHECK();
     return RG_OK;
   }
@@ -361,12 +375,39 @@ extern "C" int rg_gather_h(const int64_t* s, int B, int L, const int32_t* perm, 
                            int32_t* tok_id, float* X, int32_t* err, hipStream_t stream) {
   if (B <= 0 || (E & 3)) return RG_ERR_ARG;
   if (launch_gather_e(s, B, L, perm, lsort, offs, reinterpret_cast<const __half*>(emb16), n_rows, E, reverse, tok_id,
-                      X, err, stream)) {
+                      X, err, NegPrep{}, stream)) {
     RG_LAUNCH_CHECK();
     return RG_OK;
   }
   hipLaunchKernelGGL(k_gather<__half>, dim3(B), dim3(256), 0, stream, s, L, perm, lsort, offs,
                      reinterpret_cast<const __half*>(emb16), n_rows, E, reverse, tok_id, X, err);
+  RG_LAUNCH_CHECK();
+  return RG_OK;
+}
+
+// The embedding gather of a sampled step with the negatives' row gather in the
+// same launch (common.h NegPrep): draw `counter` of the counter-based stream
+// (seed, S, A) -> ids[S], bg[S] = bias[ids], Wg[S][HF] = W[ids] and the rows'
+// bf16 planes Wp (S·HF·6 bytes, fragment order) that rg_sampled_logits reads
+// with draw = 2.  emb16 != 0: the table is fp16 (rg_gather_h).  Needs the
+// compile-time gather (E ∈ {32, 64, 128, 256}, L <= 64), S % 32 == 0,
+// HF ∈ {32, 64, 128, 256}.
+extern "C" int rg_gather_neg(const int64_t* s, int B, int L, const int32_t* perm, const int32_t* lsort,
+                             const int32_t* offs, const void* emb, int emb16, int64_t n_rows, int E, int reverse,
+                             int32_t* tok_id, float* X, int32_t* err, const float* W, const float* bias,
+                             uint64_t seed, uint64_t counter, int64_t A, int S, int HF, int32_t* ids, float* Wg,
+                             float* bg, void* Wp, hipStream_t stream) {
+  if (B <= 0 || (E & 3) || L > GW_MAXL || !W || !bias || !ids || !Wg || !bg || !Wp) return RG_ERR_ARG;
+  if (S <= 0 || S % 32 || A <= 0 || A > INT32_MAX) return RG_ERR_ARG;
+  if (E != 32 && E != 64 && E != 128 && E != 256) return RG_ERR_SHAPE;
+  if (HF != 32 && HF != 64 && HF != 128 && HF != 256) return RG_ERR_SHAPE;
+  NegPrep np{W, bias, ids, Wg, bg, reinterpret_cast<bf16x8*>(Wp), seed, counter, (uint64_t)A, S, HF,
+             (int)(((int64_t)S * (HF / 8) + 255) / 256)};
+  const bool ok = emb16 ? launch_gather_e(s, B, L, perm, lsort, offs, reinterpret_cast<const __half*>(emb), n_rows,
+                                          E, reverse, tok_id, X, err, np, stream)
+                        : launch_gather_e(s, B, L, perm, lsort, offs, reinterpret_cast<const float*>(emb), n_rows,
+                                          E, reverse, tok_id, X, err, np, stream);
+  if (!ok) return RG_ERR_SHAPE;
   RG_LAUNCH_CHECK();
   return RG_OK;
 }

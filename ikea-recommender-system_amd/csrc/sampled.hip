@@ -34,12 +34,6 @@
 #define SF_KC 32
 #define SF_LD (SF_KC + 4)
 
-__device__ __forceinline__ uint64_t mix64(uint64_t z) {
-  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-  return z ^ (z >> 31);
-}
-
 __global__ void k_sample_uniform(uint64_t seed, uint64_t counter, int S, uint64_t A, int32_t* __restrict__ out) {
   const int s = blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= S) return;
@@ -216,10 +210,7 @@ __global__ __launch_bounds__(256) void k_sampled_fwd(const float* __restrict__ h
 //    and the (max, Σexp) partials in the epilogue; the rows are split over
 //    grid.y so S/(32·waves) negative groups still fill the chip.
 
-// fragment-order plane buffer: entry (block, slice j, plane p, lane)
-__device__ __forceinline__ int64_t plane_idx(int blk, int j, int p, int lane, int NS) {
-  return (((int64_t)blk * NS + j) * 3 + p) * 64 + lane;
-}
+// fragment-order plane buffer: common.h plane_idx
 
 template <int HF>
 __global__ __launch_bounds__(256) void k_sampled_prep(const float* __restrict__ h, const float* __restrict__ W,
@@ -349,13 +340,14 @@ extern "C" int rg_sf_stamp_read(void* dst, int64_t n) {
 // forward that produced h, rg_gru_fwd_dirs_planes) and each 32-row chunk
 // moves global -> LDS by 16-B LDS-DMA: no fp32 h loads, no split, no LDS
 // stores in this kernel.
-template <int HF, int NT, bool DRAW, bool HKP>
+template <int HF, int NT, bool DRAW, bool HKP, bool PRE>
 __global__ __launch_bounds__(sf_thr(HF)) void k_sampled_logits(const float* __restrict__ h, const float* __restrict__ W,
                                                         const float* __restrict__ bias, int32_t* __restrict__ neg,
                                                         uint64_t seed, uint64_t counter, uint64_t A, int B, int S,
                                                         float* __restrict__ Z, int64_t ldz, float* __restrict__ pmax,
                                                         float* __restrict__ psum, float* __restrict__ Wg,
-                                                        float* __restrict__ bg, const bf16x8* __restrict__ hk) {
+                                                        float* __restrict__ bg, const bf16x8* __restrict__ hk,
+                                                        const bf16x8* __restrict__ wp) {
   constexpr int NS = HF / 16;
   constexpr int CH = NS * 192;              // 16-B fragments of one 32-row chunk's planes
   constexpr int ITEMS = 32 * (HF / 8);      // (row, 8-value group) items of one chunk
@@ -433,52 +425,41 @@ __global__ __launch_bounds__(sf_thr(HF)) void k_sampled_logits(const float* __re
   // ---- this wave's negatives: draw, bias, fp32 rows in A-fragment layout.
   // Vector-memory issue order: bias, h chunk 0, the W rows, h chunk 1;
   // branch-free (a wave without negatives gathers row 0 and stores nothing).
-  int id;
+  int id = 0;
   const int s_me = nact ? s0 + l32 : 0;
-  if (DRAW) {
-    const uint64_t z = mix64(seed + 0x9E3779B97F4A7C15ull * (counter * (uint64_t)S + (uint64_t)s_me + 1ull));
-    id = nact ? (int32_t)__umul64hi(z, A) : 0;
+  if (PRE) {
+  } else if (DRAW) {
+    id = nact ? draw_id(seed, counter, S, s_me, A) : 0;
   } else {
     id = neg[s_me];
     id = (A > 0 && (uint64_t)(int64_t)id >= A) ? 0 : id;   // guard the gather (callers validate ids)
   }
-  const float bl = bias[id];
+  const float bl = PRE ? bg[s_me] : bias[id];
   if constexpr (HKP) {
-#ifndef SF_NOH
     dma_chunk(hsA, 0);
-#endif
   } else {
     load_h(0);
   }
+  // PRE: the rows' planes were written in fragment order by the gather launch
+  // (rg_gather_neg): 24 whole 1 KB wave-loads, no split here; else the fp32
+  // rows straight into the fragment layout, split per slice below
   f4 wr[NS][2];
-  {
-#if defined(SF_NOW)
+  bf16x8 a0[NS], a1[NS], a2[NS];
+  if constexpr (PRE) {
+    const int blk = (nact ? s0 : 0) >> 5;
 #pragma unroll
     for (int j = 0; j < NS; ++j) {
-      wr[j][0] = f4{(float)lane, 1.f, 2.f, (float)j};
-      wr[j][1] = f4{(float)l32, 3.f, 4.f, (float)id};
+      a0[j] = wp[plane_idx(blk, j, 0, lane, NS)];
+      a1[j] = wp[plane_idx(blk, j, 1, lane, NS)];
+      a2[j] = wp[plane_idx(blk, j, 2, lane, NS)];
     }
-#elif defined(SF_COALW)
-    // timing diagnostic: the same rows read with 2 whole rows per instruction (values land in the wrong lanes)
-    const int idr = __shfl(id, 0);
-#pragma unroll
-    for (int j = 0; j < NS; ++j) {
-      const int n = 2 * j + hh;
-      const int idn = __shfl(id, n);
-      const float* src = W + (int64_t)idn * HF + 4 * l32;
-      wr[j][0] = *reinterpret_cast<const f4*>(src);
-      const int idm = __shfl(id, n + 16);
-      wr[j][1] = *reinterpret_cast<const f4*>(W + (int64_t)idm * HF + 4 * l32);
-    }
-    (void)idr;
-#else
+  } else {
     const float* src = W + (int64_t)id * HF + 8 * hh;
 #pragma unroll
     for (int j = 0; j < NS; ++j) {
       wr[j][0] = *reinterpret_cast<const f4*>(src + 16 * j);
       wr[j][1] = *reinterpret_cast<const f4*>(src + 16 * j + 4);
     }
-#endif
   }
   __builtin_amdgcn_sched_barrier(0);
   // barrier without a memory fence: only the LDS writes must be complete
@@ -492,12 +473,11 @@ __global__ __launch_bounds__(sf_thr(HF)) void k_sampled_logits(const float* __re
     if (hh == 0) sbias[32 * w + l32] = bl;
     // every chunk's DMA is issued up front; one full wait + barrier (the W
     // rows are needed by chunk 0 anyway), then all MFMAs run barrier-free
-    // (21.7 -> 21.4 us against a second barrier behind chunk 0)
-#ifndef SF_NOH
+    // (21.7 -> 21.4 us against a second barrier behind chunk 0; with the
+    // pre-gathered planes the two forms measure the same)
     if (nch > 1) dma_chunk(hsB, 1);
     if (nch > 2) dma_chunk(hsC, 2);
     if (nch > 3) dma_chunk(hsD, 3);
-#endif
     __syncthreads();
     SFD_T(1);
   } else {
@@ -517,16 +497,15 @@ __global__ __launch_bounds__(sf_thr(HF)) void k_sampled_logits(const float* __re
   auto boff = [&](int j) __attribute__((always_inline)) {
     return ((j >> 1) * 2 + (l32 >> 4)) * 192 + 16 * (2 * (j & 1) + hh) + (l32 & 15);
   };
-  bf16x8 a0[NS], a1[NS], a2[NS];
   // chunk 0: each A slice is split right before its MFMAs
   f16v accA = {}, accB = {};
 #pragma unroll
   for (int j = 0; j < NS; ++j) {
-    split3x8(wr[j][0], wr[j][1], a0[j], a1[j], a2[j]);
+    if constexpr (!PRE) split3x8(wr[j][0], wr[j][1], a0[j], a1[j], a2[j]);
     accA = mfma_split<NT>(a0[j], a1[j], a2[j], hsA[boff(j)], hsA[boff(j) + 64], hsA[boff(j) + 128], accA);
   }
   // row tile 0 publishes the draw and the gathered rows (the backward's Wg / bg)
-  if (emit && nact) {
+  if (!PRE && emit && nact) {
     if (hh == 0) {
       if (DRAW) neg[s0 + l32] = id;
       if (bg) bg[s0 + l32] = bl;
@@ -665,28 +644,36 @@ __global__ __launch_bounds__(sf_thr(HF)) void k_sampled_logits(const float* __re
 }
 
 // The fused forward (k_sampled_logits): Z row-major (B × ldz, ldz >= S).
+// draw: 0 = the S ids are given in neg; 1 = draw them (counter-based stream)
+// and publish ids, bg and the rows Wg; 2 = pre-gathered by rg_gather_neg in
+// the step's embedding-gather launch: neg / bg / Wg already hold the ids,
+// biases and rows and w_planes their fragment-order bf16 planes.
 extern "C" int rg_sampled_logits(const float* h, const float* W, const float* bias, int32_t* neg, int draw,
                                  uint64_t seed, uint64_t counter, int64_t A, int B, int S, int HF, int terms,
                                  float* Z, int64_t ldz, float* pmax, float* psum, float* Wg, float* bg,
-                                 const void* h_planes, hipStream_t stream) {
+                                 const void* h_planes, const void* w_planes, hipStream_t stream) {
   if (B <= 0 || S <= 0 || (B % 32) || (S % 32) || !h || !W || !bias || !neg || !Z || !pmax || !psum || !bg)
     return RG_ERR_ARG;
   if (ldz < S || (ldz & 3)) return RG_ERR_ARG;
-  if (draw && (A <= 0 || A > INT32_MAX)) return RG_ERR_ARG;
+  if (draw < 0 || draw > 2 || (draw == 2 && !w_planes)) return RG_ERR_ARG;
+  if (draw == 1 && (A <= 0 || A > INT32_MAX)) return RG_ERR_ARG;
   if (terms != 6 && terms != 9) return RG_ERR_ARG;
   const int neg_wg = sf_neg(HF);
   const dim3 grid((unsigned)((S + neg_wg - 1) / neg_wg), (unsigned)((B + SF_ROWS - 1) / SF_ROWS));
   const bf16x8* hk = (const bf16x8*)h_planes;
-#define SFH(HFV, NTV, DRV, HKV)                                                                                    \
-  RG_TLAUNCH((k_sampled_logits<HFV, NTV, DRV, HKV>), grid, dim3(sf_thr(HFV)), 0, stream, h, W, bias, neg, seed,   \
-             counter, (uint64_t)(A > 0 ? A : 0), B, S, Z, ldz, pmax, psum, Wg, bg, hk)
-#define SFG(HFV, NTV)                                 \
-  if (hk && HFV <= 128) {                             \
-    if (draw) SFH(HFV, NTV, true, (HFV <= 128));      \
-    else SFH(HFV, NTV, false, (HFV <= 128));          \
-  } else {                                            \
-    if (draw) SFH(HFV, NTV, true, false);             \
-    else SFH(HFV, NTV, false, false);                 \
+  const bf16x8* wp = (const bf16x8*)w_planes;
+#define SFH(HFV, NTV, DRV, HKV, PRV)                                                                                  \
+  RG_TLAUNCH((k_sampled_logits<HFV, NTV, DRV, HKV, PRV>), grid, dim3(sf_thr(HFV)), 0, stream, h, W, bias, neg, seed, \
+             counter, (uint64_t)(A > 0 ? A : 0), B, S, Z, ldz, pmax, psum, Wg, bg, hk, wp)
+#define SFG(HFV, NTV)                                     \
+  if (hk && HFV <= 128) {                                 \
+    if (draw == 2) SFH(HFV, NTV, false, (HFV <= 128), true); \
+    else if (draw) SFH(HFV, NTV, true, (HFV <= 128), false); \
+    else SFH(HFV, NTV, false, (HFV <= 128), false);       \
+  } else {                                                \
+    if (draw == 2) SFH(HFV, NTV, false, false, true);     \
+    else if (draw) SFH(HFV, NTV, true, false, false);     \
+    else SFH(HFV, NTV, false, false, false);              \
   }
 #define SFT(HFV)    \
   if (terms == 9) { \

@@ -224,6 +224,7 @@ class Trunk:
         # (rg_gru_fwd_dirs_planes), left in h_planes for the head
         self.emit_planes = False
         self.h_planes = None
+        self.neg_job = None   # set by the sampled step for the next forward (SampledSoftmaxHead.neg_job)
         # fp16 embedding storage (config C5): the gather reads this copy, Adam
         # keeps the fp32 master and refreshes it in the same sweep
         self.emb16 = torch.empty(self.n_local, E, dtype=torch.float16, device=device) if fp16_embeddings else None
@@ -268,14 +269,25 @@ class Trunk:
         if self.comm is not None:
             with region("gather"):
                 self._exchange_rows(w, s, B, L, st, route)
+        # a sampled head's negatives row gather rides in the first gather launch
+        # (rg_gather_neg; SampledSoftmaxHead.neg_job)
+        job, self.neg_job = self.neg_job, None
+        if job is not None and (self.comm is not None or L > 64 or E not in (32, 64, 128, 256)):
+            job = None
         for d in range(self.ndir):
             w_ih, w_hh, b_ih, b_hh = self.dirs[d]
             if self.comm is None:
+                table = (self.emb16 if self.emb16 is not None else self.emb.p).data_ptr()
                 with region("gather", exact=True):
-                    call("rg_gather_h" if self.emb16 is not None else "rg_gather", s.data_ptr(), B, L,
-                         w.perm.data_ptr(), w.lsort.data_ptr(), w.offs.data_ptr(),
-                         (self.emb16 if self.emb16 is not None else self.emb.p).data_ptr(), self.N1, E, d,
-                         w.tok_id[d].data_ptr(), w.X[d].data_ptr(), self.err.data_ptr(), st)
+                    if job is not None and d == 0:
+                        call("rg_gather_neg", s.data_ptr(), B, L, w.perm.data_ptr(), w.lsort.data_ptr(),
+                             w.offs.data_ptr(), table, 1 if self.emb16 is not None else 0, self.N1, E, d,
+                             w.tok_id[d].data_ptr(), w.X[d].data_ptr(), self.err.data_ptr(), *job.args(), st)
+                        job.done()
+                    else:
+                        call("rg_gather_h" if self.emb16 is not None else "rg_gather", s.data_ptr(), B, L,
+                             w.perm.data_ptr(), w.lsort.data_ptr(), w.offs.data_ptr(), table, self.N1, E, d,
+                             w.tok_id[d].data_ptr(), w.X[d].data_ptr(), self.err.data_ptr(), st)
             else:
                 call("rg_place_rows", w.rows_in.data_ptr(), 1 if self.emb16 is not None else 0, w.slot.data_ptr(),
                      w.lsort.data_ptr(), w.offs.data_ptr(), B, E, d, w.X[d].data_ptr(), st)
@@ -1059,6 +1071,8 @@ class _SampledWS:
         self.nrows = torch.full((1,), S + B, dtype=torch.int32, device=device)
         self.Wg = z(S, HF)
         self.bg = z(S)
+        self.Wp = None    # the negatives' bf16 planes from rg_gather_neg (allocated on first use)
+        self.pre_draw = -1   # draw index whose ids / bg / Wg / Wp the gather launch already wrote
         self.work = None  # split-bf16 operand planes (allocated on first use)
         self.dh_splits = max(1, min(8, S // 256))
         self.dw_splits = max(1, min(16, B // 256))
@@ -1112,22 +1126,51 @@ class SampledSoftmaxHead(SoftmaxHead):
             self._sws[slot] = w
         return w
 
+    def neg_job(self, slot, B):
+        """The negatives' row gather of the next forward_loss(slot, B), to run
+        inside the trunk's embedding-gather launch (Trunk.neg_job ->
+        rg_gather_neg): ids, biases, rows and their fragment-order bf16 planes
+        of draw ``self.draws``.  None where the one-launch split logits do not
+        run (native fp32 forward)."""
+        w = self.sws(slot, B)
+        if w.terms == 0 or not w.zrow:
+            return None
+        if w.Wp is None:
+            w.Wp = torch.empty(self.S * self.HF * 6, dtype=torch.uint8, device=self.device)
+        head, draw = self, self.draws
+
+        class _Job:
+            @staticmethod
+            def args():
+                return (head.W.p.data_ptr(), head.b.p.data_ptr(), head.seed, draw, head.A, head.S, head.HF,
+                        w.ids.data_ptr(), w.Wg.data_ptr(), w.bg.data_ptr(), w.Wp.data_ptr())
+
+            @staticmethod
+            def done():
+                w.pre_draw = draw
+        return _Job()
+
     def forward_loss(self, h, tgt, slot="main", h_planes=None):
         """h_planes: h's bf16 K-planes from the GRU forward (Trunk.emit_planes),
-        consumed by the one-launch split logits at HF <= 128."""
+        consumed by the one-launch split logits at HF <= 128.  When the trunk's
+        gather launch already gathered this draw's negatives (neg_job), the
+        logits read their planes (draw = 2)."""
         B = h.shape[0]
         w = self.sws(slot, B)
         st = stream_ptr()
         g = _f32(1.0 / B)
         split = w.terms != 0
-        # the negatives' row gather is part of the timed logits step; with the
-        # one-launch kernel the region is kernel-exact
+        pre = w.pre_draw == self.draws
+        w.pre_draw = -1
+        # the negatives' row gather is part of the timed logits step (or of the
+        # gather launch, pre); with the one-launch kernel the region is kernel-exact
         with region("sampled_fwd", exact=bool(split and w.zrow)):
-            if split and w.zrow:  # one launch: draw, row gather, operand split, logits, partials
+            if split and w.zrow:  # one launch: [draw, row gather, operand split,] logits, partials
                 hp = h_planes.data_ptr() if h_planes is not None and self.HF <= 128 else None
                 call("rg_sampled_logits", h.data_ptr(), self.W.p.data_ptr(), self.b.p.data_ptr(), w.ids.data_ptr(),
-                     1, self.seed, self.draws, self.A, B, self.S, self.HF, w.terms, w.ZT.data_ptr(), w.ldz,
-                     w.pmax.data_ptr(), w.psum.data_ptr(), w.Wg.data_ptr(), w.bg.data_ptr(), hp, st)
+                     2 if pre else 1, self.seed, self.draws, self.A, B, self.S, self.HF, w.terms, w.ZT.data_ptr(),
+                     w.ldz, w.pmax.data_ptr(), w.psum.data_ptr(), w.Wg.data_ptr(), w.bg.data_ptr(), hp,
+                     w.Wp.data_ptr() if pre else None, st)
             elif split:  # draw + gather + operand split fused into one prep launch
                 if w.work is None:
                     w.work = torch.empty(call("rg_sampled_work_bytes", B, self.S, self.HF), dtype=torch.uint8,

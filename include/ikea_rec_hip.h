@@ -365,6 +365,16 @@ int rg_gru_bwd_wide(const float* saved, int64_t plane, const float* Whh, const i
 int rg_gather_h(const int64_t* s, int B, int L, const int32_t* perm, const int32_t* lsort, const int32_t* offs,
                 const uint16_t* emb16, int64_t n_rows, int E, int reverse, int32_t* tok_id, float* X, int32_t* err,
                 rg_stream_t stream);
+/* ---- A3 gather of a sampled step (north-star "embedding gather + sampled logits"): rg_gather (emb16 = 0)
+ * or rg_gather_h (emb16 = 1) with the S negatives' row gather in the same launch — draw `counter` of the
+ * counter-based stream (seed, S, A; rg_sample_uniform's ids) -> ids[S], bg = bias[ids], Wg (S, HF) =
+ * W[ids] and Wp (S·HF·6 bytes) = the rows' bf16 planes in fragment order for rg_sampled_logits
+ * (draw = 2).  E, HF in {32, 64, 128, 256}, L <= 64, S % 32 == 0.  Replaces the nn.Embedding forward
+ * (GRU4Rec/model.py:69,74) plus the negatives' row lookup of the build-defined sampled head. */
+int rg_gather_neg(const int64_t* s, int B, int L, const int32_t* perm, const int32_t* lsort, const int32_t* offs,
+                  const void* emb, int emb16, int64_t n_rows, int E, int reverse, int32_t* tok_id, float* X,
+                  int32_t* err, const float* W, const float* bias, uint64_t seed, uint64_t counter, int64_t A, int S,
+                  int HF, int32_t* ids, float* Wg, float* bg, void* Wp, rg_stream_t stream);
 /* rg_adam_rows (cols % 4 == 0) that also writes P16 = fp16(P); tags == NULL: every row has a gradient */
 int rg_adam_rows_h(float* P, float* M, float* V, float* G, const int32_t* tags, int32_t tag, int64_t rows, int cols,
                    const float* adam6, uint16_t* P16, rg_stream_t stream);
@@ -399,10 +409,13 @@ int rg_sampled_fwd_x(const float* h, const float* W, const float* bias, int32_t*
  * gather, both operands' bf16 split, MFMAs, logits, partials): same semantics as rg_sampled_fwd_x
  * but Z is ROW-major, Z[b·ldz + s] (ldz >= S, ldz % 4 == 0).  Wg optional, bg required.
  * h_planes (optional, HF <= 128): h's bf16 K-planes (rg_gru_fwd_dirs_planes / rg_head_planes), moved
- * to LDS by DMA instead of splitting h in the kernel. */
+ * to LDS by DMA instead of splitting h in the kernel.
+ * draw: 0 = ids given in neg, 1 = drawn here, 2 = pre-gathered by rg_gather_neg (neg, bg, Wg already
+ * hold the ids, biases and rows; w_planes = its fragment-order planes, required). */
 int rg_sampled_logits(const float* h, const float* W, const float* bias, int32_t* neg, int draw, uint64_t seed,
                       uint64_t counter, int64_t A, int B, int S, int HF, int terms, float* Z, int64_t ldz,
-                      float* pmax, float* psum, float* Wg, float* bg, const void* h_planes, rg_stream_t stream);
+                      float* pmax, float* psum, float* Wg, float* bg, const void* h_planes, const void* w_planes,
+                      rg_stream_t stream);
 /* in place dZ = exp(Z − lse)·g on the row-major Z of rg_sampled_logits; dbg[s] = Σ_b dZ[b][s]
  * through ceil(B/128) × S slabs (summed in order: deterministic) */
 int rg_sampled_dz_rows(float* Z, int64_t ldz, const float* lse, int B, int S, float gscale, float* slabs, float* dbg,

@@ -46,7 +46,7 @@ def bpr_kernels(B, S, A, HF, layout, seed=0, bad_target=False):
         zsb, zss = ldz, 1
         pm, ps = torch.empty(nT, B, device="cuda"), torch.empty(nT, B, device="cuda")
         call("rg_sampled_logits", dh_.data_ptr(), W_.data_ptr(), b_.data_ptr(), neg_.data_ptr(), 0, 0, 0, A, B, S,
-             HF, 9, Z.data_ptr(), ldz, pm.data_ptr(), ps.data_ptr(), Wg.data_ptr(), bg.data_ptr(), None, st)
+             HF, 9, Z.data_ptr(), ldz, pm.data_ptr(), ps.data_ptr(), Wg.data_ptr(), bg.data_ptr(), None, None, st)
         view = lambda: Z[:, :S]  # noqa: E731
     else:
         ldz = (B + 3) // 4 * 4

@@ -50,7 +50,7 @@ def run_head(B, S, A, HF, seed=0, collide=False, precision="f32"):
             call("rg_head_planes", dh_.data_ptr(), B, HF, hk.data_ptr(), None, None, None, st)
         call("rg_sampled_logits", dh_.data_ptr(), W_.data_ptr(), b_.data_ptr(), neg_.data_ptr(), 0, 0, 0, A, B, S,
              HF, {"f32x9": 9, "f32x6": 6}[precision], ZT.data_ptr(), ldz, pm.data_ptr(), ps.data_ptr(), Wg.data_ptr(),
-             bg.data_ptr(), None if hk is None else hk.data_ptr(), st)
+             bg.data_ptr(), None if hk is None else hk.data_ptr(), None, st)
     elif precision == "f32":
         call("rg_sampled_fwd", dh_.data_ptr(), W_.data_ptr(), b_.data_ptr(), neg_.data_ptr(), B, S, HF,
              ZT.data_ptr(), ldz, pm.data_ptr(), ps.data_ptr(), Wg.data_ptr(), bg.data_ptr(), st)
@@ -230,3 +230,86 @@ def test_sampled_trainer_matches_oracle(kind, E, H, N, L, B, S):
         zo = orc.net(s, ln)
     d = (z - zo).abs()
     assert float(d.mean()) < 1e-4, float(d.mean())
+
+
+def _planes_ref(Wg):
+    """(S, HF) fp32 rows -> the fragment-order bf16 planes of common.h
+    plane_idx: [32-row block][16-deep slice j][plane p][lane (hh, n)] × 8."""
+    S, HF = Wg.shape
+    x = Wg.double().cpu().float()
+    p0 = x.to(torch.bfloat16)
+    r1 = x - p0.float()
+    p1 = r1.to(torch.bfloat16)
+    p2 = (r1 - p1.float()).to(torch.bfloat16)
+    out = []
+    for p in (p0, p1, p2):
+        # (S/32, n, NS, hh, 8) -> (blk, j, hh, n, 8)
+        out.append(p.view(S // 32, 32, HF // 16, 2, 8).permute(0, 2, 3, 1, 4))
+    # (blk, j, p, hh, n, 8)
+    return torch.stack(out, 2).contiguous().view(torch.int16).flatten()
+
+
+@pytest.mark.parametrize("E,HF,emb16", [(128, 128, 0), (128, 256, 0), (64, 64, 1)])
+def test_gather_neg_matches_gather_and_draw(E, HF, emb16):
+    """rg_gather_neg (the sampled step's embedding gather with the negatives'
+    row gather in the same launch): the embedding rows bit-equal to rg_gather,
+    the negatives bit-equal to the draw / row lookup rg_sampled_logits makes
+    itself, and the pre-gathered logits (draw = 2) bit-equal to the one-launch
+    draw (draw = 1)."""
+    from oracle.models import sample_uniform
+    from recommenders.data_utils.synthetic import SessionStream
+    from recommenders.hip import call, stream_ptr
+    A, L, B, S = 50000, 50, 1024, 2048
+    st = stream_ptr()
+    g = torch.Generator().manual_seed(3)
+    emb = D(torch.randn(A + 1, E, generator=g) * 0.1)
+    table = emb.half() if emb16 else emb
+    W = D(torch.randn(A, HF, generator=g) * 0.1)
+    bias = D(torch.randn(A, generator=g) * 0.1)
+    s, a, r, sn, ln, nln, e = SessionStream(A, L, B, seed=4).batch(0, B)
+    s, ln = D(s), D(ln)
+    perm, ls, offs = (torch.empty(B, dtype=torch.int32, device="cuda") for _ in range(3))
+    offs = torch.empty(B + 1, dtype=torch.int32, device="cuda")
+    call("rg_pack", ln.data_ptr(), B, L, 0, perm.data_ptr(), ls.data_ptr(), offs.data_ptr(), st)
+    T = int(ln.clamp(1, L).sum())
+    err = torch.zeros(1, dtype=torch.int32, device="cuda")
+    X0, X1 = torch.full((T, E), float("nan"), device="cuda"), torch.full((T, E), float("nan"), device="cuda")
+    t0, t1 = torch.empty(T, dtype=torch.int32, device="cuda"), torch.empty(T, dtype=torch.int32, device="cuda")
+    call("rg_gather_h" if emb16 else "rg_gather", s.data_ptr(), B, L, perm.data_ptr(), ls.data_ptr(),
+         offs.data_ptr(), table.data_ptr(), A + 1, E, 0, t0.data_ptr(), X0.data_ptr(), err.data_ptr(), st)
+    ids = torch.full((S,), -7, dtype=torch.int32, device="cuda")
+    Wg = torch.full((S, HF), float("nan"), device="cuda")
+    bg = torch.full((S,), float("nan"), device="cuda")
+    Wp = torch.zeros(S * HF * 6, dtype=torch.uint8, device="cuda")
+    seed, counter = 11, 5
+    call("rg_gather_neg", s.data_ptr(), B, L, perm.data_ptr(), ls.data_ptr(), offs.data_ptr(), table.data_ptr(),
+         emb16, A + 1, E, 0, t1.data_ptr(), X1.data_ptr(), err.data_ptr(), W.data_ptr(), bias.data_ptr(), seed,
+         counter, A, S, HF, ids.data_ptr(), Wg.data_ptr(), bg.data_ptr(), Wp.data_ptr(), st)
+    torch.cuda.synchronize()
+    assert int(err) == 0
+    assert torch.equal(X0, X1) and torch.equal(t0, t1)
+    ref_ids = torch.from_numpy(sample_uniform(seed, counter, S, A)).cuda()
+    assert torch.equal(ids.long(), ref_ids.long())
+    assert torch.equal(Wg, W[ids.long()]) and torch.equal(bg, bias[ids.long()])
+    assert torch.equal(Wp.view(torch.int16).cpu(), _planes_ref(Wg))
+    # pre-gathered logits == the one-launch draw, bit for bit
+    h = D(torch.randn(B, HF, generator=g) * 0.5)
+    out = {}
+    for draw in (1, 2):
+        nT = call("rg_sampled_nparts", B, S, 6)
+        Z = torch.full((B, S), float("nan"), device="cuda")
+        pm, ps = torch.empty(nT, B, device="cuda"), torch.empty(nT, B, device="cuda")
+        i2 = ids.clone() if draw == 2 else torch.full((S,), -7, dtype=torch.int32, device="cuda")
+        Wg2 = Wg.clone() if draw == 2 else torch.full((S, HF), float("nan"), device="cuda")
+        bg2 = bg.clone() if draw == 2 else torch.full((S,), float("nan"), device="cuda")
+        call("rg_sampled_logits", h.data_ptr(), W.data_ptr(), bias.data_ptr(), i2.data_ptr(), draw, seed, counter, A,
+             B, S, HF, 6, Z.data_ptr(), S, pm.data_ptr(), ps.data_ptr(), Wg2.data_ptr(), bg2.data_ptr(), None,
+             Wp.data_ptr() if draw == 2 else None, st)
+        torch.cuda.synchronize()
+        out[draw] = (Z, pm, ps, i2, Wg2, bg2)
+    for x1, x2 in zip(out[1], out[2]):
+        assert torch.equal(x1, x2)
+    with pytest.raises(RuntimeError):   # draw = 2 needs the planes
+        call("rg_sampled_logits", h.data_ptr(), W.data_ptr(), bias.data_ptr(), ids.data_ptr(), 2, seed, counter, A,
+             B, S, HF, 6, out[1][0].data_ptr(), S, out[1][1].data_ptr(), out[1][2].data_ptr(), Wg.data_ptr(),
+             bg.data_ptr(), None, None, st)

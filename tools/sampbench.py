@@ -77,7 +77,7 @@ for HF in a.HF:
                 it[0] += 0 if a.hot else 1
                 call("rg_sampled_logits", h.data_ptr(), W.data_ptr(), bias.data_ptr(), neg.data_ptr(), 1, 7, it[0], A,
                      B, S, HF, terms, Zr.data_ptr(), ldzr, pm.data_ptr(), ps.data_ptr(), Wg.data_ptr(), bg.data_ptr(),
-                     None if hk is None else hk.data_ptr(), st)
+                     None if hk is None else hk.data_ptr(), None, st)
             for _ in range(3):
                 fz()
             torch.cuda.synchronize()

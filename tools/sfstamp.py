@@ -22,6 +22,8 @@ ap.add_argument("--S", type=int, default=2048)
 ap.add_argument("--A", type=int, default=1_000_000)
 ap.add_argument("--HF", type=int, default=128)
 ap.add_argument("--iters", type=int, default=200)
+ap.add_argument("--wp", choices=["none", "cold", "warm"], default="none",
+                help="draw = 2: W planes / biases pre-gathered; cold = written before the 256 MB of other traffic")
 a = ap.parse_args()
 dev = "cuda"
 B, S, A, HF = a.B, a.S, a.A, a.HF
@@ -45,10 +47,21 @@ nwg = (S // 256) * (B // 128)
 n = nwg * 8 * 8
 buf = np.zeros(n, dtype=np.uint64)
 rows = []
+wp_src = torch.randint(0, 1 << 14, (S * HF * 3,), dtype=torch.int16, device=dev)
+wp = torch.empty_like(wp_src)
+bg_src = torch.randn(S, device=dev)
 for it in range(a.iters):
+    if a.wp == "cold":
+        wp.copy_(wp_src)
+        bg.copy_(bg_src)
     junk.add_(1.0)   # 256 MB of other traffic between launches, as in a step
-    call("rg_sampled_logits", h.data_ptr(), W.data_ptr(), bias.data_ptr(), neg.data_ptr(), 1, 7, it + 1, A, B, S, HF,
-         6, Z.data_ptr(), S, pm.data_ptr(), ps.data_ptr(), Wg.data_ptr(), bg.data_ptr(), hk.data_ptr(), st)
+    if a.wp == "warm":
+        wp.copy_(wp_src)
+        bg.copy_(bg_src)
+    pre = a.wp != "none"
+    call("rg_sampled_logits", h.data_ptr(), W.data_ptr(), bias.data_ptr(), neg.data_ptr(), 2 if pre else 1, 7, it + 1,
+         A, B, S, HF, 6, Z.data_ptr(), S, pm.data_ptr(), ps.data_ptr(), Wg.data_ptr(), bg.data_ptr(), hk.data_ptr(),
+         wp.data_ptr() if pre else None, st)
     if it >= a.iters - 20:
         torch.cuda.synchronize()
         assert lib.rg_sf_stamp_read(buf.ctypes.data_as(C.c_void_p), C.c_int64(n)) == 0
