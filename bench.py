@@ -593,6 +593,12 @@ def main():
                 if target is not None:
                     target["workload"] = f"GRU4Rec {N} items dim{E} batch {B}/GPU, {args.negatives} sampled negatives"
                     target["kernel_ms"] = k2
+                    # HBM bytes of the two kernels per step from the PMC passes (tools/pmc_ns.sh)
+                    pmc = os.path.join(HERE, "profiles", "pmc_traffic.json")
+                    target["traffic"] = None
+                    if os.path.exists(pmc) and (N, E, B, args.negatives) == (1_000_000, 128, 4096, 2048) and terms == 6:
+                        t1 = json.load(open(pmc)).get("c2:gather+sampled_fwd:r04")
+                        target["traffic"] = None if t1 is None else int(t1) * world   # summed over ranks like the bytes
                 del tr2
     else:
         target = target_step(kern, T, B, args.negatives, E, HF, 2, terms)
@@ -602,7 +608,7 @@ def main():
             pmc = os.path.join(HERE, "profiles", "pmc_traffic.json")
             roof["traffic"] = None
             if os.path.exists(pmc) and (B, args.negatives, HF) == (4096, 2048, 256) and terms == 6:
-                roof["traffic"] = json.load(open(pmc)).get("c3:gather+sampled_fwd:r03")
+                roof["traffic"] = json.load(open(pmc)).get("c3:gather+sampled_fwd:r04")
     if rank != 0:
         if torch.distributed.is_initialized():
             torch.distributed.destroy_process_group()
