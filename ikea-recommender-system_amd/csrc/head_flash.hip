@@ -816,8 +816,26 @@ __global__ __launch_bounds__(64 * fl_nw(HF, 2)) void k_flash_dw(
   }
   const int64_t blk32 = j0 >> 5;
   const int c4 = lane & 7;
+  // W / mW / vW of the 32-column slab s, loaded one slab ahead and
+  // unconditionally (rows past A clamp to A − 1; only the stores are guarded),
+  // so the 16 (slab, q) steps do not each wait a full memory round trip (the
+  // guarded per-q loads could not be hoisted: 3 loads, vmcnt(0), Adam, 3
+  // stores, 16 times over)
+  f4 pwp[2][4], mqp[2][4], vvp[2][4];
+  auto ldp = [&](int s, int slot) __attribute__((always_inline)) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int it = min(j0 + (lane >> 3) + 8 * q, A - 1);
+      const int64_t o = (int64_t)it * HF + 32 * s + 4 * c4;
+      pwp[slot][q] = *reinterpret_cast<const f4*>(W + o);
+      mqp[slot][q] = *reinterpret_cast<const f4*>(mW + o);
+      vvp[slot][q] = *reinterpret_cast<const f4*>(vW + o);
+    }
+  };
+  if (!dW_out) ldp(0, 0);
 #pragma unroll
   for (int s = 0; s < NS; ++s) {
+    if (!dW_out && s + 1 < NS) ldp(s + 1, (s + 1) & 1);
 #pragma unroll
     for (int f2 = 0; f2 < 2; ++f2)
 #pragma unroll
@@ -834,8 +852,7 @@ __global__ __launch_bounds__(64 * fl_nw(HF, 2)) void k_flash_dw(
         if (dW_out) {
           *reinterpret_cast<f4*>(dW_out + o) = gv;
         } else {
-          f4 pw = *reinterpret_cast<const f4*>(W + o), mq = *reinterpret_cast<const f4*>(mW + o),
-             v = *reinterpret_cast<const f4*>(vW + o);
+          f4 pw = pwp[s & 1][q], mq = mqp[s & 1][q], v = vvp[s & 1][q];
 #pragma unroll
           for (int u = 0; u < 4; ++u) {
             float pu = pw[u], mu = mq[u], vu = v[u];
