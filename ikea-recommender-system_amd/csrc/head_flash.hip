@@ -144,6 +144,23 @@ __global__ void k_pad_bias(const float* __restrict__ bias, int A, int Ap, float*
 // chunk's row maximum — the inputs of the fused top-k (SMORL's rewards).
 // NG = 0 (rg_flash_score, evaluation): the S-part alone — lse partials,
 // per-split top-1 and chunk maxima, no O contraction, no R-planes read.
+// Diagnostic build only (-DFL_STAMP, tools/flstamp.py): per-wave core cycles
+// spent in pass 1's chunk barriers and in the whole wave.
+#ifdef FL_STAMP
+__device__ uint64_t g_fl_stamp[4096 * 2];
+extern "C" int rg_fl_stamp_read(void* dst, int64_t n) {
+  return hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_fl_stamp), n * 8, 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
+#define FL_SYNC()                                           \
+  do {                                                      \
+    const uint64_t _tb = __builtin_amdgcn_s_memtime();      \
+    __syncthreads();                                        \
+    fl_bw += __builtin_amdgcn_s_memtime() - _tb;            \
+  } while (0)
+#else
+#define FL_SYNC() __syncthreads()
+#endif
+
 template <int HF, int NT, int NG, bool ARG>
 __global__ __launch_bounds__(64 * fl_nw(HF, 1)) void k_flash_fwd(
     const bf16x8* __restrict__ Hk, const bf16x8* __restrict__ Wk, const bf16x8* __restrict__ Wr,
@@ -160,6 +177,10 @@ __global__ __launch_bounds__(64 * fl_nw(HF, 1)) void k_flash_fwd(
   __shared__ __attribute__((aligned(16))) float sb0[32], sb1[32];
   const int tid = threadIdx.x, lane = tid & 63, kg = lane >> 4, l16 = lane & 15, lane16 = 16 * lane;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+#ifdef FL_STAMP
+  uint64_t fl_bw = 0;
+  const uint64_t fl_t0 = __builtin_amdgcn_s_memtime();
+#endif
   // XCD-aware order: the nrb row blocks of one item split are dispatched to
   // the same XCD (round-robin dispatch), so its W chunks are fetched once
   // into that XCD's L2 and re-read from there
@@ -309,7 +330,7 @@ __global__ __launch_bounds__(64 * fl_nw(HF, 1)) void k_flash_fwd(
         spart(sk0, sb0, c, q0, q1, q2);
         opart(sr0, q0, q1, q2);
       }
-      __syncthreads();
+      FL_SYNC();
       if (c + 1 < nch) {
         if (c + 2 < nch) {
           FL_ISSUE_K(c0 + c + 2, sk0, sb0);
@@ -320,7 +341,7 @@ __global__ __launch_bounds__(64 * fl_nw(HF, 1)) void k_flash_fwd(
           spart(sk1, sb1, c + 1, q0, q1, q2);
           opart(sr1, q0, q1, q2);
         }
-        __syncthreads();
+        FL_SYNC();
       }
     } else {
       // single R buffer: R(c) was issued after the previous chunk's O-part
@@ -344,6 +365,12 @@ __global__ __launch_bounds__(64 * fl_nw(HF, 1)) void k_flash_fwd(
   }
 #undef FL_ISSUE_K
 #undef FL_ISSUE_R
+#ifdef FL_STAMP
+  if (lane == 0 && blockIdx.x < 512) {
+    g_fl_stamp[(blockIdx.x * NW + w) * 2] = fl_bw;
+    g_fl_stamp[(blockIdx.x * NW + w) * 2 + 1] = __builtin_amdgcn_s_memtime() - fl_t0;
+  }
+#endif
   if (!active) return;
 #pragma unroll
   for (int rb = 0; rb < 2; ++rb) {
