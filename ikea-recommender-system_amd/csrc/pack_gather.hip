@@ -284,7 +284,8 @@ __global__ __launch_bounds__(256) void k_gather_e(const int64_t* __restrict__ s,
                                                   int32_t* __restrict__ err, NegPrep np) {
   constexpr int V4 = E / 4;
   constexpr int TPP = 256 / V4;                       // tokens per pass of the workgroup
-  constexpr int U = GW_FLIGHT / TPP;                  // passes whose loads issue together
+  constexpr int FLT = E >= 256 ? GW_FLIGHT / 2 : GW_FLIGHT;   // rows in flight (64 VGPRs of f4 per lane)
+  constexpr int U = FLT / TPP;                        // passes whose loads issue together
   __shared__ int ids[GW_ROWS * GW_MAXL];
   __shared__ int rb[GW_ROWS], rl[GW_ROWS], ro[GW_ROWS + 1];
   if ((int)blockIdx.x < np.nwg) {
@@ -313,7 +314,7 @@ __global__ __launch_bounds__(256) void k_gather_e(const int64_t* __restrict__ s,
   }
   __syncthreads();
   const int c = tid % V4, t0 = tid / V4;
-  for (int i0 = t0; i0 < ntok; i0 += GW_FLIGHT) {
+  for (int i0 = t0; i0 < ntok; i0 += FLT) {
     f4 v[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {

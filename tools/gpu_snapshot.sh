@@ -11,3 +11,8 @@ for f in c2 c3 c4; do python -c "import json;d=json.load(open('gpurun_out/snap/b
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/snap/prof_c2 -o c2 -- python bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-native-side --no-eval > gpurun_out/snap/prof_c2.log 2>&1 || { echo "rocprof failed"; tail gpurun_out/snap/prof_c2.log; exit 1; }
 echo done
+# C3 / C4 kernel stats (round 3)
+cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/snap/prof_c3 -o c3 -- python bench.py --config c3 --steps 10 --warmup 2 --no-cpu-baseline --no-native-side --no-eval > gpurun_out/snap/prof_c3.log 2>&1 || { echo "rocprof c3 failed"; tail gpurun_out/snap/prof_c3.log; exit 1; }
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/snap/prof_c4 -o c4 -- python bench.py --config c4 --steps 6 --warmup 2 --no-cpu-baseline --no-native-side --no-eval > gpurun_out/snap/prof_c4.log 2>&1 || { echo "rocprof c4 failed"; tail gpurun_out/snap/prof_c4.log; exit 1; }
+echo done2
