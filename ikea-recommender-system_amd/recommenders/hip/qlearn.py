@@ -133,7 +133,8 @@ def _dev(x, dev, dtype=None):
 
 
 
-def double_q_step(nets, clocks, k, s, a, r, s_next, true_len, true_next_len, is_end, *, gamma, smorl=None):
+def double_q_step(nets, clocks, k, s, a, r, s_next, true_len, true_next_len, is_end, *, gamma, smorl=None,
+                  host=None):
     """One SQN (smorl=None) or SMORL step with main = nets[k].  Returns device
     (sup_loss (1,) f32, q_loss (1,) f64 for SQN / f32 for SMORL)."""
     main, boot = nets[k], nets[1 - k]
@@ -179,6 +180,8 @@ def double_q_step(nets, clocks, k, s, a, r, s_next, true_len, true_next_len, is_
         call("rg_smorl_td", q.data_ptr(), qn.data_ptr(), rr.data_ptr(), end8.data_ptr(), smorl["w_dev"].data_ptr(),
              nh, _f32(gamma), grad_row, B, row.data_ptr(), dq.data_ptr(), st)
         call("rg_sum_scale", row.data_ptr(), B, _f32(1.0 / B), q_loss.data_ptr(), None, st)
+    if host is not None:   # (SMORL: + the supervised head's top-k overflow flag)
+        host.capture(sup_loss, q_loss, *([main.sup_head_output.top_err] if smorl is not None else []))
     # ---- backward + Adam (main network, its own optimizer clock) ----
     adam6 = clocks[k].next_args()
     main.trunk_tag = getattr(main, "trunk_tag", 0) + 1

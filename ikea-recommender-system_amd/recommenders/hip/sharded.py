@@ -110,7 +110,7 @@ def _gather_rows(comm, net, name, x):
     return comm.all_gather(out, x.contiguous())
 
 
-def sharded_supervised_step(net, clock, s, a, true_len):
+def sharded_supervised_step(net, clock, s, a, true_len, host=None):
     comm = net.comm
     dev = net.device
     # the id / row exchange's splits from the host batch (no device read-back)
@@ -132,6 +132,8 @@ def sharded_supervised_step(net, clock, s, a, true_len):
         H_all = _gather_rows(comm, net, "H_all", h_in)
         a_all = _gather_rows(comm, net, "a_all", a)
     w, lse, tgt_loc = _sharded_ce_forward(net, head, H_all, a_all, st)
+    if host is not None:
+        host.capture(w.loss)
     # ---- backward ----
     adam6 = clock.next_args()
     net.trunk_tag = getattr(net, "trunk_tag", 0) + 1
@@ -207,7 +209,8 @@ def _global_topk(net, head, w, K, name):
     return out
 
 
-def sharded_double_q_step(nets, clocks, k, s, a, r, s_next, true_len, true_next_len, is_end, *, gamma, smorl=None):
+def sharded_double_q_step(nets, clocks, k, s, a, r, s_next, true_len, true_next_len, is_end, *, gamma, smorl=None,
+                          host=None):
     """SQN / SMORL step over the global batch (every rank's B rows) with the
     trunk replicated and every head item-sharded:
 
@@ -289,6 +292,8 @@ def sharded_double_q_step(nets, clocks, k, s, a, r, s_next, true_len, true_next_
              nh, _f32(gamma), grad_row, B, row.data_ptr(), dq.data_ptr(), st)
         call("rg_sum_scale", row.data_ptr(), B, _f32(1.0 / Bg), q_loss.data_ptr(), None, st)
     comm.all_reduce(q_loss)
+    if host is not None:   # (SMORL: + the supervised head's top-k overflow flag)
+        host.capture(sup_loss, q_loss, *([sup.top_err] if smorl is not None else []))
     # ---- backward + Adam (main network, its own optimizer clock) ----
     adam6 = clocks[k].next_args()
     main.trunk_tag = getattr(main, "trunk_tag", 0) + 1

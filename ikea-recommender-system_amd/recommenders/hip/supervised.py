@@ -29,8 +29,10 @@ class SupervisedNet(HipNet):
 
 
 
-def supervised_step(net: SupervisedNet, clock, s, a, true_len):
-    """Returns the device loss tensor (1,) — the caller does the .item()."""
+def supervised_step(net: SupervisedNet, clock, s, a, true_len, host=None):
+    """Returns the device loss tensor (1,) — the caller does the .item(), or,
+    with ``host`` (hostsync.HostScalars), reads the loss captured as soon as
+    it is final."""
     dev = net.device
     s = s.to(dev, non_blocking=True)
     a = a.to(dev, non_blocking=True)
@@ -51,6 +53,8 @@ def supervised_step(net: SupervisedNet, clock, s, a, true_len):
         h_in = h
     # the GRU forward's bf16 K-planes of h (sampled head) unless dropout changed h
     loss, _ = head.forward_loss(h_in, a, slot="main", h_planes=net.trunk.h_planes if mask is None else None)
+    if host is not None:
+        host.capture(loss)
     adam6 = clock.next_args()
     net.trunk_tag = getattr(net, "trunk_tag", 0) + 1
     dh = net.dh_buffer(B)

@@ -14,6 +14,7 @@ import torch.nn as nn
 
 from recommenders.hip import require_gpu
 from recommenders.hip.engine import AdamClock
+from recommenders.hip.hostsync import HostScalars
 from recommenders.hip.supervised import SupervisedNet, supervised_step
 from recommenders.models.GRU4Rec.model import _AdamFacade
 
@@ -51,7 +52,10 @@ class BidirGRU4Rec_trainer:
         self.optimizer = _AdamFacade(self.clock, [self.gru_model])
 
     def train_step(self, s, a, true_len):
-        return supervised_step(self.gru_model, self.clock, s, a, true_len).item()
+        # the loss is read back as soon as it is final (hip/hostsync.py)
+        hs = self.__dict__.setdefault("_host_scalars", HostScalars())
+        supervised_step(self.gru_model, self.clock, s, a, true_len, host=hs)
+        return hs.get()[0]
 
     def train_step_async(self, s, a, true_len):
         return supervised_step(self.gru_model, self.clock, s, a, true_len)

@@ -13,6 +13,7 @@ import torch.nn as nn
 
 from recommenders.hip import require_gpu
 from recommenders.hip.engine import AdamClock
+from recommenders.hip.hostsync import HostScalars
 from recommenders.hip.dist import Comm
 from recommenders.hip.sharded import sharded_supervised_step
 from recommenders.hip.supervised import SupervisedNet, supervised_step
@@ -137,8 +138,15 @@ class GRU4Rec_trainer:
 
     def train_step(self, s, a, true_len):
         """One step on (s, a, true_len); returns the CE loss as a Python float
-        (with shard_items: the mean over every rank's rows)."""
-        return self.train_step_async(s, a, true_len).item()
+        (with shard_items: the mean over every rank's rows).  The loss is read
+        back as soon as it is final (hip/hostsync.py): the backward and the
+        Adam sweeps are still queued when this returns."""
+        hs = self.__dict__.setdefault("_host_scalars", HostScalars())
+        if self.comm is not None:
+            sharded_supervised_step(self.gru_model, self.clock, s, a, true_len, host=hs)
+        else:
+            supervised_step(self.gru_model, self.clock, s, a, true_len, host=hs)
+        return hs.get()[0]
 
     def train_step_async(self, s, a, true_len):
         """Same step without the host sync; returns the device loss tensor."""

@@ -17,6 +17,7 @@ import torch.nn as nn
 
 from recommenders.hip import require_gpu
 from recommenders.hip.engine import AdamClock
+from recommenders.hip.hostsync import HostScalars
 from recommenders.hip.dist import Comm
 from recommenders.hip.qlearn import QNet, double_q_step, unpopular_bitmap
 from recommenders.hip.sharded import sharded_double_q_step
@@ -105,19 +106,22 @@ class SMORL_trainer:
         self.optimizer_2 = _AdamFacade(self.clock_2, [self.SMORL_2])
         self.last_main = None
 
-    def train_step_async(self, s, a, r_acc, s_next, true_len, true_next_len, is_end):
+    def train_step_async(self, s, a, r_acc, s_next, true_len, true_next_len, is_end, host=None):
         k = 0 if random.uniform(0, 1) <= 0.5 else 1
         self.last_main = k
         step = sharded_double_q_step if self.comm is not None else double_q_step
         return step([self.SMORL_1, self.SMORL_2], [self.clock_1, self.clock_2], k, s, a, r_acc, s_next,
-                    true_len, true_next_len, is_end, gamma=self.gamma, smorl=self._smorl)
+                    true_len, true_next_len, is_end, gamma=self.gamma, smorl=self._smorl, host=host)
 
     def train_step(self, s, a, r_acc, s_next, true_len, true_next_len, is_end):
-        sup, q = self.train_step_async(s, a, r_acc, s_next, true_len, true_next_len, is_end)
-        out = sup.item(), q.item()
-        for net in (self.SMORL_1, self.SMORL_2):
-            net.sup_head_output.check_top_err()
-        return out
+        # losses and the rewards' top-k overflow flag read back as soon as they
+        # are final (hip/hostsync.py); the backward is still queued on return
+        hs = self.__dict__.setdefault("_host_scalars", HostScalars())
+        self.train_step_async(s, a, r_acc, s_next, true_len, true_next_len, is_end, host=hs)
+        sup, q, top_err = hs.get()
+        if top_err:
+            (self.SMORL_1, self.SMORL_2)[self.last_main].sup_head_output.check_top_err()
+        return sup, q
 
     @property
     def last_rewards(self):

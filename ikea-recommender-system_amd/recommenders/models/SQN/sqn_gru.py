@@ -14,6 +14,7 @@ import torch.nn as nn
 
 from recommenders.hip import require_gpu
 from recommenders.hip.engine import AdamClock
+from recommenders.hip.hostsync import HostScalars
 from recommenders.hip.dist import Comm
 from recommenders.hip.qlearn import QNet, double_q_step
 from recommenders.hip.sharded import sharded_double_q_step
@@ -70,17 +71,20 @@ class SQN_trainer:
         self.optimizer_2 = _AdamFacade(self.clock_2, [self.DQN_2])
         self.last_main = None
 
-    def train_step_async(self, s, a, r, s_next, true_len, true_next_len, is_end):
+    def train_step_async(self, s, a, r, s_next, true_len, true_next_len, is_end, host=None):
         k = 0 if random.uniform(0, 1) <= 0.5 else 1
         self.last_main = k
         step = sharded_double_q_step if self.comm is not None else double_q_step
         return step([self.DQN_1, self.DQN_2], [self.clock_1, self.clock_2], k, s, a, r, s_next, true_len,
-                    true_next_len, is_end, gamma=self.gamma)
+                    true_next_len, is_end, gamma=self.gamma, host=host)
 
     def train_step(self, s, a, r, s_next, true_len, true_next_len, is_end):
-        """One double-Q step; returns (sup_loss, q_loss) as Python floats."""
-        sup, q = self.train_step_async(s, a, r, s_next, true_len, true_next_len, is_end)
-        return sup.item(), q.item()
+        """One double-Q step; returns (sup_loss, q_loss) as Python floats, read
+        back as soon as they are final (hip/hostsync.py)."""
+        hs = self.__dict__.setdefault("_host_scalars", HostScalars())
+        self.train_step_async(s, a, r, s_next, true_len, true_next_len, is_end, host=hs)
+        sup, q = hs.get()
+        return sup, q
 
     def set_train(self):
         self.DQN_1.train()
