@@ -338,77 +338,124 @@ class Trunk:
                      w.lsort.data_ptr(), w.offs.data_ptr(), B, H, dh.data_ptr(), self.ndir * H, 0, st)
         self._pending = (w, S)
 
+    # The backward's two gradient paths run on two streams: the GRU weights'
+    # (wgrad, slab reduction, Adam / the all-reduce) on the trunk's side
+    # stream, the embedding's (dX, scatter or row exchange, the dense Adam
+    # sweep) on the current one — each a chain of small kernels that, beside
+    # the head's pass 2, wait for CUs one launch at a time.  dX = dGi·W_ih is
+    # issued first: it reads W_ih before the side stream's Adam moves it.  The
+    # current stream joins the side stream before returning.
+    def _wside(self):
+        if getattr(self, "_wstream", None) is None:
+            self._wstream = torch.cuda.Stream(device=self.device)
+        return self._wstream
+
     def step(self, adam6, tag):
         """Weight gradients + Adam for the trunk (after every use of the weights)."""
         w, S = self._pending
-        self._grads(w, S, tag)
-        st = stream_ptr()
-        for d in range(self.ndir):
-            w_ih, w_hh, b_ih, b_hh = self.dirs[d]
-            for prm, sl in ((w_ih, w.sl_ih[d]), (w_hh, w.sl_hh[d]), (b_ih, w.cs_ih[d]), (b_hh, w.cs_hh[d])):
-                call("rg_adam_slabs", prm.p.data_ptr(), prm.m.data_ptr(), prm.v.data_ptr(), sl.data_ptr(), S,
-                     prm.numel(), adam6, None, st)
+        main = torch.cuda.current_stream(self.device)
+        self._grads_dx(w)
+        ws = self._wside()
+        ws.wait_stream(main)
+        with torch.cuda.stream(ws):
+            self._grads_w(w, S)
+            st = stream_ptr()
+            for d in range(self.ndir):
+                w_ih, w_hh, b_ih, b_hh = self.dirs[d]
+                for prm, sl in ((w_ih, w.sl_ih[d]), (w_hh, w.sl_hh[d]), (b_ih, w.cs_ih[d]), (b_hh, w.cs_hh[d])):
+                    call("rg_adam_slabs", prm.p.data_ptr(), prm.m.data_ptr(), prm.v.data_ptr(), sl.data_ptr(), S,
+                         prm.numel(), adam6, None, st)
+        self._grads_scatter(w, tag)
         self._adam_emb(adam6, tag)
+        main.wait_stream(ws)
         self._pending = None
 
-    def _grads(self, w, S, tag):
+    def _grads_dx(self, w):
+        """dX = dGi · W_ih (T × E) of every direction."""
         st = stream_ptr()
         H, E, TM = self.H, self.E, w.TM
-        skip = -1 if self.train_pad else self.pad
         for d in range(self.ndir):
-            w_ih = self.dirs[d][0]
-            # dX = dGi · W_ih  (T × E)
             with region("gemm_dx"):
-                call("rg_gemm_f32", w.dGi[d].data_ptr(), 3 * H, 1, w_ih.p.data_ptr(), E, 1, w.dX[d].data_ptr(),
-                     E, None, TM, w.ntok_ptr, E, 3 * H, None, 1, st)
-            # dW_ih = dGiᵀ·X, db_ih = Σ dGi ; dW_hh = dGhᵀ·H_prev, db_hh = Σ dGh  (token splits)
+                call("rg_gemm_f32", w.dGi[d].data_ptr(), 3 * H, 1, self.dirs[d][0].p.data_ptr(), E, 1,
+                     w.dX[d].data_ptr(), E, None, TM, w.ntok_ptr, E, 3 * H, None, 1, st)
+
+    def _grads_w(self, w, S):
+        """dW_ih = dGiᵀ·X, db_ih = Σ dGi ; dW_hh = dGhᵀ·H_prev, db_hh = Σ dGh (token slabs)."""
+        st = stream_ptr()
+        H, E, TM = self.H, self.E, w.TM
+        for d in range(self.ndir):
             with region("wgrad"):
                 call("rg_wgrad", w.dGi[d].data_ptr(), 3 * H, w.X[d].data_ptr(), E, TM, w.ntok_ptr, S,
                      w.sl_ih[d].data_ptr(), w.cs_ih[d].data_ptr(), st)
                 call("rg_wgrad", w.dGh[d].data_ptr(), 3 * H, w.saved[d].data_ptr(), H, TM, w.ntok_ptr, S,
                      w.sl_hh[d].data_ptr(), w.cs_hh[d].data_ptr(), st)
-            if self.comm is None:
-                with region("scatter"):
-                    self.scatter(w.tok_id[d].data_ptr(), w.dX[d].data_ptr(), E, w.ntok_ptr, w.T_host, skip,
-                                 self.G_emb.data_ptr(), self.n_local, self.tags.data_ptr(), tag, st)
+
+    def _grads_scatter(self, w, tag):
+        """The embedding rows' gradients: scatter into G_emb, or (item-sharded
+        table) sent to their owners."""
+        st = stream_ptr()
         if self.comm is not None:
             with region("scatter"):
                 self._exchange_grads(w, tag, st)
+            return
+        skip = -1 if self.train_pad else self.pad
+        for d in range(self.ndir):
+            with region("scatter"):
+                self.scatter(w.tok_id[d].data_ptr(), w.dX[d].data_ptr(), self.E, w.ntok_ptr, w.T_host, skip,
+                             self.G_emb.data_ptr(), self.n_local, self.tags.data_ptr(), tag, st)
 
     # ---- data-parallel variant: gradients summed over ranks before Adam ----
     def grads_for_allreduce(self, tag):
-        """Compute this rank's trunk gradients into flat buffers (GRU: gflat,
-        embedding: the dense G_emb table) ready for a SUM all-reduce."""
+        """Compute this rank's trunk gradients into flat buffers (GRU: gflat on
+        the side stream, embedding: rows sent to their owners) ready for a SUM
+        all-reduce of gflat."""
         w, S = self._pending
-        self._grads(w, S, tag)
         self._tag = tag
         if getattr(self, "gflat", None) is None:
             n = sum(p.numel() for p in self.gru_params[:4 * self.ndir])
             self.gflat = torch.zeros(n, device=self.device)
-        st = stream_ptr()
-        off = 0
-        for d in range(self.ndir):
-            for prm, sl in zip(self.dirs[d], (w.sl_ih[d], w.sl_hh[d], w.cs_ih[d], w.cs_hh[d])):
-                n = prm.numel()
-                call("rg_adam_slabs", prm.p.data_ptr(), prm.m.data_ptr(), prm.v.data_ptr(), sl.data_ptr(), S, n,
-                     None, self.gflat.data_ptr() + 4 * off, st)
-                off += n
+        main = torch.cuda.current_stream(self.device)
+        self._grads_dx(w)
+        ws = self._wside()
+        ws.wait_stream(main)
+        with torch.cuda.stream(ws):
+            self._grads_w(w, S)
+            st = stream_ptr()
+            off = 0
+            for d in range(self.ndir):
+                for prm, sl in zip(self.dirs[d], (w.sl_ih[d], w.sl_hh[d], w.cs_ih[d], w.cs_hh[d])):
+                    n = prm.numel()
+                    call("rg_adam_slabs", prm.p.data_ptr(), prm.m.data_ptr(), prm.v.data_ptr(), sl.data_ptr(), S,
+                         n, None, self.gflat.data_ptr() + 4 * off, st)
+                    off += n
+        self._grads_scatter(w, tag)
 
     def allreduce_start(self, comm):
         """SUM all-reduce of the GRU gradients (~0.4 MB; the embedding rows went
-        to their owners by all-to-all in _exchange_grads)."""
-        return [comm.all_reduce(self.gflat, async_op=True)]
+        to their owners by all-to-all in _exchange_grads), ordered after the
+        side stream's slab reduction."""
+        with torch.cuda.stream(self._wside()):
+            return [comm.all_reduce(self.gflat, async_op=True)]
 
-    def adam_after_allreduce(self, adam6):
-        st = stream_ptr()
-        off = 0
-        for d in range(self.ndir):
-            for prm in self.dirs[d]:
-                n = prm.numel()
-                call("rg_adam_dense", prm.p.data_ptr(), prm.m.data_ptr(), prm.v.data_ptr(),
-                     self.gflat.data_ptr() + 4 * off, n, adam6, 0, st)
-                off += n
+    def adam_after_allreduce(self, adam6, works=()):
+        """The GRU weights' Adam after the all-reduce (side stream), the
+        embedding's on the current stream; the current stream joins."""
+        main = torch.cuda.current_stream(self.device)
+        ws = self._wside()
+        with torch.cuda.stream(ws):
+            for wk in works:
+                if wk is not None:
+                    wk.wait()
+            st = stream_ptr()
+            off = 0
+            for d in range(self.ndir):
+                for prm in self.dirs[d]:
+                    n = prm.numel()
+                    call("rg_adam_dense", prm.p.data_ptr(), prm.m.data_ptr(), prm.v.data_ptr(),
+                         self.gflat.data_ptr() + 4 * off, n, adam6, 0, st)
+                    off += n
         self._adam_emb(adam6, self._tag)
+        main.wait_stream(ws)
         self._pending = None
 
     def _adam_emb(self, adam6, tag):

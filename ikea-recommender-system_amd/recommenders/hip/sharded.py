@@ -152,11 +152,7 @@ def sharded_supervised_step(net, clock, s, a, true_len, host=None):
     works = net.trunk.allreduce_start(comm)
     if not fused:
         _sharded_ce_dw_adam(net, head, w, lse, tgt_loc, H_all, adam6, st)
-    with region("comm_wait"):
-        for wk in works:
-            if wk is not None:
-                wk.wait()
-    net.trunk.adam_after_allreduce(adam6)
+    net.trunk.adam_after_allreduce(adam6, works)   # (waits for the all-reduce on the trunk's side stream)
     return w.loss
 
 
@@ -318,11 +314,7 @@ def sharded_double_q_step(nets, clocks, k, s, a, r, s_next, true_len, true_next_
         _sharded_ce_dw_adam(main, sup, w, lse, tgt_loc, H_all, adam6, st)
     for qh in main.q_heads:
         qh.adam(adam6, tag)
-    with region("comm_wait"):
-        for wk in works:
-            if wk is not None:
-                wk.wait()
-    main.trunk.adam_after_allreduce(adam6)
+    main.trunk.adam_after_allreduce(adam6, works)   # (waits for the all-reduce on the trunk's side stream)
     return sup_loss, q_loss
 
 
