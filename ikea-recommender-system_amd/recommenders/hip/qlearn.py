@@ -126,6 +126,13 @@ class QNet(HipNet):
         return q
 
 
+def q_side_stream(net):
+    """The stream a Q network's head Adam sweeps run on (created once)."""
+    if getattr(net, "_qstream", None) is None:
+        net._qstream = torch.cuda.Stream(device=net.device)
+    return net._qstream
+
+
 def _dev(x, dev, dtype=None):
     x = x.to(dev, non_blocking=True)
     return x if dtype is None else x.to(dtype)
@@ -192,10 +199,18 @@ def double_q_step(nets, clocks, k, s, a, r, s_next, true_len, true_next_len, is_
     call("rg_q_backward", h.data_ptr(), main.hf, host_ptr_array([x.W.p for x in main.q_heads]),
          host_ptr_array([x.G for x in main.q_heads]), host_ptr_array([x.Gb for x in main.q_heads]),
          host_ptr_array([x.tags for x in main.q_heads]), nh, a.data_ptr(), B, dq.data_ptr(), dh.data_ptr(), tag, st)
-    for qh in main.q_heads:
-        qh.adam(adam6, tag)
+    # the Q heads' dense Adam sweeps on their own stream beside the trunk
+    # backward (they read only the Q heads' G rows, written above); joined
+    # before the step ends
+    cur = torch.cuda.current_stream(main.device)
+    qs = q_side_stream(main)
+    qs.wait_stream(cur)
+    with torch.cuda.stream(qs):
+        for qh in main.q_heads:
+            qh.adam(adam6, tag)
     main.trunk.backward(dh, slot="main")
     main.trunk.step(adam6, tag)
+    cur.wait_stream(qs)
     return sup_loss, q_loss
 
 

@@ -27,6 +27,7 @@ import torch
 from . import call, host_ptr_array, stream_ptr
 from .engine import _f32
 from .dist import host_routes
+from .qlearn import q_side_stream
 from .remap import raise_if_unmapped, remap_ids
 from .timing import region
 
@@ -304,6 +305,12 @@ def sharded_double_q_step(nets, clocks, k, s, a, r, s_next, true_len, true_next_
          host_ptr_array([x.G for x in main.q_heads]), host_ptr_array([x.Gb for x in main.q_heads]),
          host_ptr_array([x.tags for x in main.q_heads]), nh, a_loc.data_ptr(), Bg, dq_all.data_ptr(),
          dH_all.data_ptr(), tag, st)
+    cur = torch.cuda.current_stream(main.device)
+    qs = q_side_stream(main)   # the Q heads' dense Adam sweeps beside the trunk's (qlearn.double_q_step)
+    qs.wait_stream(cur)
+    with torch.cuda.stream(qs):
+        for qh in main.q_heads:
+            qh.adam(adam6, tag)
     dh = main.dh_buffer(B)
     with region("comm_dh"):
         comm.reduce_scatter(dh, dH_all)
@@ -312,9 +319,8 @@ def sharded_double_q_step(nets, clocks, k, s, a, r, s_next, true_len, true_next_
     works = main.trunk.allreduce_start(comm)
     if not fused:
         _sharded_ce_dw_adam(main, sup, w, lse, tgt_loc, H_all, adam6, st)
-    for qh in main.q_heads:
-        qh.adam(adam6, tag)
     main.trunk.adam_after_allreduce(adam6, works)   # (waits for the all-reduce on the trunk's side stream)
+    cur.wait_stream(qs)
     return sup_loss, q_loss
 
 
