@@ -577,7 +577,7 @@ def main():
                 # whole table: it is not item-sharded)
                 tr2 = make_trainer("c2s", args, dev, False)
                 tr2.set_train()
-                _, _, k2, _ = timed_run(tr2, batches, min(2, args.warmup), min(10, args.steps), world, True, "c2")
+                _, _, k2, _ = timed_run(tr2, batches, min(5, args.warmup), min(30, args.steps), world, True, "c2")
                 target = target_step(k2, T, B, args.negatives, E, E, 1, terms)
                 if target is not None and world > 1:
                     by_sum, = max_over_ranks([float(target["bytes_per_step"])], op="sum")
