@@ -455,7 +455,9 @@ def harness_run(tr, batches, n, args, item_counts):
             "update_train_metrics_ms": round(float(np.median(tm)), 3),
             "value": round(B / (float(np.median(ta)) * 1e-3), 2), "unit": "session-steps/sec", "batches": n - 1,
             "note": "median per batch of train_step + update_train_metrics (trainGRU.py:195-224), after 1 untimed "
-                    "batch; metrics: HR/NDCG@[10,20], coverage [1,5,10], div/nov top-1"}
+                    "batch; metrics: HR/NDCG@[10,20], coverage [1,5,10], div/nov top-1; update_train_metrics_ms is "
+                    "the host time from train_step's return (at its loss readout, the backward still queued) to "
+                    "the metrics, so it includes the step's remaining GPU work"}
 
 
 def main():

@@ -53,22 +53,21 @@ def fused_scoring(head, K):
     return head.HF in (32, 64, 128, 256) and K <= min(32, head.A)
 
 
-def score_rows(head, h, K, tgt=None):
-    """(idx (B, K) int32, vals (B, K), loss_row (B,) or None, err flag tensor):
-    the canonical top-K and per-row CE of h's logits without a (B, A) buffer.
-    Without targets (update_train_metrics) the chunk maxima come from the
-    3-product screening pass; a row whose screening error band holds more
-    candidate chunks than the cap sends the batch back through the exact
-    6-product scoring (one host read of the flag)."""
+def score_rows(head, h, K, tgt=None, screen=True):
+    """(idx (B, K) int32, vals (B, K), loss_row (B,) or None, err flag tensor,
+    screened): the canonical top-K and per-row CE of h's logits without a
+    (B, A) buffer.  Without targets (update_train_metrics) the chunk maxima
+    come from the 3-product screening pass (screened = True); a row whose
+    screening error band holds more candidate chunks than the cap sets the
+    flag, and the caller (eval_batch, which reads the flag once at its end)
+    re-runs the batch through the exact 6-product scoring (screen=False)."""
     B = h.shape[0]
     if fused_scoring(head, K):
-        if tgt is None:
+        if tgt is None and screen:
             idx, vals, _ = head.score_topk(h, K, None, screen=True)
-            if not int(head.top_err.item()):
-                return idx, vals, None, head.top_err
-            head.top_err.zero_()
+            return idx, vals, None, head.top_err, True
         idx, vals, loss_row = head.score_topk(h, K, tgt)
-        return idx, vals, loss_row, head.top_err
+        return idx, vals, loss_row, head.top_err, False
     # stored-logit fallback, row-chunked
     st = stream_ptr()
     dev = head.device
@@ -93,11 +92,11 @@ def score_rows(head, h, K, tgt=None):
     # no Zᵀ stays cached after the batch (the caching allocator reuses the block)
     for k in [k for k in head._ws if k[0] == "eval_chunk"]:
         del head._ws[k]
-    return idx, vals, loss_row, err
+    return idx, vals, loss_row, err, False
 
 
 def eval_batch(model, s, s_len, a, *, head_idx=0, K=20, ks=(20,), padding_pos="end", div_table=None, k_div=1,
-               bitmap=None, k_nov=1, nov_reward=1.0, want_loss=True, lut=None, rep_ks=None):
+               bitmap=None, k_nov=1, nov_reward=1.0, want_loss=True, lut=None, rep_ks=None, screen=True):
     """CE loss, top-K, HR/NDCG sums and reward sums of one batch, on the
     device.  ``lut`` (recommenders/hip/remap.py): the top-K ids are mapped to
     the input vocabulary for the diversity reward and returned as ``idx_in``
@@ -111,7 +110,7 @@ def eval_batch(model, s, s_len, a, *, head_idx=0, K=20, ks=(20,), padding_pos="e
     st = stream_ptr()
     h = model.hidden(s, s_len, slot="eval", save=False)
     head = head_for(model, head_idx)
-    idx, vals, loss_row, top_err = score_rows(head, h, K, a if want_loss else None)
+    idx, vals, loss_row, top_err, screened = score_rows(head, h, K, a if want_loss else None, screen=screen)
     out = EvalBatch()
     out.loss = None
     if want_loss:
@@ -148,8 +147,12 @@ def eval_batch(model, s, s_len, a, *, head_idx=0, K=20, ks=(20,), padding_pos="e
         call("rg_repetitions", s.data_ptr(), s.shape[1], out.idx_in.data_ptr(), K, B, kh, len(rep_ks),
              reps.data_ptr(), st)
         out.reps = reps
-    if int(top_err.item()):
+    if int(top_err.item()):   # the batch's one host read of the flag
         top_err.zero_()
+        if screened:   # a screening band overflowed: the whole batch again on the exact scoring
+            return eval_batch(model, s, s_len, a, head_idx=head_idx, K=K, ks=ks, padding_pos=padding_pos,
+                              div_table=div_table, k_div=k_div, bitmap=bitmap, k_nov=k_nov, nov_reward=nov_reward,
+                              want_loss=want_loss, lut=lut, rep_ks=rep_ks, screen=False)
         raise RuntimeError("top-k candidate overflow (massive exact ties in the logits)")
     if rerr is not None and int(rerr.item()):
         from .remap import RemapError
