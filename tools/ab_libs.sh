@@ -1,6 +1,6 @@
 #!/bin/bash
 # same-box comparison of the in-tree library and variant libraries on a short bench:
-# LIBS="variants/lib_a.so variants/lib_b.so", CFG (default c2), two rounds
+# LIBS="abvar/lib_a.so abvar/lib_b.so", CFG (default c2), two rounds
 set -o pipefail
 for r in 1 2; do
   for v in "" $LIBS; do
