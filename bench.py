@@ -22,9 +22,10 @@ Configs: c2 (headline), c3 (BidirGRU4Rec, 2048 sampled negatives),
 c4 (SMORL: GRU4Rec trunk + supervised head + 3 Q heads, 3-reward double-Q),
 c5 (IKEA scale: SMORL at 5M items, d256, seq_len <= 100, global batch 8192
 split over the ranks, fp16 item table; fits one MI355X at ~279 GiB peak).
-Multi-GPU (torch.distributed.run, one rank per GPU, RCCL): weak scaling, each
-rank trains its own 4096-row batch shard, item tables sharded over the ranks
-(DESIGN.md §5).
+Multi-GPU (torch.distributed.run, one rank per GPU, RCCL), item tables
+sharded over the ranks: c2 weak scaling (each rank trains its
+own 4096-row batch shard); c4 / c5 strong scaling (their global batch, 4096 /
+8192, split over the ranks: per_rank_batch).
 """
 from __future__ import annotations
 
@@ -67,8 +68,11 @@ def parse():
     # reference materialises the 16.4 GB logits, their log_softmax and grads),
     # else 512; plus the C1 line (BASELINE configs[0], 100 steps)
     ap.add_argument("--cpu-batch", type=int, default=0, help="0: 4096 if host RAM >= 96 GiB else 512")
-    ap.add_argument("--cpu-steps", type=int, default=0, help="timed CPU steps (0: 2 at batch 4096, 6 below)")
+    ap.add_argument("--cpu-steps", type=int, default=0,
+                    help="timed CPU steps after 1 warm-up (0: 3 for c2 at batch 4096 (BASELINE.md §3), 6 below; "
+                         "2 for c3 / c4)")
     ap.add_argument("--c1-steps", type=int, default=100)
+    ap.add_argument("--c1-warmup", type=int, default=10)
     ap.add_argument("--harness-steps", type=int, default=10,
                     help="C2: per-batch train_step + update_train_metrics as trainGRU.py:195-224 runs them")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -117,47 +121,95 @@ def cpu_model():
 
 
 # ------------------------------------------------------------ CPU leg ------
-def _cpu_run(items, dim, seq, B, steps, seed):
-    """Oracle GRU4Rec steps on the host: (per-step seconds after 1 warm-up)."""
-    from oracle.models import OracleSupervised
+def host_threads():
+    """(threads the CPU leg uses, how they were found): the CPUs this process
+    may run on (sched_getaffinity), capped by a cgroup CPU quota when one is
+    set (a GPU box's share of a larger host)."""
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+            if q != "max":
+                quota = max(1, int(-(-int(q) // int(per))))
+    except (OSError, ValueError):
+        pass
+    n = min(aff, quota) if quota else aff
+    return n, {"affinity_cpus": aff, "cgroup_cpu_quota": quota, "os_cpu_count": os.cpu_count()}
+
+
+def _cpu_oracle(cfg, items, dim, seq, counts=None):
+    from oracle.models import OracleSMORL, OracleSupervised
+    common = dict(hidden_dim=dim, embedding_dim=dim, train_pad_embed=True, use_packed_seq=True, learning_rate=0.01,
+                  item_num=items, state_size=seq, action_dim=items)
+    if cfg in ("c2", "c1"):
+        return OracleSupervised(kind="gru4rec", gru_layers=1, **common)
+    if cfg == "c3":
+        return OracleSupervised(kind="bidir", gru_layers=1, dropout=0.0, n_negatives=2048, **common)
+    from recommenders.data_utils.synthetic import unpopular_items
+    g = torch.Generator().manual_seed(7)
+    div = torch.randn(items + 1, 64, generator=g) * 0.01
+    return OracleSMORL(padding_pos="end", gamma=0.5, gru_layers=1, q_weights=[1.0, 1.0, 1.0], alpha=1.0,
+                       div_embedding=div, unpopular_actions_set=unpopular_items(counts), topk_div=1,
+                       topk_nov=1, nov_rew_sig=1.0, **common)
+
+
+def _cpu_run(cfg, items, dim, seq, B, steps, seed, warmup=1):
+    """Oracle steps of config ``cfg`` on the host: per-step seconds after
+    ``warmup`` untimed steps."""
     from recommenders.data_utils.synthetic import SessionStream
-    orc = OracleSupervised(kind="gru4rec", hidden_dim=dim, embedding_dim=dim, gru_layers=1, train_pad_embed=True,
-                           use_packed_seq=True, learning_rate=0.01, item_num=items, state_size=seq, action_dim=items)
-    st = SessionStream(items, seq, B * (steps + 1), seed=seed)
-    b = st.batch(0, B)
-    orc.step(b[0], b[1], b[4])  # warm-up
-    times = []
-    for i in range(1, steps + 1):
+    st = SessionStream(items, seq, B * (steps + warmup), seed=seed)
+    orc = _cpu_oracle(cfg, items, dim, seq, st.item_counts())
+
+    def one(i):
         b = st.batch(i, B)
+        return orc.step(*b) if cfg == "c4" else orc.step(b[0], b[1], b[4])
+    for i in range(warmup):
+        one(i)
+    times = []
+    for i in range(warmup, warmup + steps):
         t0 = time.perf_counter()
-        orc.step(b[0], b[1], b[4])
+        one(i)
         times.append(time.perf_counter() - t0)
     return times
 
 
-def cpu_baseline(args):
+CPU_NAMES = {"c2": "GRU4Rec", "c3": "BidirGRU4Rec (2048 shared sampled negatives, dropout 0)",
+             "c4": "SMORL_trainer (sup head + 3 Q heads, 3 rewards, topk 1)"}
+
+
+def cpu_baseline(args, cfg="c2"):
     """The reference's per-step math on PyTorch-CPU (oracle/, restatement pinned
-    to the reference's golden vectors), timed on this host: the C2 workload
-    (same items, dims, seq_len; batch 4096 when the host RAM allows it, SURVEY
-    §8d) and the C1 line (BASELINE configs[0]: 10k items, dim32, L<=20,
-    batch 64, --c1-steps steps)."""
-    threads = torch.get_num_threads()
+    to the reference's golden vectors), timed on this host with every CPU the
+    process may use (host_threads): the config's workload at its items, dims
+    and seq_len — C2 at batch 4096 when the host RAM allows it (1
+    warm-up + 3 timed steps), C3 at batch 4096 and C4 at batch
+    512 (2 timed steps each: one C4 step scores 1M items for the supervised
+    head and the Q target) — plus, with C2, the C1 line (BASELINE configs[0]:
+    10k items, dim32, L<=20, batch 64, --c1-warmup + --c1-steps steps)."""
+    threads, how = host_threads()
+    torch.set_num_threads(threads)
     ram = host_ram_gib()
-    B = args.cpu_batch or (4096 if ram is not None and ram >= 96 else 512)
-    steps = args.cpu_steps or (2 if B >= 4096 else 6)
-    times = _cpu_run(args.items, args.dim, args.seq, B, steps, 2)
+    if cfg == "c2":
+        B = args.cpu_batch or (4096 if ram is not None and ram >= 96 else 512)
+        steps = args.cpu_steps or (3 if B >= 4096 else 6)
+    else:
+        B = args.cpu_batch or (4096 if cfg == "c3" else 512)
+        steps = args.cpu_steps or 2
+    times = _cpu_run(cfg, args.items, args.dim, args.seq, B, steps, 2)
     dt = float(np.sum(times))
-    out = {"value": round(B * steps / dt, 2), "unit": "session-steps/sec", "cores": threads,
-           "cpu_model": cpu_model(), "host_ram_gib": ram, "kind": "port",
+    out = {"value": round(B * steps / dt, 2), "unit": "session-steps/sec", "cores": threads, "threads": how,
+           "cpu_model": cpu_model(), "host_ram_gib": ram, "kind": "port", "batch": B, "steps": steps,
            "median_ms_per_step": round(float(np.median(times)) * 1e3, 1),
-           "sample": (f"oracle (reference PyTorch-CPU math) GRU4Rec {args.items} items dim{args.dim} "
-                      f"L<={args.seq}, batch {B}, {steps} timed steps after 1 warm-up, "
-                      f"{threads} threads, {dt:.1f} s")}
-    if args.c1_steps > 0:
-        t1 = _cpu_run(10_000, 32, 20, 64, args.c1_steps, 1)
+           "sample": (f"oracle (reference PyTorch-CPU math) {CPU_NAMES[cfg]} {args.items} items dim{args.dim} "
+                      f"L<={args.seq}, batch {B}{'' if B == args.batch else ' (reduced)'}, {steps} timed steps after "
+                      f"1 warm-up, torch.set_num_threads({threads}), {dt:.1f} s")}
+    if cfg == "c2" and args.c1_steps > 0:
+        t1 = _cpu_run("c1", 10_000, 32, 20, 64, args.c1_steps, 1, warmup=args.c1_warmup)
         d1 = float(np.sum(t1))
         out["c1"] = {"value": round(64 * args.c1_steps / d1, 2), "unit": "session-steps/sec",
                      "ms_per_step": round(d1 / args.c1_steps * 1e3, 3), "steps": args.c1_steps,
+                     "warmup": args.c1_warmup,
                      "workload": "GRU4Rec 10k items, dim32, seq_len<=20, batch 64 (BASELINE configs[0]), "
                                  f"{threads} threads"}
     return out
@@ -460,6 +512,19 @@ def harness_run(tr, batches, n, args, item_counts):
                     "the metrics, so it includes the step's remaining GPU work"}
 
 
+def per_rank_batch(config, batch, world):
+    """Rows each rank trains per step.  C4 / C5 name a GLOBAL batch on 8 GPUs
+    (BASELINE configs[3]: batch 4096 embedding-sharded across 8×MI355X, SURVEY
+    §8e: B/8 = 512 sessions per rank; configs[4]: batch 8192), so their ranks
+    split it (strong scaling); C2 / C3 are 1-GPU configs whose multi-GPU lines
+    keep the batch per GPU (weak scaling)."""
+    if config in ("c4", "c5"):
+        if batch % (32 * world):
+            raise SystemExit(f"{config}: the global batch must split into multiples of 32 rows per rank")
+        return batch // world
+    return batch
+
+
 def main():
     args = parse()
     act = check_world(args)
@@ -478,16 +543,13 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if args.config == "c5":
-        # BASELINE configs[4]: 5M items, d256, seq_len <= 100, batch 8192 (global:
-        # each of the N ranks trains 8192 / N rows), fp16 item table; flags that
-        # were left at the C2 defaults take the C5 values
+        # BASELINE configs[4]: 5M items, d256, seq_len <= 100, batch 8192, fp16
+        # item table; flags that were left at the C2 defaults take the C5 values
         for k, c2v, c5v in (("items", ITEMS, 5_000_000), ("dim", DIM, 256), ("seq", SEQ, 100),
                             ("batch", BATCH, 8192)):
             if getattr(args, k) == c2v:
                 setattr(args, k, c5v)
-        if args.batch % (32 * world):
-            raise SystemExit("c5: the global batch must split into multiples of 32 rows per rank")
-        args.batch //= world
+    args.batch = per_rank_batch(args.config, args.batch, world)
     shard = (world > 1 or args.force_shard) and args.config in ("c2", "c4", "c5")
     if world > 1 or args.force_shard:
         import torch.distributed as dist
@@ -616,8 +678,8 @@ def main():
             torch.distributed.destroy_process_group()
         return
     cpu = None
-    if world == 1 and not args.no_cpu_baseline and args.config == "c2":
-        cpu = cpu_baseline(args)
+    if world == 1 and not args.no_cpu_baseline and args.config in ("c2", "c3", "c4"):
+        cpu = cpu_baseline(args, args.config)
         if ev is not None and dev_idx is not None and parity_net is not None:
             cpu["hr_ndcg_parity"] = cpu_eval_parity(parity_net, held, dev_idx)
     if args.config == "c2":
@@ -629,8 +691,8 @@ def main():
                     f"negatives (sampled softmax), dropout 0")
     elif args.config == "c4":
         metric = "session-steps/sec, SMORL (SQN double-Q, 3 rewards) 1M items, dim128, batch 4096"
-        workload = (f"SMORL_trainer {N} items, dim{E}, seq_len<={L}, batch {B}/GPU, sup head + Q heads acc/div/nov, "
-                    f"topk_div=topk_nov=1, q_weights [1,1,1], gamma 0.5, alpha 1")
+        workload = (f"SMORL_trainer {N} items, dim{E}, seq_len<={L}, global batch {B * world} ({B}/GPU), sup head + "
+                    f"Q heads acc/div/nov, topk_div=topk_nov=1, q_weights [1,1,1], gamma 0.5, alpha 1")
     else:
         metric = "session-steps/sec, IKEA-scale SMORL (SQN double-Q, 3 rewards) 5M items, dim256, batch 8192"
         workload = (f"SMORL_trainer {N} items, dim{E}, seq_len<={L}, global batch {B * world} ({B}/GPU), fp16 item "
@@ -641,7 +703,7 @@ def main():
         "metric": metric,
         "value": round(value, 2), "unit": "session-steps/sec", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True,
-        "scaling": "strong" if args.config == "c5" else "weak",
+        "scaling": "strong" if args.config in ("c4", "c5") else "weak",
         "vs_baseline": None, "dtype": "f32", "matmul_precision": args.precision,
         "data": "synthetic (seeded Zipf session stream, random-init weights)",
         "config": {"workload": workload,

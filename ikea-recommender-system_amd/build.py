@@ -33,8 +33,8 @@ def hipcc():
 
 def _compile(src):
     obj = os.path.join(OBJ, os.path.basename(src).replace(".hip", ".o"))
-    if os.path.exists(obj) and os.path.getmtime(obj) >= max(
-            os.path.getmtime(src), os.path.getmtime(os.path.join(CSRC, "common.h"))):
+    headers = [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".h")]
+    if os.path.exists(obj) and os.path.getmtime(obj) >= max(os.path.getmtime(p) for p in [src, *headers]):
         return obj
     cmd = [hipcc(), *FLAGS, "-I", CSRC, "-c", src, "-o", obj]
     r = subprocess.run(cmd, capture_output=True, text=True)

@@ -39,6 +39,7 @@
 // with 16-byte LDS-DMA (global_load_lds_dwordx4) and are read back by
 // ds_read_b128.
 #include "common.h"
+#include "topk_scan.h"
 
 #define NEG_INF (-__builtin_inff())
 
@@ -975,7 +976,7 @@ __device__ __forceinline__ void tk_insert(float (&t)[TK_MAX], float v) {
 // Stage 1: grid (row blocks of 64, P parts of the chunk range), lane = row,
 // the 4 waves interleave the part's chunks; each wave keeps its top-K, the
 // part's top-K (merged in LDS) goes to part[p][i][row].
-__global__ __launch_bounds__(256) void k_topk_part(const float* __restrict__ cmax, int nct, int B, int K,
+__global__ __launch_bounds__(256) void k_topk_part(const float* __restrict__ cmax, int nct, int ldc, int B, int K,
                                                    float* __restrict__ part) {
   __shared__ float st[4][TK_MAX][64];
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -992,7 +993,7 @@ __global__ __launch_bounds__(256) void k_topk_part(const float* __restrict__ cma
 #pragma unroll
     for (int u = 0; u < 4; ++u) {   // four independent loads in flight per lane
       const int cc = c + 4 * u;
-      v[u] = (ok && cc < c1) ? cmax[(int64_t)cc * B + row] : NEG_INF;
+      v[u] = (ok && cc < c1) ? cmax[(int64_t)cc * ldc + row] : NEG_INF;
     }
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
@@ -1021,7 +1022,7 @@ __global__ __launch_bounds__(256) void k_topk_part(const float* __restrict__ cma
     if (ok)
 #pragma unroll
       for (int i = 0; i < TK_MAX; ++i)
-        if (i < K) part[((int64_t)blockIdx.y * K + i) * B + row] = t[i];
+        if (i < K) part[((int64_t)blockIdx.y * K + i) * ldc + row] = t[i];
   }
 }
 
@@ -1030,7 +1031,7 @@ __global__ __launch_bounds__(256) void k_topk_part(const float* __restrict__ cma
 // maxima exist: every chunk is then a candidate); ncand := 0.  With wnorm
 // (screened chunk maxima, 3 plane products): tol_abs = tol·||h_b||_2·wnorm[0]
 // per row — the screening argmax's bound (rg_flash_argmax_exact).
-__global__ void k_topk_lim(const float* __restrict__ part, int P, int K, int B, float tol_abs, float tol_rel,
+__global__ void k_topk_lim(const float* __restrict__ part, int P, int K, int ldc, int B, float tol_abs, float tol_rel,
                            float* __restrict__ lim, int32_t* __restrict__ ncand, const float* __restrict__ h, int HF,
                            const float* __restrict__ wnorm) {
   const int row = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1045,7 +1046,7 @@ __global__ void k_topk_lim(const float* __restrict__ part, int P, int K, int B, 
   for (int i = 0; i < TK_MAX; ++i) t[i] = NEG_INF;
   float thr = NEG_INF;
   for (int j = 0; j < P * K; ++j) {
-    const float v = part[(int64_t)j * B + row];
+    const float v = part[(int64_t)j * ldc + row];
     if (v > thr) {
       tk_insert(t, v);
 #pragma unroll
@@ -1057,53 +1058,53 @@ __global__ void k_topk_lim(const float* __restrict__ part, int P, int K, int B, 
   ncand[row] = 0;
 }
 
-// one workgroup (256 threads) per row: fp32 logits of the candidate items,
-// canonical top-K.  The dot is the native fp32 head's own chain (csrc/head.hip
+// The fp32 logit of one item: the native fp32 head's own chain (csrc/head.hip
 // k_head_fwd*: v_mfma_f32_32x32x2_f32 with k = s from lane half 0 and k =
 // HF/2 + s from half 1, i.e. fmaf over s of (h[s]·w[s], then h[HF/2+s]·w[HF/2+s]),
 // then + bias), so a re-scored logit is bitwise the one the model's forward()
 // stores and the top-K equals the canonical top-K of those logits.
-// A row with more than TK_CAP candidate chunks (a tie run past the cap) keeps
-// the caller's result and, with err, raises the overflow flag.
+__device__ __forceinline__ float head_logit(const float* hs, const float* __restrict__ W,
+                                            const float* __restrict__ bias, int item, int HF) {
+  const f4* wr = reinterpret_cast<const f4*>(W + (int64_t)item * HF);
+  const int kh4 = HF / 8;   // float4s per half
+  float acc = 0.f;
+  for (int s4 = 0; s4 < kh4; ++s4) {
+    const f4 xa = wr[s4], xb = wr[kh4 + s4];
+    const int ka = 4 * s4, kb = HF / 2 + 4 * s4;
+    acc = fmaf(hs[ka], xa[0], acc);
+    acc = fmaf(hs[kb], xb[0], acc);
+    acc = fmaf(hs[ka + 1], xa[1], acc);
+    acc = fmaf(hs[kb + 1], xb[1], acc);
+    acc = fmaf(hs[ka + 2], xa[2], acc);
+    acc = fmaf(hs[kb + 2], xb[2], acc);
+    acc = fmaf(hs[ka + 3], xa[3], acc);
+    acc = fmaf(hs[kb + 3], xb[3], acc);
+  }
+  return acc + bias[item];
+}
+
+__device__ __forceinline__ bool tk_overflow(int nc) { return nc < 0 || nc > TK_CAP; }
+
+// one workgroup (256 threads) per row: fp32 logits (head_logit) of the
+// candidate items, canonical top-K.  A row with more than TK_CAP candidate
+// chunks (a tie run past the cap) is left to k_flash_topk_scan.
 __global__ __launch_bounds__(256) void k_flash_topk_eval(const float* __restrict__ h, const float* __restrict__ W,
                                                          const float* __restrict__ bias, const int32_t* __restrict__ cand,
                                                          const int32_t* __restrict__ ncand, int A, int HF, int K,
-                                                         int32_t* __restrict__ out_idx, float* __restrict__ out_val,
-                                                         int32_t* __restrict__ err) {
+                                                         int32_t* __restrict__ out_idx, float* __restrict__ out_val) {
   __shared__ __attribute__((aligned(16))) float hs[256];
   __shared__ float cv[TK_CAP * 32];
   __shared__ int ci[TK_CAP * 32];
   __shared__ float rv[4];
   __shared__ int ri[4], rs[4];
   const int row = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  if (ncand[row] < 0 || ncand[row] > TK_CAP) {   // overflow: the caller's result stays
-    if (err && threadIdx.x == 0) atomicOr(err, 1);
-    return;
-  }
+  if (tk_overflow(ncand[row])) return;
   for (int k = tid; k < HF; k += 256) hs[k] = h[(int64_t)row * HF + k];
   const int n = ncand[row] * 32;
   __syncthreads();
   for (int e = tid; e < n; e += 256) {
     const int item = cand[(int64_t)row * TK_CAP + (e >> 5)] * 32 + (e & 31);
-    float z = NEG_INF;
-    if (item < A) {
-      const f4* wr = reinterpret_cast<const f4*>(W + (int64_t)item * HF);
-      const int kh4 = HF / 8;   // float4s per half
-      float acc = 0.f;
-      for (int s4 = 0; s4 < kh4; ++s4) {
-        const f4 xa = wr[s4], xb = wr[kh4 + s4];
-        const int ka = 4 * s4, kb = HF / 2 + 4 * s4;
-        acc = fmaf(hs[ka], xa[0], acc);
-        acc = fmaf(hs[kb], xb[0], acc);
-        acc = fmaf(hs[ka + 1], xa[1], acc);
-        acc = fmaf(hs[kb + 1], xb[1], acc);
-        acc = fmaf(hs[ka + 2], xa[2], acc);
-        acc = fmaf(hs[kb + 2], xb[2], acc);
-        acc = fmaf(hs[ka + 3], xa[3], acc);
-        acc = fmaf(hs[kb + 3], xb[3], acc);
-      }
-      z = acc + bias[item];
-    }
+    const float z = item < A ? head_logit(hs, W, bias, item, HF) : NEG_INF;
     cv[e] = z;
     ci[e] = item < A ? item : INT32_MAX;
   }
@@ -1151,6 +1152,34 @@ __global__ __launch_bounds__(256) void k_flash_topk_eval(const float* __restrict
   }
 }
 
+// the overflowed rows of k_flash_topk_eval (ncand > TK_CAP): every item of
+// the row re-scored by head_logit, canonical top-K (topk_scan.h); every other
+// row's workgroup exits at once.  err (optional) counts the rows scanned.
+struct HeadRowSrc {
+  const float* h;
+  const float* W;
+  const float* bias;
+  float* hs;
+  int HF;
+  __device__ void prepare(int row) {
+    for (int k = threadIdx.x; k < HF; k += 256) hs[k] = h[(int64_t)row * HF + k];
+    __syncthreads();
+  }
+  __device__ float operator()(int item) const { return head_logit(hs, W, bias, item, HF); }
+};
+
+__global__ __launch_bounds__(256) void k_flash_topk_scan(const float* __restrict__ h, const float* __restrict__ W,
+                                                         const float* __restrict__ bias, const int32_t* __restrict__ ncand,
+                                                         int A, int HF, int K, int32_t* __restrict__ out_idx,
+                                                         float* __restrict__ out_val, int32_t* __restrict__ err) {
+  __shared__ __attribute__((aligned(16))) float hs[256];
+  const int row = blockIdx.x;
+  if (!tk_overflow(ncand[row])) return;
+  if (err && threadIdx.x == 0) atomicAdd(err, 1);
+  HeadRowSrc src{h, W, bias, hs, HF};
+  topk_scan_row(src, row, A, K, out_idx, out_val);
+}
+
 // out[0] = max_a ||W_a||_2 (float bits ordered as uint: max is order-independent);
 // out[0] must be 0 on entry.  32 lanes per row, HF / 4 <= 64 float4s per row.
 __global__ __launch_bounds__(256) void k_row_norm_max(const float* __restrict__ W, int64_t A, int HF,
@@ -1187,7 +1216,7 @@ __global__ void k_amax_lim(const float* __restrict__ best, const float* __restri
 // candidate chunks (cmax >= lim) of every row, chunk range split over grid.y;
 // appended in any order through a per-row counter (the re-scoring keeps the
 // first maximum by (value, item), so the order does not matter)
-__global__ __launch_bounds__(256) void k_amax_cand(const float* __restrict__ cmax, int nct, int B,
+__global__ __launch_bounds__(256) void k_amax_cand(const float* __restrict__ cmax, int nct, int ldc, int B,
                                                    const float* __restrict__ lim, int32_t* __restrict__ cand,
                                                    int32_t* __restrict__ ncand) {
   const int row = blockIdx.x * 256 + threadIdx.x;
@@ -1196,7 +1225,7 @@ __global__ __launch_bounds__(256) void k_amax_cand(const float* __restrict__ cma
   const int c0 = blockIdx.y * per, c1 = min(nct, c0 + per);
   const float l = lim[row];
   for (int c = c0; c < c1; ++c) {
-    if (cmax[(int64_t)c * B + row] >= l) {
+    if (cmax[(int64_t)c * ldc + row] >= l) {
       const int p = atomicAdd(&ncand[row], 1);
       if (p < TK_CAP) cand[(int64_t)row * TK_CAP + p] = c;
     }
@@ -1435,43 +1464,49 @@ extern "C" int64_t rg_flash_topk_work_bytes(int B, int A, int K) {
   return ((int64_t)topk_parts(B, (A + 31) / 32) * K * B + B) * 4;
 }
 
-static int flash_topk(const float* cmax, int B, int A, int K, float tol_abs, float tol_rel, const float* wnorm,
+// rows [0, B) of a chunk whose chunk maxima have row stride ldc >= B (cmax:
+// ceil(A/32) × ldc; work sized for ldc rows, rg_flash_topk_work_bytes(ldc, …))
+static int flash_topk(const float* cmax, int ldc, int B, int A, int K, float tol_abs, float tol_rel, const float* wnorm,
                       const float* h, const float* W, const float* bias, int HF, int32_t* cand, int32_t* ncand,
                       int32_t* out_idx, float* out_val, int32_t* err, void* work, hipStream_t stream) {
-  if (B <= 0 || A <= 0 || K <= 0 || K > TK_MAX || K > A || HF <= 0 || HF > 256 || (HF % 8)) return RG_ERR_ARG;
-  if (!cmax || !h || !W || !bias || !cand || !ncand || !out_idx || !err || !work) return RG_ERR_ARG;
+  if (B <= 0 || ldc < B || A <= 0 || K <= 0 || K > TK_MAX || K > A || HF <= 0 || HF > 256 || (HF % 8))
+    return RG_ERR_ARG;
+  if (!cmax || !h || !W || !bias || !cand || !ncand || !out_idx || !work) return RG_ERR_ARG;
   const int nct = (A + 31) / 32;
-  const int P = topk_parts(B, nct);
+  const int P = topk_parts(ldc, nct);
   float* part = (float*)work;
-  float* lim = part + (int64_t)P * K * B;
-  hipLaunchKernelGGL(k_topk_part, dim3((B + 63) / 64, P), dim3(256), 0, stream, cmax, nct, B, K, part);
-  hipLaunchKernelGGL(k_topk_lim, dim3((B + 255) / 256), dim3(256), 0, stream, part, P, K, B, tol_abs, tol_rel, lim,
-                     ncand, h, HF, wnorm);
+  float* lim = part + (int64_t)P * K * ldc;
+  hipLaunchKernelGGL(k_topk_part, dim3((B + 63) / 64, P), dim3(256), 0, stream, cmax, nct, ldc, B, K, part);
+  hipLaunchKernelGGL(k_topk_lim, dim3((B + 255) / 256), dim3(256), 0, stream, part, P, K, ldc, B, tol_abs, tol_rel,
+                     lim, ncand, h, HF, wnorm);
   const int ys = max(1, min(256, 2048 / ((B + 255) / 256)));   // ~2048 workgroups over the chunk range
-  hipLaunchKernelGGL(k_amax_cand, dim3((B + 255) / 256, ys), dim3(256), 0, stream, cmax, nct, B, lim, cand, ncand);
+  hipLaunchKernelGGL(k_amax_cand, dim3((B + 255) / 256, ys), dim3(256), 0, stream, cmax, nct, ldc, B, lim, cand,
+                     ncand);
   hipLaunchKernelGGL(k_flash_topk_eval, dim3(B), dim3(256), 0, stream, h, W, bias, cand, ncand, A, HF, K, out_idx,
-                     out_val, err);
+                     out_val);
+  hipLaunchKernelGGL(k_flash_topk_scan, dim3(B), dim3(256), 0, stream, h, W, bias, ncand, A, HF, K, out_idx, out_val,
+                     err);
   RG_LAUNCH_CHECK();
   return RG_OK;
 }
 
-extern "C" int rg_flash_topk(const float* cmax, int B, int A, int K, float tol_abs, float tol_rel, const float* h,
-                             const float* W, const float* bias, int HF, int32_t* cand, int32_t* ncand, int32_t* out_idx,
-                             float* out_val, int32_t* err, void* work, hipStream_t stream) {
-  return flash_topk(cmax, B, A, K, tol_abs, tol_rel, nullptr, h, W, bias, HF, cand, ncand, out_idx, out_val, err, work,
-                    stream);
+extern "C" int rg_flash_topk(const float* cmax, int ldc, int B, int A, int K, float tol_abs, float tol_rel,
+                             const float* h, const float* W, const float* bias, int HF, int32_t* cand, int32_t* ncand,
+                             int32_t* out_idx, float* out_val, int32_t* err, void* work, hipStream_t stream) {
+  return flash_topk(cmax, ldc, B, A, K, tol_abs, tol_rel, nullptr, h, W, bias, HF, cand, ncand, out_idx, out_val, err,
+                    work, stream);
 }
 
 // Top-K from SCREENED chunk maxima (rg_flash_amax_screen: 3 plane products):
 // candidates within tol·||h_b||_2·wnorm[0] + 1e-6·|tau| of tau (wnorm from
-// rg_row_norm_max), re-scored exactly as rg_flash_topk; a candidate overflow
-// sets err (the caller re-scores the batch at 6 products).
-extern "C" int rg_flash_topk_screened(const float* cmax, int B, int A, int K, float tol, const float* wnorm,
+// rg_row_norm_max), re-scored exactly as rg_flash_topk (a row past the
+// candidate cap is scanned whole, as there).
+extern "C" int rg_flash_topk_screened(const float* cmax, int ldc, int B, int A, int K, float tol, const float* wnorm,
                                       const float* h, const float* W, const float* bias, int HF, int32_t* cand,
                                       int32_t* ncand, int32_t* out_idx, float* out_val, int32_t* err, void* work,
                                       hipStream_t stream) {
   if (!wnorm) return RG_ERR_ARG;
-  return flash_topk(cmax, B, A, K, tol, 1e-6f, wnorm, h, W, bias, HF, cand, ncand, out_idx, out_val, err, work,
+  return flash_topk(cmax, ldc, B, A, K, tol, 1e-6f, wnorm, h, W, bias, HF, cand, ncand, out_idx, out_val, err, work,
                     stream);
 }
 
@@ -1638,16 +1673,20 @@ extern "C" int rg_row_norm_max(const float* W, int64_t A, int HF, float* out, hi
 
 extern "C" int rg_flash_argmax_exact(const float* cmax, int B, int A, const float* h, const float* W, const float* bias,
                                      int HF, const float* wnorm, float tol, float* lim, int32_t* cand, int32_t* ncand,
-                                     int32_t* out_idx, float* out_val, hipStream_t stream) {
+                                     int32_t* out_idx, float* out_val, int32_t* err, hipStream_t stream) {
   if (B <= 0 || A <= 0 || HF <= 0 || HF > 256 || (HF % 8)) return RG_ERR_ARG;
   if (!cmax || !h || !W || !bias || !wnorm || !lim || !cand || !ncand || !out_idx || !out_val) return RG_ERR_ARG;
   const int nct = (A + 31) / 32;
   if (hipMemsetAsync(ncand, 0, sizeof(int32_t) * B, stream) != hipSuccess) return RG_ERR_LAUNCH;
   hipLaunchKernelGGL(k_amax_lim, dim3((B + 255) / 256), dim3(256), 0, stream, out_val, h, B, HF, wnorm, tol, lim);
   const int ys = max(1, min(256, 2048 / ((B + 255) / 256)));   // ~2048 workgroups
-  hipLaunchKernelGGL(k_amax_cand, dim3((B + 255) / 256, ys), dim3(256), 0, stream, cmax, nct, B, lim, cand, ncand);
+  hipLaunchKernelGGL(k_amax_cand, dim3((B + 255) / 256, ys), dim3(256), 0, stream, cmax, nct, B, B, lim, cand,
+                     ncand);
   hipLaunchKernelGGL(k_flash_topk_eval, dim3(B), dim3(256), 0, stream, h, W, bias, cand, ncand, A, HF, 1, out_idx,
-                     out_val, (int32_t*)nullptr);
+                     out_val);
+  // a row past the candidate cap: the first maximum of the whole fp32 row
+  hipLaunchKernelGGL(k_flash_topk_scan, dim3(B), dim3(256), 0, stream, h, W, bias, ncand, A, HF, 1, out_idx, out_val,
+                     err);
   RG_LAUNCH_CHECK();
   return RG_OK;
 }

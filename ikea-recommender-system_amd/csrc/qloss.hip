@@ -238,22 +238,27 @@ extern "C" int rg_diversity(const int64_t* s, int L, const int64_t* lens, int pa
 
 // Novelty reward (novelty.py:12-47): mean_k [idx_bk ∈ U]·reward, U as a bitmap.
 __global__ void k_novelty(const int32_t* __restrict__ idx, int k, int ldi, const uint32_t* __restrict__ bitmap,
-                          float reward, int B, float* __restrict__ out) {
+                          int n_items, float reward, int B, float* __restrict__ out) {
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= B) return;
   double acc = 0.0;
   for (int q = 0; q < k; ++q) {
     const int j = idx[(int64_t)b * ldi + q];
+    if (j < 0 || j >= n_items) {   // not an item (never read from the bitmap): NaN reward
+      out[b] = __builtin_nanf("");
+      return;
+    }
     const bool u = (bitmap[j >> 5] >> (j & 31)) & 1u;
     acc += u ? (double)reward : 0.0;
   }
   out[b] = (float)(acc / k);
 }
 
-extern "C" int rg_novelty(const int32_t* idx, int k, int ldi, const uint32_t* bitmap, float reward, int B, float* out,
-                          hipStream_t stream) {
-  if (B <= 0 || k <= 0 || ldi < k) return RG_ERR_ARG;
-  hipLaunchKernelGGL(k_novelty, dim3((B + 255) / 256), dim3(256), 0, stream, idx, k, ldi, bitmap, reward, B, out);
+extern "C" int rg_novelty(const int32_t* idx, int k, int ldi, const uint32_t* bitmap, int n_items, float reward, int B,
+                          float* out, hipStream_t stream) {
+  if (B <= 0 || k <= 0 || ldi < k || n_items <= 0) return RG_ERR_ARG;
+  hipLaunchKernelGGL(k_novelty, dim3((B + 255) / 256), dim3(256), 0, stream, idx, k, ldi, bitmap, n_items, reward, B,
+                     out);
   RG_LAUNCH_CHECK();
   return RG_OK;
 }

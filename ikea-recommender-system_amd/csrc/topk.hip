@@ -13,11 +13,16 @@
 //      blocks' logits, keep the ones ≥ τ as (value, index) candidates;
 //   4. bitonic-sort the candidates by (value desc, index asc) and emit k.
 // Exact for any data; ties are broken by the smaller index (canonical order).
+// A row with more than TK_MAXCAND logits >= tau (massive ties) is scanned
+// whole instead (k <= TS_MAX, k_topk_zscan, topk_scan.h); beyond that k it
+// raises err |= 2.
 #include "common.h"
+#include "topk_scan.h"
 
 #define TK_THREADS 256
 #define TK_MAXSEL 8192
 #define TK_MAXCAND 2048
+#define TK_SCAN_MARK INT32_MIN
 
 __device__ __forceinline__ uint32_t f2key(float f) {
   uint32_t u = __float_as_uint(f);
@@ -101,6 +106,10 @@ __global__ __launch_bounds__(TK_THREADS) void k_topk(const float* __restrict__ Z
   __syncthreads();
   uint32_t n = s_ncand;
   if (n > TK_MAXCAND) {
+    if (k <= TS_MAX) {   // left to k_topk_zscan
+      if (tid == 0) out_idx[(int64_t)b * k] = TK_SCAN_MARK;
+      return;
+    }
     if (tid == 0 && err) atomicOr(err, 2);
     n = TK_MAXCAND;
   }
@@ -132,6 +141,23 @@ __global__ __launch_bounds__(TK_THREADS) void k_topk(const float* __restrict__ Z
   }
 }
 
+// the rows k_topk marked (candidate overflow): full scan of the stored row
+struct ZtRowSrc {
+  const float* ZT;
+  int64_t ldz;
+  int row;
+  __device__ void prepare(int r) { row = r; }
+  __device__ float operator()(int item) const { return ZT[(int64_t)item * ldz + row]; }
+};
+
+__global__ __launch_bounds__(256) void k_topk_zscan(const float* __restrict__ ZT, int64_t ldz, int A, int k,
+                                                    int32_t* __restrict__ out_idx, float* __restrict__ out_val) {
+  const int b = blockIdx.x;
+  if (out_idx[(int64_t)b * k] != TK_SCAN_MARK) return;
+  ZtRowSrc src{ZT, ldz, b};
+  topk_scan_row(src, b, A, k, out_idx, out_val);
+}
+
 extern "C" int rg_topk(const float* ZT, int64_t ldz, const float* pmax, int B, int A, int k, int32_t* out_idx,
                        float* out_val, int32_t* err, hipStream_t stream) {
   if (B <= 0 || A <= 0 || k <= 0 || k > 1024 || k > A) return RG_ERR_ARG;
@@ -139,6 +165,8 @@ extern "C" int rg_topk(const float* ZT, int64_t ldz, const float* pmax, int B, i
   const int coarse = (nJ + TK_MAXSEL - 1) / TK_MAXSEL;
   hipLaunchKernelGGL(k_topk, dim3(B), dim3(TK_THREADS), 0, stream, ZT, ldz, pmax, B, A, nJ, coarse, k, out_idx,
                      out_val, err);
+  if (k <= TS_MAX)
+    hipLaunchKernelGGL(k_topk_zscan, dim3(B), dim3(TK_THREADS), 0, stream, ZT, ldz, A, k, out_idx, out_val);
   RG_LAUNCH_CHECK();
   return RG_OK;
 }

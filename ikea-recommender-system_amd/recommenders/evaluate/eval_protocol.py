@@ -115,7 +115,7 @@ def evaluate(evaluation_data_loader, model, device, loss_function, padding_pos, 
     dev = model.device
     lut = _lut(input_tokenizer, output_tokenizer, dev)
     table = _div_table(diversity_embedding, dev)
-    bitmap = unpopular_bitmap(unpopular_actions_set, model.action_dim, dev)
+    bitmap = unpopular_bitmap(unpopular_actions_set, model.action_dim, dev, fresh=True)
     K = max(max(topk_hr_ndcg), topk_to_consider_div, topk_to_consider_nov, max(topk_to_consider_cov))
     hr = np.zeros(len(topk_hr_ndcg))
     ndcg = np.zeros(len(topk_hr_ndcg))

@@ -57,11 +57,11 @@ SIGNATURES = {
     "rg_flash_score": [P, P, P, I, I, I, I, I, P, P, P, P, P, P],
     "rg_flash_amax_screen": [P, P, P, I, I, I, I, P, P, P, P],
     "rg_row_norm_max": [P, I64, I, P, P],
-    "rg_flash_argmax_exact": [P, I, I, P, P, P, I, P, F, P, P, P, P, P, P],
+    "rg_flash_argmax_exact": [P, I, I, P, P, P, I, P, F, P, P, P, P, P, P, P],
     "rg_flash_topk_cap": [],
-    "rg_flash_topk": [P, I, I, I, F, F, P, P, P, I, P, P, P, P, P, P, P],
+    "rg_flash_topk": [P, I, I, I, I, F, F, P, P, P, I, P, P, P, P, P, P, P],
     "rg_flash_topk_work_bytes": [I, I, I],
-    "rg_flash_topk_screened": [P, I, I, I, F, P, P, P, P, I, P, P, P, P, P, P, P],
+    "rg_flash_topk_screened": [P, I, I, I, I, F, P, P, P, P, I, P, P, P, P, P, P, P],
     "rg_flash_lse": [P, P, I, P, P, P, P, I64, I, I64, I, I, P, P, P],
     "rg_flash_rows": [P, P, I64, I, I, P, P],
     "rg_flash_dh": [P, P, P, I, P, F, I, I, P, P],
@@ -88,7 +88,7 @@ SIGNATURES = {
     "rg_smorl_td": [P, P, P, P, P, I, F, F, I, P, P, P],
     "rg_sum64": [P, I, D, P, P, P],
     "rg_diversity": [P, I, P, I, P, I, I, P, I64, I, F, I, P, P],
-    "rg_novelty": [P, I, I, P, F, I, P, P],
+    "rg_novelty": [P, I, I, P, I, F, I, P, P],
     "rg_topk": [P, I64, P, I, I, I, P, P, P, P],
     "rg_hits_ndcg": [P, I, P, I, P, I, P, P],
     "rg_repetitions": [P, I, P, I, I, P, I, P, P],

@@ -593,7 +593,9 @@ class _FlashWS:
             self.pbest, self.parg = z(self.nsplit, B), z(self.nsplit, B, dt=torch.int32)
             self.top_idx, self.top_val = z(B, top_k, dt=torch.int32), z(B, top_k)
         # chunk maxima for the exact top-K (K = 1 too, while they fit
-        # SCREEN_CMAX_BYTES; else K = 1 merges the per-split first maxima)
+        # SCREEN_CMAX_BYTES; else K = 1 runs the row-chunked screening argmax
+        # on this workspace's planes, SoftmaxHead.top_entries)
+        self.top1 = None
         if top_k > 1 or (top_k == 1 and -(-A // 32) * B * 4 <= SCREEN_CMAX_BYTES):
             self.cmax = z(-(-A // 32), B)
             self.cand = z(B, call("rg_flash_topk_cap"), dt=torch.int32)
@@ -649,7 +651,7 @@ class _AmaxWS:
     with ``screen`` the chunk maxima, candidates and max row norm of the
     screening argmax)."""
 
-    def __init__(self, B, A, HF, device, screen=False):
+    def __init__(self, B, A, HF, device, screen=False, planes=True):
         u8 = lambda n: torch.empty(int(n), dtype=torch.uint8, device=device)  # noqa: E731
         z = lambda *s, dt=torch.float32: torch.empty(*s, dtype=dt, device=device)  # noqa: E731
         self.B, self.screen = B, screen
@@ -662,9 +664,11 @@ class _AmaxWS:
             self.Bc = min(B, SCREEN_ROW_CHUNK)
         nrb = -(-self.Bc // rpb)
         self.nsplit = _round_up(min(max(1, 256 // nrb), nct), 8)
-        self.Hk = u8(call("rg_head_plane_bytes", B, HF))
-        self.Wk = u8(call("rg_head_plane_bytes", A, HF))
-        self.bias_pad = z(_round_up(A, 32))
+        self.Hk = self.Wk = self.bias_pad = None   # (planes=False: the caller's, e.g. a pass-1 workspace's)
+        if planes:
+            self.Hk = u8(call("rg_head_plane_bytes", B, HF))
+            self.Wk = u8(call("rg_head_plane_bytes", A, HF))
+            self.bias_pad = z(_round_up(A, 32))
         self.pbest, self.parg = z(self.nsplit, self.Bc), z(self.nsplit, self.Bc, dt=torch.int32)
         self.amax, self.mx = z(B, dt=torch.int32), z(B)
         if screen:
@@ -734,7 +738,11 @@ class SoftmaxHead:
         # entries of the row top-k a caller reads after forward_loss (SMORL's
         # rewards, ``top_entries``); the fused head computes them in pass 1
         self.top_k = 0
+        # stored-logit top-k (rg_topk, K > 32 only) candidate overflow flag
         self.top_err = torch.zeros(1, dtype=torch.int32, device=device)
+        # rows whose fused top-k / exact argmax candidates overflowed the cap and
+        # were scanned whole instead (exact either way; diagnostic count)
+        self.top_scanned = torch.zeros(1, dtype=torch.int32, device=device)
 
     # W / b (and their Adam moments) are only reachable through these
     # properties, which first order the current stream after an overlapped
@@ -823,31 +831,56 @@ class SoftmaxHead:
     def top_entries(self, w):
         """(idx (B, K) int32 local item ids, values (B, K)) of every row's top-K
         logits in the canonical (value desc, index asc) order, after
-        forward_loss with ``top_k = K``.  Fused head: the items of the
-        candidate chunks (chunk maximum within the split-bf16 error of the
-        K-th largest) are re-scored in fp32 (rg_flash_topk; a candidate
-        overflow is flagged in ``top_err``, see check_top_err) — also for
-        K = 1 unless the chunk maxima exceed SCREEN_CMAX_BYTES (C5 on one GPU:
-        then pass 1's per-split first maxima of the split-bf16 logits are
-        merged, so a near-tie within ~2^-24·Σ|h||w| may pick the other item).
-        Native head: rg_topk over the stored Zᵀ."""
+        forward_loss with ``top_k = K`` (reference: torch.topk of the fp32
+        logits, diversity.py:15-73, novelty.py:12-47).  Fused head: the items of
+        the candidate chunks (chunk maximum within the split-bf16 error of the
+        K-th largest) are re-scored in fp32 (rg_flash_topk; a row past the
+        candidate cap is scanned whole).  K = 1 when the chunk maxima would
+        exceed SCREEN_CMAX_BYTES (C5 on one GPU): the screening argmax in row
+        chunks on the planes pass 1 just read, then the same fp32 re-scoring
+        (_screened_argmax).  Native head: rg_topk over the stored Zᵀ."""
         K, B = self.top_k, w.B
         st = stream_ptr()
         if isinstance(w, _FlashWS):
             if K == 1 and w.cmax is None:
-                call("rg_flash_argmax", w.pbest.data_ptr(), w.parg.data_ptr(), w.nsplit, B, w.top_idx.data_ptr(),
-                     w.top_val.data_ptr(), st)
+                if w.top1 is None:
+                    w.top1 = _AmaxWS(B, self.A, self.HF, self.device, screen=True, planes=False)
+                self._screened_argmax(w.top1, w.Hk, w.Wk, w.bias_pad, w.h, self._Wp, self._bp, w.top_idx,
+                                      w.top_val)
             else:
-                call("rg_flash_topk", w.cmax.data_ptr(), B, self.A, K, _f32(self.TOP_TOL_ABS),
+                call("rg_flash_topk", w.cmax.data_ptr(), B, B, self.A, K, _f32(self.TOP_TOL_ABS),
                      _f32(self.TOP_TOL_REL), w.h.data_ptr(), self._Wp.p.data_ptr(), self._bp.p.data_ptr(), self.HF,
                      w.cand.data_ptr(), w.ncand.data_ptr(), w.top_idx.data_ptr(), w.top_val.data_ptr(),
-                     self.top_err.data_ptr(), w.tk_work.data_ptr(), st)
+                     self.top_scanned.data_ptr(), w.tk_work.data_ptr(), st)
             return w.top_idx, w.top_val
         idx = torch.empty(B, K, dtype=torch.int32, device=self.device)
         vals = torch.empty(B, K, device=self.device)
         call("rg_topk", w.ZT.data_ptr(), w.ldz, w.pmax.data_ptr(), B, self.A, K, idx.data_ptr(), vals.data_ptr(),
              self.top_err.data_ptr(), st)
         return idx, vals
+
+    def _screened_argmax(self, aw, Hk, Wk, bias_pad, h, Wp, bp, out_idx, out_val):
+        """First maximum of the fp32 logits h·Wᵀ + b per row into out_idx /
+        out_val: screening on 3 plane products (rows in aw.Bc chunks, so the
+        chunk maxima fit SCREEN_CMAX_BYTES), then every item of every chunk
+        within the screening's error bound re-scored in fp32
+        (rg_flash_argmax_exact; a row past the candidate cap is scanned whole)."""
+        B, A, HF = h.shape[0], self.A, self.HF
+        st = stream_ptr()
+        W, b = Wp.p.data_ptr(), bp.p.data_ptr()
+        call("rg_row_norm_max", W, A, HF, aw.wnorm.data_ptr(), st)
+        hk_row = HF * 6   # K-plane bytes per row
+        cap = call("rg_flash_topk_cap")
+        for r0 in range(0, B, aw.Bc):
+            bc = min(aw.Bc, B - r0)
+            call("rg_flash_amax_screen", Hk.data_ptr() + r0 * hk_row, Wk.data_ptr(), bias_pad.data_ptr(), bc, A, HF,
+                 aw.nsplit, aw.pbest.data_ptr(), aw.parg.data_ptr(), aw.cmax.data_ptr(), st)
+            call("rg_flash_argmax", aw.pbest.data_ptr(), aw.parg.data_ptr(), aw.nsplit, bc,
+                 out_idx.data_ptr() + 4 * r0, out_val.data_ptr() + 4 * r0, st)
+            call("rg_flash_argmax_exact", aw.cmax.data_ptr(), bc, A, h.data_ptr() + 4 * r0 * HF, W, b, HF,
+                 aw.wnorm.data_ptr(), _f32(SCREEN_TOL), aw.lim.data_ptr() + 4 * r0,
+                 aw.cand.data_ptr() + 4 * r0 * cap, aw.ncand.data_ptr() + 4 * r0,
+                 out_idx.data_ptr() + 4 * r0, out_val.data_ptr() + 4 * r0, self.top_scanned.data_ptr(), st)
 
     # ---- evaluation scoring without logits (evaluate / update_train_metrics) ----
     def score_topk(self, h, K, tgt=None, slot="eval", screen=False):
@@ -859,12 +892,12 @@ class SoftmaxHead:
         products: lse partials + chunk maxima), rg_flash_lse (lse, fp32
         target logit), rg_flash_topk (every item of the candidate chunks
         re-scored in fp32, fmaf chain + bias).  Returns (idx (B, K) int32,
-        vals (B, K), loss_row (B,) or None); a candidate overflow (massive
-        exact ties) sets ``top_err``.  HF must be in {32, 64, 128, 256}, K <= 32.
-        screen (no tgt): the chunk maxima come from the 3-product screening
-        pass (rg_flash_amax_screen) and the candidates are taken within its
-        error bound (rg_flash_topk_screened) — the same exact lists at half the
-        MFMA work; an overflow there sets ``top_err`` too (re-score without)."""
+        vals (B, K), loss_row (B,) or None); a row past the candidate cap
+        (massive ties) is scanned whole (counted in ``top_scanned``).  HF must
+        be in {32, 64, 128, 256}, K <= 32.  screen (no tgt): the chunk maxima
+        come from the 3-product screening pass (rg_flash_amax_screen) and the
+        candidates are taken within its error bound (rg_flash_topk_screened) —
+        the same exact lists at half the MFMA work."""
         B, A, HF = h.shape[0], self.A, self.HF
         if K > min(32, A) or HF not in (32, 64, 128, 256):
             raise ValueError(f"score_topk: K={K} (<= 32 and <= A) and HF={HF} in {{32, 64, 128, 256}}")
@@ -879,16 +912,16 @@ class SoftmaxHead:
         for r0 in range(0, B, R):
             n = min(R, B - r0)
             hs = w.h if n < R else h[r0:r0 + R]
-            if n < R:   # ragged tail: zero-padded rows (scored, never read back)
+            if n < R:   # ragged tail: zero-padded rows (pass 1 scores them; the top-k takes only the n real rows)
                 w.h.zero_()
                 w.h[:n].copy_(h[r0:r0 + n])
             call("rg_head_planes", hs.data_ptr(), R, HF, w.Hk.data_ptr(), None, None, None, st)
             if screen:
                 call("rg_flash_amax_screen", w.Hk.data_ptr(), Wk.data_ptr(), bias_pad.data_ptr(), R, A, HF, w.nsplit,
                      w.pbest.data_ptr(), w.parg.data_ptr(), w.cmax.data_ptr(), st)
-                call("rg_flash_topk_screened", w.cmax.data_ptr(), R, A, K, _f32(SCREEN_TOL), w.wnorm.data_ptr(),
+                call("rg_flash_topk_screened", w.cmax.data_ptr(), R, n, A, K, _f32(SCREEN_TOL), w.wnorm.data_ptr(),
                      hs.data_ptr(), Wp.p.data_ptr(), bp.p.data_ptr(), HF, w.cand.data_ptr(), w.ncand.data_ptr(),
-                     w.idx.data_ptr() + 4 * r0 * K, w.vals.data_ptr() + 4 * r0 * K, self.top_err.data_ptr(),
+                     w.idx.data_ptr() + 4 * r0 * K, w.vals.data_ptr() + 4 * r0 * K, self.top_scanned.data_ptr(),
                      w.tk_work.data_ptr(), st)
                 continue
             call("rg_flash_score", w.Hk.data_ptr(), Wk.data_ptr(), bias_pad.data_ptr(), R, A, HF, 6, w.nsplit,
@@ -901,9 +934,9 @@ class SoftmaxHead:
                 call("rg_flash_lse", w.pm.data_ptr(), w.pl.data_ptr(), w.nsplit, hs.data_ptr(), Wp.p.data_ptr(),
                      bp.p.data_ptr(), ts.data_ptr(), 0, A, A, R, HF, w.lse.data_ptr(), w.zt.data_ptr(), st)
                 call("rg_sub", w.lse.data_ptr(), w.zt.data_ptr(), n, w.loss_row.data_ptr() + 4 * r0, st)
-            call("rg_flash_topk", w.cmax.data_ptr(), R, A, K, _f32(self.TOP_TOL_ABS), _f32(self.TOP_TOL_REL),
+            call("rg_flash_topk", w.cmax.data_ptr(), R, n, A, K, _f32(self.TOP_TOL_ABS), _f32(self.TOP_TOL_REL),
                  hs.data_ptr(), Wp.p.data_ptr(), bp.p.data_ptr(), HF, w.cand.data_ptr(), w.ncand.data_ptr(),
-                 w.idx.data_ptr() + 4 * r0 * K, w.vals.data_ptr() + 4 * r0 * K, self.top_err.data_ptr(),
+                 w.idx.data_ptr() + 4 * r0 * K, w.vals.data_ptr() + 4 * r0 * K, self.top_scanned.data_ptr(),
                  w.tk_work.data_ptr(), st)
         return w.idx[:B], w.vals[:B], (w.loss_row[:B] if tgt is not None else None)
 
@@ -930,8 +963,9 @@ class SoftmaxHead:
         getattr(self, "_sws_eval", {}).clear()
 
     def check_top_err(self):
-        """Raise if a fused or stored-logit top-k of this head overflowed its
-        candidate buffer since the last check (massive exact ties)."""
+        """Raise if a stored-logit top-k with K > 32 (rg_topk) of this head
+        overflowed its candidate buffer since the last check (massive exact
+        ties); every other top-k path scans such a row whole instead."""
         if int(self.top_err.item()):
             self.top_err.zero_()
             raise RuntimeError(f"{self.name}: top-k candidate overflow (massive ties in the logits)")
@@ -1063,22 +1097,11 @@ class SoftmaxHead:
                     self._aws = {}
                 self._aws.pop(slot, None)
                 w = self._aws[slot] = _AmaxWS(B, self.A, self.HF, self.device, True)
-            W, b = self.W.p.data_ptr(), self.b.p.data_ptr()
+            Wp, bp = self.W, self.b
             call("rg_head_planes", h.data_ptr(), B, self.HF, w.Hk.data_ptr(), None, None, None, st)
-            call("rg_head_planes", W, self.A, self.HF, w.Wk.data_ptr(), None, b, w.bias_pad.data_ptr(), st)
-            call("rg_row_norm_max", W, self.A, self.HF, w.wnorm.data_ptr(), st)
-            hk_row = self.HF * 6   # K-plane bytes per row
-            for r0 in range(0, B, w.Bc):
-                bc = min(w.Bc, B - r0)
-                call("rg_flash_amax_screen", w.Hk.data_ptr() + r0 * hk_row, w.Wk.data_ptr(),
-                     w.bias_pad.data_ptr(), bc, self.A, self.HF, w.nsplit, w.pbest.data_ptr(),
-                     w.parg.data_ptr(), w.cmax.data_ptr(), st)
-                call("rg_flash_argmax", w.pbest.data_ptr(), w.parg.data_ptr(), w.nsplit, bc,
-                     w.amax.data_ptr() + 4 * r0, w.mx.data_ptr() + 4 * r0, st)
-                call("rg_flash_argmax_exact", w.cmax.data_ptr(), bc, self.A, h.data_ptr() + 4 * r0 * self.HF, W, b,
-                     self.HF, w.wnorm.data_ptr(), _f32(SCREEN_TOL), w.lim.data_ptr() + 4 * r0,
-                     w.cand.data_ptr() + 4 * r0 * call("rg_flash_topk_cap"), w.ncand.data_ptr() + 4 * r0,
-                     w.amax.data_ptr() + 4 * r0, w.mx.data_ptr() + 4 * r0, st)
+            call("rg_head_planes", Wp.p.data_ptr(), self.A, self.HF, w.Wk.data_ptr(), None, bp.p.data_ptr(),
+                 w.bias_pad.data_ptr(), st)
+            self._screened_argmax(w, w.Hk, w.Wk, w.bias_pad, h, Wp, bp, w.amax, w.mx)
             self.argmax_mx = w.mx
             return w.amax
         w = self.ws(slot, B, False)

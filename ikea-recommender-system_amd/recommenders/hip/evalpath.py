@@ -54,20 +54,17 @@ def fused_scoring(head, K):
 
 
 def score_rows(head, h, K, tgt=None, screen=True):
-    """(idx (B, K) int32, vals (B, K), loss_row (B,) or None, err flag tensor,
-    screened): the canonical top-K and per-row CE of h's logits without a
+    """(idx (B, K) int32, vals (B, K), loss_row (B,) or None, err flag tensor
+    or None): the canonical top-K and per-row CE of h's logits without a
     (B, A) buffer.  Without targets (update_train_metrics) the chunk maxima
-    come from the 3-product screening pass (screened = True); a row whose
-    screening error band holds more candidate chunks than the cap sets the
-    flag, and the caller (eval_batch, which reads the flag once at its end)
-    re-runs the batch through the exact 6-product scoring (screen=False)."""
+    come from the 3-product screening pass; a row whose candidate band holds
+    more chunks than the cap is scanned whole on the device, so the fused path
+    has no error flag.  The stored-logit fallback's flag (rg_topk, K > 32 on
+    massive ties) is read by the caller once at its end."""
     B = h.shape[0]
     if fused_scoring(head, K):
-        if tgt is None and screen:
-            idx, vals, _ = head.score_topk(h, K, None, screen=True)
-            return idx, vals, None, head.top_err, True
-        idx, vals, loss_row = head.score_topk(h, K, tgt)
-        return idx, vals, loss_row, head.top_err, False
+        idx, vals, loss_row = head.score_topk(h, K, tgt, screen=screen and tgt is None)
+        return idx, vals, loss_row, None
     # stored-logit fallback, row-chunked
     st = stream_ptr()
     dev = head.device
@@ -92,7 +89,7 @@ def score_rows(head, h, K, tgt=None, screen=True):
     # no Zᵀ stays cached after the batch (the caching allocator reuses the block)
     for k in [k for k in head._ws if k[0] == "eval_chunk"]:
         del head._ws[k]
-    return idx, vals, loss_row, err, False
+    return idx, vals, loss_row, err
 
 
 def eval_batch(model, s, s_len, a, *, head_idx=0, K=20, ks=(20,), padding_pos="end", div_table=None, k_div=1,
@@ -110,7 +107,7 @@ def eval_batch(model, s, s_len, a, *, head_idx=0, K=20, ks=(20,), padding_pos="e
     st = stream_ptr()
     h = model.hidden(s, s_len, slot="eval", save=False)
     head = head_for(model, head_idx)
-    idx, vals, loss_row, top_err, screened = score_rows(head, h, K, a if want_loss else None, screen=screen)
+    idx, vals, loss_row, top_err = score_rows(head, h, K, a if want_loss else None, screen=screen)
     out = EvalBatch()
     out.loss = None
     if want_loss:
@@ -138,7 +135,8 @@ def eval_batch(model, s, s_len, a, *, head_idx=0, K=20, ks=(20,), padding_pos="e
         out.div = div
     if bitmap is not None:
         nov = torch.empty(B, device=dev)
-        call("rg_novelty", idx.data_ptr(), k_nov, K, bitmap.data_ptr(), _f32(nov_reward), B, nov.data_ptr(), st)
+        call("rg_novelty", idx.data_ptr(), k_nov, K, bitmap.data_ptr(), head.A, _f32(nov_reward), B, nov.data_ptr(),
+             st)
         out.nov = nov
     out.reps = None
     if rep_ks is not None:   # repetitions (repetitiveness.py:21-57) on the input-vocabulary ids
@@ -147,12 +145,7 @@ def eval_batch(model, s, s_len, a, *, head_idx=0, K=20, ks=(20,), padding_pos="e
         call("rg_repetitions", s.data_ptr(), s.shape[1], out.idx_in.data_ptr(), K, B, kh, len(rep_ks),
              reps.data_ptr(), st)
         out.reps = reps
-    if int(top_err.item()):   # the batch's one host read of the flag
-        top_err.zero_()
-        if screened:   # a screening band overflowed: the whole batch again on the exact scoring
-            return eval_batch(model, s, s_len, a, head_idx=head_idx, K=K, ks=ks, padding_pos=padding_pos,
-                              div_table=div_table, k_div=k_div, bitmap=bitmap, k_nov=k_nov, nov_reward=nov_reward,
-                              want_loss=want_loss, lut=lut, rep_ks=rep_ks, screen=False)
+    if top_err is not None and int(top_err.item()):   # stored-logit fallback only (rg_topk, K > 32)
         raise RuntimeError("top-k candidate overflow (massive exact ties in the logits)")
     if rerr is not None and int(rerr.item()):
         from .remap import RemapError

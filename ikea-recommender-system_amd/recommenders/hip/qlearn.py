@@ -239,7 +239,7 @@ def smorl_rewards(main, smorl, s, a, r_acc, true_next_len, B):
          smorl["div_table"].shape[1], _f32(1e-6), B,
          r_div.data_ptr(), st)
     r_nov = main.buf("r_nov", (B,))
-    call("rg_novelty", idx.data_ptr(), k_nov, K, smorl["bitmap"].data_ptr(), _f32(smorl["nov_rew_sig"]), B,
+    call("rg_novelty", idx.data_ptr(), k_nov, K, smorl["bitmap"].data_ptr(), head.A, _f32(smorl["nov_rew_sig"]), B,
          r_nov.data_ptr(), st)
     r64 = _dev(r_acc, dev, torch.float64)
     rr = main.buf("rr", (B, 3))
@@ -251,12 +251,15 @@ def smorl_rewards(main, smorl, s, a, r_acc, true_next_len, B):
 _BITMAPS = {}
 
 
-def unpopular_bitmap(unpopular, n_actions, device):
+def unpopular_bitmap(unpopular, n_actions, device, fresh=False):
     """The unpopular set (novelty.py:12-47, item_frequency.py:8-24) as a device
-    bitmap over the actions; cached per (set object, size, n_actions, device)
-    — the harness passes the same set every batch."""
+    bitmap over the actions.  fresh=False (the per-batch update_train_metrics,
+    which the harness calls with the same set every batch): cached per (set
+    object, size, n_actions, device), so a set changed in place without a
+    change of size must be passed as a new object (or a frozenset); evaluate()
+    and the SMORL trainer's construction build it fresh."""
     key = (id(unpopular), len(unpopular), int(n_actions), str(device))
-    hit = _BITMAPS.get(key)
+    hit = None if fresh else _BITMAPS.get(key)
     if hit is not None and hit[0] is unpopular:
         return hit[1]
     j = np.fromiter((int(x) for x in unpopular), dtype=np.int64, count=len(unpopular))

@@ -338,7 +338,8 @@ def _smorl_rewards_rows(main, smorl, s, r_acc, true_next_len, idx, B):
          smorl["div_table"].shape[1],
          _f32(1e-6), B, r_div.data_ptr(), st)
     r_nov = _buf(main, "r_nov", (B,))
-    call("rg_novelty", idx.data_ptr(), smorl["topk_nov"], K, smorl["bitmap"].data_ptr(), _f32(smorl["nov_rew_sig"]),
+    call("rg_novelty", idx.data_ptr(), smorl["topk_nov"], K, smorl["bitmap"].data_ptr(), main.action_dim,
+         _f32(smorl["nov_rew_sig"]),
          B, r_nov.data_ptr(), st)
     r64 = _dev(r_acc, dev, torch.float64)
     rr = _buf(main, "rr", (B, 3))

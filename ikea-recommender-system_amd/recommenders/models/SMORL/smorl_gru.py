@@ -93,7 +93,7 @@ class SMORL_trainer:
             "nov_rew_sig": float(nov_rew_sig),
             "pad_end": padding_pos == "end",
             "div_table": table.detach().to(self.device, torch.float32).contiguous(),
-            "bitmap": unpopular_bitmap(unpopular_actions_set, action_dim, self.device),
+            "bitmap": unpopular_bitmap(unpopular_actions_set, action_dim, self.device, fresh=True),
             # tokenizer remap of the predicted ids for the diversity reward
             # (diversity.py:55-60), tabulated once (recommenders/hip/remap.py)
             "lut": (remap_table(input_tokenizer, output_tokenizer, self.device)

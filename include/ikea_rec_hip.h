@@ -161,9 +161,12 @@ int rg_flash_fwd(const void* Hk, const void* Wk, const void* Wr, const float* bi
  *   tol_rel·|tau|), tau = the K-th largest chunk maximum; their items are
  *   rescored in fp32 (the native fp32 head's fmaf chain over HF, + bias: bitwise
  *   rg_head_fwd's logits).  tau comes from a chip-wide two-stage reduction of
- *   the chunk maxima.  cand: B × rg_flash_topk_cap() int32, ncand: B int32,
- *   work: rg_flash_topk_work_bytes(B, A, K) bytes; err |= 1 on a candidate
- *   overflow (that row's output is left unchanged). */
+ *   the chunk maxima.  Rows [0, B) of cmax (ceil(A/32) × ldc, ldc >= B: a
+ *   ragged row chunk passes its valid rows as B).  cand: B × rg_flash_topk_cap()
+ *   int32, ncand: B int32, work: rg_flash_topk_work_bytes(ldc, A, K) bytes.  A
+ *   row with more candidate chunks than the cap (massive ties) is scanned whole
+ *   (every item re-scored the same way, canonical top-K): the result is exact for
+ *   every row; err (optional) counts the rows scanned. */
 int rg_flash_rows_per_block(int HF);
 int rg_flash_fwd_top(const void* Hk, const void* Wk, const void* Wr, const float* bias_pad, int B, int A, int HF,
                      int terms, int nsplit, float* pm, float* pl, float* pO, float* pbest, int32_t* parg, float* cmax,
@@ -187,25 +190,26 @@ int rg_flash_argmax(const float* pbest, const int32_t* parg, int nsplit, int B, 
  * rg_flash_argmax_exact: re-scores in fp32 (fmaf chain over k, + bias) every item of every chunk whose
  *   screened maximum is >= tau − (tol·||h_b||_2·wnorm[0] + 1e-6·|tau|), tau = out_val (rg_flash_argmax's
  *   screening maximum), and writes the first maximum into out_idx / out_val (in place over the
- *   screening result); a row with more than rg_flash_topk_cap() candidate chunks keeps the screening
- *   result.  lim: B floats, cand: B × rg_flash_topk_cap() int32, ncand: B int32 (work). */
+ *   screening result); a row with more than rg_flash_topk_cap() candidate chunks is scanned whole
+ *   (the first maximum of every item's fp32 logit) and counted in err (optional).  lim: B floats,
+ *   cand: B × rg_flash_topk_cap() int32, ncand: B int32 (work). */
 int rg_flash_amax_screen(const void* Hk, const void* Wk, const float* bias_pad, int B, int A, int HF, int nsplit,
                          float* pbest, int32_t* parg, float* cmax, rg_stream_t stream);
 int rg_row_norm_max(const float* W, int64_t A, int HF, float* out, rg_stream_t stream);
 int rg_flash_argmax_exact(const float* cmax, int B, int A, const float* h, const float* W, const float* bias, int HF,
                           const float* wnorm, float tol, float* lim, int32_t* cand, int32_t* ncand, int32_t* out_idx,
-                          float* out_val, rg_stream_t stream);
+                          float* out_val, int32_t* err, rg_stream_t stream);
 int rg_flash_topk_cap(void);
 int64_t rg_flash_topk_work_bytes(int B, int A, int K);
 /* rg_flash_topk on the screened chunk maxima of rg_flash_amax_screen (3 plane products): candidate
  * chunks within tol·||h_b||_2·wnorm[0] + 1e-6·|tau| of tau (wnorm: rg_row_norm_max), then the same
- * exact fp32 re-scoring; err |= 1 on a candidate overflow (re-score that batch with rg_flash_score). */
-int rg_flash_topk_screened(const float* cmax, int B, int A, int K, float tol, const float* wnorm, const float* h,
-                           const float* W, const float* bias, int HF, int32_t* cand, int32_t* ncand, int32_t* out_idx,
-                           float* out_val, int32_t* err, void* work, rg_stream_t stream);
-int rg_flash_topk(const float* cmax, int B, int A, int K, float tol_abs, float tol_rel, const float* h, const float* W,
-                  const float* bias, int HF, int32_t* cand, int32_t* ncand, int32_t* out_idx, float* out_val,
-                  int32_t* err, void* work, rg_stream_t stream);
+ * exact fp32 re-scoring, including the whole-row scan past the candidate cap (err counts those rows). */
+int rg_flash_topk_screened(const float* cmax, int ldc, int B, int A, int K, float tol, const float* wnorm,
+                           const float* h, const float* W, const float* bias, int HF, int32_t* cand, int32_t* ncand,
+                           int32_t* out_idx, float* out_val, int32_t* err, void* work, rg_stream_t stream);
+int rg_flash_topk(const float* cmax, int ldc, int B, int A, int K, float tol_abs, float tol_rel, const float* h,
+                  const float* W, const float* bias, int HF, int32_t* cand, int32_t* ncand, int32_t* out_idx,
+                  float* out_val, int32_t* err, void* work, rg_stream_t stream);
 int rg_flash_lse(const float* pm, const float* pl, int nsplit, const float* h, const float* W, const float* bias,
                  const int64_t* tgt, int64_t lo, int A, int64_t A_full, int B, int HF, float* lse, float* zt,
                  rg_stream_t stream);
@@ -304,9 +308,11 @@ int rg_sum64(const double* x, int n, double scale, double* out64, float* out32, 
  * and no table read. */
 int rg_diversity(const int64_t* s, int L, const int64_t* lens, int pad_end, const int32_t* idx, int k, int ldi,
                  const float* D, int64_t Drows, int Ed, float eps, int B, float* out, rg_stream_t stream);
-/* A13 novelty reward: recommenders/evaluate/novelty.py:12-47 (U as bitmap). */
-int rg_novelty(const int32_t* idx, int k, int ldi, const uint32_t* bitmap, float reward, int B, float* out,
-               rg_stream_t stream);
+/* A13 novelty reward: recommenders/evaluate/novelty.py:12-47 (U as a bitmap
+ * over n_items actions); a row with an id outside [0, n_items) gets NaN and no
+ * bitmap read. */
+int rg_novelty(const int32_t* idx, int k, int ldi, const uint32_t* bitmap, int n_items, float reward, int B,
+               float* out, rg_stream_t stream);
 
 /* ---- A14 / A12 / A13 top-k: replaces torch.topk(preds, k) on host-copied
  * (B, A) logits (recommenders/evaluate/eval_protocol.py:75,199; diversity.py:51;

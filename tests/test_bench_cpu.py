@@ -72,3 +72,23 @@ def test_world_size_mismatch_exits_nonzero():
                        capture_output=True, text=True, timeout=300)
     assert r.returncode != 0
     assert "WORLD_SIZE=2" in r.stderr
+
+
+def test_per_rank_batch_splits_the_global_c4_c5_batch():
+    """BASELINE configs[3] (C4: batch 4096 across 8×MI355X, SURVEY §8e: 512
+    sessions per rank) and configs[4] (C5: batch 8192) are global batches:
+    their ranks split them; C2 / C3 keep 4096 per GPU (weak scaling)."""
+    b = _bench()
+    assert [b.per_rank_batch("c4", 4096, w) for w in (1, 2, 4, 8)] == [4096, 2048, 1024, 512]
+    assert [b.per_rank_batch("c5", 8192, w) for w in (1, 2, 4, 8)] == [8192, 4096, 2048, 1024]
+    assert [b.per_rank_batch("c2", 4096, w) for w in (1, 2, 8)] == [4096] * 3
+    with pytest.raises(SystemExit):
+        b.per_rank_batch("c4", 4096, 3)
+
+
+def test_host_threads_reports_the_usable_cpus():
+    b = _bench()
+    n, how = b.host_threads()
+    assert 1 <= n <= how["affinity_cpus"]
+    if how["cgroup_cpu_quota"]:
+        assert n <= how["cgroup_cpu_quota"]

@@ -1,5 +1,7 @@
-"""Multi-GPU path on CPU (gloo, world_size 2): the collective wrapper and the
-item-sharded softmax decomposition equal the unsharded math."""
+"""Multi-GPU path on CPU (gloo, world_size 2 and 3 — the latter an uneven
+split: 37 items / 53 table rows over 3 ranks): the collective wrapper, the
+item-sharded softmax decomposition and the host routing equal the unsharded
+math."""
 import os
 import socket
 import sys
@@ -72,7 +74,7 @@ def _worker(rank, world, port, q):
         from oracle.sharded import sharded_embedding
         N1, E = 53, 4
         table = torch.randn(N1, E, generator=gen, dtype=torch.float64)
-        toks = [torch.randint(0, N1, (n,), generator=gen) for n in (17, 23)][:world]
+        toks = [torch.randint(0, N1, (n,), generator=gen) for n in (17, 23, 11)][:world]
         toks[0][:3] = N1 - 1                 # the pad row (last rank's shard) from every rank
         dXs = [torch.randn(len(t), E, generator=gen, dtype=torch.float64) for t in toks]
         elo, ehi = item_shard(N1, world, rank)
@@ -104,17 +106,18 @@ def _worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
-def test_sharded_decomposition_gloo_world2():
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_decomposition_gloo(world):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
     res = dict(q.get(timeout=240) for _ in procs)
     for p in procs:
         p.join(timeout=60)
-    assert res == {0: "ok", 1: "ok"}, res
+    assert res == {r: "ok" for r in range(world)}, res
 
 
 def test_item_shard_partition():

@@ -122,7 +122,7 @@ def test_score_topk_equals_native_logits_topk(N, B, H, K, screen):
     ws, z = head.logits_T(h)
     zc = z.cpu().numpy()
     ref = om.canonical_topk(zc, K)
-    assert int(head.top_err.item()) == 0
+    assert int(head.top_scanned.item()) == 0
     np.testing.assert_array_equal(idx.cpu().numpy(), ref)
     np.testing.assert_array_equal(vals.cpu().numpy(), np.take_along_axis(zc, ref, 1))
     if not screen:
@@ -151,6 +151,54 @@ def test_score_topk_row_chunks(monkeypatch):
     np.testing.assert_array_equal(i1.cpu().numpy(), i2.cpu().numpy())
     np.testing.assert_array_equal(v1.cpu().numpy(), v2.cpu().numpy())
     np.testing.assert_allclose(l1.cpu().numpy(), l2.cpu().numpy(), rtol=4e-7, atol=0)
+
+
+@pytest.mark.parametrize("screen", [False, True])
+def test_score_topk_ragged_rows_at_catalogue_scale(screen):
+    """A ragged final batch at A = 1M (B = 1000 rows in a 1024-row chunk): the
+    chunk's zero padding rows (logits = the biases, a dense band of near-ties)
+    are never selected or scanned — the top-k runs on the 1000 real rows only
+    — and every row equals the native head's canonical top-K bitwise."""
+    from recommenders.hip import engine
+    N, B, HF, K = 1_000_000, 1000, 64, 20
+    hd = engine.SoftmaxHead("x", N, HF, "cuda")
+    g = torch.Generator().manual_seed(21)
+    h = torch.tanh(torch.randn(B, HF, generator=g)).cuda()
+    tgt = torch.randint(0, N, (B,), generator=g).cuda()
+    idx, vals, _ = hd.score_topk(h, K, None if screen else tgt, screen=screen)
+    assert hd._sws_eval["eval"].R == 1024
+    torch.cuda.synchronize()
+    assert int(hd.top_scanned.item()) == 0
+    ws, z = hd.logits_T(h)
+    rows = torch.arange(0, B, 7)
+    zc = z[rows.cuda()].cpu().numpy()
+    ref = om.canonical_topk_fast(zc, K)
+    np.testing.assert_array_equal(idx[rows.cuda()].cpu().numpy(), ref)
+    np.testing.assert_array_equal(vals[rows.cuda()].cpu().numpy(), np.take_along_axis(zc, ref, 1))
+
+
+def test_eval_batch_tie_flood_is_exact():
+    """eval_batch on a head whose logits hold a flood of exact ties (every
+    item's weight row and bias equal): every row's candidate band overflows the
+    cap, the rows are scanned whole, and the top-K ids are the lowest indices
+    (canonical order) — never uninitialised ids; novelty reads valid ids."""
+    from recommenders.hip.evalpath import eval_batch, head_for
+    from recommenders.hip.qlearn import unpopular_bitmap
+    from recommenders.data_utils.synthetic import SessionStream
+    N, L, B, K = 5000, 8, 64, 20
+    m = _model(N=N, L=L)
+    head = head_for(m, 0)
+    with torch.no_grad():
+        head.W.p.copy_(head.W.p[0:1].expand_as(head.W.p))
+        head.b.p.fill_(0.25)
+    s, a, r, sn, ln, nln, e = SessionStream(N, L, B, seed=3).batch(0, B)
+    for screen in (True, False):
+        out = eval_batch(m, s, ln, a, K=K, ks=(20,), bitmap=unpopular_bitmap(set(range(0, N, 2)), N, "cuda"),
+                         k_nov=K, want_loss=not screen, screen=screen)
+        torch.cuda.synchronize()
+        assert (out.idx.cpu() == torch.arange(K, dtype=torch.int32)).all()
+        np.testing.assert_allclose(out.nov.cpu().numpy(), 0.5)
+    assert int(head.top_scanned.item()) >= B
 
 
 def test_eval_allocates_no_logits():

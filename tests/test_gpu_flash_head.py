@@ -358,7 +358,7 @@ def run_top(h, W, b, terms, nsplit, K, exact1=False):
         cap = call("rg_flash_topk_cap")
         cand, ncand = z(B, cap, dt=torch.int32), z(B, dt=torch.int32)
         work = _u8(call("rg_flash_topk_work_bytes", B, A, K))
-        call("rg_flash_topk", cmax.data_ptr(), B, A, K, 1e-4, 1e-4, h.data_ptr(), W.data_ptr(), b.data_ptr(), HF,
+        call("rg_flash_topk", cmax.data_ptr(), B, B, A, K, 1e-4, 1e-4, h.data_ptr(), W.data_ptr(), b.data_ptr(), HF,
              cand.data_ptr(), ncand.data_ptr(), idx.data_ptr(), vals.data_ptr(), err.data_ptr(), work.data_ptr(), st)
     torch.cuda.synchronize()
     return idx.cpu().long(), vals.cpu().double(), int(err.item()), (None if cmax is None else cmax.cpu().double())
@@ -531,9 +531,10 @@ def test_screening_argmax_is_exact(B, A, HF, nsplit):
     cand = torch.empty(B, cap, dtype=torch.int32, device=dev)
     ncand = torch.empty(B, dtype=torch.int32, device=dev)
     lim = torch.empty(B, device=dev)
+    scanned = torch.zeros(1, dtype=torch.int32, device=dev)
     call("rg_flash_argmax_exact", cmax.data_ptr(), B, A, hd.data_ptr(), Wd.data_ptr(), bd.data_ptr(), HF,
          wn.data_ptr(), 1e-4, lim.data_ptr(), cand.data_ptr(), ncand.data_ptr(),
-         idx.data_ptr(), val.data_ptr(), st)
+         idx.data_ptr(), val.data_ptr(), scanned.data_ptr(), st)
     torch.cuda.synchronize()
     assert abs(float(wn) - float(W.norm(dim=1).max())) <= 1e-5 * float(W.norm(dim=1).max())
     idx, val = idx.cpu().long(), val.cpu().double()
@@ -556,17 +557,34 @@ def test_screening_argmax_is_exact(B, A, HF, nsplit):
     assert int(idx[rows_eq]) == int(torch.argmax(b_eq.double()))
 
 
-def test_screening_argmax_overflow_keeps_first():
-    """Every logit of a row equal (h = 0, bias 0): more candidate chunks than
-    rg_flash_topk_cap(), so the row keeps the screening's first maximum (item
-    0); the other rows are still re-scored."""
-    call, st = C().call, C().stream_ptr()
-    B, A, HF, nsplit = 64, 5003, 64, 8
-    g = torch.Generator().manual_seed(5)
+def _tie_flood(B, A, HF, row, step, seed):
+    """Inputs where one row's best logits are a flood of exact ties (a copy of
+    one W row at every ``step``-th item, far more than the candidate cap)
+    plus, at a late copy, a winner larger by ~1e-5 relative that lives in the
+    low-order bf16 planes (the 3-product screening does not see it).  The
+    other rows are random.  Returns (h, W, b, winner)."""
+    g = torch.Generator().manual_seed(seed)
     h = torch.tanh(torch.randn(B, HF, generator=g))
-    h[7] = 0.0
     W = torch.randn(A, HF, generator=g) * 0.3
-    b = torch.zeros(A)
+    b = torch.full((A,), -4.0)
+    copy = torch.randn(HF, generator=g) * 0.3
+    W[::step] = copy
+    b[::step] = 0.0
+    win = (A - 1) // step * step - step
+    W[win] = copy + 2.0 ** -20 * copy.abs() * torch.sign(h[row])
+    return h, W, b, win
+
+
+def test_screening_argmax_overflow_scans_row():
+    """A row whose screening band holds more candidate chunks than
+    rg_flash_topk_cap() (a flood of exact ties): the row is scanned whole in
+    fp32 (counted in err) and gets the first maximum of its fp32 logits — here
+    a winner the 3-product screening cannot see; the other rows are
+    re-scored as usual.  (Reference: torch.argmax of the fp32 Q row,
+    sqn_gru.py:222-226.)"""
+    call, st = C().call, C().stream_ptr()
+    B, A, HF, nsplit, row = 64, 5003, 64, 8, 7
+    h, W, b, win = _tie_flood(B, A, HF, row, 16, 5)
     hd, Wd, bd = h.to(dev), W.to(dev), b.to(dev)
     hb, wb = call("rg_head_plane_bytes", B, HF), call("rg_head_plane_bytes", A, HF)
     Hk, Wk = _u8(hb), _u8(wb)
@@ -579,18 +597,64 @@ def test_screening_argmax_overflow_keeps_first():
          parg.data_ptr(), cmax.data_ptr(), st)
     idx, val = torch.empty(B, dtype=torch.int32, device=dev), torch.empty(B, device=dev)
     call("rg_flash_argmax", pbest.data_ptr(), parg.data_ptr(), nsplit, B, idx.data_ptr(), val.data_ptr(), st)
+    screened = idx.clone()
     wn = torch.empty(1, device=dev)
     call("rg_row_norm_max", Wd.data_ptr(), A, HF, wn.data_ptr(), st)
     cap = call("rg_flash_topk_cap")
     cand, ncand = torch.empty(B, cap, dtype=torch.int32, device=dev), torch.empty(B, dtype=torch.int32, device=dev)
     lim = torch.empty(B, device=dev)
+    scanned = torch.zeros(1, dtype=torch.int32, device=dev)
     call("rg_flash_argmax_exact", cmax.data_ptr(), B, A, hd.data_ptr(), Wd.data_ptr(), bd.data_ptr(), HF,
-         wn.data_ptr(), 1e-4, lim.data_ptr(), cand.data_ptr(), ncand.data_ptr(), idx.data_ptr(), val.data_ptr(), st)
+         wn.data_ptr(), 1e-4, lim.data_ptr(), cand.data_ptr(), ncand.data_ptr(), idx.data_ptr(), val.data_ptr(),
+         scanned.data_ptr(), st)
     torch.cuda.synchronize()
-    assert int(ncand[7]) > cap and int(idx[7]) == 0
-    Z = h.double() @ W.double().t()
-    ok = torch.arange(B) != 7
-    assert torch.equal(idx.cpu().long()[ok], Z.argmax(1)[ok])
+    Z = h.double() @ W.double().t() + b.double()
+    assert int(ncand[row]) > cap and int(scanned) >= 1
+    assert int(screened[row]) != win                 # the screening alone misses it
+    assert int(idx[row]) == win == int(Z[row].argmax())
+    assert torch.equal(idx.cpu().long(), Z.argmax(1))
+
+
+@pytest.mark.parametrize("K", [1, 5])
+def test_fused_topk_overflow_scans_row(K):
+    """rg_flash_topk past the candidate cap (the same tie flood in pass 1's
+    chunk maxima): the row is scanned whole and its list is the canonical
+    (value desc, index asc) top-K of the fp32 logits — the winner, then the
+    tied copies in index order; every other row as usual."""
+    B, A, HF, nsplit, row = 64, 5003, 64, 8, 11
+    h, W, b, win = _tie_flood(B, A, HF, row, 16, 9)
+    idx, vals, err, _ = run_top(h.to(dev), W.to(dev), b.to(dev), 6, nsplit, K, exact1=True)
+    assert err >= 1
+    Z = (h.double() @ W.double().t() + b.double()).numpy()
+    from oracle import metrics as om
+    ref = om.canonical_topk(Z, K)
+    assert int(idx[row, 0]) == win
+    np.testing.assert_array_equal(idx.numpy(), ref)
+
+
+def test_stored_logit_topk_overflow_scans_row():
+    """rg_topk over stored logits with more than its 2048 candidates >= tau
+    (3000 exact ties at the top of one row): the row is scanned whole, the
+    list is the canonical top-K (lowest tied indices), no error raised."""
+    call, st = C().call, C().stream_ptr()
+    B, A, K = 8, 9001, 20
+    g = torch.Generator().manual_seed(2)
+    Z = torch.randn(B, A, generator=g)
+    Z[3, ::3] = 9.0
+    ZT = Z.t().contiguous().to(dev)
+    from recommenders.hip import load_library
+    pb = load_library().rg_partial_block()
+    nJ = (A + pb - 1) // pb
+    pmax = torch.stack([Z[:, j * pb:(j + 1) * pb].max(1).values for j in range(nJ)]).contiguous().to(dev)
+    idx = torch.empty(B, K, dtype=torch.int32, device=dev)
+    vals = torch.empty(B, K, device=dev)
+    err = torch.zeros(1, dtype=torch.int32, device=dev)
+    call("rg_topk", ZT.data_ptr(), B, pmax.data_ptr(), B, A, K, idx.data_ptr(), vals.data_ptr(), err.data_ptr(), st)
+    torch.cuda.synchronize()
+    from oracle import metrics as om
+    assert int(err) == 0
+    np.testing.assert_array_equal(idx.cpu().numpy(), om.canonical_topk(Z.numpy(), K))
+    assert (idx[3].cpu() == torch.arange(0, 3 * K, 3, dtype=torch.int32)).all()
 
 
 def test_screening_argmax_row_chunks_match(monkeypatch):
@@ -616,3 +680,105 @@ def test_screening_argmax_row_chunks_match(monkeypatch):
     zmax = Z.max(1).values
     gap = zmax - Z[torch.arange(B), i1.cpu().long()]
     assert float(gap.max()) <= 1e-5
+
+
+def _plant_top1_ties(h, W, b, Z):
+    """Exact ties (a copy of a row's winner at a higher index) and near ties
+    (a copy 1e-6 better at a lower index) for every third row."""
+    A = W.shape[0]
+    top = Z.argmax(1)
+    for r in range(0, h.shape[0], 3):
+        j = int(top[r])
+        k = (j * 7919 + 13) % A
+        if k > j:
+            W[k], b[k] = W[j], b[j]
+    for r in range(1, h.shape[0], 3):
+        j = int(top[r])
+        k = (j * 104729 + 7) % A
+        if k < j:
+            W[k], b[k] = W[j], b[j] + 1e-6
+
+
+def _head_top1(A, HF, h, W, b):
+    from recommenders.hip import engine
+    hd = engine.SoftmaxHead("sup", A, HF, dev)
+    hd.set_matmul_precision("f32x6d3")
+    with torch.no_grad():
+        hd.W.p.copy_(W)
+        hd.b.p.copy_(b)
+    hd.top_k = 1
+    tgt = torch.zeros(h.shape[0], dtype=torch.int64, device=dev)
+    _, w = hd.forward_loss(h, tgt, slot="main")
+    idx, val = hd.top_entries(w)
+    torch.cuda.synchronize()
+    return hd, w, idx[:, 0].clone(), val[:, 0].clone()
+
+
+def test_top1_row_chunked_screening_matches_chunk_maxima(monkeypatch):
+    """SMORL's K = 1 reward item when pass 1's chunk maxima would exceed
+    SCREEN_CMAX_BYTES (C5 on one GPU): the row-chunked screening argmax on
+    pass 1's planes + fp32 re-scoring gives the same items and values as the
+    chunk-maxima path (both the first maximum of the fp32 logits)."""
+    from recommenders.hip import engine
+    B, A, HF = 1024, 20011, 128
+    g = torch.Generator().manual_seed(17)
+    h = torch.tanh(torch.randn(B, HF, generator=g))
+    W, b = torch.randn(A, HF, generator=g) * 0.3, torch.randn(A, generator=g) * 0.3
+    _plant_top1_ties(h, W, b, h.double() @ W.double().t() + b.double())
+    hd1, w1, i1, v1 = _head_top1(A, HF, h.to(dev), W.to(dev), b.to(dev))
+    assert w1.cmax is not None
+    monkeypatch.setattr(engine, "SCREEN_CMAX_BYTES", 1)
+    monkeypatch.setattr(engine, "SCREEN_ROW_CHUNK", 256)
+    hd2, w2, i2, v2 = _head_top1(A, HF, h.to(dev), W.to(dev), b.to(dev))
+    assert w2.cmax is None and w2.top1.Bc == 256
+    assert torch.equal(i1, i2) and torch.equal(v1, v2)
+    Z = h.double() @ W.double().t() + b.double()
+    first = (Z >= Z.max(1).values[:, None]).double().argmax(1)
+    for r in range(0, B, 3):
+        assert int(i2[r]) == int(first[r])
+    for r in range(1, B, 3):
+        assert int(i2[r]) == int(first[r])
+
+
+def test_top1_above_2gb_of_chunk_maxima_is_first_fp32_maximum():
+    """The same K = 1 path at a size whose chunk maxima really exceed 2 GB
+    (A = 2M, B = 8704: 2.18 GB): planted exact / 1e-6 near ties resolve to the
+    first maximum of the fp32 logits (fp64 first maximum, away from fp32
+    rounding of the two items)."""
+    B, A, HF = 8704, 2_000_000, 32
+    assert -(-A // 32) * B * 4 > 2 << 30
+    g = torch.Generator(device=dev).manual_seed(23)
+    h = torch.tanh(torch.randn(B, HF, generator=g, device=dev))
+    W = torch.randn(A, HF, generator=g, device=dev) * 0.3
+    b = torch.randn(A, generator=g, device=dev) * 0.3
+    top = torch.cat([(h[r0:r0 + 512].double() @ W.double().t() + b.double()).argmax(1)
+                     for r0 in range(0, B, 512)]).cpu()
+    Wc, bc = W.cpu(), b.cpu()
+    for r in range(0, 600, 3):
+        j = int(top[r])
+        k = (j * 7919 + 13) % A
+        if k > j:
+            Wc[k], bc[k] = Wc[j], bc[j]
+    for r in range(1, 600, 3):
+        j = int(top[r])
+        k = (j * 104729 + 7) % A
+        if k < j:
+            Wc[k], bc[k] = Wc[j], bc[j] + 1e-6
+    W, b = Wc.to(dev), bc.to(dev)
+    hd, w, idx, val = _head_top1(A, HF, h, W, b)
+    assert w.cmax is None and w.top1 is not None
+    del w
+    hd.release_eval()
+    for r0 in range(0, B, 512):
+        Z = h[r0:r0 + 512].double() @ W.double().t() + b.double()
+        zmax = Z.max(1).values
+        first = (Z >= zmax[:, None]).double().argmax(1)
+        got = idx[r0:r0 + 512].long()
+        gap = zmax - Z.gather(1, got[:, None])[:, 0]
+        sl = (h[r0:r0 + 512].abs().double() @ W.abs().double().t()).max(1).values
+        bad = (got != first) & (gap > 200 * 2.0 ** -24 * sl)
+        assert not bool(bad.any()), r0
+        if r0 == 0:   # the planted rows: exactly the first maximum
+            assert torch.equal(got[:600], first[:600])
+        torch.testing.assert_close(val[r0:r0 + 512].double(), Z.gather(1, got[:, None])[:, 0],
+                                   rtol=0, atol=float(200 * 2.0 ** -24 * sl.max()))

@@ -341,9 +341,15 @@ def test_q_kernels_and_rewards():
     for j in unpop:
         bm[j >> 5] |= np.uint32(1 << (j & 31))
     outn = torch.zeros(B, device=dev)
-    hip.call("rg_novelty", D(top).data_ptr(), 3, 3, D(torch.from_numpy(bm.view(np.int32))).data_ptr(), 2.0,
-             B, outn.data_ptr(), st())
+    bmd = D(torch.from_numpy(bm.view(np.int32)))
+    hip.call("rg_novelty", D(top).data_ptr(), 3, 3, bmd.data_ptr(), A, 2.0, B, outn.data_ptr(), st())
     np.testing.assert_allclose(outn.cpu().numpy(), om.batch_novelty_rewards(preds, unpop, 2.0, 3), atol=1e-6)
+    # an id outside [0, A) (never a real prediction): NaN for that row, no bitmap read
+    bad = top.clone()
+    bad[0, 1], bad[1, 0] = -1, A + 40
+    hip.call("rg_novelty", D(bad).data_ptr(), 3, 3, bmd.data_ptr(), A, 2.0, B, outn.data_ptr(), st())
+    o = outn.cpu().numpy()
+    assert np.isnan(o[:2]).all() and not np.isnan(o[2:]).any()
 
 
 @pytest.mark.parametrize("M,N,T,splits", [(384, 128, 5000, 16), (48, 16, 77, 3), (192, 64, 3000, 128)])
