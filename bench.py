@@ -249,7 +249,8 @@ def make_trainer(cfg, args, dev, shard):
     if cfg == "c2native":
         return GRU4Rec_trainer(matmul_precision="f32", **common)
     if cfg == "c2s":   # GRU4Rec at C2 shapes with the sampled head (north-star target step)
-        return GRU4Rec_trainer(n_negatives=args.negatives, matmul_precision=args.precision, **common)
+        return GRU4Rec_trainer(n_negatives=args.negatives, matmul_precision=args.precision, shard_items=shard,
+                               **common)
     if cfg == "c3":
         return BidirGRU4Rec_trainer(dropout=0.0, n_negatives=args.negatives, matmul_precision=args.precision,
                                     **common)
@@ -342,19 +343,34 @@ def sampled_fwd_bytes(B, S, HF):
     return B * HF * 4 + B * 4 + S * 4 + (B + S) * (HF + 1) * 4 + B * (S + 1) * 4
 
 
+def exchange_bytes(T, B, S, E, HF):
+    """Collective payload per rank of the item-sharded gather + sampled logits
+    (DESIGN §5): the token ids out and their table rows back, the negatives'
+    rows + biases all-reduced, the targets' ids out and rows + biases back."""
+    return {"token_ids": int(4 * T), "token_rows": int(4 * E * T), "neg_rows_allreduce": int(4 * S * (HF + 1)),
+            "target_ids": int(4 * B), "target_rows": int(4 * B * (HF + 1))}
+
+
 def target_step(kern, T, B, S, E, HF, n_gather, terms):
     """North-star target: embedding gather + sampled logits (fwd) against the
-    HBM roofline, with the logits' MFMA rate beside it."""
+    HBM roofline, with the logits' MFMA rate beside it.  On an
+    item-sharded run the gather region is the whole exchange (route, id / row
+    all-to-alls, owner gather, placement) and the negatives' / targets' row
+    exchange (neg_exchange) is timed into the step too; the algorithmic bytes
+    stay the one-GPU ones, the exchanged bytes are stated beside them."""
     if "gather" not in kern or "sampled_fwd" not in kern:
         return None
-    tg, ts = kern["gather"] * n_gather, kern["sampled_fwd"]
+    tg, ts, tx = kern["gather"] * n_gather, kern["sampled_fwd"], kern.get("neg_exchange", 0.0)
     by = n_gather * gather_bytes(T, E) + sampled_fwd_bytes(B, S, HF)
-    gbs = by / ((tg + ts) * 1e-3) / 1e9
+    gbs = by / ((tg + ts + tx) * 1e-3) / 1e9
     fl = 2.0 * B * S * HF
     out = {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-           "frac": round(gbs / HBM_PEAK_GBS, 4), "bytes_per_step": int(by), "ms": round(tg + ts, 4),
+           "frac": round(gbs / HBM_PEAK_GBS, 4), "bytes_per_step": int(by), "ms": round(tg + ts + tx, 4),
            "gather_ms": round(tg, 4), "gather_GBs": round(n_gather * gather_bytes(T, E) / (tg * 1e-3) / 1e9, 1),
            "sampled_fwd_ms": round(ts, 4), "sampled_fwd_alg_TFLOPs": round(fl / (ts * 1e-3) / 1e12, 2)}
+    if "neg_exchange" in kern:
+        out["neg_exchange_ms"] = round(tx, 4)
+        out["exchange_bytes_per_rank"] = exchange_bytes(T, B, S, E, HF)
     if terms:
         out["sampled_fwd_mfma_frac"] = round(terms * fl / (ts * 1e-3) / 1e12 / BF16_MFMA_PEAK_TFLOPS, 4)
         out["mfma"] = f"bf16 MFMA, {terms} plane products per fp32 product"
@@ -637,23 +653,25 @@ def main():
             if not args.no_target and kern:
                 # north-star target step measured on GRU4Rec at C2
                 # shapes with the sampled head: a short side run, own trainer, on
-                # every rank (its own batch shard; the sampled head keeps the
-                # whole table: it is not item-sharded)
-                tr2 = make_trainer("c2s", args, dev, False)
+                # every rank (its own batch shard); at N > 1 item-sharded like the
+                # C2 line (row-sharded table, engine.ShardedSampledHead)
+                tr2 = make_trainer("c2s", args, dev, shard)
                 tr2.set_train()
                 _, _, k2, _ = timed_run(tr2, batches, min(5, args.warmup), min(30, args.steps), world, True, "c2")
                 target = target_step(k2, T, B, args.negatives, E, E, 1, terms)
                 if target is not None and world > 1:
                     by_sum, = max_over_ranks([float(target["bytes_per_step"])], op="sum")
-                    tg, ts = max_over_ranks([k2["gather"], k2["sampled_fwd"]])
-                    gbs = by_sum / ((tg + ts) * 1e-3) / 1e9
+                    tg, ts, tx = max_over_ranks([k2["gather"], k2["sampled_fwd"], k2.get("neg_exchange", 0.0)])
+                    gbs = by_sum / ((tg + ts + tx) * 1e-3) / 1e9
                     target.update({"achieved": round(gbs, 1), "peak": HBM_PEAK_GBS * world,
                                    "frac": round(gbs / (HBM_PEAK_GBS * world), 4), "bytes_per_step": int(by_sum),
-                                   "ms": round(tg + ts, 4), "gather_ms": round(tg, 4), "sampled_fwd_ms": round(ts, 4),
-                                   "ranks": world,
-                                   "note": "every rank's gather + sampled logits over its own batch shard (local "
-                                           "whole table); bytes summed over ranks, kernel times max over ranks, "
-                                           "peak = ranks x 8 TB/s"})
+                                   "ms": round(tg + ts + tx, 4), "gather_ms": round(tg, 4),
+                                   "sampled_fwd_ms": round(ts, 4), "neg_exchange_ms": round(tx, 4), "ranks": world,
+                                   "note": "item-sharded: every rank's gather (route, id / row all-to-alls, owner "
+                                           "gather, placement) + the negatives' / targets' row exchange + the "
+                                           "sampled logits over its own batch shard; algorithmic bytes (one-GPU "
+                                           "definition) summed over ranks, region times max over ranks, peak = "
+                                           "ranks x 8 TB/s; exchange_bytes_per_rank beside"})
                 if target is not None:
                     target["workload"] = f"GRU4Rec {N} items dim{E} batch {B}/GPU, {args.negatives} sampled negatives"
                     target["kernel_ms"] = k2

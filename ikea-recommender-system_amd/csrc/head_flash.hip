@@ -617,6 +617,47 @@ __global__ __launch_bounds__(256) void k_flash_dh(const float* __restrict__ pm, 
 // k_flash_tail sums them in order and finishes (Adam, planes).  At C2 the
 // 67 leftover blocks of 3907 would otherwise run as a 16th round on 26% of
 // the CUs.
+// Diagnostic build only (-DFL2_STAMP, tools/fl2stamp.py): per-wave phase
+// cycles of pass 2 — prologue, S-part MFMA issue, dZ VALU, W-part MFMA issue,
+// chunk barriers, epilogue — plus the wave's start / end (s_memrealtime).
+#ifdef FL2_STAMP
+constexpr int FL2_MAXB = 4608, FL2_F = 8;
+__device__ uint64_t g_fl2_stamp[FL2_MAXB * 8 * FL2_F];
+extern "C" int rg_fl2_stamp_read(void* dst, int64_t n) {
+  return hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_fl2_stamp), n * 8, 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
+#define FL2_DECL uint64_t f2_acc[6] = {0, 0, 0, 0, 0, 0}; uint64_t f2_t = __builtin_amdgcn_s_memtime(); \
+  const uint64_t f2_r0 = __builtin_amdgcn_s_memrealtime();
+#define FL2_MARK(k)                                    \
+  do {                                                 \
+    const uint64_t _n = __builtin_amdgcn_s_memtime();  \
+    f2_acc[k] += _n - f2_t;                            \
+    f2_t = _n;                                         \
+  } while (0)
+#define FL2_SYNC()   \
+  do {               \
+    FL2_MARK(3);     \
+    __syncthreads(); \
+    FL2_MARK(4);     \
+  } while (0)
+#define FL2_STORE()                                                                          \
+  do {                                                                                       \
+    if (lane == 0 && blockIdx.x < FL2_MAXB) {                                                \
+      uint64_t* _d = g_fl2_stamp + ((int64_t)blockIdx.x * 8 + w) * FL2_F;                    \
+      _d[0] = f2_r0;                                                                         \
+      _d[1] = __builtin_amdgcn_s_memrealtime();                                              \
+      for (int _k = 0; _k < 6; ++_k) _d[2 + _k] = f2_acc[_k];                                \
+    }                                                                                        \
+  } while (0)
+#else
+#define FL2_DECL
+#define FL2_MARK(k)
+#define FL2_SYNC() __syncthreads()
+#define FL2_STORE()
+#endif
+// phases: 0 prologue, 1 S-part MFMA issue, 2 dZ VALU + split, 3 W-part MFMA
+// issue, 4 barrier wait, 5 epilogue (db / Adam / planes, or the tail partials)
+
 template <int HF, int NT>
 __global__ __launch_bounds__(64 * fl_nw(HF, 2)) void k_flash_dw(
     const bf16x8* __restrict__ Hk0, const bf16x8* __restrict__ Hr0, const bf16x8* Wk, const float* bias_pad,
@@ -634,6 +675,7 @@ __global__ __launch_bounds__(64 * fl_nw(HF, 2)) void k_flash_dw(
   __shared__ __attribute__((aligned(16))) float2 si0[32], si1[32];
   const int tid = threadIdx.x, lane = tid & 63, kg = lane >> 4, l16 = lane & 15, lane16 = 16 * lane;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  FL2_DECL
   const int bx = blockIdx.x;
   const bool tail = bx >= nfull;
   const int blk = tail ? nfull + (bx - nfull) / tsplit : bx;
@@ -674,6 +716,7 @@ __global__ __launch_bounds__(64 * fl_nw(HF, 2)) void k_flash_dw(
 #pragma unroll
     for (int fb = 0; fb < NF; ++fb) dw[ib][fb] = f4{0.f, 0.f, 0.f, 0.f};
   __syncthreads();
+  FL2_MARK(0);
   // S = h_c·Wᵀ recomputed, dZ = g·(2^(S−lse) − onehot), db; dZᵀ planes
   // (q*[ib]: the A operand of dW, k over the chunk's rows in kperm16 order)
   auto spart = [&](const bf16x8* sk, const float2* si, bf16x8 (&q0)[2], bf16x8 (&q1)[2], bf16x8 (&q2)[2])
@@ -697,6 +740,7 @@ __global__ __launch_bounds__(64 * fl_nw(HF, 2)) void k_flash_dw(
       a2 = n2;
       __builtin_amdgcn_sched_barrier(0);
     }
+    FL2_MARK(1);
 #pragma unroll
     for (int ib = 0; ib < 2; ++ib) {
       const int item = j0 + 16 * ib + l16;
@@ -718,6 +762,7 @@ __global__ __launch_bounds__(64 * fl_nw(HF, 2)) void k_flash_dw(
       dbs[ib] += cdb;
       split3x8(sa[0][ib], sa[1][ib], q0[ib], q1[ib], q2[ib]);
     }
+    FL2_MARK(2);
   };
   // dW += dZᵀ·h_c, one R-plane fragment of h per feature block
   auto wpart = [&](const bf16x8* sr, const bf16x8 (&q0)[2], const bf16x8 (&q1)[2], const bf16x8 (&q2)[2])
@@ -734,6 +779,7 @@ __global__ __launch_bounds__(64 * fl_nw(HF, 2)) void k_flash_dw(
       b2 = n2;
       __builtin_amdgcn_sched_barrier(0);
     }
+    FL2_MARK(3);
   };
   for (int c = 0; c < nch; c += 2) {
     bf16x8 q0[2], q1[2], q2[2];
@@ -747,7 +793,7 @@ __global__ __launch_bounds__(64 * fl_nw(HF, 2)) void k_flash_dw(
         spart(sk0, si0, q0, q1, q2);
         wpart(sr0, q0, q1, q2);
       }
-      __syncthreads();
+      FL2_SYNC();
       if (c + 1 < nch) {
         if (c + 2 < nch) {
           FL_ISSUE_K(c + 2, sk0, si0);
@@ -758,23 +804,23 @@ __global__ __launch_bounds__(64 * fl_nw(HF, 2)) void k_flash_dw(
           spart(sk1, si1, q0, q1, q2);
           wpart(sr1, q0, q1, q2);
         }
-        __syncthreads();
+        FL2_SYNC();
       }
     } else {
       if (c + 1 < nch) FL_ISSUE_K(c + 1, sk1, si1);
       __builtin_amdgcn_sched_barrier(0);
       if (active) spart(sk0, si0, q0, q1, q2);
-      __syncthreads();
+      FL2_SYNC();
       if (active) wpart(sr0, q0, q1, q2);
-      __syncthreads();
+      FL2_SYNC();
       if (c + 1 < nch) {
         FL_ISSUE_R(c + 1, sr0);
         if (c + 2 < nch) FL_ISSUE_K(c + 2, sk0, si0);
         __builtin_amdgcn_sched_barrier(0);
         if (active) spart(sk1, si1, q0, q1, q2);
-        __syncthreads();
+        FL2_SYNC();
         if (active) wpart(sr0, q0, q1, q2);
-        __syncthreads();
+        FL2_SYNC();
         if (c + 2 < nch) FL_ISSUE_R(c + 2, sr0);
       }
     }
@@ -802,7 +848,10 @@ __global__ __launch_bounds__(64 * fl_nw(HF, 2)) void k_flash_dw(
     bf16x8* base = ai == 0 ? sk0 : ai == 1 ? sk1 : ai == 2 ? sr0 : sr1;
     tr = reinterpret_cast<float*>(base) + ao;
   }
-  if (!active) return;
+  if (!active) {
+    FL2_STORE();
+    return;
+  }
   const bool planes = Wk_out != nullptr && dW_out == nullptr;
   float dbt[2];
 #pragma unroll
@@ -824,6 +873,8 @@ __global__ __launch_bounds__(64 * fl_nw(HF, 2)) void k_flash_dw(
           if (it < A) tail_dw[((int64_t)part * ntail + it - i0) * HF + 16 * fb + l16] = dw[ib][fb][i];
         }
     }
+    FL2_MARK(5);
+    FL2_STORE();
     return;
   }
 #pragma unroll
@@ -929,6 +980,8 @@ __global__ __launch_bounds__(64 * fl_nw(HF, 2)) void k_flash_dw(
       }
     }
   }
+  FL2_MARK(5);
+  FL2_STORE();
 }
 
 // -------------------------------------------------------- fused top-k ----

@@ -313,6 +313,8 @@ constexpr int sf_nw(int HF) { return HF <= 128 ? SF_NW : 4; }
 constexpr int sf_neg(int HF) { return 32 * sf_nw(HF); }   // negatives per workgroup
 constexpr int sf_thr(int HF) { return 64 * sf_nw(HF); }   // threads per workgroup
 constexpr int SF_ROWS = 128;  // rows per workgroup (4 chunks of 32)
+// s_waitcnt immediate: vmcnt <= n (6 bits, split), expcnt free, lgkmcnt 0
+constexpr int sf_wc_vm(int n) { return (n & 15) | ((n >> 4) << 14) | 0x70; }
 
 // Diagnostic build only (-DSF_STAMP, tools/sfstamp.py): per-wave s_memrealtime
 // stamps at the phase boundaries of k_sampled_logits, read back by rg_sf_stamp_read.
@@ -445,6 +447,7 @@ __global__ __launch_bounds__(sf_thr(HF)) void k_sampled_logits(const float* __re
   const float bl = PRE ? bg[s_me] : bias[id];
   if constexpr (HKP) {
     dma_chunk(hsA, 0);
+    __builtin_amdgcn_sched_barrier(0);   // chunk 0's DMA stays ahead of the W loads (SF_EARLY counts on it)
   } else {
     load_h(0);
   }
@@ -486,7 +489,23 @@ __global__ __launch_bounds__(sf_thr(HF)) void k_sampled_logits(const float* __re
     if (nch > 1) dma_chunk(hsB, 1);
     if (nch > 2) dma_chunk(hsC, 2);
     if (nch > 3) dma_chunk(hsD, 3);
+#ifdef SF_EARLY
+    // wait only for chunk 0's h planes (issued before the 3·NS W-plane loads and
+    // chunks 1..3's 3·NDMA DMA ops): chunk 0's MFMAs start while the W planes
+    // land slice by slice (the compiler's per-register waits) and chunks 1..3
+    // get their own wait + barrier below
+    constexpr int NDMA = CH / SF_THR;
+    constexpr bool EARLY = PRE && CH % SF_THR == 0;
+    if (EARLY && nch == 4) {
+      __builtin_amdgcn_s_waitcnt(sf_wc_vm(3 * NS + 3 * NDMA));
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+    } else {
+      __syncthreads();
+    }
+#else
     __syncthreads();
+#endif
     SFD_T(1);
   } else {
     store_h(hsA);
@@ -582,7 +601,14 @@ __global__ __launch_bounds__(sf_thr(HF)) void k_sampled_logits(const float* __re
     }
   };
   if constexpr (HKP) {
-    // chunks 1..3 landed at the first barrier
+    // chunks 1..3 landed at the first barrier (SF_EARLY: at this one)
+#ifdef SF_EARLY
+    if (PRE && CH % SF_THR == 0 && nch == 4) {
+      __builtin_amdgcn_s_waitcnt(sf_wc_vm(0));
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+    }
+#endif
     if (nch > 1) {
       if (nact) {
         mma(hsB, accB);

@@ -121,6 +121,12 @@ SIGNATURES = {
     "rg_rows_gather": [P, I, I64, I64, P, I, I, P, P, P],
     "rg_place_rows": [P, I, P, P, P, I, I, I, P, P],
     "rg_collect_grads": [P, P, P, P, P, I, I, P, P],
+    "rg_neg_pick": [U64, U64, I64, I, I, I64, I64, P, P, P, P, P, P, P],
+    "rg_neg_planes": [P, I, I, P, P],
+    "rg_target_ids": [P, I, I64, P, P, P],
+    "rg_head_rows_gather": [P, I, I64, I64, P, P, I, P, P, P, P],
+    "rg_rows_unslot": [P, P, P, P, I, I, P, P, P],
+    "rg_rows_slot": [P, P, P, I, I, P, P, P],
 }
 
 _lib = None

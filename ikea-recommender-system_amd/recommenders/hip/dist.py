@@ -93,17 +93,35 @@ def owner_counts(s, lens, L, packed, n_rows, world):
     return np.bincount(own, minlength=world).astype(np.int64)
 
 
-def host_routes(comm, trunk, passes):
+def target_owner_counts(a, n_items, world):
+    """Per owner rank, the number of this batch's targets whose output row it
+    holds (host restatement of csrc/sampled_shard.hip k_target_ids +
+    k_shard_route: owner ⌈(a+1)·W/A⌉ − 1, targets outside [0, A) to rank 0)."""
+    a = np.asarray(a, dtype=np.int64).reshape(-1)
+    ok = (a >= 0) & (a < n_items)
+    own = np.where(ok, ((a + 1) * world + n_items - 1) // n_items - 1, 0)
+    return np.bincount(own, minlength=world).astype(np.int64)
+
+
+def host_routes(comm, trunk, passes, targets=None):
     """Send / receive splits of every trunk pass's id / row exchange, from
     the host batch: owner counts per pass, one host all-gather over the gloo
-    group (W × passes × W ints).  passes: [(s, lens)] host tensors; returns
+    group (W × passes × W ints).  passes: [(s, lens)] host tensors; targets:
+    optional (a, n_items) — the item-sharded sampled head's target-row
+    exchange, routed the same way (appended last).  Returns
     [(send_splits, recv_splits)] or None when a batch is already on the device
     (then the exchange routes on the device and reads the counts back)."""
     for s, ln in passes:
         if torch.as_tensor(s).device.type != "cpu" or torch.as_tensor(ln).device.type != "cpu":
             return None
-    mine = np.stack([owner_counts(torch.as_tensor(s).numpy(), torch.as_tensor(ln).numpy(), torch.as_tensor(s).shape[1],
-                                  trunk.packed, trunk.N1, comm.world) for s, ln in passes])
+    if targets is not None and torch.as_tensor(targets[0]).device.type != "cpu":
+        return None
+    rows = [owner_counts(torch.as_tensor(s).numpy(), torch.as_tensor(ln).numpy(), torch.as_tensor(s).shape[1],
+                         trunk.packed, trunk.N1, comm.world) for s, ln in passes]
+    if targets is not None:
+        rows.append(target_owner_counts(torch.as_tensor(targets[0]).numpy(), int(targets[1]), comm.world))
+    mine = np.stack(rows)
+    passes = rows
     allc = comm.host_all_gather(torch.from_numpy(mine)).numpy()   # (W, P, W): [q, p, r]
     r = comm.rank
     return [(allc[r, p, :].tolist(), allc[:, p, r].tolist()) for p in range(len(passes))]

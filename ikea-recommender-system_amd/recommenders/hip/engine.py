@@ -266,9 +266,12 @@ class Trunk:
             call("rg_pack", w.lens.data_ptr(), B, L, 0 if self.packed else 1, w.perm.data_ptr(),
                  w.lsort.data_ptr(), w.offs.data_ptr(), st)
         H, E = self.H, self.E
-        if self.comm is not None:
+        if self.comm is not None:   # the whole row-sharded gather: route, id / row all-to-alls, placement
             with region("gather"):
                 self._exchange_rows(w, s, B, L, st, route)
+                for d in range(self.ndir):
+                    call("rg_place_rows", w.rows_in.data_ptr(), 1 if self.emb16 is not None else 0,
+                         w.slot.data_ptr(), w.lsort.data_ptr(), w.offs.data_ptr(), B, E, d, w.X[d].data_ptr(), st)
         # a sampled head's negatives row gather rides in the first gather launch
         # (rg_gather_neg; SampledSoftmaxHead.neg_job)
         job, self.neg_job = self.neg_job, None
@@ -288,9 +291,6 @@ class Trunk:
                         call("rg_gather_h" if self.emb16 is not None else "rg_gather", s.data_ptr(), B, L,
                              w.perm.data_ptr(), w.lsort.data_ptr(), w.offs.data_ptr(), table, self.N1, E, d,
                              w.tok_id[d].data_ptr(), w.X[d].data_ptr(), self.err.data_ptr(), st)
-            else:
-                call("rg_place_rows", w.rows_in.data_ptr(), 1 if self.emb16 is not None else 0, w.slot.data_ptr(),
-                     w.lsort.data_ptr(), w.offs.data_ptr(), B, E, d, w.X[d].data_ptr(), st)
             with region("gemm_ih"):
                 call("rg_gemm_f32", w.X[d].data_ptr(), E, 1, w_ih.p.data_ptr(), 1, E, w.Gi[d].data_ptr(), 3 * H,
                      b_ih.p.data_ptr(), w.TM, w.ntok_ptr, 3 * H, E, None, 1, st)
@@ -1162,14 +1162,14 @@ class SampledSoftmaxHead(SoftmaxHead):
 
     LOSSES = ("ce", "bpr")
 
-    def __init__(self, name, A, HF, device, n_neg, seed=0, loss="ce"):
+    def __init__(self, name, A, HF, device, n_neg, seed=0, loss="ce", shard=None):
         if HF % 32 or HF > 256:
             raise ValueError(f"sampled softmax needs head width in {{32, 64, 128, 256}}, got {HF}")
         if n_neg <= 0:
             raise ValueError("n_negatives must be positive")
         if loss not in self.LOSSES:
             raise ValueError(f"sampled loss must be one of {self.LOSSES}, got {loss!r}")
-        super().__init__(name, A, HF, device)
+        super().__init__(name, A, HF, device, shard=shard)
         # "ce": CE over [target ‖ negatives]; "bpr": mean_s −log σ(z_pos − z_neg_s)
         self.loss = loss
         self.S = int(n_neg)
@@ -1177,7 +1177,7 @@ class SampledSoftmaxHead(SoftmaxHead):
         self.draws = 0
         self.G = torch.zeros_like(self.W.p)
         self.Gb = torch.zeros_like(self.b.p)
-        self.tags = torch.zeros(A, dtype=torch.int32, device=device)
+        self.tags = torch.zeros(self.A, dtype=torch.int32, device=device)
         self.tag = 0
         self.scatter = SegScatter(device)
         self._sws = {}
@@ -1300,6 +1300,164 @@ class SampledSoftmaxHead(SoftmaxHead):
                          self.A, self.tags.data_ptr(), self.tag, st)
             self.scatter(w.ids.data_ptr(), w.gb.data_ptr(), 1, w.nrows.data_ptr(), S + B, -1, self.Gb.data_ptr(),
                          self.A, self.tags.data_ptr(), self.tag, st, reuse_sort=True)
+        with region("sampled_adam"):
+            call("rg_adam_rows", self.W.p.data_ptr(), self.W.m.data_ptr(), self.W.v.data_ptr(), self.G.data_ptr(),
+                 self.tags.data_ptr(), self.tag, self.A, HF, adam6, st)
+            call("rg_adam_rows", self.b.p.data_ptr(), self.b.m.data_ptr(), self.b.v.data_ptr(), self.Gb.data_ptr(),
+                 self.tags.data_ptr(), self.tag, self.A, 1, adam6, st)
+
+
+class ShardedSampledHead(SampledSoftmaxHead):
+    """SampledSoftmaxHead item-sharded over the ranks (multi-GPU; SURVEY §8e,
+    csrc/sampled_shard.hip): this rank holds output rows [lo, hi) and their
+    Adam moments and trains its own B session rows of the global batch.  Rows
+    move to the data, never logits or an item-sized gradient:
+
+      forward   the S shared negatives (the same counter-based draw on every
+                rank): each rank writes the rows it owns, one SUM all-reduce
+                of S·(HF+1) floats (1 MB at HF 128, S 2048) gives every rank
+                all of them, cut into the logits' bf16 planes; the rank's
+                targets' rows come from their owners by all-to-all; then the
+                one-launch split logits and the CE exactly as on one GPU
+      backward  dZ, dh local; the negatives' row gradients (summed over the
+                rank's rows) SUM all-reduced, each owner scatters the rows it
+                holds; the targets' row gradients go back to their owners by
+                all-to-all; row-sparse dense-semantics Adam on the local rows.
+
+    The loss is the mean over all world·B rows (gscale = 1/(world·B)), the
+    one-GPU step on the concatenated batch up to fp32 summation order."""
+
+    def __init__(self, name, A, HF, device, n_neg, seed, loss, comm, shard):
+        if loss != "ce":
+            raise NotImplementedError("item-sharded sampled head: the CE loss only")
+        super().__init__(name, A, HF, device, n_neg, seed, loss, shard=shard)
+        self.comm = comm
+
+    def neg_job(self, slot, B):
+        return None   # the negatives' rows come from their owners (forward_loss)
+
+    def sws(self, slot, B):
+        w = super().sws(slot, B)
+        if getattr(w, "wgb", None) is None:
+            S, HF, dev = self.S, self.HF, self.device
+            z = lambda *sh, dt=torch.float32: torch.empty(*sh, dtype=dt, device=dev)  # noqa: E731
+            w.wgb = z(S * HF + S)   # the negatives' rows and biases, one all-reduce
+            w.Wg, w.bg = w.wgb[:S * HF].view(S, HF), w.wgb[S * HF:]
+            w.Wp = torch.empty(S * HF * 6, dtype=torch.uint8, device=dev)
+            w.nloc = z(S, dt=torch.int32)
+            w.nS = torch.full((1,), S, dtype=torch.int32, device=dev)
+            w.t32, w.nt = z(B, dt=torch.int32), z(1, dt=torch.int32)
+            w.tslot, w.tsend = z(B, dt=torch.int32), z(B, dt=torch.int32)
+            w.tcounts = z(self.comm.world, dt=torch.int32)
+            w.tW, w.tb = z(B, HF), z(B)
+            w.iota = torch.arange(B, dtype=torch.int64, device=dev)
+            w.nR = torch.zeros(1, dtype=torch.int32, device=dev)
+            w.gsend, w.gbsend = z(B, HF), z(B)
+            w.xb = {}
+        return w
+
+    def _xb(self, w, name, rows, cols=None, dtype=torch.float32):
+        """Exchange buffer of at least ``rows`` rows (grown ×1.25 when needed)."""
+        t = w.xb.get(name)
+        if t is None or t.shape[0] < rows:
+            n = max(16, int(rows * 1.25))
+            t = w.xb[name] = torch.empty((n,) if cols is None else (n, cols), dtype=dtype, device=self.device)
+        return t
+
+    def forward_loss(self, h, tgt, slot="main", h_planes=None, gscale=None, route=None):
+        """route: the targets' (send_splits, recv_splits) from the host batch
+        (dist.host_routes); None routes on the device and reads the counts back."""
+        B = h.shape[0]
+        w = self.sws(slot, B)
+        if w.terms == 0 or not w.zrow:
+            raise NotImplementedError("item-sharded sampled head: split-bf16 logits only (B % 32 == 0, "
+                                      "S % 32 == 0, a split matmul_precision)")
+        comm, st = self.comm, stream_ptr()
+        S, HF = self.S, self.HF
+        g = _f32(1.0 / B) if gscale is None else gscale
+        W, b = self.W.p.data_ptr(), self.b.p.data_ptr()
+        with region("neg_exchange"):
+            call("rg_neg_pick", self.seed, self.draws, self.A_full, S, HF, self.lo, self.hi, W, b, w.ids.data_ptr(),
+                 w.nloc.data_ptr(), w.Wg.data_ptr(), w.bg.data_ptr(), st)
+            comm.all_reduce(w.wgb)
+            call("rg_neg_planes", w.Wg.data_ptr(), S, HF, w.Wp.data_ptr(), st)
+            # the rank's targets' rows and biases from their owners
+            call("rg_target_ids", tgt.data_ptr(), B, self.A_full, w.t32.data_ptr(), w.nt.data_ptr(), st)
+            call("rg_shard_route", w.t32.data_ptr(), w.nt.data_ptr(), self.A_full, comm.world, w.tslot.data_ptr(),
+                 w.tsend.data_ptr(), w.tcounts.data_ptr(), st)
+            if route is not None:
+                w.send_splits, w.recv_splits = list(route[0]), list(route[1])
+            else:
+                allc = torch.zeros(comm.world * comm.world, dtype=torch.int32, device=self.device)
+                comm.all_gather(allc, w.tcounts)
+                M = allc.view(comm.world, comm.world).cpu()     # one sync
+                w.send_splits, w.recv_splits = M[comm.rank].tolist(), M[:, comm.rank].tolist()
+            R = w.R = sum(w.recv_splits)
+            recv_ids = self._xb(w, "recv_ids", max(R, 1), dtype=torch.int32)
+            comm.all_to_all(recv_ids[:R], w.tsend[:B], w.recv_splits, w.send_splits)
+            rows_out, rb_out = self._xb(w, "rows_out", max(R, 1), HF), self._xb(w, "rb_out", max(R, 1))
+            w.local_ids = self._xb(w, "local_ids", max(R, 1), dtype=torch.int32)
+            call("rg_head_rows_gather", recv_ids.data_ptr(), R, self.lo, self.A, W, b, HF, rows_out.data_ptr(),
+                 rb_out.data_ptr(), w.local_ids.data_ptr(), st)
+            rows_in, rb_in = self._xb(w, "rows_in", B, HF), self._xb(w, "rb_in", B)
+            comm.all_to_all(rows_in[:B], rows_out[:R], w.send_splits, w.recv_splits)
+            comm.all_to_all(rb_in[:B], rb_out[:R], w.send_splits, w.recv_splits)
+            call("rg_rows_unslot", rows_in.data_ptr(), rb_in.data_ptr(), w.tslot.data_ptr(), w.t32.data_ptr(), B,
+                 HF, w.tW.data_ptr(), w.tb.data_ptr(), st)
+        hp = h_planes.data_ptr() if h_planes is not None and HF <= 128 else None
+        with region("sampled_fwd", exact=True):   # the one-launch logits on the exchanged planes (draw = 2)
+            call("rg_sampled_logits", h.data_ptr(), W, b, w.ids.data_ptr(), 2, self.seed, self.draws, self.A_full,
+                 B, S, HF, w.terms, w.ZT.data_ptr(), w.ldz, w.pmax.data_ptr(), w.psum.data_ptr(), w.Wg.data_ptr(),
+                 w.bg.data_ptr(), hp, w.Wp.data_ptr(), st)
+        self.draws += 1
+        # CE with the fetched target rows (row b's target is row b of tW / tb)
+        call("rg_sampled_lse", h.data_ptr(), w.tW.data_ptr(), w.tb.data_ptr(), w.iota.data_ptr(), B, B, HF,
+             w.pmax.data_ptr(), w.psum.data_ptr(), w.nT, g, w.lse.data_ptr(), w.loss_row.data_ptr(),
+             w.ids.data_ptr() + 4 * S, w.gb.data_ptr() + 4 * S, w.grows.data_ptr() + 4 * S * HF,
+             w.dh_slabs.data_ptr(), st)
+        call("rg_sum_scale", w.loss_row.data_ptr(), B, g, w.loss.data_ptr(), None, st)
+        comm.all_reduce(w.loss)
+        return w.loss, w
+
+    def backward_step(self, h, tgt, dh_out, adam6, slot="main", gscale=None, overlap=False):
+        B = h.shape[0]
+        w = self.sws(slot, B)
+        comm, st = self.comm, stream_ptr()
+        S, HF = self.S, self.HF
+        g = _f32(1.0 / B) if gscale is None else gscale
+        with region("sampled_bwd"):
+            call("rg_sampled_dz_rows", w.ZT.data_ptr(), w.ldz, w.lse.data_ptr(), B, S, g, w.dbslabs.data_ptr(),
+                 w.gb.data_ptr(), st)
+            call("rg_gemm_f32", w.ZT.data_ptr(), w.zs_b, w.zs_s, w.Wg.data_ptr(), HF, 1,
+                 w.dh_slabs.data_ptr() + 4 * B * HF, HF, None, B, None, HF, S, None, w.dh_splits, st)
+            call("rg_reduce_slabs", w.dh_slabs.data_ptr(), w.dh_splits + 1, B * HF, dh_out.data_ptr(), None, HF, 0,
+                 st)
+            call("rg_gemm_f32", w.ZT.data_ptr(), w.zs_s, w.zs_b, h.data_ptr(), HF, 1, w.dw_slabs.data_ptr(), HF, None,
+                 S, None, HF, B, None, w.dw_splits, st)
+            call("rg_reduce_slabs", w.dw_slabs.data_ptr(), w.dw_splits, S * HF, w.grows.data_ptr(), None, HF, 0,
+                 st)
+        R = w.R
+        with region("neg_grad_exchange"):
+            comm.all_reduce(w.grows[:S])   # every rank's rows' part of the negatives' gradients
+            comm.all_reduce(w.gb[:S])
+            call("rg_rows_slot", w.grows.data_ptr() + 4 * S * HF, w.gb.data_ptr() + 4 * S, w.tslot.data_ptr(), B,
+                 HF, w.gsend.data_ptr(), w.gbsend.data_ptr(), st)
+            grecv, gbrecv = self._xb(w, "grecv", max(R, 1), HF), self._xb(w, "gbrecv", max(R, 1))
+            comm.all_to_all(grecv[:R], w.gsend[:B], w.recv_splits, w.send_splits)
+            comm.all_to_all(gbrecv[:R], w.gbsend[:B], w.recv_splits, w.send_splits)
+        self.tag += 1
+        with region("sampled_bwd"):
+            G, Gb, tags = self.G.data_ptr(), self.Gb.data_ptr(), self.tags.data_ptr()
+            self.scatter(w.nloc.data_ptr(), w.grows.data_ptr(), HF, w.nS.data_ptr(), S, -1, G, self.A, tags,
+                         self.tag, st)
+            self.scatter(w.nloc.data_ptr(), w.gb.data_ptr(), 1, w.nS.data_ptr(), S, -1, Gb, self.A, tags, self.tag,
+                         st, reuse_sort=True)
+            if R > 0:
+                w.nR.fill_(R)
+                self.scatter(w.local_ids.data_ptr(), grecv.data_ptr(), HF, w.nR.data_ptr(), R, -1, G, self.A, tags,
+                             self.tag, st)
+                self.scatter(w.local_ids.data_ptr(), gbrecv.data_ptr(), 1, w.nR.data_ptr(), R, -1, Gb, self.A, tags,
+                             self.tag, st, reuse_sort=True)
         with region("sampled_adam"):
             call("rg_adam_rows", self.W.p.data_ptr(), self.W.m.data_ptr(), self.W.v.data_ptr(), self.G.data_ptr(),
                  self.tags.data_ptr(), self.tag, self.A, HF, adam6, st)

@@ -12,7 +12,7 @@ import numpy as np
 import torch
 
 from . import call, stream_ptr
-from .engine import SampledSoftmaxHead, SoftmaxHead, Trunk
+from .engine import SampledSoftmaxHead, ShardedSampledHead, SoftmaxHead, Trunk
 
 
 
@@ -63,10 +63,13 @@ class HipNet:
             shard = item_shard(action_dim, comm.world, comm.rank)
         self.shard = shard
         if n_negatives:
-            if comm is not None:
-                raise NotImplementedError("sampled softmax with item sharding")
-            self.heads = OrderedDict((n, SampledSoftmaxHead(n, action_dim, self.hf, self.device, n_negatives,
-                                                            neg_seed, loss=sampled_loss)) for n in head_names)
+            if comm is not None:   # item-sharded sampled head (rows move to the data, engine.ShardedSampledHead)
+                self.heads = OrderedDict((n, ShardedSampledHead(n, action_dim, self.hf, self.device, n_negatives,
+                                                                neg_seed, sampled_loss, comm, shard))
+                                         for n in head_names)
+            else:
+                self.heads = OrderedDict((n, SampledSoftmaxHead(n, action_dim, self.hf, self.device, n_negatives,
+                                                                neg_seed, loss=sampled_loss)) for n in head_names)
             # the split logits read h as bf16 planes written by the GRU forward
             self.trunk.emit_planes = self.hf <= 128
         else:

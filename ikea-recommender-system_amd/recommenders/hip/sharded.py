@@ -111,7 +111,49 @@ def _gather_rows(comm, net, name, x):
     return comm.all_gather(out, x.contiguous())
 
 
+def sharded_sampled_step(net, clock, s, a, true_len, host=None):
+    """GRU4Rec with the item-sharded sampled head (engine.ShardedSampledHead)
+    over the global batch: each rank's trunk on its own rows (row-sharded item
+    table, id / row exchange), the head's rows moved to the data (negatives by
+    one all-reduce, targets by all-to-all), trunk gradients all-reduced.  The
+    mean CE over all world·B rows = the one-GPU sampled step on the
+    concatenated batch (same negatives) up to fp32 summation order."""
+    comm = net.comm
+    dev = net.device
+    head = next(iter(net.heads.values()))
+    routes = host_routes(comm, net.trunk, [(s, true_len)], targets=(a, head.A_full))
+    route, troute = (routes[0], routes[1]) if routes else (None, None)
+    s = s.to(dev, non_blocking=True)
+    a = a.to(dev, non_blocking=True).contiguous()
+    h = net.trunk.forward(s, true_len, slot="main", save=True, route=route)
+    B = h.shape[0]
+    Bg = comm.world * B
+    g = _f32(1.0 / Bg)
+    mask = None
+    h_in = h
+    if net.training and net.dropout_p > 0:
+        mask = net.dropout_mask(B)
+        h_in = net.apply_mask(h, mask, _buf(net, "hd", (B, net.hf)))
+    loss, _ = head.forward_loss(h_in, a, slot="main", h_planes=net.trunk.h_planes if mask is None else None,
+                                gscale=g, route=troute)
+    if host is not None:
+        host.capture(loss)
+    adam6 = clock.next_args()
+    net.trunk_tag = getattr(net, "trunk_tag", 0) + 1
+    dh = net.dh_buffer(B)
+    head.backward_step(h_in, a, dh, adam6, slot="main", gscale=g)
+    if mask is not None:
+        net.apply_mask(dh, mask, dh)
+    net.trunk.backward(dh, slot="main")
+    net.trunk.grads_for_allreduce(net.trunk_tag)
+    works = net.trunk.allreduce_start(comm)
+    net.trunk.adam_after_allreduce(adam6, works)
+    return loss
+
+
 def sharded_supervised_step(net, clock, s, a, true_len, host=None):
+    if hasattr(next(iter(net.heads.values())), "neg_job"):   # sampled head
+        return sharded_sampled_step(net, clock, s, a, true_len, host=host)
     comm = net.comm
     dev = net.device
     # the id / row exchange's splits from the host batch (no device read-back)

@@ -470,6 +470,31 @@ int rg_place_rows(const void* rows_in, int half, const int32_t* slot, const int3
 int rg_collect_grads(const float* dX0, const float* dX1, const int32_t* slot, const int32_t* lsort,
                      const int32_t* offs, int B, int E, float* gsend, rg_stream_t stream);
 
+/* ---- §8e item-sharded sampled head (csrc/sampled_shard.hip; the multi-GPU form of the
+ * build-defined sampled softmax that replaces GRU4Rec/model.py:58-60, 80 in config C3).  Rank r
+ * holds output rows [lo, hi); rows move to the data:
+ * rg_neg_pick: draw `counter` of the counter-based stream (ids[S], global) and, for the negatives
+ *   this rank owns, their rows Wg[S][HF] / biases bg[S] (zeros elsewhere; SUM all-reduce next);
+ *   nloc[x] = id − lo or -1.
+ * rg_neg_planes: fragment-order bf16 planes of Wg (rg_sampled_logits draw = 2).
+ * rg_target_ids: int32 routing ids of n int64 targets (-1 outside [0, A)), *n_out = n (for
+ *   rg_shard_route with n_rows = A).
+ * rg_head_rows_gather: owner side, W rows and biases of n received item ids from the local shard
+ *   [lo, lo + n_local) (zeros, local_ids -1 when not held).
+ * rg_rows_unslot: tW[b] = rows[slot[b]], tb[b] = rb[slot[b]] (NaN where tid32[b] < 0).
+ * rg_rows_slot: gsend[slot[b]] = grows[b], gbsend[slot[b]] = gb[b] (the targets' row gradients
+ *   back to their owners). */
+int rg_neg_pick(uint64_t seed, uint64_t counter, int64_t A, int S, int HF, int64_t lo, int64_t hi, const float* W,
+                const float* bias, int32_t* ids, int32_t* nloc, float* Wg, float* bg, rg_stream_t stream);
+int rg_neg_planes(const float* Wg, int S, int HF, void* Wp, rg_stream_t stream);
+int rg_target_ids(const int64_t* tgt, int n, int64_t A, int32_t* out, int32_t* n_out, rg_stream_t stream);
+int rg_head_rows_gather(const int32_t* ids, int n, int64_t lo, int64_t n_local, const float* W, const float* bias,
+                        int HF, float* rows, float* rb, int32_t* local_ids, rg_stream_t stream);
+int rg_rows_unslot(const float* rows, const float* rb, const int32_t* slot, const int32_t* tid32, int n, int HF,
+                   float* tW, float* tb, rg_stream_t stream);
+int rg_rows_slot(const float* grows, const float* gb, const int32_t* slot, int n, int HF, float* gsend, float* gbsend,
+                 rg_stream_t stream);
+
 /* items per online-softmax partial block of rg_head_fwd: pmax/psum/parg hold ceil(A/that) x B */
 int rg_partial_block(void);
 int rg_abi_version(void);

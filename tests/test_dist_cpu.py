@@ -152,3 +152,21 @@ def test_owner_counts_match_token_rules():
                     o = next(r for r in range(W) if item_shard(N1, W, r)[0] <= i < item_shard(N1, W, r)[1])
                 exp[o] += 1
         np.testing.assert_array_equal(owner_counts(s, lens, L, packed, N1, W), exp)
+
+
+def test_target_owner_counts_match_item_shard():
+    """dist.target_owner_counts (host routing of the sharded sampled head's
+    target rows) = owners by item_shard ranges, invalid targets to rank 0."""
+    import numpy as np
+    sys.path.insert(0, os.path.join(REPO, "ikea-recommender-system_amd"))
+    from recommenders.hip.dist import item_shard, target_owner_counts
+    rng = np.random.default_rng(4)
+    for A, W in ((9001, 3), (1_000_000, 8), (37, 2)):
+        a = rng.integers(-3, A + 3, size=500)
+        exp = np.zeros(W, dtype=np.int64)
+        for t in a:
+            o = 0
+            if 0 <= t < A:
+                o = next(r for r in range(W) if item_shard(A, W, r)[0] <= t < item_shard(A, W, r)[1])
+            exp[o] += 1
+        np.testing.assert_array_equal(target_owner_counts(a, A, W), exp)
