@@ -678,7 +678,8 @@ def main():
                     # HBM bytes of the two kernels per step from the PMC passes (tools/pmc_ns.sh)
                     pmc = os.path.join(HERE, "profiles", "pmc_traffic.json")
                     target["traffic"] = None
-                    if os.path.exists(pmc) and (N, E, B, args.negatives) == (1_000_000, 128, 4096, 2048) and terms == 6:
+                    if (os.path.exists(pmc) and (N, E, B, args.negatives) == (1_000_000, 128, 4096, 2048) and terms == 6
+                            and not shard):   # (the PMC passes measured the one-GPU kernels)
                         t1 = json.load(open(pmc)).get("c2:gather+sampled_fwd:r04")
                         target["traffic"] = None if t1 is None else int(t1) * world   # summed over ranks like the bytes
                 del tr2

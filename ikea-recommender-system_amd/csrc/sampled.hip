@@ -445,8 +445,24 @@ __global__ __launch_bounds__(sf_thr(HF)) void k_sampled_logits(const float* __re
     id = (A > 0 && (uint64_t)(int64_t)id >= A) ? 0 : id;   // guard the gather (callers validate ids)
   }
   const float bl = PRE ? bg[s_me] : bias[id];
+#ifdef SF_KOUT
+  // k-outer form (pre-gathered planes, h planes by DMA, full 128-row tiles):
+  // every h chunk is DMA'd first, then the W planes slice by slice, and the
+  // MFMAs run slice-outer over all four chunks, so they start on slice 0 while
+  // the later slices land (the four chunk accumulators stay live); the four
+  // epilogues follow the last slice
+  constexpr bool KOUT_OK = PRE && HKP && CH % SF_THR == 0;
+#else
+  constexpr bool KOUT_OK = false;
+#endif
+  const bool kout = KOUT_OK && nch == 4;
   if constexpr (HKP) {
     dma_chunk(hsA, 0);
+    if (kout) {
+      dma_chunk(hsB, 1);
+      dma_chunk(hsC, 2);
+      dma_chunk(hsD, 3);
+    }
     __builtin_amdgcn_sched_barrier(0);   // chunk 0's DMA stays ahead of the W loads (SF_EARLY counts on it)
   } else {
     load_h(0);
@@ -463,6 +479,9 @@ __global__ __launch_bounds__(sf_thr(HF)) void k_sampled_logits(const float* __re
       a0[j] = wp[plane_idx(blk, j, 0, lane, NS)];
       a1[j] = wp[plane_idx(blk, j, 1, lane, NS)];
       a2[j] = wp[plane_idx(blk, j, 2, lane, NS)];
+#if defined(SF_EARLY) || defined(SF_KOUT)
+      __builtin_amdgcn_sched_barrier(0);   // slice order, so the MFMAs wait for their slice only
+#endif
     }
   } else {
     const float* src = W + (int64_t)id * HF + 8 * hh;
@@ -480,8 +499,18 @@ __global__ __launch_bounds__(sf_thr(HF)) void k_sampled_logits(const float* __re
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
   };
-  if constexpr (HKP) {
+  if (KOUT_OK && kout) {
     if (hh == 0) sbias[32 * w + l32] = bl;
+    // the h chunks (issued before the 3·NS W-plane loads) landed; the W planes
+    // are waited for slice by slice (the compiler's per-register waits)
+    __builtin_amdgcn_s_waitcnt(sf_wc_vm(3 * NS));
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    SFD_T(1);
+  } else if constexpr (HKP) {
+#ifndef SF_BIASLATE
+    if (hh == 0) sbias[32 * w + l32] = bl;
+#endif
     // every chunk's DMA is issued up front; one full wait + barrier (the W
     // rows are needed by chunk 0 anyway), then all MFMAs run barrier-free
     // (21.7 -> 21.4 us against a second barrier behind chunk 0; with the
@@ -489,6 +518,12 @@ __global__ __launch_bounds__(sf_thr(HF)) void k_sampled_logits(const float* __re
     if (nch > 1) dma_chunk(hsB, 1);
     if (nch > 2) dma_chunk(hsC, 2);
     if (nch > 3) dma_chunk(hsD, 3);
+#ifdef SF_BIASLATE
+    // the bias store waits for the bias load (issued first, with chunk 0's
+    // DMA retiring in order behind it): after chunks 1..3's DMA are issued,
+    // not before
+    if (hh == 0) sbias[32 * w + l32] = bl;
+#endif
 #ifdef SF_EARLY
     // wait only for chunk 0's h planes (issued before the 3·NS W-plane loads and
     // chunks 1..3's 3·NDMA DMA ops): chunk 0's MFMAs start while the W planes
@@ -526,10 +561,12 @@ __global__ __launch_bounds__(sf_thr(HF)) void k_sampled_logits(const float* __re
   };
   // chunk 0: each A slice is split right before its MFMAs
   f16v accA = {}, accB = {};
+  if (!kout) {
 #pragma unroll
-  for (int j = 0; j < NS; ++j) {
-    if constexpr (!PRE) split3x8(wr[j][0], wr[j][1], a0[j], a1[j], a2[j]);
-    accA = mfma_split<NT>(a0[j], a1[j], a2[j], hsA[boff(j)], hsA[boff(j) + 64], hsA[boff(j) + 128], accA);
+    for (int j = 0; j < NS; ++j) {
+      if constexpr (!PRE) split3x8(wr[j][0], wr[j][1], a0[j], a1[j], a2[j]);
+      accA = mfma_split<NT>(a0[j], a1[j], a2[j], hsA[boff(j)], hsA[boff(j) + 64], hsA[boff(j) + 128], accA);
+    }
   }
   // row tile 0 publishes the draw and the gathered rows (the backward's Wg / bg)
   if (!PRE && emit && nact) {
@@ -600,7 +637,29 @@ __global__ __launch_bounds__(sf_thr(HF)) void k_sampled_logits(const float* __re
       epi(acc_old, c - 1);
     }
   };
-  if constexpr (HKP) {
+  if (KOUT_OK && kout) {
+    if (nact) {
+      f16v accC = {}, accD = {};
+#pragma unroll
+      for (int j = 0; j < NS; ++j) {
+        const int o = boff(j);
+        accA = mfma_split<NT>(a0[j], a1[j], a2[j], hsA[o], hsA[o + 64], hsA[o + 128], accA);
+        accB = mfma_split<NT>(a0[j], a1[j], a2[j], hsB[o], hsB[o + 64], hsB[o + 128], accB);
+        accC = mfma_split<NT>(a0[j], a1[j], a2[j], hsC[o], hsC[o + 64], hsC[o + 128], accC);
+        accD = mfma_split<NT>(a0[j], a1[j], a2[j], hsD[o], hsD[o + 64], hsD[o + 128], accD);
+        __builtin_amdgcn_sched_barrier(0);   // slice-outer: slice j's MFMAs before slice j + 1's wait
+      }
+      SFD_T(2);
+      epi(accA, 0);
+      SFD_T(3);
+      epi(accB, 1);
+      SFD_T(4);
+      epi(accC, 2);
+      epi(accD, 3);
+      SFD_T(5);
+      SFD_C(7);
+    }
+  } else if constexpr (HKP) {
     // chunks 1..3 landed at the first barrier (SF_EARLY: at this one)
 #ifdef SF_EARLY
     if (PRE && CH % SF_THR == 0 && nch == 4) {

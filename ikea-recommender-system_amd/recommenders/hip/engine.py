@@ -718,6 +718,15 @@ class SoftmaxHead:
 
     _wgen = 0   # (class default: heads built with __new__, qlearn.py)
 
+    @property
+    def top_scanned(self):
+        """Device int32 count of rows whose top-k / exact-argmax candidates
+        overflowed the cap and were scanned whole (exact either way)."""
+        t = self.__dict__.get("_top_scanned")
+        if t is None:
+            t = self.__dict__["_top_scanned"] = torch.zeros(1, dtype=torch.int32, device=self.device)
+        return t
+
     def __init__(self, name, A, HF, device, shard=None):
         w, b = init_linear(HF, A)
         self.lo, self.hi = (0, A) if shard is None else shard
@@ -740,9 +749,6 @@ class SoftmaxHead:
         self.top_k = 0
         # stored-logit top-k (rg_topk, K > 32 only) candidate overflow flag
         self.top_err = torch.zeros(1, dtype=torch.int32, device=device)
-        # rows whose fused top-k / exact argmax candidates overflowed the cap and
-        # were scanned whole instead (exact either way; diagnostic count)
-        self.top_scanned = torch.zeros(1, dtype=torch.int32, device=device)
 
     # W / b (and their Adam moments) are only reachable through these
     # properties, which first order the current stream after an overlapped

@@ -26,6 +26,19 @@ names = ["prologue", "S MFMA issue", "dZ VALU+split", "W MFMA issue", "barrier w
 acc = b[:, :, 2:].astype(np.float64)[live]
 tot = acc.sum(1)
 print(f"waves {live.sum()}  wave cycles median {np.median(tot):.4e}")
+out = os.environ.get("FL2_OUT")
+if out:
+    np.save(out, b)
+# per wave index: barrier share and S-issue share; which wave is each workgroup's slowest (least barrier wait)
+accw = b[:, :, 2:].astype(np.float64)
+totw = accw.sum(2)
+full = live.all(1)
+bw = accw[full][:, :, 4] / totw[full]
+sw = accw[full][:, :, 1] / totw[full]
+print("  by wave: barrier share median " + " ".join(f"{np.median(bw[:, i]):.3f}" for i in range(8)))
+print("  by wave: S-issue share median " + " ".join(f"{np.median(sw[:, i]):.3f}" for i in range(8)))
+slow = np.argmin(bw, axis=1)
+print("  slowest wave of the workgroup (count by index): " + " ".join(str(int((slow == i).sum())) for i in range(8)))
 for k, n in enumerate(names):
     fr = acc[:, k] / tot
     print(f"  {n:14s} median {np.median(fr):.3f}  p10 {np.percentile(fr, 10):.3f}  p90 {np.percentile(fr, 90):.3f}"
