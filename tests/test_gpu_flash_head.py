@@ -631,8 +631,9 @@ def test_fused_topk_overflow_scans_row(K):
     # the flooded row: the winner, then the exactly tied copies in index order
     np.testing.assert_array_equal(got[row], [win] + list(range(0, 16 * (K - 1), 16)))
     # every other row: canonical up to swaps of items within fp32 rounding
+    # (the tied copies sit in every row's list, so such swaps are frequent)
     flips, gap = om.topk_flip_report(Z, got, ref, 2e-5)
-    assert flips <= max(1, B // 50), (flips, gap)
+    assert gap <= 2e-5, (flips, gap)
 
 
 def test_stored_logit_topk_overflow_scans_row():
