@@ -379,7 +379,9 @@ def target_step(kern, T, B, S, E, HF, n_gather, terms):
     return out
 
 
-def head_roofline(kern, precision, B, N, E):
+def head_roofline(kern, precision, B, N, E, zs=False):
+    """zs: the stored-logit head (pass 1 stores z, pass 2 reads it and runs
+    the dW contraction only: half of PASS_PRODUCTS' pass-2 products)."""
     flops_head = 2.0 * B * N * E  # one (B × E)·(E × A) contraction
     terms = LOGIT_TERMS.get(precision, 0)
     heads = {k: kern[k] for k in ("head_fwd", "head_dh", "head_dw_adam") if k in kern}
@@ -396,16 +398,18 @@ def head_roofline(kern, precision, B, N, E):
         traffic = json.load(open(pmc)).get(f"c5:{dom}:{precision}")
     if terms:
         # fused split-bf16 head (csrc/head_flash.hip): pass 1 (head_fwd: Z and the softmax half of
-        # dh) and pass 2 (head_dw_adam: Z recomputed, dW) each run two contractions, every fp32
-        # product as exact bf16 plane products on v_mfma_f32_32x32x16_bf16 (PASS_PRODUCTS per pass)
-        ex = PASS_PRODUCTS[precision].get(dom, 0) * flops_head
+        # dh) and pass 2 (head_dw_adam: Z recomputed — or read back when stored — and dW), every fp32
+        # product as exact bf16 plane products on v_mfma_f32_16x16x32_bf16 (PASS_PRODUCTS per pass)
+        nprod = PASS_PRODUCTS[precision].get(dom, 0) // (2 if zs and dom == "head_dw_adam" else 1)
+        ex = nprod * flops_head
         alg = {"head_fwd": 2, "head_dw_adam": 1}.get(dom, 0) * flops_head
         ach = ex / t / 1e12
         out = {"bound": "mfma", "kernel": dom, "achieved": round(ach, 2), "peak": BF16_MFMA_PEAK_TFLOPS,
                "unit": "TFLOP/s", "frac": round(ach / BF16_MFMA_PEAK_TFLOPS, 4), "traffic": traffic,
                "flops_per_launch": ex,
                "mfma": f"bf16 MFMA, fp32 operands split exactly into 3 bf16 planes, "
-                       f"{PASS_PRODUCTS[precision].get(dom, 0)} plane products per fp32 product of the pass",
+                       f"{nprod} plane products per fp32 product of the pass",
+               "stored_logits": bool(zs),
                "algorithmic_fp32_TFLOPs": round(alg / t / 1e12, 2)}
         if dom == "head_dw_adam":
             out["note"] = ("pass 2 runs on a side stream beside the trunk backward (and, in the SMORL step, the "
@@ -632,7 +636,7 @@ def main():
         if kern:
             sup = net.heads["output"] if net is not None else tr.SMORL_1.sup_head_output
             prec = args.precision if sup.flash_terms(B * world) else "f32"
-            roof = head_roofline(kern, prec, B * world, N // world, E)
+            roof = head_roofline(kern, prec, B * world, N // world, E, zs=sup.stored_logits())
         if args.config == "c2":
             if world == 1 and not args.no_cpu_baseline and not args.no_eval and net is not None:
                 parity_net = net

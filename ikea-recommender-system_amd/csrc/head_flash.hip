@@ -167,7 +167,7 @@ __global__ __launch_bounds__(64 * fl_nw(HF, 1)) void k_flash_fwd(
     const bf16x8* __restrict__ Hk, const bf16x8* __restrict__ Wk, const bf16x8* __restrict__ Wr,
     const float* __restrict__ bias_pad, int B, int A, int nrb, int nsplit, int cps, float* __restrict__ pm,
     float* __restrict__ pl, float* __restrict__ pO, float* __restrict__ pbest, int32_t* __restrict__ parg,
-    float* __restrict__ cmax) {
+    float* __restrict__ cmax, float* __restrict__ zs) {
   constexpr int NW = fl_nw(HF, 1);
   constexpr bool DR = HF <= 128;      // double-buffered R-planes
   constexpr int NS = HF / 32, NF = HF / 16;
@@ -193,6 +193,14 @@ __global__ __launch_bounds__(64 * fl_nw(HF, 1)) void k_flash_fwd(
   const bool active = r0 < B;
   const int nct = (A + 31) / 32;
   const int c0 = split * cps;
+  // stored logits z = S + b (zs != NULL; pass 2 reads them instead of
+  // recomputing S): one 1024-float tile per (32-item chunk, 32-row block),
+  // chunk-major; inside, the 16×16 quadrant (ib, rb), then this kernel's
+  // accumulator order, lane-linear: each lane stores its four logits of a
+  // quadrant as one 16-B store (whole 1 KB per instruction; pass 2 transposes
+  // through LDS).  (HF <= 128: at HF 256 the wave's registers are full,
+  // rg_flash_fwd_top refuses zs)
+  float* __restrict__ zrow = (HF <= 128 && NG > 0 && zs) ? zs + (int64_t)(r0 >> 5) * 1024 + 4 * lane : nullptr;
   const int nch = max(0, min(nct, c0 + cps) - c0);
 #define FL_ISSUE_K(C, SK, SB)                                                  \
   do {                                                                         \
@@ -263,6 +271,9 @@ __global__ __launch_bounds__(64 * fl_nw(HF, 1)) void k_flash_fwd(
 #pragma unroll
       for (int ib = 0; ib < 2; ++ib) {
         const f4 bq = *reinterpret_cast<const f4*>(&sb[16 * ib + 4 * kg]);
+        if (HF <= 128 && NG > 0 && zrow)
+          __builtin_nontemporal_store(sa[ib][rb] + bq, reinterpret_cast<f4*>(zrow + (int64_t)(c0 + c) * (B / 32) * 1024 +
+                                                                            (2 * ib + rb) * 256));
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
           const float z = sa[ib][rb][u] + bq[u];
@@ -658,13 +669,24 @@ extern "C" int rg_fl2_stamp_read(void* dst, int64_t n) {
 // phases: 0 prologue, 1 S-part MFMA issue, 2 dZ VALU + split, 3 W-part MFMA
 // issue, 4 barrier wait, 5 epilogue (db / Adam / planes, or the tail partials)
 
-template <int HF, int NT>
+// s_waitcnt immediate: vmcnt <= n (6 bits, split), expcnt free, lgkmcnt 0
+constexpr int sf2_wc_vm(int n) { return (n & 15) | ((n >> 4) << 14) | 0x70; }
+
+// ZL: the logits z = S + b come from pass 1's store (zs, k_flash_fwd) instead
+// of the S-part: no K-planes of h or W are read, the chunk is dZ VALU + the
+// W-part only, and h's R-planes run through a two-slot ring in the (then idle)
+// K-plane arrays at every HF.  Each wave's z tile (16 floats per lane, pass
+// 1's lane order) is loaded into registers two chunks ahead — the chunk
+// barriers wait for the ring's DMA only (vmcnt), not for the newest z loads —
+// and turned into this kernel's accumulator order through 1 KB of LDS per wave
+// (a 16×16 transpose per quadrant: four conflict-free 4-B writes, one 16-B read).
+template <int HF, int NT, bool ZL>
 __global__ __launch_bounds__(64 * fl_nw(HF, 2)) void k_flash_dw(
     const bf16x8* __restrict__ Hk0, const bf16x8* __restrict__ Hr0, const bf16x8* Wk, const float* bias_pad,
     const float2* __restrict__ rowinfo0, float g, int B, int A, float* __restrict__ W, float* __restrict__ mW,
     float* __restrict__ vW, float* __restrict__ bias, float* __restrict__ mb, float* __restrict__ vb, AdamArgs args,
     float* __restrict__ dW_out, float* __restrict__ db_out, bf16x8* Wk_out, bf16x8* Wr_out, float* bias_pad_out,
-    int nfull, int tsplit, float* __restrict__ tail_dw, float* __restrict__ tail_db) {
+    int nfull, int tsplit, float* __restrict__ tail_dw, float* __restrict__ tail_db, const float* __restrict__ zs) {
   constexpr int NW = fl_nw(HF, 2);
   constexpr bool DR = HF <= 128;
   constexpr int NS = HF / 32, NF = HF / 16;
@@ -673,6 +695,9 @@ __global__ __launch_bounds__(64 * fl_nw(HF, 2)) void k_flash_dw(
   __shared__ bf16x8 sk0[EK], sk1[EK];
   __shared__ bf16x8 sr0[ER], sr1[DR ? ER : 1];
   __shared__ __attribute__((aligned(16))) float2 si0[32], si1[32];
+  // ZL: per-wave 1 KB for the z tile transposes (its own array, so the
+  // compiler's LDS-DMA tracking sees it never aliases the ring)
+  __shared__ __attribute__((aligned(16))) float ztr_s[ZL ? 256 * NW : 1];
 #if defined(FL2_RING3) || defined(FL2_LATE)
   // third ring slot (HF <= 128: 3 × 48 KB): chunk c + 2 is prefetched while c
   // computes, and a chunk's barrier waits only for its own DMA (vmcnt), not
@@ -700,8 +725,18 @@ __global__ __launch_bounds__(64 * fl_nw(HF, 2)) void k_flash_dw(
     if (w == 0 && lane < 16) blds16(rsrc_of(rowinfo + 32 * (C)), SI, lane16, 0); \
   } while (0)
 #define FL_ISSUE_R(C, SR) stage<ER, NW>(Hr + (int64_t)(C) * ER, SR, w, lane16)
-  FL_ISSUE_K(0, sk0, si0);
-  FL_ISSUE_R(0, sr0);
+  // ZL: chunk C's R-planes into ring slot SR (a K-plane array: EK == ER) and its row records
+#define FL_ISSUE_Z(C, SR, SI)                                                  \
+  do {                                                                         \
+    stage<ER, NW>(Hr + (int64_t)(C) * ER, SR, w, lane16);                      \
+    if (w == 0 && lane < 16) blds16(rsrc_of(rowinfo + 32 * (C)), SI, lane16, 0); \
+  } while (0)
+  if constexpr (ZL) {
+    FL_ISSUE_Z(0, sk0, si0);
+  } else {
+    FL_ISSUE_K(0, sk0, si0);
+    FL_ISSUE_R(0, sr0);
+  }
   // this wave's 32 items of W as two 16-item B operands of S = h_c·Wᵀ
   bf16x8 wk[NS][2][3];
   float bj[2];
@@ -711,8 +746,9 @@ __global__ __launch_bounds__(64 * fl_nw(HF, 2)) void k_flash_dw(
     for (int s = 0; s < NS; ++s)
 #pragma unroll
       for (int p = 0; p < 3; ++p)
-        wk[s][ib][p] = active ? Wk[(((int64_t)(j0 >> 5) * NS + s) * 2 + ib) * 192 + p * 64 + lane] : bf16x8{};
-    bj[ib] = active ? bias_pad[j0 + 16 * ib + l16] : NEG_INF;
+        wk[s][ib][p] = (active && !ZL) ? Wk[(((int64_t)(j0 >> 5) * NS + s) * 2 + ib) * 192 + p * 64 + lane]
+                                       : bf16x8{};
+    bj[ib] = ZL ? 0.f : active ? bias_pad[j0 + 16 * ib + l16] : NEG_INF;
   }
   // dW tiles (item block ib, feature block fb): lane (kg, n) holds items
   // 16ib + 4kg + i, feature 16fb + n; db per item block: this lane's item 16ib + l16
@@ -722,10 +758,61 @@ __global__ __launch_bounds__(64 * fl_nw(HF, 2)) void k_flash_dw(
   for (int ib = 0; ib < 2; ++ib)
 #pragma unroll
     for (int fb = 0; fb < NF; ++fb) dw[ib][fb] = f4{0.f, 0.f, 0.f, 0.f};
+  // ZL: this wave's z tiles (item block j0 / 32, row chunks from cb), 16 B
+  // per lane and quadrant, as pass 1 stored them
+  // (branch-free: a wave past A reads item block 0's tiles, a chunk index past
+  // the range re-reads the last chunk — neither result is used — so the
+  // compiler's wait counting sees the same four loads on every path)
+  const float* __restrict__ zt =
+      ZL ? zs + ((int64_t)(active ? j0 >> 5 : 0) * (B / 32) + cb) * 1024 + 4 * lane : nullptr;
+  auto zload = [&](int c, f4 (&d)[2][2]) __attribute__((always_inline)) {
+    const int cc = min(c, nch - 1);
+#pragma unroll
+    for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+      for (int ib = 0; ib < 2; ++ib)
+        d[rb][ib] =
+            __builtin_nontemporal_load(reinterpret_cast<const f4*>(zt + (int64_t)cc * 1024 + (2 * ib + rb) * 256));
+  };
+  f4 za[2][2], zb[2][2], zc[2][2];
+  if constexpr (ZL) {
+    if (nch > 0) {
+      zload(0, za);
+      zload(1, zb);
+    }
+  }
   __syncthreads();
   FL2_MARK(0);
-  // S = h_c·Wᵀ recomputed, dZ = g·(2^(S−lse) − onehot), db; dZᵀ planes
-  // (q*[ib]: the A operand of dW, k over the chunk's rows in kperm16 order)
+  // dZ = g·(2^((S + b)·log2e − lse·log2e) − onehot) from the chunk's S tiles
+  // (ZL: z = S + b, bj = 0), db; dZᵀ planes (q*[ib]: the A operand of dW, k
+  // over the chunk's rows in kperm16 order)
+  auto dzpart = [&](f4 (&sa)[2][2], const float2* si, bf16x8 (&q0)[2], bf16x8 (&q1)[2], bf16x8 (&q2)[2])
+                    __attribute__((always_inline)) {
+#pragma unroll
+    for (int ib = 0; ib < 2; ++ib) {
+      const int item = j0 + 16 * ib + l16;
+      float cdb = 0.f;
+#pragma unroll
+      for (int rb = 0; rb < 2; ++rb) {
+        const f4 i0 = *reinterpret_cast<const f4*>(&si[16 * rb + 4 * kg]);
+        const f4 i1 = *reinterpret_cast<const f4*>(&si[16 * rb + 4 * kg + 2]);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const float lse2 = u < 2 ? i0[2 * u] : i1[2 * (u - 2)];
+          const int tb = __float_as_int(u < 2 ? i0[2 * u + 1] : i1[2 * (u - 2) + 1]);
+          const float zz = ZL ? sa[rb][ib][u] : sa[rb][ib][u] + bj[ib];
+          const float e = __builtin_amdgcn_exp2f(fmaf(zz, L2E, -lse2));
+          const float p = g * (e - (tb == item ? 1.f : 0.f));
+          sa[rb][ib][u] = p;
+          cdb += p;
+        }
+      }
+      dbs[ib] += cdb;
+      split3x8(sa[0][ib], sa[1][ib], q0[ib], q1[ib], q2[ib]);
+    }
+    FL2_MARK(2);
+  };
+  // S = h_c·Wᵀ recomputed, then dzpart
   auto spart = [&](const bf16x8* sk, const float2* si, bf16x8 (&q0)[2], bf16x8 (&q1)[2], bf16x8 (&q2)[2])
                    __attribute__((always_inline)) {
     f4 sa[2][2];   // [rb][ib]: lane (kg, n) holds rows 16rb + 4kg + u, item 16ib + n
@@ -748,28 +835,7 @@ __global__ __launch_bounds__(64 * fl_nw(HF, 2)) void k_flash_dw(
       __builtin_amdgcn_sched_barrier(0);
     }
     FL2_MARK(1);
-#pragma unroll
-    for (int ib = 0; ib < 2; ++ib) {
-      const int item = j0 + 16 * ib + l16;
-      float cdb = 0.f;
-#pragma unroll
-      for (int rb = 0; rb < 2; ++rb) {
-        const f4 i0 = *reinterpret_cast<const f4*>(&si[16 * rb + 4 * kg]);
-        const f4 i1 = *reinterpret_cast<const f4*>(&si[16 * rb + 4 * kg + 2]);
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const float lse2 = u < 2 ? i0[2 * u] : i1[2 * (u - 2)];
-          const int tb = __float_as_int(u < 2 ? i0[2 * u + 1] : i1[2 * (u - 2) + 1]);
-          const float e = __builtin_amdgcn_exp2f(fmaf(sa[rb][ib][u] + bj[ib], L2E, -lse2));
-          const float p = g * (e - (tb == item ? 1.f : 0.f));
-          sa[rb][ib][u] = p;
-          cdb += p;
-        }
-      }
-      dbs[ib] += cdb;
-      split3x8(sa[0][ib], sa[1][ib], q0[ib], q1[ib], q2[ib]);
-    }
-    FL2_MARK(2);
+    dzpart(sa, si, q0, q1, q2);
   };
   // dW += dZᵀ·h_c, one R-plane fragment of h per feature block
   auto wpart = [&](const bf16x8* sr, const bf16x8 (&q0)[2], const bf16x8 (&q1)[2], const bf16x8 (&q2)[2])
@@ -891,6 +957,54 @@ __global__ __launch_bounds__(64 * fl_nw(HF, 2)) void k_flash_dw(
     wpart(SR, q0_, q1_, q2_);      \
   } while (0)
 #endif
+  if constexpr (ZL) {
+    // pass 1's quadrant (item 4kg + u, row l16) -> (rows 4kg + r, item l16):
+    // value u of lane (kg, l16) at u·64 + kg·16 + l16 (each write instruction
+    // covers 64 distinct banks), read back as 16 B at (l16 & 3)·64 + (l16 >> 2)·16 + 4kg
+    float* ztr = ztr_s + 256 * w;
+    auto ztrans = [&](f4 (&d)[2][2]) __attribute__((always_inline)) {
+#pragma unroll
+      for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+        for (int ib = 0; ib < 2; ++ib) {
+#pragma unroll
+          for (int u = 0; u < 4; ++u) ztr[u * 64 + kg * 16 + l16] = d[rb][ib][u];
+          d[rb][ib] = *reinterpret_cast<const f4*>(ztr + (l16 & 3) * 64 + (l16 >> 2) * 16 + 4 * kg);
+        }
+    };
+    // step c: issue chunk c + 1's ring DMA, then z(c + 2) into the buffer chunk
+    // c − 1 used; compute c; barrier once chunk c + 1's DMA (and z(c + 1),
+    // issued a step earlier) landed — only z(c + 2)'s four loads may be in flight.
+    // Branch-free (a wave past A computes on item block 0's tiles and never
+    // stores; past the last chunk the DMA / loads repeat the last chunk into
+    // idle buffers), and slots / buffers are static per call site — unrolled by
+    // 6 — so the compiler's LDS-DMA tracking only orders reads of a slot behind
+    // its own DMA and its wait counting matches the explicit vmcnt(4)
+    auto step = [&](int c, f4 (&zcur)[2][2], f4 (&zn2)[2][2], const bf16x8* skc, const float2* sic, bf16x8* skn,
+                    float2* sin) __attribute__((always_inline)) {
+      ztrans(zcur);   // first: no DMA is in flight yet, so its LDS writes wait for nothing
+      __builtin_amdgcn_sched_barrier(0);
+      FL_ISSUE_Z(min(c + 1, nch - 1), skn, sin);
+      zload(c + 2, zn2);
+      __builtin_amdgcn_sched_barrier(0);
+      bf16x8 q0[2], q1[2], q2[2];
+      dzpart(zcur, sic, q0, q1, q2);
+      wpart(skc, q0, q1, q2);
+      FL2_MARK(3);
+      __builtin_amdgcn_s_waitcnt(sf2_wc_vm(4));
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+      FL2_MARK(4);
+    };
+    for (int c = 0; c < nch; c += 6) {
+      step(c, za, zc, sk0, si0, sk1, si1);
+      if (c + 1 < nch) step(c + 1, zb, za, sk1, si1, sk0, si0);
+      if (c + 2 < nch) step(c + 2, zc, zb, sk0, si0, sk1, si1);
+      if (c + 3 < nch) step(c + 3, za, zc, sk1, si1, sk0, si0);
+      if (c + 4 < nch) step(c + 4, zb, za, sk0, si0, sk1, si1);
+      if (c + 5 < nch) step(c + 5, zc, zb, sk1, si1, sk0, si0);
+    }
+  } else
 #ifdef FL2_LATE
   if constexpr (HF == 128) {
     // Waves 4-7 (each shares a SIMD with one of waves 0-3) run every chunk's
@@ -1012,6 +1126,7 @@ __global__ __launch_bounds__(64 * fl_nw(HF, 2)) void k_flash_dw(
   }
 #undef FL_ISSUE_K
 #undef FL_ISSUE_R
+#undef FL_ISSUE_Z
   // Epilogue, 32 feature columns (two feature blocks) at a time through a
   // per-wave LDS tile (32 items × 32 columns, rows padded to 36 floats): the
   // raw dW tile goes in, every lane then takes four (item, 4-column) pieces —
@@ -1560,15 +1675,21 @@ extern "C" int rg_head_planes(const float* X, int rows, int HF, void* planes_k, 
 
 extern "C" int rg_flash_rows_per_block(int HF) { return flash_hf_ok(HF) ? fl_rows(HF, 1) : RG_ERR_SHAPE; }
 
+extern "C" int64_t rg_flash_zs_bytes(int B, int A) {
+  if (B <= 0 || A <= 0 || (B % 32)) return RG_ERR_ARG;
+  return (int64_t)((A + 31) / 32) * 32 * B * 4;
+}
+
 extern "C" int rg_flash_fwd_top(const void* Hk, const void* Wk, const void* Wr, const float* bias_pad, int B, int A,
                                 int HF, int terms, int nsplit, float* pm, float* pl, float* pO, float* pbest,
-                                int32_t* parg, float* cmax, hipStream_t stream) {
+                                int32_t* parg, float* cmax, float* zs, hipStream_t stream) {
   if (B <= 0 || A <= 0 || (B % 32) || nsplit <= 0 || !Hk || !Wk || !Wr || !bias_pad || !pm || !pl || !pO)
     return RG_ERR_ARG;
   if (!flash_terms_ok(terms)) return RG_ERR_ARG;
   if (!flash_hf_ok(HF)) return RG_ERR_SHAPE;
   const bool arg = pbest != nullptr;
   if (arg != (parg != nullptr) || (cmax && !arg)) return RG_ERR_ARG;
+  if (zs && HF > 128) return RG_ERR_SHAPE;
   const int nct = (A + 31) / 32;
   const int cps = (nct + nsplit - 1) / nsplit;
   const int rpb = fl_rows(HF, 1);
@@ -1577,7 +1698,7 @@ extern "C" int rg_flash_fwd_top(const void* Hk, const void* Wk, const void* Wr, 
 #define FF(HFV, NTV, NGV, ARGV)                                                                              \
   hipLaunchKernelGGL((k_flash_fwd<HFV, NTV, NGV, ARGV>), grid, dim3(64 * fl_nw(HFV, 1)), 0, stream,                \
                      (const bf16x8*)Hk, (const bf16x8*)Wk, (const bf16x8*)Wr, bias_pad, B, A, nrb, nsplit, cps, pm, \
-                     pl, pO, pbest, parg, cmax)
+                     pl, pO, pbest, parg, cmax, zs)
 #define FA(HFV, NTV, NGV)     \
   if (arg) {                  \
     FF(HFV, NTV, NGV, true);  \
@@ -1608,7 +1729,7 @@ extern "C" int rg_flash_fwd_top(const void* Hk, const void* Wk, const void* Wr, 
 extern "C" int rg_flash_fwd(const void* Hk, const void* Wk, const void* Wr, const float* bias_pad, int B, int A,
                             int HF, int terms, int nsplit, float* pm, float* pl, float* pO, hipStream_t stream) {
   return rg_flash_fwd_top(Hk, Wk, Wr, bias_pad, B, A, HF, terms, nsplit, pm, pl, pO, nullptr, nullptr, nullptr,
-                          stream);
+                          nullptr, stream);
 }
 
 // Evaluation scoring (no O contraction): pass 1's S-part over the fp32
@@ -1632,7 +1753,7 @@ extern "C" int rg_flash_score(const void* Hk, const void* Wk, const float* bias_
 #define FSC(HFV, NTV)                                                                                             \
   hipLaunchKernelGGL((k_flash_fwd<HFV, NTV, 0, true>), grid, dim3(64 * fl_nw(HFV, 1)), 0, stream, (const bf16x8*)Hk, \
                      (const bf16x8*)Wk, (const bf16x8*)nullptr, bias_pad, B, A, nrb, nsplit, cps, pm, pl,         \
-                     (float*)nullptr, pbest, parg, cmax)
+                     (float*)nullptr, pbest, parg, cmax, (float*)nullptr)
 #define FT(HFV)          \
   if (terms == 9) {      \
     FSC(HFV, 9);         \
@@ -1790,12 +1911,13 @@ extern "C" int rg_flash_dw_adam_planes(const void* Hk, const void* Hr, const voi
                                        const void* rowinfo, float gscale, int B, int A, int HF, int terms, float* W,
                                        float* mW, float* vW, float* bias, float* mb, float* vb, const float* adam6,
                                        float* dW_out, float* db_out, void* Wk_out, void* Wr_out, float* bias_pad_out,
-                                       void* work, int64_t work_bytes, hipStream_t stream) {
+                                       void* work, int64_t work_bytes, const float* zs, hipStream_t stream) {
   if (B <= 0 || A <= 0 || (B % 32) || !Hk || !Hr || !Wk || !bias_pad || !rowinfo) return RG_ERR_ARG;
   if (!flash_terms_ok(terms)) return RG_ERR_ARG;
   if (!flash_hf_ok(HF)) return RG_ERR_SHAPE;
   if (dW_out ? !db_out : (!adam6 || !W || !mW || !vW || !bias || !mb || !vb)) return RG_ERR_ARG;
   if ((Wk_out != nullptr) != (Wr_out != nullptr) || (Wk_out && (dW_out || !bias_pad_out))) return RG_ERR_ARG;
+  if (zs && HF > 128) return RG_ERR_SHAPE;
   AdamArgs a{};
   if (adam6) a = AdamArgs{adam6[0], adam6[1], adam6[2], adam6[3], adam6[4], adam6[5]};
   const int rpb = fl_rows(HF, 2);
@@ -1805,16 +1927,22 @@ extern "C" int rg_flash_dw_adam_planes(const void* Hk, const void* Hr, const voi
   float* tail_db = tl.ntail ? tail_dw + (int64_t)tl.tsplit * tl.ntail * HF : nullptr;
   const int nblk = (A + rpb - 1) / rpb;
   const dim3 grid((unsigned)(tl.nfull + (nblk - tl.nfull) * tl.tsplit));
-#define FW(HFV, NTV)                                                                                          \
-  hipLaunchKernelGGL((k_flash_dw<HFV, NTV>), grid, dim3(64 * fl_nw(HFV, 2)), 0, stream, (const bf16x8*)Hk, (const bf16x8*)Hr, \
-                     (const bf16x8*)Wk, bias_pad, (const float2*)rowinfo, gscale, B, A, W, mW, vW, bias, mb, vb, \
-                     a, dW_out, db_out, (bf16x8*)Wk_out, (bf16x8*)Wr_out, bias_pad_out, tl.nfull, tl.tsplit, tail_dw, \
-                     tail_db)
+#define FW(HFV, NTV, ZLV)                                                                                     \
+  hipLaunchKernelGGL((k_flash_dw<HFV, NTV, ZLV>), grid, dim3(64 * fl_nw(HFV, 2)), 0, stream, (const bf16x8*)Hk, \
+                     (const bf16x8*)Hr, (const bf16x8*)Wk, bias_pad, (const float2*)rowinfo, gscale, B, A, W, mW, vW, \
+                     bias, mb, vb, a, dW_out, db_out, (bf16x8*)Wk_out, (bf16x8*)Wr_out, bias_pad_out, tl.nfull,    \
+                     tl.tsplit, tail_dw, tail_db, zs)
+#define FZ(HFV, NTV)               \
+  if (HFV <= 128 && zs) {          \
+    FW(HFV, NTV, (HFV <= 128));    \
+  } else {                         \
+    FW(HFV, NTV, false);           \
+  }
 #define FT(HFV)          \
   if (terms == 9) {      \
-    FW(HFV, 9);          \
+    FZ(HFV, 9);          \
   } else {               \
-    FW(HFV, 6);          \
+    FZ(HFV, 6);          \
   }
   switch (HF) {
     case 32: FT(32); break;
@@ -1823,6 +1951,7 @@ extern "C" int rg_flash_dw_adam_planes(const void* Hk, const void* Hr, const voi
     case 256: FT(256); break;
   }
 #undef FT
+#undef FZ
 #undef FW
   if (tl.ntail) {
     const int i0 = tl.nfull * rpb;
@@ -1865,7 +1994,7 @@ extern "C" int rg_flash_dw_adam(const void* Hk, const void* Hr, const void* Wk, 
                                 float* mW, float* vW, float* bias, float* mb, float* vb, const float* adam6,
                                 float* dW_out, float* db_out, hipStream_t stream) {
   return rg_flash_dw_adam_planes(Hk, Hr, Wk, bias_pad, rowinfo, gscale, B, A, HF, terms, W, mW, vW, bias, mb, vb, adam6,
-                                 dW_out, db_out, nullptr, nullptr, nullptr, nullptr, 0, stream);
+                                 dW_out, db_out, nullptr, nullptr, nullptr, nullptr, 0, nullptr, stream);
 }
 
 // Exact argmax through screening (the double-Q target of SQN / SMORL at the

@@ -71,12 +71,50 @@ __global__ void k_adam_rows4(float* __restrict__ P, float* __restrict__ M, float
   }
 }
 
+typedef int32_t i4 __attribute__((ext_vector_type(4)));
+
+// One-column tables (the heads' biases): four rows per thread, tags read
+// as int4, so the sweep streams like the wide tables; rows past the last
+// multiple of 4 go to k_adam_rows1.
+__global__ void k_adam_bias4(float* __restrict__ P, float* __restrict__ M, float* __restrict__ V,
+                             float* __restrict__ G, const int32_t* __restrict__ tags, int32_t tag, int64_t n4,
+                             AdamArgs a) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
+    const i4 t = reinterpret_cast<const i4*>(tags)[i];
+    f4 p = __builtin_nontemporal_load(reinterpret_cast<f4*>(P) + i);
+    f4 m = __builtin_nontemporal_load(reinterpret_cast<f4*>(M) + i);
+    f4 v = __builtin_nontemporal_load(reinterpret_cast<f4*>(V) + i);
+    f4 g = {0.f, 0.f, 0.f, 0.f};
+    if (t[0] == tag || t[1] == tag || t[2] == tag || t[3] == tag) {
+      const f4 gr = reinterpret_cast<f4*>(G)[i];
+      f4 gz = gr;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        g[q] = t[q] == tag ? gr[q] : 0.f;
+        gz[q] = t[q] == tag ? 0.f : gr[q];
+      }
+      reinterpret_cast<f4*>(G)[i] = gz;
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      float pq = p[q], mq = m[q], vq = v[q];
+      adam_elem(pq, mq, vq, g[q], a);
+      p[q] = pq;
+      m[q] = mq;
+      v[q] = vq;
+    }
+    __builtin_nontemporal_store(p, reinterpret_cast<f4*>(P) + i);
+    __builtin_nontemporal_store(m, reinterpret_cast<f4*>(M) + i);
+    __builtin_nontemporal_store(v, reinterpret_cast<f4*>(V) + i);
+  }
+}
+
 __global__ void k_adam_rows1(float* __restrict__ P, float* __restrict__ M, float* __restrict__ V,
                              float* __restrict__ G, const int32_t* __restrict__ tags, int32_t tag, int64_t rows,
                              int cols, AdamArgs a) {
   const int64_t n = rows * cols;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t row = i / cols;
+    const int64_t row = cols == 1 ? i : i / cols;
     float g = 0.f;
     if (tags[row] == tag) {
       g = G[i];
@@ -102,7 +140,15 @@ extern "C" int rg_adam_rows(float* P, float* M, float* V, float* G, const int32_
     hipLaunchKernelGGL(k_adam_rows4, dim3(blocks), dim3(256), 0, stream, P, M, V, G, tags, tag, rows, cols, sh,
                        to_args(adam6));
   }
-  else
+  else if (cols == 1 && rows >= 4) {
+    const int64_t n4 = rows / 4, r4 = n4 * 4;
+    int b4 = (int)((n4 + 255) / 256);
+    if (b4 > 32768) b4 = 32768;
+    hipLaunchKernelGGL(k_adam_bias4, dim3(b4), dim3(256), 0, stream, P, M, V, G, tags, tag, n4, to_args(adam6));
+    if (r4 < rows)
+      hipLaunchKernelGGL(k_adam_rows1, dim3(1), dim3(256), 0, stream, P + r4, M + r4, V + r4, G + r4, tags + r4, tag,
+                         rows - r4, 1, to_args(adam6));
+  } else
     hipLaunchKernelGGL(k_adam_rows1, dim3(blocks), dim3(256), 0, stream, P, M, V, G, tags, tag, rows, cols,
                        to_args(adam6));
   RG_LAUNCH_CHECK();

@@ -11,11 +11,6 @@ struct HeadPtrs {
   const float* W[MAXH];
   const float* b[MAXH];
 };
-struct HeadGrads {
-  float* GW[MAXH];
-  float* Gb[MAXH];
-  int32_t* tags[MAXH];
-};
 
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
@@ -58,49 +53,47 @@ extern "C" int rg_q_gather(const float* h, int HF, const float* const* W, const 
   return RG_OK;
 }
 
-// Backward of q = h·W_i[a] + b_i[a]:  dh[b] += Σ_i dq_bi W_i[a_b];
-// G_i[a_b] += dq_bi h_b; Gb_i[a_b] += dq_bi (atomics: several rows may share
-// an action), tag rows for the row-sparse Adam sweep.
-__global__ __launch_bounds__(256) void k_q_backward(const float* __restrict__ h, int HF, HeadPtrs hp,
-                                                    HeadGrads hg, int nh, const int64_t* __restrict__ idx, int B,
+// Backward of q = h·W_i[a] + b_i[a] without float atomics: dh[b] +=
+// Σ_i dq_bi W_i[a_b] (heads in order), and the per-row gradient contributions
+// rows[i][b] = dq_bi h_b, rows_b[i][b] = dq_bi with ids[b] = a_b (-1 where the
+// row's action is not held here, item-sharded heads), n_rows[0] = B.  The
+// caller sums them into G_i / Gb_i through the deterministic sorted scatter
+// (csrc/segsum.hip rg_scatter_rows, one sort shared by every head): several
+// rows of a batch share an action, and an atomic sum would depend on arrival
+// order.
+__global__ __launch_bounds__(256) void k_q_backward(const float* __restrict__ h, int HF, HeadPtrs hp, int nh,
+                                                    const int64_t* __restrict__ idx, int B,
                                                     const float* __restrict__ dq, float* __restrict__ dh,
-                                                    int32_t tag) {
+                                                    float* __restrict__ rows, float* __restrict__ rows_b,
+                                                    int32_t* __restrict__ ids, int32_t* __restrict__ n_rows) {
   const int b = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
+  if (blockIdx.x == 0 && threadIdx.x == 0) n_rows[0] = B;
   if (b >= B) return;
   const int64_t j = idx[b];
-  if (j < 0) return;  // row's action not held here (item-sharded head)
+  if (lane == 0) ids[b] = j < 0 ? -1 : (int32_t)j;
+  if (j < 0) return;  // skipped by the scatter (its rows are never read)
   for (int c = lane; c < HF; c += 64) {
     float acc = dh[(int64_t)b * HF + c];
     const float hv = h[(int64_t)b * HF + c];
     for (int i = 0; i < nh; ++i) {
       const float g = dq[(int64_t)b * nh + i];
       acc += g * hp.W[i][j * HF + c];
-      atomicAdd(&hg.GW[i][j * HF + c], g * hv);
+      rows[((int64_t)i * B + b) * HF + c] = g * hv;
     }
     dh[(int64_t)b * HF + c] = acc;
   }
-  if (lane == 0) {
-    for (int i = 0; i < nh; ++i) {
-      atomicAdd(&hg.Gb[i][j], dq[(int64_t)b * nh + i]);
-      hg.tags[i][j] = tag;
-    }
-  }
+  if (lane < nh) rows_b[(int64_t)lane * B + b] = dq[(int64_t)b * nh + lane];
 }
 
-extern "C" int rg_q_backward(const float* h, int HF, const float* const* W, float* const* GW, float* const* Gb,
-                             int32_t* const* tags, int nh, const int64_t* idx, int B, const float* dq, float* dh,
-                             int32_t tag, hipStream_t stream) {
-  if (nh <= 0 || nh > MAXH || B <= 0) return RG_ERR_ARG;
+extern "C" int rg_q_backward(const float* h, int HF, const float* const* W, int nh, const int64_t* idx, int B,
+                             const float* dq, float* dh, float* rows, float* rows_b, int32_t* ids, int32_t* n_rows,
+                             hipStream_t stream) {
+  if (nh <= 0 || nh > MAXH || B <= 0 || HF <= 0 || !rows || !rows_b || !ids || !n_rows) return RG_ERR_ARG;
   HeadPtrs hp{};
-  HeadGrads hg{};
-  for (int i = 0; i < nh; ++i) {
-    hp.W[i] = W[i];
-    hg.GW[i] = GW[i];
-    hg.Gb[i] = Gb[i];
-    hg.tags[i] = tags[i];
-  }
-  hipLaunchKernelGGL(k_q_backward, dim3((B + 3) / 4), dim3(256), 0, stream, h, HF, hp, hg, nh, idx, B, dq, dh, tag);
+  for (int i = 0; i < nh; ++i) hp.W[i] = W[i];
+  hipLaunchKernelGGL(k_q_backward, dim3((B + 3) / 4), dim3(256), 0, stream, h, HF, hp, nh, idx, B, dq, dh, rows,
+                     rows_b, ids, n_rows);
   RG_LAUNCH_CHECK();
   return RG_OK;
 }

@@ -312,7 +312,14 @@ extern "C" int rg_head_fwd_xp(const void* hplanes, const float* W, const float* 
 constexpr int sf_nw(int HF) { return HF <= 128 ? SF_NW : 4; }
 constexpr int sf_neg(int HF) { return 32 * sf_nw(HF); }   // negatives per workgroup
 constexpr int sf_thr(int HF) { return 64 * sf_nw(HF); }   // threads per workgroup
-constexpr int SF_ROWS = 128;  // rows per workgroup (4 chunks of 32)
+// rows per workgroup (chunks of 32): 128 up to HF 128; 256 at HF 256, where
+// one workgroup fills a CU — the S = 2048, B = 4096 grid (16 × 16) is then
+// one round on 256 CUs and every wave splits its negatives' planes once for
+// eight h chunks instead of twice for four
+#ifndef SF_ROWS256
+#define SF_ROWS256 256
+#endif
+constexpr int sf_rows(int HF) { return HF == 256 ? SF_ROWS256 : 128; }
 // s_waitcnt immediate: vmcnt <= n (6 bits, split), expcnt free, lgkmcnt 0
 constexpr int sf_wc_vm(int n) { return (n & 15) | ((n >> 4) << 14) | 0x70; }
 
@@ -390,8 +397,8 @@ __global__ __launch_bounds__(sf_thr(HF)) void k_sampled_logits(const float* __re
   const int s0 = tile + 32 * w;
   const bool nact = s0 < S;                 // S % 32 == 0
   const bool emit = by == 0;                // row tile 0 publishes ids, Wg, bg
-  const int rbase = by * SF_ROWS;
-  const int nch = min(SF_ROWS, B - rbase) / 32;   // B % 32 == 0
+  const int rbase = by * sf_rows(HF);
+  const int nch = min(sf_rows(HF), B - rbase) / 32;   // B % 32 == 0
   // ---- h chunk staging: item i -> (group g, row) with the row fastest
   f4 st[IPT][2];
   f4 st2[IPT][2], st3[IPT][2];   // (STAGE: chunks 2, 3)
@@ -724,14 +731,16 @@ __global__ __launch_bounds__(sf_thr(HF)) void k_sampled_logits(const float* __re
       epi(accA, 0);
     }
   } else {
-    if (nch > 1) step(1, hsB, accB, accA);
-    if (nch > 2) step(2, hsA, accA, accB);
-    if (nch > 3) step(3, hsB, accB, accA);
+    // chunk c: LDS buffer and accumulator c & 1 (A even, B odd)
+    int c = 1;
+    for (; c + 1 < nch; c += 2) {
+      step(c, hsB, accB, accA);
+      step(c + 1, hsA, accA, accB);
+    }
+    if (c < nch) step(c, hsB, accB, accA);
     if (nact) {
-      if (nch == 1) epi(accA, 0);
-      if (nch == 2) epi(accB, 1);
-      if (nch == 3) epi(accA, 2);
-      if (nch == 4) epi(accB, 3);
+      if ((nch - 1) & 1) epi(accB, nch - 1);
+      else epi(accA, nch - 1);
     }
   }
 }
@@ -752,7 +761,8 @@ extern "C" int rg_sampled_logits(const float* h, const float* W, const float* bi
   if (draw == 1 && (A <= 0 || A > INT32_MAX)) return RG_ERR_ARG;
   if (terms != 6 && terms != 9) return RG_ERR_ARG;
   const int neg_wg = sf_neg(HF);
-  const dim3 grid((unsigned)((S + neg_wg - 1) / neg_wg), (unsigned)((B + SF_ROWS - 1) / SF_ROWS));
+  const int rows_wg = sf_rows(HF);
+  const dim3 grid((unsigned)((S + neg_wg - 1) / neg_wg), (unsigned)((B + rows_wg - 1) / rows_wg));
   const bf16x8* hk = (const bf16x8*)h_planes;
   const bf16x8* wp = (const bf16x8*)w_planes;
 #define SFH(HFV, NTV, DRV, HKV, PRV)                                                                                  \

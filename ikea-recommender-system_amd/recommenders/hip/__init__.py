@@ -25,7 +25,7 @@ U64 = C.c_uint64
 # entry points returning int64_t (all others return int)
 RESTYPE_I64 = {"rg_sampled_work_bytes", "rg_head_work_bytes", "rg_head_plane_bytes", "rg_gru_wide_work_bytes",
                "rg_scatter_rows_work_bytes", "rg_flash_dw_work_bytes",
-               "rg_flash_topk_work_bytes"}
+               "rg_flash_topk_work_bytes", "rg_flash_zs_bytes"}
 
 # name -> argtypes
 SIGNATURES = {
@@ -51,7 +51,8 @@ SIGNATURES = {
     "rg_flash_rows_per_block": [I],
     "rg_remap_ids": [P, I64, P, I64, P, P, P],
     "rg_build_transitions": [P, P, P, P, P, I, I, I64, I, P, P, P, P, P, P, P, P],
-    "rg_flash_fwd_top": [P, P, P, P, I, I, I, I, I, P, P, P, P, P, P, P],
+    "rg_flash_fwd_top": [P, P, P, P, I, I, I, I, I, P, P, P, P, P, P, P, P],
+    "rg_flash_zs_bytes": [I, I],
     "rg_flash_argmax": [P, P, I, I, P, P, P],
     "rg_flash_amax_fwd": [P, P, P, I, I, I, I, I, P, P, P],
     "rg_flash_score": [P, P, P, I, I, I, I, I, P, P, P, P, P, P],
@@ -66,7 +67,7 @@ SIGNATURES = {
     "rg_flash_rows": [P, P, I64, I, I, P, P],
     "rg_flash_dh": [P, P, P, I, P, F, I, I, P, P],
     "rg_flash_dw_adam": [P, P, P, P, P, F, I, I, I, I, P, P, P, P, P, P, P, P, P, P],
-    "rg_flash_dw_adam_planes": [P, P, P, P, P, F, I, I, I, I, P, P, P, P, P, P, P, P, P, P, P, P, P, I64, P],
+    "rg_flash_dw_adam_planes": [P, P, P, P, P, F, I, I, I, I, P, P, P, P, P, P, P, P, P, P, P, P, P, I64, P, P],
     "rg_flash_dw_work_bytes": [I, I, I],
     "rg_timing_events": [P, P],
     "rg_lse_combine": [P, P, P, I, I, P, P, I64, P, I, P, P, P, P, P],
@@ -83,7 +84,7 @@ SIGNATURES = {
     "rg_adam_rows": [P, P, P, P, P, I32, I64, I, P, P],
     "rg_adam_slabs": [P, P, P, P, I, I64, P, P, P],
     "rg_q_gather": [P, I, P, P, I, P, P, I, P, P],
-    "rg_q_backward": [P, I, P, P, P, P, I, P, I, P, P, I32, P],
+    "rg_q_backward": [P, I, P, I, P, I, P, P, P, P, P, P, P],
     "rg_sqn_td": [P, P, P, P, F, I, D, P, P, P],
     "rg_smorl_td": [P, P, P, P, P, I, F, F, I, P, P, P],
     "rg_sum64": [P, I, D, P, P, P],

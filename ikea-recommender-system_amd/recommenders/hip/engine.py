@@ -563,9 +563,11 @@ class _FlashWS:
     """Workspace of the fused split-bf16 training head (csrc/head_flash.hip):
     bf16 operand planes of h and W (K- and R-layouts), the bias padded with
     -inf to whole 32-item chunks, per-(split, row) softmax partials and the
-    unnormalised dh partials O (nsplit × HF × B).  No logits are stored.
-    With top_k >= 1 pass 1 also leaves every split's (best logit, item) and,
-    for top_k > 1, every 32-item chunk's row maximum (the fused top-k)."""
+    unnormalised dh partials O (nsplit × HF × B).  zs: the logits pass 1
+    stores for pass 2 (SoftmaxHead.zs_buffer; None until decided, False when
+    they stay recomputed).  With top_k >= 1 pass 1 also leaves every split's
+    (best logit, item) and, for top_k > 1, every 32-item chunk's row maximum
+    (the fused top-k)."""
 
     def __init__(self, B, A, HF, device, top_k=0):
         u8 = lambda n: torch.empty(int(n), dtype=torch.uint8, device=device)  # noqa: E731
@@ -588,6 +590,8 @@ class _FlashWS:
         self.dw_work = u8(max(self.dw_work_bytes, 16))
         self.lse, self.zt, self.loss_row = z(B), z(B), z(B)
         self.loss = torch.zeros(1, device=device)
+        self.zs = None
+        self.zs_live = False   # zs holds the logits of the last pass 1 on this workspace
         self.pbest = self.parg = self.cmax = self.cand = self.ncand = None
         if top_k >= 1:
             self.pbest, self.parg = z(self.nsplit, B), z(self.nsplit, B, dt=torch.int32)
@@ -701,6 +705,11 @@ SCREEN_TOL = 1e-4
 SCREEN_CMAX_BYTES = 2 << 30
 SCREEN_ROW_CHUNK = 2048
 LOGIT_TERMS = {"f32x9": 9, "f32x6": 6, "f32x6d3": 6}
+# stored logits of the fused head (pass 1 writes z = S + b, pass 2 reads it
+# instead of recomputing the S contraction: 21 -> 15 bf16 plane-product terms
+# per step at f32x6d3): used while the buffer (ceil(A/32)·32 × B floats,
+# 16.4 GB at C2) stays within this budget and a third of the free HBM
+ZSTORE_MAX_BYTES = 48 << 30
 PRECISIONS = ("f32",) + tuple(SPLIT_TERMS)
 
 
@@ -807,6 +816,25 @@ class SoftmaxHead:
             self._fws[slot] = w
         return w
 
+    def zs_buffer(self, w):
+        """The stored-logit buffer of workspace w, or None (recomputed in pass
+        2).  ``zstore``: None = auto (HF <= 128 and within ZSTORE_MAX_BYTES and
+        a third of the free device memory), True / False force it (tests)."""
+        mode = getattr(self, "zstore", None)
+        if mode is False or self.HF > 128:
+            return None
+        if w.zs is None:
+            nb = int(call("rg_flash_zs_bytes", w.B, self.A))
+            if mode is None and (nb > ZSTORE_MAX_BYTES or nb > torch.cuda.mem_get_info(self.device)[0] // 3):
+                w.zs = False
+            else:
+                w.zs = torch.empty(nb // 4, dtype=torch.float32, device=self.device)
+        return w.zs if w.zs is not False else None
+
+    def stored_logits(self):
+        """True when a fused workspace of this head keeps its logits for pass 2."""
+        return any(isinstance(w.zs, torch.Tensor) for w in self._fws.values())
+
     def flash_forward(self, h, tgt, slot, terms):
         """Pass 1 + this head's lse and target logit (zt = 0 when the target
         lies outside the held items [lo, hi))."""
@@ -823,9 +851,11 @@ class SoftmaxHead:
             if w.wgen != self._wgen:   # else the previous pass 2 left this W's planes here
                 call("rg_head_planes", W, A, HF, w.Wk.data_ptr(), w.Wr.data_ptr(), b, w.bias_pad.data_ptr(), st)
                 w.wgen = self._wgen
+            zs = self.zs_buffer(w)
             call("rg_flash_fwd_top", w.Hk.data_ptr(), w.Wk.data_ptr(), w.Wr.data_ptr(), w.bias_pad.data_ptr(), B, A,
                  HF, terms, w.nsplit, w.pm.data_ptr(), w.pl.data_ptr(), w.pO.data_ptr(), ptr(w.pbest), ptr(w.parg),
-                 ptr(w.cmax), st)
+                 ptr(w.cmax), ptr(zs), st)
+            w.zs_live = zs is not None
         call("rg_flash_lse", w.pm.data_ptr(), w.pl.data_ptr(), w.nsplit, h.data_ptr(), W, b, tgt.data_ptr(), self.lo,
              A, self.A_full, B, HF, w.lse.data_ptr(), w.zt.data_ptr(), st)
         return w
@@ -1010,7 +1040,8 @@ class SoftmaxHead:
                  w.bias_pad.data_ptr(), w.rows.data_ptr(), g, w.B, self.A, self.HF, w.terms, Wp.p.data_ptr(),
                  Wp.m.data_ptr(), Wp.v.data_ptr(), bp.p.data_ptr(), bp.m.data_ptr(), bp.v.data_ptr(), adam6, None,
                  None, w.Wk.data_ptr(), w.Wr.data_ptr(), w.bias_pad.data_ptr(), w.dw_work.data_ptr(),
-                 w.dw_work_bytes, stream_ptr())
+                 w.dw_work_bytes, w.zs.data_ptr() if w.zs_live else None, stream_ptr())
+        w.zs_live = False
         self._wgen += 1
         w.wgen = self._wgen
 

@@ -18,7 +18,7 @@ import numpy as np
 import torch
 
 from . import call, host_floats, host_ptr_array, stream_ptr
-from .engine import SoftmaxHead, _f32
+from .engine import SegScatter, SoftmaxHead, _f32
 from .nets import HipNet
 from .remap import raise_if_unmapped, remap_ids
 from .timing import region
@@ -133,6 +133,29 @@ def q_side_stream(net):
     return net._qstream
 
 
+def q_heads_backward(main, h, idx, B, dq, dh, tag, st):
+    """Backward of the Q heads' gathered Q(s, a) (sqn_gru.py:221-222): dh +=
+    Σ_i dq_i W_i[a], and G_i[a] += dq_i h, Gb_i[a] += dq_i summed per action in
+    row order through one sort shared by every head (csrc/segsum.hip) — rows of
+    a batch share actions, so atomic adds would make the step
+    order-dependent.  idx: int64 action per row, -1 = not held here."""
+    nh, HF = len(main.q_heads), main.hf
+    rows = main.buf("q_grows", (nh, B, HF))
+    rows_b = main.buf("q_grows_b", (nh, B))
+    ids = main.buf("q_ids", (B,), torch.int32)
+    n = main.buf("q_n", (1,), torch.int32)
+    call("rg_q_backward", h.data_ptr(), HF, host_ptr_array([x.W.p for x in main.q_heads]), nh, idx.data_ptr(), B,
+         dq.data_ptr(), dh.data_ptr(), rows.data_ptr(), rows_b.data_ptr(), ids.data_ptr(), n.data_ptr(), st)
+    if getattr(main, "_qscatter", None) is None:
+        main._qscatter = SegScatter(main.device)
+    sc = main._qscatter
+    for i, qh in enumerate(main.q_heads):
+        sc(ids.data_ptr(), rows[i].data_ptr(), HF, n.data_ptr(), B, -1, qh.G.data_ptr(), qh.A, qh.tags.data_ptr(),
+           tag, st, reuse_sort=i > 0)
+        sc(ids.data_ptr(), rows_b[i].data_ptr(), 1, n.data_ptr(), B, -1, qh.Gb.data_ptr(), qh.A, qh.tags.data_ptr(),
+           tag, st, reuse_sort=True)
+
+
 def _dev(x, dev, dtype=None):
     x = x.to(dev, non_blocking=True)
     return x if dtype is None else x.to(dtype)
@@ -196,9 +219,7 @@ def double_q_step(nets, clocks, k, s, a, r, s_next, true_len, true_next_len, is_
     dh = main.dh_buffer(B)
     # the supervised head's pass 2 overlaps the Q heads' backward / Adam and the trunk
     main.sup_head_output.backward_step(h, a, dh, adam6, slot="main", overlap=True)
-    call("rg_q_backward", h.data_ptr(), main.hf, host_ptr_array([x.W.p for x in main.q_heads]),
-         host_ptr_array([x.G for x in main.q_heads]), host_ptr_array([x.Gb for x in main.q_heads]),
-         host_ptr_array([x.tags for x in main.q_heads]), nh, a.data_ptr(), B, dq.data_ptr(), dh.data_ptr(), tag, st)
+    q_heads_backward(main, h, a, B, dq, dh, tag, st)
     # the Q heads' dense Adam sweeps on their own stream beside the trunk
     # backward (they read only the Q heads' G rows, written above); joined
     # before the step ends

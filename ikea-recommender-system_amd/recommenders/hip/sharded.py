@@ -24,10 +24,10 @@ from __future__ import annotations
 import numpy as np
 import torch
 
-from . import call, host_ptr_array, stream_ptr
+from . import call, stream_ptr
 from .engine import _f32
 from .dist import host_routes
-from .qlearn import q_side_stream
+from .qlearn import q_heads_backward, q_side_stream
 from .remap import raise_if_unmapped, remap_ids
 from .timing import region
 
@@ -343,10 +343,7 @@ def sharded_double_q_step(nets, clocks, k, s, a, r, s_next, true_len, true_next_
     if fused:   # pass 2 on the supervised head's side stream under the rest of the step
         sup.flash_dw_adam_async(w, _f32(1.0 / Bg), adam6)
     dq_all = _gather_rows(comm, main, "dq_all", dq)
-    call("rg_q_backward", H_all.data_ptr(), HF, host_ptr_array([x.W.p for x in main.q_heads]),
-         host_ptr_array([x.G for x in main.q_heads]), host_ptr_array([x.Gb for x in main.q_heads]),
-         host_ptr_array([x.tags for x in main.q_heads]), nh, a_loc.data_ptr(), Bg, dq_all.data_ptr(),
-         dH_all.data_ptr(), tag, st)
+    q_heads_backward(main, H_all, a_loc, Bg, dq_all, dH_all, tag, st)
     cur = torch.cuda.current_stream(main.device)
     qs = q_side_stream(main)   # the Q heads' dense Adam sweeps beside the trunk's (qlearn.double_q_step)
     qs.wait_stream(cur)

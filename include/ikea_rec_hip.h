@@ -168,9 +168,12 @@ int rg_flash_fwd(const void* Hk, const void* Wk, const void* Wr, const float* bi
  *   (every item re-scored the same way, canonical top-K): the result is exact for
  *   every row; err (optional) counts the rows scanned. */
 int rg_flash_rows_per_block(int HF);
+/* zs (optional, HF <= 128): pass 1 also stores the logits z = h·Wᵀ + b as rg_flash_zs_bytes(B, A)
+ *   bytes of 32-item × 32-row tiles for rg_flash_dw_adam_planes (which then skips recomputing them). */
 int rg_flash_fwd_top(const void* Hk, const void* Wk, const void* Wr, const float* bias_pad, int B, int A, int HF,
                      int terms, int nsplit, float* pm, float* pl, float* pO, float* pbest, int32_t* parg, float* cmax,
-                     rg_stream_t stream);
+                     float* zs, rg_stream_t stream);
+int64_t rg_flash_zs_bytes(int B, int A);
 /* rg_flash_score: evaluation scoring (evaluate / update_train_metrics, eval_protocol.py:123-359)
  *   — pass 1's S-part without the O contraction: pm / pl (-> rg_flash_lse), per-split first maximum
  *   (pbest / parg) and every 32-item chunk's row maximum cmax (ceil(A/32) x B, -> rg_flash_topk for
@@ -225,12 +228,14 @@ int rg_flash_dw_adam(const void* Hk, const void* Hr, const void* Wk, const float
  * rg_head_planes of the new W is then not needed before the next rg_flash_fwd.  Wk_out, Wr_out
  * and bias_pad_out together or all NULL; not with dW_out.  work (rg_flash_dw_work_bytes(B, A, HF)
  * bytes; optional): the item blocks past the last whole round of 256 workgroups are then split
- * over the row chunks (partial dW / db summed in order by a finishing kernel). */
+ * over the row chunks (partial dW / db summed in order by a finishing kernel).  zs: the logits
+ * pass 1 stored (rg_flash_fwd_top, same h / W / b): read instead of recomputed (no K-planes of h
+ * or W are read then). */
 int rg_flash_dw_adam_planes(const void* Hk, const void* Hr, const void* Wk, const float* bias_pad,
                             const void* rowinfo, float gscale, int B, int A, int HF, int terms, float* W, float* mW,
                             float* vW, float* bias, float* mb, float* vb, const float* adam6, float* dW_out,
                             float* db_out, void* Wk_out, void* Wr_out, float* bias_pad_out, void* work,
-                            int64_t work_bytes, rg_stream_t stream);
+                            int64_t work_bytes, const float* zs, rg_stream_t stream);
 int64_t rg_flash_dw_work_bytes(int B, int A, int HF);
 /* rg_head_fwd_x from h's planes (rg_head_work_bytes layout) with the rows split
  * over workgroups: rpb rows per workgroup (multiple of 32), parg optional.
@@ -291,9 +296,12 @@ int rg_adam_slabs(float* P, float* M, float* V, const float* slabs, int nslab, i
  * W / bias: HOST arrays of nh device pointers; idx int64 or int32 (one NULL). */
 int rg_q_gather(const float* h, int HF, const float* const* W, const float* const* bias, int nh,
                 const int64_t* idx64, const int32_t* idx32, int B, float* q, rg_stream_t stream);
-int rg_q_backward(const float* h, int HF, const float* const* W, float* const* GW, float* const* Gb,
-                  int32_t* const* tags, int nh, const int64_t* idx, int B, const float* dq, float* dh, int32_t tag,
-                  rg_stream_t stream);
+/* backward without float atomics: dh += sum_i dq_bi W_i[a_b] (heads in order); writes the
+ * gradient contributions rows (nh x B x HF) = dq_bi h_b and rows_b (nh x B) = dq_bi, ids (B,
+ * int32, -1 = skipped) and n_rows[0] = B for the sorted scatter rg_scatter_rows into G_i / Gb_i
+ * (one sort shared by all heads: reuse_sort). */
+int rg_q_backward(const float* h, int HF, const float* const* W, int nh, const int64_t* idx, int B, const float* dq,
+                  float* dh, float* rows, float* rows_b, int32_t* ids, int32_t* n_rows, rg_stream_t stream);
 /* SQN TD loss (SQN/sqn_gru.py:234-239), f64 like the reference. */
 int rg_sqn_td(const float* q, float* qn, const double* r, const uint8_t* is_end, float gamma, int B, double scale,
               double* sq, float* dq, rg_stream_t stream);

@@ -24,9 +24,11 @@ def _u8(n):
     return torch.empty(int(n), dtype=torch.uint8, device=dev)
 
 
-def run_flash(h, W, b, tgt, terms, nsplit, lo=0, lse_global=None, A_full=None):
+def run_flash(h, W, b, tgt, terms, nsplit, lo=0, lse_global=None, A_full=None, zs=False):
     """Every stage of the fused head through the C ABI; pass 2 in its
-    gradient-only mode (dW_out / db_out)."""
+    gradient-only mode (dW_out / db_out).  zs: pass 1 stores the logits
+    (rg_flash_fwd_top) and pass 2 reads them instead of recomputing S; the
+    stored buffer is returned as "zs"."""
     call, st = C().call, C().stream_ptr()
     B, HF = h.shape
     A = W.shape[0]
@@ -38,8 +40,14 @@ def run_flash(h, W, b, tgt, terms, nsplit, lo=0, lse_global=None, A_full=None):
     pm = torch.full((nsplit, B), float("nan"), device=dev)
     pl = torch.full((nsplit, B), float("nan"), device=dev)
     pO = torch.full((nsplit, HF, B), float("nan"), device=dev)
-    call("rg_flash_fwd", Hk.data_ptr(), Wk.data_ptr(), Wr.data_ptr(), bp.data_ptr(), B, A, HF, terms, nsplit,
-         pm.data_ptr(), pl.data_ptr(), pO.data_ptr(), st)
+    zbuf = None
+    if zs:
+        zbuf = torch.full((call("rg_flash_zs_bytes", B, A) // 4,), float("nan"), device=dev)
+        call("rg_flash_fwd_top", Hk.data_ptr(), Wk.data_ptr(), Wr.data_ptr(), bp.data_ptr(), B, A, HF, terms, nsplit,
+             pm.data_ptr(), pl.data_ptr(), pO.data_ptr(), None, None, None, zbuf.data_ptr(), st)
+    else:
+        call("rg_flash_fwd", Hk.data_ptr(), Wk.data_ptr(), Wr.data_ptr(), bp.data_ptr(), B, A, HF, terms, nsplit,
+             pm.data_ptr(), pl.data_ptr(), pO.data_ptr(), st)
     lse = torch.full((B,), float("nan"), device=dev)
     zt = torch.full((B,), float("nan"), device=dev)
     call("rg_flash_lse", pm.data_ptr(), pl.data_ptr(), nsplit, h.data_ptr(), W.data_ptr(), b.data_ptr(),
@@ -53,10 +61,29 @@ def run_flash(h, W, b, tgt, terms, nsplit, lo=0, lse_global=None, A_full=None):
          dh.data_ptr(), st)
     dW = torch.full((A, HF), float("nan"), device=dev)
     db = torch.full((A,), float("nan"), device=dev)
-    call("rg_flash_dw_adam", Hk.data_ptr(), Hr.data_ptr(), Wk.data_ptr(), bp.data_ptr(), rows.data_ptr(), g, B, A,
-         HF, terms, None, None, None, None, None, None, None, dW.data_ptr(), db.data_ptr(), st)
+    if zs:
+        call("rg_flash_dw_adam_planes", Hk.data_ptr(), Hr.data_ptr(), Wk.data_ptr(), bp.data_ptr(), rows.data_ptr(), g,
+             B, A, HF, terms, None, None, None, None, None, None, None, dW.data_ptr(), db.data_ptr(), None, None, None,
+             None, 0, zbuf.data_ptr(), st)
+    else:
+        call("rg_flash_dw_adam", Hk.data_ptr(), Hr.data_ptr(), Wk.data_ptr(), bp.data_ptr(), rows.data_ptr(), g, B, A,
+             HF, terms, None, None, None, None, None, None, None, dW.data_ptr(), db.data_ptr(), st)
     torch.cuda.synchronize()
-    return {k: v.cpu().double() for k, v in dict(lse=lse, zt=zt, dh=dh, dW=dW, db=db).items()}
+    out = {k: v.cpu().double() for k, v in dict(lse=lse, zt=zt, dh=dh, dW=dW, db=db).items()}
+    if zs:
+        out["zs"] = zbuf.cpu().double()
+    return out
+
+
+def zs_to_logits(zs, B, A):
+    """(B, A) logits from the stored tiles (csrc/head_flash.hip k_flash_fwd: one
+    1024-float tile per (32-item chunk, 32-row block), chunk-major; inside,
+    quadrant (item half ib, row half rb), then lane (kg, l16), then u: the
+    logit of item 16ib + 4kg + u, row 16rb + l16)."""
+    nct = (A + 31) // 32
+    t = zs.reshape(nct, B // 32, 2, 2, 4, 16, 4)            # chunk, row block, ib, rb, kg, l16, u
+    t = t.permute(1, 3, 5, 0, 2, 4, 6).reshape(B, nct * 32)   # row block, rb, l16 | chunk, ib, kg, u
+    return t[:, :A]
 
 
 @pytest.mark.parametrize("B,A,HF", [(64, 1000, 32), (96, 3001, 64), (128, 4133, 128), (64, 2077, 256),
@@ -97,7 +124,7 @@ def test_pass2_writes_next_planes(B, A, HF):
             nb = call("rg_flash_dw_work_bytes", B, A, HF)
             work = _u8(max(nb, 16))
             call("rg_flash_dw_adam_planes", *args, Wk2.data_ptr(), Wr2.data_ptr(), bp2.data_ptr(), work.data_ptr(),
-                 nb, st)
+                 nb, None, st)
         else:
             call("rg_flash_dw_adam", *args, st)
         torch.cuda.synchronize()
@@ -140,7 +167,7 @@ def test_pass2_tail_split_matches_fp64(B, A, HF):
     g = float(np.float32(1.0 / B))
     call("rg_flash_dw_adam_planes", Hk.data_ptr(), Hr.data_ptr(), Wk.data_ptr(), bp.data_ptr(), rows.data_ptr(), g, B,
          A, HF, 6, None, None, None, None, None, None, None, dW.data_ptr(), db.data_ptr(), None, None, None,
-         work.data_ptr(), nb, st)
+         work.data_ptr(), nb, None, st)
     torch.cuda.synchronize()
     torch.testing.assert_close(dW.cpu().double(), r["dW"], rtol=0, atol=1e-7)
     torch.testing.assert_close(db.cpu().double(), r["db"], rtol=0, atol=1e-7)
@@ -182,6 +209,85 @@ def test_flash_head_matches_fp64(precision, B, A, HF, nsplit):
     torch.testing.assert_close(o["dh"], r["dh"], rtol=0, atol=1e-6)
     torch.testing.assert_close(o["dW"], r["dW"], rtol=0, atol=1e-7)
     torch.testing.assert_close(o["db"], r["db"], rtol=0, atol=1e-7)
+
+
+@pytest.mark.parametrize("precision", ["f32x6", "f32x6d3"])
+@pytest.mark.parametrize("B,A,HF,nsplit", [(64, 1000, 32, 8), (128, 3001, 64, 16), (256, 4133, 128, 8),
+                                           (512, 2077, 128, 64), (96, 777, 128, 3), (288, 50000, 128, 16)])
+def test_stored_logits_match_fp64(precision, B, A, HF, nsplit):
+    """Stored-logit head (zs): pass 1 writes z = h·Wᵀ + b tile by tile, pass 2
+    reads it instead of recomputing the S contraction.  The stored logits
+    against fp64 (and −inf past A inside the last chunk), and every output at
+    the recomputing head's tolerances; dW / db within a few fp32 ulps of the
+    recomputing pass 2's (same products, other accumulation order)."""
+    h, W, b, tgt = inputs(B, A, HF, B + A + HF)
+    hd, Wd, bd, td = h.to(dev), W.to(dev), b.to(dev), tgt.to(dev)
+    o = run_flash(hd, Wd, bd, td, TERMS[precision], nsplit, zs=True)
+    o2 = run_flash(hd, Wd, bd, td, TERMS[precision], nsplit)
+    r = fp64_reference(h, W, b, tgt)
+    nct = (A + 31) // 32
+    Z = zs_to_logits(o["zs"], B, nct * 32)
+    torch.testing.assert_close(Z[:, :A], r["Z"], rtol=0, atol=2e-6)
+    assert torch.isneginf(Z[:, A:]).all()
+    torch.testing.assert_close(o["lse"], r["lse"], rtol=0, atol=2e-5)
+    torch.testing.assert_close(o["dh"], r["dh"], rtol=0, atol=1e-6)
+    torch.testing.assert_close(o["dW"], r["dW"], rtol=0, atol=1e-7)
+    torch.testing.assert_close(o["db"], r["db"], rtol=0, atol=1e-7)
+    torch.testing.assert_close(o["dW"], o2["dW"], rtol=0, atol=2e-8)
+    torch.testing.assert_close(o["db"], o2["db"], rtol=0, atol=2e-8)
+
+
+def test_stored_logits_refused_at_hf256():
+    call = C().call
+    B, A, HF = 64, 1000, 256
+    z = torch.empty(call("rg_flash_zs_bytes", B, A) // 4, device=dev)
+    x = torch.empty(16, device=dev)
+    with pytest.raises(RuntimeError, match="status -3"):   # RG_ERR_SHAPE, nothing launched
+        call("rg_flash_fwd_top", x.data_ptr(), x.data_ptr(), x.data_ptr(), x.data_ptr(), B, A, HF, 6, 8, x.data_ptr(),
+             x.data_ptr(), x.data_ptr(), None, None, None, z.data_ptr(), C().stream_ptr())
+
+
+@pytest.mark.parametrize("B,A,HF", [(96, 78341, 64), (64, 70000, 128)])
+def test_stored_logits_tail_split_adam(B, A, HF):
+    """Stored logits through the trainer's pass 2 (Adam + next planes, the
+    leftover item blocks split over the row chunks): W / b / moments and the
+    planes equal the recomputing pass 2's within fp32 rounding."""
+    call, st = C().call, C().stream_ptr()
+    h, W, b, tgt = inputs(B, A, HF, 5 + HF)
+    h, W, b, tgt = h.to(dev), W.to(dev), b.to(dev), tgt.to(dev)
+    hb, wb = call("rg_head_plane_bytes", B, HF), call("rg_head_plane_bytes", A, HF)
+    Hk, Hr, Wk, Wr = _u8(hb), _u8(hb), _u8(wb), _u8(wb)
+    bp = torch.empty((A + 31) // 32 * 32, device=dev)
+    call("rg_head_planes", h.data_ptr(), B, HF, Hk.data_ptr(), Hr.data_ptr(), None, None, st)
+    call("rg_head_planes", W.data_ptr(), A, HF, Wk.data_ptr(), Wr.data_ptr(), b.data_ptr(), bp.data_ptr(), st)
+    ns = 8
+    pm, pl, pO = torch.empty(ns, B, device=dev), torch.empty(ns, B, device=dev), torch.empty(ns, HF, B, device=dev)
+    zbuf = torch.empty(call("rg_flash_zs_bytes", B, A) // 4, device=dev)
+    call("rg_flash_fwd_top", Hk.data_ptr(), Wk.data_ptr(), Wr.data_ptr(), bp.data_ptr(), B, A, HF, 636, ns,
+         pm.data_ptr(), pl.data_ptr(), pO.data_ptr(), None, None, None, zbuf.data_ptr(), st)
+    lse, zt, rows = torch.empty(B, device=dev), torch.empty(B, device=dev), torch.empty(B, 2, device=dev)
+    call("rg_flash_lse", pm.data_ptr(), pl.data_ptr(), ns, h.data_ptr(), W.data_ptr(), b.data_ptr(), tgt.data_ptr(),
+         0, A, A, B, HF, lse.data_ptr(), zt.data_ptr(), st)
+    call("rg_flash_rows", lse.data_ptr(), tgt.data_ptr(), 0, A, B, rows.data_ptr(), st)
+    adam6 = C().host_floats([0.1, 0.999, 0.001, 0.0316, 1e-8, -0.01])
+    g = float(np.float32(1.0 / B))
+    nb = call("rg_flash_dw_work_bytes", B, A, HF)
+    assert nb > 0
+    outs = []
+    for use_z in (False, True):
+        Wx, bx = W.clone(), b.clone()
+        mW, vW = torch.full_like(W, 0.01), torch.full_like(W, 0.02)
+        mb, vb = torch.full_like(b, 0.01), torch.full_like(b, 0.02)
+        Wk2, Wr2, bp2 = Wk.clone(), Wr.clone(), bp.clone()
+        work = _u8(nb)
+        call("rg_flash_dw_adam_planes", Hk.data_ptr(), Hr.data_ptr(), Wk2.data_ptr(), bp2.data_ptr(), rows.data_ptr(),
+             g, B, A, HF, 636, Wx.data_ptr(), mW.data_ptr(), vW.data_ptr(), bx.data_ptr(), mb.data_ptr(),
+             vb.data_ptr(), adam6, None, None, Wk2.data_ptr(), Wr2.data_ptr(), bp2.data_ptr(), work.data_ptr(), nb,
+             zbuf.data_ptr() if use_z else None, st)
+        torch.cuda.synchronize()
+        outs.append((Wx, bx, mW, vW, mb, vb))
+    for x, y in zip(outs[0], outs[1]):
+        torch.testing.assert_close(x, y, rtol=1e-5, atol=1e-7)
 
 
 def test_flash_head_item_shard():
@@ -349,7 +455,7 @@ def run_top(h, W, b, terms, nsplit, K, exact1=False):
     cmax = z((A + 31) // 32, B) if K > 1 or exact1 else None
     call("rg_flash_fwd_top", Hk.data_ptr(), Wk.data_ptr(), Wr.data_ptr(), bp.data_ptr(), B, A, HF, terms, nsplit,
          pm.data_ptr(), pl.data_ptr(), pO.data_ptr(), pbest.data_ptr(), parg.data_ptr(),
-         None if cmax is None else cmax.data_ptr(), st)
+         None if cmax is None else cmax.data_ptr(), None, st)
     idx, vals = z(B, K, dt=torch.int32), z(B, K)
     err = torch.zeros(1, dtype=torch.int32, device=dev)
     if K == 1 and not exact1:

@@ -252,10 +252,12 @@ def test_head_forward_backward(B, A, HF):
     torch.testing.assert_close(db.cpu().double(), br.grad, rtol=0, atol=1e-7)
 
 
-def test_adam_kernels_match_torch():
+@pytest.mark.parametrize("rows,cols", [(300, 16), (303, 1), (300, 1), (3, 1), (301, 3)])
+def test_adam_kernels_match_torch(rows, cols):
+    """Row-sparse Adam: wide rows (f4), one-column tables (the heads' biases:
+    four rows per thread plus the tail), other widths (scalar)."""
     from recommenders.hip.engine import AdamClock
     g = torch.Generator().manual_seed(5)
-    rows, cols = 300, 16
     p0 = torch.randn(rows, cols, generator=g)
     grads = [torch.randn(rows, cols, generator=g) for _ in range(3)]
     touched = [torch.rand(rows, generator=g) < 0.3 for _ in range(3)]
@@ -323,6 +325,55 @@ def test_q_kernels_and_rewards():
              D(idx).data_ptr(), None, B, q.data_ptr(), st())
     ref = torch.stack([(h * Ws[i][idx]).sum(1) + bs[i][idx] for i in range(3)], 1)
     torch.testing.assert_close(q.cpu(), ref, rtol=0, atol=1e-5)
+    # backward: dh += Σ_i dq_i W_i[a]; G_i[a] += dq_i h, Gb_i[a] += dq_i through the sorted scatter
+    # (many rows share an action: idx drawn from 7 actions), -1 rows skipped; bitwise repeatable
+    from recommenders.hip.qlearn import q_heads_backward
+
+    class _QH:
+        def __init__(self, W):
+            self.W = type("P", (), {"p": W})()
+            self.A = A
+            self.G = torch.zeros(A, HF, device=dev)
+            self.Gb = torch.zeros(A, device=dev)
+            self.tags = torch.zeros(A, dtype=torch.int32, device=dev)
+
+    class _Main:
+        def __init__(self):
+            self.q_heads = [_QH(w) for w in Wd]
+            self.hf, self.device, self._b = HF, dev, {}
+
+        def buf(self, name, shape, dtype=torch.float32):
+            t = self._b.get(name)
+            if t is None or tuple(t.shape) != tuple(shape) or t.dtype != dtype:
+                t = self._b[name] = torch.empty(*shape, dtype=dtype, device=dev)
+            return t
+
+    ib = torch.randint(0, 7, (B,), generator=g) * 37
+    ib[3] = -1
+    dq = torch.randn(B, 3, generator=g)
+    dh0 = torch.randn(B, HF, generator=g)
+    outs = []
+    for rep in range(2):
+        mn = _Main()
+        dh = dh0.to(dev)
+        q_heads_backward(mn, hd, D(ib), B, D(dq), dh, 5, st())
+        torch.cuda.synchronize()
+        outs.append((dh.cpu(), [x.G.cpu() for x in mn.q_heads], [x.Gb.cpu() for x in mn.q_heads],
+                     [x.tags.cpu() for x in mn.q_heads]))
+    ok = ib >= 0
+    dh_ref = dh0.double().clone()
+    for i in range(3):
+        dh_ref[ok] += dq[ok, i:i + 1].double() * Ws[i][ib[ok]].double()
+        Gr = torch.zeros(A, HF, dtype=torch.float64).index_add_(0, ib[ok], dq[ok, i:i + 1].double() * h[ok].double())
+        Gbr = torch.zeros(A, dtype=torch.float64).index_add_(0, ib[ok], dq[ok, i].double())
+        torch.testing.assert_close(outs[0][1][i].double(), Gr, rtol=0, atol=1e-5)
+        torch.testing.assert_close(outs[0][2][i].double(), Gbr, rtol=0, atol=1e-5)
+        tg = torch.zeros(A, dtype=torch.int32)
+        tg[ib[ok]] = 5
+        assert torch.equal(outs[0][3][i], tg)
+        assert torch.equal(outs[0][1][i], outs[1][1][i]) and torch.equal(outs[0][2][i], outs[1][2][i])
+    torch.testing.assert_close(outs[0][0].double(), dh_ref, rtol=0, atol=1e-5)
+    assert torch.equal(outs[0][0], outs[1][0])
     # diversity / novelty
     from oracle import metrics as om
     L = 5

@@ -211,3 +211,37 @@ def test_smorl_unmapped_token_raises_before_update():
     for net, sd in zip((tr.SMORL_1, tr.SMORL_2), before):
         for k, v in net.state_dict().items():
             assert torch.equal(v, sd[k]), k
+
+
+@pytest.mark.parametrize("kind", ["sqn", "smorl"])
+def test_double_q_steps_are_bitwise_repeatable(kind):
+    """Two runs of the same SQN / SMORL steps are bit for bit identical: the
+    Q heads' row gradients are summed per action through the sorted scatter
+    (recommenders/hip/qlearn.q_heads_backward), not float atomics — 300
+    actions for 512 rows, so most actions collect several contributions."""
+    from recommenders.data_utils.synthetic import SessionStream
+    N, L, B, E = 300, 8, 512, 32
+    st = SessionStream(N, L, B * 3, seed=23)
+    cfg = dict(hidden_dim=E, embedding_dim=E, train_pad_embed=True, use_packed_seq=True, learning_rate=0.01,
+               item_num=N, state_size=L, action_dim=N, gamma=0.5, gru_layers=1)
+    runs = []
+    for _ in range(2):
+        random.seed(4)
+        if kind == "sqn":
+            from recommenders.models.SQN.sqn_gru import SQN_trainer
+            tr = SQN_trainer(device="cuda", **cfg)
+            nets = (tr.DQN_1, tr.DQN_2)
+        else:
+            from recommenders.models.SMORL.smorl_gru import SMORL_trainer
+            g = torch.Generator().manual_seed(7)
+            tr = SMORL_trainer(device="cuda", padding_pos="end", q_weights=[1.0, 0.5, 2.0], alpha=1.0,
+                               div_embedding=torch.randn(N + 1, 16, generator=g) * 0.01,
+                               unpopular_actions_set=set(range(0, N, 3)), nov_rew_sig=1.0, topk_div=1, topk_nov=1,
+                               **cfg)
+            nets = (tr.SMORL_1, tr.SMORL_2)
+        losses = [tr.train_step(*st.batch(i, B)) for i in range(3)]
+        runs.append((losses, [{k: v.cpu() for k, v in n.state_dict().items()} for n in nets]))
+    assert runs[0][0] == runs[1][0]
+    for sd0, sd1 in zip(runs[0][1], runs[1][1]):
+        for k in sd0:
+            assert torch.equal(sd0[k], sd1[k]), k

@@ -95,7 +95,8 @@ def test_sample_uniform_matches_oracle_bit_exact():
 
 @pytest.mark.parametrize("B,S,A,HF,collide", [(256, 256, 5000, 128, False), (37, 200, 300, 64, True),
                                               (300, 130, 100, 256, True), (128, 2048, 100000, 32, False),
-                                              (2240, 2048, 50000, 256, True), (1120, 64, 700, 64, True)])
+                                              (2240, 2048, 50000, 256, True), (1120, 64, 700, 64, True),
+                                              (416, 96, 3000, 256, False)])
 @pytest.mark.parametrize("precision", ["f32", "f32x9", "f32x6", "f32x9-fused", "f32x6-fused", "f32x6-fusedp"])
 def test_sampled_kernels_match_torch_fp32(B, S, A, HF, collide, precision):
     if precision != "f32" and (B % 32 or S % 32):

@@ -1,6 +1,8 @@
 """Time the fused split-bf16 head stages at C2 shapes (B 4096, A 1M, H 128):
 W planes, pass 1 (rg_flash_fwd), the dh combine and pass 2 with Adam
-(rg_flash_dw_adam).  IKEA_REC_HIP_LIB selects a diagnostic variant build."""
+(rg_flash_dw_adam).  --zs: pass 1 also stores the logits and pass 2 reads
+them (the stored-logit head).  IKEA_REC_HIP_LIB selects a diagnostic variant
+build."""
 import argparse
 import os
 import sys
@@ -17,6 +19,7 @@ ap.add_argument("--A", type=int, default=1_000_000)
 ap.add_argument("--H", type=int, default=128)
 ap.add_argument("--iters", type=int, default=4)
 ap.add_argument("--terms", type=int, nargs="+", default=[6, 9])
+ap.add_argument("--zs", action="store_true")
 a = ap.parse_args()
 B, A, H = a.B, a.A, a.H
 dev = "cuda"
@@ -43,14 +46,16 @@ st = stream_ptr()
 gs = 1.0 / B
 dwb = call("rg_flash_dw_work_bytes", B, A, H)
 dww = u8(max(dwb, 16))
+zs = torch.empty(call("rg_flash_zs_bytes", B, A) // 4, device=dev) if a.zs else None
+zp = None if zs is None else zs.data_ptr()
 call("rg_head_planes", h.data_ptr(), B, H, Hk.data_ptr(), Hr.data_ptr(), None, None, st)
 fl = 2.0 * B * A * H
 for terms in a.terms:
     stages = {
         "planes_W": lambda: call("rg_head_planes", W.data_ptr(), A, H, Wk.data_ptr(), Wr.data_ptr(), bias.data_ptr(),
                                  bp.data_ptr(), st),
-        "pass1": lambda: call("rg_flash_fwd", Hk.data_ptr(), Wk.data_ptr(), Wr.data_ptr(), bp.data_ptr(), B, A, H,
-                              terms, ns, pm.data_ptr(), pl.data_ptr(), pO.data_ptr(), st),
+        "pass1": lambda: call("rg_flash_fwd_top", Hk.data_ptr(), Wk.data_ptr(), Wr.data_ptr(), bp.data_ptr(), B, A,
+                              H, terms, ns, pm.data_ptr(), pl.data_ptr(), pO.data_ptr(), None, None, None, zp, st),
         "combine": lambda: (call("rg_flash_lse", pm.data_ptr(), pl.data_ptr(), ns, h.data_ptr(), W.data_ptr(),
                                  bias.data_ptr(), tgt.data_ptr(), 0, A, A, B, H, lse.data_ptr(), zt.data_ptr(), st),
                             call("rg_flash_rows", lse.data_ptr(), tgt.data_ptr(), 0, A, B, rows.data_ptr(), st),
@@ -60,7 +65,7 @@ for terms in a.terms:
         "pass2": lambda: call("rg_flash_dw_adam_planes", Hk.data_ptr(), Hr.data_ptr(), Wk.data_ptr(), bp.data_ptr(),
                               rows.data_ptr(), gs, B, A, H, terms, W.data_ptr(), mW.data_ptr(), vW.data_ptr(),
                               bias.data_ptr(), mb.data_ptr(), vb.data_ptr(), adam6, None, None, Wk.data_ptr(),
-                              Wr.data_ptr(), bp.data_ptr(), dww.data_ptr(), dwb, st),
+                              Wr.data_ptr(), bp.data_ptr(), dww.data_ptr(), dwb, zp, st),
     }
     for name, fn in stages.items():
         fn()
@@ -75,5 +80,7 @@ for terms in a.terms:
         extra = ""
         if name in ("pass1", "pass2"):
             nprod = {6: 12, 9: 18, 636: 9 if name == "pass1" else 12}[terms]   # plane products per pass
+            if a.zs and name == "pass2":
+                nprod //= 2   # (the S contraction is read, not recomputed)
             extra = f"  {nprod * fl / ms / 1e9:7.1f} TFLOP/s bf16 MFMA ({nprod * fl / ms / 1e9 / 2500:.3f} of peak)"
         print(f"terms {terms} {name:8s} {ms:8.3f} ms{extra}", flush=True)

@@ -4,12 +4,12 @@
 set -e
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out/pmcns
-for c in c2 c3; do
+for c in ${PMC_CONFIGS:-c2 c3}; do
 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmcns/${c}F -o f -- python3 tools/nsrun.py --config $c > gpurun_out/pmcns/${c}F.log 2>&1
 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmcns/${c}W -o w -- python3 tools/nsrun.py --config $c > gpurun_out/pmcns/${c}W.log 2>&1
 done
 python3 - <<'PY'
-import csv, glob, collections
+import csv, glob, collections, os
 def load(pat, ctr):
     acc = collections.defaultdict(list)
     for f in glob.glob(pat, recursive=True):
@@ -17,7 +17,7 @@ def load(pat, ctr):
             if r.get("Counter_Name") == ctr:
                 acc[r["Kernel_Name"]].append(float(r["Counter_Value"]))
     return acc
-for c in ("c2", "c3"):
+for c in os.environ.get("PMC_CONFIGS", "c2 c3").split():
     F = load(f"gpurun_out/pmcns/{c}F/**/*counter_collection.csv", "FETCH_SIZE")
     W = load(f"gpurun_out/pmcns/{c}W/**/*counter_collection.csv", "WRITE_SIZE")
     for k in sorted(F):
