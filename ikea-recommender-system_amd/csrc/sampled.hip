@@ -368,6 +368,9 @@ __global__ __launch_bounds__(sf_thr(HF)) void k_sampled_logits(const float* __re
   // 25.5 -> 22.8 us at C2 shapes); HF 256 (48 KB per chunk) keeps the
   // two-buffer ring with a barrier per chunk
   constexpr bool STAGE = HF <= 128;
+  // HF 256 with h's planes (HKP): two-slot ring, chunk c + 1's DMA issued
+  // behind the barrier that retires chunk c − 1's slot
+  constexpr bool HRING = HKP && !STAGE;
   __shared__ bf16x8 hsA[CH], hsB[CH];
   __shared__ bf16x8 hsC[STAGE ? CH : 1], hsD[STAGE ? CH : 1];
   __shared__ __attribute__((aligned(16))) float sbias[SF_NEG];
@@ -458,7 +461,7 @@ __global__ __launch_bounds__(sf_thr(HF)) void k_sampled_logits(const float* __re
   // MFMAs run slice-outer over all four chunks, so they start on slice 0 while
   // the later slices land (the four chunk accumulators stay live); the four
   // epilogues follow the last slice
-  constexpr bool KOUT_OK = PRE && HKP && CH % SF_THR == 0;
+  constexpr bool KOUT_OK = PRE && HKP && STAGE && CH % SF_THR == 0;
 #else
   constexpr bool KOUT_OK = false;
 #endif
@@ -513,6 +516,11 @@ __global__ __launch_bounds__(sf_thr(HF)) void k_sampled_logits(const float* __re
     __builtin_amdgcn_s_waitcnt(sf_wc_vm(3 * NS));
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
+    SFD_T(1);
+  } else if constexpr (HRING) {
+    if (hh == 0) sbias[32 * w + l32] = bl;
+    __syncthreads();   // chunk 0's planes, the W rows / planes and the biases
+    if (nch > 1) dma_chunk(hsB, 1);
     SFD_T(1);
   } else if constexpr (HKP) {
 #ifndef SF_BIASLATE
@@ -666,6 +674,28 @@ __global__ __launch_bounds__(sf_thr(HF)) void k_sampled_logits(const float* __re
       SFD_T(5);
       SFD_C(7);
     }
+  } else if constexpr (HRING) {
+    // step c: chunk c landed and every wave is done with chunk c − 1's slot ->
+    // DMA chunk c + 1 into it -> chunk c's MFMAs with chunk c − 1's epilogue
+    auto step_k = [&](int c, const bf16x8* hs_cur, bf16x8* hs_nxt, f16v& acc_new, f16v& acc_old)
+                      __attribute__((always_inline)) {
+      __syncthreads();
+      if (c + 1 < nch) dma_chunk(hs_nxt, c + 1);
+      if (nact) {
+        mma(hs_cur, acc_new);
+        epi(acc_old, c - 1);
+      }
+    };
+    int c = 1;
+    for (; c + 1 < nch; c += 2) {
+      step_k(c, hsB, hsA, accB, accA);
+      step_k(c + 1, hsA, hsB, accA, accB);
+    }
+    if (c < nch) step_k(c, hsB, hsA, accB, accA);
+    if (nact) {
+      if ((nch - 1) & 1) epi(accB, nch - 1);
+      else epi(accA, nch - 1);
+    }
   } else if constexpr (HKP) {
     // chunks 1..3 landed at the first barrier (SF_EARLY: at this one)
 #ifdef SF_EARLY
@@ -769,10 +799,10 @@ extern "C" int rg_sampled_logits(const float* h, const float* W, const float* bi
   RG_TLAUNCH((k_sampled_logits<HFV, NTV, DRV, HKV, PRV>), grid, dim3(sf_thr(HFV)), 0, stream, h, W, bias, neg, seed, \
              counter, (uint64_t)(A > 0 ? A : 0), B, S, Z, ldz, pmax, psum, Wg, bg, hk, wp)
 #define SFG(HFV, NTV)                                     \
-  if (hk && HFV <= 128) {                                 \
-    if (draw == 2) SFH(HFV, NTV, false, (HFV <= 128), true); \
-    else if (draw) SFH(HFV, NTV, true, (HFV <= 128), false); \
-    else SFH(HFV, NTV, false, (HFV <= 128), false);       \
+  if (hk) {                                               \
+    if (draw == 2) SFH(HFV, NTV, false, true, true);      \
+    else if (draw) SFH(HFV, NTV, true, true, false);      \
+    else SFH(HFV, NTV, false, true, false);               \
   } else {                                                \
     if (draw == 2) SFH(HFV, NTV, false, false, true);     \
     else if (draw) SFH(HFV, NTV, true, false, false);     \

@@ -1273,7 +1273,7 @@ class SampledSoftmaxHead(SoftmaxHead):
         # gather launch, pre); with the one-launch kernel the region is kernel-exact
         with region("sampled_fwd", exact=bool(split and w.zrow)):
             if split and w.zrow:  # one launch: [draw, row gather, operand split,] logits, partials
-                hp = h_planes.data_ptr() if h_planes is not None and self.HF <= 128 else None
+                hp = h_planes.data_ptr() if h_planes is not None else None
                 call("rg_sampled_logits", h.data_ptr(), self.W.p.data_ptr(), self.b.p.data_ptr(), w.ids.data_ptr(),
                      2 if pre else 1, self.seed, self.draws, self.A, B, self.S, self.HF, w.terms, w.ZT.data_ptr(),
                      w.ldz, w.pmax.data_ptr(), w.psum.data_ptr(), w.Wg.data_ptr(), w.bg.data_ptr(), hp,
@@ -1441,7 +1441,7 @@ class ShardedSampledHead(SampledSoftmaxHead):
             comm.all_to_all(rb_in[:B], rb_out[:R], w.send_splits, w.recv_splits)
             call("rg_rows_unslot", rows_in.data_ptr(), rb_in.data_ptr(), w.tslot.data_ptr(), w.t32.data_ptr(), B,
                  HF, w.tW.data_ptr(), w.tb.data_ptr(), st)
-        hp = h_planes.data_ptr() if h_planes is not None and HF <= 128 else None
+        hp = h_planes.data_ptr() if h_planes is not None else None
         with region("sampled_fwd", exact=True):   # the one-launch logits on the exchanged planes (draw = 2)
             call("rg_sampled_logits", h.data_ptr(), W, b, w.ids.data_ptr(), 2, self.seed, self.draws, self.A_full,
                  B, S, HF, w.terms, w.ZT.data_ptr(), w.ldz, w.pmax.data_ptr(), w.psum.data_ptr(), w.Wg.data_ptr(),

@@ -71,7 +71,7 @@ class HipNet:
                 self.heads = OrderedDict((n, SampledSoftmaxHead(n, action_dim, self.hf, self.device, n_negatives,
                                                                 neg_seed, loss=sampled_loss)) for n in head_names)
             # the split logits read h as bf16 planes written by the GRU forward
-            self.trunk.emit_planes = self.hf <= 128
+            self.trunk.emit_planes = self.hf <= 256
         else:
             self.heads = OrderedDict((n, SoftmaxHead(n, action_dim, self.hf, self.device, shard=shard))
                                      for n in head_names)

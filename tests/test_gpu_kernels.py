@@ -468,7 +468,8 @@ def test_scatter_rows_deterministic(E, n_rows, n, n_max):
     assert torch.equal(tags == 9, touched)
 
 
-@pytest.mark.parametrize("H,ndir,B,L", [(128, 1, 100, 9), (64, 2, 70, 6), (32, 1, 33, 5), (16, 2, 64, 4)])
+@pytest.mark.parametrize("H,ndir,B,L", [(128, 1, 100, 9), (128, 2, 70, 6), (64, 2, 70, 6), (32, 1, 33, 5),
+                                        (16, 2, 64, 4)])
 def test_gru_forward_emits_h_planes(H, ndir, B, L):
     """rg_gru_fwd_dirs_planes: the same final h as rg_gru_fwd_dirs, and its
     bf16 K-planes (the sampled head's operand) bitwise equal to
