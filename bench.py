@@ -93,6 +93,9 @@ def parse():
     # top-20 / HR@20
     ap.add_argument("--precision", choices=["f32", "f32x9", "f32x6", "f32x6d3"], default="f32x6d3",
                     help="head GEMM arithmetic (hip/engine.py SPLIT_TERMS): native fp32 MFMA or split-bf16")
+    ap.add_argument("--stored-logits", choices=["auto", "off"], default="auto",
+                    help="fused head: pass 1 stores the logits for pass 2 (auto: where they fit, HF <= 128; "
+                         "hip/engine.py ZSTORE_MAX_BYTES) or pass 2 recomputes them (off)")
     ap.add_argument("--no-target", action="store_true", help="skip the north-star gather+sampled-logits side run")
     ap.add_argument("--no-native-side", action="store_true", help="skip the native-f32 side run")
     return ap.parse_args()
@@ -265,6 +268,17 @@ def make_trainer(cfg, args, dev, shard):
                              device=dev, shard_items=shard, matmul_precision=args.precision,
                              fp16_embeddings=(cfg == "c5"), **common)
     raise ValueError(cfg)
+
+
+def apply_stored_logits(tr, mode):
+    """--stored-logits off: every fused full-softmax head recomputes its logits in pass 2."""
+    if mode == "auto":
+        return
+    from recommenders.hip.engine import SoftmaxHead
+    for name in ("gru_model", "SMORL_1", "SMORL_2", "DQN_1", "DQN_2"):
+        for h in getattr(getattr(tr, name, None), "heads", {}).values():
+            if isinstance(h, SoftmaxHead):
+                h.zstore = False
 
 
 def step_args(cfg, b):
@@ -601,6 +615,7 @@ def main():
     T = float(np.mean(tok[args.warmup:]))
     t_init = time.perf_counter()
     tr = make_trainer(args.config, args, dev, shard)
+    apply_stored_logits(tr, args.stored_logits)
     tr.set_train()
     print(f"bench: trainer built in {time.perf_counter() - t_init:.1f} s, "
           f"{torch.cuda.memory_allocated(dev) / 2**30:.1f} GiB on the device", file=sys.stderr, flush=True)
@@ -727,7 +742,7 @@ def main():
         "value": round(value, 2), "unit": "session-steps/sec", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True,
         "scaling": "strong" if args.config in ("c4", "c5") else "weak",
-        "vs_baseline": None, "dtype": "f32", "matmul_precision": args.precision,
+        "vs_baseline": None, "dtype": "f32", "matmul_precision": args.precision, "stored_logits": args.stored_logits,
         "data": "synthetic (seeded Zipf session stream, random-init weights)",
         "config": {"workload": workload,
                    "global_batch": B * world, "seq_len": L, "items": N, "dim": E,

@@ -162,7 +162,7 @@ extern "C" int rg_fl_stamp_read(void* dst, int64_t n) {
 #define FL_SYNC() __syncthreads()
 #endif
 
-template <int HF, int NT, int NG, bool ARG>
+template <int HF, int NT, int NG, bool ARG, bool ZS = false>
 __global__ __launch_bounds__(64 * fl_nw(HF, 1)) void k_flash_fwd(
     const bf16x8* __restrict__ Hk, const bf16x8* __restrict__ Wk, const bf16x8* __restrict__ Wr,
     const float* __restrict__ bias_pad, int B, int A, int nrb, int nsplit, int cps, float* __restrict__ pm,
@@ -198,9 +198,12 @@ __global__ __launch_bounds__(64 * fl_nw(HF, 1)) void k_flash_fwd(
   // chunk-major; inside, the 16×16 quadrant (ib, rb), then this kernel's
   // accumulator order, lane-linear: each lane stores its four logits of a
   // quadrant as one 16-B store (whole 1 KB per instruction; pass 2 transposes
-  // through LDS).  (HF <= 128: at HF 256 the wave's registers are full,
-  // rg_flash_fwd_top refuses zs)
-  float* __restrict__ zrow = (HF <= 128 && NG > 0 && zs) ? zs + (int64_t)(r0 >> 5) * 1024 + 4 * lane : nullptr;
+  // through LDS).  ZS: HF <= 128 (at HF 256 the wave's registers are full),
+  // launched by rg_flash_fwd_top only for B % 256 == 0, so every wave is
+  // active and its four stores per chunk are unconditional — the compiler then
+  // counts them exactly against the barrier's vmcnt(4)
+  static_assert(!ZS || (HF <= 128 && NG > 0), "stored logits: HF <= 128, training pass");
+  float* __restrict__ zrow = ZS ? zs + (int64_t)(r0 >> 5) * 1024 + 4 * lane : nullptr;
   const int nch = max(0, min(nct, c0 + cps) - c0);
 #define FL_ISSUE_K(C, SK, SB)                                                  \
   do {                                                                         \
@@ -271,9 +274,14 @@ __global__ __launch_bounds__(64 * fl_nw(HF, 1)) void k_flash_fwd(
 #pragma unroll
       for (int ib = 0; ib < 2; ++ib) {
         const f4 bq = *reinterpret_cast<const f4*>(&sb[16 * ib + 4 * kg]);
-        if (HF <= 128 && NG > 0 && zrow)
+        if constexpr (ZS) {
+#ifdef ZS_PLAIN_STORE
+          *reinterpret_cast<f4*>(zrow + (int64_t)(c0 + c) * (B / 32) * 1024 + (2 * ib + rb) * 256) = sa[ib][rb] + bq;
+#else
           __builtin_nontemporal_store(sa[ib][rb] + bq, reinterpret_cast<f4*>(zrow + (int64_t)(c0 + c) * (B / 32) * 1024 +
                                                                             (2 * ib + rb) * 256));
+#endif
+        }
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
           const float z = sa[ib][rb][u] + bq[u];
@@ -330,6 +338,18 @@ __global__ __launch_bounds__(64 * fl_nw(HF, 1)) void k_flash_fwd(
       }
     }
   };
+  // chunk barrier; a wave storing logits waits for the ring's DMA only
+  // (issued before the chunk's four z stores: vmcnt(4)), not for its stores'
+  // write acknowledgements (a full vmcnt(0) here cost pass 1 ~0.7 µs per chunk)
+  auto csync = [&]() __attribute__((always_inline)) {
+    if constexpr (ZS) {
+      __builtin_amdgcn_s_waitcnt((4 & 15) | 0x70);   // vmcnt(4) lgkmcnt(0)
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+    } else {
+      FL_SYNC();
+    }
+  };
   for (int c = 0; c < nch; c += 2) {
     bf16x8 q0[2], q1[2], q2[2];
     if (DR || NG == 0) {
@@ -338,22 +358,22 @@ __global__ __launch_bounds__(64 * fl_nw(HF, 1)) void k_flash_fwd(
         FL_ISSUE_R(c0 + c + 1, sr1);
       }
       __builtin_amdgcn_sched_barrier(0);   // keep the prefetch at the top
-      if (active) {
+      if (ZS || active) {
         spart(sk0, sb0, c, q0, q1, q2);
         opart(sr0, q0, q1, q2);
       }
-      FL_SYNC();
+      csync();
       if (c + 1 < nch) {
         if (c + 2 < nch) {
           FL_ISSUE_K(c0 + c + 2, sk0, sb0);
           FL_ISSUE_R(c0 + c + 2, sr0);
         }
         __builtin_amdgcn_sched_barrier(0);
-        if (active) {
+        if (ZS || active) {
           spart(sk1, sb1, c + 1, q0, q1, q2);
           opart(sr1, q0, q1, q2);
         }
-        FL_SYNC();
+        csync();
       }
     } else {
       // single R buffer: R(c) was issued after the previous chunk's O-part
@@ -698,6 +718,7 @@ __global__ __launch_bounds__(64 * fl_nw(HF, 2)) void k_flash_dw(
   // ZL: per-wave 1 KB for the z tile transposes (its own array, so the
   // compiler's LDS-DMA tracking sees it never aliases the ring)
   __shared__ __attribute__((aligned(16))) float ztr_s[ZL ? 256 * NW : 1];
+  __shared__ __attribute__((aligned(16))) float2 si2[ZL ? 32 : 1];   // ZL: third row-record slot
 #if defined(FL2_RING3) || defined(FL2_LATE)
   // third ring slot (HF <= 128: 3 × 48 KB): chunk c + 2 is prefetched while c
   // computes, and a chunk's barrier waits only for its own DMA (vmcnt), not
@@ -733,6 +754,7 @@ __global__ __launch_bounds__(64 * fl_nw(HF, 2)) void k_flash_dw(
   } while (0)
   if constexpr (ZL) {
     FL_ISSUE_Z(0, sk0, si0);
+    if (w == 0 && lane < 16) blds16(rsrc_of(rowinfo + 32 * max(0, min(1, nch - 1))), si1, lane16, 0);
   } else {
     FL_ISSUE_K(0, sk0, si0);
     FL_ISSUE_R(0, sr0);
@@ -779,6 +801,7 @@ __global__ __launch_bounds__(64 * fl_nw(HF, 2)) void k_flash_dw(
     if (nch > 0) {
       zload(0, za);
       zload(1, zb);
+      zload(2, zc);
     }
   }
   __syncthreads();
@@ -786,8 +809,8 @@ __global__ __launch_bounds__(64 * fl_nw(HF, 2)) void k_flash_dw(
   // dZ = g·(2^((S + b)·log2e − lse·log2e) − onehot) from the chunk's S tiles
   // (ZL: z = S + b, bj = 0), db; dZᵀ planes (q*[ib]: the A operand of dW, k
   // over the chunk's rows in kperm16 order)
-  auto dzpart = [&](f4 (&sa)[2][2], const float2* si, bf16x8 (&q0)[2], bf16x8 (&q1)[2], bf16x8 (&q2)[2])
-                    __attribute__((always_inline)) {
+  auto dzpart = [&](f4 (&sa)[2][2], const float2* si, bf16x8 (&q0)[2], bf16x8 (&q1)[2], bf16x8 (&q2)[2],
+                    bool add_db = true) __attribute__((always_inline)) {
 #pragma unroll
     for (int ib = 0; ib < 2; ++ib) {
       const int item = j0 + 16 * ib + l16;
@@ -807,7 +830,7 @@ __global__ __launch_bounds__(64 * fl_nw(HF, 2)) void k_flash_dw(
           cdb += p;
         }
       }
-      dbs[ib] += cdb;
+      dbs[ib] += add_db ? cdb : 0.f;
       split3x8(sa[0][ib], sa[1][ib], q0[ib], q1[ib], q2[ib]);
     }
     FL2_MARK(2);
@@ -963,6 +986,9 @@ __global__ __launch_bounds__(64 * fl_nw(HF, 2)) void k_flash_dw(
     // covers 64 distinct banks), read back as 16 B at (l16 & 3)·64 + (l16 >> 2)·16 + 4kg
     float* ztr = ztr_s + 256 * w;
     auto ztrans = [&](f4 (&d)[2][2]) __attribute__((always_inline)) {
+#ifdef ZS_NO_TRANS
+      return;   // diagnostic build: the transposes' cost (results wrong)
+#endif
 #pragma unroll
       for (int rb = 0; rb < 2; ++rb)
 #pragma unroll
@@ -972,24 +998,61 @@ __global__ __launch_bounds__(64 * fl_nw(HF, 2)) void k_flash_dw(
           d[rb][ib] = *reinterpret_cast<const f4*>(ztr + (l16 & 3) * 64 + (l16 >> 2) * 16 + 4 * kg);
         }
     };
-    // step c: issue chunk c + 1's ring DMA, then z(c + 2) into the buffer chunk
-    // c − 1 used; compute c; barrier once chunk c + 1's DMA (and z(c + 1),
-    // issued a step earlier) landed — only z(c + 2)'s four loads may be in flight.
-    // Branch-free (a wave past A computes on item block 0's tiles and never
-    // stores; past the last chunk the DMA / loads repeat the last chunk into
-    // idle buffers), and slots / buffers are static per call site — unrolled by
-    // 6 — so the compiler's LDS-DMA tracking only orders reads of a slot behind
-    // its own DMA and its wait counting matches the explicit vmcnt(4)
-    auto step = [&](int c, f4 (&zcur)[2][2], f4 (&zn2)[2][2], const bf16x8* skc, const float2* sic, bf16x8* skn,
-                    float2* sin) __attribute__((always_inline)) {
-      ztrans(zcur);   // first: no DMA is in flight yet, so its LDS writes wait for nothing
+    // Software-pipelined by one chunk: step c runs chunk c + 1's transpose and
+    // dZ VALU (z tile in registers, row records in a three-slot ring) beside
+    // chunk c's W-part MFMAs, whose dZ planes the previous step made — the two
+    // are independent, so a wave's softmax no longer idles the MFMA pipe.
+    // Step c issues chunk c + 1's R-plane DMA (two-slot ring), chunk c + 2's
+    // row records and z(c + 3) (three register buffers); its barrier waits
+    // for everything but those four z loads (vmcnt(4)).  Branch-free (a wave
+    // past A computes on item block 0's tiles and never stores; past the last
+    // chunk the DMA / loads repeat the last chunk into idle slots), and slots /
+    // buffers are static per call site — unrolled by 6 — so the compiler's
+    // LDS-DMA tracking orders reads of a slot behind its own DMA only.
+    // the W-part with chunk c + 1's dZ VALU woven into its MFMA stream: per
+    // feature block 3 LDS reads, then each of its 12 MFMAs followed by up to
+    // two VALU instructions (no sched barriers inside, unlike wpart)
+    auto wpart_il = [&](const bf16x8* sr, const bf16x8 (&q0)[2], const bf16x8 (&q1)[2], const bf16x8 (&q2)[2])
+                        __attribute__((always_inline)) {
+      bf16x8 b0 = sr[lane], b1 = sr[64 + lane], b2 = sr[128 + lane];
+#pragma unroll
+      for (int fb = 0; fb < NF; ++fb) {
+        const int en = (fb + 1 < NF ? fb + 1 : fb) * 192 + lane;
+        const bf16x8 n0 = sr[en], n1 = sr[en + 64], n2 = sr[en + 128];
+#pragma unroll
+        for (int ib = 0; ib < 2; ++ib) dw[ib][fb] = mfma16_split<NT>(q0[ib], q1[ib], q2[ib], b0, b1, b2, dw[ib][fb]);
+        b0 = n0;
+        b1 = n1;
+        b2 = n2;
+      }
+#pragma unroll
+      for (int fb = 0; fb < NF; ++fb) {
+        __builtin_amdgcn_sched_group_barrier(0x0100, 3, 0);
+#pragma unroll
+        for (int m = 0; m < 2 * NT; ++m) {
+          __builtin_amdgcn_sched_group_barrier(0x0008, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x0002, 2, 0);
+        }
+      }
+    };
+    bf16x8 qa0[2], qa1[2], qa2[2], qb0[2], qb1[2], qb2[2];
+    if (nch > 0) {
+      ztrans(za);
+      dzpart(za, si0, qa0, qa1, qa2);
+    }
+    auto step = [&](int c, f4 (&zn1)[2][2], f4 (&zn3)[2][2], const bf16x8* rcur, bf16x8* rnext,
+                    const float2* sin1, float2* sin2, const bf16x8 (&qc0)[2], const bf16x8 (&qc1)[2],
+                    const bf16x8 (&qc2)[2], bf16x8 (&qn0)[2], bf16x8 (&qn1)[2], bf16x8 (&qn2)[2])
+                    __attribute__((always_inline)) {
+      ztrans(zn1);   // z(c + 1) landed by the previous barrier; no DMA in flight yet
       __builtin_amdgcn_sched_barrier(0);
-      FL_ISSUE_Z(min(c + 1, nch - 1), skn, sin);
-      zload(c + 2, zn2);
+      stage<ER, NW>(Hr + (int64_t)min(c + 1, nch - 1) * ER, rnext, w, lane16);
+      if (w == 0 && lane < 16) blds16(rsrc_of(rowinfo + 32 * min(c + 2, nch - 1)), sin2, lane16, 0);
+      zload(c + 3, zn3);
       __builtin_amdgcn_sched_barrier(0);
-      bf16x8 q0[2], q1[2], q2[2];
-      dzpart(zcur, sic, q0, q1, q2);
-      wpart(skc, q0, q1, q2);
+      dzpart(zn1, sin1, qn0, qn1, qn2, c + 1 < nch);   // (past the last chunk: planes unused, no db)
+      wpart_il(rcur, qc0, qc1, qc2);
+      __builtin_amdgcn_sched_barrier(0);
       FL2_MARK(3);
       __builtin_amdgcn_s_waitcnt(sf2_wc_vm(4));
       __builtin_amdgcn_s_barrier();
@@ -997,12 +1060,12 @@ __global__ __launch_bounds__(64 * fl_nw(HF, 2)) void k_flash_dw(
       FL2_MARK(4);
     };
     for (int c = 0; c < nch; c += 6) {
-      step(c, za, zc, sk0, si0, sk1, si1);
-      if (c + 1 < nch) step(c + 1, zb, za, sk1, si1, sk0, si0);
-      if (c + 2 < nch) step(c + 2, zc, zb, sk0, si0, sk1, si1);
-      if (c + 3 < nch) step(c + 3, za, zc, sk1, si1, sk0, si0);
-      if (c + 4 < nch) step(c + 4, zb, za, sk0, si0, sk1, si1);
-      if (c + 5 < nch) step(c + 5, zc, zb, sk1, si1, sk0, si0);
+      step(c, zb, za, sk0, sk1, si1, si2, qa0, qa1, qa2, qb0, qb1, qb2);
+      if (c + 1 < nch) step(c + 1, zc, zb, sk1, sk0, si2, si0, qb0, qb1, qb2, qa0, qa1, qa2);
+      if (c + 2 < nch) step(c + 2, za, zc, sk0, sk1, si0, si1, qa0, qa1, qa2, qb0, qb1, qb2);
+      if (c + 3 < nch) step(c + 3, zb, za, sk1, sk0, si1, si2, qb0, qb1, qb2, qa0, qa1, qa2);
+      if (c + 4 < nch) step(c + 4, zc, zb, sk0, sk1, si2, si0, qa0, qa1, qa2, qb0, qb1, qb2);
+      if (c + 5 < nch) step(c + 5, za, zc, sk1, sk0, si0, si1, qb0, qb1, qb2, qa0, qa1, qa2);
     }
   } else
 #ifdef FL2_LATE
@@ -1689,21 +1752,27 @@ extern "C" int rg_flash_fwd_top(const void* Hk, const void* Wk, const void* Wr, 
   if (!flash_hf_ok(HF)) return RG_ERR_SHAPE;
   const bool arg = pbest != nullptr;
   if (arg != (parg != nullptr) || (cmax && !arg)) return RG_ERR_ARG;
-  if (zs && HF > 128) return RG_ERR_SHAPE;
+  const int rpb = fl_rows(HF, 1);
+  if (zs && (HF > 128 || B % rpb)) return RG_ERR_SHAPE;   // stored logits: HF <= 128, whole row blocks
   const int nct = (A + 31) / 32;
   const int cps = (nct + nsplit - 1) / nsplit;
-  const int rpb = fl_rows(HF, 1);
   const int nrb = (B + rpb - 1) / rpb;
   const dim3 grid((unsigned)(nrb * nsplit));
-#define FF(HFV, NTV, NGV, ARGV)                                                                              \
-  hipLaunchKernelGGL((k_flash_fwd<HFV, NTV, NGV, ARGV>), grid, dim3(64 * fl_nw(HFV, 1)), 0, stream,                \
+#define FF(HFV, NTV, NGV, ARGV, ZSV)                                                                          \
+  hipLaunchKernelGGL((k_flash_fwd<HFV, NTV, NGV, ARGV, ZSV>), grid, dim3(64 * fl_nw(HFV, 1)), 0, stream,           \
                      (const bf16x8*)Hk, (const bf16x8*)Wk, (const bf16x8*)Wr, bias_pad, B, A, nrb, nsplit, cps, pm, \
                      pl, pO, pbest, parg, cmax, zs)
-#define FA(HFV, NTV, NGV)     \
-  if (arg) {                  \
-    FF(HFV, NTV, NGV, true);  \
-  } else {                    \
-    FF(HFV, NTV, NGV, false); \
+#define FZ1(HFV, NTV, NGV, ARGV)            \
+  if (zs) {                                 \
+    FF(HFV, NTV, NGV, ARGV, (HFV <= 128));  \
+  } else {                                  \
+    FF(HFV, NTV, NGV, ARGV, false);         \
+  }
+#define FA(HFV, NTV, NGV)      \
+  if (arg) {                   \
+    FZ1(HFV, NTV, NGV, true);  \
+  } else {                     \
+    FZ1(HFV, NTV, NGV, false); \
   }
 #define FT(HFV)                        \
   if (terms == 9) {                    \
@@ -1720,6 +1789,7 @@ extern "C" int rg_flash_fwd_top(const void* Hk, const void* Wk, const void* Wr, 
     case 256: FT(256); break;
   }
 #undef FT
+#undef FZ1
 #undef FA
 #undef FF
   RG_LAUNCH_CHECK();

@@ -818,10 +818,11 @@ class SoftmaxHead:
 
     def zs_buffer(self, w):
         """The stored-logit buffer of workspace w, or None (recomputed in pass
-        2).  ``zstore``: None = auto (HF <= 128 and within ZSTORE_MAX_BYTES and
-        a third of the free device memory), True / False force it (tests)."""
+        2).  Needs HF <= 128 and B a multiple of pass 1's 256-row blocks.
+        ``zstore``: None = auto (within ZSTORE_MAX_BYTES and a third of the
+        free device memory), True / False force it (tests)."""
         mode = getattr(self, "zstore", None)
-        if mode is False or self.HF > 128:
+        if mode is False or self.HF > 128 or w.B % call("rg_flash_rows_per_block", self.HF):
             return None
         if w.zs is None:
             nb = int(call("rg_flash_zs_bytes", w.B, self.A))

@@ -168,8 +168,9 @@ int rg_flash_fwd(const void* Hk, const void* Wk, const void* Wr, const float* bi
  *   (every item re-scored the same way, canonical top-K): the result is exact for
  *   every row; err (optional) counts the rows scanned. */
 int rg_flash_rows_per_block(int HF);
-/* zs (optional, HF <= 128): pass 1 also stores the logits z = h·Wᵀ + b as rg_flash_zs_bytes(B, A)
- *   bytes of 32-item × 32-row tiles for rg_flash_dw_adam_planes (which then skips recomputing them). */
+/* zs (optional; HF <= 128 and B a multiple of rg_flash_rows_per_block(HF), else RG_ERR_SHAPE): pass 1
+ *   also stores the logits z = h·Wᵀ + b as rg_flash_zs_bytes(B, A) bytes of 32-item × 32-row tiles for
+ *   rg_flash_dw_adam_planes (which then skips recomputing them). */
 int rg_flash_fwd_top(const void* Hk, const void* Wk, const void* Wr, const float* bias_pad, int B, int A, int HF,
                      int terms, int nsplit, float* pm, float* pl, float* pO, float* pbest, int32_t* parg, float* cmax,
                      float* zs, rg_stream_t stream);

@@ -212,8 +212,8 @@ def test_flash_head_matches_fp64(precision, B, A, HF, nsplit):
 
 
 @pytest.mark.parametrize("precision", ["f32x6", "f32x6d3"])
-@pytest.mark.parametrize("B,A,HF,nsplit", [(64, 1000, 32, 8), (128, 3001, 64, 16), (256, 4133, 128, 8),
-                                           (512, 2077, 128, 64), (96, 777, 128, 3), (288, 50000, 128, 16)])
+@pytest.mark.parametrize("B,A,HF,nsplit", [(256, 1000, 32, 8), (256, 3001, 64, 16), (256, 4133, 128, 8),
+                                           (512, 2077, 128, 64), (768, 777, 128, 3), (512, 50000, 128, 16)])
 def test_stored_logits_match_fp64(precision, B, A, HF, nsplit):
     """Stored-logit head (zs): pass 1 writes z = h·Wᵀ + b tile by tile, pass 2
     reads it instead of recomputing the S contraction.  The stored logits
@@ -237,9 +237,12 @@ def test_stored_logits_match_fp64(precision, B, A, HF, nsplit):
     torch.testing.assert_close(o["db"], o2["db"], rtol=0, atol=2e-8)
 
 
-def test_stored_logits_refused_at_hf256():
+@pytest.mark.parametrize("B,HF", [(256, 256), (96, 64), (288, 128)])
+def test_stored_logits_refused_shapes(B, HF):
+    """Stored logits need HF <= 128 and whole 256-row pass-1 blocks (the
+    trainers then recompute in pass 2)."""
     call = C().call
-    B, A, HF = 64, 1000, 256
+    A = 1000
     z = torch.empty(call("rg_flash_zs_bytes", B, A) // 4, device=dev)
     x = torch.empty(16, device=dev)
     with pytest.raises(RuntimeError, match="status -3"):   # RG_ERR_SHAPE, nothing launched
@@ -247,7 +250,7 @@ def test_stored_logits_refused_at_hf256():
              x.data_ptr(), x.data_ptr(), None, None, None, z.data_ptr(), C().stream_ptr())
 
 
-@pytest.mark.parametrize("B,A,HF", [(96, 78341, 64), (64, 70000, 128)])
+@pytest.mark.parametrize("B,A,HF", [(256, 78341, 64), (512, 70000, 128)])
 def test_stored_logits_tail_split_adam(B, A, HF):
     """Stored logits through the trainer's pass 2 (Adam + next planes, the
     leftover item blocks split over the row chunks): W / b / moments and the
