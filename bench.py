@@ -406,8 +406,11 @@ def head_roofline(kern, precision, B, N, E, zs=False):
     traffic = None
     pmc = os.path.join(HERE, "profiles", "pmc_traffic.json")
     if os.path.exists(pmc) and (B, N, E) == (BATCH, ITEMS, DIM):   # the PMC passes ran at the C2 shapes
-        tab = json.load(open(pmc))   # the round-3 (16x16x32 head) measurement where there is one
-        traffic = tab.get(f"{dom}:{precision}:r03", tab.get(f"{dom}:{precision}")) if terms else tab.get(dom)
+        tab = json.load(open(pmc))
+        if zs and terms:   # the stored-logit head's passes (round 4, tools/pmc_head.sh with ZS=1)
+            traffic = tab.get(f"{dom}:{precision}:zs")
+        else:   # the round-3 (16x16x32 head) measurement where there is one
+            traffic = tab.get(f"{dom}:{precision}:r03", tab.get(f"{dom}:{precision}")) if terms else tab.get(dom)
     elif os.path.exists(pmc) and (B, N, E) == (8192, 5_000_000, 256) and terms:   # ... and at C5 (r03g)
         traffic = json.load(open(pmc)).get(f"c5:{dom}:{precision}")
     if terms:

@@ -4,10 +4,11 @@
 # summarised per kernel as 2·FETCH_SIZE + WRITE_SIZE (KB -> bytes; MI355X_MICROARCH.md HBM section)
 set -e
 T=${TERMS:-636}
+Z=${ZS:+--zs}   # ZS=1: the stored-logit head (pass 1 stores z, pass 2 reads it)
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out/hpmc
-timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/hpmc/F -o f -- python3 tools/flashx.py --terms $T --iters 1 > gpurun_out/hpmc/F.log 2>&1
-timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/hpmc/W -o w -- python3 tools/flashx.py --terms $T --iters 1 > gpurun_out/hpmc/W.log 2>&1
+timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/hpmc/F -o f -- python3 tools/flashx.py --terms $T --iters 1 $Z > gpurun_out/hpmc/F.log 2>&1
+timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/hpmc/W -o w -- python3 tools/flashx.py --terms $T --iters 1 $Z > gpurun_out/hpmc/W.log 2>&1
 python3 - <<'PY'
 import csv, glob, collections
 def load(pat, ctr):
