@@ -1012,9 +1012,10 @@ __global__ __launch_bounds__(64 * fl_nw(HF, 2)) void k_flash_dw(
     // chunk the DMA / loads repeat the last chunk into idle slots), and slots /
     // buffers are static per call site — unrolled by 6 — so the compiler's
     // LDS-DMA tracking orders reads of a slot behind its own DMA only.
-    // the W-part with chunk c + 1's dZ VALU woven into its MFMA stream: per
-    // feature block 3 LDS reads, then each of its 12 MFMAs followed by up to
-    // two VALU instructions (no sched barriers inside, unlike wpart)
+    // the W-part with no sched barriers inside (unlike wpart), so the compiler
+    // weaves chunk c + 1's dZ VALU into its MFMA stream (explicit
+    // sched_group_barrier patterns — 1 MFMA + 2 VALU, 2 + 4, VALU front-loaded
+    // — measured 0.2–0.5 ms slower at C2, profiles/r05/flashx_pass2_interleave.txt)
     auto wpart_il = [&](const bf16x8* sr, const bf16x8 (&q0)[2], const bf16x8 (&q1)[2], const bf16x8 (&q2)[2])
                         __attribute__((always_inline)) {
       bf16x8 b0 = sr[lane], b1 = sr[64 + lane], b2 = sr[128 + lane];
@@ -1027,15 +1028,6 @@ __global__ __launch_bounds__(64 * fl_nw(HF, 2)) void k_flash_dw(
         b0 = n0;
         b1 = n1;
         b2 = n2;
-      }
-#pragma unroll
-      for (int fb = 0; fb < NF; ++fb) {
-        __builtin_amdgcn_sched_group_barrier(0x0100, 3, 0);
-#pragma unroll
-        for (int m = 0; m < 2 * NT; ++m) {
-          __builtin_amdgcn_sched_group_barrier(0x0008, 1, 0);
-          __builtin_amdgcn_sched_group_barrier(0x0002, 2, 0);
-        }
       }
     };
     bf16x8 qa0[2], qa1[2], qa2[2], qb0[2], qb1[2], qb2[2];
