@@ -360,11 +360,60 @@ def test_flash_trainer_matches_oracle(precision):
         lo = orc.step(s, a, ln)
         lg = tr.train_step(s, a, ln)
         assert abs(lo - lg) < 1e-4, (i, lo, lg)
+    assert tr.gru_model.heads["output"].stored_logits()   # B 1024, HF 128: the stored-logit head ran
     sd_o = orc.net.state_dict()
     for k, v in tr.gru_model.state_dict().items():
         d = (v.cpu() - sd_o[k]).abs()
         assert float(d.max()) <= 2 * cfg["learning_rate"] + 1e-5, k
         assert float((d > 1e-4).float().mean()) < 1e-3, (k, float((d > 1e-4).float().mean()))
+
+
+@pytest.mark.parametrize("kind", ["gru4rec", "smorl"])
+def test_stored_logit_trainer_equals_recomputing(kind):
+    """The trainers with stored logits (default where they fit) and with
+    pass 2 recomputing them (head.zstore = False) take the same steps (same
+    plane products, other accumulation order): losses within 1e-5, weights at
+    the training tolerances of the oracle tests (Adam's normalised step can
+    turn a last-bit difference of a near-zero gradient into up to 2·lr) —
+    GRU4Rec, and SMORL's supervised head (pass 1 with the top-k outputs and the
+    stored logits together)."""
+    import random
+    from recommenders.data_utils.synthetic import SessionStream
+    N, L, B, E = 20000, 12, 512, 64
+    cfg = dict(hidden_dim=E, embedding_dim=E, gru_layers=1, train_pad_embed=True, use_packed_seq=True,
+               learning_rate=0.005, item_num=N, state_size=L, action_dim=N)
+    st = SessionStream(N, L, B * 3, seed=13)
+    runs = []
+    for zstore in (None, False):
+        random.seed(3)
+        if kind == "gru4rec":
+            from recommenders.models.GRU4Rec.model import GRU4Rec_trainer
+            tr = GRU4Rec_trainer(device="cuda", **cfg)
+            nets, heads = (tr.gru_model,), [tr.gru_model.heads["output"]]
+        else:
+            from recommenders.models.SMORL.smorl_gru import SMORL_trainer
+            g = torch.Generator().manual_seed(7)
+            tr = SMORL_trainer(device="cuda", padding_pos="end", gamma=0.5, q_weights=[1.0, 0.5, 2.0], alpha=1.0,
+                               div_embedding=torch.randn(N + 1, 16, generator=g) * 0.01,
+                               unpopular_actions_set=set(range(0, N, 3)), topk_div=2, topk_nov=1, **cfg)
+            nets = (tr.SMORL_1, tr.SMORL_2)
+            heads = [n.sup_head_output for n in nets]
+        for hd in heads:
+            hd.zstore = zstore
+        losses = []
+        for i in range(3):
+            b = st.batch(i, B)
+            out = tr.train_step(b[0], b[1], b[4]) if kind == "gru4rec" else tr.train_step(*b)
+            losses.append(np.atleast_1d(np.array(out, dtype=np.float64)))
+        assert any(hd.stored_logits() for hd in heads) == (zstore is None)
+        runs.append((np.concatenate(losses), [{k: v.cpu() for k, v in n.state_dict().items()} for n in nets]))
+    np.testing.assert_allclose(runs[0][0], runs[1][0], rtol=0, atol=1e-5)
+    lr = cfg["learning_rate"]
+    for sd0, sd1 in zip(runs[0][1], runs[1][1]):
+        for k in sd0:
+            d = (sd0[k] - sd1[k]).abs()
+            assert float(d.max()) <= 2 * lr + 1e-5, k
+            assert float((d > 1e-4).float().mean()) < 1e-3, (k, float((d > 1e-4).float().mean()))
 
 
 def run_native(h, W, b, tgt):
