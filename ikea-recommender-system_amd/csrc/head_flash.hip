@@ -203,7 +203,12 @@ __global__ __launch_bounds__(64 * fl_nw(HF, 1)) void k_flash_fwd(
   // active and its four stores per chunk are unconditional — the compiler then
   // counts them exactly against the barrier's vmcnt(4)
   static_assert(!ZS || (HF <= 128 && NG > 0), "stored logits: HF <= 128, training pass");
-  float* __restrict__ zrow = ZS ? zs + (int64_t)(r0 >> 5) * 1024 + 4 * lane : nullptr;
+  // lane (kg, l16) stores its f4 at slot 16kg + 4(l16 >> 2) + ((l16 & 3) ^ kg) of
+  // the quadrant (a bijection: still 1 KB contiguous per instruction), so that
+  // pass 2, which DMAs the tile into LDS unchanged, reads it back transposed
+  // with conflict-free 4-B reads (zs_slot, k_flash_dw)
+  float* __restrict__ zrow =
+      ZS ? zs + (int64_t)(r0 >> 5) * 1024 + 4 * (16 * kg + 4 * (l16 >> 2) + ((l16 & 3) ^ kg)) : nullptr;
   const int nch = max(0, min(nct, c0 + cps) - c0);
 #define FL_ISSUE_K(C, SK, SB)                                                  \
   do {                                                                         \
@@ -719,11 +724,13 @@ __global__ __launch_bounds__(64 * fl_nw(HF, 2)) void k_flash_dw(
   constexpr int EK = NS * 2 * 192;
   constexpr int ER = NF * 192;
   __shared__ bf16x8 sk0[EK], sk1[EK];
-  __shared__ bf16x8 sr0[ER], sr1[DR ? ER : 1];
+  __shared__ bf16x8 sr0[ZL ? 1 : ER], sr1[(DR && !ZL) ? ER : 1];   // (ZL: h's R-planes ring in sk0 / sk1)
   __shared__ __attribute__((aligned(16))) float2 si0[32], si1[32];
-  // ZL: per-wave 1 KB for the z tile transposes (its own array, so the
-  // compiler's LDS-DMA tracking sees it never aliases the ring)
-  __shared__ __attribute__((aligned(16))) float ztr_s[ZL ? 256 * NW : 1];
+  // ZL: three-slot ring of the waves' z tiles (4 KB per wave and slot, DMA'd
+  // straight from pass 1's store; separate arrays, so the compiler's LDS-DMA
+  // tracking orders reads of a slot behind its own DMA only)
+  __shared__ __attribute__((aligned(16))) float zr0[ZL ? 1024 * NW : 1], zr1[ZL ? 1024 * NW : 1],
+      zr2[ZL ? 1024 * NW : 1];
   __shared__ __attribute__((aligned(16))) float2 si2[ZL ? 32 : 1];   // ZL: third row-record slot
 #if defined(FL2_RING3) || defined(FL2_LATE)
   // third ring slot (HF <= 128: 3 × 48 KB): chunk c + 2 is prefetched while c
@@ -786,28 +793,22 @@ __global__ __launch_bounds__(64 * fl_nw(HF, 2)) void k_flash_dw(
   for (int ib = 0; ib < 2; ++ib)
 #pragma unroll
     for (int fb = 0; fb < NF; ++fb) dw[ib][fb] = f4{0.f, 0.f, 0.f, 0.f};
-  // ZL: this wave's z tiles (item block j0 / 32, row chunks from cb), 16 B
-  // per lane and quadrant, as pass 1 stored them
-  // (branch-free: a wave past A reads item block 0's tiles, a chunk index past
-  // the range re-reads the last chunk — neither result is used — so the
-  // compiler's wait counting sees the same four loads on every path)
-  const float* __restrict__ zt =
-      ZL ? zs + ((int64_t)(active ? j0 >> 5 : 0) * (B / 32) + cb) * 1024 + 4 * lane : nullptr;
-  auto zload = [&](int c, f4 (&d)[2][2]) __attribute__((always_inline)) {
-    const int cc = min(c, nch - 1);
+  // ZL: this wave's z tiles (item block j0 / 32, row chunks from cb), DMA'd
+  // 1 KB per quadrant into the wave's 4 KB of a ring slot (branch-free: a
+  // wave past A reads item block 0's tiles, a chunk index past the range
+  // re-reads the last chunk — neither result is used — so every step issues
+  // the same four DMA ops)
+  const float* __restrict__ zt = ZL ? zs + ((int64_t)(active ? j0 >> 5 : 0) * (B / 32) + cb) * 1024 : nullptr;
+  auto zdma = [&](int c, float* slot) __attribute__((always_inline)) {
+    const __amdgpu_buffer_rsrc_t r = rsrc_of(zt + (int64_t)min(c, nch - 1) * 1024);
 #pragma unroll
-    for (int rb = 0; rb < 2; ++rb)
-#pragma unroll
-      for (int ib = 0; ib < 2; ++ib)
-        d[rb][ib] =
-            __builtin_nontemporal_load(reinterpret_cast<const f4*>(zt + (int64_t)cc * 1024 + (2 * ib + rb) * 256));
+    for (int q = 0; q < 4; ++q) blds16(r, slot + 1024 * w + 256 * q, lane16, 1024 * q);
   };
-  f4 za[2][2], zb[2][2], zc[2][2];
   if constexpr (ZL) {
     if (nch > 0) {
-      zload(0, za);
-      zload(1, zb);
-      zload(2, zc);
+      zdma(0, zr0);
+      zdma(1, zr1);
+      zdma(2, zr2);
     }
   }
   __syncthreads();
@@ -987,19 +988,18 @@ __global__ __launch_bounds__(64 * fl_nw(HF, 2)) void k_flash_dw(
   } while (0)
 #endif
   if constexpr (ZL) {
-    // pass 1's quadrant (item 4kg + u, row l16) -> (rows 4kg + r, item l16):
-    // value u of lane (kg, l16) at u·64 + kg·16 + l16 (each write instruction
-    // covers 64 distinct banks), read back as 16 B at (l16 & 3)·64 + (l16 >> 2)·16 + 4kg
-    float* ztr = ztr_s + 256 * w;
-    auto ztrans = [&](f4 (&d)[2][2]) __attribute__((always_inline)) {
+    // pass 1's quadrant value (item 4a + u, row b) sits at 4·(16a + 4(b >> 2) +
+    // ((b & 3) ^ a)) + u; this lane (kg, l16) needs rows 4kg + r of item l16
+    // (a = l16 >> 2, u = l16 & 3): four 4-B reads per quadrant, each
+    // instruction over 64 distinct banks
+    auto zread = [&](const float* slot, f4 (&d)[2][2]) __attribute__((always_inline)) {
+      const float* zb = slot + 1024 * w + 64 * (l16 >> 2) + 16 * kg + (l16 & 3);
 #pragma unroll
       for (int rb = 0; rb < 2; ++rb)
 #pragma unroll
-        for (int ib = 0; ib < 2; ++ib) {
+        for (int ib = 0; ib < 2; ++ib)
 #pragma unroll
-          for (int u = 0; u < 4; ++u) ztr[u * 64 + kg * 16 + l16] = d[rb][ib][u];
-          d[rb][ib] = *reinterpret_cast<const f4*>(ztr + (l16 & 3) * 64 + (l16 >> 2) * 16 + 4 * kg);
-        }
+          for (int r = 0; r < 4; ++r) d[rb][ib][r] = zb[256 * (2 * ib + rb) + 4 * (r ^ (l16 >> 2))];
     };
     // Software-pipelined by one chunk: step c runs chunk c + 1's transpose and
     // dZ VALU (z tile in registers, row records in a three-slot ring) beside
@@ -1032,20 +1032,22 @@ __global__ __launch_bounds__(64 * fl_nw(HF, 2)) void k_flash_dw(
     };
     bf16x8 qa0[2], qa1[2], qa2[2], qb0[2], qb1[2], qb2[2];
     if (nch > 0) {
-      ztrans(za);
-      dzpart(za, si0, qa0, qa1, qa2);
+      f4 z0[2][2];
+      zread(zr0, z0);
+      dzpart(z0, si0, qa0, qa1, qa2);
     }
-    auto step = [&](int c, f4 (&zn1)[2][2], f4 (&zn3)[2][2], const bf16x8* rcur, bf16x8* rnext,
+    auto step = [&](int c, const float* zn1, float* zn3, const bf16x8* rcur, bf16x8* rnext,
                     const float2* sin1, float2* sin2, const bf16x8 (&qc0)[2], const bf16x8 (&qc1)[2],
                     const bf16x8 (&qc2)[2], bf16x8 (&qn0)[2], bf16x8 (&qn1)[2], bf16x8 (&qn2)[2])
                     __attribute__((always_inline)) {
-      ztrans(zn1);   // z(c + 1) landed by the previous barrier; no DMA in flight yet
+      f4 z1[2][2];
+      zread(zn1, z1);   // z(c + 1) landed by the previous barrier; no DMA in flight yet
       __builtin_amdgcn_sched_barrier(0);
       stage<ER, NW>(Hr + (int64_t)min(c + 1, nch - 1) * ER, rnext, w, lane16);
       if (w == 0 && lane < 16) blds16(rsrc_of(rowinfo + 32 * min(c + 2, nch - 1)), sin2, lane16, 0);
-      zload(c + 3, zn3);
+      zdma(c + 3, zn3);
       __builtin_amdgcn_sched_barrier(0);
-      dzpart(zn1, sin1, qn0, qn1, qn2, c + 1 < nch);   // (past the last chunk: planes unused, no db)
+      dzpart(z1, sin1, qn0, qn1, qn2, c + 1 < nch);   // (past the last chunk: planes unused, no db)
       wpart_il(rcur, qc0, qc1, qc2);
       __builtin_amdgcn_sched_barrier(0);
       FL2_MARK(3);
@@ -1054,14 +1056,22 @@ __global__ __launch_bounds__(64 * fl_nw(HF, 2)) void k_flash_dw(
       __builtin_amdgcn_sched_barrier(0);
       FL2_MARK(4);
     };
-    for (int c = 0; c < nch; c += 6) {
-      step(c, zb, za, sk0, sk1, si1, si2, qa0, qa1, qa2, qb0, qb1, qb2);
-      if (c + 1 < nch) step(c + 1, zc, zb, sk1, sk0, si2, si0, qb0, qb1, qb2, qa0, qa1, qa2);
-      if (c + 2 < nch) step(c + 2, za, zc, sk0, sk1, si0, si1, qa0, qa1, qa2, qb0, qb1, qb2);
-      if (c + 3 < nch) step(c + 3, zb, za, sk1, sk0, si1, si2, qb0, qb1, qb2, qa0, qa1, qa2);
-      if (c + 4 < nch) step(c + 4, zc, zb, sk0, sk1, si2, si0, qa0, qa1, qa2, qb0, qb1, qb2);
-      if (c + 5 < nch) step(c + 5, za, zc, sk1, sk0, si0, si1, qb0, qb1, qb2, qa0, qa1, qa2);
+    // whole groups of six steps unguarded (straight-line, so the compiler's
+    // wait counting across the loop's back edge stays exact), then the rest
+    int c = 0;
+    for (; c + 6 <= nch; c += 6) {
+      step(c, zr1, zr0, sk0, sk1, si1, si2, qa0, qa1, qa2, qb0, qb1, qb2);
+      step(c + 1, zr2, zr1, sk1, sk0, si2, si0, qb0, qb1, qb2, qa0, qa1, qa2);
+      step(c + 2, zr0, zr2, sk0, sk1, si0, si1, qa0, qa1, qa2, qb0, qb1, qb2);
+      step(c + 3, zr1, zr0, sk1, sk0, si1, si2, qb0, qb1, qb2, qa0, qa1, qa2);
+      step(c + 4, zr2, zr1, sk0, sk1, si2, si0, qa0, qa1, qa2, qb0, qb1, qb2);
+      step(c + 5, zr0, zr2, sk1, sk0, si0, si1, qb0, qb1, qb2, qa0, qa1, qa2);
     }
+    if (c < nch) step(c, zr1, zr0, sk0, sk1, si1, si2, qa0, qa1, qa2, qb0, qb1, qb2);
+    if (c + 1 < nch) step(c + 1, zr2, zr1, sk1, sk0, si2, si0, qb0, qb1, qb2, qa0, qa1, qa2);
+    if (c + 2 < nch) step(c + 2, zr0, zr2, sk0, sk1, si0, si1, qa0, qa1, qa2, qb0, qb1, qb2);
+    if (c + 3 < nch) step(c + 3, zr1, zr0, sk1, sk0, si1, si2, qb0, qb1, qb2, qa0, qa1, qa2);
+    if (c + 4 < nch) step(c + 4, zr2, zr1, sk0, sk1, si2, si0, qa0, qa1, qa2, qb0, qb1, qb2);
   } else
 #ifdef FL2_LATE
   if constexpr (HF == 128) {
@@ -1197,9 +1207,11 @@ __global__ __launch_bounds__(64 * fl_nw(HF, 2)) void k_flash_dw(
   // too small, so it has its own)
   constexpr int TRP = 36, TRW = 32 * TRP;         // floats per wave (16-B aligned rows)
   constexpr int WPA = EK * 16 / (TRW * 4);        // waves per ring array
-  __shared__ __attribute__((aligned(16))) float trd[HF == 32 ? NW * TRW : 4];
+  __shared__ __attribute__((aligned(16))) float trd[(HF == 32 && !ZL) ? NW * TRW : 4];
   float* tr;
-  if (HF == 32) {
+  if constexpr (ZL) {
+    tr = (w < 4 ? zr0 : zr1) + (w & 3) * TRW;   // (the ring is idle after the last barrier)
+  } else if (HF == 32) {
     tr = trd + w * TRW;
   } else {
     const int ai = w / WPA, ao = (w % WPA) * TRW;

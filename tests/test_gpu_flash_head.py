@@ -78,11 +78,16 @@ def run_flash(h, W, b, tgt, terms, nsplit, lo=0, lse_global=None, A_full=None, z
 def zs_to_logits(zs, B, A):
     """(B, A) logits from the stored tiles (csrc/head_flash.hip k_flash_fwd: one
     1024-float tile per (32-item chunk, 32-row block), chunk-major; inside,
-    quadrant (item half ib, row half rb), then lane (kg, l16), then u: the
-    logit of item 16ib + 4kg + u, row 16rb + l16)."""
+    quadrant (item half ib, row half rb), then 16-B slot 16a + 4(b >> 2) +
+    ((b & 3) ^ a) holding the logits of items 16ib + 4a + u (u < 4), row
+    16rb + b)."""
     nct = (A + 31) // 32
-    t = zs.reshape(nct, B // 32, 2, 2, 4, 16, 4)            # chunk, row block, ib, rb, kg, l16, u
-    t = t.permute(1, 3, 5, 0, 2, 4, 6).reshape(B, nct * 32)   # row block, rb, l16 | chunk, ib, kg, u
+    t = zs.reshape(nct, B // 32, 2, 2, 64, 4)                # chunk, row block, ib, rb, slot, u
+    a = torch.arange(4).view(4, 1)
+    b = torch.arange(16).view(1, 16)
+    slot = 16 * a + 4 * (b >> 2) + ((b & 3) ^ a)              # (a, b) -> slot
+    t = t[:, :, :, :, slot.reshape(-1), :].reshape(nct, B // 32, 2, 2, 4, 16, 4)   # ..., a, b, u
+    t = t.permute(1, 3, 5, 0, 2, 4, 6).reshape(B, nct * 32)   # row block, rb, b | chunk, ib, a, u
     return t[:, :A]
 
 
