@@ -705,6 +705,9 @@ SCREEN_TOL = 1e-4
 SCREEN_CMAX_BYTES = 2 << 30
 SCREEN_ROW_CHUNK = 2048
 LOGIT_TERMS = {"f32x9": 9, "f32x6": 6, "f32x6d3": 6}
+# HIP stream priority of the fused head's pass 2 (its side stream, §4b of
+# DESIGN): pass 2 is the step's critical path, the trunk work beside it is not
+PASS2_STREAM_PRIORITY = 0
 # stored logits of the fused head (pass 1 writes z = S + b, pass 2 reads it
 # instead of recomputing the S contraction: 21 -> 15 bf16 plane-product terms
 # per step at f32x6d3): used while the buffer (ceil(A/32)·32 × B floats,
@@ -1025,7 +1028,7 @@ class SoftmaxHead:
         """Pass 2 on this head's side stream, ordered after everything issued so
         far; the head joins it on the next access of W / b or its workspace."""
         if getattr(self, "_side", None) is None:
-            self._side = torch.cuda.Stream(device=self.device)
+            self._side = torch.cuda.Stream(device=self.device, priority=PASS2_STREAM_PRIORITY)
         self._side.wait_stream(torch.cuda.current_stream(self.device))
         with torch.cuda.stream(self._side):
             self.flash_dw_adam(w, g, adam6)
