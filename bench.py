@@ -441,6 +441,13 @@ def head_roofline(kern, precision, B, N, E, zs=False):
                 out["other"] = mf
             else:
                 out["other"] = {k: hbm[k] for k in ("bound", "achieved", "peak", "unit", "frac", "bytes_per_launch")}
+        if "head_fwd" in kern and "head_dw_adam" in kern:   # the two passes together (the head's step share)
+            p1 = PASS_PRODUCTS[precision].get("head_fwd", 0) * flops_head
+            p2 = PASS_PRODUCTS[precision].get("head_dw_adam", 0) // (2 if zs else 1) * flops_head
+            tt = (kern["head_fwd"] + kern["head_dw_adam"]) * 1e-3
+            out["both_passes"] = {"ms": round(tt * 1e3, 4), "executed_bf16_TFLOP": round((p1 + p2) / 1e12, 3),
+                                  "achieved": round((p1 + p2) / tt / 1e12, 2), "unit": "TFLOP/s",
+                                  "frac": round((p1 + p2) / tt / 1e12 / BF16_MFMA_PEAK_TFLOPS, 4)}
         if dom == "head_dw_adam":
             out["note"] = ("pass 2 runs on a side stream beside the trunk backward (and, in the SMORL step, the "
                            "target and Q-head passes): its event time is the kernel's duration while sharing "
