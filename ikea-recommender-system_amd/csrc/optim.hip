@@ -131,16 +131,20 @@ __global__ void k_adam_rows1(float* __restrict__ P, float* __restrict__ M, float
 extern "C" int rg_adam_rows(float* P, float* M, float* V, float* G, const int32_t* tags, int32_t tag, int64_t rows,
                             int cols, const float* adam6, hipStream_t stream) {
   if (rows <= 0 || cols <= 0) return RG_ERR_ARG;
-  const int64_t n = (cols % 4 == 0) ? rows * (cols / 4) : rows * cols;
+  // the 16-B paths need 16-B aligned tables (torch allocations are; views at odd offsets take the scalar path)
+  const bool a16 = ((reinterpret_cast<uintptr_t>(P) | reinterpret_cast<uintptr_t>(M) | reinterpret_cast<uintptr_t>(V) |
+                     reinterpret_cast<uintptr_t>(G)) & 15) == 0;
+  const bool wide = cols % 4 == 0 && a16;
+  const int64_t n = wide ? rows * (cols / 4) : rows * cols;
   int blocks = (int)((n + 255) / 256);
   if (blocks > 32768) blocks = 32768;
-  if (cols % 4 == 0) {
+  if (wide) {
     const int c4n = cols / 4;
     const int sh = (c4n & (c4n - 1)) == 0 ? __builtin_ctz((unsigned)c4n) : -1;
     hipLaunchKernelGGL(k_adam_rows4, dim3(blocks), dim3(256), 0, stream, P, M, V, G, tags, tag, rows, cols, sh,
                        to_args(adam6));
   }
-  else if (cols == 1 && rows >= 4) {
+  else if (cols == 1 && rows >= 4 && a16 && (reinterpret_cast<uintptr_t>(tags) & 15) == 0) {
     const int64_t n4 = rows / 4, r4 = n4 * 4;
     int b4 = (int)((n4 + 255) / 256);
     if (b4 > 32768) b4 = 32768;

@@ -252,10 +252,12 @@ def test_head_forward_backward(B, A, HF):
     torch.testing.assert_close(db.cpu().double(), br.grad, rtol=0, atol=1e-7)
 
 
-@pytest.mark.parametrize("rows,cols", [(300, 16), (303, 1), (300, 1), (3, 1), (301, 3)])
-def test_adam_kernels_match_torch(rows, cols):
+@pytest.mark.parametrize("rows,cols,offset", [(300, 16, 0), (303, 1, 0), (300, 1, 0), (3, 1, 0), (301, 3, 0),
+                                             (300, 1, 1), (300, 16, 1)])
+def test_adam_kernels_match_torch(rows, cols, offset):
     """Row-sparse Adam: wide rows (f4), one-column tables (the heads' biases:
-    four rows per thread plus the tail), other widths (scalar)."""
+    four rows per thread plus the tail; offset 1: tensors not 16-B aligned take
+    the scalar path), other widths (scalar)."""
     from recommenders.hip.engine import AdamClock
     g = torch.Generator().manual_seed(5)
     p0 = torch.randn(rows, cols, generator=g)
@@ -263,11 +265,12 @@ def test_adam_kernels_match_torch(rows, cols):
     touched = [torch.rand(rows, generator=g) < 0.3 for _ in range(3)]
     pt = p0.clone().requires_grad_(True)
     opt = torch.optim.Adam([pt], lr=0.01)
-    P = p0.to(dev)
-    M = torch.zeros_like(P)
-    V = torch.zeros_like(P)
-    G = torch.zeros_like(P)
-    tags = torch.zeros(rows, dtype=torch.int32, device=dev)
+    P = torch.empty(rows * cols + offset, device=dev)[offset:].view(rows, cols)
+    P.copy_(p0)
+    M = torch.zeros(rows * cols + offset, device=dev)[offset:].view(rows, cols)
+    V = torch.zeros(rows * cols + offset, device=dev)[offset:].view(rows, cols)
+    G = torch.zeros(rows * cols + offset, device=dev)[offset:].view(rows, cols)
+    tags = torch.zeros(rows + offset, dtype=torch.int32, device=dev)[offset:]
     clock = AdamClock(0.01)
     for i in range(3):
         gi = grads[i] * touched[i].float().unsqueeze(1)
