@@ -166,7 +166,7 @@ def _cpu_run(cfg, items, dim, seq, B, steps, seed, warmup=1):
 
     def one(i):
         b = st.batch(i, B)
-        return orc.step(*b) if cfg == "c4" else orc.step(b[0], b[1], b[4])
+        return orc.step(*b) if cfg in ("c4", "c5") else orc.step(b[0], b[1], b[4])
     for i in range(warmup):
         one(i)
     times = []
@@ -178,7 +178,14 @@ def _cpu_run(cfg, items, dim, seq, B, steps, seed, warmup=1):
 
 
 CPU_NAMES = {"c2": "GRU4Rec", "c3": "BidirGRU4Rec (2048 shared sampled negatives, dropout 0)",
-             "c4": "SMORL_trainer (sup head + 3 Q heads, 3 rewards, topk 1)"}
+             "c4": "SMORL_trainer (sup head + 3 Q heads, 3 rewards, topk 1)",
+             "c5": "SMORL_trainer (sup head + 3 Q heads, 3 rewards, topk 1; fp32 item table as the reference)"}
+# C5's CPU sample ("Configs 4-5: CPU numbers ... single-process
+# restatement at a reduced batch, stated"): the full 5M x 256 tables of both
+# double-Q nets with their Adam moments and gradients (~200 GB) do not fit a
+# few-minute host run, so the sample keeps dim 256 and seq_len 100 at a tenth
+# of the items and batch 256
+C5_CPU_ITEMS, C5_CPU_BATCH = 500_000, 256
 
 
 def cpu_baseline(args, cfg="c2"):
@@ -187,26 +194,33 @@ def cpu_baseline(args, cfg="c2"):
     process may use (host_threads): the config's workload at its items, dims
     and seq_len — C2 at batch 4096 when the host RAM allows it (1
     warm-up + 3 timed steps), C3 at batch 4096 and C4 at batch
-    512 (2 timed steps each: one C4 step scores 1M items for the supervised
-    head and the Q target) — plus, with C2, the C1 line (BASELINE configs[0]:
+    512 (3 timed steps each: one C4 step scores 1M items for the supervised
+    head and the Q target), C5 at 500k items and batch 256 (dim 256, L <= 100,
+    2 timed steps; C5_CPU_ITEMS) — plus, with C2, the C1 line (BASELINE configs[0]:
     10k items, dim32, L<=20, batch 64, --c1-warmup + --c1-steps steps)."""
     threads, how = host_threads()
     torch.set_num_threads(threads)
     ram = host_ram_gib()
+    items = args.items
     if cfg == "c2":
         B = args.cpu_batch or (4096 if ram is not None and ram >= 96 else 512)
         steps = args.cpu_steps or (3 if B >= 4096 else 6)
+    elif cfg == "c5":
+        items = min(items, C5_CPU_ITEMS)
+        B = args.cpu_batch or C5_CPU_BATCH
+        steps = args.cpu_steps or 2
     else:
         B = args.cpu_batch or (4096 if cfg == "c3" else 512)
-        steps = args.cpu_steps or 2
-    times = _cpu_run(cfg, args.items, args.dim, args.seq, B, steps, 2)
+        steps = args.cpu_steps or 3
+    times = _cpu_run(cfg, items, args.dim, args.seq, B, steps, 2)
     dt = float(np.sum(times))
+    red = [x for x, full in (("items", items == args.items), ("batch", B == args.batch)) if not full]
     out = {"value": round(B * steps / dt, 2), "unit": "session-steps/sec", "cores": threads, "threads": how,
-           "cpu_model": cpu_model(), "host_ram_gib": ram, "kind": "port", "batch": B, "steps": steps,
+           "cpu_model": cpu_model(), "host_ram_gib": ram, "kind": "port", "batch": B, "items": items, "steps": steps,
            "median_ms_per_step": round(float(np.median(times)) * 1e3, 1),
-           "sample": (f"oracle (reference PyTorch-CPU math) {CPU_NAMES[cfg]} {args.items} items dim{args.dim} "
-                      f"L<={args.seq}, batch {B}{'' if B == args.batch else ' (reduced)'}, {steps} timed steps after "
-                      f"1 warm-up, torch.set_num_threads({threads}), {dt:.1f} s")}
+           "sample": (f"oracle (reference PyTorch-CPU math) {CPU_NAMES[cfg]} {items} items dim{args.dim} "
+                      f"L<={args.seq}, batch {B}{' (reduced ' + ' and '.join(red) + ')' if red else ''}, {steps} "
+                      f"timed steps after 1 warm-up, torch.set_num_threads({threads}), {dt:.1f} s")}
     if cfg == "c2" and args.c1_steps > 0:
         t1 = _cpu_run("c1", 10_000, 32, 20, 64, args.c1_steps, 1, warmup=args.c1_warmup)
         d1 = float(np.sum(t1))
@@ -288,12 +302,28 @@ def step_args(cfg, b):
     return (s, a, ln)
 
 
+def top_scanned(tr, reset=False):
+    """Rows whose exact top-k / argmax candidates overflowed the cap and were
+    scanned whole (engine.SoftmaxHead.top_scanned), summed over the trainer's
+    heads; reset zeroes the counters."""
+    n = 0
+    for name in ("gru_model", "SMORL_1", "SMORL_2", "DQN_1", "DQN_2"):
+        for h in getattr(getattr(tr, name, None), "heads", {}).values():
+            t = h.__dict__.get("_top_scanned")
+            if t is not None:
+                n += int(t.item())
+                if reset:
+                    t.zero_()
+    return n
+
+
 def timed_run(tr, batches, warmup, steps, world, kernel_timing, cfg):
     """W untimed steps, then K steps between barrier + synchronize; max over ranks.
     Batches are host (pinned) tensors: the H2D copy is inside every step."""
     from recommenders.hip.timing import KernelTimer, timing
     for i in range(warmup):
         tr.train_step(*step_args(cfg, batches[i]))
+    top_scanned(tr, reset=True)
     timer = KernelTimer()
     if world > 1:
         torch.distributed.barrier()
@@ -644,6 +674,7 @@ def main():
           f"{torch.cuda.memory_allocated(dev) / 2**30:.1f} GiB on the device", file=sys.stderr, flush=True)
     dt, losses, kern, per_step = timed_run(tr, batches, args.warmup, args.steps, world, not args.no_kernel_timing,
                                            args.config)
+    scanned = top_scanned(tr)   # over the timed steps (exact either way; each costs one whole-row scan)
     print(f"bench: peak device memory {torch.cuda.max_memory_allocated(dev) / 2**30:.1f} GiB", file=sys.stderr,
           flush=True)
     net = getattr(tr, "gru_model", None)
@@ -739,7 +770,7 @@ def main():
             torch.distributed.destroy_process_group()
         return
     cpu = None
-    if world == 1 and not args.no_cpu_baseline and args.config in ("c2", "c3", "c4"):
+    if world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args, args.config)
         if ev is not None and dev_idx is not None and parity_net is not None:
             cpu["hr_ndcg_parity"] = cpu_eval_parity(parity_net, held, dev_idx)
@@ -778,6 +809,7 @@ def main():
         "roofline": roof, "cpu_baseline": cpu, "north_star_target": target, "eval_heldout": ev,
         "harness": harness, "native_f32": native, "kernel_ms": kern,
         "loss_first_last": [round(losses[0], 5), round(losses[-1], 5)],
+        "top_scanned_rows": scanned,
     }
     os.write(json_fd, (json.dumps(line) + "\n").encode())
     if torch.distributed.is_initialized():

@@ -732,13 +732,6 @@ __global__ __launch_bounds__(64 * fl_nw(HF, 2)) void k_flash_dw(
   __shared__ __attribute__((aligned(16))) float zr0[ZL ? 1024 * NW : 1], zr1[ZL ? 1024 * NW : 1],
       zr2[ZL ? 1024 * NW : 1];
   __shared__ __attribute__((aligned(16))) float2 si2[ZL ? 32 : 1];   // ZL: third row-record slot
-#if defined(FL2_RING3) || defined(FL2_LATE)
-  // third ring slot (HF <= 128: 3 × 48 KB): chunk c + 2 is prefetched while c
-  // computes, and a chunk's barrier waits only for its own DMA (vmcnt), not
-  // for the prefetch issued in the same step
-  __shared__ bf16x8 sk2[HF == 128 ? EK : 1], sr2[HF == 128 ? ER : 1];
-  __shared__ __attribute__((aligned(16))) float2 si2[32];
-#endif
   const int tid = threadIdx.x, lane = tid & 63, kg = lane >> 4, l16 = lane & 15, lane16 = 16 * lane;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   FL2_DECL
@@ -884,109 +877,12 @@ __global__ __launch_bounds__(64 * fl_nw(HF, 2)) void k_flash_dw(
     }
     FL2_MARK(3);
   };
-#ifdef FL2_IBO
-  // Item-block-outer chunk body: the S-part of item block 0, then the S-part
-  // of block 1 with block 0's dZ VALU interleaved into its MFMAs, then block
-  // 0's W-part with block 1's dZ VALU interleaved, then block 1's W-part — so
-  // a wave's softmax runs under its own MFMAs instead of after all of them
-  // (the h fragments are read from LDS once per item block instead of once).
-  auto s_ib = [&](const bf16x8* sk, int ib, f4 (&sa)[2]) __attribute__((always_inline)) {
-    sa[0] = sa[1] = f4{0.f, 0.f, 0.f, 0.f};
-    bf16x8 a0 = sk[lane], a1 = sk[64 + lane], a2 = sk[128 + lane];
-#pragma unroll
-    for (int t = 0; t < 2 * NS; ++t) {
-      const int s = t >> 1, rb = t & 1;
-      const int en = (t + 1 < 2 * NS ? t + 1 : t) * 192 + lane;
-      const bf16x8 n0 = sk[en], n1 = sk[en + 64], n2 = sk[en + 128];
-      sa[rb] = mfma16_split<NT>(a0, a1, a2, wk[s][ib][0], wk[s][ib][1], wk[s][ib][2], sa[rb]);
-      a0 = n0;
-      a1 = n1;
-      a2 = n2;
-    }
-  };
-  auto valu_ib = [&](const float2* si, int ib, f4 (&sa)[2], bf16x8& q0, bf16x8& q1, bf16x8& q2)
-                     __attribute__((always_inline)) {
-    const int item = j0 + 16 * ib + l16;
-    float cdb = 0.f;
-#pragma unroll
-    for (int rb = 0; rb < 2; ++rb) {
-      const f4 i0 = *reinterpret_cast<const f4*>(&si[16 * rb + 4 * kg]);
-      const f4 i1 = *reinterpret_cast<const f4*>(&si[16 * rb + 4 * kg + 2]);
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const float lse2 = u < 2 ? i0[2 * u] : i1[2 * (u - 2)];
-        const int tb = __float_as_int(u < 2 ? i0[2 * u + 1] : i1[2 * (u - 2) + 1]);
-        const float e = __builtin_amdgcn_exp2f(fmaf(sa[rb][u] + bj[ib], L2E, -lse2));
-        const float p = g * (e - (tb == item ? 1.f : 0.f));
-        sa[rb][u] = p;
-        cdb += p;
-      }
-    }
-    dbs[ib] += cdb;
-    split3x8(sa[0], sa[1], q0, q1, q2);
-  };
-  auto w_ib = [&](const bf16x8* sr, int ib, const bf16x8& q0, const bf16x8& q1, const bf16x8& q2)
-                  __attribute__((always_inline)) {
-    bf16x8 b0 = sr[lane], b1 = sr[64 + lane], b2 = sr[128 + lane];
-#pragma unroll
-    for (int fb = 0; fb < NF; ++fb) {
-      const int en = (fb + 1 < NF ? fb + 1 : fb) * 192 + lane;
-      const bf16x8 n0 = sr[en], n1 = sr[en + 64], n2 = sr[en + 128];
-      dw[ib][fb] = mfma16_split<NT>(q0, q1, q2, b0, b1, b2, dw[ib][fb]);
-      b0 = n0;
-      b1 = n1;
-      b2 = n2;
-    }
-  };
-  // per step of an interleaved section: 3 LDS reads, then the step's 6 MFMAs
-  // each followed by up to 2 VALU instructions of the other item block's dZ
-  auto interleave = [&]() __attribute__((always_inline)) {
-#pragma unroll
-    for (int t = 0; t < 8; ++t) {
-      __builtin_amdgcn_sched_group_barrier(0x0100, 3, 0);
-#pragma unroll
-      for (int m = 0; m < 6; ++m) {
-        __builtin_amdgcn_sched_group_barrier(0x0008, 1, 0);
-        __builtin_amdgcn_sched_group_barrier(0x0002, 2, 0);
-      }
-    }
-  };
-  auto chunk_ibo = [&](const bf16x8* sk, const float2* si, const bf16x8* sr) __attribute__((always_inline)) {
-    f4 s0[2], s1[2];
-    bf16x8 qa0, qa1, qa2, qb0, qb1, qb2;
-    s_ib(sk, 0, s0);
-    __builtin_amdgcn_sched_barrier(0);
-    FL2_MARK(1);
-    s_ib(sk, 1, s1);
-    valu_ib(si, 0, s0, qa0, qa1, qa2);
-    interleave();
-    __builtin_amdgcn_sched_barrier(0);
-    FL2_MARK(2);
-    w_ib(sr, 0, qa0, qa1, qa2);
-    valu_ib(si, 1, s1, qb0, qb1, qb2);
-    interleave();
-    __builtin_amdgcn_sched_barrier(0);
-    w_ib(sr, 1, qb0, qb1, qb2);
-    __builtin_amdgcn_sched_barrier(0);
-  };
-#define FL2_CHUNK(SK, SI, SR)                           \
-  do {                                                  \
-    if constexpr (HF == 128) {                          \
-      chunk_ibo(SK, SI, SR);                            \
-    } else {                                            \
-      bf16x8 q0_[2], q1_[2], q2_[2];                    \
-      spart(SK, SI, q0_, q1_, q2_);                     \
-      wpart(SR, q0_, q1_, q2_);                         \
-    }                                                   \
-  } while (0)
-#else
 #define FL2_CHUNK(SK, SI, SR)      \
   do {                             \
     bf16x8 q0_[2], q1_[2], q2_[2]; \
     spart(SK, SI, q0_, q1_, q2_);  \
     wpart(SR, q0_, q1_, q2_);      \
   } while (0)
-#endif
   if constexpr (ZL) {
     // pass 1's quadrant value (item 4a + u, row b) sits at 4·(16a + 4(b >> 2) +
     // ((b & 3) ^ a)) + u; this lane (kg, l16) needs rows 4kg + r of item l16
@@ -1049,6 +945,10 @@ __global__ __launch_bounds__(64 * fl_nw(HF, 2)) void k_flash_dw(
       __builtin_amdgcn_sched_barrier(0);
       dzpart(z1, sin1, qn0, qn1, qn2, c + 1 < nch);   // (past the last chunk: planes unused, no db)
       wpart_il(rcur, qc0, qc1, qc2);
+#ifdef FL2_PIN
+#pragma unroll
+      for (int ib = 0; ib < 2; ++ib) asm volatile("" : "+v"(qn0[ib]), "+v"(qn1[ib]), "+v"(qn2[ib]), "+v"(dbs[ib]));
+#endif
       __builtin_amdgcn_sched_barrier(0);
       FL2_MARK(3);
       __builtin_amdgcn_s_waitcnt(sf2_wc_vm(4));
@@ -1059,6 +959,9 @@ __global__ __launch_bounds__(64 * fl_nw(HF, 2)) void k_flash_dw(
     // whole groups of six steps unguarded (straight-line, so the compiler's
     // wait counting across the loop's back edge stays exact), then the rest
     int c = 0;
+#ifdef FL2_PRIO
+    if (w >= 4) __builtin_amdgcn_s_setprio(1);
+#endif
     for (; c + 6 <= nch; c += 6) {
       step(c, zr1, zr0, sk0, sk1, si1, si2, qa0, qa1, qa2, qb0, qb1, qb2);
       step(c + 1, zr2, zr1, sk1, sk0, si2, si0, qb0, qb1, qb2, qa0, qa1, qa2);
@@ -1073,87 +976,6 @@ __global__ __launch_bounds__(64 * fl_nw(HF, 2)) void k_flash_dw(
     if (c + 3 < nch) step(c + 3, zr1, zr0, sk1, sk0, si1, si2, qb0, qb1, qb2, qa0, qa1, qa2);
     if (c + 4 < nch) step(c + 4, zr2, zr1, sk0, sk1, si2, si0, qa0, qa1, qa2, qb0, qb1, qb2);
   } else
-#ifdef FL2_LATE
-  if constexpr (HF == 128) {
-    // Waves 4-7 (each shares a SIMD with one of waves 0-3) run every chunk's
-    // W-part one chunk late, at the start of the next barrier interval, so
-    // their dZ VALU is not the tail of the interval that waves 0-3 wait out
-    // at the barrier.  Three ring slots: chunk c + 1 is prefetched into the
-    // slot of chunk c − 2, whose last reader (a late W-part) ran in the
-    // previous interval.
-    const bool late = w >= 4;
-    bf16x8 lq0[2], lq1[2], lq2[2];
-    auto slot_k = [&](int c) __attribute__((always_inline)) { return c % 3 == 0 ? sk0 : c % 3 == 1 ? sk1 : sk2; };
-    auto slot_r = [&](int c) __attribute__((always_inline)) { return c % 3 == 0 ? sr0 : c % 3 == 1 ? sr1 : sr2; };
-    auto slot_i = [&](int c) __attribute__((always_inline)) { return c % 3 == 0 ? si0 : c % 3 == 1 ? si1 : si2; };
-    for (int c = 0; c < nch; ++c) {
-      FL2_SYNC();   // chunk c landed (issued one interval ago); interval c − 1 done by every wave
-      if (c + 1 < nch) {
-        FL_ISSUE_K(c + 1, slot_k(c + 1), slot_i(c + 1));
-        FL_ISSUE_R(c + 1, slot_r(c + 1));
-      }
-      __builtin_amdgcn_sched_barrier(0);
-      if (active) {
-        if (late && c > 0) wpart(slot_r(c - 1), lq0, lq1, lq2);
-        bf16x8 q0[2], q1[2], q2[2];
-        spart(slot_k(c), slot_i(c), q0, q1, q2);
-        if (!late) {
-          wpart(slot_r(c), q0, q1, q2);
-        } else {
-#pragma unroll
-          for (int ib = 0; ib < 2; ++ib) {
-            lq0[ib] = q0[ib];
-            lq1[ib] = q1[ib];
-            lq2[ib] = q2[ib];
-          }
-        }
-      }
-    }
-    if (late && active && nch > 0) wpart(slot_r(nch - 1), lq0, lq1, lq2);
-    FL2_SYNC();   // the epilogue reuses the ring arrays
-  } else
-#endif
-#ifdef FL2_RING3
-  if constexpr (HF == 128) {
-    // step(c): chunk c's DMA landed (vmcnt: only chunk c + 1's, issued one
-    // step ago, may be outstanding: 6 ops per wave at HF 128 — 3 K- and 3
-    // R-plane DMAs; 7 on wave 0, which also waits for one of them) and every
-    // wave is done with chunk c − 1's slot -> prefetch c + 2 into it -> compute c
-    if (nch > 1) {
-      FL_ISSUE_K(1, sk1, si1);
-      FL_ISSUE_R(1, sr1);
-    }
-    auto step = [&](int c, const bf16x8* sk, const float2* si, const bf16x8* sr, bf16x8* pk, float2* pi,
-                    bf16x8* pr) __attribute__((always_inline)) {
-      FL2_MARK(3);
-      if (c + 1 < nch)
-        __builtin_amdgcn_s_waitcnt(0x0076);   // vmcnt(6) lgkmcnt(0)
-      else
-        __builtin_amdgcn_s_waitcnt(0x0070);   // vmcnt(0) lgkmcnt(0)
-      __builtin_amdgcn_s_barrier();
-      __builtin_amdgcn_sched_barrier(0);
-      FL2_MARK(4);
-      if (c + 2 < nch) {
-        FL_ISSUE_K(c + 2, pk, pi);
-        FL_ISSUE_R(c + 2, pr);
-      }
-      __builtin_amdgcn_sched_barrier(0);
-      if (active) {
-        bf16x8 q0[2], q1[2], q2[2];
-        spart(sk, si, q0, q1, q2);
-        wpart(sr, q0, q1, q2);
-      }
-    };
-    for (int c = 0; c < nch; c += 3) {
-      step(c, sk0, si0, sr0, sk2, si2, sr2);
-      if (c + 1 < nch) step(c + 1, sk1, si1, sr1, sk0, si0, sr0);
-      if (c + 2 < nch) step(c + 2, sk2, si2, sr2, sk1, si1, sr1);
-    }
-    FL2_MARK(3);
-    __syncthreads();   // the epilogue reuses the ring arrays
-    FL2_MARK(4);
-  } else
-#endif
   for (int c = 0; c < nch; c += 2) {
     bf16x8 q0[2], q1[2], q2[2];
     if (DR) {

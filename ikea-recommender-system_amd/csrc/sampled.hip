@@ -303,9 +303,7 @@ extern "C" int rg_head_fwd_xp(const void* hplanes, const float* W, const float* 
 // a per-wave stamp breakdown puts ~40% in the prologue (the W rows' fragment
 // loads) and the rest at ~2× the MFMA time — see DESIGN.md §4 for the
 // variants tried (plane-fed GEMM, LDS-DMA row images, sliced epilogues).
-#ifndef SF_NW
-#define SF_NW 8               // waves per workgroup (each 32 negatives) up to HF 128
-#endif
+constexpr int SF_NW = 8;   // waves per workgroup (each 32 negatives) up to HF 128
 // HF 256: a wave's 32 negatives are 192 VGPRs of operand planes plus 128 of
 // fp32 rows in flight, so one wave per SIMD (four per workgroup) and the
 // whole 512-entry register file
@@ -316,12 +314,7 @@ constexpr int sf_thr(int HF) { return 64 * sf_nw(HF); }   // threads per workgro
 // one workgroup fills a CU — the S = 2048, B = 4096 grid (16 × 16) is then
 // one round on 256 CUs and every wave splits its negatives' planes once for
 // eight h chunks instead of twice for four
-#ifndef SF_ROWS256
-#define SF_ROWS256 256
-#endif
-constexpr int sf_rows(int HF) { return HF == 256 ? SF_ROWS256 : 128; }
-// s_waitcnt immediate: vmcnt <= n (6 bits, split), expcnt free, lgkmcnt 0
-constexpr int sf_wc_vm(int n) { return (n & 15) | ((n >> 4) << 14) | 0x70; }
+constexpr int sf_rows(int HF) { return HF == 256 ? 256 : 128; }
 
 // Diagnostic build only (-DSF_STAMP, tools/sfstamp.py): per-wave s_memrealtime
 // stamps at the phase boundaries of k_sampled_logits, read back by rg_sf_stamp_read.
@@ -455,25 +448,9 @@ __global__ __launch_bounds__(sf_thr(HF)) void k_sampled_logits(const float* __re
     id = (A > 0 && (uint64_t)(int64_t)id >= A) ? 0 : id;   // guard the gather (callers validate ids)
   }
   const float bl = PRE ? bg[s_me] : bias[id];
-#ifdef SF_KOUT
-  // k-outer form (pre-gathered planes, h planes by DMA, full 128-row tiles):
-  // every h chunk is DMA'd first, then the W planes slice by slice, and the
-  // MFMAs run slice-outer over all four chunks, so they start on slice 0 while
-  // the later slices land (the four chunk accumulators stay live); the four
-  // epilogues follow the last slice
-  constexpr bool KOUT_OK = PRE && HKP && STAGE && CH % SF_THR == 0;
-#else
-  constexpr bool KOUT_OK = false;
-#endif
-  const bool kout = KOUT_OK && nch == 4;
   if constexpr (HKP) {
     dma_chunk(hsA, 0);
-    if (kout) {
-      dma_chunk(hsB, 1);
-      dma_chunk(hsC, 2);
-      dma_chunk(hsD, 3);
-    }
-    __builtin_amdgcn_sched_barrier(0);   // chunk 0's DMA stays ahead of the W loads (SF_EARLY counts on it)
+    __builtin_amdgcn_sched_barrier(0);   // chunk 0's DMA stays ahead of the W loads
   } else {
     load_h(0);
   }
@@ -489,9 +466,6 @@ __global__ __launch_bounds__(sf_thr(HF)) void k_sampled_logits(const float* __re
       a0[j] = wp[plane_idx(blk, j, 0, lane, NS)];
       a1[j] = wp[plane_idx(blk, j, 1, lane, NS)];
       a2[j] = wp[plane_idx(blk, j, 2, lane, NS)];
-#if defined(SF_EARLY) || defined(SF_KOUT)
-      __builtin_amdgcn_sched_barrier(0);   // slice order, so the MFMAs wait for their slice only
-#endif
     }
   } else {
     const float* src = W + (int64_t)id * HF + 8 * hh;
@@ -509,23 +483,13 @@ __global__ __launch_bounds__(sf_thr(HF)) void k_sampled_logits(const float* __re
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
   };
-  if (KOUT_OK && kout) {
-    if (hh == 0) sbias[32 * w + l32] = bl;
-    // the h chunks (issued before the 3·NS W-plane loads) landed; the W planes
-    // are waited for slice by slice (the compiler's per-register waits)
-    __builtin_amdgcn_s_waitcnt(sf_wc_vm(3 * NS));
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-    SFD_T(1);
-  } else if constexpr (HRING) {
+  if constexpr (HRING) {
     if (hh == 0) sbias[32 * w + l32] = bl;
     __syncthreads();   // chunk 0's planes, the W rows / planes and the biases
     if (nch > 1) dma_chunk(hsB, 1);
     SFD_T(1);
   } else if constexpr (HKP) {
-#ifndef SF_BIASLATE
     if (hh == 0) sbias[32 * w + l32] = bl;
-#endif
     // every chunk's DMA is issued up front; one full wait + barrier (the W
     // rows are needed by chunk 0 anyway), then all MFMAs run barrier-free
     // (21.7 -> 21.4 us against a second barrier behind chunk 0; with the
@@ -533,29 +497,7 @@ __global__ __launch_bounds__(sf_thr(HF)) void k_sampled_logits(const float* __re
     if (nch > 1) dma_chunk(hsB, 1);
     if (nch > 2) dma_chunk(hsC, 2);
     if (nch > 3) dma_chunk(hsD, 3);
-#ifdef SF_BIASLATE
-    // the bias store waits for the bias load (issued first, with chunk 0's
-    // DMA retiring in order behind it): after chunks 1..3's DMA are issued,
-    // not before
-    if (hh == 0) sbias[32 * w + l32] = bl;
-#endif
-#ifdef SF_EARLY
-    // wait only for chunk 0's h planes (issued before the 3·NS W-plane loads and
-    // chunks 1..3's 3·NDMA DMA ops): chunk 0's MFMAs start while the W planes
-    // land slice by slice (the compiler's per-register waits) and chunks 1..3
-    // get their own wait + barrier below
-    constexpr int NDMA = CH / SF_THR;
-    constexpr bool EARLY = PRE && CH % SF_THR == 0;
-    if (EARLY && nch == 4) {
-      __builtin_amdgcn_s_waitcnt(sf_wc_vm(3 * NS + 3 * NDMA));
-      __builtin_amdgcn_s_barrier();
-      __builtin_amdgcn_sched_barrier(0);
-    } else {
-      __syncthreads();
-    }
-#else
     __syncthreads();
-#endif
     SFD_T(1);
   } else {
     store_h(hsA);
@@ -576,12 +518,10 @@ __global__ __launch_bounds__(sf_thr(HF)) void k_sampled_logits(const float* __re
   };
   // chunk 0: each A slice is split right before its MFMAs
   f16v accA = {}, accB = {};
-  if (!kout) {
 #pragma unroll
-    for (int j = 0; j < NS; ++j) {
-      if constexpr (!PRE) split3x8(wr[j][0], wr[j][1], a0[j], a1[j], a2[j]);
-      accA = mfma_split<NT>(a0[j], a1[j], a2[j], hsA[boff(j)], hsA[boff(j) + 64], hsA[boff(j) + 128], accA);
-    }
+  for (int j = 0; j < NS; ++j) {
+    if constexpr (!PRE) split3x8(wr[j][0], wr[j][1], a0[j], a1[j], a2[j]);
+    accA = mfma_split<NT>(a0[j], a1[j], a2[j], hsA[boff(j)], hsA[boff(j) + 64], hsA[boff(j) + 128], accA);
   }
   // row tile 0 publishes the draw and the gathered rows (the backward's Wg / bg)
   if (!PRE && emit && nact) {
@@ -652,29 +592,7 @@ __global__ __launch_bounds__(sf_thr(HF)) void k_sampled_logits(const float* __re
       epi(acc_old, c - 1);
     }
   };
-  if (KOUT_OK && kout) {
-    if (nact) {
-      f16v accC = {}, accD = {};
-#pragma unroll
-      for (int j = 0; j < NS; ++j) {
-        const int o = boff(j);
-        accA = mfma_split<NT>(a0[j], a1[j], a2[j], hsA[o], hsA[o + 64], hsA[o + 128], accA);
-        accB = mfma_split<NT>(a0[j], a1[j], a2[j], hsB[o], hsB[o + 64], hsB[o + 128], accB);
-        accC = mfma_split<NT>(a0[j], a1[j], a2[j], hsC[o], hsC[o + 64], hsC[o + 128], accC);
-        accD = mfma_split<NT>(a0[j], a1[j], a2[j], hsD[o], hsD[o + 64], hsD[o + 128], accD);
-        __builtin_amdgcn_sched_barrier(0);   // slice-outer: slice j's MFMAs before slice j + 1's wait
-      }
-      SFD_T(2);
-      epi(accA, 0);
-      SFD_T(3);
-      epi(accB, 1);
-      SFD_T(4);
-      epi(accC, 2);
-      epi(accD, 3);
-      SFD_T(5);
-      SFD_C(7);
-    }
-  } else if constexpr (HRING) {
+  if constexpr (HRING) {
     // step c: chunk c landed and every wave is done with chunk c − 1's slot ->
     // DMA chunk c + 1 into it -> chunk c's MFMAs with chunk c − 1's epilogue
     auto step_k = [&](int c, const bf16x8* hs_cur, bf16x8* hs_nxt, f16v& acc_new, f16v& acc_old)
@@ -697,14 +615,7 @@ __global__ __launch_bounds__(sf_thr(HF)) void k_sampled_logits(const float* __re
       else epi(accA, nch - 1);
     }
   } else if constexpr (HKP) {
-    // chunks 1..3 landed at the first barrier (SF_EARLY: at this one)
-#ifdef SF_EARLY
-    if (PRE && CH % SF_THR == 0 && nch == 4) {
-      __builtin_amdgcn_s_waitcnt(sf_wc_vm(0));
-      __builtin_amdgcn_s_barrier();
-      __builtin_amdgcn_sched_barrier(0);
-    }
-#endif
+    // chunks 1..3 landed at the first barrier
     if (nch > 1) {
       if (nact) {
         mma(hsB, accB);

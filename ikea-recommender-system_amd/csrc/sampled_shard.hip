@@ -107,22 +107,28 @@ __global__ __launch_bounds__(256) void k_head_rows_gather(const int32_t* __restr
   }
 }
 
-// requester side: tW[b] = rows[slot[b]], tb[b] = rb[slot[b]]; a row whose
-// target was invalid gets NaN (its CE row is NaN, as on one GPU)
+// requester side: tW[b] = rows[slot[b]], tb[b] = rb[slot[b]], trow[b] = b: the
+// CE's target table is tW / tb, row b's target is entry b.  A row whose target
+// was invalid gets a zero row and trow[b] = −1, so k_sampled_lse's range
+// guard gives it a NaN loss row with zero gradients — as on one GPU, where
+// the same guard sees the invalid id itself
 __global__ __launch_bounds__(256) void k_rows_unslot(const float* __restrict__ rows, const float* __restrict__ rb,
                                                      const int32_t* __restrict__ slot,
                                                      const int32_t* __restrict__ tid32, int n, int HF,
-                                                     float* __restrict__ tW, float* __restrict__ tb) {
+                                                     float* __restrict__ tW, float* __restrict__ tb,
+                                                     int64_t* __restrict__ trow) {
   const int per = HF / 4;
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (i >= (int64_t)n * per) return;
   const int b = (int)(i / per), c = (int)(i % per);
   const bool ok = tid32[b] >= 0;
-  const float nan = __builtin_nanf("");
-  f4 v = reinterpret_cast<const f4*>(rows + (int64_t)slot[b] * HF)[c];
-  if (!ok) v = f4{nan, nan, nan, nan};
+  f4 v = {0.f, 0.f, 0.f, 0.f};
+  if (ok) v = reinterpret_cast<const f4*>(rows + (int64_t)slot[b] * HF)[c];
   reinterpret_cast<f4*>(tW + (int64_t)b * HF)[c] = v;
-  if (c == 0) tb[b] = ok ? rb[slot[b]] : nan;
+  if (c == 0) {
+    tb[b] = ok ? rb[slot[b]] : 0.f;
+    trow[b] = ok ? b : -1;
+  }
 }
 
 // backward: gsend[slot[b]] = grows[b], gbsend[slot[b]] = gb[b]
@@ -183,10 +189,10 @@ extern "C" int rg_head_rows_gather(const int32_t* ids, int n, int64_t lo, int64_
 }
 
 extern "C" int rg_rows_unslot(const float* rows, const float* rb, const int32_t* slot, const int32_t* tid32, int n,
-                              int HF, float* tW, float* tb, hipStream_t stream) {
-  if (n <= 0 || HF <= 0 || (HF & 3) || !rows || !rb || !slot || !tid32 || !tW || !tb) return RG_ERR_ARG;
+                              int HF, float* tW, float* tb, int64_t* trow, hipStream_t stream) {
+  if (n <= 0 || HF <= 0 || (HF & 3) || !rows || !rb || !slot || !tid32 || !tW || !tb || !trow) return RG_ERR_ARG;
   hipLaunchKernelGGL(k_rows_unslot, dim3(blocks((int64_t)n * (HF / 4))), dim3(256), 0, stream, rows, rb, slot, tid32,
-                     n, HF, tW, tb);
+                     n, HF, tW, tb, trow);
   RG_LAUNCH_CHECK();
   return RG_OK;
 }

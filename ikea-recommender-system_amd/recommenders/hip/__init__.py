@@ -126,7 +126,7 @@ SIGNATURES = {
     "rg_neg_planes": [P, I, I, P, P],
     "rg_target_ids": [P, I, I64, P, P, P],
     "rg_head_rows_gather": [P, I, I64, I64, P, P, I, P, P, P, P],
-    "rg_rows_unslot": [P, P, P, P, I, I, P, P, P],
+    "rg_rows_unslot": [P, P, P, P, I, I, P, P, P, P],
     "rg_rows_slot": [P, P, P, I, I, P, P, P],
 }
 

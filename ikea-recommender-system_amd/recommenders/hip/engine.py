@@ -19,6 +19,7 @@ LinearHead   a Linear(H→A) used only through row gathers / argmax (Q heads).
 from __future__ import annotations
 
 import math
+import weakref
 
 import numpy as np
 import torch
@@ -710,8 +711,9 @@ LOGIT_TERMS = {"f32x9": 9, "f32x6": 6, "f32x6d3": 6}
 PASS2_STREAM_PRIORITY = 0
 # stored logits of the fused head (pass 1 writes z = S + b, pass 2 reads it
 # instead of recomputing the S contraction: 21 -> 15 bf16 plane-product terms
-# per step at f32x6d3): used while the buffer (ceil(A/32)·32 × B floats,
-# 16.4 GB at C2) stays within this budget and a third of the free HBM
+# per step at f32x6d3): used while every head's buffers on the device together
+# (ceil(A/32)·32 × B floats each, 16.4 GB at C2) stay within this budget and a
+# third of the memory they and the free HBM make up (SoftmaxHead.zs_buffer)
 ZSTORE_MAX_BYTES = 48 << 30
 PRECISIONS = ("f32",) + tuple(SPLIT_TERMS)
 
@@ -729,6 +731,7 @@ class SoftmaxHead:
     exactly like the single-GPU (and reference) construction."""
 
     _wgen = 0   # (class default: heads built with __new__, qlearn.py)
+    _live = weakref.WeakSet()   # every head, for the per-device stored-logit budget
 
     @property
     def top_scanned(self):
@@ -761,6 +764,7 @@ class SoftmaxHead:
         self.top_k = 0
         # stored-logit top-k (rg_topk, K > 32 only) candidate overflow flag
         self.top_err = torch.zeros(1, dtype=torch.int32, device=device)
+        SoftmaxHead._live.add(self)
 
     # W / b (and their Adam moments) are only reachable through these
     # properties, which first order the current stream after an overlapped
@@ -819,21 +823,45 @@ class SoftmaxHead:
             self._fws[slot] = w
         return w
 
+    @staticmethod
+    def zs_bytes_on(device):
+        """Bytes of stored-logit buffers every live head holds on ``device``."""
+        dev = torch.device(device)
+        return sum(w.zs.numel() * 4 for h in list(SoftmaxHead._live) if torch.device(h.device) == dev
+                   for w in h.__dict__.get("_fws", {}).values() if isinstance(w.zs, torch.Tensor))
+
     def zs_buffer(self, w):
         """The stored-logit buffer of workspace w, or None (recomputed in pass
         2).  Needs HF <= 128 and B a multiple of pass 1's 256-row blocks.
-        ``zstore``: None = auto (within ZSTORE_MAX_BYTES and a third of the
-        free device memory), True / False force it (tests)."""
+        ``zstore``: None = auto, True / False force it (tests).  Auto: one
+        budget for all heads of the device — the buffers already held plus
+        this one within ZSTORE_MAX_BYTES and within a third of (held + free
+        device memory) — so a double-Q trainer's two heads cannot pin most of
+        the HBM; an allocation that fails leaves the logits recomputed."""
         mode = getattr(self, "zstore", None)
         if mode is False or self.HF > 128 or w.B % call("rg_flash_rows_per_block", self.HF):
             return None
         if w.zs is None:
             nb = int(call("rg_flash_zs_bytes", w.B, self.A))
-            if mode is None and (nb > ZSTORE_MAX_BYTES or nb > torch.cuda.mem_get_info(self.device)[0] // 3):
+            held = self.zs_bytes_on(self.device)
+            if mode is None and (held + nb > ZSTORE_MAX_BYTES
+                                 or held + nb > (held + torch.cuda.mem_get_info(self.device)[0]) // 3):
                 w.zs = False
             else:
-                w.zs = torch.empty(nb // 4, dtype=torch.float32, device=self.device)
+                try:
+                    w.zs = torch.empty(nb // 4, dtype=torch.float32, device=self.device)
+                except torch.cuda.OutOfMemoryError:
+                    if mode:
+                        raise
+                    w.zs = False
         return w.zs if w.zs is not False else None
+
+    def release_stored_logits(self):
+        """Free every workspace's stored-logit buffer (pass 2 recomputes the
+        logits from then on; the next pass 1 re-decides)."""
+        self.join()   # an overlapped pass 2 may still read them
+        for w in self._fws.values():
+            w.zs, w.zs_live = None, False
 
     def stored_logits(self):
         """True when a fused workspace of this head keeps its logits for pass 2."""
@@ -1391,7 +1419,7 @@ class ShardedSampledHead(SampledSoftmaxHead):
             w.tslot, w.tsend = z(B, dt=torch.int32), z(B, dt=torch.int32)
             w.tcounts = z(self.comm.world, dt=torch.int32)
             w.tW, w.tb = z(B, HF), z(B)
-            w.iota = torch.arange(B, dtype=torch.int64, device=dev)
+            w.trow = z(B, dt=torch.int64)
             w.nR = torch.zeros(1, dtype=torch.int32, device=dev)
             w.gsend, w.gbsend = z(B, HF), z(B)
             w.xb = {}
@@ -1444,15 +1472,16 @@ class ShardedSampledHead(SampledSoftmaxHead):
             comm.all_to_all(rows_in[:B], rows_out[:R], w.send_splits, w.recv_splits)
             comm.all_to_all(rb_in[:B], rb_out[:R], w.send_splits, w.recv_splits)
             call("rg_rows_unslot", rows_in.data_ptr(), rb_in.data_ptr(), w.tslot.data_ptr(), w.t32.data_ptr(), B,
-                 HF, w.tW.data_ptr(), w.tb.data_ptr(), st)
+                 HF, w.tW.data_ptr(), w.tb.data_ptr(), w.trow.data_ptr(), st)
         hp = h_planes.data_ptr() if h_planes is not None else None
         with region("sampled_fwd", exact=True):   # the one-launch logits on the exchanged planes (draw = 2)
             call("rg_sampled_logits", h.data_ptr(), W, b, w.ids.data_ptr(), 2, self.seed, self.draws, self.A_full,
                  B, S, HF, w.terms, w.ZT.data_ptr(), w.ldz, w.pmax.data_ptr(), w.psum.data_ptr(), w.Wg.data_ptr(),
                  w.bg.data_ptr(), hp, w.Wp.data_ptr(), st)
         self.draws += 1
-        # CE with the fetched target rows (row b's target is row b of tW / tb)
-        call("rg_sampled_lse", h.data_ptr(), w.tW.data_ptr(), w.tb.data_ptr(), w.iota.data_ptr(), B, B, HF,
+        # CE with the fetched target rows (row b's target is row b of tW / tb; −1 for an invalid
+        # target: NaN loss row, zero gradients, as on one GPU)
+        call("rg_sampled_lse", h.data_ptr(), w.tW.data_ptr(), w.tb.data_ptr(), w.trow.data_ptr(), B, B, HF,
              w.pmax.data_ptr(), w.psum.data_ptr(), w.nT, g, w.lse.data_ptr(), w.loss_row.data_ptr(),
              w.ids.data_ptr() + 4 * S, w.gb.data_ptr() + 4 * S, w.grows.data_ptr() + 4 * S * HF,
              w.dh_slabs.data_ptr(), st)

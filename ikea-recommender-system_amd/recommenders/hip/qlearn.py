@@ -210,8 +210,10 @@ def double_q_step(nets, clocks, k, s, a, r, s_next, true_len, true_next_len, is_
         call("rg_smorl_td", q.data_ptr(), qn.data_ptr(), rr.data_ptr(), end8.data_ptr(), smorl["w_dev"].data_ptr(),
              nh, _f32(gamma), grad_row, B, row.data_ptr(), dq.data_ptr(), st)
         call("rg_sum_scale", row.data_ptr(), B, _f32(1.0 / B), q_loss.data_ptr(), None, st)
-    if host is not None:   # (SMORL: + the supervised head's top-k overflow flag)
-        host.capture(sup_loss, q_loss, *([main.sup_head_output.top_err] if smorl is not None else []))
+    if host is not None:   # (SMORL on the native fp32 head: + rg_topk's K > 32 overflow flag; the
+        # fused head never raises it — its overflowing rows are scanned whole, counted in top_scanned)
+        fused = bool(main.sup_head_output.flash_terms(B))
+        host.capture(sup_loss, q_loss, *([main.sup_head_output.top_err] if smorl is not None and not fused else []))
     # ---- backward + Adam (main network, its own optimizer clock) ----
     adam6 = clocks[k].next_args()
     main.trunk_tag = getattr(main, "trunk_tag", 0) + 1

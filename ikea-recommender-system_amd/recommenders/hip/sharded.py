@@ -331,8 +331,8 @@ def sharded_double_q_step(nets, clocks, k, s, a, r, s_next, true_len, true_next_
              nh, _f32(gamma), grad_row, B, row.data_ptr(), dq.data_ptr(), st)
         call("rg_sum_scale", row.data_ptr(), B, _f32(1.0 / Bg), q_loss.data_ptr(), None, st)
     comm.all_reduce(q_loss)
-    if host is not None:   # (SMORL: + the supervised head's top-k overflow flag)
-        host.capture(sup_loss, q_loss, *([sup.top_err] if smorl is not None else []))
+    if host is not None:   # (SMORL on the native fp32 head: + rg_topk's K > 32 overflow flag)
+        host.capture(sup_loss, q_loss, *([sup.top_err] if smorl is not None and not getattr(w, "terms", 0) else []))
     # ---- backward + Adam (main network, its own optimizer clock) ----
     adam6 = clocks[k].next_args()
     main.trunk_tag = getattr(main, "trunk_tag", 0) + 1

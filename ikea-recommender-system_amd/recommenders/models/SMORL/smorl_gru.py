@@ -118,10 +118,10 @@ class SMORL_trainer:
         # are final (hip/hostsync.py); the backward is still queued on return
         hs = self.__dict__.setdefault("_host_scalars", HostScalars())
         self.train_step_async(s, a, r_acc, s_next, true_len, true_next_len, is_end, host=hs)
-        sup, q, top_err = hs.get()
-        if top_err:
+        vals = hs.get()
+        if len(vals) > 2 and vals[2]:   # (native fp32 head only: rg_topk's K > 32 overflow)
             (self.SMORL_1, self.SMORL_2)[self.last_main].sup_head_output.check_top_err()
-        return sup, q
+        return vals[0], vals[1]
 
     @property
     def last_rewards(self):

@@ -490,7 +490,9 @@ int rg_collect_grads(const float* dX0, const float* dX1, const int32_t* slot, co
  *   rg_shard_route with n_rows = A).
  * rg_head_rows_gather: owner side, W rows and biases of n received item ids from the local shard
  *   [lo, lo + n_local) (zeros, local_ids -1 when not held).
- * rg_rows_unslot: tW[b] = rows[slot[b]], tb[b] = rb[slot[b]] (NaN where tid32[b] < 0).
+ * rg_rows_unslot: tW[b] = rows[slot[b]], tb[b] = rb[slot[b]], trow[b] = b (the CE's per-row target
+ *   into tW / tb); where tid32[b] < 0 a zero row and trow[b] = -1, so rg_sampled_lse writes a NaN
+ *   loss row with zero gradients, as the one-GPU head does for an invalid target.
  * rg_rows_slot: gsend[slot[b]] = grows[b], gbsend[slot[b]] = gb[b] (the targets' row gradients
  *   back to their owners). */
 int rg_neg_pick(uint64_t seed, uint64_t counter, int64_t A, int S, int HF, int64_t lo, int64_t hi, const float* W,
@@ -500,7 +502,7 @@ int rg_target_ids(const int64_t* tgt, int n, int64_t A, int32_t* out, int32_t* n
 int rg_head_rows_gather(const int32_t* ids, int n, int64_t lo, int64_t n_local, const float* W, const float* bias,
                         int HF, float* rows, float* rb, int32_t* local_ids, rg_stream_t stream);
 int rg_rows_unslot(const float* rows, const float* rb, const int32_t* slot, const int32_t* tid32, int n, int HF,
-                   float* tW, float* tb, rg_stream_t stream);
+                   float* tW, float* tb, int64_t* trow, rg_stream_t stream);
 int rg_rows_slot(const float* grows, const float* gb, const int32_t* slot, int n, int HF, float* gsend, float* gbsend,
                  rg_stream_t stream);
 

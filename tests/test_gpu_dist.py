@@ -28,13 +28,21 @@ def _port():
     return p
 
 
-def _batches(world=WORLD):
+def _batches(world=WORLD, bad=False):
+    """bad: step 1 carries an out-of-range target on rank 0's rows and a
+    negative one on rank 1's (the reference's CrossEntropyLoss raises; here a
+    NaN loss row with zero gradients, on one GPU and on every rank alike)."""
     from recommenders.data_utils.synthetic import SessionStream
     st = SessionStream(CFG["item_num"], CFG["state_size"], world * B * STEPS, seed=21)
-    return [st.batch(i, world * B) for i in range(STEPS)]
+    out = [list(st.batch(i, world * B)) for i in range(STEPS)]
+    if bad:
+        a = out[1][1] = torch.as_tensor(out[1][1]).clone()
+        a[3] = CFG["action_dim"] + 7
+        a[B + 5] = -2
+    return [tuple(b) for b in out]
 
 
-def _rank(rank, port, out, precision, world=WORLD, extra=None):
+def _rank(rank, port, out, precision, world=WORLD, extra=None, bad=False):
     sys.path.insert(0, REPO)
     sys.path.insert(0, os.path.join(REPO, "ikea-recommender-system_amd"))
     import torch.distributed as dist
@@ -44,11 +52,13 @@ def _rank(rank, port, out, precision, world=WORLD, extra=None):
         tr = GRU4Rec_trainer(device="cuda:0", shard_items=True, matmul_precision=precision, **CFG, **(extra or {}))
         assert tr.gru_model.trunk.n_local < CFG["item_num"] + 1   # the item table is row-sharded
         losses = []
-        for s, a, r, sn, ln, nln, e in _batches(world):
+        for s, a, r, sn, ln, nln, e in _batches(world, bad):
             sl = slice(rank * B, (rank + 1) * B)
             losses.append(tr.train_step(s[sl], a[sl], ln[sl]))
         sd = {k: v.cpu().numpy() for k, v in tr.gru_model.state_dict().items()}
-        np.savez(os.path.join(out, f"rank{rank}.npz"), losses=np.array(losses), **sd)
+        head = tr.gru_model.output
+        stored = bool(head.stored_logits()) if hasattr(head, "stored_logits") else False
+        np.savez(os.path.join(out, f"rank{rank}.npz"), losses=np.array(losses), stored=np.array(stored), **sd)
     finally:
         dist.destroy_process_group()
 
@@ -76,6 +86,8 @@ def test_item_sharded_step_equals_single_gpu_global_batch(precision):
     for rank in range(WORLD):
         g = np.load(os.path.join(out, f"rank{rank}.npz"))
         np.testing.assert_allclose(g["losses"], ref_losses, rtol=0, atol=1e-4)
+        # WORLD·B = 256 gathered rows: the fused precisions keep the shard's logits for pass 2
+        assert bool(g["stored"]) == (precision != "f32"), (rank, precision)
         lo, hi = item_shard(CFG["action_dim"], WORLD, rank)
         elo, ehi = item_shard(CFG["item_num"] + 1, WORLD, rank)
         for k, v in sd.items():
@@ -86,20 +98,22 @@ def test_item_sharded_step_equals_single_gpu_global_batch(precision):
             assert (d > 1e-4).mean() < 1e-3, (rank, k)
 
 
-@pytest.mark.parametrize("world,precision", [(2, "f32x6d3"), (3, "f32x6")])
-def test_item_sharded_sampled_step_equals_single_gpu_global_batch(world, precision):
+@pytest.mark.parametrize("world,precision,bad", [(2, "f32x6d3", False), (3, "f32x6", False), (2, "f32x6d3", True)])
+def test_item_sharded_sampled_step_equals_single_gpu_global_batch(world, precision, bad):
     """The item-sharded sampled head (engine.ShardedSampledHead,
     csrc/sampled_shard.hip: the negatives' rows by one all-reduce, the targets'
     rows by all-to-all, gradients back to their owners) with the row-sharded
     item table, 2 and 3 ranks (9001 items: an uneven split over 3): every rank
     equals the single-GPU sampled step on the concatenated batch (same
-    counter-based negatives) — losses, and its shard of every weight."""
+    counter-based negatives) — losses, and its shard of every weight.  bad:
+    invalid targets on both ranks give the NaN loss of the one-GPU step and
+    leave every weight finite and equal to it."""
     sys.path.insert(0, os.path.join(REPO, "ikea-recommender-system_amd"))
     extra = dict(n_negatives=256, neg_seed=5)
     out = tempfile.mkdtemp()
     ctx = mp.get_context("spawn")
     port = _port()
-    procs = [ctx.Process(target=_rank, args=(r, port, out, precision, world, extra)) for r in range(world)]
+    procs = [ctx.Process(target=_rank, args=(r, port, out, precision, world, extra, bad)) for r in range(world)]
     for p in procs:
         p.start()
     for p in procs:
@@ -107,7 +121,8 @@ def test_item_sharded_sampled_step_equals_single_gpu_global_batch(world, precisi
         assert p.exitcode == 0
     from recommenders.models.GRU4Rec.model import GRU4Rec_trainer
     ref = GRU4Rec_trainer(device="cuda", matmul_precision=precision, **CFG, **extra)
-    ref_losses = [ref.train_step(s, a, ln) for s, a, r, sn, ln, nln, e in _batches(world)]
+    ref_losses = [ref.train_step(s, a, ln) for s, a, r, sn, ln, nln, e in _batches(world, bad)]
+    assert np.isnan(ref_losses[1]) == bad and np.isfinite(ref_losses[0])
     sd = {k: v.cpu().numpy() for k, v in ref.gru_model.state_dict().items()}
     from recommenders.hip.dist import item_shard
     lr = CFG["learning_rate"]
@@ -120,6 +135,7 @@ def test_item_sharded_sampled_step_equals_single_gpu_global_batch(world, precisi
             got = g[k]
             want = v[lo:hi] if k.startswith("output.") else (v[elo:ehi] if k == "embedding.weight" else v)
             assert got.shape == want.shape, (rank, k)
+            assert np.isfinite(got).all(), (rank, k)
             d = np.abs(got - want)
             assert d.max() <= 2 * lr + 1e-5, (rank, k, float(d.max()))
             assert (d > 1e-4).mean() < 1e-3, (rank, k)

@@ -73,14 +73,16 @@ def _rank(rank, port, out, kind, topk, extra, c=CFG):
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=c["WORLD"])
     try:
         tr = _make(kind, topk, c, device="cuda:0", shard_items=True, **extra)
-        losses, rewards = [], []
+        losses, rewards, stored = [], [], []
         Bk = c["B"]
         for s, a, r, sn, ln, nln, e in _batches(c):
             sl = slice(rank * Bk, (rank + 1) * Bk)
             losses.append(tr.train_step(s[sl], a[sl], r[sl], sn[sl], ln[sl], nln[sl], e[sl]))
             if kind == "smorl":
                 rewards.append(tr.last_rewards.cpu().numpy())
-        res = {"losses": np.array(losses)}
+            # did the trained net's item-sharded supervised head keep its logits for pass 2?
+            stored.append(bool(_nets(tr)[getattr(tr, "last_main", 0)].sup_head_output.stored_logits()))
+        res = {"losses": np.array(losses), "stored": np.array(stored)}
         if rewards:
             res["rewards"] = np.stack(rewards)
         for i, net in enumerate(_nets(tr)):
@@ -147,20 +149,27 @@ def test_item_sharded_double_q_equals_single_gpu_global_batch(kind, topk, extra)
     _check_shards(ranks, ref)
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 8])
 def test_item_sharded_smorl_c4_instantiation(world):
-    """The benched C4 kernels item-sharded: SMORL 3-reward, H = E = 128, L 50,
+    """The benched C4 kernels item-sharded: SMORL 3-reward, H = E = 128,
     f32x6d3 (k_flash_fwd<128, 6, 3, true> with a shard offset, the rewards'
     top-1 re-scored in fp32 and merged across ranks, k_flash_amax<128, 3,
     true> screening for the double-Q target), topk_div = topk_nov = 1,
-    q_weights [1, 1, 1], 64 rows per rank (B % 32 == 0), and an uneven split:
-    N = 30001 items over 2 or 3 ranks (the 30002-row item table over 3).
-    Every rank equals the single-GPU step on the concatenated batch (losses,
-    rewards of its rows, its shard of every weight), and the single-GPU step
-    equals OracleSMORL (the reference's helpers composed, smorl_gru.py:233-334)."""
+    q_weights [1, 1, 1], and an uneven split: N = 30001 items over 2, 3 or 8
+    ranks (the 30002-row item table too).  2 / 3 ranks: 64 rows each, L 50;
+    8 ranks (the partition of the C4 / C5 lines): 32 rows each, L 20 — 256
+    gathered rows, one whole pass-1 row block, so every rank's shard of the
+    head stores its logits (k_flash_fwd<128, 6, 3, true, true> with lo != 0,
+    storing z while emitting the top-1 for the cross-rank merge) and pass 2
+    reads them (asserted).  Every rank equals the single-GPU step on the
+    concatenated batch (losses, rewards of its rows, its shard of every
+    weight), and the single-GPU step equals OracleSMORL (the reference's
+    helpers composed, smorl_gru.py:233-334)."""
     import random
     sys.path.insert(0, os.path.join(REPO, "ikea-recommender-system_amd"))
-    c = dict(CFG, N=30001, L=50, H=128, B=64, STEPS=3, WORLD=world, seed=41, q_weights=(1.0, 1.0, 1.0), lr=0.01)
+    Bk, L, steps = (32, 20, 2) if world == 8 else (64, 50, 3)
+    c = dict(CFG, N=30001, L=L, H=128, B=Bk, STEPS=steps, WORLD=world, seed=41, q_weights=(1.0, 1.0, 1.0),
+             lr=0.01)
     extra = dict(X6D3)
     ranks = _run_ranks("smorl", (1, 1), extra, c)
     from oracle.models import OracleSMORL
@@ -189,4 +198,6 @@ def test_item_sharded_smorl_c4_instantiation(world):
         np.testing.assert_allclose(g["losses"], ref_losses, rtol=0, atol=1e-4)
         rows = slice(rank * c["B"], (rank + 1) * c["B"])
         np.testing.assert_allclose(g["rewards"], ref_rewards[:, rows], rtol=0, atol=1e-6)
+        # 256 gathered rows: the stored-logit head on every rank's shard
+        assert g["stored"].all() == (world * c["B"] % 256 == 0), (rank, g["stored"])
     _check_shards(ranks, ref, c)
