@@ -4,23 +4,27 @@
 //
 // Rank r owns the contiguous rows [lo_r, hi_r) of the (N+1) × E table with
 // lo_r = ⌊r·(N+1)/world⌋ (recommenders/hip/dist.py item_shard), plus their
-// Adam moments and gradient rows.  A trunk pass exchanges ids and rows:
+// Adam moments and gradient rows.  A trunk pass exchanges each DISTINCT id of
+// its batch once (a C2 batch: ~88K tokens, ~1.7K distinct items):
 //
 //   rg_token_ids      packed token t -> item id (forward time order)
-//   rg_shard_route    stable partition of the tokens by owner rank:
-//                     slot[t] = position in the send buffer, send_ids, counts
-//   (host: all_to_all of the counts, then of the ids)
+//   rg_shard_dedup    (csrc/segsum.hip) the distinct ids sorted — grouped by
+//                     owner — uslot[t] = the token's distinct index, counts
+//   (host: all_to_all of the distinct ids; the splits come from the host batch)
 //   rg_rows_gather    owner side: rows of the received ids from the local
 //                     shard (fp32 or the fp16 storage copy), local row ids
 //   (host: all_to_all of the rows back)
-//   rg_place_rows     requester: X[d][t] = rows_in[slot[t]] (d = 1: the
+//   rg_place_rows     requester: X[d][t] = rows_in[uslot[t]] (d = 1: the
 //                     row's valid prefix reversed, BidirGRU4Rec)
 // and in the backward:
-//   rg_collect_grads  gsend[slot[t]] = dX[0][t] (+ dX[1][rev t])
-//   (host: all_to_all of the row-gradients to their owners)
-//   then rg_scatter_add into the local gradient rows and rg_adam_rows over
-//   the local shard (csrc/pack_gather.hip, csrc/optim.hip).
-// No item-sized table is ever all-reduced.
+//   rg_combine_dirs   (Bidir) dX[0][t] += dX[1][rev t]
+//   rg_shard_dedup_grads  gsend[u] = Σ over the tokens of distinct id u, in
+//                     token order (csrc/segsum.hip)
+//   (host: all_to_all of the per-id row-gradients to their owners)
+//   then rg_scatter_rows into the local gradient rows and rg_adam_rows over
+//   the local shard (csrc/segsum.hip, csrc/optim.hip).
+// No item-sized table is ever all-reduced.  (rg_shard_route, a per-row stable
+// partition by owner, routes the sharded sampled head's B targets.)
 #include "common.h"
 #include <hip/hip_fp16.h>
 
@@ -158,21 +162,18 @@ __global__ __launch_bounds__(256) void k_place_rows(const TE* __restrict__ rows_
   }
 }
 
-// backward: gsend[slot[t]] = dX0[t] + dX1[rev(t)] (dX1 optional: Bidir)
-__global__ __launch_bounds__(256) void k_collect_grads(const float* __restrict__ dX0, const float* __restrict__ dX1,
-                                                       const int32_t* __restrict__ slot,
-                                                       const int32_t* __restrict__ lsort,
-                                                       const int32_t* __restrict__ offs, int E,
-                                                       float* __restrict__ gsend) {
+// backward, Bidir: dX0[t] += dX1[rev(t)] in place (the token's gradient of both
+// directions, before the per-distinct-id sums of rg_shard_dedup_grads)
+__global__ __launch_bounds__(256) void k_combine_dirs(float* __restrict__ dX0, const float* __restrict__ dX1,
+                                                      const int32_t* __restrict__ lsort,
+                                                      const int32_t* __restrict__ offs, int E) {
   const int r = blockIdx.x;
   const int len = lsort[r], base = offs[r];
   const int v4 = E / 4;
   for (int e = threadIdx.x; e < len * v4; e += blockDim.x) {
     const int tau = e / v4, c = e % v4;
-    const int t = base + tau;
-    f4 g = reinterpret_cast<const f4*>(dX0 + (int64_t)t * E)[c];
-    if (dX1) g += reinterpret_cast<const f4*>(dX1 + (int64_t)(base + len - 1 - tau) * E)[c];
-    reinterpret_cast<f4*>(gsend + (int64_t)slot[t] * E)[c] = g;
+    f4* d = reinterpret_cast<f4*>(dX0 + (int64_t)(base + tau) * E) + c;
+    *d += reinterpret_cast<const f4*>(dX1 + (int64_t)(base + len - 1 - tau) * E)[c];
   }
 }
 
@@ -225,10 +226,10 @@ extern "C" int rg_place_rows(const void* rows_in, int half, const int32_t* slot,
   return RG_OK;
 }
 
-extern "C" int rg_collect_grads(const float* dX0, const float* dX1, const int32_t* slot, const int32_t* lsort,
-                                const int32_t* offs, int B, int E, float* gsend, hipStream_t stream) {
-  if (B <= 0 || E <= 0 || (E & 3) || !dX0 || !slot || !lsort || !offs || !gsend) return RG_ERR_ARG;
-  hipLaunchKernelGGL(k_collect_grads, dim3(B), dim3(256), 0, stream, dX0, dX1, slot, lsort, offs, E, gsend);
+extern "C" int rg_combine_dirs(float* dX0, const float* dX1, const int32_t* lsort, const int32_t* offs, int B, int E,
+                               hipStream_t stream) {
+  if (B <= 0 || E <= 0 || (E & 3) || !dX0 || !dX1 || !lsort || !offs) return RG_ERR_ARG;
+  hipLaunchKernelGGL(k_combine_dirs, dim3(B), dim3(256), 0, stream, dX0, dX1, lsort, offs, E);
   RG_LAUNCH_CHECK();
   return RG_OK;
 }

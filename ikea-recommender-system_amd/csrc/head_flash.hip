@@ -198,11 +198,16 @@ __global__ __launch_bounds__(64 * fl_nw(HF, 1)) void k_flash_fwd(
   // chunk-major; inside, the 16×16 quadrant (ib, rb), then this kernel's
   // accumulator order, lane-linear: each lane stores its four logits of a
   // quadrant as one 16-B store (whole 1 KB per instruction; pass 2 transposes
-  // through LDS).  ZS: HF <= 128 (at HF 256 the wave's registers are full),
-  // launched by rg_flash_fwd_top only for B % 256 == 0, so every wave is
-  // active and its four stores per chunk are unconditional — the compiler then
-  // counts them exactly against the barrier's vmcnt(4)
-  static_assert(!ZS || (HF <= 128 && NG > 0), "stored logits: HF <= 128, training pass");
+  // through LDS).  Launched by rg_flash_fwd_top only for B a multiple of the
+  // row block (256 rows; 128 at HF 256), so every wave is active and its four
+  // stores per chunk are unconditional — the compiler then counts them
+  // exactly against the barrier's vmcnt(4).  HF 256 (ZSI): the wave's 512
+  // registers are full, so z leaves straight from the S accumulators inside
+  // the softmax section (no held copy), and the single-R-buffer loop's two
+  // barriers per chunk wait vmcnt(4) (the ring's DMA, not the z stores) and
+  // LDS only
+  static_assert(!ZS || NG > 0, "stored logits: training pass");
+  constexpr bool ZSI = ZS && HF > 128;
   // lane (kg, l16) stores its f4 at slot 16kg + 4(l16 >> 2) + ((l16 & 3) ^ kg) of
   // the quadrant (a bijection: still 1 KB contiguous per instruction), so that
   // pass 2, which DMAs the tile into LDS unchanged, reads it back transposed
@@ -251,7 +256,7 @@ __global__ __launch_bounds__(64 * fl_nw(HF, 1)) void k_flash_fwd(
   // chunk max, online max / Σexp, P planes (q*[rb]: the B operand of the O-part)
   // ZS: the chunk's z tiles leave after its O-part MFMAs are issued (stores
   // in the softmax section, between the two MFMA phases, measured 0.15 ms slower)
-  f4 zsv[2][2];
+  f4 zsv[ZS && HF <= 128 ? 2 : 1][2];
   auto zflush = [&](int c) __attribute__((always_inline)) {
 #pragma unroll
     for (int ib = 0; ib < 2; ++ib)
@@ -290,7 +295,10 @@ __global__ __launch_bounds__(64 * fl_nw(HF, 1)) void k_flash_fwd(
 #pragma unroll
       for (int ib = 0; ib < 2; ++ib) {
         const f4 bq = *reinterpret_cast<const f4*>(&sb[16 * ib + 4 * kg]);
-        if constexpr (ZS) zsv[ib][rb] = sa[ib][rb] + bq;   // stored after the O-part (zflush)
+        if constexpr (ZS && !ZSI) zsv[ib][rb] = sa[ib][rb] + bq;   // stored after the O-part (zflush)
+        if constexpr (ZSI)
+          __builtin_nontemporal_store(sa[ib][rb] + bq, reinterpret_cast<f4*>(zrow + (int64_t)(c0 + c) * (B / 32) * 1024 +
+                                                                             (2 * ib + rb) * 256));
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
           const float z = sa[ib][rb][u] + bq[u];
@@ -370,7 +378,7 @@ __global__ __launch_bounds__(64 * fl_nw(HF, 1)) void k_flash_fwd(
       if (ZS || active) {
         spart(sk0, sb0, c, q0, q1, q2);
         opart(sr0, q0, q1, q2);
-        if constexpr (ZS) zflush(c);
+        if constexpr (ZS && !ZSI) zflush(c);
       }
       csync();
       if (c + 1 < nch) {
@@ -382,26 +390,46 @@ __global__ __launch_bounds__(64 * fl_nw(HF, 1)) void k_flash_fwd(
         if (ZS || active) {
           spart(sk1, sb1, c + 1, q0, q1, q2);
           opart(sr1, q0, q1, q2);
-          if constexpr (ZS) zflush(c + 1);
+          if constexpr (ZS && !ZSI) zflush(c + 1);
         }
         csync();
       }
     } else {
-      // single R buffer: R(c) was issued after the previous chunk's O-part
+      // single R buffer: R(c) was issued after the previous chunk's O-part.
+      // ZSI: the first barrier waits for the ring's DMA (older than the
+      // chunk's z stores: vmcnt(4)), the second for LDS reads only
+      auto sync_dma = [&]() __attribute__((always_inline)) {
+        if constexpr (ZSI) {
+          __builtin_amdgcn_s_waitcnt((4 & 15) | 0x70);   // vmcnt(4) lgkmcnt(0)
+          __builtin_amdgcn_s_barrier();
+          __builtin_amdgcn_sched_barrier(0);
+        } else {
+          __syncthreads();
+        }
+      };
+      auto sync_lds = [&]() __attribute__((always_inline)) {
+        if constexpr (ZSI) {
+          __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0), vmcnt / expcnt free
+          __builtin_amdgcn_s_barrier();
+          __builtin_amdgcn_sched_barrier(0);
+        } else {
+          __syncthreads();
+        }
+      };
       if (c + 1 < nch) FL_ISSUE_K(c0 + c + 1, sk1, sb1);
       __builtin_amdgcn_sched_barrier(0);
-      if (active) spart(sk0, sb0, c, q0, q1, q2);
-      __syncthreads();   // R(c) and K(c+1) landed for every wave
-      if (active) opart(sr0, q0, q1, q2);
-      __syncthreads();   // every wave is done with sr0 and sk0
+      if (ZS || active) spart(sk0, sb0, c, q0, q1, q2);
+      sync_dma();   // R(c) and K(c+1) landed for every wave
+      if (ZS || active) opart(sr0, q0, q1, q2);
+      sync_lds();   // every wave is done with sr0 and sk0
       if (c + 1 < nch) {
         FL_ISSUE_R(c0 + c + 1, sr0);
         if (c + 2 < nch) FL_ISSUE_K(c0 + c + 2, sk0, sb0);
         __builtin_amdgcn_sched_barrier(0);
-        if (active) spart(sk1, sb1, c + 1, q0, q1, q2);
-        __syncthreads();
-        if (active) opart(sr0, q0, q1, q2);
-        __syncthreads();
+        if (ZS || active) spart(sk1, sb1, c + 1, q0, q1, q2);
+        sync_dma();
+        if (ZS || active) opart(sr0, q0, q1, q2);
+        sync_lds();
         if (c + 2 < nch) FL_ISSUE_R(c0 + c + 2, sr0);
       }
     }
@@ -945,10 +973,14 @@ __global__ __launch_bounds__(64 * fl_nw(HF, 2)) void k_flash_dw(
       __builtin_amdgcn_sched_barrier(0);
       dzpart(z1, sin1, qn0, qn1, qn2, c + 1 < nch);   // (past the last chunk: planes unused, no db)
       wpart_il(rcur, qc0, qc1, qc2);
-#ifdef FL2_PIN
+      // pin chunk c + 1's dZ planes (and db) to this step: without it the IR
+      // sinks the whole dZ VALU into the next step, next to the MFMAs that
+      // consume it, and the pipelining is undone (each step then opened with
+      // ~170 VALU before its first MFMA); pinned, the scheduler weaves them
+      // into this step's W-part: pass 2 6.49 -> 6.22 ms at C2
+      // (profiles/r06/flashx_pass2_pin.txt)
 #pragma unroll
       for (int ib = 0; ib < 2; ++ib) asm volatile("" : "+v"(qn0[ib]), "+v"(qn1[ib]), "+v"(qn2[ib]), "+v"(dbs[ib]));
-#endif
       __builtin_amdgcn_sched_barrier(0);
       FL2_MARK(3);
       __builtin_amdgcn_s_waitcnt(sf2_wc_vm(4));
@@ -959,9 +991,6 @@ __global__ __launch_bounds__(64 * fl_nw(HF, 2)) void k_flash_dw(
     // whole groups of six steps unguarded (straight-line, so the compiler's
     // wait counting across the loop's back edge stays exact), then the rest
     int c = 0;
-#ifdef FL2_PRIO
-    if (w >= 4) __builtin_amdgcn_s_setprio(1);
-#endif
     for (; c + 6 <= nch; c += 6) {
       step(c, zr1, zr0, sk0, sk1, si1, si2, qa0, qa1, qa2, qb0, qb1, qb2);
       step(c + 1, zr2, zr1, sk1, sk0, si2, si0, qb0, qb1, qb2, qa0, qa1, qa2);
@@ -1032,7 +1061,10 @@ __global__ __launch_bounds__(64 * fl_nw(HF, 2)) void k_flash_dw(
   __shared__ __attribute__((aligned(16))) float trd[(HF == 32 && !ZL) ? NW * TRW : 4];
   float* tr;
   if constexpr (ZL) {
-    tr = (w < 4 ? zr0 : zr1) + (w & 3) * TRW;   // (the ring is idle after the last barrier)
+    // (the z ring is idle after the last barrier; each array holds 1024·NW floats)
+    constexpr int WPZ = 1024 * NW / TRW;
+    static_assert(WPZ * 3 >= NW, "epilogue tiles fit the z ring");
+    tr = (w / WPZ == 0 ? zr0 : w / WPZ == 1 ? zr1 : zr2) + (w % WPZ) * TRW;
   } else if (HF == 32) {
     tr = trd + w * TRW;
   } else {
@@ -1582,7 +1614,7 @@ extern "C" int rg_flash_fwd_top(const void* Hk, const void* Wk, const void* Wr, 
   const bool arg = pbest != nullptr;
   if (arg != (parg != nullptr) || (cmax && !arg)) return RG_ERR_ARG;
   const int rpb = fl_rows(HF, 1);
-  if (zs && (HF > 128 || B % rpb)) return RG_ERR_SHAPE;   // stored logits: HF <= 128, whole row blocks
+  if (zs && B % rpb) return RG_ERR_SHAPE;   // stored logits: whole row blocks
   const int nct = (A + 31) / 32;
   const int cps = (nct + nsplit - 1) / nsplit;
   const int nrb = (B + rpb - 1) / rpb;
@@ -1593,7 +1625,7 @@ extern "C" int rg_flash_fwd_top(const void* Hk, const void* Wk, const void* Wr, 
                      pl, pO, pbest, parg, cmax, zs)
 #define FZ1(HFV, NTV, NGV, ARGV)            \
   if (zs) {                                 \
-    FF(HFV, NTV, NGV, ARGV, (HFV <= 128));  \
+    FF(HFV, NTV, NGV, ARGV, true);          \
   } else {                                  \
     FF(HFV, NTV, NGV, ARGV, false);         \
   }
@@ -1816,7 +1848,6 @@ extern "C" int rg_flash_dw_adam_planes(const void* Hk, const void* Hr, const voi
   if (!flash_hf_ok(HF)) return RG_ERR_SHAPE;
   if (dW_out ? !db_out : (!adam6 || !W || !mW || !vW || !bias || !mb || !vb)) return RG_ERR_ARG;
   if ((Wk_out != nullptr) != (Wr_out != nullptr) || (Wk_out && (dW_out || !bias_pad_out))) return RG_ERR_ARG;
-  if (zs && HF > 128) return RG_ERR_SHAPE;
   AdamArgs a{};
   if (adam6) a = AdamArgs{adam6[0], adam6[1], adam6[2], adam6[3], adam6[4], adam6[5]};
   const int rpb = fl_rows(HF, 2);
@@ -1832,8 +1863,8 @@ extern "C" int rg_flash_dw_adam_planes(const void* Hk, const void* Hr, const voi
                      bias, mb, vb, a, dW_out, db_out, (bf16x8*)Wk_out, (bf16x8*)Wr_out, bias_pad_out, tl.nfull,    \
                      tl.tsplit, tail_dw, tail_db, zs)
 #define FZ(HFV, NTV)               \
-  if (HFV <= 128 && zs) {          \
-    FW(HFV, NTV, (HFV <= 128));    \
+  if (zs) {                        \
+    FW(HFV, NTV, true);            \
   } else {                         \
     FW(HFV, NTV, false);           \
   }

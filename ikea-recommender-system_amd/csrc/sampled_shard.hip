@@ -14,11 +14,12 @@
 //             rank (exact: one nonzero term per element), k_neg_planes cuts
 //             them into the logits' fragment-order bf16 planes; the rank's B
 //             targets go to their owners (all-to-all of ids, k_head_rows_gather
-//             on the owner, all-to-all of the rows back, k_rows_unslot)
+//             on the owner, ONE all-to-all of the rows with their biases
+//             back, k_rows_unslot)
 //   backward  the negatives' row gradients (S × HF, summed over the rank's
 //             rows) SUM all-reduced, each owner scatters the rows it holds;
-//             the targets' row gradients go back to their owners by
-//             all-to-all (k_rows_slot) and are scattered there
+//             the targets' row and bias gradients go back to their owners
+//             by one all-to-all (k_rows_slot) and are scattered there
 #include "common.h"
 
 namespace {
@@ -85,13 +86,16 @@ __global__ void k_target_ids(const int64_t* __restrict__ tgt, int n, int64_t A, 
   out[i] = (t >= 0 && t < A) ? (int32_t)t : -1;
 }
 
+// Exchange rows carry the bias too: ld = HF + 4 floats per row (row, bias,
+// 3 pad: 16-B aligned rows), so each direction is ONE all-to-all.
+//
 // owner side: W rows and biases of n received item ids from the local shard
-// [lo, lo + n_local); local_ids[k] = id − lo (−1 and zeros when not held)
+// [lo, lo + n_local) into rows[k·ld ..]: the row, then the bias at + HF;
+// local_ids[k] = id − lo (−1 and zeros when not held)
 __global__ __launch_bounds__(256) void k_head_rows_gather(const int32_t* __restrict__ ids, int n, int64_t lo,
                                                           int64_t n_local, const float* __restrict__ W,
-                                                          const float* __restrict__ bias, int HF,
-                                                          float* __restrict__ rows, float* __restrict__ rb,
-                                                          int32_t* __restrict__ local_ids) {
+                                                          const float* __restrict__ bias, int HF, int ld,
+                                                          float* __restrict__ rows, int32_t* __restrict__ local_ids) {
   const int per = HF / 4;
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (i >= (int64_t)n * per) return;
@@ -100,19 +104,19 @@ __global__ __launch_bounds__(256) void k_head_rows_gather(const int32_t* __restr
   const bool ok = ids[k] >= 0 && l >= 0 && l < n_local;
   f4 v = {0.f, 0.f, 0.f, 0.f};
   if (ok) v = reinterpret_cast<const f4*>(W + l * HF)[c];
-  reinterpret_cast<f4*>(rows + (int64_t)k * HF)[c] = v;
+  reinterpret_cast<f4*>(rows + (int64_t)k * ld)[c] = v;
   if (c == 0) {
     local_ids[k] = ok ? (int32_t)l : -1;
-    rb[k] = ok ? bias[l] : 0.f;
+    rows[(int64_t)k * ld + HF] = ok ? bias[l] : 0.f;
   }
 }
 
-// requester side: tW[b] = rows[slot[b]], tb[b] = rb[slot[b]], trow[b] = b: the
+// requester side: tW[b] = row slot[b], tb[b] = its bias, trow[b] = b: the
 // CE's target table is tW / tb, row b's target is entry b.  A row whose target
 // was invalid gets a zero row and trow[b] = −1, so k_sampled_lse's range
 // guard gives it a NaN loss row with zero gradients — as on one GPU, where
 // the same guard sees the invalid id itself
-__global__ __launch_bounds__(256) void k_rows_unslot(const float* __restrict__ rows, const float* __restrict__ rb,
+__global__ __launch_bounds__(256) void k_rows_unslot(const float* __restrict__ rows, int ld,
                                                      const int32_t* __restrict__ slot,
                                                      const int32_t* __restrict__ tid32, int n, int HF,
                                                      float* __restrict__ tW, float* __restrict__ tb,
@@ -122,25 +126,27 @@ __global__ __launch_bounds__(256) void k_rows_unslot(const float* __restrict__ r
   if (i >= (int64_t)n * per) return;
   const int b = (int)(i / per), c = (int)(i % per);
   const bool ok = tid32[b] >= 0;
+  const float* src = rows + (int64_t)slot[b] * ld;
   f4 v = {0.f, 0.f, 0.f, 0.f};
-  if (ok) v = reinterpret_cast<const f4*>(rows + (int64_t)slot[b] * HF)[c];
+  if (ok) v = reinterpret_cast<const f4*>(src)[c];
   reinterpret_cast<f4*>(tW + (int64_t)b * HF)[c] = v;
   if (c == 0) {
-    tb[b] = ok ? rb[slot[b]] : 0.f;
+    tb[b] = ok ? src[HF] : 0.f;
     trow[b] = ok ? b : -1;
   }
 }
 
-// backward: gsend[slot[b]] = grows[b], gbsend[slot[b]] = gb[b]
+// backward: row slot[b] of gsend = grows[b], its bias entry (+ HF) = gb[b]
 __global__ __launch_bounds__(256) void k_rows_slot(const float* __restrict__ grows, const float* __restrict__ gb,
-                                                   const int32_t* __restrict__ slot, int n, int HF,
-                                                   float* __restrict__ gsend, float* __restrict__ gbsend) {
+                                                   const int32_t* __restrict__ slot, int n, int HF, int ld,
+                                                   float* __restrict__ gsend) {
   const int per = HF / 4;
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (i >= (int64_t)n * per) return;
   const int b = (int)(i / per), c = (int)(i % per);
-  reinterpret_cast<f4*>(gsend + (int64_t)slot[b] * HF)[c] = reinterpret_cast<const f4*>(grows + (int64_t)b * HF)[c];
-  if (c == 0) gbsend[slot[b]] = gb[b];
+  float* dst = gsend + (int64_t)slot[b] * ld;
+  reinterpret_cast<f4*>(dst)[c] = reinterpret_cast<const f4*>(grows + (int64_t)b * HF)[c];
+  if (c == 0) dst[HF] = gb[b];
 }
 
 inline unsigned blocks(int64_t n) { return (unsigned)((n + 255) / 256); }
@@ -177,31 +183,34 @@ extern "C" int rg_target_ids(const int64_t* tgt, int n, int64_t A, int32_t* out,
 }
 
 extern "C" int rg_head_rows_gather(const int32_t* ids, int n, int64_t lo, int64_t n_local, const float* W,
-                                   const float* bias, int HF, float* rows, float* rb, int32_t* local_ids,
+                                   const float* bias, int HF, int ld, float* rows, int32_t* local_ids,
                                    hipStream_t stream) {
-  if (n < 0 || HF <= 0 || (HF & 3) || !local_ids || (n > 0 && (!ids || !rows || !rb))) return RG_ERR_ARG;
+  if (n < 0 || HF <= 0 || (HF & 3) || ld < HF + 1 || (ld & 3) || !local_ids || (n > 0 && (!ids || !rows)))
+    return RG_ERR_ARG;
   if (n == 0) return RG_OK;
   if (n_local > 0 && (!W || !bias)) return RG_ERR_ARG;
   hipLaunchKernelGGL(k_head_rows_gather, dim3(blocks((int64_t)n * (HF / 4))), dim3(256), 0, stream, ids, n, lo,
-                     n_local, W, bias, HF, rows, rb, local_ids);
+                     n_local, W, bias, HF, ld, rows, local_ids);
   RG_LAUNCH_CHECK();
   return RG_OK;
 }
 
-extern "C" int rg_rows_unslot(const float* rows, const float* rb, const int32_t* slot, const int32_t* tid32, int n,
-                              int HF, float* tW, float* tb, int64_t* trow, hipStream_t stream) {
-  if (n <= 0 || HF <= 0 || (HF & 3) || !rows || !rb || !slot || !tid32 || !tW || !tb || !trow) return RG_ERR_ARG;
-  hipLaunchKernelGGL(k_rows_unslot, dim3(blocks((int64_t)n * (HF / 4))), dim3(256), 0, stream, rows, rb, slot, tid32,
+extern "C" int rg_rows_unslot(const float* rows, int ld, const int32_t* slot, const int32_t* tid32, int n, int HF,
+                              float* tW, float* tb, int64_t* trow, hipStream_t stream) {
+  if (n <= 0 || HF <= 0 || (HF & 3) || ld < HF + 1 || (ld & 3) || !rows || !slot || !tid32 || !tW || !tb || !trow)
+    return RG_ERR_ARG;
+  hipLaunchKernelGGL(k_rows_unslot, dim3(blocks((int64_t)n * (HF / 4))), dim3(256), 0, stream, rows, ld, slot, tid32,
                      n, HF, tW, tb, trow);
   RG_LAUNCH_CHECK();
   return RG_OK;
 }
 
-extern "C" int rg_rows_slot(const float* grows, const float* gb, const int32_t* slot, int n, int HF, float* gsend,
-                            float* gbsend, hipStream_t stream) {
-  if (n <= 0 || HF <= 0 || (HF & 3) || !grows || !gb || !slot || !gsend || !gbsend) return RG_ERR_ARG;
+extern "C" int rg_rows_slot(const float* grows, const float* gb, const int32_t* slot, int n, int HF, int ld,
+                            float* gsend, hipStream_t stream) {
+  if (n <= 0 || HF <= 0 || (HF & 3) || ld < HF + 1 || (ld & 3) || !grows || !gb || !slot || !gsend)
+    return RG_ERR_ARG;
   hipLaunchKernelGGL(k_rows_slot, dim3(blocks((int64_t)n * (HF / 4))), dim3(256), 0, stream, grows, gb, slot, n, HF,
-                     gsend, gbsend);
+                     ld, gsend);
   RG_LAUNCH_CHECK();
   return RG_OK;
 }

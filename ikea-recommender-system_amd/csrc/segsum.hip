@@ -1,4 +1,5 @@
-// Deterministic, atomic-free row scatter-add: G[id[i]] += src[i] over the
+// Deterministic, atomic-free row scatter-add: G[id[i]] += src[i] (row i at
+// src + i·lds, E floats) over the
 // rows i < *n_ptr whose id is valid and not skip_id, and tags[id] = tag for
 // every touched row.  It replaces atomic float adds (whose result depends on
 // the arrival order as soon as a row gets three or more contributions — the
@@ -69,9 +70,13 @@ struct vec_t<4> {
   using T = f4;
 };
 
-template <int V>
+// ASSIGN (the dedup exchange's per-unique-id sums, rg_shard_dedup_grads): G
+// is a fresh buffer and every run is written exactly once — by the lane that
+// closes it or, for a run crossing blocks, by k_seg_cross — so the sums are
+// stored, not added; tags may be null
+template <int V, bool ASSIGN = false>
 __global__ __launch_bounds__(256) void k_seg_blocks(const uint32_t* __restrict__ keys, const int32_t* __restrict__ rows,
-                                                    int n_max, const float* __restrict__ src, int E,
+                                                    int n_max, const float* __restrict__ src, int E, int lds,
                                                     float* __restrict__ G, int32_t* __restrict__ tags, int32_t tag,
                                                     float* __restrict__ part_first, float* __restrict__ part_last) {
   using T = typename vec_t<V>::T;
@@ -96,7 +101,7 @@ __global__ __launch_bounds__(256) void k_seg_blocks(const uint32_t* __restrict__
   const bool open_right = valid && lane == 63 && key == after;          // run continues into the next block
   const bool closed = end && !open_right && !(open_left && lane == first_end);
   if (__ballot(valid) == 0) return;   // a block of skipped rows only
-  const T* r = reinterpret_cast<const T*>(src + (int64_t)row * E);
+  const T* r = reinterpret_cast<const T*>(src + (int64_t)row * lds);
   T* g = reinterpret_cast<T*>(G + (int64_t)key * E);
   const int nv = E / V;
   for (int c = 0; c < nv; ++c) {
@@ -114,17 +119,20 @@ __global__ __launch_bounds__(256) void k_seg_blocks(const uint32_t* __restrict__
       if (lane >= d && !hd) x += y;
       if (lane >= d) hd = hd || hy;
     }
-    if (closed) g[c] += x;
+    if (closed) {
+      if constexpr (ASSIGN) g[c] = x;
+      else g[c] += x;
+    }
     if (end && open_left && lane == first_end) reinterpret_cast<T*>(part_first + (int64_t)blk * E)[c] = x;
     if (open_right) reinterpret_cast<T*>(part_last + (int64_t)blk * E)[c] = x;
   }
-  if (closed) tags[key] = tag;
+  if (closed && tags) tags[key] = tag;
 }
 
 // A run crossing block edges: the block where it starts adds its last-run
 // partial and the first-run partials of the following blocks that continue
 // it (their first keys equal the run's id), in block order.
-template <int EPL>
+template <int EPL, bool ASSIGN = false>
 __global__ __launch_bounds__(256) void k_seg_cross(const uint32_t* __restrict__ keys, int n_max, int E,
                                                    float* __restrict__ G, int32_t* __restrict__ tags, int32_t tag,
                                                    const float* __restrict__ part_first,
@@ -170,9 +178,12 @@ __global__ __launch_bounds__(256) void k_seg_cross(const uint32_t* __restrict__ 
 #pragma unroll
   for (int x = 0; x < EPL; ++x) {
     const int c = lane + 64 * x;
-    if (c < E) g[c] += acc[x];
+    if (c < E) {
+      if constexpr (ASSIGN) g[c] = acc[x];
+      else g[c] += acc[x];
+    }
   }
-  if (lane == 0) tags[k] = tag;
+  if (lane == 0 && tags) tags[k] = tag;
 }
 
 struct SegLayout {
@@ -229,11 +240,12 @@ extern "C" int64_t rg_scatter_rows_work_bytes(int n_max, int E, int64_t n_rows) 
   return (int64_t)seg_layout(n_max, E, n_rows).total;
 }
 
-extern "C" int rg_scatter_rows(const int32_t* ids, const float* src, int E, const int32_t* n_ptr, int n_max,
+extern "C" int rg_scatter_rows(const int32_t* ids, const float* src, int E, int lds, const int32_t* n_ptr, int n_max,
                                int skip_id, float* G, int64_t n_rows, int32_t* tags, int32_t tag, int reuse_sort,
                                void* work, int64_t work_bytes, hipStream_t stream) {
-  if (n_max <= 0 || E <= 0 || E > 512 || n_rows <= 0 || !ids || !src || !n_ptr || !G || !tags || !work)
+  if (n_max <= 0 || E <= 0 || E > 512 || lds < E || n_rows <= 0 || !ids || !src || !n_ptr || !G || !tags || !work)
     return RG_ERR_ARG;
+  if (E % 4 == 0 && (lds % 4 || (reinterpret_cast<uintptr_t>(src) & 15))) return RG_ERR_ARG;   // f4 rows
   const SegLayout L = seg_layout(n_max, E, n_rows);
   if (work_bytes < (int64_t)L.total) return RG_ERR_ARG;
   char* w = static_cast<char*>(work);
@@ -254,9 +266,11 @@ extern "C" int rg_scatter_rows(const int32_t* ids, const float* src, int E, cons
   const int nb = (n_max + SB - 1) / SB;
   const dim3 grid((unsigned)((nb + 3) / 4));
   if (E % 4 == 0)
-    hipLaunchKernelGGL(k_seg_blocks<4>, grid, dim3(256), 0, stream, kout, vout, n_max, src, E, G, tags, tag, pf, pl);
+    hipLaunchKernelGGL(k_seg_blocks<4>, grid, dim3(256), 0, stream, kout, vout, n_max, src, E, lds, G, tags, tag, pf,
+                       pl);
   else
-    hipLaunchKernelGGL(k_seg_blocks<1>, grid, dim3(256), 0, stream, kout, vout, n_max, src, E, G, tags, tag, pf, pl);
+    hipLaunchKernelGGL(k_seg_blocks<1>, grid, dim3(256), 0, stream, kout, vout, n_max, src, E, lds, G, tags, tag, pf,
+                       pl);
 #define SEG(EPLV) \
   hipLaunchKernelGGL(k_seg_cross<EPLV>, grid, dim3(256), 0, stream, kout, n_max, E, G, tags, tag, pf, pl)
   if (E <= 64) {
@@ -269,6 +283,185 @@ extern "C" int rg_scatter_rows(const int32_t* ids, const float* src, int E, cons
     SEG(8);
   }
 #undef SEG
+  RG_LAUNCH_CHECK();
+  return RG_OK;
+}
+
+// ------------------------------------------------------ dedup exchange ----
+// Row-sharded item table (csrc/emb_shard.hip): a trunk pass
+// requests each DISTINCT id once.  A C2 batch's ~88K packed tokens carry
+// ~1.7K distinct (Zipf) items, so the ids sent, the rows returned and the
+// row-gradients sent back shrink ~50× against one per token.
+//
+// rg_shard_dedup: stable radix sort of (id + 1, token) — invalid ids (−1)
+// become key 0, so they sort first and go with rank 0's group; the ids of
+// one owner are a contiguous range, so the sorted distinct ids are already
+// grouped by owner — then run heads, an inclusive scan (distinct index u per
+// sorted position), and
+//   uslot[t]  = u of token t (rg_place_rows reads rows_in[uslot[t]]),
+//   uids[u]   = the distinct ids in increasing order (−1 first, if any),
+//   counts[o] = distinct ids owned by rank o (owner ⌈(id+1)·W/N1⌉ − 1),
+//   *nuniq    = U,
+// and keeps the sorted order in the work buffer for
+// rg_shard_dedup_grads: gsend[u] = Σ of the token rows of id u, summed in
+// token order (k_seg_blocks / k_seg_cross over the sorted runs: a fixed
+// order, so the step stays bitwise repeatable), stored once per u.
+namespace {
+
+__global__ void k_dd_keys(const int32_t* __restrict__ tok_id, const int32_t* __restrict__ n_ptr, int n_max,
+                          uint32_t* __restrict__ keys, int32_t* __restrict__ vals) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n_max) return;
+  const int n = *n_ptr;
+  keys[i] = i < n ? (uint32_t)(max(tok_id[i], -1) + 1) : SENT;
+  vals[i] = i;
+}
+
+__global__ void k_dd_heads(const uint32_t* __restrict__ ks, const int32_t* __restrict__ n_ptr, int n_max,
+                           int32_t* __restrict__ head) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n_max) return;
+  head[i] = (i < *n_ptr && (i == 0 || ks[i] != ks[i - 1])) ? 1 : 0;
+}
+
+__global__ void k_dd_write(const uint32_t* __restrict__ ks, const int32_t* __restrict__ vs,
+                           const int32_t* __restrict__ incl, const int32_t* __restrict__ n_ptr, int n_max,
+                           int32_t* __restrict__ uslot, int32_t* __restrict__ uids, uint32_t* __restrict__ ukeys,
+                           int32_t* __restrict__ nuniq) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n_max) return;
+  const int n = *n_ptr;
+  if (i >= n) {
+    ukeys[i] = SENT;
+    if (i == 0) *nuniq = 0;
+    return;
+  }
+  const int u = incl[i] - 1;
+  uslot[vs[i]] = u;
+  ukeys[i] = (uint32_t)u;
+  if (i == 0 || ks[i] != ks[i - 1]) uids[u] = (int32_t)ks[i] - 1;
+  if (i == n - 1) *nuniq = u + 1;
+}
+
+// counts[o] = #{u : owner(uids[u]) == o}; uids sorted (−1 first, owned by rank 0)
+__global__ void k_dd_counts(const int32_t* __restrict__ uids, const int32_t* __restrict__ nuniq, int64_t N1, int W,
+                            int32_t* __restrict__ counts) {
+  const int o = threadIdx.x;
+  if (o >= W) return;
+  const int U = *nuniq;
+  auto lower = [&](int64_t v) {   // first u with uids[u] >= v (v = 0 for rank 0's start: −1 sorts before)
+    int a = 0, b = U;
+    while (a < b) {
+      const int m = (a + b) >> 1;
+      if ((int64_t)uids[m] < v) a = m + 1;
+      else b = m;
+    }
+    return a;
+  };
+  const int lo = o == 0 ? 0 : lower(((int64_t)o * N1) / W);
+  const int hi = o == W - 1 ? U : lower(((int64_t)(o + 1) * N1) / W);
+  counts[o] = hi - lo;
+}
+
+struct DedupLayout {
+  size_t keys_in, keys_out, vals_in, vals_out, head, incl, ukeys, part_first, part_last, tmp, total, sort_bytes,
+      scan_bytes;
+  int bits;
+};
+
+DedupLayout dedup_layout(int n_max, int E, int64_t N1) {
+  DedupLayout L{};
+  const size_t nb = (size_t)(n_max + SB - 1) / SB;
+  auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+  size_t off = 0;
+  L.keys_in = off; off += al(sizeof(uint32_t) * n_max);
+  L.keys_out = off; off += al(sizeof(uint32_t) * n_max);
+  L.vals_in = off; off += al(sizeof(int32_t) * n_max);
+  L.vals_out = off; off += al(sizeof(int32_t) * n_max);
+  L.head = off; off += al(sizeof(int32_t) * n_max);
+  L.incl = off; off += al(sizeof(int32_t) * n_max);
+  L.ukeys = off; off += al(sizeof(uint32_t) * n_max);
+  L.part_first = off; off += al(sizeof(float) * nb * E);
+  L.part_last = off; off += al(sizeof(float) * nb * E);
+  L.bits = key_bits(N1 + 1);   // keys 0 .. N1, the sentinel's low bits above them
+  size_t ts = 0, tc = 0;
+  hipcub::DeviceRadixSort::SortPairs(nullptr, ts, (const uint32_t*)nullptr, (uint32_t*)nullptr,
+                                     (const int32_t*)nullptr, (int32_t*)nullptr, n_max, 0, L.bits);
+  hipcub::DeviceScan::InclusiveSum(nullptr, tc, (const int32_t*)nullptr, (int32_t*)nullptr, n_max);
+  L.sort_bytes = ts;
+  L.scan_bytes = tc;
+  L.tmp = off; off += al(ts > tc ? ts : tc);
+  L.total = off;
+  return L;
+}
+
+}  // namespace
+
+extern "C" int64_t rg_shard_dedup_work_bytes(int n_max, int E, int64_t N1) {
+  if (n_max <= 0 || E <= 0 || N1 <= 0 || N1 >= INT32_MAX) return RG_ERR_ARG;
+  return (int64_t)dedup_layout(n_max, E, N1).total;
+}
+
+extern "C" int rg_shard_dedup(const int32_t* tok_id, const int32_t* n_ptr, int n_max, int64_t N1, int W, int E,
+                              int32_t* uslot, int32_t* uids, int32_t* counts, int32_t* nuniq, void* work,
+                              int64_t work_bytes, hipStream_t stream) {
+  if (n_max <= 0 || N1 <= 0 || N1 >= INT32_MAX || W <= 0 || W > N1 || W > 256 || E <= 0 || !tok_id || !n_ptr ||
+      !uslot || !uids || !counts || !nuniq || !work)
+    return RG_ERR_ARG;
+  const DedupLayout L = dedup_layout(n_max, E, N1);
+  if (work_bytes < (int64_t)L.total) return RG_ERR_ARG;
+  char* w = static_cast<char*>(work);
+  uint32_t* kin = (uint32_t*)(w + L.keys_in);
+  uint32_t* kout = (uint32_t*)(w + L.keys_out);
+  int32_t* vin = (int32_t*)(w + L.vals_in);
+  int32_t* vout = (int32_t*)(w + L.vals_out);
+  int32_t* head = (int32_t*)(w + L.head);
+  int32_t* incl = (int32_t*)(w + L.incl);
+  uint32_t* ukeys = (uint32_t*)(w + L.ukeys);
+  const dim3 g((unsigned)((n_max + 255) / 256));
+  hipLaunchKernelGGL(k_dd_keys, g, dim3(256), 0, stream, tok_id, n_ptr, n_max, kin, vin);
+  size_t ts = L.sort_bytes;
+  if (hipcub::DeviceRadixSort::SortPairs(w + L.tmp, ts, kin, kout, vin, vout, n_max, 0, L.bits, stream) !=
+      hipSuccess)
+    return RG_ERR_LAUNCH;
+  hipLaunchKernelGGL(k_dd_heads, g, dim3(256), 0, stream, kout, n_ptr, n_max, head);
+  size_t tc = L.scan_bytes;
+  if (hipcub::DeviceScan::InclusiveSum(w + L.tmp, tc, head, incl, n_max, stream) != hipSuccess)
+    return RG_ERR_LAUNCH;
+  hipLaunchKernelGGL(k_dd_write, g, dim3(256), 0, stream, kout, vout, incl, n_ptr, n_max, uslot, uids, ukeys,
+                     nuniq);
+  hipLaunchKernelGGL(k_dd_counts, dim3(1), dim3(256), 0, stream, uids, nuniq, N1, W, counts);
+  RG_LAUNCH_CHECK();
+  return RG_OK;
+}
+
+extern "C" int rg_shard_dedup_grads(const float* src, int E, int n_max, int64_t N1, float* gsend, void* work,
+                                    int64_t work_bytes, hipStream_t stream) {
+  if (n_max <= 0 || E <= 0 || E > 512 || (E & 3) || N1 <= 0 || !src || !gsend || !work) return RG_ERR_ARG;
+  const DedupLayout L = dedup_layout(n_max, E, N1);
+  if (work_bytes < (int64_t)L.total) return RG_ERR_ARG;
+  char* w = static_cast<char*>(work);
+  const int32_t* vout = (const int32_t*)(w + L.vals_out);
+  const uint32_t* ukeys = (const uint32_t*)(w + L.ukeys);
+  float* pf = (float*)(w + L.part_first);
+  float* pl = (float*)(w + L.part_last);
+  const int nb = (n_max + SB - 1) / SB;
+  const dim3 grid((unsigned)((nb + 3) / 4));
+  hipLaunchKernelGGL((k_seg_blocks<4, true>), grid, dim3(256), 0, stream, ukeys, vout, n_max, src, E, E, gsend,
+                     (int32_t*)nullptr, 0, pf, pl);
+#define SEGA(EPLV)                                                                                                \
+  hipLaunchKernelGGL((k_seg_cross<EPLV, true>), grid, dim3(256), 0, stream, ukeys, n_max, E, gsend, (int32_t*)nullptr, \
+                     0, pf, pl)
+  if (E <= 64) {
+    SEGA(1);
+  } else if (E <= 128) {
+    SEGA(2);
+  } else if (E <= 256) {
+    SEGA(4);
+  } else {
+    SEGA(8);
+  }
+#undef SEGA
   RG_LAUNCH_CHECK();
   return RG_OK;
 }

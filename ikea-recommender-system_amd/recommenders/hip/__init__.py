@@ -24,7 +24,7 @@ U64 = C.c_uint64
 
 # entry points returning int64_t (all others return int)
 RESTYPE_I64 = {"rg_sampled_work_bytes", "rg_head_work_bytes", "rg_head_plane_bytes", "rg_gru_wide_work_bytes",
-               "rg_scatter_rows_work_bytes", "rg_flash_dw_work_bytes",
+               "rg_scatter_rows_work_bytes", "rg_flash_dw_work_bytes", "rg_shard_dedup_work_bytes",
                "rg_flash_topk_work_bytes", "rg_flash_zs_bytes"}
 
 # name -> argtypes
@@ -34,7 +34,7 @@ SIGNATURES = {
     "rg_pack": [P, I, I, I, P, P, P, P],
     "rg_gather": [P, I, I, P, P, P, P, I64, I, I, P, P, P, P],
     "rg_scatter_rows_work_bytes": [I, I, I64],
-    "rg_scatter_rows": [P, P, I, P, I, I, P, I64, P, I32, I, P, I64, P],
+    "rg_scatter_rows": [P, P, I, I, P, I, I, P, I64, P, I32, I, P, I64, P],
     "rg_gemm_f32": [P, I64, I64, P, I64, I64, P, I64, P, I, P, I, I, P, I, P],
     "rg_reduce_slabs": [P, I, I64, P, P, I, I, P],
     "rg_colsum": [P, I, I, P, I, P, P],
@@ -121,13 +121,16 @@ SIGNATURES = {
     "rg_shard_route": [P, P, I64, I, P, P, P, P],
     "rg_rows_gather": [P, I, I64, I64, P, I, I, P, P, P],
     "rg_place_rows": [P, I, P, P, P, I, I, I, P, P],
-    "rg_collect_grads": [P, P, P, P, P, I, I, P, P],
+    "rg_combine_dirs": [P, P, P, P, I, I, P],
+    "rg_shard_dedup_work_bytes": [I, I, I64],
+    "rg_shard_dedup": [P, P, I, I64, I, I, P, P, P, P, P, I64, P],
+    "rg_shard_dedup_grads": [P, I, I, I64, P, P, I64, P],
     "rg_neg_pick": [U64, U64, I64, I, I, I64, I64, P, P, P, P, P, P, P],
     "rg_neg_planes": [P, I, I, P, P],
     "rg_target_ids": [P, I, I64, P, P, P],
-    "rg_head_rows_gather": [P, I, I64, I64, P, P, I, P, P, P, P],
-    "rg_rows_unslot": [P, P, P, P, I, I, P, P, P, P],
-    "rg_rows_slot": [P, P, P, I, I, P, P, P],
+    "rg_head_rows_gather": [P, I, I64, I64, P, P, I, I, P, P, P],
+    "rg_rows_unslot": [P, I, P, P, I, I, P, P, P, P],
+    "rg_rows_slot": [P, P, P, I, I, I, P, P],
 }
 
 _lib = None

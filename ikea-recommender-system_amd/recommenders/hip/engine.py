@@ -131,14 +131,15 @@ class SegScatter:
         self.work = None
         self.sizes = {}
 
-    def __call__(self, ids, src, E, n_ptr, n_max, skip, G, n_rows, tags, tag, st, reuse_sort=False):
+    def __call__(self, ids, src, E, n_ptr, n_max, skip, G, n_rows, tags, tag, st, reuse_sort=False, ld=None):
+        """ld: floats between consecutive source rows (default E)."""
         need = self.sizes.get((n_max, E, n_rows))
         if need is None:
             need = self.sizes[(n_max, E, n_rows)] = int(call("rg_scatter_rows_work_bytes", n_max, E, n_rows))
         if self.work is None or self.work.numel() < need:
             self.work = torch.empty(need, dtype=torch.uint8, device=self.device)
-        call("rg_scatter_rows", ids, src, E, n_ptr, n_max, skip, G, n_rows, tags, tag, 1 if reuse_sort else 0,
-             self.work.data_ptr(), self.work.numel(), st)
+        call("rg_scatter_rows", ids, src, E, E if ld is None else ld, n_ptr, n_max, skip, G, n_rows, tags, tag,
+             1 if reuse_sort else 0, self.work.data_ptr(), self.work.numel(), st)
 
 
 class _TrunkWS:
@@ -484,52 +485,64 @@ class Trunk:
         return t
 
     def _exchange_rows(self, w, s, B, L, st, route=None):
-        """Rows of every packed token of this rank's batch from their owners:
-        route by owner, all-to-all the ids, owners gather, all-to-all the rows.
-        With ``route`` (splits computed on the host from the host batch) no
-        device value is read back; otherwise the device counts are (one sync)."""
+        """Rows of the distinct ids of this rank's batch from their owners
+        (rg_shard_dedup: one row per distinct id, not per token): all-to-all
+        of the ids, owners gather, all-to-all of the rows back.  With
+        ``route`` (the distinct-id splits computed on the host from the host
+        batch, dist.owner_counts) no device value is read back; otherwise the
+        device counts are (one sync)."""
         comm, W = self.comm, self.comm.world
-        if getattr(w, "slot", None) is None:
-            w.slot = torch.empty(w.TM, dtype=torch.int32, device=self.device)
-            w.send_ids = torch.empty(w.TM, dtype=torch.int32, device=self.device)
+        n_max = max(1, w.T_host)
+        if getattr(w, "uslot", None) is None:
+            w.uslot = torch.empty(w.TM, dtype=torch.int32, device=self.device)
+            w.uids = torch.empty(w.TM, dtype=torch.int32, device=self.device)
             w.counts = torch.zeros(W, dtype=torch.int32, device=self.device)
             w.counts_all = torch.zeros(W * W, dtype=torch.int32, device=self.device)
+            w.nuniq = torch.zeros(1, dtype=torch.int32, device=self.device)
             w.nrecv = torch.zeros(1, dtype=torch.int32, device=self.device)
+        need = int(call("rg_shard_dedup_work_bytes", n_max, self.E, self.N1))
+        dd = self._xbuf(w, "dd_work", need, dtype=torch.uint8)
+        w.dd_nmax = n_max
         call("rg_token_ids", s.data_ptr(), B, L, w.perm.data_ptr(), w.lsort.data_ptr(), w.offs.data_ptr(), self.N1,
              w.tok_id[0].data_ptr(), self.err.data_ptr(), st)
-        call("rg_shard_route", w.tok_id[0].data_ptr(), w.ntok_ptr, self.N1, W, w.slot.data_ptr(),
-             w.send_ids.data_ptr(), w.counts.data_ptr(), st)
+        call("rg_shard_dedup", w.tok_id[0].data_ptr(), w.ntok_ptr, n_max, self.N1, W, self.E, w.uslot.data_ptr(),
+             w.uids.data_ptr(), w.counts.data_ptr(), w.nuniq.data_ptr(), dd.data_ptr(), dd.numel(), st)
         if route is not None:
             w.send_splits, w.recv_splits = list(route[0]), list(route[1])
         else:
             comm.all_gather(w.counts_all, w.counts)
-            M = w.counts_all.view(W, W).cpu()            # M[q][r]: tokens of rank q owned by rank r (one sync)
+            M = w.counts_all.view(W, W).cpu()            # M[q][r]: distinct ids of rank q owned by rank r (one sync)
             w.send_splits = M[comm.rank].tolist()
             w.recv_splits = M[:, comm.rank].tolist()
-        T, R = sum(w.send_splits), sum(w.recv_splits)
-        w.T, w.R = T, R
+        U, R = sum(w.send_splits), sum(w.recv_splits)
+        w.U, w.R = U, R
         half = self.emb16 is not None
         rdt = torch.float16 if half else torch.float32
         recv_ids = self._xbuf(w, "recv_ids", max(R, 1))
         w.local_ids = self._xbuf(w, "local_ids_buf", max(R, 1))
         w.nrecv.fill_(R)
-        comm.all_to_all(recv_ids[:R], w.send_ids[:T], w.recv_splits, w.send_splits)
+        comm.all_to_all(recv_ids[:R], w.uids[:U], w.recv_splits, w.send_splits)
         rows_out = self._xbuf(w, "rows_out", max(R, 1), self.E, rdt)
         call("rg_rows_gather", recv_ids.data_ptr(), R, self.lo, self.n_local,
              (self.emb16 if half else self.emb.p).data_ptr(), self.E, 1 if half else 0, rows_out.data_ptr(),
              w.local_ids.data_ptr(), st)
-        w.rows_in = self._xbuf(w, "rows_in_buf", max(T, 1), self.E, rdt)
-        comm.all_to_all(w.rows_in[:T], rows_out[:R], w.send_splits, w.recv_splits)
+        w.rows_in = self._xbuf(w, "rows_in_buf", max(U, 1), self.E, rdt)
+        comm.all_to_all(w.rows_in[:U], rows_out[:R], w.send_splits, w.recv_splits)
+        w.slot = w.uslot   # rg_place_rows: X[t] = rows_in[uslot[t]]
 
     def _exchange_grads(self, w, tag, st):
-        """Row-gradients of this rank's tokens to their owners; the owner adds
-        them into its gradient rows (tagged for the row-sparse Adam)."""
+        """Per distinct id, the sum of its tokens' row-gradients (in token
+        order) goes to the owner, which adds the ranks' sums into its
+        gradient rows (tagged for the row-sparse Adam)."""
         comm = self.comm
-        gsend = self._xbuf(w, "gsend", max(w.T, 1), self.E, torch.float32)
-        call("rg_collect_grads", w.dX[0].data_ptr(), w.dX[1].data_ptr() if self.ndir == 2 else None,
-             w.slot.data_ptr(), w.lsort.data_ptr(), w.offs.data_ptr(), w.B, self.E, gsend.data_ptr(), st)
+        if self.ndir == 2:
+            call("rg_combine_dirs", w.dX[0].data_ptr(), w.dX[1].data_ptr(), w.lsort.data_ptr(), w.offs.data_ptr(),
+                 w.B, self.E, st)
+        gsend = self._xbuf(w, "gsend", max(w.U, 1), self.E, torch.float32)
+        call("rg_shard_dedup_grads", w.dX[0].data_ptr(), self.E, w.dd_nmax, self.N1, gsend.data_ptr(),
+             w.dd_work.data_ptr(), w.dd_work.numel(), st)
         grecv = self._xbuf(w, "grecv", max(w.R, 1), self.E, torch.float32)
-        comm.all_to_all(grecv[:w.R], gsend[:w.T], w.recv_splits, w.send_splits)
+        comm.all_to_all(grecv[:w.R], gsend[:w.U], w.recv_splits, w.send_splits)
         pad = self.pad - self.lo
         skip = -1 if self.train_pad or not (0 <= pad < self.n_local) else pad
         self.scatter(w.local_ids.data_ptr(), grecv.data_ptr(), self.E, w.nrecv.data_ptr(), max(w.R, 1), skip,
@@ -1421,7 +1434,7 @@ class ShardedSampledHead(SampledSoftmaxHead):
             w.tW, w.tb = z(B, HF), z(B)
             w.trow = z(B, dt=torch.int64)
             w.nR = torch.zeros(1, dtype=torch.int32, device=dev)
-            w.gsend, w.gbsend = z(B, HF), z(B)
+            w.gsend = z(B, HF + 4)   # target row + bias gradients, one all-to-all
             w.xb = {}
         return w
 
@@ -1462,17 +1475,17 @@ class ShardedSampledHead(SampledSoftmaxHead):
                 M = allc.view(comm.world, comm.world).cpu()     # one sync
                 w.send_splits, w.recv_splits = M[comm.rank].tolist(), M[:, comm.rank].tolist()
             R = w.R = sum(w.recv_splits)
+            ld = HF + 4   # row, bias, pad: one all-to-all carries both
             recv_ids = self._xb(w, "recv_ids", max(R, 1), dtype=torch.int32)
             comm.all_to_all(recv_ids[:R], w.tsend[:B], w.recv_splits, w.send_splits)
-            rows_out, rb_out = self._xb(w, "rows_out", max(R, 1), HF), self._xb(w, "rb_out", max(R, 1))
+            rows_out = self._xb(w, "rows_out", max(R, 1), ld)
             w.local_ids = self._xb(w, "local_ids", max(R, 1), dtype=torch.int32)
-            call("rg_head_rows_gather", recv_ids.data_ptr(), R, self.lo, self.A, W, b, HF, rows_out.data_ptr(),
-                 rb_out.data_ptr(), w.local_ids.data_ptr(), st)
-            rows_in, rb_in = self._xb(w, "rows_in", B, HF), self._xb(w, "rb_in", B)
+            call("rg_head_rows_gather", recv_ids.data_ptr(), R, self.lo, self.A, W, b, HF, ld, rows_out.data_ptr(),
+                 w.local_ids.data_ptr(), st)
+            rows_in = self._xb(w, "rows_in", B, ld)
             comm.all_to_all(rows_in[:B], rows_out[:R], w.send_splits, w.recv_splits)
-            comm.all_to_all(rb_in[:B], rb_out[:R], w.send_splits, w.recv_splits)
-            call("rg_rows_unslot", rows_in.data_ptr(), rb_in.data_ptr(), w.tslot.data_ptr(), w.t32.data_ptr(), B,
-                 HF, w.tW.data_ptr(), w.tb.data_ptr(), w.trow.data_ptr(), st)
+            call("rg_rows_unslot", rows_in.data_ptr(), ld, w.tslot.data_ptr(), w.t32.data_ptr(), B, HF,
+                 w.tW.data_ptr(), w.tb.data_ptr(), w.trow.data_ptr(), st)
         hp = h_planes.data_ptr() if h_planes is not None else None
         with region("sampled_fwd", exact=True):   # the one-launch logits on the exchanged planes (draw = 2)
             call("rg_sampled_logits", h.data_ptr(), W, b, w.ids.data_ptr(), 2, self.seed, self.draws, self.A_full,
@@ -1510,11 +1523,11 @@ class ShardedSampledHead(SampledSoftmaxHead):
         with region("neg_grad_exchange"):
             comm.all_reduce(w.grows[:S])   # every rank's rows' part of the negatives' gradients
             comm.all_reduce(w.gb[:S])
+            ld = HF + 4
             call("rg_rows_slot", w.grows.data_ptr() + 4 * S * HF, w.gb.data_ptr() + 4 * S, w.tslot.data_ptr(), B,
-                 HF, w.gsend.data_ptr(), w.gbsend.data_ptr(), st)
-            grecv, gbrecv = self._xb(w, "grecv", max(R, 1), HF), self._xb(w, "gbrecv", max(R, 1))
+                 HF, ld, w.gsend.data_ptr(), st)
+            grecv = self._xb(w, "grecv", max(R, 1), ld)
             comm.all_to_all(grecv[:R], w.gsend[:B], w.recv_splits, w.send_splits)
-            comm.all_to_all(gbrecv[:R], w.gbsend[:B], w.recv_splits, w.send_splits)
         self.tag += 1
         with region("sampled_bwd"):
             G, Gb, tags = self.G.data_ptr(), self.Gb.data_ptr(), self.tags.data_ptr()
@@ -1525,9 +1538,9 @@ class ShardedSampledHead(SampledSoftmaxHead):
             if R > 0:
                 w.nR.fill_(R)
                 self.scatter(w.local_ids.data_ptr(), grecv.data_ptr(), HF, w.nR.data_ptr(), R, -1, G, self.A, tags,
-                             self.tag, st)
-                self.scatter(w.local_ids.data_ptr(), gbrecv.data_ptr(), 1, w.nR.data_ptr(), R, -1, Gb, self.A, tags,
-                             self.tag, st, reuse_sort=True)
+                             self.tag, st, ld=ld)
+                self.scatter(w.local_ids.data_ptr(), grecv.data_ptr() + 4 * HF, 1, w.nR.data_ptr(), R, -1, Gb, self.A,
+                             tags, self.tag, st, reuse_sort=True, ld=ld)
         with region("sampled_adam"):
             call("rg_adam_rows", self.W.p.data_ptr(), self.W.m.data_ptr(), self.W.v.data_ptr(), self.G.data_ptr(),
                  self.tags.data_ptr(), self.tag, self.A, HF, adam6, st)

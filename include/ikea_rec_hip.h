@@ -51,10 +51,11 @@ int rg_gather(const int64_t* s, int B, int L, const int32_t* perm, const int32_t
  * row order, so the result does not depend on scheduling — and tagged with `tag` for
  * rg_adam_rows.  Also the sampled head's row gradients.  work: rg_scatter_rows_work_bytes;
  * reuse_sort = 1 reuses the sorted order of the previous call on the same work buffer (same ids,
- * n_ptr, n_max, skip_id, n_rows): a second source over the same rows (the sampled head's bias). */
+ * n_ptr, n_max, skip_id, n_rows): a second source over the same rows (the sampled head's bias).
+ * Source row i is E floats at src + i·lds (lds >= E; 16-B aligned rows when E % 4 == 0). */
 int64_t rg_scatter_rows_work_bytes(int n_max, int E, int64_t n_rows);
-int rg_scatter_rows(const int32_t* ids, const float* src, int E, const int32_t* n_ptr, int n_max, int skip_id,
-                    float* G, int64_t n_rows, int32_t* tags, int32_t tag, int reuse_sort, void* work,
+int rg_scatter_rows(const int32_t* ids, const float* src, int E, int lds, const int32_t* n_ptr, int n_max,
+                    int skip_id, float* G, int64_t n_rows, int32_t* tags, int32_t tag, int reuse_sort, void* work,
                     int64_t work_bytes, rg_stream_t stream);
 
 /* ---- A5 dense contractions of the GRU (input projection W_ih x + b_ih, its
@@ -456,28 +457,44 @@ int rg_bpr_rows(const float* h, const float* W, const float* bias, const int64_t
 int rg_bpr_dz(float* Z, int64_t zsb, int64_t zss, const float* zpos, int B, int S, float gscale, float* slabs,
               float* dbg, rg_stream_t stream);
 
-/* ---- §8e row-sharded item-embedding table (csrc/emb_shard.hip): the multi-GPU form of
- * self.embedding(s) and its dense gradient + Adam (GRU4Rec/model.py:35-47, 69, 150-153).  Rank r
- * holds rows [⌊r·n_rows/world⌋, ⌊(r+1)·n_rows/world⌋).  Per trunk pass:
+/* ---- §8e row-sharded item-embedding table (csrc/emb_shard.hip, csrc/segsum.hip): the multi-GPU
+ * form of self.embedding(s) and its dense gradient + Adam (GRU4Rec/model.py:35-47, 69, 150-153).
+ * Rank r holds rows [⌊r·n_rows/world⌋, ⌊(r+1)·n_rows/world⌋).  Per trunk pass each DISTINCT id of
+ * the rank's batch is requested once:
  * rg_token_ids: tok_id[t] = item id of packed token t (forward time order; -1 + err if invalid).
- * rg_shard_route: stable partition of the T = *ntok_ptr tokens by owner rank: slot[t] (send
- *   position), send_ids[slot[t]] = tok_id[t], counts[world] (world <= 8).
+ * rg_shard_dedup: over the T = *n_ptr tokens (n_max >= T): uids[0..U) = the distinct ids in
+ *   increasing order (-1 first when a token was invalid: it goes to rank 0, whose gather returns a
+ *   zero row), uslot[t] = the token's index into uids, counts[o] = distinct ids owned by rank o
+ *   (world <= 256; uids is grouped by owner), *nuniq = U.  work: rg_shard_dedup_work_bytes(n_max,
+ *   E, n_rows); it keeps the sorted order for rg_shard_dedup_grads of the same pass.
+ * rg_shard_dedup_grads: gsend[u] = Σ_{t : uslot[t] = u} src[t] (E floats per row, summed in token
+ *   order — deterministic), for the pass's last rg_shard_dedup on `work` (same n_max, n_rows).
+ * rg_shard_route: stable partition of the T = *ntok_ptr rows by owner rank: slot[t] (send
+ *   position), send_ids[slot[t]] = tok_id[t], counts[world] (world <= 8; the sharded sampled
+ *   head's per-row target exchange).
  * rg_rows_gather: owner side, rows of n received global ids from the local shard [lo, lo + n_local)
  *   (fp32, or fp16 when half = 1) and local_ids (id − lo, or -1 with a zero row).
- * rg_place_rows: X[t] = rows_in[slot[t]] widened to fp32; reverse = 1: each row's valid prefix
- *   reversed (the backward direction of BidirGRU4Rec).
- * rg_collect_grads: gsend[slot[t]] = dX0[t] + dX1[rev t] (dX1 optional) — the row-gradients each
- *   owner adds into its rows (rg_scatter_rows with local_ids) before rg_adam_rows on its shard. */
+ * rg_place_rows: X[t] = rows_in[slot[t]] widened to fp32 (slot = uslot); reverse = 1: each row's
+ *   valid prefix reversed (the backward direction of BidirGRU4Rec).
+ * rg_combine_dirs: dX0[t] += dX1[rev t] in place (Bidir: both directions' token gradients before
+ *   rg_shard_dedup_grads).  The owner adds the received per-id sums into its rows
+ *   (rg_scatter_rows with local_ids) before rg_adam_rows on its shard. */
 int rg_token_ids(const int64_t* s, int B, int L, const int32_t* perm, const int32_t* lsort, const int32_t* offs,
                  int64_t n_rows, int32_t* tok_id, int32_t* err, rg_stream_t stream);
+int64_t rg_shard_dedup_work_bytes(int n_max, int E, int64_t n_rows);
+int rg_shard_dedup(const int32_t* tok_id, const int32_t* n_ptr, int n_max, int64_t n_rows, int world, int E,
+                   int32_t* uslot, int32_t* uids, int32_t* counts, int32_t* nuniq, void* work, int64_t work_bytes,
+                   rg_stream_t stream);
+int rg_shard_dedup_grads(const float* src, int E, int n_max, int64_t n_rows, float* gsend, void* work,
+                         int64_t work_bytes, rg_stream_t stream);
 int rg_shard_route(const int32_t* tok_id, const int32_t* ntok_ptr, int64_t n_rows, int world, int32_t* slot,
                    int32_t* send_ids, int32_t* counts, rg_stream_t stream);
 int rg_rows_gather(const int32_t* ids, int n, int64_t lo, int64_t n_local, const void* table, int E, int half,
                    void* rows, int32_t* local_ids, rg_stream_t stream);
 int rg_place_rows(const void* rows_in, int half, const int32_t* slot, const int32_t* lsort, const int32_t* offs, int B,
                   int E, int reverse, float* X, rg_stream_t stream);
-int rg_collect_grads(const float* dX0, const float* dX1, const int32_t* slot, const int32_t* lsort,
-                     const int32_t* offs, int B, int E, float* gsend, rg_stream_t stream);
+int rg_combine_dirs(float* dX0, const float* dX1, const int32_t* lsort, const int32_t* offs, int B, int E,
+                    rg_stream_t stream);
 
 /* ---- §8e item-sharded sampled head (csrc/sampled_shard.hip; the multi-GPU form of the
  * build-defined sampled softmax that replaces GRU4Rec/model.py:58-60, 80 in config C3).  Rank r
@@ -489,21 +506,23 @@ int rg_collect_grads(const float* dX0, const float* dX1, const int32_t* slot, co
  * rg_target_ids: int32 routing ids of n int64 targets (-1 outside [0, A)), *n_out = n (for
  *   rg_shard_route with n_rows = A).
  * rg_head_rows_gather: owner side, W rows and biases of n received item ids from the local shard
- *   [lo, lo + n_local) (zeros, local_ids -1 when not held).
- * rg_rows_unslot: tW[b] = rows[slot[b]], tb[b] = rb[slot[b]], trow[b] = b (the CE's per-row target
- *   into tW / tb); where tid32[b] < 0 a zero row and trow[b] = -1, so rg_sampled_lse writes a NaN
- *   loss row with zero gradients, as the one-GPU head does for an invalid target.
- * rg_rows_slot: gsend[slot[b]] = grows[b], gbsend[slot[b]] = gb[b] (the targets' row gradients
- *   back to their owners). */
+ *   [lo, lo + n_local): row k at rows + k·ld (ld >= HF + 1, ld % 4 == 0), its bias at + HF (zeros,
+ *   local_ids -1 when not held) — rows and biases travel in ONE all-to-all.
+ * rg_rows_unslot: tW[b] = row slot[b] of `rows` (stride ld), tb[b] = its bias, trow[b] = b (the CE's
+ *   per-row target into tW / tb); where tid32[b] < 0 a zero row and trow[b] = -1, so
+ *   rg_sampled_lse writes a NaN loss row with zero gradients, as the one-GPU head does for an
+ *   invalid target.
+ * rg_rows_slot: row slot[b] of gsend (stride ld) = grows[b], its bias entry = gb[b] (the targets'
+ *   row and bias gradients back to their owners in one all-to-all). */
 int rg_neg_pick(uint64_t seed, uint64_t counter, int64_t A, int S, int HF, int64_t lo, int64_t hi, const float* W,
                 const float* bias, int32_t* ids, int32_t* nloc, float* Wg, float* bg, rg_stream_t stream);
 int rg_neg_planes(const float* Wg, int S, int HF, void* Wp, rg_stream_t stream);
 int rg_target_ids(const int64_t* tgt, int n, int64_t A, int32_t* out, int32_t* n_out, rg_stream_t stream);
 int rg_head_rows_gather(const int32_t* ids, int n, int64_t lo, int64_t n_local, const float* W, const float* bias,
-                        int HF, float* rows, float* rb, int32_t* local_ids, rg_stream_t stream);
-int rg_rows_unslot(const float* rows, const float* rb, const int32_t* slot, const int32_t* tid32, int n, int HF,
-                   float* tW, float* tb, int64_t* trow, rg_stream_t stream);
-int rg_rows_slot(const float* grows, const float* gb, const int32_t* slot, int n, int HF, float* gsend, float* gbsend,
+                        int HF, int ld, float* rows, int32_t* local_ids, rg_stream_t stream);
+int rg_rows_unslot(const float* rows, int ld, const int32_t* slot, const int32_t* tid32, int n, int HF, float* tW,
+                   float* tb, int64_t* trow, rg_stream_t stream);
+int rg_rows_slot(const float* grows, const float* gb, const int32_t* slot, int n, int HF, int ld, float* gsend,
                  rg_stream_t stream);
 
 /* items per online-softmax partial block of rg_head_fwd: pmax/psum/parg hold ceil(A/that) x B */

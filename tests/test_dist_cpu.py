@@ -132,26 +132,31 @@ def test_item_shard_partition():
 
 
 def test_owner_counts_match_token_rules():
-    """dist.owner_counts (host routing) = the tokens k_token_ids / k_shard_route
-    send to each owner: t < clamp(len, 1, L) (all L unpacked), owner by
-    item_shard ranges, ids outside [0, N1) to rank 0."""
+    """dist.owner_counts (host routing) = the distinct ids k_token_ids /
+    rg_shard_dedup send to each owner: tokens t < clamp(len, 1, L) (all L
+    unpacked), owner by item_shard ranges, every id outside [0, N1) one entry
+    of rank 0; repeated calls (the reused bitmap) agree."""
     import numpy as np
     sys.path.insert(0, os.path.join(REPO, "ikea-recommender-system_amd"))
     from recommenders.hip.dist import item_shard, owner_counts
     rng = np.random.default_rng(3)
-    for N1, W, L, packed in ((1001, 8, 7, True), (50, 3, 5, False), (9, 2, 4, True)):
-        s = rng.integers(-2, N1 + 3, size=(13, L))
-        lens = rng.integers(0, L + 3, size=13)
-        exp = np.zeros(W, dtype=np.int64)
-        for b in range(13):
-            n = L if not packed else min(max(int(lens[b]), 1), L)
-            for t in range(n):
-                i = int(s[b, t])
-                o = 0
-                if 0 <= i < N1:
-                    o = next(r for r in range(W) if item_shard(N1, W, r)[0] <= i < item_shard(N1, W, r)[1])
-                exp[o] += 1
-        np.testing.assert_array_equal(owner_counts(s, lens, L, packed, N1, W), exp)
+    for N1, W, L, packed, lo_id in ((1001, 8, 7, True, -2), (50, 3, 5, False, -2), (9, 2, 4, True, -2),
+                                    (1001, 8, 7, True, 0), (200, 3, 30, True, 0)):
+        for rep in range(2):
+            s = rng.integers(lo_id, N1 + (3 if lo_id < 0 else 0), size=(13, L))
+            lens = rng.integers(0, L + 3, size=13)
+            seen = [set() for _ in range(W)]
+            for b in range(13):
+                n = L if not packed else min(max(int(lens[b]), 1), L)
+                for t in range(n):
+                    i = int(s[b, t])
+                    if 0 <= i < N1:
+                        o = next(r for r in range(W) if item_shard(N1, W, r)[0] <= i < item_shard(N1, W, r)[1])
+                        seen[o].add(i)
+                    else:
+                        seen[0].add(-1)
+            exp = np.array([len(x) for x in seen], dtype=np.int64)
+            np.testing.assert_array_equal(owner_counts(s, lens, L, packed, N1, W), exp)
 
 
 def test_target_owner_counts_match_item_shard():

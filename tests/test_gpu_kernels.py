@@ -447,11 +447,12 @@ def test_scatter_rows_deterministic(E, n_rows, n, n_max):
         G = torch.zeros(n_rows, E, device=dev)
         G[0] = 1.0                                      # adds, not overwrites
         tags = torch.zeros(n_rows, dtype=torch.int32, device=dev)
-        C().call("rg_scatter_rows", D(ids).data_ptr(), D(src).data_ptr(), E, n_t.data_ptr(), n_max, skip,
+        C().call("rg_scatter_rows", D(ids).data_ptr(), D(src).data_ptr(), E, E, n_t.data_ptr(), n_max, skip,
                  G.data_ptr(), n_rows, tags.data_ptr(), 9, 0, work.data_ptr(), nb, st())
-        # a second source over the same rows reuses the sort (the sampled head's bias)
+        # a second source over the same rows reuses the sort (the sampled head's bias): column 0 of
+        # the same rows, read with the row stride E
         G1 = torch.zeros(n_rows, 1, device=dev)
-        C().call("rg_scatter_rows", D(ids).data_ptr(), D(src[:, :1].contiguous()).data_ptr(), 1, n_t.data_ptr(),
+        C().call("rg_scatter_rows", D(ids).data_ptr(), D(src).data_ptr(), 1, E, n_t.data_ptr(),
                  n_max, skip, G1.data_ptr(), n_rows, tags.data_ptr(), 9, 1, work.data_ptr(), nb, st())
         torch.cuda.synchronize()
         outs.append((G.cpu(), tags.cpu(), G1.cpu()))
@@ -510,3 +511,58 @@ def test_gru_forward_emits_h_planes(H, ndir, B, L):
         blk = outs[1][1][n:].view(HF // 16, 3, 2, 32, 16)[..., :B % 32, :]
         rblk = ref[n:].view(HF // 16, 3, 2, 32, 16)[..., :B % 32, :]
         assert torch.equal(blk, rblk)
+
+
+@pytest.mark.parametrize("n_rows,W,n,n_max,E,zipf", [(1_000_001, 8, 88_000, 90_000, 128, True),
+                                                     (53, 3, 700, 700, 4, False), (9001, 2, 1, 64, 64, False),
+                                                     (5_000_001, 8, 30_000, 30_000, 256, True)])
+def test_shard_dedup_distinct_ids_and_sums(n_rows, W, n, n_max, E, zipf):
+    """rg_shard_dedup (the row-sharded table's deduplicated exchange, csrc/
+    segsum.hip): the distinct ids sorted (−1 first for invalid tokens), every
+    token's index into them, the per-owner counts of dist.owner_counts'
+    rules; rg_shard_dedup_grads: per distinct id the sum of its tokens' rows
+    (fp64 reference) — bitwise repeatable; Zipf-hot ids whose runs cross many
+    64-position blocks."""
+    from recommenders.hip.dist import item_shard
+    rng = np.random.default_rng(n)
+    if zipf:
+        ids = (rng.zipf(1.3, size=n) - 1) % n_rows
+    else:
+        ids = rng.integers(0, n_rows, size=n)
+    ids = ids.astype(np.int64)
+    if n > 10:
+        ids[rng.integers(0, n, size=5)] = -1     # invalid tokens (k_token_ids writes -1)
+    tok = D(torch.from_numpy(ids.astype(np.int32)))
+    nptr = D(torch.tensor([n], dtype=torch.int32))
+    call = C().call
+    wb = call("rg_shard_dedup_work_bytes", n_max, E, n_rows)
+    work = torch.empty(wb, dtype=torch.uint8, device=dev)
+    uslot = torch.full((n_max,), -7, dtype=torch.int32, device=dev)
+    uids = torch.full((n_max,), -7, dtype=torch.int32, device=dev)
+    counts = torch.zeros(W, dtype=torch.int32, device=dev)
+    nuniq = torch.zeros(1, dtype=torch.int32, device=dev)
+    call("rg_shard_dedup", tok.data_ptr(), nptr.data_ptr(), n_max, n_rows, W, E, uslot.data_ptr(), uids.data_ptr(),
+         counts.data_ptr(), nuniq.data_ptr(), work.data_ptr(), wb, st())
+    src = torch.from_numpy(rng.standard_normal((n, E)).astype(np.float32))
+    srcd = D(src)
+    g1 = torch.full((n_max, E), 3.0, device=dev)
+    g2 = torch.full((n_max, E), -3.0, device=dev)
+    call("rg_shard_dedup_grads", srcd.data_ptr(), E, n_max, n_rows, g1.data_ptr(), work.data_ptr(), wb, st())
+    call("rg_shard_dedup_grads", srcd.data_ptr(), E, n_max, n_rows, g2.data_ptr(), work.data_ptr(), wb, st())
+    torch.cuda.synchronize()
+    U = int(nuniq.item())
+    exp_u = np.unique(ids)
+    assert U == exp_u.size
+    np.testing.assert_array_equal(uids[:U].cpu().numpy(), exp_u)
+    sl = uslot[:n].cpu().numpy()
+    np.testing.assert_array_equal(exp_u[sl], ids)
+    seen = np.zeros(W, dtype=np.int64)
+    for x in exp_u:
+        seen[0 if x < 0 else next(r for r in range(W) if item_shard(n_rows, W, r)[0] <= x < item_shard(n_rows, W, r)[1])] += 1
+    np.testing.assert_array_equal(counts.cpu().numpy(), seen)
+    ref = np.zeros((U, E))
+    np.add.at(ref, sl, src.numpy().astype(np.float64))
+    got = g1[:U].cpu().numpy()
+    scale = np.maximum(1.0, np.sqrt(np.bincount(sl, minlength=U)))[:, None]
+    assert (np.abs(got - ref) <= 1e-5 * scale).all()
+    assert torch.equal(g1[:U], g2[:U])   # fixed order: bitwise repeatable, stored not added

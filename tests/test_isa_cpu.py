@@ -12,9 +12,9 @@ VMEM instructions before the wait.  A compiler change that moved another
 VMEM op after them would make the barrier under-wait and silently corrupt
 logits or gradients, so this test compiles head_flash.hip with the build's
 own flags and checks, for every such wait in every ZS / ZL instantiation,
-that the four preceding VMEM instructions (program order) are the expected
-four: stores in pass 1; LDS-DMA loads through one buffer resource (the z
-tile's) in pass 2."""
+that the four preceding VMEM instructions — in program order, over every
+control-flow path into the wait — are the expected four: stores in pass 1;
+LDS-DMA loads through one buffer resource (the z tile's) in pass 2."""
 import os
 import re
 import shutil
@@ -49,25 +49,113 @@ def _functions(asm):
                 name = None
                 continue
             t = line.split(";")[0].rstrip()
-            if t.strip() and not t.strip().startswith("."):
-                body.append(t)
+            if t.strip() and (not t.strip().startswith(".") or re.match(r"^\.LBB\S+:", t.strip())):
+                body.append(t)   # instructions and block labels
     return out
 
 
 def _hand_waits(body):
-    """Indices of `s_waitcnt vmcnt(4) …` immediately followed by s_barrier."""
-    return [i for i, l in enumerate(body)
-            if re.match(r"^\s*s_waitcnt\s+vmcnt\(4\)", l) and i + 1 < len(body)
-            and body[i + 1].strip().startswith("s_barrier")]
-
-
-def _last_vmem(body, i, n=4):
+    """Indices of `s_waitcnt vmcnt(4) lgkmcnt(0)` that reach an s_barrier
+    with no memory instruction or block edge in between (the scheduler may
+    move ALU work between the two)."""
     out = []
-    j = i - 1
-    while j >= 0 and len(out) < n:
-        if VMEM.match(body[j]):
-            out.append(body[j].strip())
-        j -= 1
+    for i, l in enumerate(body):
+        if not re.match(r"^\s*s_waitcnt\s+vmcnt\(4\)\s+lgkmcnt\(0\)", l):
+            continue
+        for j in range(i + 1, len(body)):
+            t = body[j].strip()
+            if t.startswith("s_barrier"):
+                out.append(i)
+                break
+            if (VMEM.match(t) or t.startswith(("ds_", "s_waitcnt", ".LBB")) or
+                    re.match(r"^s_(branch|cbranch_\w+|endpgm)\b", t)):
+                break
+    return out
+
+
+def _cfg(body):
+    """Basic blocks of a kernel body: (starts, block_of_index, preds)."""
+    starts = [0]
+    for i, l in enumerate(body):
+        t = l.strip()
+        if re.match(r"^\.LBB\S+:", t) and i not in starts:
+            starts.append(i)
+        elif re.match(r"^s_(branch|cbranch_\w+|endpgm|setpc_b64)\b", t) and i + 1 < len(body):
+            starts.append(i + 1)
+    starts = sorted(set(starts))
+    label_block = {}
+    for k, st in enumerate(starts):
+        m = re.match(r"^(\.LBB\S+):", body[st].strip())
+        if m:
+            label_block[m.group(1)] = k
+    preds = {k: [] for k in range(len(starts))}
+    for k, st in enumerate(starts):
+        end = starts[k + 1] if k + 1 < len(starts) else len(body)
+        last = body[end - 1].strip()
+        m = re.match(r"^s_(branch|cbranch_\w+)\s+(\.LBB\S+)", last)
+        succ = []
+        if m:
+            succ.append(label_block[m.group(2)])
+            if m.group(1) != "branch" and k + 1 < len(starts):
+                succ.append(k + 1)
+        elif not re.match(r"^s_(endpgm|setpc_b64)\b", last) and k + 1 < len(starts):
+            succ.append(k + 1)
+        for q in succ:
+            preds[q].append(k)
+    block_of = []
+    for k, st in enumerate(starts):
+        end = starts[k + 1] if k + 1 < len(starts) else len(body)
+        block_of += [k] * (end - st)
+    return starts, block_of, preds
+
+
+def _kind(line):
+    """Abstract VMEM instruction: a store, an LDS-DMA load through buffer
+    resource s[a:b], or another op (its opcode)."""
+    op = line.split()[0]
+    if "store" in op:
+        return "store"
+    if op == "buffer_load_dwordx4" and line.endswith(" lds"):
+        return "lds " + re.search(r"s\[\d+:\d+\]", line).group(0)
+    return op
+
+
+def _last_vmem_kinds(body, n=4):
+    """For every `s_waitcnt vmcnt(…)` index i of the body: the set of possible
+    kinds of the n VMEM instructions preceding it in program order, over all
+    control-flow paths (newest first) — a forward dataflow fixed point over
+    the basic blocks."""
+    starts, block_of, preds = _cfg(body)
+    nb = len(starts)
+    ends = [starts[k + 1] if k + 1 < nb else len(body) for k in range(nb)]
+    kinds = [_kind(body[j].strip()) if VMEM.match(body[j]) else None for j in range(len(body))]
+
+    def run(states, lo, hi):
+        add = tuple(kinds[j] for j in range(hi - 1, lo - 1, -1) if kinds[j] is not None)
+        return {(add + st)[:n] for st in states} if add else set(states)
+
+    succs = {k: [] for k in range(nb)}
+    for q, ps in preds.items():
+        for pb in ps:
+            succs[pb].append(q)
+    entry = {k: set() for k in range(nb)}
+    entry[0] = {()}
+    exit_ = {k: None for k in range(nb)}
+    work = list(range(nb))
+    while work:
+        k = work.pop()
+        new = run(entry[k], starts[k], ends[k])
+        if new != exit_[k]:
+            exit_[k] = new
+            for q in succs[k]:
+                if not new <= entry[q]:
+                    entry[q] |= new
+                    work.append(q)
+    out = {}
+    for i, l in enumerate(body):
+        if re.match(r"^\s*s_waitcnt\s+vmcnt", l):
+            b = block_of[i]
+            out[i] = run(entry[b], starts[b], i)
     return out
 
 
@@ -95,18 +183,18 @@ def test_stored_logit_waits_cover_only_the_z_traffic(asm):
     for name, body in zs.items():
         waits = _hand_waits(body)
         assert waits, name
+        kinds = _last_vmem_kinds(body)
         for i in waits:
-            last = _last_vmem(body, i)
-            assert len(last) == 4 and all("store" in l for l in last), (name, i, last)
-            checked += 1
+            for last in kinds[i]:
+                assert last == ("store",) * 4, (name, i, last)
+                checked += 1
     for name, body in zl.items():
         waits = _hand_waits(body)
         assert waits, name
+        kinds = _last_vmem_kinds(body)
         for i in waits:
-            last = _last_vmem(body, i)
-            assert len(last) == 4 and all(l.startswith("buffer_load_dwordx4") and l.endswith(" lds")
-                                          for l in last), (name, i, last)
-            rsrc = {re.search(r"s\[\d+:\d+\]", l).group(0) for l in last}
-            assert len(rsrc) == 1, (name, i, last)   # one buffer resource: the z tile's
-            checked += 1
+            for last in kinds[i]:
+                # four LDS-DMA loads through one buffer resource: the z tile's
+                assert len(last) == 4 and len(set(last)) == 1 and last[0].startswith("lds "), (name, i, last)
+                checked += 1
     assert checked >= 2 * (len(zs) + len(zl))

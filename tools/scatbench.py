@@ -18,7 +18,7 @@ for n_max, n, E, rows in ((204800, 90000, 128, 1000001), (6144, 6144, 128, 10000
     nt = torch.tensor([n], dtype=torch.int32, device=dev)
     nb = call("rg_scatter_rows_work_bytes", n_max, E, rows)
     work = torch.empty(nb, dtype=torch.uint8, device=dev)
-    f = lambda: call("rg_scatter_rows", ids.data_ptr(), src.data_ptr(), E, nt.data_ptr(), n_max, -1, G.data_ptr(),
+    f = lambda: call("rg_scatter_rows", ids.data_ptr(), src.data_ptr(), E, E, nt.data_ptr(), n_max, -1, G.data_ptr(),
                      rows, tags.data_ptr(), 1, 0, work.data_ptr(), nb, stream_ptr())
     for _ in range(3):
         f()
