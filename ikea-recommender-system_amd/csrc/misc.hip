@@ -47,6 +47,91 @@ extern "C" int rg_weighted_sum(const float* const* X, const float* w, int nh, in
   return RG_OK;
 }
 
+// The SMORL double-Q target's combined head in one pass over the nh Q heads
+// (tensor_operations.py:50-70 through the weighted argmax): per (item row x,
+// 8-value group g) the same fp32 sum as k_weighted_sum (W_0·w_0 + W_1·w_1 +
+// ..., in head order: bitwise rg_weighted_sum's W_comb), written as fp32
+// (the exact re-scoring reads it) and as its three bf16 K-planes (the
+// screening argmax's operand, common.h kplane16: bitwise rg_head_planes);
+// the biases likewise into b_comb and the −inf-padded bias; and the largest
+// row norm ||W_comb[x]||₂ (the screening's error bound) by one atomicMax of
+// the non-negative float bits per wave (order-independent: deterministic).
+// Replaces rg_weighted_sum (W, b) + rg_head_planes + rg_row_norm_max: the Q
+// heads are read once and W_comb is not re-read.
+template <int HF>
+__global__ __launch_bounds__(256) void k_qcomb(Ptr4 in, Ptr4 inb, int nh, int A, int Ap, float* __restrict__ Wc,
+                                               float* __restrict__ bc, bf16x8* __restrict__ P,
+                                               float* __restrict__ bias_pad, float* __restrict__ wnorm) {
+  constexpr int G = HF / 8;   // threads per item row (a power of two dividing 64)
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int x = (int)(i / G), g = (int)(i % G);
+  f4 lo = {0.f, 0.f, 0.f, 0.f}, hi = lo;
+  float ss = 0.f;
+  if (x < A) {
+    const int64_t off = (int64_t)x * HF + 8 * g;
+    lo = *reinterpret_cast<const f4*>(in.p[0] + off) * in.w[0];
+    hi = *reinterpret_cast<const f4*>(in.p[0] + off + 4) * in.w[0];
+    for (int k = 1; k < nh; ++k) {
+      lo = lo + *reinterpret_cast<const f4*>(in.p[k] + off) * in.w[k];
+      hi = hi + *reinterpret_cast<const f4*>(in.p[k] + off + 4) * in.w[k];
+    }
+    *reinterpret_cast<f4*>(Wc + off) = lo;
+    *reinterpret_cast<f4*>(Wc + off + 4) = hi;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) ss = fmaf(lo[u], lo[u], fmaf(hi[u], hi[u], ss));
+    if (g == 0) {
+      float sb = inb.p[0][x] * inb.w[0];
+      for (int k = 1; k < nh; ++k) sb = sb + inb.p[k][x] * inb.w[k];
+      bc[x] = sb;
+      bias_pad[x] = sb;
+    }
+  } else if (x < Ap && g == 0) {
+    bias_pad[x] = -__builtin_inff();
+  }
+  if (x < Ap) {   // (rows past A: zero planes, as rg_head_planes pads the last chunk)
+    bf16x8 p0, p1, p2;
+    split3x8(lo, hi, p0, p1, p2);
+    const int64_t base = kplane16(x, g, HF);
+    P[base] = p0;
+    P[base + 64] = p1;
+    P[base + 128] = p2;
+  }
+#pragma unroll
+  for (int o = G / 2; o >= 1; o >>= 1) ss += __shfl_xor(ss, o);
+  float best = sqrtf(ss);
+#pragma unroll
+  for (int o = 32; o >= G; o >>= 1) best = fmaxf(best, __shfl_xor(best, o));
+  if ((threadIdx.x & 63) == 0) atomicMax(reinterpret_cast<unsigned int*>(wnorm), __float_as_uint(best));
+}
+
+extern "C" int rg_qcomb(const float* const* W, const float* const* b, const float* w, int nh, int A, int HF,
+                        float* Wc, float* bc, void* planes_k, float* bias_pad, float* wnorm, hipStream_t stream) {
+  if (nh <= 0 || nh > 4 || A <= 0 || !W || !b || !w || !Wc || !bc || !planes_k || !bias_pad || !wnorm)
+    return RG_ERR_ARG;
+  if (HF != 32 && HF != 64 && HF != 128 && HF != 256) return RG_ERR_SHAPE;
+  Ptr4 in{}, inb{};
+  for (int k = 0; k < nh; ++k) {
+    in.p[k] = W[k];
+    inb.p[k] = b[k];
+    in.w[k] = inb.w[k] = w[k];
+  }
+  if (hipMemsetAsync(wnorm, 0, sizeof(float), stream) != hipSuccess) return RG_ERR_LAUNCH;
+  const int Ap = (A + 31) / 32 * 32;
+  const unsigned grid = (unsigned)(((int64_t)Ap * (HF / 8) + 255) / 256);
+#define QC(HFV)                                                                                            \
+  hipLaunchKernelGGL(k_qcomb<HFV>, dim3(grid), dim3(256), 0, stream, in, inb, nh, A, Ap, Wc, bc,         \
+                     reinterpret_cast<bf16x8*>(planes_k), bias_pad, wnorm)
+  switch (HF) {
+    case 32: QC(32); break;
+    case 64: QC(64); break;
+    case 128: QC(128); break;
+    case 256: QC(256); break;
+  }
+#undef QC
+  RG_LAUNCH_CHECK();
+  return RG_OK;
+}
+
 extern "C" int rg_abi_version(void) { return 1; }
 
 // SMORL reward matrix r = stack([r_acc, r_div, r_nov], 1).to(float32)

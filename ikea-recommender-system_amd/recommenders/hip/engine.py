@@ -610,16 +610,49 @@ class _FlashWS:
         if top_k >= 1:
             self.pbest, self.parg = z(self.nsplit, B), z(self.nsplit, B, dt=torch.int32)
             self.top_idx, self.top_val = z(B, top_k, dt=torch.int32), z(B, top_k)
-        # chunk maxima for the exact top-K (K = 1 too, while they fit
-        # SCREEN_CMAX_BYTES; else K = 1 runs the row-chunked screening argmax
-        # on this workspace's planes, SoftmaxHead.top_entries)
+        # chunk maxima for the exact top-K, from one buffer per device shared
+        # by every head (a pass 1 with top-k outputs is consumed by its
+        # top_entries on the same stream before any other head's pass 1); K = 1
+        # uses them while they fit the free device memory (CMAX_FREE_MARGIN),
+        # else the row-chunked screening argmax on this workspace's planes
+        # (SoftmaxHead.top_entries)
         self.top1 = None
-        if top_k > 1 or (top_k == 1 and -(-A // 32) * B * 4 <= SCREEN_CMAX_BYTES):
-            self.cmax = z(-(-A // 32), B)
+        cm = _shared_cmax(device, -(-A // 32) * B, required=top_k > 1) if top_k >= 1 else None
+        if cm is not None:
+            self.cmax = cm.view(-(-A // 32), B)
             self.cand = z(B, call("rg_flash_topk_cap"), dt=torch.int32)
             self.ncand = z(B, dt=torch.int32)
             self.tk_work = torch.empty(call("rg_flash_topk_work_bytes", B, A, top_k), dtype=torch.uint8,
                                        device=device)
+
+
+# the chunk maxima of the fused heads' top-k (_FlashWS.cmax): one growing
+# buffer per device; a K = 1 consumer takes it only while this much device
+# memory stays free beside it (else the screening argmax runs in row chunks)
+CMAX_FREE_MARGIN = 6 << 30
+_CMAX = {}
+
+
+def _shared_cmax(device, n, required):
+    """A float tensor of at least n elements shared by every head on
+    ``device`` (grown when needed), or None when K = 1 (not required) and it
+    would not fit beside CMAX_FREE_MARGIN of free memory."""
+    dev = torch.device(device)
+    t = _CMAX.get(dev)
+    if t is not None and t.numel() >= n:
+        return t[:n]
+    have = 0 if t is None else t.numel() * 4
+    if not required and torch.cuda.mem_get_info(dev)[0] + have - 4 * n < CMAX_FREE_MARGIN:
+        return None
+    _CMAX.pop(dev, None)
+    del t
+    try:
+        t = _CMAX[dev] = torch.empty(n, dtype=torch.float32, device=dev)
+    except torch.cuda.OutOfMemoryError:
+        if required:
+            raise
+        return None
+    return t
 
 
 # evaluation scoring (SoftmaxHead.score_topk): rows per chunk such that the
@@ -845,14 +878,14 @@ class SoftmaxHead:
 
     def zs_buffer(self, w):
         """The stored-logit buffer of workspace w, or None (recomputed in pass
-        2).  Needs HF <= 128 and B a multiple of pass 1's 256-row blocks.
+        2).  Needs B a multiple of pass 1's row blocks (256 rows; 128 at HF 256).
         ``zstore``: None = auto, True / False force it (tests).  Auto: one
         budget for all heads of the device — the buffers already held plus
         this one within ZSTORE_MAX_BYTES and within a third of (held + free
         device memory) — so a double-Q trainer's two heads cannot pin most of
         the HBM; an allocation that fails leaves the logits recomputed."""
         mode = getattr(self, "zstore", None)
-        if mode is False or self.HF > 128 or w.B % call("rg_flash_rows_per_block", self.HF):
+        if mode is False or w.B % call("rg_flash_rows_per_block", self.HF):
             return None
         if w.zs is None:
             nb = int(call("rg_flash_zs_bytes", w.B, self.A))
@@ -940,16 +973,18 @@ class SoftmaxHead:
              self.top_err.data_ptr(), st)
         return idx, vals
 
-    def _screened_argmax(self, aw, Hk, Wk, bias_pad, h, Wp, bp, out_idx, out_val):
+    def _screened_argmax(self, aw, Hk, Wk, bias_pad, h, Wp, bp, out_idx, out_val, wnorm_ready=False):
         """First maximum of the fp32 logits h·Wᵀ + b per row into out_idx /
         out_val: screening on 3 plane products (rows in aw.Bc chunks, so the
         chunk maxima fit SCREEN_CMAX_BYTES), then every item of every chunk
         within the screening's error bound re-scored in fp32
-        (rg_flash_argmax_exact; a row past the candidate cap is scanned whole)."""
+        (rg_flash_argmax_exact; a row past the candidate cap is scanned whole).
+        wnorm_ready: aw.wnorm already holds max_a ||W_a||₂ (rg_qcomb)."""
         B, A, HF = h.shape[0], self.A, self.HF
         st = stream_ptr()
         W, b = Wp.p.data_ptr(), bp.p.data_ptr()
-        call("rg_row_norm_max", W, A, HF, aw.wnorm.data_ptr(), st)
+        if not wnorm_ready:
+            call("rg_row_norm_max", W, A, HF, aw.wnorm.data_ptr(), st)
         hk_row = HF * 6   # K-plane bytes per row
         cap = call("rg_flash_topk_cap")
         for r0 in range(0, B, aw.Bc):
@@ -1161,11 +1196,23 @@ class SoftmaxHead:
                  self.A, self.HF, self.W.p.data_ptr(), self.W.m.data_ptr(), self.W.v.data_ptr(),
                  self.b.p.data_ptr(), self.b.m.data_ptr(), self.b.v.data_ptr(), adam6, None, None, st)
 
-    def argmax(self, h, slot="argmax"):
+    def amax_ws(self, slot, B):
+        """The screening-argmax workspace of ``slot`` for B rows."""
+        w = self._aws.get(slot) if hasattr(self, "_aws") else None
+        if w is None or w.B != B:
+            if not hasattr(self, "_aws"):
+                self._aws = {}
+            self._aws.pop(slot, None)
+            w = self._aws[slot] = _AmaxWS(B, self.A, self.HF, self.device, True)
+        return w
+
+    def argmax(self, h, slot="argmax", planes_ready=False):
         """argmax_j (h·Wᵀ + b)[b, j] without storing Z (first maximum); the
         row maxima are left in ``self.argmax_mx``.  With a split-bf16
         precision the contraction runs on bf16 MFMAs (csrc/head_flash.hip
-        k_flash_amax: pass 1's S-part with first-maximum tracking)."""
+        k_flash_amax: pass 1's S-part with first-maximum tracking).
+        planes_ready: the slot's workspace already holds W's K-planes, padded
+        bias and max row norm (QNet.argmax_q's rg_qcomb)."""
         B = h.shape[0]
         st = stream_ptr()
         terms = self.flash_terms(B)
@@ -1173,17 +1220,13 @@ class SoftmaxHead:
             # screening (3 plane products) + exact fp32 re-scoring of the
             # chunks within the error bound (rows in chunks when the chunk
             # maxima would not fit SCREEN_CMAX_BYTES)
-            w = self._aws.get(slot) if hasattr(self, "_aws") else None
-            if w is None or w.B != B:
-                if not hasattr(self, "_aws"):
-                    self._aws = {}
-                self._aws.pop(slot, None)
-                w = self._aws[slot] = _AmaxWS(B, self.A, self.HF, self.device, True)
+            w = self.amax_ws(slot, B)
             Wp, bp = self.W, self.b
             call("rg_head_planes", h.data_ptr(), B, self.HF, w.Hk.data_ptr(), None, None, None, st)
-            call("rg_head_planes", Wp.p.data_ptr(), self.A, self.HF, w.Wk.data_ptr(), None, bp.p.data_ptr(),
-                 w.bias_pad.data_ptr(), st)
-            self._screened_argmax(w, w.Hk, w.Wk, w.bias_pad, h, Wp, bp, w.amax, w.mx)
+            if not planes_ready:
+                call("rg_head_planes", Wp.p.data_ptr(), self.A, self.HF, w.Wk.data_ptr(), None, bp.p.data_ptr(),
+                     w.bias_pad.data_ptr(), st)
+            self._screened_argmax(w, w.Hk, w.Wk, w.bias_pad, h, Wp, bp, w.amax, w.mx, wnorm_ready=planes_ready)
             self.argmax_mx = w.mx
             return w.amax
         w = self.ws(slot, B, False)

@@ -110,6 +110,16 @@ class QNet(HipNet):
         hd = self._argmax_head
         wts = host_floats(weights)
         st = stream_ptr()
+        B = h.shape[0]
+        if hd.flash_terms(B):
+            # one pass over the Q heads: W_c, b_c, W_c's K-planes, padded bias and
+            # max row norm for the screening argmax (csrc/misc.hip rg_qcomb)
+            w = hd.amax_ws("argmax", B)
+            call("rg_qcomb", host_ptr_array([q.W.p for q in self.q_heads]),
+                 host_ptr_array([q.b.p for q in self.q_heads]), wts, len(self.q_heads), hd.A, hd.HF,
+                 hd.W.p.data_ptr(), hd.b.p.data_ptr(), w.Wk.data_ptr(), w.bias_pad.data_ptr(), w.wnorm.data_ptr(),
+                 st)
+            return hd.argmax(h, slot="argmax", planes_ready=True)
         call("rg_weighted_sum", host_ptr_array([q.W.p for q in self.q_heads]), wts, len(self.q_heads),
              hd.W.p.numel(), hd.W.p.data_ptr(), st)
         call("rg_weighted_sum", host_ptr_array([q.b.p for q in self.q_heads]), wts, len(self.q_heads),

@@ -566,3 +566,37 @@ def test_shard_dedup_distinct_ids_and_sums(n_rows, W, n, n_max, E, zipf):
     scale = np.maximum(1.0, np.sqrt(np.bincount(sl, minlength=U)))[:, None]
     assert (np.abs(got - ref) <= 1e-5 * scale).all()
     assert torch.equal(g1[:U], g2[:U])   # fixed order: bitwise repeatable, stored not added
+
+
+@pytest.mark.parametrize("A,HF,nh", [(20011, 128, 3), (777, 256, 2), (1000, 64, 3), (4096, 32, 1)])
+def test_qcomb_equals_weighted_sum_planes_norm(A, HF, nh):
+    """rg_qcomb (the SMORL target's combined Q head in one pass) against the
+    separate kernels it replaces: W_c / b_c bitwise rg_weighted_sum's, the
+    K-planes and padded bias bitwise rg_head_planes', the max row norm within
+    fp32 rounding of rg_row_norm_max's (another summation order) and of fp64."""
+    call = C().call
+    g = torch.Generator().manual_seed(A + HF)
+    Ws = [D(torch.randn(A, HF, generator=g) * 0.1) for _ in range(nh)]
+    bs = [D(torch.randn(A, generator=g) * 0.1) for _ in range(nh)]
+    wts = [1.0, 0.5, 2.0][:nh]
+    hw = C().host_floats(wts)
+    Wc, bc = torch.empty(A, HF, device=dev), torch.empty(A, device=dev)
+    pk = torch.empty(call("rg_head_plane_bytes", A, HF), dtype=torch.uint8, device=dev)
+    Ap = (A + 31) // 32 * 32
+    bp = torch.empty(Ap, device=dev)
+    wn = torch.full((1,), 7.0, device=dev)
+    call("rg_qcomb", C().host_ptr_array(Ws), C().host_ptr_array(bs), hw, nh, A, HF, Wc.data_ptr(), bc.data_ptr(),
+         pk.data_ptr(), bp.data_ptr(), wn.data_ptr(), st())
+    Wr, br = torch.empty_like(Wc), torch.empty_like(bc)
+    call("rg_weighted_sum", C().host_ptr_array(Ws), hw, nh, A * HF, Wr.data_ptr(), st())
+    call("rg_weighted_sum", C().host_ptr_array(bs), hw, nh, A, br.data_ptr(), st())
+    pk2 = torch.empty_like(pk)
+    bp2 = torch.empty_like(bp)
+    call("rg_head_planes", Wr.data_ptr(), A, HF, pk2.data_ptr(), None, br.data_ptr(), bp2.data_ptr(), st())
+    wn2 = torch.zeros(1, device=dev)
+    call("rg_row_norm_max", Wr.data_ptr(), A, HF, wn2.data_ptr(), st())
+    torch.cuda.synchronize()
+    assert torch.equal(Wc, Wr) and torch.equal(bc, br)
+    assert torch.equal(pk, pk2) and torch.equal(bp, bp2)
+    ref = float(Wr.double().norm(dim=1).max())
+    assert abs(float(wn) - float(wn2)) <= 2e-6 * ref and abs(float(wn) - ref) <= 2e-6 * ref
