@@ -387,15 +387,16 @@ def sampled_fwd_bytes(B, S, HF):
     return B * HF * 4 + B * 4 + S * 4 + (B + S) * (HF + 1) * 4 + B * (S + 1) * 4
 
 
-def exchange_bytes(T, B, S, E, HF):
+def exchange_bytes(U, B, S, E, HF):
     """Collective payload per rank of the item-sharded gather + sampled logits
-    (DESIGN §5): the token ids out and their table rows back, the negatives'
-    rows + biases all-reduced, the targets' ids out and rows + biases back."""
-    return {"token_ids": int(4 * T), "token_rows": int(4 * E * T), "neg_rows_allreduce": int(4 * S * (HF + 1)),
-            "target_ids": int(4 * B), "target_rows": int(4 * B * (HF + 1))}
+    (DESIGN §5): the batch's U distinct ids out and their table rows back
+    (rg_shard_dedup), the negatives' rows + biases all-reduced, the targets'
+    ids out and rows + biases back (HF + 4 floats per row, one all-to-all)."""
+    return {"distinct_ids": int(4 * U), "distinct_rows": int(4 * E * U), "neg_rows_allreduce": int(4 * S * (HF + 1)),
+            "target_ids": int(4 * B), "target_rows": int(4 * B * (HF + 4))}
 
 
-def target_step(kern, T, B, S, E, HF, n_gather, terms):
+def target_step(kern, T, B, S, E, HF, n_gather, terms, U=None):
     """North-star target: embedding gather + sampled logits (fwd) against the
     HBM roofline, with the logits' MFMA rate beside it.  On an
     item-sharded run the gather region is the whole exchange (route, id / row
@@ -414,7 +415,8 @@ def target_step(kern, T, B, S, E, HF, n_gather, terms):
            "sampled_fwd_ms": round(ts, 4), "sampled_fwd_alg_TFLOPs": round(fl / (ts * 1e-3) / 1e12, 2)}
     if "neg_exchange" in kern:
         out["neg_exchange_ms"] = round(tx, 4)
-        out["exchange_bytes_per_rank"] = exchange_bytes(T, B, S, E, HF)
+        out["exchange_bytes_per_rank"] = exchange_bytes(T if U is None else U, B, S, E, HF)
+        out["tokens_per_rank"], out["unique_ids_per_rank"] = int(T), (None if U is None else int(U))
     if terms:
         out["sampled_fwd_mfma_frac"] = round(terms * fl / (ts * 1e-3) / 1e12 / BF16_MFMA_PEAK_TFLOPS, 4)
         out["mfma"] = f"bf16 MFMA, {terms} plane products per fp32 product"
@@ -658,14 +660,17 @@ def main():
     # one extra batch is held out for evaluation
     st = SessionStream(N, L, B * (nsteps + 1), seed=2 + rank)
     args.item_counts = st.item_counts()
-    batches, tok = [], []
+    batches, tok, uniq = [], [], []
     for i in range(nsteps):
         b = st.batch(i, B)
         batches.append(pinned(b))
         tok.append(int(b[4].sum()))
+        ln = np.clip(b[4].numpy(), 1, L)
+        uniq.append(int(np.unique(b[0].numpy()[np.arange(L)[None, :] < ln[:, None]]).size))
     hb = st.batch(nsteps, B)
     held = (hb[0], hb[1], hb[4])
     T = float(np.mean(tok[args.warmup:]))
+    U = float(np.mean(uniq[args.warmup:]))   # distinct items per batch (the sharded exchange's rows)
     t_init = time.perf_counter()
     tr = make_trainer(args.config, args, dev, shard)
     apply_stored_logits(tr, args.stored_logits)
@@ -731,7 +736,7 @@ def main():
                 tr2 = make_trainer("c2s", args, dev, shard)
                 tr2.set_train()
                 _, _, k2, _ = timed_run(tr2, batches, min(5, args.warmup), min(30, args.steps), world, True, "c2")
-                target = target_step(k2, T, B, args.negatives, E, E, 1, terms)
+                target = target_step(k2, T, B, args.negatives, E, E, 1, terms, U=U)
                 if target is not None and world > 1:
                     by_sum, = max_over_ranks([float(target["bytes_per_step"])], op="sum")
                     tg, ts, tx = max_over_ranks([k2["gather"], k2["sampled_fwd"], k2.get("neg_exchange", 0.0)])
@@ -803,7 +808,7 @@ def main():
                    "parallelism": (f"dp{world} trunk + {world}-way item-sharded tables "
                                    f"({torch.distributed.get_backend() if torch.distributed.is_initialized() else ''})"
                                    if shard else "single"),
-                   "tokens_per_batch": int(T)},
+                   "tokens_per_batch": int(T), "distinct_items_per_batch": int(U)},
         "step_ms": {"median": round(float(np.median(ps)), 3), "p10": round(float(np.percentile(ps, 10)), 3),
                     "p90": round(float(np.percentile(ps, 90)), 3), "mean": round(float(ps.mean()), 3)},
         "roofline": roof, "cpu_baseline": cpu, "north_star_target": target, "eval_heldout": ev,
