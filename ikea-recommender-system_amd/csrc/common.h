@@ -140,6 +140,29 @@ __device__ __forceinline__ void split3x8(const f4& lo, const f4& hi, bf16x8& p0,
   }
 }
 
+// split3x8 with the conversions paired explicitly (one v_cvt_pk_bf16_f32 per
+// two values and plane) and the fp32 arithmetic scalar: the same RNE planes,
+// bitwise.  For units built without SLP vectorisation (head_flash.hip), where
+// the plain loop converts one value per instruction
+__device__ __forceinline__ void split3x8_pair(const f4& lo, const f4& hi, bf16x8& p0, bf16x8& p1, bf16x8& p2) {
+  typedef __bf16 bf2 __attribute__((ext_vector_type(2)));
+  typedef float fl2 __attribute__((ext_vector_type(2)));
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const float xa = i < 2 ? lo[2 * i] : hi[2 * i - 4], xb = i < 2 ? lo[2 * i + 1] : hi[2 * i - 3];
+    const bf2 b0 = __builtin_convertvector((fl2){xa, xb}, bf2);
+    const uint32_t u0 = __builtin_bit_cast(uint32_t, b0);
+    const float ra = xa - __uint_as_float(u0 << 16), rb = xb - __uint_as_float(u0 & 0xFFFF0000u);
+    const bf2 b1 = __builtin_convertvector((fl2){ra, rb}, bf2);
+    const uint32_t u1 = __builtin_bit_cast(uint32_t, b1);
+    const float sa = ra - __uint_as_float(u1 << 16), sb = rb - __uint_as_float(u1 & 0xFFFF0000u);
+    const bf2 b2 = __builtin_convertvector((fl2){sa, sb}, bf2);
+    p0[2 * i] = b0.x; p0[2 * i + 1] = b0.y;
+    p1[2 * i] = b1.x; p1[2 * i + 1] = b1.y;
+    p2[2 * i] = b2.x; p2[2 * i + 1] = b2.y;
+  }
+}
+
 // ---- sampled negatives (csrc/sampled.hip, csrc/pack_gather.hip) ----
 // Counter-based uniform draw: negative s of draw `counter` is the high 64 bits
 // of splitmix64(seed + φ·(counter·S + s + 1))·A — reproducible on the host.

@@ -68,16 +68,23 @@ __device__ __forceinline__ void blds16(__amdgpu_buffer_rsrc_t r, void* lds_wave_
 }
 
 // copy E 16-B entries (E % 64 == 0) from global to LDS, sliced over NW waves
-// (w wave-uniform, lane16 = 16·lane)
-// (P2 = false: the third plane of every [p < 3][lane] group is not copied —
-// the 3-term gradient contractions never read it)
+// (w wave-uniform, lane16 = 16·lane), one 64-entry group per wave and step.
+// P2 = false: the third plane of every [p < 3][lane] triple of groups is not
+// copied (the 3-term contractions never read it); the kept groups are dealt
+// to the waves evenly.  The only condition is gk < NK, and only when the
+// groups do not divide evenly (per-step conditions were hoisted out of the
+// chunk loop as VGPR booleans and spilled at HF 256)
 template <int E, int NW, bool P2 = true>
 __device__ __forceinline__ void stage(const bf16x8* __restrict__ src, bf16x8* dst, int w, int lane16) {
   const __amdgpu_buffer_rsrc_t r = rsrc_of(src);
+  constexpr int NGR = E / 64;                       // 64-entry groups
+  constexpr int NK = P2 ? NGR : NGR / 3 * 2;        // groups copied
+  static_assert(P2 || NGR % 3 == 0, "plane triples");
 #pragma unroll
-  for (int q = 0; q < (E + 64 * NW - 1) / (64 * NW); ++q) {
-    const int e0 = 64 * NW * q + 64 * w;  // wave-uniform
-    if (e0 < E && (P2 || (e0 >> 6) % 3 != 2)) blds16(r, dst + e0, lane16, 16 * e0);
+  for (int q = 0; q < (NK + NW - 1) / NW; ++q) {
+    const int gk = NW * q + w;                       // wave-uniform
+    const int g = P2 ? gk : (gk >> 1) * 3 + (gk & 1);
+    if (NK % NW == 0 || gk < NK) blds16(r, dst + 64 * g, lane16, 1024 * g);
   }
 }
 
@@ -649,30 +656,37 @@ __global__ __launch_bounds__(64) void k_flash_lse(const float* __restrict__ pm, 
   }
 }
 
-// (lse·log2e, local target or −1) per row: what pass 2 stages through LDS
+// Row records, what pass 2 stages through LDS (256 B per 32-row chunk): per
+// chunk the 32 rows' lse·log2e, then their local targets (or −1) — split, so
+// pass 2 reads four consecutive rows' values of one kind as a vector and
+// works on them in packed pairs
+__device__ __forceinline__ int ri_lse(int b) { return 64 * (b >> 5) + (b & 31); }
+__device__ __forceinline__ int ri_tgt(int b) { return 64 * (b >> 5) + 32 + (b & 31); }
+
 __global__ void k_flash_rows(const float* __restrict__ lse, const int64_t* __restrict__ tgt, int64_t lo, int A, int B,
-                             float2* __restrict__ rowinfo) {
+                             float* __restrict__ rowinfo) {
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= B) return;
   const int64_t t = tgt[b] - lo;
-  rowinfo[b] = make_float2(lse[b] * L2E, __int_as_float(t >= 0 && t < A ? (int)t : -1));
+  rowinfo[ri_lse(b)] = lse[b] * L2E;
+  rowinfo[ri_tgt(b)] = __int_as_float(t >= 0 && t < A ? (int)t : -1);
 }
 
 // dh[b][k] = g·(Σ_s 2^(m_s − lse2_b)·O_s[k][b] − W[t_b][k])
 __global__ __launch_bounds__(256) void k_flash_dh(const float* __restrict__ pm, const float* __restrict__ pO,
-                                                  const float2* __restrict__ rowinfo, int nsplit,
+                                                  const float* __restrict__ rowinfo, int nsplit,
                                                   const float* __restrict__ W, float g, int B, int HF,
                                                   float* __restrict__ dh) {
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (i >= (int64_t)B * HF) return;
   const int b = (int)(i % B), k = (int)(i / B);
-  const float2 ri = rowinfo[b];
+  const float lse2 = rowinfo[ri_lse(b)];
   float acc = 0.f;
   for (int s = 0; s < nsplit; ++s) {
     const float ms = pm[(int64_t)s * B + b];
-    if (ms != NEG_INF) acc = fmaf(__builtin_amdgcn_exp2f(ms - ri.x), pO[((int64_t)s * HF + k) * B + b], acc);
+    if (ms != NEG_INF) acc = fmaf(__builtin_amdgcn_exp2f(ms - lse2), pO[((int64_t)s * HF + k) * B + b], acc);
   }
-  const int t = __float_as_int(ri.y);
+  const int t = __float_as_int(rowinfo[ri_tgt(b)]);
   dh[(int64_t)b * HF + k] = g * (t >= 0 ? acc - W[(int64_t)t * HF + k] : acc);
 }
 
@@ -742,7 +756,7 @@ constexpr int sf2_wc_vm(int n) { return (n & 15) | ((n >> 4) << 14) | 0x70; }
 template <int HF, int NT, bool ZL>
 __global__ __launch_bounds__(64 * fl_nw(HF, 2)) void k_flash_dw(
     const bf16x8* __restrict__ Hk0, const bf16x8* __restrict__ Hr0, const bf16x8* Wk, const float* bias_pad,
-    const float2* __restrict__ rowinfo0, float g, int B, int A, float* __restrict__ W, float* __restrict__ mW,
+    const float* __restrict__ rowinfo0, float g, int B, int A, float* __restrict__ W, float* __restrict__ mW,
     float* __restrict__ vW, float* __restrict__ bias, float* __restrict__ mb, float* __restrict__ vb, AdamArgs args,
     float* __restrict__ dW_out, float* __restrict__ db_out, bf16x8* Wk_out, bf16x8* Wr_out, float* bias_pad_out,
     int nfull, int tsplit, float* __restrict__ tail_dw, float* __restrict__ tail_db, const float* __restrict__ zs) {
@@ -753,13 +767,13 @@ __global__ __launch_bounds__(64 * fl_nw(HF, 2)) void k_flash_dw(
   constexpr int ER = NF * 192;
   __shared__ bf16x8 sk0[EK], sk1[EK];
   __shared__ bf16x8 sr0[ZL ? 1 : ER], sr1[(DR && !ZL) ? ER : 1];   // (ZL: h's R-planes ring in sk0 / sk1)
-  __shared__ __attribute__((aligned(16))) float2 si0[32], si1[32];
+  __shared__ __attribute__((aligned(16))) float si0[64], si1[64];   // row records of a chunk
   // ZL: three-slot ring of the waves' z tiles (4 KB per wave and slot, DMA'd
   // straight from pass 1's store; separate arrays, so the compiler's LDS-DMA
   // tracking orders reads of a slot behind its own DMA only)
   __shared__ __attribute__((aligned(16))) float zr0[ZL ? 1024 * NW : 1], zr1[ZL ? 1024 * NW : 1],
       zr2[ZL ? 1024 * NW : 1];
-  __shared__ __attribute__((aligned(16))) float2 si2[ZL ? 32 : 1];   // ZL: third row-record slot
+  __shared__ __attribute__((aligned(16))) float si2[ZL ? 64 : 1];   // ZL: third row-record slot
   const int tid = threadIdx.x, lane = tid & 63, kg = lane >> 4, l16 = lane & 15, lane16 = 16 * lane;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   FL2_DECL
@@ -773,22 +787,22 @@ __global__ __launch_bounds__(64 * fl_nw(HF, 2)) void k_flash_dw(
   const int nch = tail ? max(0, min(nct, cb + cper) - cb) : nct;
   const bf16x8* __restrict__ Hk = Hk0 + (int64_t)cb * EK;
   const bf16x8* __restrict__ Hr = Hr0 + (int64_t)cb * ER;
-  const float2* __restrict__ rowinfo = rowinfo0 + 32 * cb;
+  const float* __restrict__ rowinfo = rowinfo0 + 64 * cb;
 #define FL_ISSUE_K(C, SK, SI)                                                  \
   do {                                                                         \
     stage<EK, NW>(Hk + (int64_t)(C) * EK, SK, w, lane16);                      \
-    if (w == 0 && lane < 16) blds16(rsrc_of(rowinfo + 32 * (C)), SI, lane16, 0); \
+    if (w == 0 && lane < 16) blds16(rsrc_of(rowinfo + 64 * (C)), SI, lane16, 0); \
   } while (0)
 #define FL_ISSUE_R(C, SR) stage<ER, NW>(Hr + (int64_t)(C) * ER, SR, w, lane16)
   // ZL: chunk C's R-planes into ring slot SR (a K-plane array: EK == ER) and its row records
 #define FL_ISSUE_Z(C, SR, SI)                                                  \
   do {                                                                         \
     stage<ER, NW>(Hr + (int64_t)(C) * ER, SR, w, lane16);                      \
-    if (w == 0 && lane < 16) blds16(rsrc_of(rowinfo + 32 * (C)), SI, lane16, 0); \
+    if (w == 0 && lane < 16) blds16(rsrc_of(rowinfo + 64 * (C)), SI, lane16, 0); \
   } while (0)
   if constexpr (ZL) {
     FL_ISSUE_Z(0, sk0, si0);
-    if (w == 0 && lane < 16) blds16(rsrc_of(rowinfo + 32 * max(0, min(1, nch - 1))), si1, lane16, 0);
+    if (w == 0 && lane < 16) blds16(rsrc_of(rowinfo + 64 * max(0, min(1, nch - 1))), si1, lane16, 0);
   } else {
     FL_ISSUE_K(0, sk0, si0);
     FL_ISSUE_R(0, sr0);
@@ -836,8 +850,9 @@ __global__ __launch_bounds__(64 * fl_nw(HF, 2)) void k_flash_dw(
   FL2_MARK(0);
   // dZ = g·(2^((S + b)·log2e − lse·log2e) − onehot) from the chunk's S tiles
   // (ZL: z = S + b, bj = 0), db; dZᵀ planes (q*[ib]: the A operand of dW, k
-  // over the chunk's rows in kperm16 order)
-  auto dzpart = [&](f4 (&sa)[2][2], const float2* si, bf16x8 (&q0)[2], bf16x8 (&q1)[2], bf16x8 (&q2)[2],
+  // over the chunk's rows in kperm16 order).  Scalar fp32 only: packed f32
+  // ops (v_pk_*) cost more issue beside the MFMAs than two scalar ones
+  auto dzpart = [&](f4 (&sa)[2][2], const float* si, bf16x8 (&q0)[2], bf16x8 (&q1)[2], bf16x8 (&q2)[2],
                     bool add_db = true) __attribute__((always_inline)) {
 #pragma unroll
     for (int ib = 0; ib < 2; ++ib) {
@@ -845,26 +860,24 @@ __global__ __launch_bounds__(64 * fl_nw(HF, 2)) void k_flash_dw(
       float cdb = 0.f;
 #pragma unroll
       for (int rb = 0; rb < 2; ++rb) {
-        const f4 i0 = *reinterpret_cast<const f4*>(&si[16 * rb + 4 * kg]);
-        const f4 i1 = *reinterpret_cast<const f4*>(&si[16 * rb + 4 * kg + 2]);
+        const f4 ls = *reinterpret_cast<const f4*>(&si[16 * rb + 4 * kg]);
+        const f4 tb = *reinterpret_cast<const f4*>(&si[32 + 16 * rb + 4 * kg]);
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
-          const float lse2 = u < 2 ? i0[2 * u] : i1[2 * (u - 2)];
-          const int tb = __float_as_int(u < 2 ? i0[2 * u + 1] : i1[2 * (u - 2) + 1]);
           const float zz = ZL ? sa[rb][ib][u] : sa[rb][ib][u] + bj[ib];
-          const float e = __builtin_amdgcn_exp2f(fmaf(zz, L2E, -lse2));
-          const float p = g * (e - (tb == item ? 1.f : 0.f));
+          const float e = __builtin_amdgcn_exp2f(fmaf(zz, L2E, -ls[u]));
+          const float p = fmaf(g, e, __float_as_int(tb[u]) == item ? -g : 0.f);   // g·(e − onehot)
           sa[rb][ib][u] = p;
           cdb += p;
         }
       }
       dbs[ib] += add_db ? cdb : 0.f;
-      split3x8(sa[0][ib], sa[1][ib], q0[ib], q1[ib], q2[ib]);
+      split3x8_pair(sa[0][ib], sa[1][ib], q0[ib], q1[ib], q2[ib]);
     }
     FL2_MARK(2);
   };
   // S = h_c·Wᵀ recomputed, then dzpart
-  auto spart = [&](const bf16x8* sk, const float2* si, bf16x8 (&q0)[2], bf16x8 (&q1)[2], bf16x8 (&q2)[2])
+  auto spart = [&](const bf16x8* sk, const float* si, bf16x8 (&q0)[2], bf16x8 (&q1)[2], bf16x8 (&q2)[2])
                    __attribute__((always_inline)) {
     f4 sa[2][2];   // [rb][ib]: lane (kg, n) holds rows 16rb + 4kg + u, item 16ib + n
 #pragma unroll
@@ -961,14 +974,14 @@ __global__ __launch_bounds__(64 * fl_nw(HF, 2)) void k_flash_dw(
       dzpart(z0, si0, qa0, qa1, qa2);
     }
     auto step = [&](int c, const float* zn1, float* zn3, const bf16x8* rcur, bf16x8* rnext,
-                    const float2* sin1, float2* sin2, const bf16x8 (&qc0)[2], const bf16x8 (&qc1)[2],
+                    const float* sin1, float* sin2, const bf16x8 (&qc0)[2], const bf16x8 (&qc1)[2],
                     const bf16x8 (&qc2)[2], bf16x8 (&qn0)[2], bf16x8 (&qn1)[2], bf16x8 (&qn2)[2])
                     __attribute__((always_inline)) {
       f4 z1[2][2];
       zread(zn1, z1);   // z(c + 1) landed by the previous barrier; no DMA in flight yet
       __builtin_amdgcn_sched_barrier(0);
       stage<ER, NW>(Hr + (int64_t)min(c + 1, nch - 1) * ER, rnext, w, lane16);
-      if (w == 0 && lane < 16) blds16(rsrc_of(rowinfo + 32 * min(c + 2, nch - 1)), sin2, lane16, 0);
+      if (w == 0 && lane < 16) blds16(rsrc_of(rowinfo + 64 * min(c + 2, nch - 1)), sin2, lane16, 0);
       zdma(c + 3, zn3);
       __builtin_amdgcn_sched_barrier(0);
       dzpart(z1, sin1, qn0, qn1, qn2, c + 1 < nch);   // (past the last chunk: planes unused, no db)
@@ -1824,7 +1837,7 @@ extern "C" int rg_flash_rows(const float* lse, const int64_t* tgt, int64_t lo, i
                              hipStream_t stream) {
   if (B <= 0 || A <= 0 || !lse || !tgt || !rowinfo) return RG_ERR_ARG;
   hipLaunchKernelGGL(k_flash_rows, dim3((B + 255) / 256), dim3(256), 0, stream, lse, tgt, lo, A, B,
-                     (float2*)rowinfo);
+                     (float*)rowinfo);
   RG_LAUNCH_CHECK();
   return RG_OK;
 }
@@ -1833,7 +1846,7 @@ extern "C" int rg_flash_dh(const float* pm, const float* pO, const void* rowinfo
                            float gscale, int B, int HF, float* dh, hipStream_t stream) {
   if (B <= 0 || nsplit <= 0 || HF <= 0 || !pm || !pO || !rowinfo || !W || !dh) return RG_ERR_ARG;
   hipLaunchKernelGGL(k_flash_dh, dim3((unsigned)(((int64_t)B * HF + 255) / 256)), dim3(256), 0, stream, pm, pO,
-                     (const float2*)rowinfo, nsplit, W, gscale, B, HF, dh);
+                     (const float*)rowinfo, nsplit, W, gscale, B, HF, dh);
   RG_LAUNCH_CHECK();
   return RG_OK;
 }
@@ -1859,7 +1872,7 @@ extern "C" int rg_flash_dw_adam_planes(const void* Hk, const void* Hr, const voi
   const dim3 grid((unsigned)(tl.nfull + (nblk - tl.nfull) * tl.tsplit));
 #define FW(HFV, NTV, ZLV)                                                                                     \
   hipLaunchKernelGGL((k_flash_dw<HFV, NTV, ZLV>), grid, dim3(64 * fl_nw(HFV, 2)), 0, stream, (const bf16x8*)Hk, \
-                     (const bf16x8*)Hr, (const bf16x8*)Wk, bias_pad, (const float2*)rowinfo, gscale, B, A, W, mW, vW, \
+                     (const bf16x8*)Hr, (const bf16x8*)Wk, bias_pad, (const float*)rowinfo, gscale, B, A, W, mW, vW, \
                      bias, mb, vb, a, dW_out, db_out, (bf16x8*)Wk_out, (bf16x8*)Wr_out, bias_pad_out, tl.nfull,    \
                      tl.tsplit, tail_dw, tail_db, zs)
 #define FZ(HFV, NTV)               \

@@ -54,8 +54,10 @@ extern "C" int rg_weighted_sum(const float* const* X, const float* w, int nh, in
 // (the exact re-scoring reads it) and as its three bf16 K-planes (the
 // screening argmax's operand, common.h kplane16: bitwise rg_head_planes);
 // the biases likewise into b_comb and the −inf-padded bias; and the largest
-// row norm ||W_comb[x]||₂ (the screening's error bound) by one atomicMax of
-// the non-negative float bits per wave (order-independent: deterministic).
+// row norm ||W_comb[x]||₂ (the screening's error bound): a running max per
+// lane over a grid-stride loop, reduced per block through LDS, then one
+// atomicMax of the non-negative float bits per block (order-independent:
+// deterministic; one atomic per wave serialised ~A/4 atomics on one address).
 // Replaces rg_weighted_sum (W, b) + rg_head_planes + rg_row_norm_max: the Q
 // heads are read once and W_comb is not re-read.
 template <int HF>
@@ -63,45 +65,53 @@ __global__ __launch_bounds__(256) void k_qcomb(Ptr4 in, Ptr4 inb, int nh, int A,
                                                float* __restrict__ bc, bf16x8* __restrict__ P,
                                                float* __restrict__ bias_pad, float* __restrict__ wnorm) {
   constexpr int G = HF / 8;   // threads per item row (a power of two dividing 64)
-  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  const int x = (int)(i / G), g = (int)(i % G);
-  f4 lo = {0.f, 0.f, 0.f, 0.f}, hi = lo;
-  float ss = 0.f;
-  if (x < A) {
-    const int64_t off = (int64_t)x * HF + 8 * g;
-    lo = *reinterpret_cast<const f4*>(in.p[0] + off) * in.w[0];
-    hi = *reinterpret_cast<const f4*>(in.p[0] + off + 4) * in.w[0];
-    for (int k = 1; k < nh; ++k) {
-      lo = lo + *reinterpret_cast<const f4*>(in.p[k] + off) * in.w[k];
-      hi = hi + *reinterpret_cast<const f4*>(in.p[k] + off + 4) * in.w[k];
-    }
-    *reinterpret_cast<f4*>(Wc + off) = lo;
-    *reinterpret_cast<f4*>(Wc + off + 4) = hi;
+  __shared__ float red[4];
+  float best = 0.f;
+  // Ap·G is a multiple of 64 and the stride of 256, so every wave is wholly
+  // inside or outside the range: the shuffles below see full waves.
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < (int64_t)Ap * G; i += (int64_t)gridDim.x * 256) {
+    const int x = (int)(i / G), g = (int)(i % G);
+    f4 lo = {0.f, 0.f, 0.f, 0.f}, hi = lo;
+    float ss = 0.f;
+    if (x < A) {
+      const int64_t off = (int64_t)x * HF + 8 * g;
+      lo = *reinterpret_cast<const f4*>(in.p[0] + off) * in.w[0];
+      hi = *reinterpret_cast<const f4*>(in.p[0] + off + 4) * in.w[0];
+      for (int k = 1; k < nh; ++k) {
+        lo = lo + *reinterpret_cast<const f4*>(in.p[k] + off) * in.w[k];
+        hi = hi + *reinterpret_cast<const f4*>(in.p[k] + off + 4) * in.w[k];
+      }
+      *reinterpret_cast<f4*>(Wc + off) = lo;
+      *reinterpret_cast<f4*>(Wc + off + 4) = hi;
 #pragma unroll
-    for (int u = 0; u < 4; ++u) ss = fmaf(lo[u], lo[u], fmaf(hi[u], hi[u], ss));
-    if (g == 0) {
-      float sb = inb.p[0][x] * inb.w[0];
-      for (int k = 1; k < nh; ++k) sb = sb + inb.p[k][x] * inb.w[k];
-      bc[x] = sb;
-      bias_pad[x] = sb;
+      for (int u = 0; u < 4; ++u) ss = fmaf(lo[u], lo[u], fmaf(hi[u], hi[u], ss));
+      if (g == 0) {
+        float sb = inb.p[0][x] * inb.w[0];
+        for (int k = 1; k < nh; ++k) sb = sb + inb.p[k][x] * inb.w[k];
+        bc[x] = sb;
+        bias_pad[x] = sb;
+      }
+    } else if (g == 0) {
+      bias_pad[x] = -__builtin_inff();
     }
-  } else if (x < Ap && g == 0) {
-    bias_pad[x] = -__builtin_inff();
-  }
-  if (x < Ap) {   // (rows past A: zero planes, as rg_head_planes pads the last chunk)
+    // (rows past A: zero planes, as rg_head_planes pads the last chunk)
     bf16x8 p0, p1, p2;
     split3x8(lo, hi, p0, p1, p2);
     const int64_t base = kplane16(x, g, HF);
     P[base] = p0;
     P[base + 64] = p1;
     P[base + 128] = p2;
+#pragma unroll
+    for (int o = G / 2; o >= 1; o >>= 1) ss += __shfl_xor(ss, o);
+    best = fmaxf(best, sqrtf(ss));
   }
 #pragma unroll
-  for (int o = G / 2; o >= 1; o >>= 1) ss += __shfl_xor(ss, o);
-  float best = sqrtf(ss);
-#pragma unroll
-  for (int o = 32; o >= G; o >>= 1) best = fmaxf(best, __shfl_xor(best, o));
-  if ((threadIdx.x & 63) == 0) atomicMax(reinterpret_cast<unsigned int*>(wnorm), __float_as_uint(best));
+  for (int o = 32; o >= 1; o >>= 1) best = fmaxf(best, __shfl_xor(best, o));
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = best;
+  __syncthreads();
+  if (threadIdx.x == 0)
+    atomicMax(reinterpret_cast<unsigned int*>(wnorm),
+              __float_as_uint(fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]))));
 }
 
 extern "C" int rg_qcomb(const float* const* W, const float* const* b, const float* w, int nh, int A, int HF,
@@ -117,7 +127,8 @@ extern "C" int rg_qcomb(const float* const* W, const float* const* b, const floa
   }
   if (hipMemsetAsync(wnorm, 0, sizeof(float), stream) != hipSuccess) return RG_ERR_LAUNCH;
   const int Ap = (A + 31) / 32 * 32;
-  const unsigned grid = (unsigned)(((int64_t)Ap * (HF / 8) + 255) / 256);
+  int64_t need = ((int64_t)Ap * (HF / 8) + 255) / 256;
+  const unsigned grid = (unsigned)(need < 4096 ? need : 4096);
 #define QC(HFV)                                                                                            \
   hipLaunchKernelGGL(k_qcomb<HFV>, dim3(grid), dim3(256), 0, stream, in, inb, nh, A, Ap, Wc, bc,         \
                      reinterpret_cast<bf16x8*>(planes_k), bias_pad, wnorm)

@@ -293,78 +293,64 @@ extern "C" int rg_scatter_rows(const int32_t* ids, const float* src, int E, int 
 // ~1.7K distinct (Zipf) items, so the ids sent, the rows returned and the
 // row-gradients sent back shrink ~50× against one per token.
 //
-// rg_shard_dedup: stable radix sort of (id + 1, token) — invalid ids (−1)
-// become key 0, so they sort first and go with rank 0's group; the ids of
-// one owner are a contiguous range, so the sorted distinct ids are already
-// grouped by owner — then run heads, an inclusive scan (distinct index u per
-// sorted position), and
+// rg_shard_dedup (the forward, on the gather's critical path): no sort.  A
+// mark per table row — marks[id + 1] = 1 for every token's id (invalid ids
+// −1 at index 0, so they come first and go with rank 0's group) — and one
+// inclusive scan over the N1 + 1 marks give each distinct id its index u =
+// pos[id + 1] − 1 in increasing id order; the ids of one owner are a
+// contiguous range, so that order is grouped by owner and
 //   uslot[t]  = u of token t (rg_place_rows reads rows_in[uslot[t]]),
 //   uids[u]   = the distinct ids in increasing order (−1 first, if any),
-//   counts[o] = distinct ids owned by rank o (owner ⌈(id+1)·W/N1⌉ − 1),
-//   *nuniq    = U,
-// and keeps the sorted order in the work buffer for
-// rg_shard_dedup_grads: gsend[u] = Σ of the token rows of id u, summed in
-// token order (k_seg_blocks / k_seg_cross over the sorted runs: a fixed
-// order, so the step stays bitwise repeatable), stored once per u.
+//   counts[o] = distinct ids owned by rank o (owner ⌈(id+1)·W/N1⌉ − 1):
+//               pos at the owner's last index minus pos before its first,
+//   *nuniq    = U = pos[N1];
+// four launches (clear, mark, scan, write) whose cost is the scan's ~8 B per
+// table row instead of a multi-pass sort of the tokens.  The write also
+// leaves (u, t) key / value pairs in the work buffer for the backward.
+// rg_shard_dedup_grads (the backward): a stable radix sort of those pairs
+// by u (token order within one u) and gsend[u] = Σ of the token rows of u,
+// summed in token order (k_seg_blocks / k_seg_cross over the sorted runs: a
+// fixed order, so the step stays bitwise repeatable), stored once per u.
 namespace {
 
-__global__ void k_dd_keys(const int32_t* __restrict__ tok_id, const int32_t* __restrict__ n_ptr, int n_max,
-                          uint32_t* __restrict__ keys, int32_t* __restrict__ vals) {
+// mark index of a token's id: id + 1, 0 for an invalid id (outside [0, N1))
+__device__ __forceinline__ int dd_index(int32_t id, int64_t N1) { return id >= 0 && id < N1 ? id + 1 : 0; }
+
+__global__ void k_dd_mark(const int32_t* __restrict__ tok_id, const int32_t* __restrict__ n_ptr, int n_max,
+                          int64_t N1, int32_t* __restrict__ marks) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n_max || i >= *n_ptr) return;
+  marks[dd_index(tok_id[i], N1)] = 1;   // (same value from every token of an id)
+}
+
+__global__ void k_dd_write(const int32_t* __restrict__ tok_id, const int32_t* __restrict__ pos,
+                           const int32_t* __restrict__ n_ptr, int n_max, int64_t N1, int W,
+                           int32_t* __restrict__ uslot, int32_t* __restrict__ uids, uint32_t* __restrict__ keys,
+                           int32_t* __restrict__ vals, int32_t* __restrict__ counts, int32_t* __restrict__ nuniq) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (blockIdx.x == 0) {
+    if (threadIdx.x < W) {   // owner o: ids [o·N1/W, (o+1)·N1/W) = mark indices (o·N1/W, (o+1)·N1/W]
+      const int o = threadIdx.x;
+      const int64_t hi = ((int64_t)(o + 1) * N1) / W, lo = ((int64_t)o * N1) / W;
+      counts[o] = pos[hi] - (o == 0 ? 0 : pos[lo]);
+    }
+    if (threadIdx.x == 0) *nuniq = pos[N1];
+  }
   if (i >= n_max) return;
-  const int n = *n_ptr;
-  keys[i] = i < n ? (uint32_t)(max(tok_id[i], -1) + 1) : SENT;
   vals[i] = i;
-}
-
-__global__ void k_dd_heads(const uint32_t* __restrict__ ks, const int32_t* __restrict__ n_ptr, int n_max,
-                           int32_t* __restrict__ head) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n_max) return;
-  head[i] = (i < *n_ptr && (i == 0 || ks[i] != ks[i - 1])) ? 1 : 0;
-}
-
-__global__ void k_dd_write(const uint32_t* __restrict__ ks, const int32_t* __restrict__ vs,
-                           const int32_t* __restrict__ incl, const int32_t* __restrict__ n_ptr, int n_max,
-                           int32_t* __restrict__ uslot, int32_t* __restrict__ uids, uint32_t* __restrict__ ukeys,
-                           int32_t* __restrict__ nuniq) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n_max) return;
-  const int n = *n_ptr;
-  if (i >= n) {
-    ukeys[i] = SENT;
-    if (i == 0) *nuniq = 0;
+  if (i >= *n_ptr) {
+    keys[i] = SENT;
     return;
   }
-  const int u = incl[i] - 1;
-  uslot[vs[i]] = u;
-  ukeys[i] = (uint32_t)u;
-  if (i == 0 || ks[i] != ks[i - 1]) uids[u] = (int32_t)ks[i] - 1;
-  if (i == n - 1) *nuniq = u + 1;
-}
-
-// counts[o] = #{u : owner(uids[u]) == o}; uids sorted (−1 first, owned by rank 0)
-__global__ void k_dd_counts(const int32_t* __restrict__ uids, const int32_t* __restrict__ nuniq, int64_t N1, int W,
-                            int32_t* __restrict__ counts) {
-  const int o = threadIdx.x;
-  if (o >= W) return;
-  const int U = *nuniq;
-  auto lower = [&](int64_t v) {   // first u with uids[u] >= v (v = 0 for rank 0's start: −1 sorts before)
-    int a = 0, b = U;
-    while (a < b) {
-      const int m = (a + b) >> 1;
-      if ((int64_t)uids[m] < v) a = m + 1;
-      else b = m;
-    }
-    return a;
-  };
-  const int lo = o == 0 ? 0 : lower(((int64_t)o * N1) / W);
-  const int hi = o == W - 1 ? U : lower(((int64_t)(o + 1) * N1) / W);
-  counts[o] = hi - lo;
+  const int k = dd_index(tok_id[i], N1);
+  const int u = pos[k] - 1;
+  uslot[i] = u;
+  keys[i] = (uint32_t)u;
+  uids[u] = k - 1;   // (same value from every token of an id)
 }
 
 struct DedupLayout {
-  size_t keys_in, keys_out, vals_in, vals_out, head, incl, ukeys, part_first, part_last, tmp, total, sort_bytes,
+  size_t keys_in, keys_out, vals_in, vals_out, marks, pos, part_first, part_last, tmp, total, sort_bytes,
       scan_bytes;
   int bits;
 };
@@ -378,16 +364,15 @@ DedupLayout dedup_layout(int n_max, int E, int64_t N1) {
   L.keys_out = off; off += al(sizeof(uint32_t) * n_max);
   L.vals_in = off; off += al(sizeof(int32_t) * n_max);
   L.vals_out = off; off += al(sizeof(int32_t) * n_max);
-  L.head = off; off += al(sizeof(int32_t) * n_max);
-  L.incl = off; off += al(sizeof(int32_t) * n_max);
-  L.ukeys = off; off += al(sizeof(uint32_t) * n_max);
+  L.marks = off; off += al(sizeof(int32_t) * (N1 + 1));
+  L.pos = off; off += al(sizeof(int32_t) * (N1 + 1));
   L.part_first = off; off += al(sizeof(float) * nb * E);
   L.part_last = off; off += al(sizeof(float) * nb * E);
-  L.bits = key_bits(N1 + 1);   // keys 0 .. N1, the sentinel's low bits above them
+  L.bits = key_bits(n_max);   // keys u < U <= n_max, the sentinel's low bits above them
   size_t ts = 0, tc = 0;
   hipcub::DeviceRadixSort::SortPairs(nullptr, ts, (const uint32_t*)nullptr, (uint32_t*)nullptr,
                                      (const int32_t*)nullptr, (int32_t*)nullptr, n_max, 0, L.bits);
-  hipcub::DeviceScan::InclusiveSum(nullptr, tc, (const int32_t*)nullptr, (int32_t*)nullptr, n_max);
+  hipcub::DeviceScan::InclusiveSum(nullptr, tc, (const int32_t*)nullptr, (int32_t*)nullptr, (int)(N1 + 1));
   L.sort_bytes = ts;
   L.scan_bytes = tc;
   L.tmp = off; off += al(ts > tc ? ts : tc);
@@ -411,26 +396,16 @@ extern "C" int rg_shard_dedup(const int32_t* tok_id, const int32_t* n_ptr, int n
   const DedupLayout L = dedup_layout(n_max, E, N1);
   if (work_bytes < (int64_t)L.total) return RG_ERR_ARG;
   char* w = static_cast<char*>(work);
-  uint32_t* kin = (uint32_t*)(w + L.keys_in);
-  uint32_t* kout = (uint32_t*)(w + L.keys_out);
-  int32_t* vin = (int32_t*)(w + L.vals_in);
-  int32_t* vout = (int32_t*)(w + L.vals_out);
-  int32_t* head = (int32_t*)(w + L.head);
-  int32_t* incl = (int32_t*)(w + L.incl);
-  uint32_t* ukeys = (uint32_t*)(w + L.ukeys);
+  int32_t* marks = (int32_t*)(w + L.marks);
+  int32_t* pos = (int32_t*)(w + L.pos);
   const dim3 g((unsigned)((n_max + 255) / 256));
-  hipLaunchKernelGGL(k_dd_keys, g, dim3(256), 0, stream, tok_id, n_ptr, n_max, kin, vin);
-  size_t ts = L.sort_bytes;
-  if (hipcub::DeviceRadixSort::SortPairs(w + L.tmp, ts, kin, kout, vin, vout, n_max, 0, L.bits, stream) !=
-      hipSuccess)
-    return RG_ERR_LAUNCH;
-  hipLaunchKernelGGL(k_dd_heads, g, dim3(256), 0, stream, kout, n_ptr, n_max, head);
+  if (hipMemsetAsync(marks, 0, sizeof(int32_t) * (N1 + 1), stream) != hipSuccess) return RG_ERR_LAUNCH;
+  hipLaunchKernelGGL(k_dd_mark, g, dim3(256), 0, stream, tok_id, n_ptr, n_max, N1, marks);
   size_t tc = L.scan_bytes;
-  if (hipcub::DeviceScan::InclusiveSum(w + L.tmp, tc, head, incl, n_max, stream) != hipSuccess)
+  if (hipcub::DeviceScan::InclusiveSum(w + L.tmp, tc, marks, pos, (int)(N1 + 1), stream) != hipSuccess)
     return RG_ERR_LAUNCH;
-  hipLaunchKernelGGL(k_dd_write, g, dim3(256), 0, stream, kout, vout, incl, n_ptr, n_max, uslot, uids, ukeys,
-                     nuniq);
-  hipLaunchKernelGGL(k_dd_counts, dim3(1), dim3(256), 0, stream, uids, nuniq, N1, W, counts);
+  hipLaunchKernelGGL(k_dd_write, g, dim3(256), 0, stream, tok_id, pos, n_ptr, n_max, N1, W, uslot, uids,
+                     (uint32_t*)(w + L.keys_in), (int32_t*)(w + L.vals_in), counts, nuniq);
   RG_LAUNCH_CHECK();
   return RG_OK;
 }
@@ -441,8 +416,12 @@ extern "C" int rg_shard_dedup_grads(const float* src, int E, int n_max, int64_t 
   const DedupLayout L = dedup_layout(n_max, E, N1);
   if (work_bytes < (int64_t)L.total) return RG_ERR_ARG;
   char* w = static_cast<char*>(work);
-  const int32_t* vout = (const int32_t*)(w + L.vals_out);
-  const uint32_t* ukeys = (const uint32_t*)(w + L.ukeys);
+  uint32_t* ukeys = (uint32_t*)(w + L.keys_out);
+  int32_t* vout = (int32_t*)(w + L.vals_out);
+  size_t ts = L.sort_bytes;
+  if (hipcub::DeviceRadixSort::SortPairs(w + L.tmp, ts, (const uint32_t*)(w + L.keys_in), ukeys,
+                                         (const int32_t*)(w + L.vals_in), vout, n_max, 0, L.bits, stream) != hipSuccess)
+    return RG_ERR_LAUNCH;
   float* pf = (float*)(w + L.part_first);
   float* pl = (float*)(w + L.part_last);
   const int nb = (n_max + SB - 1) / SB;

@@ -530,13 +530,23 @@ def test_shard_dedup_distinct_ids_and_sums(n_rows, W, n, n_max, E, zipf):
     else:
         ids = rng.integers(0, n_rows, size=n)
     ids = ids.astype(np.int64)
+    raw = ids.copy()
     if n > 10:
         ids[rng.integers(0, n, size=5)] = -1     # invalid tokens (k_token_ids writes -1)
-    tok = D(torch.from_numpy(ids.astype(np.int32)))
-    nptr = D(torch.tensor([n], dtype=torch.int32))
+        raw = ids.copy()
+        raw[rng.integers(0, n, size=3)] = n_rows + 2   # out of range: counted as -1
+        ids = np.where(raw >= n_rows, -1, raw)
     call = C().call
     wb = call("rg_shard_dedup_work_bytes", n_max, E, n_rows)
-    work = torch.empty(wb, dtype=torch.uint8, device=dev)
+    work = torch.full((wb,), 0x5A, dtype=torch.uint8, device=dev)   # (no zeroed work buffer needed)
+    # an earlier pass on the same work buffer leaves no marks behind
+    other = D(torch.from_numpy(rng.integers(0, n_rows, size=n).astype(np.int32)))
+    nptr = D(torch.tensor([n], dtype=torch.int32))
+    scratch = [torch.empty(n_max, dtype=torch.int32, device=dev) for _ in range(2)]
+    call("rg_shard_dedup", other.data_ptr(), nptr.data_ptr(), n_max, n_rows, W, E, scratch[0].data_ptr(),
+         scratch[1].data_ptr(), torch.zeros(W, dtype=torch.int32, device=dev).data_ptr(),
+         torch.zeros(1, dtype=torch.int32, device=dev).data_ptr(), work.data_ptr(), wb, st())
+    tok = D(torch.from_numpy(raw.astype(np.int32)))
     uslot = torch.full((n_max,), -7, dtype=torch.int32, device=dev)
     uids = torch.full((n_max,), -7, dtype=torch.int32, device=dev)
     counts = torch.zeros(W, dtype=torch.int32, device=dev)

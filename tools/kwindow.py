@@ -17,6 +17,7 @@ ap = argparse.ArgumentParser()
 ap.add_argument("trace")
 ap.add_argument("--steps", type=int, default=0)
 ap.add_argument("--timeline", default="")
+ap.add_argument("--min-us", type=float, default=500.0, help="timeline: dispatches at least this long")
 a = ap.parse_args()
 rows = list(csv.DictReader(open(a.trace)))
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
@@ -39,8 +40,8 @@ if a.timeline:
     with open(a.timeline, "w") as f:
         for r in win:
             s0, e0 = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
-            if e0 - s0 >= 500_000:
-                f.write(f"{(s0 - t0) / 1e6:10.3f} {(e0 - s0) / 1e6:9.3f}  {r['Kernel_Name'][:110]}\n")
+            if e0 - s0 >= a.min_us * 1e3:
+                f.write(f"{(s0 - t0) / 1e6:10.4f} {(e0 - s0) / 1e6:9.4f}  {r['Kernel_Name'][:110]}\n")
 span = (int(win[-1]["End_Timestamp"]) - int(win[0]["Start_Timestamp"])) / 1e6
 sys.stderr.write(f"kwindow: {len(win)} dispatches, kernel time {tot / 1e6:.2f} ms, wall span {span:.2f} ms"
                  + (f" ({span / a.steps:.2f} ms per step)" if a.steps else "") + "\n")

@@ -22,20 +22,25 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--config", default="c5")
 ap.add_argument("--steps", type=int, default=4)
 ap.add_argument("--warmup", type=int, default=2)
+ap.add_argument("--shard", action="store_true",
+                help="item-sharded trainer over a one-rank process group (RANK / WORLD_SIZE / MASTER_* from the env)")
 a = ap.parse_args()
-sys.argv = [sys.argv[0], "--config", a.config]
+sys.argv = [sys.argv[0], "--config", "c2" if a.config == "c2s" else a.config]
 args = bench.parse()
 if a.config == "c5":
     args.items, args.dim, args.seq, args.batch = 5_000_000, 256, 100, 8192
 from recommenders.data_utils.synthetic import SessionStream  # noqa: E402
 from recommenders.hip import call, stream_ptr  # noqa: E402
 dev = torch.device("cuda", 0)
+if a.shard:
+    torch.cuda.set_device(0)
+    torch.distributed.init_process_group("nccl")
 B, L, N = args.batch, args.seq, args.items
 n = a.warmup + a.steps
 st = SessionStream(N, L, B * n, seed=2)
 args.item_counts = st.item_counts()
 batches = [bench.pinned(st.batch(i, B)) for i in range(n)]
-tr = bench.make_trainer(a.config, args, dev, False)
+tr = bench.make_trainer(a.config, args, dev, a.shard)
 tr.set_train()
 x = torch.zeros(4, device=dev)
 y = torch.zeros(8, dtype=torch.float16, device=dev)
@@ -54,3 +59,5 @@ for i in range(a.warmup, n):
     tr.train_step(*bench.step_args(a.config, batches[i]))
 marker()
 print(f"stepprof: {a.config} {a.steps} steps between the markers", flush=True)
+if a.shard:
+    torch.distributed.destroy_process_group()
