@@ -22,6 +22,7 @@ OUT_DIR = os.path.join(HERE, "recommenders", "hip")
 LIB = os.path.join(OUT_DIR, "libikea_rec_hip.so")
 OBJ = os.path.join(HERE, "build", "obj")
 FLAGS = ["--offload-arch=gfx950", "-O3", "-fPIC", "-std=c++17", "-Wno-unused-result"]
+LINK = ["-L/opt/rocm/lib", "-lrccl"]
 
 
 def hipcc():
@@ -34,7 +35,8 @@ def hipcc():
 def _compile(src):
     obj = os.path.join(OBJ, os.path.basename(src).replace(".hip", ".o"))
     headers = [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".h")]
-    if os.path.exists(obj) and os.path.getmtime(obj) >= max(os.path.getmtime(p) for p in [src, *headers]):
+    deps = [src, *headers, os.path.abspath(__file__)]
+    if os.path.exists(obj) and os.path.getmtime(obj) >= max(os.path.getmtime(p) for p in deps):
         return obj
     cmd = [hipcc(), *FLAGS, "-I", CSRC, "-c", src, "-o", obj]
     r = subprocess.run(cmd, capture_output=True, text=True)
@@ -51,7 +53,8 @@ def build(jobs: int = 8, verbose: bool = True) -> str:
         objs = list(ex.map(_compile, srcs))
     newest = max(os.path.getmtime(o) for o in objs)
     if not os.path.exists(LIB) or os.path.getmtime(LIB) < newest:
-        cmd = [hipcc(), "--offload-arch=gfx950", "-shared", "-fPIC", *objs, "-o", LIB]
+        # librccl: csrc/comm.hip (the item-sharded step's collectives on the compute stream)
+        cmd = [hipcc(), "--offload-arch=gfx950", "-shared", "-fPIC", *objs, "-o", LIB, *LINK]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link failed:\n{r.stderr}")

@@ -246,6 +246,7 @@ __device__ __forceinline__ f4 mfma16bf(bf16x8 a, bf16x8 b, f4 c) {
 template <int NT>
 __device__ __forceinline__ f4 mfma16_split(const bf16x8& a0, const bf16x8& a1, const bf16x8& a2, const bf16x8& b0,
                                           const bf16x8& b1, const bf16x8& b2, f4 acc) {
+  if (NT == 1) return mfma16bf(a0, b0, acc);
   if (NT == 3) {
     acc = mfma16bf(a0, b1, acc);
     acc = mfma16bf(a1, b0, acc);

@@ -53,7 +53,8 @@ __global__ __launch_bounds__(256) void k_token_ids(const int64_t* __restrict__ s
 }
 
 // Stable partition of the T tokens by owner (one workgroup, 256 threads,
-// each a contiguous token range): counts[o], slot[t], send_ids[slot[t]].
+// each a contiguous token range; the per-owner offsets by a shuffle scan):
+// counts[o], slot[t], send_ids[slot[t]].
 // Invalid ids (-1) go to rank 0, whose gather returns a zero row for them.
 // Deterministic: the send order is the packed token order within each owner.
 constexpr int RT_THREADS = 256;
@@ -64,50 +65,56 @@ __global__ __launch_bounds__(RT_THREADS) void k_shard_route(const int32_t* __res
                                                             int32_t* __restrict__ slot,
                                                             int32_t* __restrict__ send_ids,
                                                             int32_t* __restrict__ counts) {
-  __shared__ int cnt[RT_MAXW][RT_THREADS + 1];  // per (owner, thread) counts, then exclusive offsets
-  __shared__ int tot[RT_MAXW];
-  const int tid = threadIdx.x;
+  __shared__ int wtot[RT_THREADS / 64][RT_MAXW];   // per (wave, owner) totals
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int T = *ntok_ptr;
   const int per = (T + RT_THREADS - 1) / RT_THREADS;
   const int t0 = min(T, tid * per), t1 = min(T, t0 + per);
-  for (int o = 0; o < W; ++o) cnt[o][tid] = 0;
+  int cnt[RT_MAXW];
+#pragma unroll
+  for (int o = 0; o < RT_MAXW; ++o) cnt[o] = 0;
   for (int t = t0; t < t1; ++t) {
     const int id = tok_id[t];
-    ++cnt[id < 0 ? 0 : owner_of(id, N1, W)][tid];
-  }
-  __syncthreads();
-  // exclusive scan over threads, one thread per owner
-  if (tid < W) {
-    int acc = 0;
-    for (int i = 0; i < RT_THREADS; ++i) {
-      const int c = cnt[tid][i];
-      cnt[tid][i] = acc;
-      acc += c;
-    }
-    tot[tid] = acc;
-  }
-  __syncthreads();
-  if (tid == 0) {
-    int acc = 0;
-    for (int o = 0; o < W; ++o) {
-      counts[o] = tot[o];
-      const int c = tot[o];
-      tot[o] = acc;  // owner's base in the send buffer
-      acc += c;
-    }
-  }
-  __syncthreads();
-  // running positions stay in registers (fully unrolled over RT_MAXW owners)
-  int pos[RT_MAXW];
+    const int o = id < 0 ? 0 : owner_of(id, N1, W);
 #pragma unroll
-  for (int o = 0; o < RT_MAXW; ++o) pos[o] = o < W ? tot[o] + cnt[o][tid] : 0;
+    for (int q = 0; q < RT_MAXW; ++q) cnt[q] += q == o;
+  }
+  // exclusive scan over the threads (token order), per owner: wave shuffles,
+  // then the waves' totals through LDS
+  int pre[RT_MAXW];
+#pragma unroll
+  for (int o = 0; o < RT_MAXW; ++o) {
+    int x = cnt[o];
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const int y = __shfl_up(x, d);
+      if (lane >= d) x += y;
+    }
+    pre[o] = x - cnt[o];
+    if (lane == 63) wtot[wv][o] = x;
+  }
+  __syncthreads();
+  int base = 0;
+#pragma unroll
+  for (int o = 0; o < RT_MAXW; ++o) {
+    int tot = 0, before = 0;
+#pragma unroll
+    for (int q = 0; q < RT_THREADS / 64; ++q) {
+      const int v = wtot[q][o];
+      before += q < wv ? v : 0;
+      tot += v;
+    }
+    if (tid == 0 && o < W) counts[o] = tot;
+    pre[o] += base + before;   // the owner's base in the send buffer + the earlier threads' tokens
+    base += o < W ? tot : 0;
+  }
   for (int t = t0; t < t1; ++t) {
     const int id = tok_id[t];
     const int o = id < 0 ? 0 : owner_of(id, N1, W);
     int p = 0;
 #pragma unroll
     for (int q = 0; q < RT_MAXW; ++q)
-      if (q == o) p = pos[q]++;
+      if (q == o) p = pre[q]++;
     slot[t] = p;
     send_ids[p] = id;
   }

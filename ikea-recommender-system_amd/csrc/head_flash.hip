@@ -74,16 +74,16 @@ __device__ __forceinline__ void blds16(__amdgpu_buffer_rsrc_t r, void* lds_wave_
 // to the waves evenly.  The only condition is gk < NK, and only when the
 // groups do not divide evenly (per-step conditions were hoisted out of the
 // chunk loop as VGPR booleans and spilled at HF 256)
-template <int E, int NW, bool P2 = true>
+template <int E, int NW, int NP = 3>
 __device__ __forceinline__ void stage(const bf16x8* __restrict__ src, bf16x8* dst, int w, int lane16) {
   const __amdgpu_buffer_rsrc_t r = rsrc_of(src);
   constexpr int NGR = E / 64;                       // 64-entry groups
-  constexpr int NK = P2 ? NGR : NGR / 3 * 2;        // groups copied
-  static_assert(P2 || NGR % 3 == 0, "plane triples");
+  constexpr int NK = NP == 3 ? NGR : NGR / 3 * NP;  // groups copied: planes 0 .. NP − 1 of each triple
+  static_assert(NP == 3 || NGR % 3 == 0, "plane triples");
 #pragma unroll
   for (int q = 0; q < (NK + NW - 1) / NW; ++q) {
     const int gk = NW * q + w;                       // wave-uniform
-    const int g = P2 ? gk : (gk >> 1) * 3 + (gk & 1);
+    const int g = NP == 3 ? gk : (gk / NP) * 3 + (gk % NP);
     if (NK % NW == 0 || gk < NK) blds16(r, dst + 64 * g, lane16, 1024 * g);
   }
 }
@@ -229,7 +229,7 @@ __global__ __launch_bounds__(64 * fl_nw(HF, 1)) void k_flash_fwd(
   } while (0)
 #define FL_ISSUE_R(C, SR)                                                                \
   do {                                                                                   \
-    if constexpr (NG > 0) stage<ER, NW, NG != 3>(Wr + (int64_t)(C) * ER, SR, w, lane16); \
+    if constexpr (NG > 0) stage<ER, NW, NG == 3 ? 2 : 3>(Wr + (int64_t)(C) * ER, SR, w, lane16); \
   } while (0)
   if (nch > 0) {
     FL_ISSUE_K(c0, sk0, sb0);
@@ -492,9 +492,10 @@ __global__ __launch_bounds__(64 * fl_nw(HF, 1)) void k_flash_fwd(
 // 222-226, tensor_operations.py:50-70 via the combined head).  Same
 // workgroup / split / XCD layout and K-plane DMA ring as pass 1; per split the
 // row's best logit and item go to pbest / parg (merged by rg_flash_argmax).
-// CM (screening, NT = 3): also every 32-item chunk's row maximum (cmax,
-// ceil(A/32) × B) for the exact re-scoring of rg_flash_argmax_exact; plane 2
-// of the operands is then never read (not even DMA'd).
+// CM (screening, NT = 3 or 1): also every 32-item chunk's row maximum (cmax,
+// ceil(A/32) × B) for the exact re-scoring of rg_flash_argmax_exact; the
+// operand planes past the ones it multiplies (2, or 1 and 2) are never read
+// (not even DMA'd).
 template <int HF, int NT, bool CM>
 __global__ __launch_bounds__(64 * fl_nw(HF, 1)) void k_flash_amax(
     const bf16x8* __restrict__ Hk, const bf16x8* __restrict__ Wk, const float* __restrict__ bias_pad, int B, int A,
@@ -517,7 +518,7 @@ __global__ __launch_bounds__(64 * fl_nw(HF, 1)) void k_flash_amax(
   const int nch = max(0, min(nct, c0 + cps) - c0);
 #define FA_ISSUE(C, SK, SB)                                                    \
   do {                                                                         \
-    stage<EK, NW, NT != 3>(Wk + (int64_t)(C) * EK, SK, w, lane16);             \
+    stage<EK, NW, NT == 1 ? 1 : NT == 3 ? 2 : 3>(Wk + (int64_t)(C) * EK, SK, w, lane16); \
     if (w == 0 && lane < 8) blds16(rsrc_of(bias_pad + 32 * (C)), SB, lane16, 0); \
   } while (0)
   if (nch > 0) FA_ISSUE(c0, sk0, sb0);
@@ -528,7 +529,7 @@ __global__ __launch_bounds__(64 * fl_nw(HF, 1)) void k_flash_amax(
     for (int rb = 0; rb < 2; ++rb)
 #pragma unroll
       for (int p = 0; p < 3; ++p)
-        hk[s][rb][p] = active && (NT != 3 || p < 2)
+        hk[s][rb][p] = active && p < (NT == 1 ? 1 : NT == 3 ? 2 : 3)
                            ? Hk[(((int64_t)(r0 >> 5) * NS + s) * 2 + rb) * 192 + p * 64 + lane]
                            : bf16x8{};
   float bv[2] = {NEG_INF, NEG_INF};
@@ -540,12 +541,12 @@ __global__ __launch_bounds__(64 * fl_nw(HF, 1)) void k_flash_amax(
     for (int ib = 0; ib < 2; ++ib)
 #pragma unroll
       for (int rb = 0; rb < 2; ++rb) sa[ib][rb] = f4{0.f, 0.f, 0.f, 0.f};
-    bf16x8 a0 = sk[lane], a1 = sk[64 + lane], a2 = NT == 3 ? a0 : sk[128 + lane];
+    bf16x8 a0 = sk[lane], a1 = NT == 1 ? a0 : sk[64 + lane], a2 = NT <= 3 ? a0 : sk[128 + lane];
 #pragma unroll
     for (int t = 0; t < 2 * NS; ++t) {
       const int s = t >> 1, ib = t & 1;
       const int en = (t + 1 < 2 * NS ? t + 1 : t) * 192 + lane;
-      const bf16x8 n0 = sk[en], n1 = sk[en + 64], n2 = NT == 3 ? n0 : sk[en + 128];
+      const bf16x8 n0 = sk[en], n1 = NT == 1 ? n0 : sk[en + 64], n2 = NT <= 3 ? n0 : sk[en + 128];
 #pragma unroll
       for (int rb = 0; rb < 2; ++rb)
         sa[ib][rb] = mfma16_split<NT>(a0, a1, a2, hk[s][rb][0], hk[s][rb][1], hk[s][rb][2], sa[ib][rb]);
@@ -1941,15 +1942,22 @@ extern "C" int rg_flash_dw_adam(const void* Hk, const void* Hr, const void* Wk, 
 }
 
 // Exact argmax through screening (the double-Q target of SQN / SMORL at the
-// cost of 3 plane products instead of 6): k_flash_amax<NT = 3> leaves the
-// per-split first maximum and every chunk's row maximum of the 3-term logits;
-// the caller merges the former (rg_flash_argmax) and then
+// cost of 3 plane products — or 1 — instead of 6): k_flash_amax<NT = terms>
+// leaves the per-split first maximum and every chunk's row maximum of the
+// screened logits; the caller merges the former (rg_flash_argmax) and then
 // rg_flash_argmax_exact re-scores, in fp32 (fmaf chain over k, + bias), every
-// item of every chunk whose 3-term maximum lies within the error bound
+// item of every chunk whose screened maximum lies within the error bound
 // tol·||h_b||_2·max_a||W_a||_2 of the row's best, and keeps the first maximum.
+// The bound on |z − z_screened| per item: 3 products drop terms of 2^-16
+// |a||b| and smaller (≈ 3·2^-18 summed), 1 product keeps a0·b0 only:
+// |ab − a0 b0| ≤ (2^-8 + 2^-18)|a||b| (RNE to bf16: |a − a0| ≤ 2^-9 |a|),
+// so ≤ 3.91e-3·||h||·||W_a|| over k; the candidates need twice that (the
+// screened best may itself be over-estimated) — the caller's tol.
 extern "C" int rg_flash_amax_screen(const void* Hk, const void* Wk, const float* bias_pad, int B, int A, int HF,
-                                    int nsplit, float* pbest, int32_t* parg, float* cmax, hipStream_t stream) {
-  if (B <= 0 || A <= 0 || (B % 32) || nsplit <= 0 || !Hk || !Wk || !bias_pad || !pbest || !parg || !cmax)
+                                    int nsplit, int terms, float* pbest, int32_t* parg, float* cmax,
+                                    hipStream_t stream) {
+  if (B <= 0 || A <= 0 || (B % 32) || nsplit <= 0 || (terms != 1 && terms != 3) || !Hk || !Wk || !bias_pad ||
+      !pbest || !parg || !cmax)
     return RG_ERR_ARG;
   if (!flash_hf_ok(HF)) return RG_ERR_SHAPE;
   const int nct = (A + 31) / 32;
@@ -1957,9 +1965,15 @@ extern "C" int rg_flash_amax_screen(const void* Hk, const void* Wk, const float*
   const int rpb = fl_rows(HF, 1);
   const int nrb = (B + rpb - 1) / rpb;
   const dim3 grid((unsigned)(nrb * nsplit));
-#define FS(HFV)                                                                                                   \
-  hipLaunchKernelGGL((k_flash_amax<HFV, 3, true>), grid, dim3(64 * fl_nw(HFV, 1)), 0, stream, (const bf16x8*)Hk,  \
+#define FS1(HFV, NTV)                                                                                             \
+  hipLaunchKernelGGL((k_flash_amax<HFV, NTV, true>), grid, dim3(64 * fl_nw(HFV, 1)), 0, stream, (const bf16x8*)Hk, \
                      (const bf16x8*)Wk, bias_pad, B, A, nrb, nsplit, cps, pbest, parg, cmax)
+#define FS(HFV)      \
+  if (terms == 1) {  \
+    FS1(HFV, 1);     \
+  } else {           \
+    FS1(HFV, 3);     \
+  }
   switch (HF) {
     case 32: FS(32); break;
     case 64: FS(64); break;
@@ -1967,6 +1981,7 @@ extern "C" int rg_flash_amax_screen(const void* Hk, const void* Wk, const float*
     case 256: FS(256); break;
   }
 #undef FS
+#undef FS1
   RG_LAUNCH_CHECK();
   return RG_OK;
 }

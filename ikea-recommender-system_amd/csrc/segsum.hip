@@ -294,19 +294,23 @@ extern "C" int rg_scatter_rows(const int32_t* ids, const float* src, int E, int 
 // row-gradients sent back shrink ~50× against one per token.
 //
 // rg_shard_dedup (the forward, on the gather's critical path): no sort.  A
-// mark per table row — marks[id + 1] = 1 for every token's id (invalid ids
-// −1 at index 0, so they come first and go with rank 0's group) — and one
-// inclusive scan over the N1 + 1 marks give each distinct id its index u =
-// pos[id + 1] − 1 in increasing id order; the ids of one owner are a
-// contiguous range, so that order is grouped by owner and
+// mark byte per table row — byte id + 1 set to 1 for every token's id (an
+// invalid id −1 is byte 0, so it comes first and goes with rank 0's group;
+// plain byte stores: every token of an id writes the same value, where
+// atomic bit-ORs serialised on the Zipf-hot words, 134 µs at C2) — and one
+// exclusive scan of the popcounts of the marks' 32-bit words (a word holds
+// four 0/1 bytes) rank the marked ids: u = rank(id + 1) in increasing id
+// order.  The ids of one owner are a contiguous range, so that order is
+// grouped by owner and
 //   uslot[t]  = u of token t (rg_place_rows reads rows_in[uslot[t]]),
 //   uids[u]   = the distinct ids in increasing order (−1 first, if any),
 //   counts[o] = distinct ids owned by rank o (owner ⌈(id+1)·W/N1⌉ − 1):
-//               pos at the owner's last index minus pos before its first,
-//   *nuniq    = U = pos[N1];
-// four launches (clear, mark, scan, write) whose cost is the scan's ~8 B per
-// table row instead of a multi-pass sort of the tokens.  The write also
-// leaves (u, t) key / value pairs in the work buffer for the backward.
+//               rank past the owner's last byte minus rank of its first,
+//   *nuniq    = U = rank(N1 + 1);
+// five short launches (clear, mark, scan init + scan, write) over N1 bytes
+// of marks and N1 of prefix instead of a multi-pass sort of the tokens.
+// The write also leaves (u, t) key / value pairs in the work buffer for the
+// backward.
 // rg_shard_dedup_grads (the backward): a stable radix sort of those pairs
 // by u (token order within one u) and gsend[u] = Σ of the token rows of u,
 // summed in token order (k_seg_blocks / k_seg_cross over the sorted runs: a
@@ -317,24 +321,43 @@ namespace {
 __device__ __forceinline__ int dd_index(int32_t id, int64_t N1) { return id >= 0 && id < N1 ? id + 1 : 0; }
 
 __global__ void k_dd_mark(const int32_t* __restrict__ tok_id, const int32_t* __restrict__ n_ptr, int n_max,
-                          int64_t N1, int32_t* __restrict__ marks) {
+                          int64_t N1, uint8_t* __restrict__ marks) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n_max || i >= *n_ptr) return;
   marks[dd_index(tok_id[i], N1)] = 1;   // (same value from every token of an id)
 }
 
-__global__ void k_dd_write(const int32_t* __restrict__ tok_id, const int32_t* __restrict__ pos,
-                           const int32_t* __restrict__ n_ptr, int n_max, int64_t N1, int W,
-                           int32_t* __restrict__ uslot, int32_t* __restrict__ uids, uint32_t* __restrict__ keys,
-                           int32_t* __restrict__ vals, int32_t* __restrict__ counts, int32_t* __restrict__ nuniq) {
+struct Popc {
+  __host__ __device__ int operator()(uint32_t x) const {
+#ifdef __HIP_DEVICE_COMPILE__
+    return __popc(x);
+#else
+    return __builtin_popcount(x);
+#endif
+  }
+};
+
+// marked indices below k (k <= N1 + 1; pos = exclusive prefix over the mark words)
+__device__ __forceinline__ int dd_rank(const uint32_t* words, const int32_t* pos, int64_t k, int64_t nwords) {
+  const int64_t w = k >> 2;
+  if (w >= nwords) return pos[nwords - 1] + __popc(words[nwords - 1]);
+  const int sh = 8 * (int)(k & 3);
+  return pos[w] + (sh ? __popc(words[w] & ((1u << sh) - 1u)) : 0);
+}
+
+__global__ void k_dd_write(const int32_t* __restrict__ tok_id, const uint32_t* __restrict__ words,
+                           const int32_t* __restrict__ pos, int64_t nwords, const int32_t* __restrict__ n_ptr,
+                           int n_max, int64_t N1, int W, int32_t* __restrict__ uslot, int32_t* __restrict__ uids,
+                           uint32_t* __restrict__ keys, int32_t* __restrict__ vals, int32_t* __restrict__ counts,
+                           int32_t* __restrict__ nuniq) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (blockIdx.x == 0) {
     if (threadIdx.x < W) {   // owner o: ids [o·N1/W, (o+1)·N1/W) = mark indices (o·N1/W, (o+1)·N1/W]
       const int o = threadIdx.x;
       const int64_t hi = ((int64_t)(o + 1) * N1) / W, lo = ((int64_t)o * N1) / W;
-      counts[o] = pos[hi] - (o == 0 ? 0 : pos[lo]);
+      counts[o] = dd_rank(words, pos, hi + 1, nwords) - (o == 0 ? 0 : dd_rank(words, pos, lo + 1, nwords));
     }
-    if (threadIdx.x == 0) *nuniq = pos[N1];
+    if (threadIdx.x == 0) *nuniq = dd_rank(words, pos, N1 + 1, nwords);
   }
   if (i >= n_max) return;
   vals[i] = i;
@@ -343,7 +366,7 @@ __global__ void k_dd_write(const int32_t* __restrict__ tok_id, const int32_t* __
     return;
   }
   const int k = dd_index(tok_id[i], N1);
-  const int u = pos[k] - 1;
+  const int u = dd_rank(words, pos, k, nwords);
   uslot[i] = u;
   keys[i] = (uint32_t)u;
   uids[u] = k - 1;   // (same value from every token of an id)
@@ -352,6 +375,7 @@ __global__ void k_dd_write(const int32_t* __restrict__ tok_id, const int32_t* __
 struct DedupLayout {
   size_t keys_in, keys_out, vals_in, vals_out, marks, pos, part_first, part_last, tmp, total, sort_bytes,
       scan_bytes;
+  int64_t nwords;
   int bits;
 };
 
@@ -364,15 +388,17 @@ DedupLayout dedup_layout(int n_max, int E, int64_t N1) {
   L.keys_out = off; off += al(sizeof(uint32_t) * n_max);
   L.vals_in = off; off += al(sizeof(int32_t) * n_max);
   L.vals_out = off; off += al(sizeof(int32_t) * n_max);
-  L.marks = off; off += al(sizeof(int32_t) * (N1 + 1));
-  L.pos = off; off += al(sizeof(int32_t) * (N1 + 1));
+  L.nwords = (N1 + 1 + 3) / 4;   // mark bytes, four per word
+  L.marks = off; off += al(sizeof(uint32_t) * L.nwords);
+  L.pos = off; off += al(sizeof(int32_t) * L.nwords);
   L.part_first = off; off += al(sizeof(float) * nb * E);
   L.part_last = off; off += al(sizeof(float) * nb * E);
   L.bits = key_bits(n_max);   // keys u < U <= n_max, the sentinel's low bits above them
   size_t ts = 0, tc = 0;
   hipcub::DeviceRadixSort::SortPairs(nullptr, ts, (const uint32_t*)nullptr, (uint32_t*)nullptr,
                                      (const int32_t*)nullptr, (int32_t*)nullptr, n_max, 0, L.bits);
-  hipcub::DeviceScan::InclusiveSum(nullptr, tc, (const int32_t*)nullptr, (int32_t*)nullptr, (int)(N1 + 1));
+  hipcub::TransformInputIterator<int, Popc, const uint32_t*> pc((const uint32_t*)nullptr, Popc());
+  hipcub::DeviceScan::ExclusiveSum(nullptr, tc, pc, (int32_t*)nullptr, (int)L.nwords);
   L.sort_bytes = ts;
   L.scan_bytes = tc;
   L.tmp = off; off += al(ts > tc ? ts : tc);
@@ -396,16 +422,17 @@ extern "C" int rg_shard_dedup(const int32_t* tok_id, const int32_t* n_ptr, int n
   const DedupLayout L = dedup_layout(n_max, E, N1);
   if (work_bytes < (int64_t)L.total) return RG_ERR_ARG;
   char* w = static_cast<char*>(work);
-  int32_t* marks = (int32_t*)(w + L.marks);
+  uint32_t* bits = (uint32_t*)(w + L.marks);
   int32_t* pos = (int32_t*)(w + L.pos);
   const dim3 g((unsigned)((n_max + 255) / 256));
-  if (hipMemsetAsync(marks, 0, sizeof(int32_t) * (N1 + 1), stream) != hipSuccess) return RG_ERR_LAUNCH;
-  hipLaunchKernelGGL(k_dd_mark, g, dim3(256), 0, stream, tok_id, n_ptr, n_max, N1, marks);
+  if (hipMemsetAsync(bits, 0, sizeof(uint32_t) * L.nwords, stream) != hipSuccess) return RG_ERR_LAUNCH;
+  hipLaunchKernelGGL(k_dd_mark, g, dim3(256), 0, stream, tok_id, n_ptr, n_max, N1, (uint8_t*)bits);
   size_t tc = L.scan_bytes;
-  if (hipcub::DeviceScan::InclusiveSum(w + L.tmp, tc, marks, pos, (int)(N1 + 1), stream) != hipSuccess)
+  hipcub::TransformInputIterator<int, Popc, const uint32_t*> pc(bits, Popc());
+  if (hipcub::DeviceScan::ExclusiveSum(w + L.tmp, tc, pc, pos, (int)L.nwords, stream) != hipSuccess)
     return RG_ERR_LAUNCH;
-  hipLaunchKernelGGL(k_dd_write, g, dim3(256), 0, stream, tok_id, pos, n_ptr, n_max, N1, W, uslot, uids,
-                     (uint32_t*)(w + L.keys_in), (int32_t*)(w + L.vals_in), counts, nuniq);
+  hipLaunchKernelGGL(k_dd_write, g, dim3(256), 0, stream, tok_id, bits, pos, L.nwords, n_ptr, n_max, N1, W, uslot,
+                     uids, (uint32_t*)(w + L.keys_in), (int32_t*)(w + L.vals_in), counts, nuniq);
   RG_LAUNCH_CHECK();
   return RG_OK;
 }

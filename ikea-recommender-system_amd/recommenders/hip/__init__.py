@@ -56,8 +56,16 @@ SIGNATURES = {
     "rg_flash_argmax": [P, P, I, I, P, P, P],
     "rg_flash_amax_fwd": [P, P, P, I, I, I, I, I, P, P, P],
     "rg_flash_score": [P, P, P, I, I, I, I, I, P, P, P, P, P, P],
-    "rg_flash_amax_screen": [P, P, P, I, I, I, I, P, P, P, P],
+    "rg_flash_amax_screen": [P, P, P, I, I, I, I, I, P, P, P, P],
     "rg_row_norm_max": [P, I64, I, P, P],
+    "rg_comm_id_bytes": [],
+    "rg_comm_unique_id": [P],
+    "rg_comm_init": [P, I, I, I, P],
+    "rg_comm_destroy": [P],
+    "rg_comm_alltoallv": [P, P, P, P, P, I, P],
+    "rg_comm_allreduce": [P, P, P, I64, I, P],
+    "rg_comm_allgather": [P, P, P, I64, I, P],
+    "rg_comm_reduce_scatter": [P, P, P, I64, I, P],
     "rg_flash_argmax_exact": [P, I, I, P, P, P, I, P, F, P, P, P, P, P, P, P],
     "rg_flash_topk_cap": [],
     "rg_flash_topk": [P, I, I, I, I, F, F, P, P, P, I, P, P, P, P, P, P, P],

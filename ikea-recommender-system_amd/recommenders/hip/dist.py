@@ -1,13 +1,53 @@
 """Collectives for the multi-GPU step (one process per GPU, torch.distributed).
 
 With the "nccl" backend (= RCCL on ROCm, xGMI inside a node) device tensors
-go straight to the collective; with "gloo" the same calls are staged through
-host memory — used to run several ranks on one GPU in tests and on CPU.
+go to the library's own RCCL communicator (csrc/comm.hip): every collective
+is enqueued on the CURRENT stream — the stream of the kernels around it — so
+it costs no cross-stream hops and no process-group bookkeeping (the step's
+exchanges are latency-bound: KB to MB between microsecond kernels).
+RG_COMM=torch routes them through torch.distributed's own RCCL calls instead
+(A/B).  With "gloo" the same calls are staged through host memory — used to
+run several ranks on one GPU in tests and on CPU.
 """
 from __future__ import annotations
 
+import ctypes
+import os
+
 import numpy as np
 import torch
+
+# dtype codes of csrc/comm.hip
+_DT = {torch.uint8: 0, torch.int32: 1, torch.float32: 2, torch.float16: 3, torch.int64: 4}
+_NATIVE = {}   # (process group, world, rank) -> (group, communicator handle)
+
+
+def _native_comm(dist, group, host_group, rank, world):
+    """The library's RCCL communicator for this process group (one per group
+    and process: trainers built on the same group share it)."""
+    from . import call
+    pg = group if group is not None else dist.distributed_c10d._get_default_group()
+    key = (id(pg), world, rank)
+    hit = _NATIVE.get(key)
+    if hit is not None:
+        return hit[1]
+    uid = torch.zeros(call("rg_comm_id_bytes"), dtype=torch.uint8)
+    if rank == 0:
+        call("rg_comm_unique_id", uid.data_ptr())
+    src = dist.get_global_rank(host_group, 0) if host_group is not None else 0
+    dist.broadcast(uid, src=src, group=host_group)
+    h = ctypes.c_void_p()
+    call("rg_comm_init", uid.data_ptr(), world, rank, torch.cuda.current_device(), ctypes.addressof(h))
+    _NATIVE[key] = (pg, h.value)   # (the group is kept alive: its id stays unique)
+    return h.value
+
+
+class _Done:
+    """Work handle of a stream-ordered native collective: already ordered on
+    the stream it was issued on."""
+
+    def wait(self):
+        return None
 
 
 class Comm:
@@ -24,6 +64,23 @@ class Comm:
         # the host from the host batch): a gloo group next to RCCL, so the
         # count exchange never waits on the device stream
         self.host_group = dist.new_group(backend="gloo") if self.native else group
+        self.rc = None
+        if self.native and os.environ.get("RG_COMM", "native") != "torch":
+            self.rc = _native_comm(dist, group, self.host_group, self.rank, self.world)
+
+    def _st(self):
+        from . import stream_ptr
+        return stream_ptr()
+
+    @staticmethod
+    def _dt(t):
+        return _DT.get(t.dtype, 0)
+
+    @staticmethod
+    def _units(t):
+        """elements of the collective's dtype per row of t (bytes for other dtypes)"""
+        n = int(np.prod(t.shape[1:])) if t.dim() > 1 else 1
+        return n if t.dtype in _DT else n * t.element_size()
 
     def host_all_gather(self, t):
         """(world, *t.shape) CPU tensor of every rank's CPU tensor ``t`` (no device sync)."""
@@ -34,6 +91,13 @@ class Comm:
 
     def all_gather(self, out, inp):
         """out (world·n) ← concat over ranks of inp (n), rank-major."""
+        if self.rc is not None:
+            inp = inp.contiguous()
+            assert out.is_contiguous() and out.numel() == self.world * inp.numel() and out.dtype == inp.dtype
+            n = inp.numel() if inp.dtype in _DT else inp.numel() * inp.element_size()
+            from . import call
+            call("rg_comm_allgather", self.rc, inp.data_ptr(), out.data_ptr(), n, self._dt(inp), self._st())
+            return out
         if self.native:
             self.dist.all_gather_into_tensor(out, inp.contiguous(), group=self.group)
             return out
@@ -44,6 +108,13 @@ class Comm:
 
     def reduce_scatter(self, out, inp):
         """out (n) ← slice `rank` of the elementwise sum over ranks of inp (world·n)."""
+        if self.rc is not None:
+            inp = inp.contiguous()
+            assert out.is_contiguous() and inp.numel() == self.world * out.numel() and inp.dtype in _DT
+            from . import call
+            call("rg_comm_reduce_scatter", self.rc, inp.data_ptr(), out.data_ptr(), out.numel(), self._dt(inp),
+                 self._st())
+            return out
         if self.native:
             self.dist.reduce_scatter_tensor(out, inp.contiguous(), group=self.group)
             return out
@@ -56,6 +127,16 @@ class Comm:
     def all_to_all(self, out, inp, out_splits, in_splits):
         """Variable all-to-all along dim 0: rows [Σ in_splits[:q], +in_splits[q])
         of ``inp`` go to rank q; ``out`` receives out_splits[q] rows from q."""
+        if self.rc is not None:
+            inp = inp.contiguous()
+            assert out.is_contiguous() and out.dtype == inp.dtype
+            from . import call
+            u = self._units(inp)
+            sc = (ctypes.c_int64 * self.world)(*[int(x) * u for x in in_splits])
+            rc = (ctypes.c_int64 * self.world)(*[int(x) * u for x in out_splits])
+            call("rg_comm_alltoallv", self.rc, inp.data_ptr() if inp.numel() else None, sc,
+                 out.data_ptr() if out.numel() else None, rc, self._dt(inp), self._st())
+            return out
         if self.native:
             self.dist.all_to_all_single(out, inp.contiguous(), list(out_splits), list(in_splits), group=self.group)
             return out
@@ -66,6 +147,11 @@ class Comm:
         return out
 
     def all_reduce(self, t, async_op=False):
+        if self.rc is not None:
+            assert t.is_contiguous() and t.dtype in _DT and t.dtype != torch.uint8
+            from . import call
+            call("rg_comm_allreduce", self.rc, t.data_ptr(), t.data_ptr(), t.numel(), self._dt(t), self._st())
+            return _Done() if async_op else None
         if self.native:
             return self.dist.all_reduce(t, group=self.group, async_op=async_op)
         c = t.detach().cpu().contiguous()

@@ -749,6 +749,13 @@ SPLIT_TERMS = {"f32x9": 9, "f32x6": 6, "f32x6d3": 636}
 # (DESIGN §4a).  Needs ceil(A/32)·B floats of chunk maxima; above SCREEN_CMAX_BYTES the rows
 # are screened in 2048-row chunks (C5 at one GPU).
 SCREEN_TOL = 1e-4
+# screening plane products of the double-Q argmax: 1 (the leading bf16 planes
+# only: a third of the MFMA work of 3) with the wider bound SCREEN_TOL_1 =
+# 2 × 3.91e-3 + margin (csrc/head_flash.hip rg_flash_amax_screen) — C4 184.6K
+# -> 198.6K session-steps/s with no row past the candidate cap
+# (profiles/r06/ab_c4_screen_terms.txt); 3 keeps SCREEN_TOL
+SCREEN_TERMS = 1
+SCREEN_TOL_1 = 8e-3
 SCREEN_CMAX_BYTES = 2 << 30
 SCREEN_ROW_CHUNK = 2048
 LOGIT_TERMS = {"f32x9": 9, "f32x6": 6, "f32x6d3": 6}
@@ -975,7 +982,7 @@ class SoftmaxHead:
 
     def _screened_argmax(self, aw, Hk, Wk, bias_pad, h, Wp, bp, out_idx, out_val, wnorm_ready=False):
         """First maximum of the fp32 logits h·Wᵀ + b per row into out_idx /
-        out_val: screening on 3 plane products (rows in aw.Bc chunks, so the
+        out_val: screening on SCREEN_TERMS plane products (rows in aw.Bc chunks, so the
         chunk maxima fit SCREEN_CMAX_BYTES), then every item of every chunk
         within the screening's error bound re-scored in fp32
         (rg_flash_argmax_exact; a row past the candidate cap is scanned whole).
@@ -990,11 +997,12 @@ class SoftmaxHead:
         for r0 in range(0, B, aw.Bc):
             bc = min(aw.Bc, B - r0)
             call("rg_flash_amax_screen", Hk.data_ptr() + r0 * hk_row, Wk.data_ptr(), bias_pad.data_ptr(), bc, A, HF,
-                 aw.nsplit, aw.pbest.data_ptr(), aw.parg.data_ptr(), aw.cmax.data_ptr(), st)
+                 aw.nsplit, SCREEN_TERMS, aw.pbest.data_ptr(), aw.parg.data_ptr(), aw.cmax.data_ptr(), st)
             call("rg_flash_argmax", aw.pbest.data_ptr(), aw.parg.data_ptr(), aw.nsplit, bc,
                  out_idx.data_ptr() + 4 * r0, out_val.data_ptr() + 4 * r0, st)
             call("rg_flash_argmax_exact", aw.cmax.data_ptr(), bc, A, h.data_ptr() + 4 * r0 * HF, W, b, HF,
-                 aw.wnorm.data_ptr(), _f32(SCREEN_TOL), aw.lim.data_ptr() + 4 * r0,
+                 aw.wnorm.data_ptr(), _f32(SCREEN_TOL if SCREEN_TERMS == 3 else SCREEN_TOL_1),
+                 aw.lim.data_ptr() + 4 * r0,
                  aw.cand.data_ptr() + 4 * r0 * cap, aw.ncand.data_ptr() + 4 * r0,
                  out_idx.data_ptr() + 4 * r0, out_val.data_ptr() + 4 * r0, self.top_scanned.data_ptr(), st)
 
@@ -1034,7 +1042,7 @@ class SoftmaxHead:
             call("rg_head_planes", hs.data_ptr(), R, HF, w.Hk.data_ptr(), None, None, None, st)
             if screen:
                 call("rg_flash_amax_screen", w.Hk.data_ptr(), Wk.data_ptr(), bias_pad.data_ptr(), R, A, HF, w.nsplit,
-                     w.pbest.data_ptr(), w.parg.data_ptr(), w.cmax.data_ptr(), st)
+                     3, w.pbest.data_ptr(), w.parg.data_ptr(), w.cmax.data_ptr(), st)
                 call("rg_flash_topk_screened", w.cmax.data_ptr(), R, n, A, K, _f32(SCREEN_TOL), w.wnorm.data_ptr(),
                      hs.data_ptr(), Wp.p.data_ptr(), bp.p.data_ptr(), HF, w.cand.data_ptr(), w.ncand.data_ptr(),
                      w.idx.data_ptr() + 4 * r0 * K, w.vals.data_ptr() + 4 * r0 * K, self.top_scanned.data_ptr(),

@@ -189,8 +189,10 @@ int rg_flash_amax_fwd(const void* Hk, const void* Wk, const float* bias_pad, int
 int rg_flash_argmax(const float* pbest, const int32_t* parg, int nsplit, int B, int32_t* out, float* out_max,
                     rg_stream_t stream);
 /* Exact argmax by screening (the same double-Q target at half the MFMA work):
- * rg_flash_amax_screen: rg_flash_amax_fwd on 3 plane products (planes 0-1 only) that also writes
- *   every 32-item chunk's row maximum cmax (ceil(A/32) × B); merge pbest/parg with rg_flash_argmax.
+ * rg_flash_amax_screen: rg_flash_amax_fwd on terms = 3 plane products (planes 0-1 only) or 1
+ *   (plane 0 only) that also writes every 32-item chunk's row maximum cmax (ceil(A/32) × B); merge
+ *   pbest/parg with rg_flash_argmax.  The screened logit is within 3·2^-18 (terms 3) / 3.91e-3
+ *   (terms 1) of ||h_b||_2·||W_a||_2 of the fp32 one; tol below must cover twice that.
  * rg_row_norm_max: out[0] = max_a ||W_a||_2 (A × HF rows, HF % 4 == 0).
  * rg_flash_argmax_exact: re-scores in fp32 (fmaf chain over k, + bias) every item of every chunk whose
  *   screened maximum is >= tau − (tol·||h_b||_2·wnorm[0] + 1e-6·|tau|), tau = out_val (rg_flash_argmax's
@@ -199,7 +201,7 @@ int rg_flash_argmax(const float* pbest, const int32_t* parg, int nsplit, int B, 
  *   (the first maximum of every item's fp32 logit) and counted in err (optional).  lim: B floats,
  *   cand: B × rg_flash_topk_cap() int32, ncand: B int32 (work). */
 int rg_flash_amax_screen(const void* Hk, const void* Wk, const float* bias_pad, int B, int A, int HF, int nsplit,
-                         float* pbest, int32_t* parg, float* cmax, rg_stream_t stream);
+                         int terms, float* pbest, int32_t* parg, float* cmax, rg_stream_t stream);
 int rg_row_norm_max(const float* W, int64_t A, int HF, float* out, rg_stream_t stream);
 int rg_flash_argmax_exact(const float* cmax, int B, int A, const float* h, const float* W, const float* bias, int HF,
                           const float* wnorm, float tol, float* lim, int32_t* cand, int32_t* ncand, int32_t* out_idx,
@@ -471,10 +473,13 @@ int rg_bpr_dz(float* Z, int64_t zsb, int64_t zss, const float* zpos, int B, int 
  * rg_shard_dedup: over the T = *n_ptr tokens (n_max >= T): uids[0..U) = the distinct ids in
  *   increasing order (-1 first when a token was invalid: it goes to rank 0, whose gather returns a
  *   zero row), uslot[t] = the token's index into uids, counts[o] = distinct ids owned by rank o
- *   (world <= 256; uids is grouped by owner), *nuniq = U.  work: rg_shard_dedup_work_bytes(n_max,
- *   E, n_rows); it keeps the sorted order for rg_shard_dedup_grads of the same pass.
+ *   (world <= 256; uids is grouped by owner), *nuniq = U; ids outside [0, n_rows) count as -1.
+ *   No sort: a mark per table row and one scan over the n_rows + 1 marks.  work:
+ *   rg_shard_dedup_work_bytes(n_max, E, n_rows); it keeps the (u, t) pairs for
+ *   rg_shard_dedup_grads of the same pass.
  * rg_shard_dedup_grads: gsend[u] = Σ_{t : uslot[t] = u} src[t] (E floats per row, summed in token
- *   order — deterministic), for the pass's last rg_shard_dedup on `work` (same n_max, n_rows).
+ *   order — a stable sort of the pairs by u, then segmented sums: deterministic), for the pass's
+ *   last rg_shard_dedup on `work` (same n_max, n_rows).
  * rg_shard_route: stable partition of the T = *ntok_ptr rows by owner rank: slot[t] (send
  *   position), send_ids[slot[t]] = tok_id[t], counts[world] (world <= 8; the sharded sampled
  *   head's per-row target exchange).
@@ -530,6 +535,28 @@ int rg_rows_unslot(const float* rows, int ld, const int32_t* slot, const int32_t
                    float* tb, int64_t* trow, rg_stream_t stream);
 int rg_rows_slot(const float* grows, const float* gb, const int32_t* slot, int n, int HF, int ld, float* gsend,
                  rg_stream_t stream);
+
+/* ---- §8e collectives of the item-sharded step (csrc/comm.hip; RCCL over xGMI): the library's own
+ * communicator, every collective enqueued on the CALLER's stream (the stream of the kernels that
+ * produce and consume its buffers: no cross-stream hops).  Replaces the torch.distributed calls
+ * of recommenders/hip/dist.py Comm on the nccl backend.  dtype codes: 0 u8, 1 i32, 2 f32, 3 f16,
+ * 4 i64.
+ * rg_comm_unique_id: rank 0's id (rg_comm_id_bytes() bytes), broadcast by the host to every rank.
+ * rg_comm_init: *comm = the communicator of `rank` among `world` (collective; device made current).
+ * rg_comm_alltoallv: send_counts[q] elements (consecutive, rank order) to rank q, recv_counts[q]
+ *   from rank q (HOST int64 arrays of world entries); one group of sends / receives.
+ * rg_comm_allreduce: SUM of n elements (in place when send == recv).
+ * rg_comm_allgather: recv (world·n) <- every rank's n, rank-major.
+ * rg_comm_reduce_scatter: recv (n) <- slice rank of the SUM over ranks of send (world·n). */
+int rg_comm_id_bytes(void);
+int rg_comm_unique_id(void* out);
+int rg_comm_init(const void* id, int world, int rank, int device, void** comm);
+int rg_comm_destroy(void* comm);
+int rg_comm_alltoallv(void* comm, const void* send, const int64_t* send_counts, void* recv,
+                      const int64_t* recv_counts, int dtype, rg_stream_t stream);
+int rg_comm_allreduce(void* comm, const void* send, void* recv, int64_t n, int dtype, rg_stream_t stream);
+int rg_comm_allgather(void* comm, const void* send, void* recv, int64_t n, int dtype, rg_stream_t stream);
+int rg_comm_reduce_scatter(void* comm, const void* send, void* recv, int64_t n, int dtype, rg_stream_t stream);
 
 /* items per online-softmax partial block of rg_head_fwd: pmax/psum/parg hold ceil(A/that) x B */
 int rg_partial_block(void);

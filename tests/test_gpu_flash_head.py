@@ -666,14 +666,16 @@ def test_fused_argmax_only(precision, B, A, HF, nsplit):
     assert not (got == A - 5).any()            # never the later duplicate of 11
 
 
+@pytest.mark.parametrize("terms,tol", [(3, 1e-4), (1, 8e-3)])
 @pytest.mark.parametrize("B,A,HF,nsplit", [(256, 50000, 128, 8), (96, 20011, 64, 16), (64, 5003, 256, 8),
                                            (64, 777, 32, 3)])
-def test_screening_argmax_is_exact(B, A, HF, nsplit):
+def test_screening_argmax_is_exact(B, A, HF, nsplit, terms, tol):
     """rg_flash_amax_screen + rg_flash_argmax_exact (the SQN / SMORL double-Q
     target, sqn_gru.py:222-226): the first maximum of the fp32 logits, also
-    where the 3-term screening alone would pick a different item — planted
-    exact ties (duplicate rows: lowest index) and near-ties (1e-6 apart, far
-    below the screening error) — and a row with h = 0 (logits = bias)."""
+    where the 3-term (or 1-term, with its wider bound) screening alone would
+    pick a different item — planted exact ties (duplicate rows: lowest index)
+    and near-ties (1e-6 apart, far below the screening error) — and a row
+    with h = 0 (logits = bias)."""
     call, st = C().call, C().stream_ptr()
     g = torch.Generator().manual_seed(A + HF)
     h = torch.tanh(torch.randn(B, HF, generator=g) * 2)
@@ -704,8 +706,8 @@ def test_screening_argmax_is_exact(B, A, HF, nsplit):
     pbest = torch.empty(nsplit, B, device=dev)
     parg = torch.empty(nsplit, B, dtype=torch.int32, device=dev)
     cmax = torch.empty((A + 31) // 32, B, device=dev)
-    call("rg_flash_amax_screen", Hk.data_ptr(), Wk.data_ptr(), bp.data_ptr(), B, A, HF, nsplit, pbest.data_ptr(),
-         parg.data_ptr(), cmax.data_ptr(), st)
+    call("rg_flash_amax_screen", Hk.data_ptr(), Wk.data_ptr(), bp.data_ptr(), B, A, HF, nsplit, terms,
+         pbest.data_ptr(), parg.data_ptr(), cmax.data_ptr(), st)
     idx = torch.empty(B, dtype=torch.int32, device=dev)
     val = torch.empty(B, device=dev)
     call("rg_flash_argmax", pbest.data_ptr(), parg.data_ptr(), nsplit, B, idx.data_ptr(), val.data_ptr(), st)
@@ -717,7 +719,7 @@ def test_screening_argmax_is_exact(B, A, HF, nsplit):
     lim = torch.empty(B, device=dev)
     scanned = torch.zeros(1, dtype=torch.int32, device=dev)
     call("rg_flash_argmax_exact", cmax.data_ptr(), B, A, hd.data_ptr(), Wd.data_ptr(), bd.data_ptr(), HF,
-         wn.data_ptr(), 1e-4, lim.data_ptr(), cand.data_ptr(), ncand.data_ptr(),
+         wn.data_ptr(), tol, lim.data_ptr(), cand.data_ptr(), ncand.data_ptr(),
          idx.data_ptr(), val.data_ptr(), scanned.data_ptr(), st)
     torch.cuda.synchronize()
     assert abs(float(wn) - float(W.norm(dim=1).max())) <= 1e-5 * float(W.norm(dim=1).max())
@@ -778,7 +780,7 @@ def test_screening_argmax_overflow_scans_row():
     call("rg_head_planes", Wd.data_ptr(), A, HF, Wk.data_ptr(), None, bd.data_ptr(), bp.data_ptr(), st)
     pbest, parg = torch.empty(nsplit, B, device=dev), torch.empty(nsplit, B, dtype=torch.int32, device=dev)
     cmax = torch.empty((A + 31) // 32, B, device=dev)
-    call("rg_flash_amax_screen", Hk.data_ptr(), Wk.data_ptr(), bp.data_ptr(), B, A, HF, nsplit, pbest.data_ptr(),
+    call("rg_flash_amax_screen", Hk.data_ptr(), Wk.data_ptr(), bp.data_ptr(), B, A, HF, nsplit, 3, pbest.data_ptr(),
          parg.data_ptr(), cmax.data_ptr(), st)
     idx, val = torch.empty(B, dtype=torch.int32, device=dev), torch.empty(B, device=dev)
     call("rg_flash_argmax", pbest.data_ptr(), parg.data_ptr(), nsplit, B, idx.data_ptr(), val.data_ptr(), st)

@@ -610,3 +610,34 @@ def test_qcomb_equals_weighted_sum_planes_norm(A, HF, nh):
     assert torch.equal(pk, pk2) and torch.equal(bp, bp2)
     ref = float(Wr.double().norm(dim=1).max())
     assert abs(float(wn) - float(wn2)) <= 2e-6 * ref and abs(float(wn) - ref) <= 2e-6 * ref
+
+
+@pytest.mark.parametrize("T,W", [(4096, 8), (4096, 1), (3001, 3), (20000, 2), (1, 8), (0, 4)])
+def test_shard_route_is_stable_partition_by_owner(T, W):
+    """rg_shard_route (the sharded sampled head's per-row target exchange,
+    csrc/emb_shard.hip): counts per owner, and every row's send slot — rows
+    grouped by owner (invalid ids with rank 0), in row order within an owner."""
+    from recommenders.hip.dist import item_shard
+    n_rows = 90001
+    rng = np.random.default_rng(T + W)
+    ids = rng.integers(0, n_rows, size=max(T, 1)).astype(np.int32)
+    if T > 10:
+        ids[rng.integers(0, T, size=7)] = -1
+    call = C().call
+    tok = D(torch.from_numpy(ids))
+    nptr = D(torch.tensor([T], dtype=torch.int32))
+    slot = torch.full((max(T, 1),), -5, dtype=torch.int32, device=dev)
+    send = torch.full((max(T, 1),), -5, dtype=torch.int32, device=dev)
+    counts = torch.full((W,), -5, dtype=torch.int32, device=dev)
+    call("rg_shard_route", tok.data_ptr(), nptr.data_ptr(), n_rows, W, slot.data_ptr(), send.data_ptr(),
+         counts.data_ptr(), st())
+    torch.cuda.synchronize()
+    ids = ids[:T]
+    own = np.array([0 if x < 0 else next(r for r in range(W) if item_shard(n_rows, W, r)[0] <= x < item_shard(n_rows, W, r)[1])
+                    for x in ids], dtype=np.int64)
+    order = np.argsort(own, kind="stable")
+    exp_slot = np.empty(T, dtype=np.int64)
+    exp_slot[order] = np.arange(T)
+    np.testing.assert_array_equal(counts.cpu().numpy(), np.bincount(own, minlength=W))
+    np.testing.assert_array_equal(slot[:T].cpu().numpy(), exp_slot)
+    np.testing.assert_array_equal(send[:T].cpu().numpy(), ids[order])
