@@ -1,13 +1,19 @@
 """Collectives for the multi-GPU step (one process per GPU, torch.distributed).
 
 With the "nccl" backend (= RCCL on ROCm, xGMI inside a node) device tensors
-go to the library's own RCCL communicator (csrc/comm.hip): every collective
-is enqueued on the CURRENT stream — the stream of the kernels around it — so
-it costs no cross-stream hops and no process-group bookkeeping (the step's
-exchanges are latency-bound: KB to MB between microsecond kernels).
-RG_COMM=torch routes them through torch.distributed's own RCCL calls instead
-(A/B).  With "gloo" the same calls are staged through host memory — used to
-run several ranks on one GPU in tests and on CPU.
+go straight to torch.distributed's RCCL collectives, which run on the process
+group's own stream.  RG_COMM=native routes them to the library's own RCCL
+communicator instead (csrc/comm.hip): every collective enqueued on the
+CURRENT stream — no cross-stream hops, less host bookkeeping (11 vs 15 µs a
+call at one rank, profiles/r06/commlat_one_rank.txt).  It is not the default:
+without the process group's stream the step's streams land on the GPU's four
+hardware queues differently, and at one rank the default stream then shared
+a queue with the head's pass-2 stream — the trunk backward waited for pass 2,
+C2 item-sharded 285K (torch) vs 265K (native) session-steps/s; with 16
+hardware queues the order flipped (286K native vs 231K torch) and C4 lost
+7 % (profiles/r06/hwqueue_ab.txt), so neither is a fix by itself.
+With "gloo" the same calls are staged through host memory — used to run
+several ranks on one GPU in tests and on CPU.
 """
 from __future__ import annotations
 
@@ -65,7 +71,7 @@ class Comm:
         # count exchange never waits on the device stream
         self.host_group = dist.new_group(backend="gloo") if self.native else group
         self.rc = None
-        if self.native and os.environ.get("RG_COMM", "native") != "torch":
+        if self.native and os.environ.get("RG_COMM", "torch") == "native":
             self.rc = _native_comm(dist, group, self.host_group, self.rank, self.world)
 
     def _st(self):
