@@ -520,7 +520,6 @@ class Trunk:
         rdt = torch.float16 if half else torch.float32
         recv_ids = self._xbuf(w, "recv_ids", max(R, 1))
         w.local_ids = self._xbuf(w, "local_ids_buf", max(R, 1))
-        w.nrecv.fill_(R)
         comm.all_to_all(recv_ids[:R], w.uids[:U], w.recv_splits, w.send_splits)
         rows_out = self._xbuf(w, "rows_out", max(R, 1), self.E, rdt)
         call("rg_rows_gather", recv_ids.data_ptr(), R, self.lo, self.n_local,
@@ -542,6 +541,7 @@ class Trunk:
         call("rg_shard_dedup_grads", w.dX[0].data_ptr(), self.E, w.dd_nmax, self.N1, gsend.data_ptr(),
              w.dd_work.data_ptr(), w.dd_work.numel(), st)
         grecv = self._xbuf(w, "grecv", max(w.R, 1), self.E, torch.float32)
+        w.nrecv.fill_(w.R)   # (the scatter's device row count; off the forward's gather)
         comm.all_to_all(grecv[:w.R], gsend[:w.U], w.recv_splits, w.send_splits)
         pad = self.pad - self.lo
         skip = -1 if self.train_pad or not (0 <= pad < self.n_local) else pad
