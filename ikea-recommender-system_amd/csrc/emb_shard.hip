@@ -30,11 +30,6 @@
 
 namespace {
 
-// owner of row id: the largest r with ⌊r·N1/W⌋ <= id, i.e. ⌈(id+1)·W/N1⌉ − 1
-__device__ __forceinline__ int owner_of(int64_t id, int64_t N1, int W) {
-  return (int)(((id + 1) * W + N1 - 1) / N1) - 1;
-}
-
 // one workgroup per sorted row r: tok_id[offs[r] + t] = s[perm[r]][t] (ids
 // outside [0, n_rows) -> -1 and the err flag, as nn.Embedding raises)
 __global__ __launch_bounds__(256) void k_token_ids(const int64_t* __restrict__ s, int L,
@@ -52,12 +47,12 @@ __global__ __launch_bounds__(256) void k_token_ids(const int64_t* __restrict__ s
   }
 }
 
-// Stable partition of the T tokens by owner (one workgroup, 256 threads,
+// Stable partition of the T tokens by owner (one workgroup, 1024 threads,
 // each a contiguous token range; the per-owner offsets by a shuffle scan):
 // counts[o], slot[t], send_ids[slot[t]].
 // Invalid ids (-1) go to rank 0, whose gather returns a zero row for them.
 // Deterministic: the send order is the packed token order within each owner.
-constexpr int RT_THREADS = 256;
+constexpr int RT_THREADS = 1024;
 constexpr int RT_MAXW = 8;    // ranks of one node
 
 __global__ __launch_bounds__(RT_THREADS) void k_shard_route(const int32_t* __restrict__ tok_id,
@@ -70,12 +65,23 @@ __global__ __launch_bounds__(RT_THREADS) void k_shard_route(const int32_t* __res
   const int T = *ntok_ptr;
   const int per = (T + RT_THREADS - 1) / RT_THREADS;
   const int t0 = min(T, tid * per), t1 = min(T, t0 + per);
+  // owner boundaries ⌊r·N1/W⌋ (the owner of id is the number of boundaries
+  // r >= 1 at or below it): compares per token instead of a 64-bit division
+  int bnd[RT_MAXW];
+#pragma unroll
+  for (int r = 1; r < RT_MAXW; ++r) bnd[r] = r < W ? (int)(((int64_t)r * N1) / W) : INT32_MAX;
+  auto owner = [&](int id) {
+    int o = 0;
+#pragma unroll
+    for (int r = 1; r < RT_MAXW; ++r) o += id >= bnd[r];
+    return id < 0 ? 0 : o;
+  };
   int cnt[RT_MAXW];
 #pragma unroll
   for (int o = 0; o < RT_MAXW; ++o) cnt[o] = 0;
   for (int t = t0; t < t1; ++t) {
     const int id = tok_id[t];
-    const int o = id < 0 ? 0 : owner_of(id, N1, W);
+    const int o = owner(id);
 #pragma unroll
     for (int q = 0; q < RT_MAXW; ++q) cnt[q] += q == o;
   }
@@ -110,7 +116,7 @@ __global__ __launch_bounds__(RT_THREADS) void k_shard_route(const int32_t* __res
   }
   for (int t = t0; t < t1; ++t) {
     const int id = tok_id[t];
-    const int o = id < 0 ? 0 : owner_of(id, N1, W);
+    const int o = owner(id);
     int p = 0;
 #pragma unroll
     for (int q = 0; q < RT_MAXW; ++q)

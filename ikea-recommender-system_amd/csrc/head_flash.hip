@@ -503,8 +503,13 @@ __global__ __launch_bounds__(64 * fl_nw(HF, 1)) void k_flash_amax(
   constexpr int NW = fl_nw(HF, 1);
   constexpr int NS = HF / 32;
   constexpr int EK = NS * 2 * 192;
+  // chunks per LDS slot: NT = 1 multiplies plane 0 only, so a slot's plane-1
+  // and plane-2 positions hold the next two chunks' plane 0 — three chunks
+  // between barriers (the 1-product loop is otherwise barrier- and
+  // DMA-latency-bound: 16 MFMAs per wave and chunk)
+  constexpr int PG = NT == 1 ? 3 : 1;
   __shared__ bf16x8 sk0[EK], sk1[EK];
-  __shared__ __attribute__((aligned(16))) float sb0[32], sb1[32];
+  __shared__ __attribute__((aligned(16))) float sb0[32 * PG], sb1[32 * PG];
   const int tid = threadIdx.x, lane = tid & 63, kg = lane >> 4, l16 = lane & 15, lane16 = 16 * lane;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   int bid = blockIdx.x;
@@ -516,12 +521,18 @@ __global__ __launch_bounds__(64 * fl_nw(HF, 1)) void k_flash_amax(
   const int nct = (A + 31) / 32;
   const int c0 = split * cps;
   const int nch = max(0, min(nct, c0 + cps) - c0);
-#define FA_ISSUE(C, SK, SB)                                                    \
-  do {                                                                         \
-    stage<EK, NW, NT == 1 ? 1 : NT == 3 ? 2 : 3>(Wk + (int64_t)(C) * EK, SK, w, lane16); \
-    if (w == 0 && lane < 8) blds16(rsrc_of(bias_pad + 32 * (C)), SB, lane16, 0); \
+  // chunks CR .. CR + PG − 1 (relative) into one slot
+#define FA_ISSUE(CR, SK, SB)                                                                       \
+  do {                                                                                             \
+    _Pragma("unroll") for (int q_ = 0; q_ < PG; ++q_) {                                            \
+      if ((CR) + q_ < nch) {                                                                       \
+        stage<EK, NW, NT == 1 ? 1 : NT == 3 ? 2 : 3>(Wk + (int64_t)(c0 + (CR) + q_) * EK, (SK) + 64 * q_, w, \
+                                                     lane16);                                      \
+        if (w == 0 && lane < 8) blds16(rsrc_of(bias_pad + 32 * (c0 + (CR) + q_)), (SB) + 32 * q_, lane16, 0); \
+      }                                                                                            \
+    }                                                                                              \
   } while (0)
-  if (nch > 0) FA_ISSUE(c0, sk0, sb0);
+  if (nch > 0) FA_ISSUE(0, sk0, sb0);
   bf16x8 hk[NS][2][3];
 #pragma unroll
   for (int s = 0; s < NS; ++s)
@@ -578,15 +589,20 @@ __global__ __launch_bounds__(64 * fl_nw(HF, 1)) void k_flash_amax(
       }
     }
   };
-  for (int c = 0; c < nch; c += 2) {
-    if (c + 1 < nch) FA_ISSUE(c0 + c + 1, sk1, sb1);
+  auto group = [&](const bf16x8* sk, const float* sb, int c) __attribute__((always_inline)) {
+#pragma unroll
+    for (int q = 0; q < PG; ++q)
+      if (c + q < nch) chunk(sk + 64 * q, sb + 32 * q, c + q);
+  };
+  for (int c = 0; c < nch; c += 2 * PG) {
+    if (c + PG < nch) FA_ISSUE(c + PG, sk1, sb1);
     __builtin_amdgcn_sched_barrier(0);
-    if (active) chunk(sk0, sb0, c);
+    if (active) group(sk0, sb0, c);
     __syncthreads();
-    if (c + 1 < nch) {
-      if (c + 2 < nch) FA_ISSUE(c0 + c + 2, sk0, sb0);
+    if (c + PG < nch) {
+      if (c + 2 * PG < nch) FA_ISSUE(c + 2 * PG, sk0, sb0);
       __builtin_amdgcn_sched_barrier(0);
-      if (active) chunk(sk1, sb1, c + 1);
+      if (active) group(sk1, sb1, c + PG);
       __syncthreads();
     }
   }
