@@ -60,7 +60,7 @@ extern "C" int rg_weighted_sum(const float* const* X, const float* w, int nh, in
 // deterministic; one atomic per wave serialised ~A/4 atomics on one address).
 // Replaces rg_weighted_sum (W, b) + rg_head_planes + rg_row_norm_max: the Q
 // heads are read once and W_comb is not re-read.
-template <int HF>
+template <int HF, int NP>
 __global__ __launch_bounds__(256) void k_qcomb(Ptr4 in, Ptr4 inb, int nh, int A, int Ap, float* __restrict__ Wc,
                                                float* __restrict__ bc, bf16x8* __restrict__ P,
                                                float* __restrict__ bias_pad, float* __restrict__ wnorm) {
@@ -99,8 +99,10 @@ __global__ __launch_bounds__(256) void k_qcomb(Ptr4 in, Ptr4 inb, int nh, int A,
     split3x8(lo, hi, p0, p1, p2);
     const int64_t base = kplane16(x, g, HF);
     P[base] = p0;
-    P[base + 64] = p1;
-    P[base + 128] = p2;
+    if (NP == 3) {   // (NP = 1: the one-product screening reads plane 0 only)
+      P[base + 64] = p1;
+      P[base + 128] = p2;
+    }
 #pragma unroll
     for (int o = G / 2; o >= 1; o >>= 1) ss += __shfl_xor(ss, o);
     best = fmaxf(best, sqrtf(ss));
@@ -115,8 +117,10 @@ __global__ __launch_bounds__(256) void k_qcomb(Ptr4 in, Ptr4 inb, int nh, int A,
 }
 
 extern "C" int rg_qcomb(const float* const* W, const float* const* b, const float* w, int nh, int A, int HF,
-                        float* Wc, float* bc, void* planes_k, float* bias_pad, float* wnorm, hipStream_t stream) {
-  if (nh <= 0 || nh > 4 || A <= 0 || !W || !b || !w || !Wc || !bc || !planes_k || !bias_pad || !wnorm)
+                        int nplanes, float* Wc, float* bc, void* planes_k, float* bias_pad, float* wnorm,
+                        hipStream_t stream) {
+  if (nh <= 0 || nh > 4 || A <= 0 || (nplanes != 1 && nplanes != 3) || !W || !b || !w || !Wc || !bc || !planes_k ||
+      !bias_pad || !wnorm)
     return RG_ERR_ARG;
   if (HF != 32 && HF != 64 && HF != 128 && HF != 256) return RG_ERR_SHAPE;
   Ptr4 in{}, inb{};
@@ -129,9 +133,15 @@ extern "C" int rg_qcomb(const float* const* W, const float* const* b, const floa
   const int Ap = (A + 31) / 32 * 32;
   int64_t need = ((int64_t)Ap * (HF / 8) + 255) / 256;
   const unsigned grid = (unsigned)(need < 4096 ? need : 4096);
-#define QC(HFV)                                                                                            \
-  hipLaunchKernelGGL(k_qcomb<HFV>, dim3(grid), dim3(256), 0, stream, in, inb, nh, A, Ap, Wc, bc,         \
+#define QC1(HFV, NPV)                                                                                     \
+  hipLaunchKernelGGL((k_qcomb<HFV, NPV>), dim3(grid), dim3(256), 0, stream, in, inb, nh, A, Ap, Wc, bc,  \
                      reinterpret_cast<bf16x8*>(planes_k), bias_pad, wnorm)
+#define QC(HFV)        \
+  if (nplanes == 1) {  \
+    QC1(HFV, 1);       \
+  } else {             \
+    QC1(HFV, 3);       \
+  }
   switch (HF) {
     case 32: QC(32); break;
     case 64: QC(64); break;
@@ -139,6 +149,7 @@ extern "C" int rg_qcomb(const float* const* W, const float* const* b, const floa
     case 256: QC(256); break;
   }
 #undef QC
+#undef QC1
   RG_LAUNCH_CHECK();
   return RG_OK;
 }

@@ -130,7 +130,7 @@ SIGNATURES = {
     "rg_rows_gather": [P, I, I64, I64, P, I, I, P, P, P],
     "rg_place_rows": [P, I, P, P, P, I, I, I, P, P],
     "rg_combine_dirs": [P, P, P, P, I, I, P],
-    "rg_qcomb": [P, P, P, I, I, I, P, P, P, P, P, P],
+    "rg_qcomb": [P, P, P, I, I, I, I, P, P, P, P, P, P],
     "rg_shard_dedup_work_bytes": [I, I, I64],
     "rg_shard_dedup": [P, P, I, I64, I, I, P, P, P, P, P, I64, P],
     "rg_shard_dedup_grads": [P, I, I, I64, P, P, I64, P],

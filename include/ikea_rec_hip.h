@@ -350,9 +350,10 @@ int rg_weighted_sum(const float* const* X, const float* w, int nh, int64_t n, fl
 /* The SMORL target's combined Q head in one pass (csrc/misc.hip): Wc = sum_i w_i W_i (A × HF),
  * bc = sum_i w_i b_i (as rg_weighted_sum), Wc's K-planes and the -inf padded bias (as
  * rg_head_planes, ceil(A/32)·32 rows) and *wnorm = max_a ||Wc[a]||_2 (for rg_flash_argmax_exact).
- * W, b, w: HOST arrays of nh <= 4 device pointers / weights; HF in {32, 64, 128, 256}. */
-int rg_qcomb(const float* const* W, const float* const* b, const float* w, int nh, int A, int HF, float* Wc,
-             float* bc, void* planes_k, float* bias_pad, float* wnorm, rg_stream_t stream);
+ * W, b, w: HOST arrays of nh <= 4 device pointers / weights; HF in {32, 64, 128, 256}.  nplanes 3
+ * writes all three K-planes, 1 only plane 0 (what rg_flash_amax_screen with terms = 1 reads). */
+int rg_qcomb(const float* const* W, const float* const* b, const float* w, int nh, int A, int HF, int nplanes,
+             float* Wc, float* bc, void* planes_k, float* bias_pad, float* wnorm, rg_stream_t stream);
 /* replay-buffer transitions from a device session store (csrc/replay.hip; SURVEY §8f rank 2,
  * rules of preprocessing.py:5-29, 143-170, 426-464): sessions as CSR — items (int32) and rewards
  * (f64) per event, ev_sess (int32) the event's session, sess_off (int64, n_sess + 1) — and B event

@@ -578,12 +578,14 @@ def test_shard_dedup_distinct_ids_and_sums(n_rows, W, n, n_max, E, zipf):
     assert torch.equal(g1[:U], g2[:U])   # fixed order: bitwise repeatable, stored not added
 
 
+@pytest.mark.parametrize("nplanes", [3, 1])
 @pytest.mark.parametrize("A,HF,nh", [(20011, 128, 3), (777, 256, 2), (1000, 64, 3), (4096, 32, 1)])
-def test_qcomb_equals_weighted_sum_planes_norm(A, HF, nh):
+def test_qcomb_equals_weighted_sum_planes_norm(A, HF, nh, nplanes):
     """rg_qcomb (the SMORL target's combined Q head in one pass) against the
     separate kernels it replaces: W_c / b_c bitwise rg_weighted_sum's, the
-    K-planes and padded bias bitwise rg_head_planes', the max row norm within
-    fp32 rounding of rg_row_norm_max's (another summation order) and of fp64."""
+    K-planes (all three, or plane 0 only for the one-product screening) and
+    padded bias bitwise rg_head_planes', the max row norm within fp32
+    rounding of rg_row_norm_max's (another summation order) and of fp64."""
     call = C().call
     g = torch.Generator().manual_seed(A + HF)
     Ws = [D(torch.randn(A, HF, generator=g) * 0.1) for _ in range(nh)]
@@ -595,8 +597,8 @@ def test_qcomb_equals_weighted_sum_planes_norm(A, HF, nh):
     Ap = (A + 31) // 32 * 32
     bp = torch.empty(Ap, device=dev)
     wn = torch.full((1,), 7.0, device=dev)
-    call("rg_qcomb", C().host_ptr_array(Ws), C().host_ptr_array(bs), hw, nh, A, HF, Wc.data_ptr(), bc.data_ptr(),
-         pk.data_ptr(), bp.data_ptr(), wn.data_ptr(), st())
+    call("rg_qcomb", C().host_ptr_array(Ws), C().host_ptr_array(bs), hw, nh, A, HF, nplanes, Wc.data_ptr(),
+         bc.data_ptr(), pk.data_ptr(), bp.data_ptr(), wn.data_ptr(), st())
     Wr, br = torch.empty_like(Wc), torch.empty_like(bc)
     call("rg_weighted_sum", C().host_ptr_array(Ws), hw, nh, A * HF, Wr.data_ptr(), st())
     call("rg_weighted_sum", C().host_ptr_array(bs), hw, nh, A, br.data_ptr(), st())
@@ -607,7 +609,8 @@ def test_qcomb_equals_weighted_sum_planes_norm(A, HF, nh):
     call("rg_row_norm_max", Wr.data_ptr(), A, HF, wn2.data_ptr(), st())
     torch.cuda.synchronize()
     assert torch.equal(Wc, Wr) and torch.equal(bc, br)
-    assert torch.equal(pk, pk2) and torch.equal(bp, bp2)
+    planes = lambda t: t.view(-1, 3, 64, 16)[:, :nplanes]   # noqa: E731  (plane p: entries 64p .. 64p + 63 of each triple)
+    assert torch.equal(planes(pk), planes(pk2)) and torch.equal(bp, bp2)
     ref = float(Wr.double().norm(dim=1).max())
     assert abs(float(wn) - float(wn2)) <= 2e-6 * ref and abs(float(wn) - ref) <= 2e-6 * ref
 
