@@ -17,7 +17,7 @@ from __future__ import annotations
 import numpy as np
 import torch
 
-from . import call, host_floats, host_ptr_array, stream_ptr
+from . import call, engine, host_floats, host_ptr_array, stream_ptr
 from .engine import SegScatter, SoftmaxHead, _f32
 from .nets import HipNet
 from .remap import raise_if_unmapped, remap_ids
@@ -117,8 +117,8 @@ class QNet(HipNet):
             w = hd.amax_ws("argmax", B)
             call("rg_qcomb", host_ptr_array([q.W.p for q in self.q_heads]),
                  host_ptr_array([q.b.p for q in self.q_heads]), wts, len(self.q_heads), hd.A, hd.HF,
-                 hd.W.p.data_ptr(), hd.b.p.data_ptr(), w.Wk.data_ptr(), w.bias_pad.data_ptr(), w.wnorm.data_ptr(),
-                 st)
+                 1 if engine.SCREEN_TERMS == 1 else 3, hd.W.p.data_ptr(), hd.b.p.data_ptr(), w.Wk.data_ptr(),
+                 w.bias_pad.data_ptr(), w.wnorm.data_ptr(), st)
             return hd.argmax(h, slot="argmax", planes_ready=True)
         call("rg_weighted_sum", host_ptr_array([q.W.p for q in self.q_heads]), wts, len(self.q_heads),
              hd.W.p.numel(), hd.W.p.data_ptr(), st)
@@ -141,6 +141,19 @@ def q_side_stream(net):
     if getattr(net, "_qstream", None) is None:
         net._qstream = torch.cuda.Stream(device=net.device)
     return net._qstream
+
+
+# the double-Q target (the next-state trunk forwards, the combined Q head,
+# the screening argmax, Q_boot(s', a*)) on its own stream beside the main
+# state's forward and the supervised head's pass 1, joined before the TD loss
+TARGET_SIDE_STREAM = True
+
+
+def target_stream(net):
+    """The stream a network's double-Q target runs on when it is main (created once)."""
+    if getattr(net, "_tstream", None) is None:
+        net._tstream = torch.cuda.Stream(device=net.device)
+    return net._tstream
 
 
 def q_heads_backward(main, h, idx, B, dq, dh, tag, st):
@@ -186,8 +199,7 @@ def double_q_step(nets, clocks, k, s, a, r, s_next, true_len, true_next_len, is_
     B = s.shape[0]
     nh = len(main.q_heads)
     st = stream_ptr()
-    with region("sqn_trunk_main"):
-        h = main.trunk.forward(s, true_len, slot="main", save=True)
+    cur = torch.cuda.current_stream(dev)
 
     def target():
         with region("sqn_target"):
@@ -196,13 +208,26 @@ def double_q_step(nets, clocks, k, s, a, r, s_next, true_len, true_next_len, is_
             h_b = boot.trunk.forward(s_next, true_len, slot="boot", save=False)   # quirk: true_len
             return boot.gather_q(h_b, idx32=a_star, out=main.buf("qn", (B, nh)))
 
-    # the double-Q target needs neither the supervised head nor its workspace,
-    # so it is issued before forward_loss, whose access of the head waits for
-    # the previous step's overlapped pass 2: target and pass 2 share the GPU
-    qn = target()
+    # the double-Q target needs neither the supervised head nor its workspace
+    # (nor the main state's trunk pass: its own trunk slots, the combined Q
+    # head's workspace), so it runs on its own stream, ordered after
+    # everything queued so far — the previous steps' updates — and beside the
+    # main state's forward and pass 1, instead of ahead of pass 1 on the
+    # serial chain; joined before the TD loss reads qn
+    ts = target_stream(main) if TARGET_SIDE_STREAM else None
+    if ts is not None:
+        ts.wait_stream(cur)
+        with torch.cuda.stream(ts):
+            qn = target()
+    with region("sqn_trunk_main"):
+        h = main.trunk.forward(s, true_len, slot="main", save=True)
+    if ts is None:
+        qn = target()
     sup_loss, _ = main.sup_head_output.forward_loss(h, a, slot="main")
     q = main.gather_q(h, idx64=a, out=main.buf("q", (B, nh)))
     dq = main.buf("dq", (B, nh))
+    if ts is not None:
+        cur.wait_stream(ts)
     if smorl is None:
         r64 = _dev(r, dev, torch.float64)
         sq = main.buf("sq", (B,), torch.float64)
@@ -235,7 +260,6 @@ def double_q_step(nets, clocks, k, s, a, r, s_next, true_len, true_next_len, is_
     # the Q heads' dense Adam sweeps on their own stream beside the trunk
     # backward (they read only the Q heads' G rows, written above); joined
     # before the step ends
-    cur = torch.cuda.current_stream(main.device)
     qs = q_side_stream(main)
     qs.wait_stream(cur)
     with torch.cuda.stream(qs):
