@@ -148,8 +148,11 @@ __global__ void k_pad_bias(const float* __restrict__ bias, int A, int Ap, float*
 // array it waited for the just-issued prefetch every chunk).  HF 256: the
 // R-planes (48 KB per chunk) are single-buffered: chunk c+1's R DMA is issued
 // after chunk c's O-MFMAs and lands under chunk c+1's S-MFMAs and softmax.
-// ARG: also the row's top-1 (value, item) per split and, with cmax, every
-// chunk's row maximum — the inputs of the fused top-k (SMORL's rewards).
+// AM (top-k outputs): 1 every chunk's row maximum (cmax) — what the fused
+// top-k of SMORL's rewards reads (rg_flash_topk re-scores the candidate
+// chunks); 2 also the row's top-1 (value, item) per split (rg_flash_argmax),
+// whose per-logit compare-and-select is a third of the softmax section's
+// VALU — only evaluation's rg_flash_score and the ABI's pbest / parg take it.
 // NG = 0 (rg_flash_score, evaluation): the S-part alone — lse partials,
 // per-split top-1 and chunk maxima, no O contraction, no R-planes read.
 // Diagnostic build only (-DFL_STAMP, tools/flstamp.py): per-wave core cycles
@@ -169,7 +172,7 @@ extern "C" int rg_fl_stamp_read(void* dst, int64_t n) {
 #define FL_SYNC() __syncthreads()
 #endif
 
-template <int HF, int NT, int NG, bool ARG, bool ZS = false>
+template <int HF, int NT, int NG, int AM, bool ZS = false>
 __global__ __launch_bounds__(64 * fl_nw(HF, 1)) void k_flash_fwd(
     const bf16x8* __restrict__ Hk, const bf16x8* __restrict__ Wk, const bf16x8* __restrict__ Wr,
     const float* __restrict__ bias_pad, int B, int A, int nrb, int nsplit, int cps, float* __restrict__ pm,
@@ -309,7 +312,7 @@ __global__ __launch_bounds__(64 * fl_nw(HF, 1)) void k_flash_fwd(
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
           const float z = sa[ib][rb][u] + bq[u];
-          if (ARG && z > bv[rb]) {  // items increase with (ib, u): strict > keeps the first maximum
+          if (AM == 2 && z > bv[rb]) {  // items increase with (ib, u): strict > keeps the first maximum
             bv[rb] = z;
             bi[rb] = 32 * (c0 + c) + 16 * ib + 4 * kg + u;
           }
@@ -319,7 +322,7 @@ __global__ __launch_bounds__(64 * fl_nw(HF, 1)) void k_flash_fwd(
       }
       cm = fmaxf(cm, __shfl_xor(cm, 16));
       cm = fmaxf(cm, __shfl_xor(cm, 32));
-      if (ARG && cmax != nullptr && kg == 0) cmax[(int64_t)(c0 + c) * B + r0 + 16 * rb + l16] = cm;
+      if (AM >= 1 && cmax != nullptr && kg == 0) cmax[(int64_t)(c0 + c) * B + r0 + 16 * rb + l16] = cm;
       cm *= L2E;
       const float mn = fmaxf(m[rb], cm);
       if (__any(mn > m[rb])) {
@@ -457,7 +460,7 @@ __global__ __launch_bounds__(64 * fl_nw(HF, 1)) void k_flash_fwd(
     const int row = r0 + 16 * rb + l16;
     float bvj = bv[rb];
     int bij = bi[rb];
-    if (ARG) {  // merge the four lane groups: larger value, ties to the smaller item
+    if (AM == 2) {  // merge the four lane groups: larger value, ties to the smaller item
 #pragma unroll
       for (int d = 16; d <= 32; d *= 2) {
         const float v2 = __shfl_xor(bvj, d);
@@ -471,7 +474,7 @@ __global__ __launch_bounds__(64 * fl_nw(HF, 1)) void k_flash_fwd(
     if (kg == 0) {
       pm[(int64_t)split * B + row] = m[rb];
       pl[(int64_t)split * B + row] = lt;
-      if (ARG) {
+      if (AM == 2) {
         pbest[(int64_t)split * B + row] = bvj;
         parg[(int64_t)split * B + row] = bij;
       }
@@ -1642,7 +1645,7 @@ extern "C" int rg_flash_fwd_top(const void* Hk, const void* Wk, const void* Wr, 
   if (!flash_terms_ok(terms)) return RG_ERR_ARG;
   if (!flash_hf_ok(HF)) return RG_ERR_SHAPE;
   const bool arg = pbest != nullptr;
-  if (arg != (parg != nullptr) || (cmax && !arg)) return RG_ERR_ARG;
+  if (arg != (parg != nullptr)) return RG_ERR_ARG;
   const int rpb = fl_rows(HF, 1);
   if (zs && B % rpb) return RG_ERR_SHAPE;   // stored logits: whole row blocks
   const int nct = (A + 31) / 32;
@@ -1661,9 +1664,11 @@ extern "C" int rg_flash_fwd_top(const void* Hk, const void* Wk, const void* Wr, 
   }
 #define FA(HFV, NTV, NGV)      \
   if (arg) {                   \
-    FZ1(HFV, NTV, NGV, true);  \
+    FZ1(HFV, NTV, NGV, 2);     \
+  } else if (cmax) {           \
+    FZ1(HFV, NTV, NGV, 1);     \
   } else {                     \
-    FZ1(HFV, NTV, NGV, false); \
+    FZ1(HFV, NTV, NGV, 0);     \
   }
 #define FT(HFV)                        \
   if (terms == 9) {                    \
@@ -1712,7 +1717,7 @@ extern "C" int rg_flash_score(const void* Hk, const void* Wk, const float* bias_
   const int nrb = (B + rpb - 1) / rpb;
   const dim3 grid((unsigned)(nrb * nsplit));
 #define FSC(HFV, NTV)                                                                                             \
-  hipLaunchKernelGGL((k_flash_fwd<HFV, NTV, 0, true>), grid, dim3(64 * fl_nw(HFV, 1)), 0, stream, (const bf16x8*)Hk, \
+  hipLaunchKernelGGL((k_flash_fwd<HFV, NTV, 0, 2>), grid, dim3(64 * fl_nw(HFV, 1)), 0, stream, (const bf16x8*)Hk, \
                      (const bf16x8*)Wk, (const bf16x8*)nullptr, bias_pad, B, A, nrb, nsplit, cps, pm, pl,         \
                      (float*)nullptr, pbest, parg, cmax, (float*)nullptr)
 #define FT(HFV)          \

@@ -606,9 +606,8 @@ class _FlashWS:
         self.loss = torch.zeros(1, device=device)
         self.zs = None
         self.zs_live = False   # zs holds the logits of the last pass 1 on this workspace
-        self.pbest = self.parg = self.cmax = self.cand = self.ncand = None
+        self.cmax = self.cand = self.ncand = None
         if top_k >= 1:
-            self.pbest, self.parg = z(self.nsplit, B), z(self.nsplit, B, dt=torch.int32)
             self.top_idx, self.top_val = z(B, top_k, dt=torch.int32), z(B, top_k)
         # chunk maxima for the exact top-K, from one buffer per device shared
         # by every head (a pass 1 with top-k outputs is consumed by its
@@ -937,8 +936,10 @@ class SoftmaxHead:
                 call("rg_head_planes", W, A, HF, w.Wk.data_ptr(), w.Wr.data_ptr(), b, w.bias_pad.data_ptr(), st)
                 w.wgen = self._wgen
             zs = self.zs_buffer(w)
+            # top-k outputs: the chunk maxima only (top_entries re-scores the candidate chunks; without
+            # them K = 1 re-screens) — no per-split first maximum
             call("rg_flash_fwd_top", w.Hk.data_ptr(), w.Wk.data_ptr(), w.Wr.data_ptr(), w.bias_pad.data_ptr(), B, A,
-                 HF, terms, w.nsplit, w.pm.data_ptr(), w.pl.data_ptr(), w.pO.data_ptr(), ptr(w.pbest), ptr(w.parg),
+                 HF, terms, w.nsplit, w.pm.data_ptr(), w.pl.data_ptr(), w.pO.data_ptr(), None, None,
                  ptr(w.cmax), ptr(zs), st)
             w.zs_live = zs is not None
         call("rg_flash_lse", w.pm.data_ptr(), w.pl.data_ptr(), w.nsplit, h.data_ptr(), W, b, tgt.data_ptr(), self.lo,

@@ -152,9 +152,10 @@ int rg_flash_fwd(const void* Hk, const void* Wk, const void* Wr, const float* bi
  * rewards, smorl_gru.py:298-308 -> diversity.py:15-73 / novelty.py:12-47:
  * torch.topk(sup, k) of the supervised logits), no logits stored.
  * rg_flash_rows_per_block: rows of one pass-1 workgroup (row-block size).
- * rg_flash_fwd_top: rg_flash_fwd plus (optional) per-split first maximum
- *   pbest/parg (nsplit × B, item local to the head) and, with cmax, every
- *   32-item chunk's row maximum (ceil(A/32) × B).
+ * rg_flash_fwd_top: rg_flash_fwd plus (optional, independent) per-split first maximum
+ *   pbest/parg (nsplit × B, item local to the head) and every 32-item chunk's row
+ *   maximum cmax (ceil(A/32) × B).  cmax alone is what rg_flash_topk needs, and skips the
+ *   per-logit compare-and-select of the first maximum.
  * rg_flash_argmax: top-1 over the splits (first maximum), out = -1 for a row
  *   with no finite logit; out_max optional.
  * rg_flash_topk: canonical top-K (value desc, index asc; K <= 32) from cmax:
@@ -169,7 +170,7 @@ int rg_flash_fwd(const void* Hk, const void* Wk, const void* Wr, const float* bi
  *   (every item re-scored the same way, canonical top-K): the result is exact for
  *   every row; err (optional) counts the rows scanned. */
 int rg_flash_rows_per_block(int HF);
-/* zs (optional; HF <= 128 and B a multiple of rg_flash_rows_per_block(HF), else RG_ERR_SHAPE): pass 1
+/* zs (optional; B a multiple of rg_flash_rows_per_block(HF), else RG_ERR_SHAPE): pass 1
  *   also stores the logits z = h·Wᵀ + b as rg_flash_zs_bytes(B, A) bytes of 32-item × 32-row tiles for
  *   rg_flash_dw_adam_planes (which then skips recomputing them). */
 int rg_flash_fwd_top(const void* Hk, const void* Wk, const void* Wr, const float* bias_pad, int B, int A, int HF,

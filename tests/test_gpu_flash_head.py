@@ -996,3 +996,33 @@ def test_top1_above_2gb_of_chunk_maxima_is_first_fp32_maximum(monkeypatch):
             assert torch.equal(got[:600], first[:600])
         torch.testing.assert_close(val[r0:r0 + 512].double(), Z.gather(1, got[:, None])[:, 0],
                                    rtol=0, atol=float(200 * 2.0 ** -24 * sl.max()))
+
+
+@pytest.mark.parametrize("B,A,HF,zs", [(128, 3001, 64, False), (256, 20011, 128, True), (128, 5003, 256, True)])
+def test_chunk_maxima_without_first_maximum_match(B, A, HF, zs):
+    """rg_flash_fwd_top with cmax alone (the trainers' fused top-k: no per-logit
+    compare-and-select of the first maximum) writes the same chunk maxima,
+    softmax partials, O partials and stored logits, bit for bit, as with
+    pbest / parg too."""
+    call, st = C().call, C().stream_ptr()
+    h, W, b, _ = inputs(B, A, HF, 11 * B + A)
+    h, W, b = h.to(dev), W.to(dev), b.to(dev)
+    nsplit = 8
+    hb, wb = call("rg_head_plane_bytes", B, HF), call("rg_head_plane_bytes", A, HF)
+    Hk, Hr, Wk, Wr = _u8(hb), _u8(hb), _u8(wb), _u8(wb)
+    bp = torch.empty((A + 31) // 32 * 32, device=dev)
+    call("rg_head_planes", h.data_ptr(), B, HF, Hk.data_ptr(), Hr.data_ptr(), None, None, st)
+    call("rg_head_planes", W.data_ptr(), A, HF, Wk.data_ptr(), Wr.data_ptr(), b.data_ptr(), bp.data_ptr(), st)
+    outs = []
+    for full in (True, False):
+        z = lambda *s, dt=torch.float32: torch.full(s, -7, dtype=dt, device=dev)  # noqa: E731
+        pm, pl, pO, cmax = z(nsplit, B), z(nsplit, B), z(nsplit, HF, B), z((A + 31) // 32, B)
+        pbest, parg = (z(nsplit, B), z(nsplit, B, dt=torch.int32)) if full else (None, None)
+        zbuf = torch.zeros(call("rg_flash_zs_bytes", B, A) // 4, device=dev) if zs else None
+        call("rg_flash_fwd_top", Hk.data_ptr(), Wk.data_ptr(), Wr.data_ptr(), bp.data_ptr(), B, A, HF, 636, nsplit,
+             pm.data_ptr(), pl.data_ptr(), pO.data_ptr(), None if pbest is None else pbest.data_ptr(),
+             None if parg is None else parg.data_ptr(), cmax.data_ptr(), None if zbuf is None else zbuf.data_ptr(), st)
+        outs.append([pm, pl, pO, cmax] + ([zbuf] if zs else []))
+    torch.cuda.synchronize()
+    for a_, b_ in zip(*outs):
+        assert torch.equal(a_, b_)

@@ -176,7 +176,7 @@ def asm(tmp_path_factory):
 
 def test_stored_logit_waits_cover_only_the_z_traffic(asm):
     fns = _functions(asm)
-    zs = {k: v for k, v in fns.items() if re.search(r"k_flash_fwdI(Li\d+E){3}Lb[01]ELb1EE", k)}
+    zs = {k: v for k, v in fns.items() if re.search(r"k_flash_fwdI(Li\d+E){4}Lb1EE", k)}
     zl = {k: v for k, v in fns.items() if re.search(r"k_flash_dwI(Li\d+E){2}Lb1EE", k)}
     assert zs and zl, sorted(fns)[:8]
     checked = 0
