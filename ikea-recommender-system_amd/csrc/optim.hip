@@ -136,8 +136,10 @@ extern "C" int rg_adam_rows(float* P, float* M, float* V, float* G, const int32_
                      reinterpret_cast<uintptr_t>(G)) & 15) == 0;
   const bool wide = cols % 4 == 0 && a16;
   const int64_t n = wide ? rows * (cols / 4) : rows * cols;
+  // about one float4 per thread up to 64M float4s (a 1M × 256 table): a 32768-block grid-stride
+  // sweep ran 1.14 ms there, this one 1.07 ms (profiles/r06/adam_sweep_grid.txt)
   int blocks = (int)((n + 255) / 256);
-  if (blocks > 32768) blocks = 32768;
+  if (blocks > 262144) blocks = 262144;
   if (wide) {
     const int c4n = cols / 4;
     const int sh = (c4n & (c4n - 1)) == 0 ? __builtin_ctz((unsigned)c4n) : -1;
