@@ -205,7 +205,7 @@ extern "C" int rg_adam_rows_h(float* P, float* M, float* V, float* G, const int3
   if (rows <= 0 || cols <= 0 || cols % 4 || !P16) return RG_ERR_ARG;
   const int64_t n = rows * (cols / 4);
   int blocks = (int)((n + 255) / 256);
-  if (blocks > 32768) blocks = 32768;
+  if (blocks > 262144) blocks = 262144;   // (as rg_adam_rows)
   hipLaunchKernelGGL(k_adam_rows4_h, dim3(blocks), dim3(256), 0, stream, P, M, V, G, tags, tag, rows, cols,
                      to_args(adam6), reinterpret_cast<__half*>(P16));
   RG_LAUNCH_CHECK();
