@@ -180,6 +180,13 @@ __device__ __forceinline__ int32_t draw_id(uint64_t seed, uint64_t counter, int 
 __device__ __forceinline__ int64_t plane_idx(int blk, int j, int p, int lane, int NS) {
   return (((int64_t)blk * NS + j) * 3 + p) * 64 + lane;
 }
+// The same blocks as fp32 fragments (rg_gather_neg wfmt 1, rg_sampled_logits
+// draw 3): entry (block, slice j, half q, lane) = one f4, lane (hh, n) = row n,
+// k = 16j + 8hh + 4q .. +4 — two thirds of the planes' bytes, split in the
+// logits kernel right before each slice's MFMAs.
+__device__ __forceinline__ int64_t frag_idx(int blk, int j, int q, int lane, int NS) {
+  return (((int64_t)blk * NS + j) * 2 + q) * 64 + lane;
+}
 // The negatives' row gather of a sampled step, done by extra workgroups of the
 // embedding-gather launch (rg_gather_neg): ids, biases, fp32 rows (the
 // backward's operands) and the rows' bf16 planes in fragment order (the
@@ -191,9 +198,9 @@ struct NegPrep {
   int32_t* ids;
   float* Wg;
   float* bg;
-  bf16x8* Wp;
+  bf16x8* Wp;   // wfmt 0: bf16 planes (plane_idx); 1: fp32 fragments (frag_idx)
   uint64_t seed, counter, A;
-  int S, HF, nwg;
+  int S, HF, nwg, wfmt;
 };
 
 // acc += Σ_terms a_p · b_q over one 16-wide k slice (NT = 9, 6 or 3 terms),

@@ -263,9 +263,19 @@ __device__ __forceinline__ void neg_prep(const NegPrep& np, int bid) {
   float* dst = np.Wg + (int64_t)x * np.HF + 8 * g;
   *reinterpret_cast<f4*>(dst) = lo;
   *reinterpret_cast<f4*>(dst + 4) = hi;
+  const int lane = (g & 1) * 32 + (x & 31);
+  if (np.wfmt) {
+    f4* wf = reinterpret_cast<f4*>(np.Wp);
+    wf[frag_idx(blk, g >> 1, 0, lane, NS)] = lo;
+    wf[frag_idx(blk, g >> 1, 1, lane, NS)] = hi;
+    if (g == 0) {
+      np.ids[x] = id;
+      np.bg[x] = np.bias[id];
+    }
+    return;
+  }
   bf16x8 p0, p1, p2;
   split3x8(lo, hi, p0, p1, p2);
-  const int lane = (g & 1) * 32 + (x & 31);
   np.Wp[plane_idx(blk, g >> 1, 0, lane, NS)] = p0;
   np.Wp[plane_idx(blk, g >> 1, 1, lane, NS)] = p1;
   np.Wp[plane_idx(blk, g >> 1, 2, lane, NS)] = p2;
@@ -391,20 +401,22 @@ extern "C" int rg_gather_h(const int64_t* s, int B, int L, const int32_t* perm, 
 // same launch (common.h NegPrep): draw `counter` of the counter-based stream
 // (seed, S, A) -> ids[S], bg[S] = bias[ids], Wg[S][HF] = W[ids] and the rows'
 // bf16 planes Wp (S·HF·6 bytes, fragment order) that rg_sampled_logits reads
-// with draw = 2.  emb16 != 0: the table is fp16 (rg_gather_h).  Needs the
+// with draw = 2 — or, wfmt 1 (HF <= 128), the rows as fp32 fragments
+// (S·HF·4 bytes, common.h frag_idx) for draw = 3.  emb16 != 0: the table is fp16 (rg_gather_h).  Needs the
 // compile-time gather (E ∈ {32, 64, 128, 256}, L <= 64), S % 32 == 0,
 // HF ∈ {32, 64, 128, 256}.
 extern "C" int rg_gather_neg(const int64_t* s, int B, int L, const int32_t* perm, const int32_t* lsort,
                              const int32_t* offs, const void* emb, int emb16, int64_t n_rows, int E, int reverse,
                              int32_t* tok_id, float* X, int32_t* err, const float* W, const float* bias,
                              uint64_t seed, uint64_t counter, int64_t A, int S, int HF, int32_t* ids, float* Wg,
-                             float* bg, void* Wp, hipStream_t stream) {
+                             float* bg, void* Wp, int wfmt, hipStream_t stream) {
   if (B <= 0 || (E & 3) || L > GW_MAXL || !W || !bias || !ids || !Wg || !bg || !Wp) return RG_ERR_ARG;
+  if (wfmt < 0 || wfmt > 1 || (wfmt == 1 && HF > 128)) return RG_ERR_ARG;
   if (S <= 0 || S % 32 || A <= 0 || A > INT32_MAX) return RG_ERR_ARG;
   if (E != 32 && E != 64 && E != 128 && E != 256) return RG_ERR_SHAPE;
   if (HF != 32 && HF != 64 && HF != 128 && HF != 256) return RG_ERR_SHAPE;
   NegPrep np{W, bias, ids, Wg, bg, reinterpret_cast<bf16x8*>(Wp), seed, counter, (uint64_t)A, S, HF,
-             (int)(((int64_t)S * (HF / 8) + 255) / 256)};
+             (int)(((int64_t)S * (HF / 8) + 255) / 256), wfmt};
   const bool ok = emb16 ? launch_gather_e(s, B, L, perm, lsort, offs, reinterpret_cast<const __half*>(emb), n_rows,
                                           E, reverse, tok_id, X, err, np, stream)
                         : launch_gather_e(s, B, L, perm, lsort, offs, reinterpret_cast<const float*>(emb), n_rows,

@@ -342,7 +342,9 @@ extern "C" int rg_sf_stamp_read(void* dst, int64_t n) {
 // forward that produced h, rg_gru_fwd_dirs_planes) and each 32-row chunk
 // moves global -> LDS by 16-B LDS-DMA: no fp32 h loads, no split, no LDS
 // stores in this kernel.
-template <int HF, int NT, bool DRAW, bool HKP, bool PRE>
+// PF (with PRE, HF <= 128): the pre-gathered rows are fp32 fragments
+// (common.h frag_idx), split here right before each slice's MFMAs.
+template <int HF, int NT, bool DRAW, bool HKP, bool PRE, bool PF = false>
 __global__ __launch_bounds__(sf_thr(HF)) void k_sampled_logits(const float* __restrict__ h, const float* __restrict__ W,
                                                         const float* __restrict__ bias, int32_t* __restrict__ neg,
                                                         uint64_t seed, uint64_t counter, uint64_t A, int B, int S,
@@ -459,7 +461,15 @@ __global__ __launch_bounds__(sf_thr(HF)) void k_sampled_logits(const float* __re
   // rows straight into the fragment layout, split per slice below
   f4 wr[NS][2];
   bf16x8 a0[NS], a1[NS], a2[NS];
-  if constexpr (PRE) {
+  if constexpr (PF) {
+    const int blk = (nact ? s0 : 0) >> 5;
+    const f4* wf = reinterpret_cast<const f4*>(wp);
+#pragma unroll
+    for (int j = 0; j < NS; ++j) {
+      wr[j][0] = wf[frag_idx(blk, j, 0, lane, NS)];
+      wr[j][1] = wf[frag_idx(blk, j, 1, lane, NS)];
+    }
+  } else if constexpr (PRE) {
     const int blk = (nact ? s0 : 0) >> 5;
 #pragma unroll
     for (int j = 0; j < NS; ++j) {
@@ -520,7 +530,7 @@ __global__ __launch_bounds__(sf_thr(HF)) void k_sampled_logits(const float* __re
   f16v accA = {}, accB = {};
 #pragma unroll
   for (int j = 0; j < NS; ++j) {
-    if constexpr (!PRE) split3x8(wr[j][0], wr[j][1], a0[j], a1[j], a2[j]);
+    if constexpr (!PRE || PF) split3x8(wr[j][0], wr[j][1], a0[j], a1[j], a2[j]);
     accA = mfma_split<NT>(a0[j], a1[j], a2[j], hsA[boff(j)], hsA[boff(j) + 64], hsA[boff(j) + 128], accA);
   }
   // row tile 0 publishes the draw and the gathered rows (the backward's Wg / bg)
@@ -690,7 +700,9 @@ __global__ __launch_bounds__(sf_thr(HF)) void k_sampled_logits(const float* __re
 // draw: 0 = the S ids are given in neg; 1 = draw them (counter-based stream)
 // and publish ids, bg and the rows Wg; 2 = pre-gathered by rg_gather_neg in
 // the step's embedding-gather launch: neg / bg / Wg already hold the ids,
-// biases and rows and w_planes their fragment-order bf16 planes.
+// biases and rows and w_planes their fragment-order bf16 planes; 3 = the same
+// with w_planes holding the rows as fp32 fragments (rg_gather_neg wfmt 1,
+// HF <= 128).
 extern "C" int rg_sampled_logits(const float* h, const float* W, const float* bias, int32_t* neg, int draw,
                                  uint64_t seed, uint64_t counter, int64_t A, int B, int S, int HF, int terms,
                                  float* Z, int64_t ldz, float* pmax, float* psum, float* Wg, float* bg,
@@ -698,7 +710,8 @@ extern "C" int rg_sampled_logits(const float* h, const float* W, const float* bi
   if (B <= 0 || S <= 0 || (B % 32) || (S % 32) || !h || !W || !bias || !neg || !Z || !pmax || !psum || !bg)
     return RG_ERR_ARG;
   if (ldz < S || (ldz & 3)) return RG_ERR_ARG;
-  if (draw < 0 || draw > 2 || (draw == 2 && !w_planes)) return RG_ERR_ARG;
+  if (draw < 0 || draw > 3 || (draw >= 2 && !w_planes)) return RG_ERR_ARG;
+  if (draw == 3 && HF > 128) return RG_ERR_ARG;
   if (draw == 1 && (A <= 0 || A > INT32_MAX)) return RG_ERR_ARG;
   if (terms != 6 && terms != 9) return RG_ERR_ARG;
   const int neg_wg = sf_neg(HF);
@@ -706,16 +719,18 @@ extern "C" int rg_sampled_logits(const float* h, const float* W, const float* bi
   const dim3 grid((unsigned)((S + neg_wg - 1) / neg_wg), (unsigned)((B + rows_wg - 1) / rows_wg));
   const bf16x8* hk = (const bf16x8*)h_planes;
   const bf16x8* wp = (const bf16x8*)w_planes;
-#define SFH(HFV, NTV, DRV, HKV, PRV)                                                                                  \
-  RG_TLAUNCH((k_sampled_logits<HFV, NTV, DRV, HKV, PRV>), grid, dim3(sf_thr(HFV)), 0, stream, h, W, bias, neg, seed, \
-             counter, (uint64_t)(A > 0 ? A : 0), B, S, Z, ldz, pmax, psum, Wg, bg, hk, wp)
+#define SFH(HFV, NTV, DRV, HKV, PRV, ...)                                                                          \
+  RG_TLAUNCH((k_sampled_logits<HFV, NTV, DRV, HKV, PRV, ##__VA_ARGS__>), grid, dim3(sf_thr(HFV)), 0, stream, h, W, \
+             bias, neg, seed, counter, (uint64_t)(A > 0 ? A : 0), B, S, Z, ldz, pmax, psum, Wg, bg, hk, wp)
 #define SFG(HFV, NTV)                                     \
   if (hk) {                                               \
-    if (draw == 2) SFH(HFV, NTV, false, true, true);      \
+    if (draw == 3) SFH(HFV, NTV, false, true, true, HFV <= 128); \
+    else if (draw == 2) SFH(HFV, NTV, false, true, true); \
     else if (draw) SFH(HFV, NTV, true, true, false);      \
     else SFH(HFV, NTV, false, true, false);               \
   } else {                                                \
-    if (draw == 2) SFH(HFV, NTV, false, false, true);     \
+    if (draw == 3) SFH(HFV, NTV, false, false, true, HFV <= 128); \
+    else if (draw == 2) SFH(HFV, NTV, false, false, true); \
     else if (draw) SFH(HFV, NTV, true, false, false);     \
     else SFH(HFV, NTV, false, false, false);              \
   }

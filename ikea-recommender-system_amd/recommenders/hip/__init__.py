@@ -116,7 +116,7 @@ SIGNATURES = {
     "rg_sampled_work_bytes": [I, I, I],
     "rg_sampled_fwd_x": [P, P, P, P, I, U64, U64, I64, I, I, I, I, P, I64, P, P, P, P, P, P],
     "rg_sampled_logits": [P, P, P, P, I, U64, U64, I64, I, I, I, I, P, I64, P, P, P, P, P, P, P],
-    "rg_gather_neg": [P, I, I, P, P, P, P, I, I64, I, I, P, P, P, P, P, U64, U64, I64, I, I, P, P, P, P, P],
+    "rg_gather_neg": [P, I, I, P, P, P, P, I, I64, I, I, P, P, P, P, P, U64, U64, I64, I, I, P, P, P, P, I, P],
     "rg_sampled_dz_rows": [P, I64, P, I, I, F, P, P, P],
     "rg_sampled_fwd": [P, P, P, P, I, I, I, P, I64, P, P, P, P, P],
     "rg_sampled_lse": [P, P, P, P, I, I64, I, P, P, I, F, P, P, P, P, P, P, P],

@@ -401,10 +401,15 @@ class Trunk:
                 self._exchange_grads(w, tag, st)
             return
         skip = -1 if self.train_pad else self.pad
-        for d in range(self.ndir):
-            with region("scatter"):
-                self.scatter(w.tok_id[d].data_ptr(), w.dX[d].data_ptr(), self.E, w.ntok_ptr, w.T_host, skip,
-                             self.G_emb.data_ptr(), self.n_local, self.tags.data_ptr(), tag, st)
+        with region("scatter"):
+            if self.ndir == 2:
+                # Bidir: the reverse direction's token gradients (stored time-reversed) are
+                # added into the forward direction's first (rg_combine_dirs), so one sort and
+                # one segmented sum scatter both (as the row-sharded exchange does)
+                call("rg_combine_dirs", w.dX[0].data_ptr(), w.dX[1].data_ptr(), w.lsort.data_ptr(),
+                     w.offs.data_ptr(), w.B, self.E, st)
+            self.scatter(w.tok_id[0].data_ptr(), w.dX[0].data_ptr(), self.E, w.ntok_ptr, w.T_host, skip,
+                         self.G_emb.data_ptr(), self.n_local, self.tags.data_ptr(), tag, st)
 
     # ---- data-parallel variant: gradients summed over ranks before Adam ----
     def grads_for_allreduce(self, tag):
@@ -757,6 +762,9 @@ SCREEN_TERMS = 1
 SCREEN_TOL_1 = 8e-3
 SCREEN_CMAX_BYTES = 2 << 30
 SCREEN_ROW_CHUNK = 2048
+# the sampled step's pre-gathered negatives (rg_gather_neg) as fp32 fragments
+# the logits kernel splits itself (draw 3), not bf16 planes (draw 2), at HF <= 128
+NEG_FP32_FRAGS = True
 LOGIT_TERMS = {"f32x9": 9, "f32x6": 6, "f32x6d3": 6}
 # HIP stream priority of the fused head's pass 2 (its side stream, §4b of
 # DESIGN): pass 2 is the step's critical path, the trunk work beside it is not
@@ -1277,6 +1285,7 @@ class _SampledWS:
         self.bg = z(S)
         self.Wp = None    # the negatives' bf16 planes from rg_gather_neg (allocated on first use)
         self.pre_draw = -1   # draw index whose ids / bg / Wg / Wp the gather launch already wrote
+        self.pre_fmt = 0     # Wp's format then (rg_gather_neg wfmt)
         self.work = None  # split-bf16 operand planes (allocated on first use)
         self.dh_splits = max(1, min(8, S // 256))
         self.dw_splits = max(1, min(16, B // 256))
@@ -1342,16 +1351,18 @@ class SampledSoftmaxHead(SoftmaxHead):
         if w.Wp is None:
             w.Wp = torch.empty(self.S * self.HF * 6, dtype=torch.uint8, device=self.device)
         head, draw = self, self.draws
+        wfmt = 1 if NEG_FP32_FRAGS and self.HF <= 128 else 0
 
         class _Job:
             @staticmethod
             def args():
                 return (head.W.p.data_ptr(), head.b.p.data_ptr(), head.seed, draw, head.A, head.S, head.HF,
-                        w.ids.data_ptr(), w.Wg.data_ptr(), w.bg.data_ptr(), w.Wp.data_ptr())
+                        w.ids.data_ptr(), w.Wg.data_ptr(), w.bg.data_ptr(), w.Wp.data_ptr(), wfmt)
 
             @staticmethod
             def done():
                 w.pre_draw = draw
+                w.pre_fmt = wfmt
         return _Job()
 
     def forward_loss(self, h, tgt, slot="main", h_planes=None):
@@ -1372,7 +1383,7 @@ class SampledSoftmaxHead(SoftmaxHead):
             if split and w.zrow:  # one launch: [draw, row gather, operand split,] logits, partials
                 hp = h_planes.data_ptr() if h_planes is not None else None
                 call("rg_sampled_logits", h.data_ptr(), self.W.p.data_ptr(), self.b.p.data_ptr(), w.ids.data_ptr(),
-                     2 if pre else 1, self.seed, self.draws, self.A, B, self.S, self.HF, w.terms, w.ZT.data_ptr(),
+                     (3 if w.pre_fmt else 2) if pre else 1, self.seed, self.draws, self.A, B, self.S, self.HF, w.terms, w.ZT.data_ptr(),
                      w.ldz, w.pmax.data_ptr(), w.psum.data_ptr(), w.Wg.data_ptr(), w.bg.data_ptr(), hp,
                      w.Wp.data_ptr() if pre else None, st)
             elif split:  # draw + gather + operand split fused into one prep launch

@@ -395,12 +395,12 @@ int rg_gather_h(const int64_t* s, int B, int L, const int32_t* perm, const int32
  * or rg_gather_h (emb16 = 1) with the S negatives' row gather in the same launch — draw `counter` of the
  * counter-based stream (seed, S, A; rg_sample_uniform's ids) -> ids[S], bg = bias[ids], Wg (S, HF) =
  * W[ids] and Wp (S·HF·6 bytes) = the rows' bf16 planes in fragment order for rg_sampled_logits
- * (draw = 2).  E, HF in {32, 64, 128, 256}, L <= 64, S % 32 == 0.  Replaces the nn.Embedding forward
+ * (draw = 2); wfmt 1 (HF <= 128): Wp (S·HF·4 bytes) = the rows as fp32 fragments instead (draw = 3).  E, HF in {32, 64, 128, 256}, L <= 64, S % 32 == 0.  Replaces the nn.Embedding forward
  * (GRU4Rec/model.py:69,74) plus the negatives' row lookup of the build-defined sampled head. */
 int rg_gather_neg(const int64_t* s, int B, int L, const int32_t* perm, const int32_t* lsort, const int32_t* offs,
                   const void* emb, int emb16, int64_t n_rows, int E, int reverse, int32_t* tok_id, float* X,
                   int32_t* err, const float* W, const float* bias, uint64_t seed, uint64_t counter, int64_t A, int S,
-                  int HF, int32_t* ids, float* Wg, float* bg, void* Wp, rg_stream_t stream);
+                  int HF, int32_t* ids, float* Wg, float* bg, void* Wp, int wfmt, rg_stream_t stream);
 /* rg_adam_rows (cols % 4 == 0) that also writes P16 = fp16(P); tags == NULL: every row has a gradient */
 int rg_adam_rows_h(float* P, float* M, float* V, float* G, const int32_t* tags, int32_t tag, int64_t rows, int cols,
                    const float* adam6, uint16_t* P16, rg_stream_t stream);
@@ -437,7 +437,8 @@ int rg_sampled_fwd_x(const float* h, const float* W, const float* bias, int32_t*
  * h_planes (optional, HF <= 128): h's bf16 K-planes (rg_gru_fwd_dirs_planes / rg_head_planes), moved
  * to LDS by DMA instead of splitting h in the kernel.
  * draw: 0 = ids given in neg, 1 = drawn here, 2 = pre-gathered by rg_gather_neg (neg, bg, Wg already
- * hold the ids, biases and rows; w_planes = its fragment-order planes, required). */
+ * hold the ids, biases and rows; w_planes = its fragment-order planes, required); 3 = the same with
+ * w_planes = its fp32 fragments (wfmt 1; HF <= 128). */
 int rg_sampled_logits(const float* h, const float* W, const float* bias, int32_t* neg, int draw, uint64_t seed,
                       uint64_t counter, int64_t A, int B, int S, int HF, int terms, float* Z, int64_t ldz,
                       float* pmax, float* psum, float* Wg, float* bg, const void* h_planes, const void* w_planes,

@@ -255,8 +255,8 @@ def test_gather_neg_matches_gather_and_draw(E, HF, emb16):
     """rg_gather_neg (the sampled step's embedding gather with the negatives'
     row gather in the same launch): the embedding rows bit-equal to rg_gather,
     the negatives bit-equal to the draw / row lookup rg_sampled_logits makes
-    itself, and the pre-gathered logits (draw = 2) bit-equal to the one-launch
-    draw (draw = 1)."""
+    itself, and the pre-gathered logits (draw = 2: bf16 planes, draw = 3: fp32
+    fragments) bit-equal to the one-launch draw (draw = 1)."""
     from oracle.models import sample_uniform
     from recommenders.data_utils.synthetic import SessionStream
     from recommenders.hip import call, stream_ptr
@@ -285,7 +285,7 @@ def test_gather_neg_matches_gather_and_draw(E, HF, emb16):
     seed, counter = 11, 5
     call("rg_gather_neg", s.data_ptr(), B, L, perm.data_ptr(), ls.data_ptr(), offs.data_ptr(), table.data_ptr(),
          emb16, A + 1, E, 0, t1.data_ptr(), X1.data_ptr(), err.data_ptr(), W.data_ptr(), bias.data_ptr(), seed,
-         counter, A, S, HF, ids.data_ptr(), Wg.data_ptr(), bg.data_ptr(), Wp.data_ptr(), st)
+         counter, A, S, HF, ids.data_ptr(), Wg.data_ptr(), bg.data_ptr(), Wp.data_ptr(), 0, st)
     torch.cuda.synchronize()
     assert int(err) == 0
     assert torch.equal(X0, X1) and torch.equal(t0, t1)
@@ -314,3 +314,38 @@ def test_gather_neg_matches_gather_and_draw(E, HF, emb16):
         call("rg_sampled_logits", h.data_ptr(), W.data_ptr(), bias.data_ptr(), ids.data_ptr(), 2, seed, counter, A,
              B, S, HF, 6, out[1][0].data_ptr(), S, out[1][1].data_ptr(), out[1][2].data_ptr(), Wg.data_ptr(),
              bg.data_ptr(), None, None, st)
+    if HF > 128:
+        with pytest.raises(RuntimeError):   # fp32 fragments: HF <= 128 only
+            call("rg_gather_neg", s.data_ptr(), B, L, perm.data_ptr(), ls.data_ptr(), offs.data_ptr(),
+                 table.data_ptr(), emb16, A + 1, E, 0, t1.data_ptr(), X1.data_ptr(), err.data_ptr(), W.data_ptr(),
+                 bias.data_ptr(), seed, counter, A, S, HF, ids.data_ptr(), Wg.data_ptr(), bg.data_ptr(),
+                 Wp.data_ptr(), 1, st)
+        return
+    # wfmt 1: the rows as fp32 fragments (common.h frag_idx), the rest unchanged;
+    # draw = 3 reads them and splits in the kernel: bit-equal to draw = 1, with h
+    # as fp32 rows and as its K-planes
+    Wf = torch.full((S * HF,), float("nan"), device="cuda")
+    ids3 = torch.full((S,), -7, dtype=torch.int32, device="cuda")
+    Wg3, bg3 = torch.full((S, HF), float("nan"), device="cuda"), torch.full((S,), float("nan"), device="cuda")
+    X3 = torch.full((T, E), float("nan"), device="cuda")
+    call("rg_gather_neg", s.data_ptr(), B, L, perm.data_ptr(), ls.data_ptr(), offs.data_ptr(), table.data_ptr(),
+         emb16, A + 1, E, 0, t1.data_ptr(), X3.data_ptr(), err.data_ptr(), W.data_ptr(), bias.data_ptr(), seed,
+         counter, A, S, HF, ids3.data_ptr(), Wg3.data_ptr(), bg3.data_ptr(), Wf.data_ptr(), 1, st)
+    torch.cuda.synchronize()
+    assert torch.equal(X3, X0) and torch.equal(ids3, ids) and torch.equal(Wg3, Wg) and torch.equal(bg3, bg)
+    # (blk, n, j, hh, q, 4) -> (blk, j, q, hh, n, 4)
+    fr = Wg.view(S // 32, 32, HF // 16, 2, 2, 4).permute(0, 2, 4, 3, 1, 5).contiguous().flatten()
+    assert torch.equal(Wf, fr)
+    hk = torch.empty(call("rg_head_plane_bytes", B, HF), dtype=torch.uint8, device="cuda")
+    call("rg_head_planes", h.data_ptr(), B, HF, hk.data_ptr(), None, None, None, st)
+    for hp in (None, hk):
+        Z = torch.full((B, S), float("nan"), device="cuda")
+        nT = call("rg_sampled_nparts", B, S, 6)
+        pm, ps = torch.empty(nT, B, device="cuda"), torch.empty(nT, B, device="cuda")
+        i2, Wg2, bg2 = ids.clone(), Wg.clone(), bg.clone()
+        call("rg_sampled_logits", h.data_ptr(), W.data_ptr(), bias.data_ptr(), i2.data_ptr(), 3, seed, counter, A,
+             B, S, HF, 6, Z.data_ptr(), S, pm.data_ptr(), ps.data_ptr(), Wg2.data_ptr(), bg2.data_ptr(),
+             None if hp is None else hp.data_ptr(), Wf.data_ptr(), st)
+        torch.cuda.synchronize()
+        for x1, x2 in zip(out[1], (Z, pm, ps, i2, Wg2, bg2)):
+            assert torch.equal(x1, x2)
