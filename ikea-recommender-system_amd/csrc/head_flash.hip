@@ -1590,7 +1590,11 @@ inline FlTail fl_tail(int B, int A, int HF) {
   const int rpb = fl_rows(HF, 2), nblk = (A + rpb - 1) / rpb, nct = B / 32;
   const int nfull = nblk / 256 * 256, left = nblk - nfull;
   if (nfull == 0 || left == 0 || left > 192) return FlTail{nblk, 1, 0};
-  const int ts = min(min(8, 256 / left), nct);
+  int ts = min(min(8, 256 / left), nct);
+  // no part without row chunks: k_flash_dw's prologue DMAs its part's first
+  // chunk (rows past the last chunk otherwise) before it knows nch
+  const int cper = (nct + ts - 1) / ts;
+  ts = (nct + cper - 1) / cper;
   if (ts < 2) return FlTail{nblk, 1, 0};
   return FlTail{nfull, ts, A - nfull * rpb};
 }
