@@ -60,3 +60,25 @@ def test_adam_scalars_match_torch_rounding():
     assert a[5] == np.float32(-0.01 / (1 - 0.9))
     a2 = list(c.next_args())
     assert a2[3] == np.float32((1 - 0.999 ** 2) ** 0.5)
+
+
+@pytest.mark.parametrize("B,A,HF", [(256, 78341, 64), (512, 70000, 128), (256, 40011, 256), (96, 78341, 64),
+                                    (128, 78341, 64), (4096, 1_000_001, 128), (64, 66000, 32), (8192, 5_000_001, 256)])
+def test_pass2_tail_split_has_no_empty_part(B, A, HF):
+    """rg_flash_dw's leftover item blocks go to tsplit workgroups of ceil(nct /
+    tsplit) row chunks each (csrc/head_flash.hip fl_tail): every part must get
+    at least one chunk — its prologue DMAs the part's first chunk before the
+    chunk count is known (a part past the last chunk read past h's planes)."""
+    from recommenders.hip import load_library
+    nb = load_library().rg_flash_dw_work_bytes(B, A, HF)
+    rpb = 256 if HF <= 128 else 128
+    nblk = -(-A // rpb)
+    nfull = nblk // 256 * 256
+    ntail = A - nfull * rpb
+    if nb == 0:
+        return   # no tail split at this shape
+    tsplit = nb // (ntail * (HF + 1) * 4)
+    assert tsplit * ntail * (HF + 1) * 4 == nb and tsplit >= 2
+    nct = B // 32
+    cper = -(-nct // tsplit)
+    assert (tsplit - 1) * cper < nct
