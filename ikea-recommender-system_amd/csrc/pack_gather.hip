@@ -92,60 +92,21 @@ __global__ __launch_bounds__(PACK_THREADS) void k_pack(const int64_t* __restrict
   if (tid == 0) offs[B] = carry;
 }
 
-// B <= PACK_SORT_MAX: the same permutation from one LDS bitonic sort of the
-// unique keys (L - len)·B + row (length descending, row ascending = stable),
-// then a block scan of the sorted lengths.  No serial per-thread loops: the
-// general kernel above spends ~0.1 ms at B 4096 in its O(block) rank scans.
 #define PACK_SORT_MAX 8192
-__global__ __launch_bounds__(PACK_THREADS) void k_pack_sort(const int64_t* __restrict__ lens, int B, int L,
-                                                            int unpacked, int n2, int32_t* __restrict__ perm,
-                                                            int32_t* __restrict__ lsort, int32_t* __restrict__ offs) {
-  __shared__ uint32_t key[PACK_SORT_MAX];
-  __shared__ int wsum[PACK_THREADS / 64];
-  const int tid = threadIdx.x;
-  for (int i = tid; i < n2; i += PACK_THREADS) {
-    uint32_t k = 0xFFFFFFFFu;
-    if (i < B) {
-      int l = unpacked ? L : (int)lens[i];
-      l = l < 1 ? 1 : (l > L ? L : l);
-      k = (uint32_t)(L - l) * (uint32_t)B + (uint32_t)i;
-    }
-    key[i] = k;
-  }
-  __syncthreads();
-  for (int size = 2; size <= n2; size <<= 1)
-    for (int stride = size >> 1; stride > 0; stride >>= 1) {
-      for (int i = tid; i < n2 / 2; i += PACK_THREADS) {
-        const int lo = 2 * i - (i & (stride - 1));
-        const int hi = lo + stride;
-        const bool up = (lo & size) == 0;
-        const uint32_t a = key[lo], b = key[hi];
-        if ((a > b) == up) {
-          key[lo] = b;
-          key[hi] = a;
-        }
-      }
-      __syncthreads();
-    }
-  // rows r of the sorted order; offs = exclusive scan of the lengths
-  constexpr int PER = PACK_SORT_MAX / PACK_THREADS;
-  const int r0 = tid * PER;
-  int lv[PER], run = 0;
-#pragma unroll
-  for (int q = 0; q < PER; ++q) {
-    const int r = r0 + q;
-    lv[q] = 0;
-    if (r < B) {
-      const uint32_t k = key[r];
-      lv[q] = L - (int)(k / (uint32_t)B);
-      perm[r] = (int32_t)(k % (uint32_t)B);
-      lsort[r] = lv[q];
-    }
-    run += lv[q];
-  }
-  // block exclusive scan of the per-thread sums (wave scan + wave totals)
-  const int lane = tid & 63, w = tid >> 6;
-  int inc = run;
+
+// B <= PACK_SORT_MAX (the step's pack): a stable counting sort by length in
+// one workgroup, no comparison network.  Wave w takes rows w·64·per .. +64·per,
+// round q of it rows q·64 + lane (so (wave, round, lane) order is row order);
+// bin = L − len (ascending bin = descending length).  Per-wave bin counts in
+// LDS -> per bin the waves' exclusive prefix and total -> bin starts and token
+// offsets by one scan over the L bins (every row of a bin has the same
+// length: offs[r] = binoff[b] + (r − binstart[b])·len) -> each round's rows
+// ranked by a match loop over the wave's distinct bins (one ballot per value
+// and round).  The bitonic sort it replaces ran 78 barrier-separated stages,
+// 40 us at B 4096.
+__device__ __forceinline__ int pack_block_exscan(int v, int* wsum, int& total) {
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  int inc = v;
 #pragma unroll
   for (int d = 1; d < 64; d <<= 1) {
     const int y = __shfl_up(inc, d);
@@ -153,25 +114,102 @@ __global__ __launch_bounds__(PACK_THREADS) void k_pack_sort(const int64_t* __res
   }
   if (lane == 63) wsum[w] = inc;
   __syncthreads();
-  int base = 0;
-  for (int q = 0; q < w; ++q) base += wsum[q];
-  int acc = base + inc - run;
-#pragma unroll
-  for (int q = 0; q < PER; ++q) {
-    const int r = r0 + q;
-    if (r < B) offs[r] = acc;
-    acc += lv[q];
+  int base = 0, all = 0;
+  for (int q = 0; q < PACK_THREADS / 64; ++q) {
+    base += q < w ? wsum[q] : 0;
+    all += wsum[q];
   }
-  if (tid == PACK_THREADS - 1) offs[B] = acc;
+  __syncthreads();   // wsum reusable
+  total = all;
+  return base + inc - v;
+}
+
+__global__ __launch_bounds__(PACK_THREADS) void k_pack_count(const int64_t* __restrict__ lens, int B, int L,
+                                                             int unpacked, int per, int32_t* __restrict__ perm,
+                                                             int32_t* __restrict__ lsort, int32_t* __restrict__ offs) {
+  constexpr int NWV = PACK_THREADS / 64, PMAX = PACK_SORT_MAX / PACK_THREADS;
+  __shared__ int cnt[NWV][PACK_MAXL];   // wave w's rows in bin b -> the earlier waves' rows in bin b
+  __shared__ int bstart[PACK_MAXL], boff[PACK_MAXL];
+  __shared__ int wsum[NWV];
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+  for (int i = tid; i < NWV * PACK_MAXL; i += PACK_THREADS) (&cnt[0][0])[i] = 0;
+  __syncthreads();
+  const int rw = w * 64 * per + lane;   // row of round 0
+  int bins[PMAX];
+#pragma unroll
+  for (int q = 0; q < PMAX; ++q) {
+    const int r = rw + 64 * q;
+    bins[q] = -1;
+    if (q < per && r < B) {
+      int l = unpacked ? L : (int)lens[r];
+      l = l < 1 ? 1 : (l > L ? L : l);
+      bins[q] = L - l;
+      atomicAdd(&cnt[w][L - l], 1);
+    }
+  }
+  __syncthreads();
+  int tot = 0;
+  if (tid < L) {
+    for (int q = 0; q < NWV; ++q) {
+      const int c = cnt[q][tid];
+      cnt[q][tid] = tot;
+      tot += c;
+    }
+  }
+  int T = 0, nb = 0;
+  const int bs = pack_block_exscan(tid < L ? tot : 0, wsum, nb);
+  const int bo = pack_block_exscan(tid < L ? tot * (L - tid) : 0, wsum, T);
+  if (tid < L) {
+    bstart[tid] = bs;
+    boff[tid] = bo;
+  }
+  __syncthreads();
+  // ranks inside the wave: one match step per distinct bin of its rows (the
+  // leader value's ballot in every round; no LDS traffic in the loop)
+  const uint64_t lt = (1ull << lane) - 1ull;
+  uint64_t pend[PMAX];
+  int rk[PMAX];
+#pragma unroll
+  for (int q = 0; q < PMAX; ++q) {
+    pend[q] = q < per ? __ballot(bins[q] >= 0) : 0ull;
+    rk[q] = 0;
+  }
+  for (;;) {
+    int v = -1;
+#pragma unroll
+    for (int q = 0; q < PMAX; ++q)
+      if (v < 0 && pend[q] != 0ull) v = __builtin_amdgcn_readlane(bins[q], __builtin_ctzll(pend[q]));
+    if (v < 0) break;
+    int acc = 0;   // rows of bin v in the wave's earlier rounds
+#pragma unroll
+    for (int q = 0; q < PMAX; ++q) {
+      if (q < per) {
+        const uint64_t m = __ballot(bins[q] == v);
+        if (bins[q] == v) rk[q] = acc + __popcll(m & lt);
+        acc += __popcll(m);
+        pend[q] &= ~m;
+      }
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < PMAX; ++q) {
+    const int b = bins[q];
+    if (q < per && b >= 0) {
+      const int pos = bstart[b] + cnt[w][b] + rk[q];
+      perm[pos] = rw + 64 * q;
+      lsort[pos] = L - b;
+      offs[pos] = boff[b] + (pos - bstart[b]) * (L - b);
+    }
+  }
+  if (tid == 0) offs[B] = T;
 }
 
 extern "C" int rg_pack(const int64_t* lens, int B, int L, int unpacked, int32_t* perm, int32_t* lsort,
                        int32_t* offs, hipStream_t stream) {
   if (B <= 0 || L <= 0 || L > PACK_MAXL) return RG_ERR_ARG;
   if (B <= PACK_SORT_MAX) {
-    int n2 = 2;
-    while (n2 < B) n2 <<= 1;
-    hipLaunchKernelGGL(k_pack_sort, dim3(1), dim3(PACK_THREADS), 0, stream, lens, B, L, unpacked, n2, perm, lsort,
+    const int per = (B + PACK_THREADS - 1) / PACK_THREADS;
+    hipLaunchKernelGGL(k_pack_count, dim3(1), dim3(PACK_THREADS), 0, stream, lens, B, L, unpacked, per, perm, lsort,
                        offs);
   } else {
     hipLaunchKernelGGL(k_pack, dim3(1), dim3(PACK_THREADS), 0, stream, lens, B, L, unpacked, perm, lsort, offs);
