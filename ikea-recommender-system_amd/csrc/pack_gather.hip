@@ -265,8 +265,8 @@ __global__ __launch_bounds__(256) void k_gather(const int64_t* __restrict__ s, i
 }
 
 // Compile-time-E variant (E ∈ {32, 64, 128, 256}, L <= GW_MAXL): a workgroup
-// takes GW_ROWS consecutive sorted rows, whose tokens are one contiguous
-// packed range [offs[r0], offs[r0 + GW_ROWS]).  Three dependent memory steps
+// takes GW_ROWS sorted rows (two long, two short when B % 4 == 0; else
+// consecutive ones), each row's tokens at its own packed range.  Three dependent memory steps
 // per workgroup: the rows' (perm, length, offset), their item ids (into LDS),
 // then every table row of the range — a lane issues all of its (up to U) row
 // loads before any store, so up to GW_FLIGHT random 512-B rows are in flight
@@ -335,31 +335,45 @@ __global__ __launch_bounds__(256) void k_gather_e(const int64_t* __restrict__ s,
   constexpr int TPP = 256 / V4;                       // tokens per pass of the workgroup
   constexpr int FLT = E >= 256 ? GW_FLIGHT / 2 : GW_FLIGHT;   // rows in flight (64 VGPRs of f4 per lane)
   constexpr int U = FLT / TPP;                        // passes whose loads issue together
-  __shared__ int ids[GW_ROWS * GW_MAXL];
-  __shared__ int rb[GW_ROWS], rl[GW_ROWS], ro[GW_ROWS + 1];
+  __shared__ int ids[GW_ROWS * GW_MAXL], dsts[GW_ROWS * GW_MAXL];
+  __shared__ int rb[GW_ROWS], rl[GW_ROWS], ro[GW_ROWS];
   if ((int)blockIdx.x < np.nwg) {
     neg_prep(np, blockIdx.x);
     return;
   }
   const int tid = threadIdx.x;
-  const int r0 = ((int)blockIdx.x - np.nwg) * GW_ROWS;
-  const int nr = min(GW_ROWS, B - r0);
+  // B % 4 == 0: workgroup k takes sorted rows 2k, 2k + 1 (long) and B − 2 − 2k,
+  // B − 1 − 2k (short), so every workgroup gathers about the mean token count
+  // (four consecutive sorted rows: 4 to 4·L tokens); the longest pairs still
+  // dispatch first
+  constexpr int GH = GW_ROWS / 2;
+  const int k = (int)blockIdx.x - np.nwg;
+  const bool pair = B % GW_ROWS == 0;
+  const int r0 = k * GW_ROWS;
+  const int nr = pair ? GW_ROWS : min(GW_ROWS, B - r0);
   if (tid < nr) {
-    rb[tid] = perm[r0 + tid];
-    rl[tid] = lsort[r0 + tid];
-    ro[tid] = offs[r0 + tid];
+    const int r = !pair ? r0 + tid : tid < GH ? GH * k + tid : B - GH * (k + 1) + tid - GH;
+    rb[tid] = perm[r];
+    rl[tid] = lsort[r];
+    ro[tid] = offs[r];   // packed position of the row's token 0
   }
-  if (tid == 0) ro[nr] = offs[r0 + nr];
   __syncthreads();
-  // item ids of every (row, t), stored at the token's packed position
-  const int tok0 = ro[0], ntok = ro[nr] - tok0;
+  int pre[GW_ROWS];   // workgroup token index where row j starts
+  int ntok = 0;
+#pragma unroll
+  for (int q = 0; q < GW_ROWS; ++q) {
+    pre[q] = q < nr ? ntok : INT32_MAX;
+    ntok += q < nr ? rl[q] : 0;
+  }
+  // item ids of every (row, t) and its packed position
   for (int i = tid; i < ntok; i += 256) {
     int j = 0;
 #pragma unroll
-    for (int q = 1; q < GW_ROWS; ++q) j += (q < nr && i >= ro[q] - tok0);
-    const int t = i - (ro[j] - tok0), len = rl[j];
+    for (int q = 1; q < GW_ROWS; ++q) j += i >= pre[q];
+    const int t = i - pre[j], len = rl[j];
     const int64_t id = s[(int64_t)rb[j] * L + (reverse ? len - 1 - t : t)];
     ids[i] = (id >= 0 && id < n_rows) ? (int32_t)id : -1;   // nn.Embedding raises on such ids
+    dsts[i] = ro[j] + t;
   }
   __syncthreads();
   const int c = tid % V4, t0 = tid / V4;
@@ -375,9 +389,10 @@ __global__ __launch_bounds__(256) void k_gather_e(const int64_t* __restrict__ s,
     for (int u = 0; u < U; ++u) {
       const int i = i0 + TPP * u;
       if (i < ntok) {
-        reinterpret_cast<f4*>(X + (int64_t)(tok0 + i) * E)[c] = v[u];
+        const int d = dsts[i];
+        reinterpret_cast<f4*>(X + (int64_t)d * E)[c] = v[u];
         if (c == 0) {
-          tok_id[tok0 + i] = ids[i];
+          tok_id[d] = ids[i];
           if (ids[i] < 0 && err) atomicOr(err, 1);
         }
       }
