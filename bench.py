@@ -98,6 +98,8 @@ def parse():
                          "hip/engine.py ZSTORE_MAX_BYTES) or pass 2 recomputes them (off)")
     ap.add_argument("--no-target", action="store_true", help="skip the north-star gather+sampled-logits side run")
     ap.add_argument("--no-native-side", action="store_true", help="skip the native-f32 side run")
+    ap.add_argument("--extra-steps", type=int, default=10,
+                    help="C2 at N=1: timed steps of the short C3 / C4 side lines (configs_extra); 0 skips them")
     return ap.parse_args()
 
 
@@ -157,24 +159,28 @@ def _cpu_oracle(cfg, items, dim, seq, counts=None):
                        topk_nov=1, nov_rew_sig=1.0, **common)
 
 
-def _cpu_run(cfg, items, dim, seq, B, steps, seed, warmup=1):
+def _cpu_run(cfg, items, dim, seq, B, steps, seed, warmup=1, batches=None, counts=None):
     """Oracle steps of config ``cfg`` on the host: per-step seconds after
-    ``warmup`` untimed steps."""
-    from recommenders.data_utils.synthetic import SessionStream
-    st = SessionStream(items, seq, B * (steps + warmup), seed=seed)
-    orc = _cpu_oracle(cfg, items, dim, seq, st.item_counts())
+    ``warmup`` untimed steps, every step's loss, and the oracle.  ``batches``
+    (with ``counts``): the GPU run's own host batches (the loss-parity leg);
+    else a stream of its own (seed ``seed``)."""
+    if batches is None:
+        from recommenders.data_utils.synthetic import SessionStream
+        st = SessionStream(items, seq, B * (steps + warmup), seed=seed)
+        batches = [st.batch(i, B) for i in range(warmup + steps)]
+        counts = st.item_counts()
+    orc = _cpu_oracle(cfg, items, dim, seq, counts)
 
     def one(i):
-        b = st.batch(i, B)
+        b = batches[i]
         return orc.step(*b) if cfg in ("c4", "c5") else orc.step(b[0], b[1], b[4])
-    for i in range(warmup):
-        one(i)
+    losses = [one(i) for i in range(warmup)]
     times = []
     for i in range(warmup, warmup + steps):
         t0 = time.perf_counter()
-        one(i)
+        losses.append(one(i))
         times.append(time.perf_counter() - t0)
-    return times
+    return times, losses, orc
 
 
 CPU_NAMES = {"c2": "GRU4Rec", "c3": "BidirGRU4Rec (2048 shared sampled negatives, dropout 0)",
@@ -188,18 +194,13 @@ CPU_NAMES = {"c2": "GRU4Rec", "c3": "BidirGRU4Rec (2048 shared sampled negatives
 C5_CPU_ITEMS, C5_CPU_BATCH = 500_000, 256
 
 
-def cpu_baseline(args, cfg="c2"):
-    """The reference's per-step math on PyTorch-CPU (oracle/, restatement pinned
-    to the reference's golden vectors), timed on this host with every CPU the
-    process may use (host_threads): the config's workload at its items, dims
-    and seq_len — C2 at batch 4096 when the host RAM allows it (1
-    warm-up + 3 timed steps), C3 at batch 4096 and C4 at batch
-    512 (3 timed steps each: one C4 step scores 1M items for the supervised
-    head and the Q target), C5 at 500k items and batch 256 (dim 256, L <= 100,
-    2 timed steps; C5_CPU_ITEMS) — plus, with C2, the C1 line (BASELINE configs[0]:
-    10k items, dim32, L<=20, batch 64, --c1-warmup + --c1-steps steps)."""
-    threads, how = host_threads()
-    torch.set_num_threads(threads)
+def cpu_sample(args, cfg):
+    """(items, batch, timed steps) of the CPU leg's bounded sample: C2 at batch
+    4096 when the host RAM allows it (1 warm-up + 3 timed steps,
+    BASELINE.md §3), else 512 (6 steps), C3 at batch 4096 and C4 at batch 512
+    (3 timed steps each: one C4 step scores 1M items for the supervised head and
+    the Q target), C5 at 500k items and batch 256 (dim 256, L <= 100, 2 timed
+    steps; C5_CPU_ITEMS)."""
     ram = host_ram_gib()
     items = args.items
     if cfg == "c2":
@@ -212,7 +213,25 @@ def cpu_baseline(args, cfg="c2"):
     else:
         B = args.cpu_batch or (4096 if cfg == "c3" else 512)
         steps = args.cpu_steps or 3
-    times = _cpu_run(cfg, items, args.dim, args.seq, B, steps, 2)
+    return items, B, steps
+
+
+def cpu_baseline(args, cfg="c2", batches=None, counts=None):
+    """The reference's per-step math on PyTorch-CPU (oracle/, restatement pinned
+    to the reference's golden vectors), timed on this host with every CPU the
+    process may use (host_threads) on the bounded sample of ``cpu_sample`` —
+    plus, with C2, the C1 line (BASELINE configs[0]: 10k items, dim32, L<=20,
+    batch 64, --c1-warmup + --c1-steps steps).  ``batches``: the GPU run's
+    first host batches at the sample's batch size (C2: the loss-parity leg
+    trains the oracle on exactly what the GPU trainer saw); the oracle's
+    per-step losses and final parameters come back in ``out["_oracle"]``."""
+    threads, how = host_threads()
+    torch.set_num_threads(threads)
+    ram = host_ram_gib()
+    items, B, steps = cpu_sample(args, cfg)
+    if batches is not None:
+        batches = batches[:1 + steps]
+    times, losses, orc = _cpu_run(cfg, items, args.dim, args.seq, B, steps, 2, batches=batches, counts=counts)
     dt = float(np.sum(times))
     red = [x for x, full in (("items", items == args.items), ("batch", B == args.batch)) if not full]
     out = {"value": round(B * steps / dt, 2), "unit": "session-steps/sec", "cores": threads, "threads": how,
@@ -220,9 +239,12 @@ def cpu_baseline(args, cfg="c2"):
            "median_ms_per_step": round(float(np.median(times)) * 1e3, 1),
            "sample": (f"oracle (reference PyTorch-CPU math) {CPU_NAMES[cfg]} {items} items dim{args.dim} "
                       f"L<={args.seq}, batch {B}{' (reduced ' + ' and '.join(red) + ')' if red else ''}, {steps} "
-                      f"timed steps after 1 warm-up, torch.set_num_threads({threads}), {dt:.1f} s")}
+                      f"timed steps after 1 warm-up, torch.set_num_threads({threads}), {dt:.1f} s"
+                      f"{'; on the first batches the GPU trainer saw' if batches is not None else ''}")}
+    if batches is not None:
+        out["_oracle"] = (losses, orc)
     if cfg == "c2" and args.c1_steps > 0:
-        t1 = _cpu_run("c1", 10_000, 32, 20, 64, args.c1_steps, 1, warmup=args.c1_warmup)
+        t1, _, _ = _cpu_run("c1", 10_000, 32, 20, 64, args.c1_steps, 1, warmup=args.c1_warmup)
         d1 = float(np.sum(t1))
         out["c1"] = {"value": round(64 * args.c1_steps / d1, 2), "unit": "session-steps/sec",
                      "ms_per_step": round(d1 / args.c1_steps * 1e3, 3), "steps": args.c1_steps,
@@ -252,6 +274,48 @@ def cpu_eval_parity(net, ev, dev_idx, rows=256):
     return {"rows": rows, "top20_rows_identical": same, "hr20_cpu": h_c[0] / rows, "hr20_gpu": h_g[0] / rows,
             "ndcg20_cpu": round(n_c[0] / rows, 6), "ndcg20_gpu": round(n_g[0] / rows, 6),
             "note": "reference CPU math on the GPU-trained weights vs the device top-20 (canonical ties)"}
+
+
+def gpu_parity_run(args, dev, batches):
+    """The benched C2 trainer (same precision and stored-logit mode as the
+    line) built afresh — the same seeds, so the reference's initial weights —
+    and trained on ``batches``, the CPU leg's batches: per-step losses and the
+    parameters after the last step (host copies)."""
+    tr = make_trainer("c2", args, dev, False)
+    apply_stored_logits(tr, args.stored_logits)
+    tr.set_train()
+    losses = [float(tr.train_step(*step_args("c2", b))) for b in batches]
+    sd = {k: v.detach().cpu() for k, v in tr.gru_model.state_dict().items()}
+    del tr
+    torch.cuda.empty_cache()
+    return losses, sd
+
+
+# the trainer-vs-oracle bars of tests/test_gpu_supervised.py:33-43 / 79-100: losses within 1e-4;
+# parameters within 2·lr everywhere and within 1e-4 for all but 0.1 % of the elements (Adam's first
+# steps are sign-like, so a gradient that is zero up to summation order may move one element by 2·lr)
+PARITY_LOSS_TOL, PARITY_PARAM_TOL, PARITY_PARAM_FRAC = 1e-4, 1e-4, 1e-3
+
+
+def loss_parity(gpu_losses, cpu_losses, gpu_sd, cpu_sd, lr, batch):
+    """GPU trainer vs the CPU oracle on the same batches, seeds and init:
+    per-step |Δloss|, and per parameter tensor max |Δ| and the fraction of
+    elements more than 1e-4 apart."""
+    dl = [abs(a - b) for a, b in zip(gpu_losses, cpu_losses)]
+    params = {}
+    for k, v in gpu_sd.items():
+        d = (v.float() - cpu_sd[k].float()).abs()
+        params[k] = {"max_abs": float(d.max()), "frac_gt_1e-4": float((d > PARITY_PARAM_TOL).float().mean())}
+    ok = (max(dl) <= PARITY_LOSS_TOL and
+          all(p["max_abs"] <= 2 * lr + 1e-5 and p["frac_gt_1e-4"] < PARITY_PARAM_FRAC for p in params.values()))
+    return {"steps": len(dl), "batch": batch, "gpu_losses": [round(x, 6) for x in gpu_losses],
+            "cpu_losses": [round(x, 6) for x in cpu_losses], "max_abs_dloss": max(dl),
+            "abs_dloss": [float(f"{x:.3g}") for x in dl], "params": params, "pass": bool(ok),
+            "bars": {"loss": PARITY_LOSS_TOL, "param_max": 2 * lr + 1e-5, "param_tol": PARITY_PARAM_TOL,
+                     "param_frac_over_tol": PARITY_PARAM_FRAC},
+            "note": "the benched trainer (fresh, seeds 118 / 999) and the oracle (the reference's PyTorch-CPU "
+                    "math) trained side by side on the same first batches of the bench stream at the same lr; "
+                    "bars as tests/test_gpu_supervised.py"}
 
 
 # ------------------------------------------------------------ GPU runs -----
@@ -425,7 +489,36 @@ def target_step(kern, T, B, S, E, HF, n_gather, terms, U=None):
     return out
 
 
-def head_roofline(kern, precision, B, N, E, zs=False):
+# HBM traffic from the PMC passes (tools/pmc_head.sh, tools/pmc_ns.sh; profiles/pmc_traffic.json):
+# an entry {"bytes": per launch / per step, "src": hash, "file": the PMC output under profiles/} counts
+# only while "src" equals the hash of the sources that define the kernels measured (kernel_src_hash),
+# so a kernel edited after its PMC pass reports traffic null instead of a stale number
+KERNEL_SRC = {"head": ("head_flash.hip", "common.h"),
+              "gather+sampled_fwd": ("pack_gather.hip", "sampled.hip", "common.h")}
+
+
+def kernel_src_hash(group):
+    import hashlib
+    h = hashlib.sha256()
+    for f in KERNEL_SRC[group]:
+        with open(os.path.join(HERE, "ikea-recommender-system_amd", "csrc", f), "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
+def pmc_traffic(key, group):
+    """Measured HBM bytes of ``key`` when its PMC pass ran on the current
+    sources of ``group``, else None."""
+    pmc = os.path.join(HERE, "profiles", "pmc_traffic.json")
+    if not os.path.exists(pmc):
+        return None
+    e = json.load(open(pmc)).get(key)
+    if not isinstance(e, dict) or e.get("src") != kernel_src_hash(group):
+        return None
+    return int(e["bytes"])
+
+
+def head_roofline(kern, precision, B, N, E, zs=False, cfg="c2"):
     """zs: the stored-logit head (pass 1 stores z, pass 2 reads it and runs
     the dW contraction only: half of PASS_PRODUCTS' pass-2 products)."""
     flops_head = 2.0 * B * N * E  # one (B × E)·(E × A) contraction
@@ -435,16 +528,9 @@ def head_roofline(kern, precision, B, N, E, zs=False):
         return None
     dom = max(heads, key=heads.get)
     t = heads[dom] * 1e-3
-    traffic = None
-    pmc = os.path.join(HERE, "profiles", "pmc_traffic.json")
-    if os.path.exists(pmc) and (B, N, E) == (BATCH, ITEMS, DIM):   # the PMC passes ran at the C2 shapes
-        tab = json.load(open(pmc))
-        if zs and terms:   # the stored-logit head's passes (round 4, tools/pmc_head.sh with ZS=1)
-            traffic = tab.get(f"{dom}:{precision}:zs")
-        else:   # the round-3 (16x16x32 head) measurement where there is one
-            traffic = tab.get(f"{dom}:{precision}:r03", tab.get(f"{dom}:{precision}")) if terms else tab.get(dom)
-    elif os.path.exists(pmc) and (B, N, E) == (8192, 5_000_000, 256) and terms:   # ... and at C5 (r03g)
-        traffic = json.load(open(pmc)).get(f"c5:{dom}:{precision}")
+    # the PMC passes ran at the C2 shapes (B 4096, 1M items, d128), stored-logit head
+    traffic = (pmc_traffic(f"{dom}:{precision}:zs", "head") if (B, N, E) == (BATCH, ITEMS, DIM) and zs and cfg == "c2"
+               else None)
     if terms:
         # fused split-bf16 head (csrc/head_flash.hip): pass 1 (head_fwd: Z and the softmax half of
         # dh) and pass 2 (head_dw_adam: Z recomputed — or read back when stored — and dW), every fp32
@@ -489,6 +575,61 @@ def head_roofline(kern, precision, B, N, E, zs=False):
     return {"bound": "mfma", "kernel": dom, "achieved": round(ach, 2), "peak": FP32_MFMA_PEAK_TFLOPS,
             "unit": "TFLOP/s", "frac": round(ach / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": traffic,
             "flops_per_launch": flops_head}
+
+
+def describe(cfg, N, E, L, B, world, S):
+    """(metric, workload) of a config's line."""
+    if cfg == "c2":
+        return ("session-steps/sec at 1M items, dim128, batch 4096; HR@20/NDCG@20 parity",
+                f"GRU4Rec {N} items, dim{E}, seq_len<={L}, batch {B}/GPU, full-softmax logits")
+    if cfg == "c3":
+        return ("session-steps/sec, BidirGRU4Rec 1M items, dim128, batch 4096, 2048 sampled negatives",
+                f"BidirGRU4Rec {N} items, dim{E}, seq_len<={L}, batch {B}, {S} shared uniform "
+                f"negatives (sampled softmax), dropout 0")
+    if cfg == "c4":
+        return ("session-steps/sec, SMORL (SQN double-Q, 3 rewards) 1M items, dim128, batch 4096",
+                f"SMORL_trainer {N} items, dim{E}, seq_len<={L}, global batch {B * world} ({B}/GPU), sup head + "
+                f"Q heads acc/div/nov, topk_div=topk_nov=1, q_weights [1,1,1], gamma 0.5, alpha 1")
+    return ("session-steps/sec, IKEA-scale SMORL (SQN double-Q, 3 rewards) 5M items, dim256, batch 8192",
+            f"SMORL_trainer {N} items, dim{E}, seq_len<={L}, global batch {B * world} ({B}/GPU), fp16 item "
+            f"table (fp32 master + Adam), sup head + Q heads acc/div/nov, topk_div=topk_nov=1, "
+            f"q_weights [1,1,1], gamma 0.5, alpha 1")
+
+
+def side_line(cfg, args, dev, batches, tok, steps, warmup):
+    """A short line of another BASELINE config on one GPU, same stream and
+    device as the C2 line (C3: BidirGRU4Rec with 2048 sampled negatives,
+    configs[2]; C4: SMORL 3-reward double-Q, configs[3] at its global batch on
+    one GPU): value, step times, roofline and kernel times — no CPU leg."""
+    B, N, E, L = args.batch, args.items, args.dim, args.seq
+    tr = make_trainer(cfg, args, dev, False)
+    apply_stored_logits(tr, args.stored_logits)
+    tr.set_train()
+    dt, losses, kern, per_step = timed_run(tr, batches, warmup, steps, 1, True, cfg)
+    terms = LOGIT_TERMS.get(args.precision, 0)
+    roof = None
+    if cfg == "c3":
+        T = float(np.mean(tok[warmup:warmup + steps]))
+        roof = target_step(kern, T, B, args.negatives, E, 2 * E, 2, terms)
+        if roof:
+            roof["kernel"] = "gather + sampled_fwd"
+            roof["traffic"] = (pmc_traffic("c3:gather+sampled_fwd", "gather+sampled_fwd")
+                               if (B, args.negatives, E) == (4096, 2048, 128) and terms == 6 else None)
+    elif kern:
+        sup = tr.SMORL_1.sup_head_output
+        roof = head_roofline(kern, args.precision if sup.flash_terms(B) else "f32", B, N, E,
+                             zs=sup.stored_logits(), cfg=cfg)
+    scanned = top_scanned(tr)
+    del tr
+    torch.cuda.empty_cache()
+    metric, workload = describe(cfg, N, E, L, B, 1, args.negatives)
+    ps = np.array(per_step) * 1e3
+    return {"metric": metric, "workload": workload, "value": round(B * steps / dt, 2), "unit": "session-steps/sec",
+            "n_gpus": 1, "steps": steps, "warmup": warmup, "ms_per_step": round(dt / steps * 1e3, 3),
+            "step_ms": {"median": round(float(np.median(ps)), 3), "p10": round(float(np.percentile(ps, 10)), 3),
+                        "p90": round(float(np.percentile(ps, 90)), 3)},
+            "roofline": roof, "kernel_ms": kern, "loss_first_last": [round(losses[0], 5), round(losses[-1], 5)],
+            "top_scanned_rows": scanned}
 
 
 def pinned(b):
@@ -704,13 +845,22 @@ def main():
     target = None
     native = None
     parity_net = None
+    gpar = None
+    extra = None
     HF = E * (2 if args.config == "c3" else 1)
     terms = LOGIT_TERMS.get(args.precision, 0)
+    want_cpu = world == 1 and rank == 0 and not args.no_cpu_baseline
+    cpu_items, cpu_B, cpu_steps = cpu_sample(args, args.config)
+    # the loss-parity leg (C2): the CPU leg's sample is the first batches of THIS stream at the
+    # CPU leg's batch size, trained by the oracle and by a fresh copy of the benched GPU trainer
+    par_batches = None
+    if want_cpu and args.config == "c2" and cpu_items == N and (1 + cpu_steps) * cpu_B <= len(st):
+        par_batches = [st.batch(i, cpu_B) for i in range(1 + cpu_steps)]
     if args.config in ("c2", "c4", "c5"):
         if kern:
             sup = net.heads["output"] if net is not None else tr.SMORL_1.sup_head_output
             prec = args.precision if sup.flash_terms(B * world) else "f32"
-            roof = head_roofline(kern, prec, B * world, N // world, E, zs=sup.stored_logits())
+            roof = head_roofline(kern, prec, B * world, N // world, E, zs=sup.stored_logits(), cfg=args.config)
         if args.config == "c2":
             if world == 1 and not args.no_cpu_baseline and not args.no_eval and net is not None:
                 parity_net = net
@@ -753,48 +903,45 @@ def main():
                 if target is not None:
                     target["workload"] = f"GRU4Rec {N} items dim{E} batch {B}/GPU, {args.negatives} sampled negatives"
                     target["kernel_ms"] = k2
-                    # HBM bytes of the two kernels per step from the PMC passes (tools/pmc_ns.sh)
-                    pmc = os.path.join(HERE, "profiles", "pmc_traffic.json")
+                    # HBM bytes of the two kernels per step from the PMC passes (tools/pmc_ns.sh), which
+                    # measured the one-GPU kernels at these shapes
                     target["traffic"] = None
-                    if (os.path.exists(pmc) and (N, E, B, args.negatives) == (1_000_000, 128, 4096, 2048) and terms == 6
-                            and not shard):   # (the PMC passes measured the one-GPU kernels)
-                        t1 = json.load(open(pmc)).get("c2:gather+sampled_fwd:r04")
-                        target["traffic"] = None if t1 is None else int(t1) * world   # summed over ranks like the bytes
+                    if (N, E, B, args.negatives) == (1_000_000, 128, 4096, 2048) and terms == 6 and not shard:
+                        target["traffic"] = pmc_traffic("c2:gather+sampled_fwd", "gather+sampled_fwd")
                 del tr2
+                torch.cuda.empty_cache()
+            if par_batches is not None:
+                gpar = gpu_parity_run(args, dev, par_batches)
+            if world == 1 and args.extra_steps > 0:
+                # driver-visible C3 / C4 lines (BASELINE configs[2] / [3] on one GPU) on the same stream
+                extra = {}
+                wx = min(3, args.warmup)
+                nx = min(args.extra_steps, len(batches) - wx)
+                for c in ("c3", "c4"):
+                    extra[c] = side_line(c, args, dev, batches, tok, nx, wx)
     else:
         target = target_step(kern, T, B, args.negatives, E, HF, 2, terms)
         roof = dict(target) if target else None
         if roof:
             roof["kernel"] = "gather + sampled_fwd"
-            pmc = os.path.join(HERE, "profiles", "pmc_traffic.json")
             roof["traffic"] = None
-            if os.path.exists(pmc) and (B, args.negatives, HF) == (4096, 2048, 256) and terms == 6:
-                roof["traffic"] = json.load(open(pmc)).get("c3:gather+sampled_fwd:r04")
+            if (B, args.negatives, HF) == (4096, 2048, 256) and terms == 6:
+                roof["traffic"] = pmc_traffic("c3:gather+sampled_fwd", "gather+sampled_fwd")
     if rank != 0:
         if torch.distributed.is_initialized():
             torch.distributed.destroy_process_group()
         return
     cpu = None
-    if world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(args, args.config)
+    lparity = None
+    if want_cpu:
+        cpu = cpu_baseline(args, args.config, batches=par_batches, counts=args.item_counts)
+        orc_out = cpu.pop("_oracle", None)
+        if gpar is not None and orc_out is not None:
+            lparity = loss_parity(gpar[0], orc_out[0], gpar[1], orc_out[1].net.state_dict(), 0.01, cpu_B)
+        del orc_out
         if ev is not None and dev_idx is not None and parity_net is not None:
             cpu["hr_ndcg_parity"] = cpu_eval_parity(parity_net, held, dev_idx)
-    if args.config == "c2":
-        metric = "session-steps/sec at 1M items, dim128, batch 4096; HR@20/NDCG@20 parity"
-        workload = f"GRU4Rec {N} items, dim{E}, seq_len<={L}, batch {B}/GPU, full-softmax logits"
-    elif args.config == "c3":
-        metric = "session-steps/sec, BidirGRU4Rec 1M items, dim128, batch 4096, 2048 sampled negatives"
-        workload = (f"BidirGRU4Rec {N} items, dim{E}, seq_len<={L}, batch {B}, {args.negatives} shared uniform "
-                    f"negatives (sampled softmax), dropout 0")
-    elif args.config == "c4":
-        metric = "session-steps/sec, SMORL (SQN double-Q, 3 rewards) 1M items, dim128, batch 4096"
-        workload = (f"SMORL_trainer {N} items, dim{E}, seq_len<={L}, global batch {B * world} ({B}/GPU), sup head + "
-                    f"Q heads acc/div/nov, topk_div=topk_nov=1, q_weights [1,1,1], gamma 0.5, alpha 1")
-    else:
-        metric = "session-steps/sec, IKEA-scale SMORL (SQN double-Q, 3 rewards) 5M items, dim256, batch 8192"
-        workload = (f"SMORL_trainer {N} items, dim{E}, seq_len<={L}, global batch {B * world} ({B}/GPU), fp16 item "
-                    f"table (fp32 master + Adam), sup head + Q heads acc/div/nov, topk_div=topk_nov=1, "
-                    f"q_weights [1,1,1], gamma 0.5, alpha 1")
+    metric, workload = describe(args.config, N, E, L, B, world, args.negatives)
     ps = np.array(per_step) * 1e3
     line = {
         "metric": metric,
@@ -814,7 +961,7 @@ def main():
         "roofline": roof, "cpu_baseline": cpu, "north_star_target": target, "eval_heldout": ev,
         "harness": harness, "native_f32": native, "kernel_ms": kern,
         "loss_first_last": [round(losses[0], 5), round(losses[-1], 5)],
-        "top_scanned_rows": scanned,
+        "top_scanned_rows": scanned, "loss_parity": lparity, "configs_extra": extra,
     }
     os.write(json_fd, (json.dumps(line) + "\n").encode())
     if torch.distributed.is_initialized():

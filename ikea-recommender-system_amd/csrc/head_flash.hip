@@ -820,12 +820,16 @@ __global__ __launch_bounds__(64 * fl_nw(HF, 2)) void k_flash_dw(
     stage<ER, NW>(Hr + (int64_t)(C) * ER, SR, w, lane16);                      \
     if (w == 0 && lane < 16) blds16(rsrc_of(rowinfo + 64 * (C)), SI, lane16, 0); \
   } while (0)
-  if constexpr (ZL) {
-    FL_ISSUE_Z(0, sk0, si0);
-    if (w == 0 && lane < 16) blds16(rsrc_of(rowinfo + 64 * max(0, min(1, nch - 1))), si1, lane16, 0);
-  } else {
-    FL_ISSUE_K(0, sk0, si0);
-    FL_ISSUE_R(0, sr0);
+  // a part with no row chunks (nch == 0) reads nothing: every DMA below and in
+  // the loops indexes chunks 0 .. nch − 1 only
+  if (nch > 0) {
+    if constexpr (ZL) {
+      FL_ISSUE_Z(0, sk0, si0);
+      if (w == 0 && lane < 16) blds16(rsrc_of(rowinfo + 64 * min(1, nch - 1)), si1, lane16, 0);
+    } else {
+      FL_ISSUE_K(0, sk0, si0);
+      FL_ISSUE_R(0, sr0);
+    }
   }
   // this wave's 32 items of W as two 16-item B operands of S = h_c·Wᵀ
   bf16x8 wk[NS][2][3];
@@ -1861,7 +1865,8 @@ extern "C" int rg_flash_lse(const float* pm, const float* pl, int nsplit, const 
 
 extern "C" int rg_flash_rows(const float* lse, const int64_t* tgt, int64_t lo, int A, int B, void* rowinfo,
                              hipStream_t stream) {
-  if (B <= 0 || A <= 0 || !lse || !tgt || !rowinfo) return RG_ERR_ARG;
+  // records of 32-row chunks (ri_lse / ri_tgt): the fused head's batches are whole chunks
+  if (B <= 0 || A <= 0 || (B % 32) || !lse || !tgt || !rowinfo) return RG_ERR_ARG;
   hipLaunchKernelGGL(k_flash_rows, dim3((B + 255) / 256), dim3(256), 0, stream, lse, tgt, lo, A, B,
                      (float*)rowinfo);
   RG_LAUNCH_CHECK();

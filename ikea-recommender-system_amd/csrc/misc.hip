@@ -154,7 +154,10 @@ extern "C" int rg_qcomb(const float* const* W, const float* const* b, const floa
   return RG_OK;
 }
 
-extern "C" int rg_abi_version(void) { return 1; }
+// 2: the changes listed in INTEGRATION.md §3 (argument lists of rg_scatter_rows, rg_gather_neg,
+// rg_flash_amax_screen, rg_head_rows_gather, rg_rows_unslot, rg_rows_slot; rg_collect_grads
+// removed; rg_flash_rows' per-chunk record layout; the catch-up Adam entry points)
+extern "C" int rg_abi_version(void) { return 2; }
 
 // SMORL reward matrix r = stack([r_acc, r_div, r_nov], 1).to(float32)
 // (smorl_gru.py:311-314 with the third reward): f64 -> f32 per column.

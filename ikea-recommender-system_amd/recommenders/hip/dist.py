@@ -44,8 +44,24 @@ def _native_comm(dist, group, host_group, rank, world):
     dist.broadcast(uid, src=src, group=host_group)
     h = ctypes.c_void_p()
     call("rg_comm_init", uid.data_ptr(), world, rank, torch.cuda.current_device(), ctypes.addressof(h))
+    if not _NATIVE:
+        import atexit
+        atexit.register(destroy_native_comms)
     _NATIVE[key] = (pg, h.value)   # (the group is kept alive: its id stays unique)
     return h.value
+
+
+def destroy_native_comms():
+    """Free every communicator of the library's own RCCL path (rg_comm_destroy),
+    after the device has drained; registered with atexit by the first one and
+    safe to call earlier, e.g. before the process group is destroyed."""
+    from . import call
+    if not _NATIVE:
+        return
+    torch.cuda.synchronize()
+    for key in list(_NATIVE):
+        _, h = _NATIVE.pop(key)
+        call("rg_comm_destroy", h)
 
 
 class _Done:

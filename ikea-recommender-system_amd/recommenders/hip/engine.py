@@ -620,14 +620,23 @@ class _FlashWS:
         # uses them while they fit the free device memory (CMAX_FREE_MARGIN),
         # else the row-chunked screening argmax on this workspace's planes
         # (SoftmaxHead.top_entries)
+        # The view is taken per pass 1 (fetch_cmax) and dropped by its top_entries, so a workspace
+        # never pins an outgrown buffer.
         self.top1 = None
-        cm = _shared_cmax(device, -(-A // 32) * B, required=top_k > 1) if top_k >= 1 else None
-        if cm is not None:
-            self.cmax = cm.view(-(-A // 32), B)
-            self.cand = z(B, call("rg_flash_topk_cap"), dt=torch.int32)
-            self.ncand = z(B, dt=torch.int32)
-            self.tk_work = torch.empty(call("rg_flash_topk_work_bytes", B, A, top_k), dtype=torch.uint8,
-                                       device=device)
+        self.A, self.device = A, device
+        self.tk_work = None
+
+    def fetch_cmax(self):
+        """Before a pass 1 with top-k outputs: this pass's view of the shared
+        chunk-maxima buffer (None: K = 1 without room, top_entries screens)."""
+        A, B, K = self.A, self.B, self.top_k
+        cm = _shared_cmax(self.device, -(-A // 32) * B, required=K > 1) if K >= 1 else None
+        self.cmax = None if cm is None else cm.view(-(-A // 32), B)
+        if self.cmax is not None and self.tk_work is None:
+            self.cand = torch.empty(B, call("rg_flash_topk_cap"), dtype=torch.int32, device=self.device)
+            self.ncand = torch.empty(B, dtype=torch.int32, device=self.device)
+            self.tk_work = torch.empty(call("rg_flash_topk_work_bytes", B, A, K), dtype=torch.uint8,
+                                       device=self.device)
 
 
 # the chunk maxima of the fused heads' top-k (_FlashWS.cmax): one growing
@@ -645,8 +654,8 @@ def _shared_cmax(device, n, required):
     t = _CMAX.get(dev)
     if t is not None and t.numel() >= n:
         return t[:n]
-    have = 0 if t is None else t.numel() * 4
-    if not required and torch.cuda.mem_get_info(dev)[0] + have - 4 * n < CMAX_FREE_MARGIN:
+    # (the buffer being outgrown is not counted as reclaimable: a view of it may still be alive)
+    if not required and torch.cuda.mem_get_info(dev)[0] - 4 * n < CMAX_FREE_MARGIN:
         return None
     _CMAX.pop(dev, None)
     del t
@@ -944,6 +953,7 @@ class SoftmaxHead:
                 call("rg_head_planes", W, A, HF, w.Wk.data_ptr(), w.Wr.data_ptr(), b, w.bias_pad.data_ptr(), st)
                 w.wgen = self._wgen
             zs = self.zs_buffer(w)
+            w.fetch_cmax()
             # top-k outputs: the chunk maxima only (top_entries re-scores the candidate chunks; without
             # them K = 1 re-screens) — no per-split first maximum
             call("rg_flash_fwd_top", w.Hk.data_ptr(), w.Wk.data_ptr(), w.Wr.data_ptr(), w.bias_pad.data_ptr(), B, A,
@@ -982,6 +992,7 @@ class SoftmaxHead:
                      _f32(self.TOP_TOL_REL), w.h.data_ptr(), self._Wp.p.data_ptr(), self._bp.p.data_ptr(), self.HF,
                      w.cand.data_ptr(), w.ncand.data_ptr(), w.top_idx.data_ptr(), w.top_val.data_ptr(),
                      self.top_scanned.data_ptr(), w.tk_work.data_ptr(), st)
+            w.cmax = None   # (consumed: the shared buffer may be regrown before the next pass 1)
             return w.top_idx, w.top_val
         idx = torch.empty(B, K, dtype=torch.int32, device=self.device)
         vals = torch.empty(B, K, device=self.device)

@@ -139,7 +139,9 @@ int rg_head_fwd_x(const float* h, const float* W, const float* bias, int B, int 
  * rg_flash_lse: lse (natural units) over the splits; zt = the target logit
  *   when the target is one of items [lo, lo + A), 0 when another shard holds
  *   it, NaN when it lies outside [0, A_full) (CrossEntropyLoss raises there).
- * rg_flash_rows: row records (lse·log2 e, target − lo or -1), B × 8 bytes.
+ * rg_flash_rows: row records, B × 8 bytes, B % 32 == 0 (else RG_ERR_ARG): per 32-row chunk
+ *   c, 64 floats — the 32 rows' lse·log2 e, then their targets − lo (int32 bits; -1 outside
+ *   [0, A)).
  * rg_flash_dh: dh = gscale·(Σ_s 2^(m_s − lse)·O_s − W[target]) (B × HF).
  * rg_flash_dw_adam: pass 2 — dW = dZᵀ·h, db = Σ_b dZ, then Adam (adam6, host
  *   array) on W / bias / moments; with dW_out / db_out the raw gradients. */
@@ -563,7 +565,7 @@ int rg_comm_reduce_scatter(void* comm, const void* send, void* recv, int64_t n, 
 
 /* items per online-softmax partial block of rg_head_fwd: pmax/psum/parg hold ceil(A/that) x B */
 int rg_partial_block(void);
-int rg_abi_version(void);
+int rg_abi_version(void);   /* 2 (changes since 1) */
 /* Kernel-exact timing (bench.py): arm two hipEvent_t (created, timing-enabled) so the next
  * gather / one-launch sampled-logits kernel stamps them at its own start / end
  * (hipExtLaunchKernelGGL) and disarms them; NULL, NULL disarms.  Returns 1 when the previous

@@ -30,7 +30,7 @@ def test_library_loads_and_exports_every_declared_symbol():
     lib = load_library()
     for name in declared_symbols():
         assert hasattr(lib, name), name
-    assert lib.rg_abi_version() == 1
+    assert lib.rg_abi_version() == 2
 
 
 def test_argument_validation_without_gpu():

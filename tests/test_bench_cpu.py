@@ -92,3 +92,43 @@ def test_host_threads_reports_the_usable_cpus():
     assert 1 <= n <= how["affinity_cpus"]
     if how["cgroup_cpu_quota"]:
         assert n <= how["cgroup_cpu_quota"]
+
+
+def test_loss_parity_bars():
+    """The C2 line's loss_parity (GPU trainer vs the oracle on the same first
+    batches): the bars of tests/test_gpu_supervised.py."""
+    import torch
+    b = _bench()
+    sd = {"w": torch.zeros(1000), "b": torch.zeros(10)}
+    near = {"w": torch.zeros(1000), "b": torch.full((10,), 5e-5)}
+    ok = b.loss_parity([9.1, 9.2], [9.10005, 9.2], sd, near, 0.01, 4096)
+    assert ok["pass"] and ok["steps"] == 2 and ok["max_abs_dloss"] < 1e-4
+    assert ok["params"]["b"]["max_abs"] == pytest.approx(5e-5) and ok["params"]["b"]["frac_gt_1e-4"] == 0
+    assert not b.loss_parity([9.1], [9.1003], sd, near, 0.01, 4096)["pass"]
+    flip = {"w": torch.zeros(1000), "b": torch.zeros(10)}
+    flip["w"][:2] = 0.02   # two sign-like Adam flips of 2·lr in 1000 elements: 0.2 % > 0.1 %
+    assert not b.loss_parity([9.1], [9.1], sd, flip, 0.01, 4096)["pass"]
+
+
+def test_pmc_traffic_needs_the_measured_sources(tmp_path, monkeypatch):
+    """A PMC traffic entry counts only while its source hash matches the
+    current kernel sources (bench.py kernel_src_hash)."""
+    import json
+    b = _bench()
+    h = b.kernel_src_hash("head")
+    assert len(h) == 16 and h == b.kernel_src_hash("head") and h != b.kernel_src_hash("gather+sampled_fwd")
+    prof = tmp_path / "profiles"
+    prof.mkdir()
+    (prof / "pmc_traffic.json").write_text(json.dumps({
+        "head_fwd:f32x6d3:zs": {"bytes": 123, "src": h, "file": "x"},
+        "head_dw_adam:f32x6d3:zs": {"bytes": 456, "src": "0" * 16, "file": "y"},
+        "old": 789}))
+    csrc = tmp_path / "ikea-recommender-system_amd" / "csrc"
+    csrc.mkdir(parents=True)
+    for f in b.KERNEL_SRC["head"]:
+        (csrc / f).write_bytes(open(os.path.join(ROOT, "ikea-recommender-system_amd", "csrc", f), "rb").read())
+    monkeypatch.setattr(b, "HERE", str(tmp_path))
+    assert b.pmc_traffic("head_fwd:f32x6d3:zs", "head") == 123
+    assert b.pmc_traffic("head_dw_adam:f32x6d3:zs", "head") is None   # measured on other sources
+    assert b.pmc_traffic("old", "head") is None                       # unversioned entry
+    assert b.pmc_traffic("missing", "head") is None

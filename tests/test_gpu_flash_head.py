@@ -933,14 +933,14 @@ def test_top1_row_chunked_screening_matches_chunk_maxima(monkeypatch):
     W, b = torch.randn(A, HF, generator=g) * 0.3, torch.randn(A, generator=g) * 0.3
     _plant_top1_ties(h, W, b, h.double() @ W.double().t() + b.double())
     hd1, w1, i1, v1 = _head_top1(A, HF, h.to(dev), W.to(dev), b.to(dev))
-    assert w1.cmax is not None
+    assert w1.top1 is None   # the chunk-maxima path (its view is dropped after top_entries)
     # no room for the (shared) chunk maxima: the screening fallback, in 256-row chunks
     monkeypatch.setattr(engine, "CMAX_FREE_MARGIN", 1 << 62)
     monkeypatch.setattr(engine, "_CMAX", {})
     monkeypatch.setattr(engine, "SCREEN_CMAX_BYTES", 1)
     monkeypatch.setattr(engine, "SCREEN_ROW_CHUNK", 256)
     hd2, w2, i2, v2 = _head_top1(A, HF, h.to(dev), W.to(dev), b.to(dev))
-    assert w2.cmax is None and w2.top1.Bc == 256
+    assert w2.cmax is None and w2.top1 is not None and w2.top1.Bc == 256
     assert torch.equal(i1, i2) and torch.equal(v1, v2)
     Z = h.double() @ W.double().t() + b.double()
     first = (Z >= Z.max(1).values[:, None]).double().argmax(1)

@@ -56,9 +56,13 @@ def test_pack_stable_descending():
         assert int(offs[-1]) == B * L
 
 
-def test_gather_packed_and_reverse():
-    g = torch.Generator().manual_seed(1)
-    B, L, N, E = 33, 6, 100, 16
+@pytest.mark.parametrize("B,L,N,E", [(33, 6, 100, 16),
+                                     # k_gather_e's long / short sorted-row pairing (B % 4 == 0) and the
+                                     # general form (B % 4 != 0) at every table width it takes
+                                     (256, 50, 5000, 32), (252, 50, 5000, 64), (512, 50, 20000, 128),
+                                     (130, 40, 3000, 128), (96, 20, 2000, 256), (101, 20, 2000, 256)])
+def test_gather_packed_and_reverse(B, L, N, E):
+    g = torch.Generator().manual_seed(1 + B + E)
     s = torch.randint(0, N + 1, (B, L), generator=g)
     lens = torch.randint(1, L + 1, (B,), generator=g)
     emb = torch.randn(N + 1, E, generator=g)
