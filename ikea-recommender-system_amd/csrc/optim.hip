@@ -293,3 +293,148 @@ extern "C" int rg_adam_slabs(float* P, float* M, float* V, const float* slabs, i
   RG_LAUNCH_CHECK();
   return RG_OK;
 }
+
+// ---- catch-up ("lazy") Adam with the dense semantics, bit for bit --------
+// torch.optim.Adam moves EVERY row of a table every step (a row without a
+// gradient sees g = 0: m ← m + w1·(0 − m), v ← β2·v, p moves by −lr·m̂/(√v̂ + ε)),
+// and for a table read only a few rows at a time (the embedding; the sampled
+// head's targets and negatives) the eager sweep is 24 B of HBM traffic per
+// parameter and step for rows nobody reads.  Here a row's zero-gradient steps
+// are replayed only when it is next read: last[r] = the table steps already
+// applied to row r; hist[s − 1] = step s's six fp32 scalars (written by step
+// s's own rg_lazy_adam_rows).  A replayed step is adam_elem with a gradient of
+// runtime value 0 and that step's scalars — the same fp32 operations in the
+// same order as k_adam_rows4's untagged rows, so the table after any sequence
+// of reads equals the eager one bitwise (tests/test_gpu_lazy_adam.py).
+//
+// One wave per 64 rows: lane i tests row r0 + i, the wave then walks the
+// selected rows (ballot) and updates each row's cols values 64 lanes at a
+// time; a 1-column companion table (the bias of a head: Pb / Mb / Vb / Gb)
+// shares last[] and is updated by lane 0 of the same wave.
+struct LazyTab {
+  float* P;
+  float* M;
+  float* V;
+  float* G;        // adam: gradient rows (cleared after use)
+  __half* P16;     // optional fp16 copy of P (config C5's gather table)
+  float* Pb;       // optional 1-column companion (bias), same rows
+  float* Mb;
+  float* Vb;
+  float* Gb;
+  int cols;
+};
+
+__device__ __forceinline__ AdamArgs hist_args(const float* __restrict__ hist, int s) {
+  const float* h = hist + 6 * (int64_t)(s - 1);
+  return AdamArgs{h[0], h[1], h[2], h[3], h[4], h[5]};
+}
+
+// replay steps s0 .. s1 (inclusive) with g = zero, then (adam) one step with g
+__device__ __forceinline__ void lazy_elem(float* P, float* M, float* V, int64_t i, const float* __restrict__ hist,
+                                          int s0, int s1, float zero, bool step, float g, const AdamArgs& a) {
+  float p = P[i], m = M[i], v = V[i];
+  for (int s = s0; s <= s1; ++s) adam_elem(p, m, v, zero, hist_args(hist, s));
+  if (step) adam_elem(p, m, v, g, a);
+  P[i] = p;
+  M[i] = m;
+  V[i] = v;
+}
+
+// mode 0 (catch-up): rows with sel[r] == selv (sel NULL: every row) replay
+// last[r] + 1 .. n; mode 1 (adam step n): rows with sel[r] == selv replay
+// last[r] + 1 .. n − 1, then step n with their gradient (cleared); hist[n − 1] = a
+template <int MODE>
+__global__ __launch_bounds__(256) void k_lazy_rows(LazyTab t, const int32_t* __restrict__ sel, int32_t selv,
+                                                   int32_t* __restrict__ last, int64_t rows, int n,
+                                                   float* __restrict__ hist, AdamArgs a, float zero) {
+  const int lane = threadIdx.x & 63;
+  if (MODE == 1 && blockIdx.x == 0 && threadIdx.x == 0) {
+    float* h = hist + 6 * (int64_t)(n - 1);
+    h[0] = a.w1; h[1] = a.beta2; h[2] = a.c2; h[3] = a.bc2_sqrt; h[4] = a.eps; h[5] = a.neg_step;
+  }
+  const int64_t r0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 64;
+  if (r0 >= rows) return;
+  const int64_t rl = r0 + lane;
+  const bool hit = rl < rows && (sel == nullptr || sel[rl] == selv);
+  const int32_t lst = hit ? last[rl] : 0;
+  uint64_t mask = __ballot(hit && (MODE == 1 || lst < n));
+  while (mask) {
+    const int j = __builtin_ctzll(mask);
+    mask &= mask - 1;
+    const int64_t r = r0 + j;
+    const int s0 = __shfl(lst, j) + 1, s1 = MODE == 1 ? n - 1 : n;
+    const int64_t base = r * t.cols;
+    for (int c = lane; c < t.cols; c += 64) {
+      float g = 0.f;
+      if (MODE == 1) {
+        g = t.G[base + c];
+        t.G[base + c] = 0.f;
+      }
+      lazy_elem(t.P, t.M, t.V, base + c, hist, s0, s1, zero, MODE == 1, g, a);
+      if (t.P16) t.P16[base + c] = __float2half_rn(t.P[base + c]);
+    }
+    if (lane == 0) {
+      if (t.Pb) {
+        float gb = 0.f;
+        if (MODE == 1) {
+          gb = t.Gb[r];
+          t.Gb[r] = 0.f;
+        }
+        lazy_elem(t.Pb, t.Mb, t.Vb, r, hist, s0, s1, zero, MODE == 1, gb, a);
+      }
+      last[r] = n;
+    }
+  }
+}
+
+// need[id] = stamp for the n ids (int64) in [0, rows) and, with S > 0, the S
+// negatives of draw `counter` (draw_id over [0, rows), csrc/common.h)
+__global__ void k_lazy_mark(const int64_t* __restrict__ ids, int64_t n, int64_t rows, uint64_t seed,
+                            uint64_t counter, int S, int32_t* __restrict__ need, int32_t stamp) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) {
+    const int64_t id = ids[i];
+    if (id >= 0 && id < rows) need[id] = stamp;
+  } else if (i < n + S) {
+    need[draw_id(seed, counter, S, (int)(i - n), (uint64_t)rows)] = stamp;
+  }
+}
+
+static inline bool lazy_tab_ok(const LazyTab& t) {
+  return t.P && t.M && t.V && t.cols > 0 && (!t.Pb || (t.Mb && t.Vb));
+}
+
+static inline unsigned lazy_grid(int64_t rows) { return (unsigned)((rows + 255) / 256); }
+
+extern "C" int rg_lazy_mark_rows(const int64_t* ids, int64_t n, int64_t rows, uint64_t seed, uint64_t counter, int S,
+                                 int32_t* need, int32_t stamp, hipStream_t stream) {
+  if (n < 0 || S < 0 || rows <= 0 || !need || (n > 0 && !ids) || n + S == 0) return RG_ERR_ARG;
+  hipLaunchKernelGGL(k_lazy_mark, dim3((unsigned)((n + S + 255) / 256)), dim3(256), 0, stream, ids, n, rows, seed,
+                     counter, S, need, stamp);
+  RG_LAUNCH_CHECK();
+  return RG_OK;
+}
+
+extern "C" int rg_lazy_catch_up(float* P, float* M, float* V, int cols, uint16_t* P16, float* Pb, float* Mb, float* Vb,
+                                int64_t rows, int32_t* last, const int32_t* need, int32_t stamp, int32_t n_steps,
+                                float* hist, hipStream_t stream) {
+  const LazyTab t{P, M, V, nullptr, reinterpret_cast<__half*>(P16), Pb, Mb, Vb, nullptr, cols};
+  if (!lazy_tab_ok(t) || rows <= 0 || !last || n_steps < 0 || (n_steps > 0 && !hist)) return RG_ERR_ARG;
+  if (n_steps == 0) return RG_OK;
+  hipLaunchKernelGGL(k_lazy_rows<0>, dim3(lazy_grid(rows)), dim3(256), 0, stream, t, need, stamp, last, rows, n_steps,
+                     hist, AdamArgs{}, 0.f);
+  RG_LAUNCH_CHECK();
+  return RG_OK;
+}
+
+extern "C" int rg_lazy_adam_rows(float* P, float* M, float* V, float* G, int cols, uint16_t* P16, float* Pb, float* Mb,
+                                 float* Vb, float* Gb, int64_t rows, int32_t* last, const int32_t* tags, int32_t tag,
+                                 int32_t step, float* hist, const float* adam6, hipStream_t stream) {
+  const LazyTab t{P, M, V, G, reinterpret_cast<__half*>(P16), Pb, Mb, Vb, Gb, cols};
+  if (!lazy_tab_ok(t) || !G || (Pb && !Gb) || rows <= 0 || !last || !tags || step < 1 || !hist || !adam6)
+    return RG_ERR_ARG;
+  hipLaunchKernelGGL(k_lazy_rows<1>, dim3(lazy_grid(rows)), dim3(256), 0, stream, t, tags, tag, last, rows, step, hist,
+                     to_args(adam6), 0.f);
+  RG_LAUNCH_CHECK();
+  return RG_OK;
+}

@@ -140,6 +140,9 @@ SIGNATURES = {
     "rg_head_rows_gather": [P, I, I64, I64, P, P, I, I, P, P, P],
     "rg_rows_unslot": [P, I, P, P, I, I, P, P, P, P],
     "rg_rows_slot": [P, P, P, I, I, I, P, P],
+    "rg_lazy_mark_rows": [P, I64, I64, U64, U64, I, P, I32, P],
+    "rg_lazy_catch_up": [P, P, P, I, P, P, P, P, I64, P, P, I32, I32, P, P],
+    "rg_lazy_adam_rows": [P, P, P, P, I, P, P, P, P, P, I64, P, P, I32, I32, P, P, P],
 }
 
 _lib = None

@@ -120,6 +120,65 @@ def _round_up(x, m):
     return (x + m - 1) // m * m
 
 
+# ------------------------------------------------------- catch-up Adam ----
+# Tables read a few rows per step — the item embedding (the batch's tokens) and
+# the sampled head's W / b (targets and negatives) — take their zero-gradient
+# Adam steps only when a row is next read (csrc/optim.hip rg_lazy_*): bitwise
+# the reference's dense torch.optim.Adam (GRU4Rec/model.py:124-127,153; every
+# row moves every step), without the sweep over every row (C3: 1.6 of 3.7 ms).
+# False: the eager sweeps (rg_adam_rows), e.g. for A/B checks.
+LAZY_ADAM = True
+
+
+class LazyRows:
+    """Catch-up bookkeeping of one table (and an optional one-column
+    companion, a head's bias): last[r] = table steps applied to row r, hist
+    = every step's six Adam scalars (written by the step's own kernel), need /
+    stamp = the rows a read is about to touch.  ``tab``: (P, M, V, cols, P16,
+    Pb, Mb, Vb) device pointers / widths of the table."""
+
+    def __init__(self, rows, device):
+        self.rows = int(rows)
+        self.device = device
+        self.last = torch.zeros(self.rows, dtype=torch.int32, device=device)
+        self.need = torch.zeros(self.rows, dtype=torch.int32, device=device)
+        self.stamp = 0
+        self.n = 0        # table steps so far
+        self.full = 0     # n at the last catch-up of every row
+        self.hist = torch.zeros(256, 6, device=device)
+
+    def catch_up(self, tab, ids=None, n_ids=0, seed=0, counter=0, S=0):
+        """Bring the rows a read is about to touch — ``n_ids`` int64 ids at
+        ``ids`` (device) and the S negatives of draw ``counter`` — up to date."""
+        if self.n == self.full or n_ids + S == 0:
+            return
+        st = stream_ptr()
+        self.stamp += 1
+        call("rg_lazy_mark_rows", ids, n_ids, self.rows, seed, counter, S, self.need.data_ptr(), self.stamp, st)
+        call("rg_lazy_catch_up", *tab, self.rows, self.last.data_ptr(), self.need.data_ptr(), self.stamp, self.n,
+             self.hist.data_ptr(), st)
+
+    def materialize(self, tab):
+        """Every row up to date (before a read of the whole table: evaluation,
+        state_dict, the optimizer state, a load)."""
+        if self.n > self.full:
+            call("rg_lazy_catch_up", *tab, self.rows, self.last.data_ptr(), None, 0, self.n, self.hist.data_ptr(),
+                 stream_ptr())
+            self.full = self.n
+
+    def adam(self, tab, G, Gb, tags, tag, adam6):
+        """Table step n + 1 on the rows tagged ``tag`` (their gradient rows G / Gb)."""
+        n = self.n + 1
+        if n > self.hist.shape[0]:
+            grown = torch.zeros(2 * self.hist.shape[0], 6, device=self.device)
+            grown[:self.hist.shape[0]].copy_(self.hist)
+            self.hist = grown
+        P, M, V, cols, P16, Pb, Mb, Vb = tab
+        call("rg_lazy_adam_rows", P, M, V, G, cols, P16, Pb, Mb, Vb, Gb, self.rows, self.last.data_ptr(), tags, tag, n,
+             self.hist.data_ptr(), adam6, stream_ptr())
+        self.n = n
+
+
 # ---------------------------------------------------------------- trunk ----
 class SegScatter:
     """Deterministic row scatter-add (csrc/segsum.hip rg_scatter_rows: sort by
@@ -231,14 +290,27 @@ class Trunk:
         # keeps the fp32 master and refreshes it in the same sweep
         self.emb16 = torch.empty(self.n_local, E, dtype=torch.float16, device=device) if fp16_embeddings else None
         self.refresh_half()
+        # catch-up Adam of the table (one GPU; the row-sharded table keeps the eager sweep)
+        self.lazy = LazyRows(self.n_local, device) if LAZY_ADAM and comm is None else None
+
+    def _lazy_tab(self):
+        return (self.emb.p.data_ptr(), self.emb.m.data_ptr(), self.emb.v.data_ptr(), self.E,
+                None if self.emb16 is None else self.emb16.data_ptr(), None, None, None)
+
+    def materialize(self):
+        """Every row of the table up to date (catch-up Adam)."""
+        if self.lazy is not None:
+            self.lazy.materialize(self._lazy_tab())
 
     def refresh_half(self):
         """Re-derive the fp16 table from the fp32 master (init, load_state_dict)."""
         if self.emb16 is not None:
             call("rg_f32_to_f16", self.emb.p.data_ptr(), self.emb.numel(), self.emb16.data_ptr(), stream_ptr())
 
-    # parameters in reference registration order
+    # parameters in reference registration order (every row up to date: the
+    # callers read or write whole tables)
     def named_params(self):
+        self.materialize()
         return [self.emb] + self.gru_params
 
     def ws(self, slot, B, L, save):
@@ -274,6 +346,9 @@ class Trunk:
                 for d in range(self.ndir):
                     call("rg_place_rows", w.rows_in.data_ptr(), 1 if self.emb16 is not None else 0,
                          w.slot.data_ptr(), w.lsort.data_ptr(), w.offs.data_ptr(), B, E, d, w.X[d].data_ptr(), st)
+        if self.lazy is not None:   # the rows this pass reads (every position of s), caught up
+            s = s.contiguous()
+            self.lazy.catch_up(self._lazy_tab(), s.data_ptr(), B * L)
         # a sampled head's negatives row gather rides in the first gather launch
         # (rg_gather_neg; SampledSoftmaxHead.neg_job)
         job, self.neg_job = self.neg_job, None
@@ -470,7 +545,9 @@ class Trunk:
         row-sparse gradient rows tagged with this step's epoch."""
         st = stream_ptr()
         with region("adam_emb"):
-            if self.emb16 is not None:
+            if self.lazy is not None:   # only the rows with a gradient (catch-up Adam)
+                self.lazy.adam(self._lazy_tab(), self.G_emb.data_ptr(), None, self.tags.data_ptr(), tag, adam6)
+            elif self.emb16 is not None:
                 call("rg_adam_rows_h", self.emb.p.data_ptr(), self.emb.m.data_ptr(), self.emb.v.data_ptr(),
                      self.G_emb.data_ptr(), self.tags.data_ptr(), tag, self.n_local, self.E, adam6,
                      self.emb16.data_ptr(), st)
@@ -1329,12 +1406,58 @@ class SampledSoftmaxHead(SoftmaxHead):
         self.S = int(n_neg)
         self.seed = int(seed) & (2**64 - 1)
         self.draws = 0
-        self.G = torch.zeros_like(self.W.p)
-        self.Gb = torch.zeros_like(self.b.p)
+        self.G = torch.zeros_like(self._Wp.p)
+        self.Gb = torch.zeros_like(self._bp.p)
         self.tags = torch.zeros(self.A, dtype=torch.int32, device=device)
         self.tag = 0
         self.scatter = SegScatter(device)
         self._sws = {}
+        # catch-up Adam of W / b (one GPU; the item-sharded head keeps the eager sweeps): a
+        # step's targets and negatives are caught up before they are read (prepare_rows),
+        # every row before any other read — the W / b properties, named_params, evaluation
+        self.lazy = LazyRows(self.A, device) if LAZY_ADAM and shard is None else None
+        self._ready_draw = -1
+
+    # the step's own kernels use _Wp / _bp (their rows are caught up by
+    # prepare_rows); every other access goes through these properties
+    @property
+    def W(self):
+        self.materialize()
+        return SoftmaxHead.W.fget(self)
+
+    @W.setter
+    def W(self, v):
+        SoftmaxHead.W.fset(self, v)
+
+    @property
+    def b(self):
+        self.materialize()
+        return SoftmaxHead.b.fget(self)
+
+    @b.setter
+    def b(self, v):
+        SoftmaxHead.b.fset(self, v)
+
+    def params_ro(self):
+        self.materialize()
+        return SoftmaxHead.params_ro(self)
+
+    def _lazy_tab(self):
+        W, b = self._Wp, self._bp
+        return (W.p.data_ptr(), W.m.data_ptr(), W.v.data_ptr(), self.HF, None, b.p.data_ptr(), b.m.data_ptr(),
+                b.v.data_ptr())
+
+    def materialize(self):
+        lz = self.__dict__.get("lazy")
+        if lz is not None:
+            lz.materialize(self._lazy_tab())
+
+    def prepare_rows(self, tgt, B):
+        """Catch up the rows the next forward_loss reads: its B targets (device
+        int64) and the S negatives of draw ``self.draws``."""
+        if self.lazy is not None and self._ready_draw != self.draws:
+            self.lazy.catch_up(self._lazy_tab(), tgt.data_ptr(), B, self.seed, self.draws, self.S)
+            self._ready_draw = self.draws
 
     def split_terms(self, B):
         """bf16 terms of the forward for batch B (0: native fp32 MFMA)."""
@@ -1350,12 +1473,16 @@ class SampledSoftmaxHead(SoftmaxHead):
             self._sws[slot] = w
         return w
 
-    def neg_job(self, slot, B):
+    def neg_job(self, slot, B, tgt=None):
         """The negatives' row gather of the next forward_loss(slot, B), to run
         inside the trunk's embedding-gather launch (Trunk.neg_job ->
         rg_gather_neg): ids, biases, rows and their fragment-order bf16 planes
         of draw ``self.draws``.  None where the one-launch split logits do not
-        run (native fp32 forward)."""
+        run (native fp32 forward).  ``tgt``: the step's targets, whose rows (and
+        the negatives') are caught up here, before the trunk's gather launch
+        reads the negatives (catch-up Adam)."""
+        if tgt is not None:
+            self.prepare_rows(tgt, B)
         w = self.sws(slot, B)
         if w.terms == 0 or not w.zrow:
             return None
@@ -1367,7 +1494,7 @@ class SampledSoftmaxHead(SoftmaxHead):
         class _Job:
             @staticmethod
             def args():
-                return (head.W.p.data_ptr(), head.b.p.data_ptr(), head.seed, draw, head.A, head.S, head.HF,
+                return (head._Wp.p.data_ptr(), head._bp.p.data_ptr(), head.seed, draw, head.A, head.S, head.HF,
                         w.ids.data_ptr(), w.Wg.data_ptr(), w.bg.data_ptr(), w.Wp.data_ptr(), wfmt)
 
             @staticmethod
@@ -1382,18 +1509,20 @@ class SampledSoftmaxHead(SoftmaxHead):
         gather launch already gathered this draw's negatives (neg_job), the
         logits read their planes (draw = 2)."""
         B = h.shape[0]
+        self.prepare_rows(tgt, B)   # (a no-op when neg_job already did it for this draw)
         w = self.sws(slot, B)
         st = stream_ptr()
         g = _f32(1.0 / B)
         split = w.terms != 0
         pre = w.pre_draw == self.draws
+        W, bb = (self._Wp, self._bp) if self.lazy is not None else (self.W, self.b)
         w.pre_draw = -1
         # the negatives' row gather is part of the timed logits step (or of the
         # gather launch, pre); with the one-launch kernel the region is kernel-exact
         with region("sampled_fwd", exact=bool(split and w.zrow)):
             if split and w.zrow:  # one launch: [draw, row gather, operand split,] logits, partials
                 hp = h_planes.data_ptr() if h_planes is not None else None
-                call("rg_sampled_logits", h.data_ptr(), self.W.p.data_ptr(), self.b.p.data_ptr(), w.ids.data_ptr(),
+                call("rg_sampled_logits", h.data_ptr(), W.p.data_ptr(), bb.p.data_ptr(), w.ids.data_ptr(),
                      (3 if w.pre_fmt else 2) if pre else 1, self.seed, self.draws, self.A, B, self.S, self.HF, w.terms, w.ZT.data_ptr(),
                      w.ldz, w.pmax.data_ptr(), w.psum.data_ptr(), w.Wg.data_ptr(), w.bg.data_ptr(), hp,
                      w.Wp.data_ptr() if pre else None, st)
@@ -1401,23 +1530,23 @@ class SampledSoftmaxHead(SoftmaxHead):
                 if w.work is None:
                     w.work = torch.empty(call("rg_sampled_work_bytes", B, self.S, self.HF), dtype=torch.uint8,
                                          device=self.device)
-                call("rg_sampled_fwd_x", h.data_ptr(), self.W.p.data_ptr(), self.b.p.data_ptr(), w.ids.data_ptr(),
+                call("rg_sampled_fwd_x", h.data_ptr(), W.p.data_ptr(), bb.p.data_ptr(), w.ids.data_ptr(),
                      1, self.seed, self.draws, self.A, B, self.S, self.HF, w.terms,
                      w.ZT.data_ptr(), w.ldz, w.pmax.data_ptr(), w.psum.data_ptr(), w.Wg.data_ptr(),
                      w.bg.data_ptr(), w.work.data_ptr(), st)
             else:
                 call("rg_sample_uniform", self.seed, self.draws, self.S, self.A, w.ids.data_ptr(), st)
-                call("rg_sampled_fwd", h.data_ptr(), self.W.p.data_ptr(), self.b.p.data_ptr(), w.ids.data_ptr(),
+                call("rg_sampled_fwd", h.data_ptr(), W.p.data_ptr(), bb.p.data_ptr(), w.ids.data_ptr(),
                      B, self.S, self.HF, w.ZT.data_ptr(), w.ldz, w.pmax.data_ptr(), w.psum.data_ptr(),
                      w.Wg.data_ptr(), w.bg.data_ptr(), st)
         self.draws += 1
         if self.loss == "bpr":   # w.lse holds z_pos for the backward
-            call("rg_bpr_rows", h.data_ptr(), self.W.p.data_ptr(), self.b.p.data_ptr(), tgt.data_ptr(), B, self.A,
+            call("rg_bpr_rows", h.data_ptr(), W.p.data_ptr(), bb.p.data_ptr(), tgt.data_ptr(), B, self.A,
                  self.HF, w.ZT.data_ptr(), w.zs_b, w.zs_s, self.S, g, w.lse.data_ptr(), w.loss_row.data_ptr(),
                  w.ids.data_ptr() + 4 * self.S, w.gb.data_ptr() + 4 * self.S,
                  w.grows.data_ptr() + 4 * self.S * self.HF, w.dh_slabs.data_ptr(), st)
         else:
-            call("rg_sampled_lse", h.data_ptr(), self.W.p.data_ptr(), self.b.p.data_ptr(), tgt.data_ptr(), B,
+            call("rg_sampled_lse", h.data_ptr(), W.p.data_ptr(), bb.p.data_ptr(), tgt.data_ptr(), B,
                  self.A, self.HF, w.pmax.data_ptr(), w.psum.data_ptr(), w.nT, g, w.lse.data_ptr(),
                  w.loss_row.data_ptr(), w.ids.data_ptr() + 4 * self.S, w.gb.data_ptr() + 4 * self.S,
                  w.grows.data_ptr() + 4 * self.S * self.HF, w.dh_slabs.data_ptr(), st)
@@ -1457,6 +1586,10 @@ class SampledSoftmaxHead(SoftmaxHead):
             self.scatter(w.ids.data_ptr(), w.gb.data_ptr(), 1, w.nrows.data_ptr(), S + B, -1, self.Gb.data_ptr(),
                          self.A, self.tags.data_ptr(), self.tag, st, reuse_sort=True)
         with region("sampled_adam"):
+            if self.lazy is not None:   # the touched rows only (catch-up Adam)
+                self.lazy.adam(self._lazy_tab(), self.G.data_ptr(), self.Gb.data_ptr(), self.tags.data_ptr(),
+                               self.tag, adam6)
+                return
             call("rg_adam_rows", self.W.p.data_ptr(), self.W.m.data_ptr(), self.W.v.data_ptr(), self.G.data_ptr(),
                  self.tags.data_ptr(), self.tag, self.A, HF, adam6, st)
             call("rg_adam_rows", self.b.p.data_ptr(), self.b.m.data_ptr(), self.b.v.data_ptr(), self.Gb.data_ptr(),
@@ -1489,7 +1622,7 @@ class ShardedSampledHead(SampledSoftmaxHead):
         super().__init__(name, A, HF, device, n_neg, seed, loss, shard=shard)
         self.comm = comm
 
-    def neg_job(self, slot, B):
+    def neg_job(self, slot, B, tgt=None):
         return None   # the negatives' rows come from their owners (forward_loss)
 
     def sws(self, slot, B):

@@ -38,7 +38,8 @@ def supervised_step(net: SupervisedNet, clock, s, a, true_len, host=None):
     a = a.to(dev, non_blocking=True)
     head = next(iter(net.heads.values()))
     # sampled head: its negatives' row gather joins the embedding-gather launch
-    net.trunk.neg_job = head.neg_job("main", s.shape[0]) if hasattr(head, "neg_job") else None
+    # (and, catch-up Adam, the step's target and negative rows are brought up to date first)
+    net.trunk.neg_job = head.neg_job("main", s.shape[0], tgt=a) if hasattr(head, "neg_job") else None
     h = net.trunk.forward(s, true_len, slot="main", save=True)
     B = h.shape[0]
     mask = None

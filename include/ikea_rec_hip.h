@@ -294,6 +294,26 @@ int rg_adam_dense(float* P, float* M, float* V, float* G, int64_t n, const float
  * untagged rows take g = 0 (moments still decay, p still moves). */
 int rg_adam_rows(float* P, float* M, float* V, float* G, const int32_t* tags, int32_t tag, int64_t rows, int cols,
                  const float* adam6, rg_stream_t stream);
+/* Catch-up Adam (dense semantics, bitwise): a table read a few rows at a time (the
+ * embedding, the sampled head) keeps last[r] = table steps applied to row r and hist (float[6] per
+ * step, step s at 6·(s − 1)) = every step's adam6; a row's zero-gradient steps are replayed only
+ * before it is read.  Replaces rg_adam_rows' sweep over every row (GRU4Rec/model.py:124-127,153).
+ * rg_lazy_mark_rows: need[id] = stamp for the n int64 ids in [0, rows) and, with S > 0, the S
+ *   negatives of draw `counter` (rg_sample_uniform's stream over [0, rows)).
+ * rg_lazy_catch_up: rows with need[r] == stamp (need NULL: every row) replay steps
+ *   last[r] + 1 .. n_steps with g = 0; P16 (optional) = fp16(P) of those rows; Pb / Mb / Vb
+ *   (optional): a one-column companion table (a head's bias) sharing last[].
+ * rg_lazy_adam_rows: table step `step` (hist[step − 1] = adam6): rows with tags[r] == tag replay
+ *   last[r] + 1 .. step − 1, then step with their gradient rows G (Gb), cleared; last[r] = step.
+ *   Rows without a gradient are not touched. */
+int rg_lazy_mark_rows(const int64_t* ids, int64_t n, int64_t rows, uint64_t seed, uint64_t counter, int S,
+                      int32_t* need, int32_t stamp, rg_stream_t stream);
+int rg_lazy_catch_up(float* P, float* M, float* V, int cols, uint16_t* P16, float* Pb, float* Mb, float* Vb,
+                     int64_t rows, int32_t* last, const int32_t* need, int32_t stamp, int32_t n_steps, float* hist,
+                     rg_stream_t stream);
+int rg_lazy_adam_rows(float* P, float* M, float* V, float* G, int cols, uint16_t* P16, float* Pb, float* Mb, float* Vb,
+                      float* Gb, int64_t rows, int32_t* last, const int32_t* tags, int32_t tag, int32_t step,
+                      float* hist, const float* adam6, rg_stream_t stream);
 /* split-K weight-gradient slabs summed in order, then Adam (or g_out). */
 int rg_adam_slabs(float* P, float* M, float* V, const float* slabs, int nslab, int64_t n, const float* adam6,
                   float* g_out, rg_stream_t stream);
