@@ -87,8 +87,13 @@ struct AdamArgs {
   float neg_step;  // -lr / (1 - beta1^t)
 };
 
+// Every rounding is explicit (fp contraction off; lerp as ATen's vectorised
+// fmadd), so the update is the same fp32 sequence in every kernel that inlines
+// it — the eager sweeps, the fused head epilogues and the catch-up Adam's
+// replays (csrc/optim.hip rg_lazy_*), which must agree bit for bit.
 __device__ __forceinline__ void adam_elem(float& p, float& m, float& v, float g, const AdamArgs& a) {
-  m = m + a.w1 * (g - m);
+#pragma clang fp contract(off)
+  m = __builtin_fmaf(a.w1, g - m, m);
   v = v * a.beta2;
   v = v + a.c2 * g * g;
   const float denom = sqrtf(v) / a.bc2_sqrt + a.eps;

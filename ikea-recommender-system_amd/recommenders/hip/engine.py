@@ -147,14 +147,19 @@ class LazyRows:
         self.full = 0     # n at the last catch-up of every row
         self.hist = torch.zeros(256, 6, device=device)
 
-    def catch_up(self, tab, ids=None, n_ids=0, seed=0, counter=0, S=0):
+    def catch_up(self, tab, ids=None, n_ids=0, seed=0, counter=0, S=0, more=()):
         """Bring the rows a read is about to touch — ``n_ids`` int64 ids at
-        ``ids`` (device) and the S negatives of draw ``counter`` — up to date."""
-        if self.n == self.full or n_ids + S == 0:
+        ``ids`` (device), the S negatives of draw ``counter`` and the (ptr, n)
+        id sets of ``more`` — up to date.  On the stream every read of the
+        table is ordered behind (two streams must not catch up one table
+        concurrently: the double-Q step catches up all its passes' rows first)."""
+        if self.n == self.full or n_ids + S + sum(n for _, n in more) == 0:
             return
         st = stream_ptr()
         self.stamp += 1
-        call("rg_lazy_mark_rows", ids, n_ids, self.rows, seed, counter, S, self.need.data_ptr(), self.stamp, st)
+        for p, n, sd, cn, ns in [(ids, n_ids, seed, counter, S)] + [(p, n, 0, 0, 0) for p, n in more]:
+            if n + ns:
+                call("rg_lazy_mark_rows", p, n, self.rows, sd, cn, ns, self.need.data_ptr(), self.stamp, st)
         call("rg_lazy_catch_up", *tab, self.rows, self.last.data_ptr(), self.need.data_ptr(), self.stamp, self.n,
              self.hist.data_ptr(), st)
 
@@ -302,6 +307,16 @@ class Trunk:
         if self.lazy is not None:
             self.lazy.materialize(self._lazy_tab())
 
+    def catch_up_rows(self, *states):
+        """Catch up every row the trunk passes over ``states`` (device int64
+        (B, L) tensors) will read, on the current stream — for passes that then
+        run on other streams (forward(..., catch_up=False))."""
+        if self.lazy is not None and states:
+            sts = [x.contiguous() for x in states]
+            self._keep = sts   # (alive until the kernels reading them have run: the next call replaces it)
+            self.lazy.catch_up(self._lazy_tab(), sts[0].data_ptr(), sts[0].numel(),
+                               more=[(x.data_ptr(), x.numel()) for x in sts[1:]])
+
     def refresh_half(self):
         """Re-derive the fp16 table from the fp32 master (init, load_state_dict)."""
         if self.emb16 is not None:
@@ -324,7 +339,7 @@ class Trunk:
             self._ws[key] = w
         return w
 
-    def forward(self, s, lens, slot="main", save=False, route=None):
+    def forward(self, s, lens, slot="main", save=False, route=None, catch_up=True):
         """s: int64 (B, L) device; lens: int64 (B,) device or CPU. Returns h (B, ndir*H).
         route (item-sharded table): this pass's (send_splits, recv_splits) from
         the host batch (dist.host_routes); None routes on the device and reads
@@ -346,7 +361,7 @@ class Trunk:
                 for d in range(self.ndir):
                     call("rg_place_rows", w.rows_in.data_ptr(), 1 if self.emb16 is not None else 0,
                          w.slot.data_ptr(), w.lsort.data_ptr(), w.offs.data_ptr(), B, E, d, w.X[d].data_ptr(), st)
-        if self.lazy is not None:   # the rows this pass reads (every position of s), caught up
+        if self.lazy is not None and catch_up:   # the rows this pass reads (every position of s), caught up
             s = s.contiguous()
             self.lazy.catch_up(self._lazy_tab(), s.data_ptr(), B * L)
         # a sampled head's negatives row gather rides in the first gather launch

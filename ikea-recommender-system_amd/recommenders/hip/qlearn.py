@@ -147,6 +147,9 @@ def q_side_stream(net):
 # the screening argmax, Q_boot(s', a*)) on its own stream beside the main
 # state's forward and the supervised head's pass 1, joined before the TD loss
 TARGET_SIDE_STREAM = True
+# ... started only after the previous step's supervised pass 2 (either net's): the target's
+# kernels then share the CUs with the main state's forward and pass 1, not with pass 2
+TARGET_AFTER_PASS2 = False
 
 
 def target_stream(net):
@@ -201,11 +204,16 @@ def double_q_step(nets, clocks, k, s, a, r, s_next, true_len, true_next_len, is_
     st = stream_ptr()
     cur = torch.cuda.current_stream(dev)
 
+    # catch-up Adam: every embedding row the three trunk passes read is brought up to
+    # date here, on the current stream, before the target pass forks onto its own
+    main.trunk.catch_up_rows(s, s_next)
+    boot.trunk.catch_up_rows(s_next)
+
     def target():
         with region("sqn_target"):
-            h_n = main.trunk.forward(s_next, true_next_len, slot="next", save=False)
+            h_n = main.trunk.forward(s_next, true_next_len, slot="next", save=False, catch_up=False)
             a_star = main.argmax_q(h_n, None if smorl is None else smorl["w"])
-            h_b = boot.trunk.forward(s_next, true_len, slot="boot", save=False)   # quirk: true_len
+            h_b = boot.trunk.forward(s_next, true_len, slot="boot", save=False, catch_up=False)   # quirk: true_len
             return boot.gather_q(h_b, idx32=a_star, out=main.buf("qn", (B, nh)))
 
     # the double-Q target needs neither the supervised head nor its workspace
@@ -217,10 +225,15 @@ def double_q_step(nets, clocks, k, s, a, r, s_next, true_len, true_next_len, is_
     ts = target_stream(main) if TARGET_SIDE_STREAM else None
     if ts is not None:
         ts.wait_stream(cur)
+        if TARGET_AFTER_PASS2:
+            for net in nets:
+                hd = net.sup_head_output
+                if not getattr(hd, "_joined", True):
+                    ts.wait_stream(hd._side)
         with torch.cuda.stream(ts):
             qn = target()
     with region("sqn_trunk_main"):
-        h = main.trunk.forward(s, true_len, slot="main", save=True)
+        h = main.trunk.forward(s, true_len, slot="main", save=True, catch_up=False)
     if ts is None:
         qn = target()
     sup_loss, _ = main.sup_head_output.forward_loss(h, a, slot="main")
