@@ -147,9 +147,9 @@ def q_side_stream(net):
 # the screening argmax, Q_boot(s', a*)) on its own stream beside the main
 # state's forward and the supervised head's pass 1, joined before the TD loss
 TARGET_SIDE_STREAM = True
-# ... started only after the previous step's supervised pass 2 (either net's): the target's
-# kernels then share the CUs with the main state's forward and pass 1, not with pass 2
-TARGET_AFTER_PASS2 = False
+# (round 6: starting it only after the previous step's pass 2, so that it shares the CUs with
+# pass 1 instead, measured 214.5K vs 215.1K session-steps/s at C4 — not kept,
+# profiles/r07/ab_c4_target_after_pass2.txt)
 
 
 def target_stream(net):
@@ -225,11 +225,6 @@ def double_q_step(nets, clocks, k, s, a, r, s_next, true_len, true_next_len, is_
     ts = target_stream(main) if TARGET_SIDE_STREAM else None
     if ts is not None:
         ts.wait_stream(cur)
-        if TARGET_AFTER_PASS2:
-            for net in nets:
-                hd = net.sup_head_output
-                if not getattr(hd, "_joined", True):
-                    ts.wait_stream(hd._side)
         with torch.cuda.stream(ts):
             qn = target()
     with region("sqn_trunk_main"):
