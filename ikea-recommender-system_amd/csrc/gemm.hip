@@ -409,3 +409,270 @@ extern "C" int rg_wgrad(const float* G, int M, const float* X, int N, int T_max,
   RG_LAUNCH_CHECK();
   return RG_OK;
 }
+
+// ---------------------------------------------------------------------------
+// Split-bf16 forms of the trunk's GEMMs (precision f32x6 / f32x6d3 / f32x9:
+// the trainers' matmul_precision; "f32" keeps the fp32 MFMA kernels above).
+// Every fp32 operand is split exactly into three bf16 planes while it is
+// staged into LDS (common.h split3x8's RNE split), and each 16 × 16 output
+// tile takes the plane products a_p·b_q with p + q <= 2 (NT = 6) or all nine
+// (NT = 9) on v_mfma_f32_16x16x32_bf16 with fp32 accumulation — the fused
+// head's arithmetic (the dropped products are below fp32's unit
+// roundoff), at 1024 bf16 FLOP per SIMD-cycle instead of the fp32 MFMA's 64.
+//
+// LDS planes: [plane][row][32 k + 8 pad] bf16 (80-B rows: the sixteen rows
+// one 16-lane group reads with ds_read_b128 fall on 16 distinct 4-bank groups).
+constexpr int GX_T = 128, GX_K = 32, GX_RS = GX_K + 8;   // tile rows, k per stage, bf16 per LDS row
+
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ void split3x4(const f4& x, bf16x4& p0, bf16x4& p1, bf16x4& p2) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const __bf16 b0 = (__bf16)x[i];
+    const float r1 = x[i] - (float)b0;
+    const __bf16 b1 = (__bf16)r1;
+    p0[i] = b0;
+    p1[i] = b1;
+    p2[i] = (__bf16)(r1 - (float)b1);
+  }
+}
+
+// acc (16 × 16 tiles of a wave's 64 × 64 block) += A_tile · B_tileᵀ over one
+// 32-deep stage: fragments straight from the LDS planes
+template <int NT>
+__device__ __forceinline__ void gx_stage_mfma(const __bf16* __restrict__ ap, const __bf16* __restrict__ bp, int wm,
+                                              int wn, int lane, f4 (&acc)[4][4]) {
+  constexpr int PL = GX_T * GX_RS;   // bf16 per plane
+  const int r = lane & 15, kg = lane >> 4;
+  bf16x8 b[4][3];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int p = 0; p < 3; ++p)
+      b[j][p] = *reinterpret_cast<const bf16x8*>(bp + p * PL + (wn * 64 + 16 * j + r) * GX_RS + 8 * kg);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    bf16x8 a[3];
+#pragma unroll
+    for (int p = 0; p < 3; ++p)
+      a[p] = *reinterpret_cast<const bf16x8*>(ap + p * PL + (wm * 64 + 16 * i + r) * GX_RS + 8 * kg);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = mfma16_split<NT>(a[0], a[1], a[2], b[j][0], b[j][1], b[j][2], acc[i][j]);
+  }
+}
+
+// C = A · Bᵀ (+ bias): A (M × K) k-contiguous, B (N × K) k-contiguous
+// (B_KCONTIG) or (K × N) n-contiguous; K % 32 == 0; M may come from the
+// device.  128 × 128 tile per 256-thread workgroup, two per CU (one 60 KB
+// plane stage each; the next stage's fp32 pieces are prefetched into
+// registers under this stage's MFMAs).
+template <int NT, bool B_KCONTIG>
+__global__ __launch_bounds__(256, 2) void k_gemm_x6(const float* __restrict__ A, int64_t lda,
+                                                    const float* __restrict__ Bm, int64_t ldb,
+                                                    float* __restrict__ C, int64_t ldc, const float* __restrict__ bias,
+                                                    int M_, const int32_t* __restrict__ Mptr, int N, int K) {
+  constexpr int PL = GX_T * GX_RS;
+  __shared__ __attribute__((aligned(16))) __bf16 As[3 * PL];
+  __shared__ __attribute__((aligned(16))) __bf16 Bs[3 * PL];
+  const int M = Mptr ? *Mptr : M_;
+  const int m0 = blockIdx.y * GX_T, n0 = blockIdx.x * GX_T;
+  if (m0 >= M) return;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, wm = w >> 1, wn = w & 1;
+  // this thread's four 16-B pieces of each stage (rows clamped: rows past M /
+  // columns past N compute values that are never stored)
+  // (B n-contiguous: thread = column n0 + (tid & 127), k = 16·(tid >> 7) .. +15
+  // of the stage, one coalesced 4-B load per k, written as whole 16-B k-runs)
+  const float* ap[4];
+  const float* bq[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int e = tid + 256 * q;
+    ap[q] = A + (int64_t)min(m0 + (e >> 3), M - 1) * lda + 4 * (e & 7);
+    if (B_KCONTIG) bq[q] = Bm + (int64_t)min(n0 + (e >> 3), N - 1) * ldb + 4 * (e & 7);
+  }
+  const float* bcol = Bm + min(n0 + (tid & 127), N - 1) + (int64_t)(16 * (tid >> 7)) * ldb;
+  f4 ra[4], rb[4];
+  auto load = [&](int k0) __attribute__((always_inline)) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      ra[q] = *reinterpret_cast<const f4*>(ap[q] + k0);
+      if (B_KCONTIG) {
+        rb[q] = *reinterpret_cast<const f4*>(bq[q] + k0);
+      } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) rb[q][i] = bcol[(int64_t)(k0 + 4 * q + i) * ldb];
+      }
+    }
+  };
+  auto store = [&]() __attribute__((always_inline)) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int e = tid + 256 * q;
+      bf16x4 p0, p1, p2;
+      split3x4(ra[q], p0, p1, p2);
+      const int ao = (e >> 3) * GX_RS + 4 * (e & 7);
+      *reinterpret_cast<bf16x4*>(&As[ao]) = p0;
+      *reinterpret_cast<bf16x4*>(&As[PL + ao]) = p1;
+      *reinterpret_cast<bf16x4*>(&As[2 * PL + ao]) = p2;
+      split3x4(rb[q], p0, p1, p2);
+      // (n-contiguous B: this thread's k-run 16·(tid >> 7) + 4q .. +3 of column tid & 127)
+      const int bo = B_KCONTIG ? ao : (tid & 127) * GX_RS + 16 * (tid >> 7) + 4 * q;
+      *reinterpret_cast<bf16x4*>(&Bs[bo]) = p0;
+      *reinterpret_cast<bf16x4*>(&Bs[PL + bo]) = p1;
+      *reinterpret_cast<bf16x4*>(&Bs[2 * PL + bo]) = p2;
+    }
+  };
+  f4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+  load(0);
+  for (int k0 = 0; k0 < K; k0 += GX_K) {
+    store();
+    __syncthreads();
+    if (k0 + GX_K < K) load(k0 + GX_K);
+    gx_stage_mfma<NT>(As, Bs, wm, wn, lane, acc);
+    __syncthreads();
+  }
+  const int r = lane & 15, kg = lane >> 4;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int col = n0 + wn * 64 + 16 * j + r;
+    if (col >= N) continue;
+    const float bv = bias ? bias[col] : 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int row = m0 + wm * 64 + 16 * i + 4 * kg + u;
+        if (row < M) C[(int64_t)row * ldc + col] = acc[i][j][u] + bv;
+      }
+  }
+}
+
+extern "C" int rg_gemm_x6(const float* A, int64_t lda, const float* B, int64_t ldb, int b_kcontig, float* C,
+                          int64_t ldc, const float* bias, int M, const int32_t* Mptr, int N, int K, int terms,
+                          hipStream_t stream) {
+  if (M <= 0 || N < 4 || K <= 0 || K % GX_K || N % 4 || lda % 4 || ldb % 4 || ldc < N || (terms != 6 && terms != 9))
+    return RG_ERR_ARG;
+  if (((reinterpret_cast<uintptr_t>(A) | reinterpret_cast<uintptr_t>(B)) & 15) != 0) return RG_ERR_ARG;
+  const dim3 grid((N + GX_T - 1) / GX_T, (M + GX_T - 1) / GX_T);
+#define GX(NTV, BK)                                                                                        \
+  hipLaunchKernelGGL((k_gemm_x6<NTV, BK>), grid, dim3(256), 0, stream, A, lda, B, ldb, C, ldc, bias, M, Mptr, N, K)
+  if (terms == 6) {
+    if (b_kcontig) GX(6, true);
+    else GX(6, false);
+  } else {
+    if (b_kcontig) GX(9, true);
+    else GX(9, false);
+  }
+#undef GX
+  RG_LAUNCH_CHECK();
+  return RG_OK;
+}
+
+// Split-bf16 weight gradient over packed tokens (rg_wgrad's contract):
+// dW[m][n] = Σ_t G[t][m]·X[t][n] and db[m] = Σ_t G[t][m] into token-split
+// slabs.  Workgroup = 128 m × 128 n (N = 256: two column tiles, grid.x) over
+// one token split; k = tokens, 32 per stage: G's and X's fp32 rows are read
+// coalesced and written transposed into the [m][t] / [n][t] planes.
+template <int NT>
+__global__ __launch_bounds__(256, 2) void k_wgrad_x6(const float* __restrict__ G, int M, const float* __restrict__ X,
+                                                     int N, const int32_t* __restrict__ Tptr,
+                                                     float* __restrict__ dw_slabs, float* __restrict__ db_slabs) {
+  constexpr int PL = GX_T * GX_RS;
+  __shared__ __attribute__((aligned(16))) __bf16 As[3 * PL];
+  __shared__ __attribute__((aligned(16))) __bf16 Bs[3 * PL];
+  __shared__ float csum[2][GX_T];
+  const int T = *Tptr;
+  const int ntile_m = (M + GX_T - 1) / GX_T;
+  const int mt = blockIdx.x % ntile_m, nt = blockIdx.x / ntile_m;
+  const int m0 = mt * GX_T, n0 = nt * GX_T;
+  const int tchunk = ((T + (int)gridDim.y - 1) / (int)gridDim.y + GX_K - 1) / GX_K * GX_K;
+  const int t0 = blockIdx.y * tchunk, t1 = min(T, t0 + tchunk);
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, wm = w >> 1, wn = w & 1;
+  // staging: thread = column c = tid & 127 of the G tile (m0 + c) and of the X
+  // tile (n0 + c), tokens 16·(tid >> 7) .. +15 of the stage: one coalesced 4-B
+  // load per token and operand, the 16 values written as whole 16-B runs of k
+  const int c = tid & 127, tg = 16 * (tid >> 7);
+  const float* gcol = G + min(m0 + c, M - 1);
+  const float* xcol = X + min(n0 + c, N - 1);
+  float cs = 0.f;
+  f4 rg[4], rx[4];
+  auto load = [&](int tb) __attribute__((always_inline)) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int t = tb + tg + 4 * q + i;
+        const bool ok = t < t1;
+        const int64_t tc = ok ? t : t0;
+        rg[q][i] = ok ? gcol[tc * M] : 0.f;
+        rx[q][i] = ok ? xcol[tc * N] : 0.f;
+      }
+  };
+  auto store = [&]() __attribute__((always_inline)) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      cs += (rg[q][0] + rg[q][1]) + (rg[q][2] + rg[q][3]);
+      const int o = c * GX_RS + tg + 4 * q;
+      bf16x4 p0, p1, p2;
+      split3x4(rg[q], p0, p1, p2);
+      *reinterpret_cast<bf16x4*>(&As[o]) = p0;
+      *reinterpret_cast<bf16x4*>(&As[PL + o]) = p1;
+      *reinterpret_cast<bf16x4*>(&As[2 * PL + o]) = p2;
+      split3x4(rx[q], p0, p1, p2);
+      *reinterpret_cast<bf16x4*>(&Bs[o]) = p0;
+      *reinterpret_cast<bf16x4*>(&Bs[PL + o]) = p1;
+      *reinterpret_cast<bf16x4*>(&Bs[2 * PL + o]) = p2;
+    }
+  };
+  f4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+  if (t0 < t1) load(t0);
+  for (int tb = t0; tb < t1; tb += GX_K) {
+    store();
+    __syncthreads();
+    if (tb + GX_K < t1) load(tb + GX_K);
+    gx_stage_mfma<NT>(As, Bs, wm, wn, lane, acc);
+    __syncthreads();
+  }
+  float* dw = dw_slabs + (int64_t)blockIdx.y * M * N;
+  const int r = lane & 15, kg = lane >> 4;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int n = n0 + wn * 64 + 16 * j + r;
+    if (n >= N) continue;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int m = m0 + wm * 64 + 16 * i + 4 * kg + u;
+        if (m < M) dw[(int64_t)m * N + n] = acc[i][j][u];
+      }
+  }
+  if (nt != 0) return;   // (one column tile writes the bias sums: column c's two token halves)
+  csum[tid >> 7][c] = cs;
+  __syncthreads();
+  if (tid < GX_T && m0 + tid < M) db_slabs[(int64_t)blockIdx.y * M + m0 + tid] = csum[0][tid] + csum[1][tid];
+}
+
+extern "C" int rg_wgrad_x6(const float* G, int M, const float* X, int N, int T_max, const int32_t* Tptr, int splits,
+                           float* dw_slabs, float* db_slabs, int terms, hipStream_t stream) {
+  if (M <= 0 || M % 4 || N < 4 || N % 4 || T_max <= 0 || splits <= 0 || !Tptr || (terms != 6 && terms != 9))
+    return RG_ERR_ARG;
+  if (((reinterpret_cast<uintptr_t>(G) | reinterpret_cast<uintptr_t>(X)) & 15) != 0) return RG_ERR_ARG;
+  const int ntm = (M + GX_T - 1) / GX_T, ntn = (N + GX_T - 1) / GX_T;
+  const dim3 grid((unsigned)(ntm * ntn), (unsigned)splits);
+  if (terms == 6)
+    hipLaunchKernelGGL(k_wgrad_x6<6>, grid, dim3(256), 0, stream, G, M, X, N, Tptr, dw_slabs, db_slabs);
+  else
+    hipLaunchKernelGGL(k_wgrad_x6<9>, grid, dim3(256), 0, stream, G, M, X, N, Tptr, dw_slabs, db_slabs);
+  RG_LAUNCH_CHECK();
+  return RG_OK;
+}

@@ -285,6 +285,10 @@ class Trunk:
         self.err = torch.zeros(1, dtype=torch.int32, device=device)  # out-of-range item ids seen
         self.scatter = SegScatter(device)
         self._ws = {}
+        # bf16 plane products of the trunk GEMMs (csrc/gemm.hip rg_gemm_x6 / rg_wgrad_x6; the
+        # nets set it with the heads' matmul_precision); 0: the fp32 MFMA kernels.  Needs
+        # E % 32 == 0 and H % 32 == 0 (the GEMMs' K and N), else the fp32 kernels run
+        self.gemm_terms = 0
         # emit_planes (set for the sampled head's split logits): the training
         # forward's GRU launch also writes the final h as bf16 K-planes
         # (rg_gru_fwd_dirs_planes), left in h_planes for the head
@@ -384,8 +388,12 @@ class Trunk:
                              w.perm.data_ptr(), w.lsort.data_ptr(), w.offs.data_ptr(), table, self.N1, E, d,
                              w.tok_id[d].data_ptr(), w.X[d].data_ptr(), self.err.data_ptr(), st)
             with region("gemm_ih"):
-                call("rg_gemm_f32", w.X[d].data_ptr(), E, 1, w_ih.p.data_ptr(), 1, E, w.Gi[d].data_ptr(), 3 * H,
-                     b_ih.p.data_ptr(), w.TM, w.ntok_ptr, 3 * H, E, None, 1, st)
+                if self._x6():
+                    call("rg_gemm_x6", w.X[d].data_ptr(), E, w_ih.p.data_ptr(), E, 1, w.Gi[d].data_ptr(), 3 * H,
+                         b_ih.p.data_ptr(), w.TM, w.ntok_ptr, 3 * H, E, self.gemm_terms, st)
+                else:
+                    call("rg_gemm_f32", w.X[d].data_ptr(), E, 1, w_ih.p.data_ptr(), 1, E, w.Gi[d].data_ptr(), 3 * H,
+                         b_ih.p.data_ptr(), w.TM, w.ntok_ptr, 3 * H, E, None, 1, st)
             if self.wide:
                 with region("gru_fwd"):
                     call("rg_gru_fwd_wide", w.Gi[d].data_ptr(), w_hh.p.data_ptr(), b_hh.p.data_ptr(),
@@ -468,19 +476,33 @@ class Trunk:
         H, E, TM = self.H, self.E, w.TM
         for d in range(self.ndir):
             with region("gemm_dx"):
-                call("rg_gemm_f32", w.dGi[d].data_ptr(), 3 * H, 1, self.dirs[d][0].p.data_ptr(), E, 1,
-                     w.dX[d].data_ptr(), E, None, TM, w.ntok_ptr, E, 3 * H, None, 1, st)
+                if self._x6():
+                    call("rg_gemm_x6", w.dGi[d].data_ptr(), 3 * H, self.dirs[d][0].p.data_ptr(), E, 0,
+                         w.dX[d].data_ptr(), E, None, TM, w.ntok_ptr, E, 3 * H, self.gemm_terms, st)
+                else:
+                    call("rg_gemm_f32", w.dGi[d].data_ptr(), 3 * H, 1, self.dirs[d][0].p.data_ptr(), E, 1,
+                         w.dX[d].data_ptr(), E, None, TM, w.ntok_ptr, E, 3 * H, None, 1, st)
 
     def _grads_w(self, w, S):
         """dW_ih = dGiᵀ·X, db_ih = Σ dGi ; dW_hh = dGhᵀ·H_prev, db_hh = Σ dGh (token slabs)."""
         st = stream_ptr()
         H, E, TM = self.H, self.E, w.TM
+        x6 = self._x6()
         for d in range(self.ndir):
             with region("wgrad"):
-                call("rg_wgrad", w.dGi[d].data_ptr(), 3 * H, w.X[d].data_ptr(), E, TM, w.ntok_ptr, S,
-                     w.sl_ih[d].data_ptr(), w.cs_ih[d].data_ptr(), st)
-                call("rg_wgrad", w.dGh[d].data_ptr(), 3 * H, w.saved[d].data_ptr(), H, TM, w.ntok_ptr, S,
-                     w.sl_hh[d].data_ptr(), w.cs_hh[d].data_ptr(), st)
+                if x6:
+                    call("rg_wgrad_x6", w.dGi[d].data_ptr(), 3 * H, w.X[d].data_ptr(), E, TM, w.ntok_ptr, S,
+                         w.sl_ih[d].data_ptr(), w.cs_ih[d].data_ptr(), self.gemm_terms, st)
+                    call("rg_wgrad_x6", w.dGh[d].data_ptr(), 3 * H, w.saved[d].data_ptr(), H, TM, w.ntok_ptr, S,
+                         w.sl_hh[d].data_ptr(), w.cs_hh[d].data_ptr(), self.gemm_terms, st)
+                else:
+                    call("rg_wgrad", w.dGi[d].data_ptr(), 3 * H, w.X[d].data_ptr(), E, TM, w.ntok_ptr, S,
+                         w.sl_ih[d].data_ptr(), w.cs_ih[d].data_ptr(), st)
+                    call("rg_wgrad", w.dGh[d].data_ptr(), 3 * H, w.saved[d].data_ptr(), H, TM, w.ntok_ptr, S,
+                         w.sl_hh[d].data_ptr(), w.cs_hh[d].data_ptr(), st)
+
+    def _x6(self):
+        return self.gemm_terms and self.E % 32 == 0 and self.H % 32 == 0
 
     def _grads_scatter(self, w, tag):
         """The embedding rows' gradients: scatter into G_emb, or (item-sharded

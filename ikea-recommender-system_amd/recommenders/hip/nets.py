@@ -89,6 +89,8 @@ class HipNet:
         Q heads' row gathers stay native fp32."""
         for hd in self.heads.values():
             hd.set_matmul_precision(precision)
+        # the trunk's GEMMs (Gi, dX, the weight gradients) on the same arithmetic
+        self.trunk.gemm_terms = {"f32": 0, "f32x9": 9}.get(precision, 6)
         _log_precision_once(precision)
         return self
 

@@ -314,6 +314,16 @@ int rg_lazy_catch_up(float* P, float* M, float* V, int cols, uint16_t* P16, floa
 int rg_lazy_adam_rows(float* P, float* M, float* V, float* G, int cols, uint16_t* P16, float* Pb, float* Mb, float* Vb,
                       float* Gb, int64_t rows, int32_t* last, const int32_t* tags, int32_t tag, int32_t step,
                       float* hist, const float* adam6, rg_stream_t stream);
+/* Split-bf16 trunk GEMMs (precision f32x6* / f32x9: terms 6 or 9 plane products of exact
+ * 3-way bf16 splits, fp32 accumulation; GRU4Rec/model.py:49-55,76 via nn.GRU).
+ * rg_gemm_x6: C = A·Bᵀ (+ bias): A (M × K, row stride lda) k-contiguous; B (N × K) k-contiguous
+ *   (b_kcontig = 1) or (K × N) n-contiguous, row stride ldb; K % 32 == 0, N % 4 == 0; M read from
+ *   Mptr when given (grid sized for M).  Replaces rg_gemm_f32 for Gi = X·W_ihᵀ + b, dX = dGi·W_ih.
+ * rg_wgrad_x6: rg_wgrad's contract (dW, db token-split slabs) on the same arithmetic. */
+int rg_gemm_x6(const float* A, int64_t lda, const float* B, int64_t ldb, int b_kcontig, float* C, int64_t ldc,
+               const float* bias, int M, const int32_t* Mptr, int N, int K, int terms, rg_stream_t stream);
+int rg_wgrad_x6(const float* G, int M, const float* X, int N, int T_max, const int32_t* Tptr, int splits,
+                float* dw_slabs, float* db_slabs, int terms, rg_stream_t stream);
 /* split-K weight-gradient slabs summed in order, then Adam (or g_out). */
 int rg_adam_slabs(float* P, float* M, float* V, const float* slabs, int nslab, int64_t n, const float* adam6,
                   float* g_out, rg_stream_t stream);

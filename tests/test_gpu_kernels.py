@@ -648,3 +648,60 @@ def test_shard_route_is_stable_partition_by_owner(T, W):
     np.testing.assert_array_equal(counts.cpu().numpy(), np.bincount(own, minlength=W))
     np.testing.assert_array_equal(slot[:T].cpu().numpy(), exp_slot)
     np.testing.assert_array_equal(send[:T].cpu().numpy(), ids[order])
+
+
+@pytest.mark.parametrize("terms", [6, 9])
+@pytest.mark.parametrize("M,N,K,bk", [(85003, 384, 128, 1), (300, 128, 384, 0), (129, 768, 256, 1), (4100, 64, 96, 0),
+                                      (7, 32, 32, 1), (1000, 256, 384, 0)])
+def test_gemm_x6_split_bf16(terms, M, N, K, bk):
+    """rg_gemm_x6 (split-bf16 trunk GEMM: Gi = X·W_ihᵀ + b with B k-contiguous,
+    dX = dGi·W_ih with B n-contiguous): against fp64, within 2× the native
+    fp32 MFMA kernel's own error (rg_gemm_f32) plus fp32 rounding of the
+    output; device-side row count, partial tiles, rows past M untouched."""
+    g = torch.Generator().manual_seed(5 + M + K)
+    A = torch.randn(M, K, generator=g)
+    Bnk = torch.randn(N, K, generator=g) * 0.1
+    bias = torch.randn(N, generator=g) if bk else None
+    ref = A.double() @ Bnk.double().t() + (bias.double() if bk else 0)
+    Ad = D(A)
+    Bd = D(Bnk) if bk else D(Bnk.t().contiguous())
+    ldb = K if bk else N
+    Mdev = D(torch.tensor([M], dtype=torch.int32))
+    out = torch.full((M + 5, N), float("nan"), device=dev)
+    C().call("rg_gemm_x6", Ad.data_ptr(), K, Bd.data_ptr(), ldb, bk, out.data_ptr(), N,
+             D(bias).data_ptr() if bk else None, M + 300, Mdev.data_ptr(), N, K, terms, st())
+    nat = torch.full((M, N), float("nan"), device=dev)
+    C().call("rg_gemm_f32", Ad.data_ptr(), K, 1, Bd.data_ptr(), 1 if bk else N, K if bk else 1, nat.data_ptr(), N,
+             D(bias).data_ptr() if bk else None, M, None, N, K, None, 1, st())
+    torch.cuda.synchronize()
+    assert torch.isnan(out[M:]).all()
+    e_x6 = (out[:M].cpu().double() - ref).abs().max().item()
+    e_nat = (nat.cpu().double() - ref).abs().max().item()
+    ulp = ref.abs().max().item() * 2.0 ** -24
+    assert e_x6 <= 2 * e_nat + 2 * ulp, (e_x6, e_nat, ulp)
+
+
+@pytest.mark.parametrize("terms", [6, 9])
+@pytest.mark.parametrize("M,N,T,splits", [(384, 128, 5000, 16), (384, 256, 3000, 7), (192, 64, 3000, 128),
+                                          (96, 32, 777, 3), (384, 128, 85000, 128)])
+def test_wgrad_x6_split_bf16(terms, M, N, T, splits):
+    """rg_wgrad_x6 (split-bf16 dW = Gᵀ·X and db = Σ G over device-counted
+    tokens, token-split slabs): against fp64, within 2× rg_wgrad's error."""
+    g = torch.Generator().manual_seed(9 + T)
+    G = torch.randn(T + 40, M, generator=g)
+    X = torch.randn(T + 40, N, generator=g)
+    Tdev = D(torch.tensor([T], dtype=torch.int32))
+    out = {}
+    for name in ("rg_wgrad_x6", "rg_wgrad"):
+        dw = torch.full((splits, M, N), float("nan"), device=dev)
+        db = torch.full((splits, M), float("nan"), device=dev)
+        extra = (terms,) if name.endswith("x6") else ()
+        C().call(name, D(G).data_ptr(), M, D(X).data_ptr(), N, T + 40, Tdev.data_ptr(), splits, dw.data_ptr(),
+                 db.data_ptr(), *extra, st())
+        out[name] = (dw.sum(0).cpu().double(), db.sum(0).cpu().double())
+    ref_w = G[:T].double().t() @ X[:T].double()
+    ref_b = G[:T].double().sum(0)
+    e_w = {k: (v[0] - ref_w).abs().max().item() for k, v in out.items()}
+    e_b = {k: (v[1] - ref_b).abs().max().item() for k, v in out.items()}
+    assert e_w["rg_wgrad_x6"] <= 2 * e_w["rg_wgrad"] + 1e-6 * T ** 0.5, e_w
+    assert e_b["rg_wgrad_x6"] <= 2 * e_b["rg_wgrad"] + 1e-6 * T ** 0.5, e_b
