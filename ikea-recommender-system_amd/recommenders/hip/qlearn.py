@@ -147,6 +147,7 @@ def q_side_stream(net):
 # the screening argmax, Q_boot(s', a*)) on its own stream beside the main
 # state's forward and the supervised head's pass 1, joined before the TD loss
 TARGET_SIDE_STREAM = True
+PASS2_BEFORE_TARGET = True
 # (round 6: starting it only after the previous step's pass 2, so that it shares the CUs with
 # pass 1 instead, measured 214.5K vs 215.1K session-steps/s at C4 — not kept,
 # profiles/r07/ab_c4_target_after_pass2.txt)
@@ -234,8 +235,26 @@ def double_q_step(nets, clocks, k, s, a, r, s_next, true_len, true_next_len, is_
     sup_loss, _ = main.sup_head_output.forward_loss(h, a, slot="main")
     q = main.gather_q(h, idx64=a, out=main.buf("q", (B, nh)))
     dq = main.buf("dq", (B, nh))
+    if smorl is not None:   # the rewards' top-k re-scores pass 1's candidates with W: before pass 2 moves it
+        rr = smorl_rewards(main, smorl, s, a, r, true_next_len, B)
+        if smorl.get("lut") is not None:   # the reference raises in the reward, before any update
+            raise_if_unmapped(smorl["remap_err"])
+    # ---- backward + Adam (main network, its own optimizer clock) ----
+    adam6 = clocks[k].next_args()
+    main.trunk_tag = getattr(main, "trunk_tag", 0) + 1
+    tag = main.trunk_tag
+    dh = main.dh_buffer(B)
+    # the supervised head's dh and pass 2 (side stream) need pass 1 only, not the double-Q
+    # target: launched before the target is joined, so pass 2 never waits behind it (a target
+    # whose kernels found the CUs busy with pass 1 used to run between pass 1 and pass 2,
+    # profiles/r06/c4_timeline_target_stream.txt); pass 2 overlaps the target's tail, the TD
+    # loss, the Q heads' backward / Adam and the trunk
+    if PASS2_BEFORE_TARGET:
+        main.sup_head_output.backward_step(h, a, dh, adam6, slot="main", overlap=True)
     if ts is not None:
         cur.wait_stream(ts)
+    if not PASS2_BEFORE_TARGET:
+        main.sup_head_output.backward_step(h, a, dh, adam6, slot="main", overlap=True)
     if smorl is None:
         r64 = _dev(r, dev, torch.float64)
         sq = main.buf("sq", (B,), torch.float64)
@@ -244,9 +263,6 @@ def double_q_step(nets, clocks, k, s, a, r, s_next, true_len, true_next_len, is_
              sq.data_ptr(), dq.data_ptr(), st)
         call("rg_sum64", sq.data_ptr(), B, 1.0 / B, q_loss.data_ptr(), None, st)
     else:
-        rr = smorl_rewards(main, smorl, s, a, r, true_next_len, B)
-        if smorl.get("lut") is not None:   # the reference raises in the reward, before any update
-            raise_if_unmapped(smorl["remap_err"])
         row = main.buf("qrow", (B,))
         q_loss = main.buf("qloss32", (1,))
         grad_row = _f32(np.float32(smorl["alpha"]) / np.float32(B))
@@ -257,13 +273,6 @@ def double_q_step(nets, clocks, k, s, a, r, s_next, true_len, true_next_len, is_
         # fused head never raises it — its overflowing rows are scanned whole, counted in top_scanned)
         fused = bool(main.sup_head_output.flash_terms(B))
         host.capture(sup_loss, q_loss, *([main.sup_head_output.top_err] if smorl is not None and not fused else []))
-    # ---- backward + Adam (main network, its own optimizer clock) ----
-    adam6 = clocks[k].next_args()
-    main.trunk_tag = getattr(main, "trunk_tag", 0) + 1
-    tag = main.trunk_tag
-    dh = main.dh_buffer(B)
-    # the supervised head's pass 2 overlaps the Q heads' backward / Adam and the trunk
-    main.sup_head_output.backward_step(h, a, dh, adam6, slot="main", overlap=True)
     q_heads_backward(main, h, a, B, dq, dh, tag, st)
     # the Q heads' dense Adam sweeps on their own stream beside the trunk
     # backward (they read only the Q heads' G rows, written above); joined
