@@ -5,7 +5,7 @@
 # profiles/pmc_traffic.json entries keyed with the hash of the measured sources
 set -e
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
-O=gpurun_out/pmc
+O=gpurun_out/s6c/pmc
 mkdir -p $O
 for C in FETCH_SIZE WRITE_SIZE; do
   timeout -s KILL 120 rocprofv3 --pmc $C --output-format csv -d $O/head_$C -o p -- python3 tools/flashx.py --terms 636 --iters 2 --zs > $O/head_$C.log 2>&1
