@@ -324,66 +324,118 @@ struct LazyTab {
   int cols;
 };
 
-__device__ __forceinline__ AdamArgs hist_args(const float* __restrict__ hist, int s) {
-  const float* h = hist + 6 * (int64_t)(s - 1);
+// the six scalars of step s: from the workgroup's LDS window of the newest
+// LAZY_WIN steps (hs: steps base .. base + LAZY_WIN − 1), older ones from hist
+constexpr int LAZY_WIN = 1024;
+__device__ __forceinline__ AdamArgs hist_args(const float* __restrict__ hist, const float* hs, int base, int s) {
+  const float* h = s >= base ? hs + 6 * (s - base) : hist + 6 * (int64_t)(s - 1);
   return AdamArgs{h[0], h[1], h[2], h[3], h[4], h[5]};
 }
 
-// replay steps s0 .. s1 (inclusive) with g = zero, then (adam) one step with g
-__device__ __forceinline__ void lazy_elem(float* P, float* M, float* V, int64_t i, const float* __restrict__ hist,
-                                          int s0, int s1, float zero, bool step, float g, const AdamArgs& a) {
-  float p = P[i], m = M[i], v = V[i];
-  for (int s = s0; s <= s1; ++s) adam_elem(p, m, v, zero, hist_args(hist, s));
-  if (step) adam_elem(p, m, v, g, a);
-  P[i] = p;
-  M[i] = m;
-  V[i] = v;
+// replay steps s0 .. s1 (inclusive, wave-uniform) with g = zero, then (adam)
+// one step with g; the step scalars are read once per step for all of the
+// lane's values (a dependent chain per value: the k steps of a row that was
+// skipped k times run back to back, the values of a lane interleaved)
+template <int NV>
+__device__ __forceinline__ void lazy_vals(float* P, float* M, float* V, const int64_t (&idx)[NV], const bool (&ok)[NV],
+                                          const float* __restrict__ hist, const float* hs, int base, int s0, int s1,
+                                          float zero, bool step, const float (&g)[NV], const AdamArgs& a) {
+  float p[NV], m[NV], v[NV];
+#pragma unroll
+  for (int u = 0; u < NV; ++u) {
+    p[u] = ok[u] ? P[idx[u]] : 0.f;
+    m[u] = ok[u] ? M[idx[u]] : 0.f;
+    v[u] = ok[u] ? V[idx[u]] : 0.f;
+  }
+#pragma unroll 2
+  for (int s = s0; s <= s1; ++s) {
+    const AdamArgs as = hist_args(hist, hs, base, s);
+#pragma unroll
+    for (int u = 0; u < NV; ++u) adam_elem(p[u], m[u], v[u], zero, as);
+  }
+  if (step) {
+#pragma unroll
+    for (int u = 0; u < NV; ++u) adam_elem(p[u], m[u], v[u], g[u], a);
+  }
+#pragma unroll
+  for (int u = 0; u < NV; ++u)
+    if (ok[u]) {
+      P[idx[u]] = p[u];
+      M[idx[u]] = m[u];
+      V[idx[u]] = v[u];
+    }
 }
 
 // mode 0 (catch-up): rows with sel[r] == selv (sel NULL: every row) replay
 // last[r] + 1 .. n; mode 1 (adam step n): rows with sel[r] == selv replay
-// last[r] + 1 .. n − 1, then step n with their gradient (cleared); hist[n − 1] = a
-template <int MODE>
+// last[r] + 1 .. n − 1, then step n with their gradient (cleared); hist[n − 1] = a.
+// A row's cols values: 64 lanes × NV (cols ≤ 64·NV, NV = 4 covers 256); its
+// bias rides as value cols of the same chain (lane cols % 64 of slot cols / 64)
+template <int MODE, int NV>
 __global__ __launch_bounds__(256) void k_lazy_rows(LazyTab t, const int32_t* __restrict__ sel, int32_t selv,
                                                    int32_t* __restrict__ last, int64_t rows, int n,
                                                    float* __restrict__ hist, AdamArgs a, float zero) {
+  __shared__ float hs[6 * LAZY_WIN];
+  __shared__ int s_lo;
   const int lane = threadIdx.x & 63;
+  const int nr = MODE == 1 ? n - 1 : n;                 // newest replayed step
   if (MODE == 1 && blockIdx.x == 0 && threadIdx.x == 0) {
     float* h = hist + 6 * (int64_t)(n - 1);
     h[0] = a.w1; h[1] = a.beta2; h[2] = a.c2; h[3] = a.bc2_sqrt; h[4] = a.eps; h[5] = a.neg_step;
   }
+  if (threadIdx.x == 0) s_lo = INT32_MAX;
+  __syncthreads();
   const int64_t r0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 64;
-  if (r0 >= rows) return;
   const int64_t rl = r0 + lane;
   const bool hit = rl < rows && (sel == nullptr || sel[rl] == selv);
   const int32_t lst = hit ? last[rl] : 0;
-  uint64_t mask = __ballot(hit && (MODE == 1 || lst < n));
+  const bool go = hit && (MODE == 1 || lst < n);
+  if (go) atomicMin(&s_lo, lst + 1);   // (LDS) the oldest step this workgroup replays
+  __syncthreads();
+  if (s_lo == INT32_MAX) return;       // no selected row in this workgroup (uniform)
+  // the scalars of the steps replayed here, newest LAZY_WIN of them, into LDS
+  const int base = max(s_lo, nr - LAZY_WIN + 1);
+  for (int i = threadIdx.x; i < 6 * (nr - base + 1); i += blockDim.x) hs[i] = hist[6 * (int64_t)(base - 1) + i];
+  __syncthreads();
+  if (r0 >= rows) return;
+  uint64_t mask = __ballot(go);
   while (mask) {
     const int j = __builtin_ctzll(mask);
     mask &= mask - 1;
     const int64_t r = r0 + j;
-    const int s0 = __shfl(lst, j) + 1, s1 = MODE == 1 ? n - 1 : n;
-    const int64_t base = r * t.cols;
-    for (int c = lane; c < t.cols; c += 64) {
-      float g = 0.f;
+    const int s0 = __builtin_amdgcn_readfirstlane(__shfl(lst, j)) + 1, s1 = nr;
+    const int64_t base_r = r * t.cols;
+    int64_t idx[NV];
+    bool ok[NV];
+    float g[NV];
+#pragma unroll
+    for (int u = 0; u < NV; ++u) {
+      const int c = lane + 64 * u;
+      ok[u] = c < t.cols;
+      idx[u] = base_r + (ok[u] ? c : 0);
+      g[u] = 0.f;
+      if (MODE == 1 && ok[u]) {
+        g[u] = t.G[idx[u]];
+        t.G[idx[u]] = 0.f;
+      }
+    }
+    lazy_vals<NV>(t.P, t.M, t.V, idx, ok, hist, hs, base, s0, s1, zero, MODE == 1, g, a);
+    if (t.P16) {
+#pragma unroll
+      for (int u = 0; u < NV; ++u)
+        if (ok[u]) t.P16[idx[u]] = __float2half_rn(t.P[idx[u]]);
+    }
+    if (t.Pb && lane == 0) {
+      const int64_t bi[1] = {r};
+      const bool bo[1] = {true};
+      float gb[1] = {0.f};
       if (MODE == 1) {
-        g = t.G[base + c];
-        t.G[base + c] = 0.f;
+        gb[0] = t.Gb[r];
+        t.Gb[r] = 0.f;
       }
-      lazy_elem(t.P, t.M, t.V, base + c, hist, s0, s1, zero, MODE == 1, g, a);
-      if (t.P16) t.P16[base + c] = __float2half_rn(t.P[base + c]);
+      lazy_vals<1>(t.Pb, t.Mb, t.Vb, bi, bo, hist, hs, base, s0, s1, zero, MODE == 1, gb, a);
     }
-    if (lane == 0) {
-      if (t.Pb) {
-        float gb = 0.f;
-        if (MODE == 1) {
-          gb = t.Gb[r];
-          t.Gb[r] = 0.f;
-        }
-        lazy_elem(t.Pb, t.Mb, t.Vb, r, hist, s0, s1, zero, MODE == 1, gb, a);
-      }
-      last[r] = n;
-    }
+    if (lane == 0) last[r] = n;
   }
 }
 
@@ -421,8 +473,13 @@ extern "C" int rg_lazy_catch_up(float* P, float* M, float* V, int cols, uint16_t
   const LazyTab t{P, M, V, nullptr, reinterpret_cast<__half*>(P16), Pb, Mb, Vb, nullptr, cols};
   if (!lazy_tab_ok(t) || rows <= 0 || !last || n_steps < 0 || (n_steps > 0 && !hist)) return RG_ERR_ARG;
   if (n_steps == 0) return RG_OK;
-  hipLaunchKernelGGL(k_lazy_rows<0>, dim3(lazy_grid(rows)), dim3(256), 0, stream, t, need, stamp, last, rows, n_steps,
-                     hist, AdamArgs{}, 0.f);
+#define LZ(NV) hipLaunchKernelGGL((k_lazy_rows<0, NV>), dim3(lazy_grid(rows)), dim3(256), 0, stream, t, need, stamp, \
+                                 last, rows, n_steps, hist, AdamArgs{}, 0.f)
+  if (cols <= 64) LZ(1);
+  else if (cols <= 128) LZ(2);
+  else if (cols <= 256) LZ(4);
+  else return RG_ERR_SHAPE;
+#undef LZ
   RG_LAUNCH_CHECK();
   return RG_OK;
 }
@@ -433,8 +490,13 @@ extern "C" int rg_lazy_adam_rows(float* P, float* M, float* V, float* G, int col
   const LazyTab t{P, M, V, G, reinterpret_cast<__half*>(P16), Pb, Mb, Vb, Gb, cols};
   if (!lazy_tab_ok(t) || !G || (Pb && !Gb) || rows <= 0 || !last || !tags || step < 1 || !hist || !adam6)
     return RG_ERR_ARG;
-  hipLaunchKernelGGL(k_lazy_rows<1>, dim3(lazy_grid(rows)), dim3(256), 0, stream, t, tags, tag, last, rows, step, hist,
-                     to_args(adam6), 0.f);
+#define LZ(NV) hipLaunchKernelGGL((k_lazy_rows<1, NV>), dim3(lazy_grid(rows)), dim3(256), 0, stream, t, tags, tag, last, \
+                                 rows, step, hist, to_args(adam6), 0.f)
+  if (cols <= 64) LZ(1);
+  else if (cols <= 128) LZ(2);
+  else if (cols <= 256) LZ(4);
+  else return RG_ERR_SHAPE;
+#undef LZ
   RG_LAUNCH_CHECK();
   return RG_OK;
 }
