@@ -332,40 +332,6 @@ __device__ __forceinline__ AdamArgs hist_args(const float* __restrict__ hist, co
   return AdamArgs{h[0], h[1], h[2], h[3], h[4], h[5]};
 }
 
-// replay steps s0 .. s1 (inclusive, wave-uniform) with g = zero, then (adam)
-// one step with g; the step scalars are read once per step for all of the
-// lane's values (a dependent chain per value: the k steps of a row that was
-// skipped k times run back to back, the values of a lane interleaved)
-template <int NV>
-__device__ __forceinline__ void lazy_vals(float* P, float* M, float* V, const int64_t (&idx)[NV], const bool (&ok)[NV],
-                                          const float* __restrict__ hist, const float* hs, int base, int s0, int s1,
-                                          float zero, bool step, const float (&g)[NV], const AdamArgs& a) {
-  float p[NV], m[NV], v[NV];
-#pragma unroll
-  for (int u = 0; u < NV; ++u) {
-    p[u] = ok[u] ? P[idx[u]] : 0.f;
-    m[u] = ok[u] ? M[idx[u]] : 0.f;
-    v[u] = ok[u] ? V[idx[u]] : 0.f;
-  }
-#pragma unroll 2
-  for (int s = s0; s <= s1; ++s) {
-    const AdamArgs as = hist_args(hist, hs, base, s);
-#pragma unroll
-    for (int u = 0; u < NV; ++u) adam_elem(p[u], m[u], v[u], zero, as);
-  }
-  if (step) {
-#pragma unroll
-    for (int u = 0; u < NV; ++u) adam_elem(p[u], m[u], v[u], g[u], a);
-  }
-#pragma unroll
-  for (int u = 0; u < NV; ++u)
-    if (ok[u]) {
-      P[idx[u]] = p[u];
-      M[idx[u]] = m[u];
-      V[idx[u]] = v[u];
-    }
-}
-
 // mode 0 (catch-up): rows with sel[r] == selv (sel NULL: every row) replay
 // last[r] + 1 .. n; mode 1 (adam step n): rows with sel[r] == selv replay
 // last[r] + 1 .. n − 1, then step n with their gradient (cleared); hist[n − 1] = a.
@@ -405,35 +371,54 @@ __global__ __launch_bounds__(256) void k_lazy_rows(LazyTab t, const int32_t* __r
     const int64_t r = r0 + j;
     const int s0 = __builtin_amdgcn_readfirstlane(__shfl(lst, j)) + 1, s1 = nr;
     const int64_t base_r = r * t.cols;
-    int64_t idx[NV];
-    bool ok[NV];
-    float g[NV];
+    // the row's values (lane + 64u < cols) and, in slot NV of lane 0, its bias: one
+    // interleaved chain per lane, the k replayed steps back to back
+    float p[NV + 1], m[NV + 1], v[NV + 1], g[NV + 1];
+    const bool bias_lane = t.Pb != nullptr && lane == 0;
 #pragma unroll
-    for (int u = 0; u < NV; ++u) {
+    for (int u = 0; u <= NV; ++u) {
       const int c = lane + 64 * u;
-      ok[u] = c < t.cols;
-      idx[u] = base_r + (ok[u] ? c : 0);
+      const bool ok = u < NV ? c < t.cols : bias_lane;
+      // (every address valid whether used or not: the bias slot of a lane that carries no
+      // bias points at the row's first value)
+      float* P = u < NV || !bias_lane ? t.P + base_r + (ok ? c : 0) : t.Pb + r;
+      float* Mm = u < NV || !bias_lane ? t.M + base_r + (ok ? c : 0) : t.Mb + r;
+      float* Vv = u < NV || !bias_lane ? t.V + base_r + (ok ? c : 0) : t.Vb + r;
+      p[u] = ok ? *P : 0.f;
+      m[u] = ok ? *Mm : 0.f;
+      v[u] = ok ? *Vv : 0.f;
       g[u] = 0.f;
-      if (MODE == 1 && ok[u]) {
-        g[u] = t.G[idx[u]];
-        t.G[idx[u]] = 0.f;
+      if (MODE == 1 && ok) {
+        float* G = u < NV ? t.G + base_r + c : t.Gb + r;   // (ok: a valid address)
+        g[u] = *G;
+        *G = 0.f;
       }
     }
-    lazy_vals<NV>(t.P, t.M, t.V, idx, ok, hist, hs, base, s0, s1, zero, MODE == 1, g, a);
-    if (t.P16) {
+#pragma unroll 2
+    for (int s = s0; s <= s1; ++s) {
+      const AdamArgs as = hist_args(hist, hs, base, s);
 #pragma unroll
-      for (int u = 0; u < NV; ++u)
-        if (ok[u]) t.P16[idx[u]] = __float2half_rn(t.P[idx[u]]);
+      for (int u = 0; u <= NV; ++u) adam_elem(p[u], m[u], v[u], zero, as);
     }
-    if (t.Pb && lane == 0) {
-      const int64_t bi[1] = {r};
-      const bool bo[1] = {true};
-      float gb[1] = {0.f};
-      if (MODE == 1) {
-        gb[0] = t.Gb[r];
-        t.Gb[r] = 0.f;
+    if (MODE == 1) {
+#pragma unroll
+      for (int u = 0; u <= NV; ++u) adam_elem(p[u], m[u], v[u], g[u], a);
+    }
+#pragma unroll
+    for (int u = 0; u <= NV; ++u) {
+      const int c = lane + 64 * u;
+      const bool ok = u < NV ? c < t.cols : bias_lane;
+      if (!ok) continue;
+      if (u < NV) {
+        t.P[base_r + c] = p[u];
+        t.M[base_r + c] = m[u];
+        t.V[base_r + c] = v[u];
+        if (t.P16) t.P16[base_r + c] = __float2half_rn(p[u]);
+      } else {
+        t.Pb[r] = p[u];
+        t.Mb[r] = m[u];
+        t.Vb[r] = v[u];
       }
-      lazy_vals<1>(t.Pb, t.Mb, t.Vb, bi, bo, hist, hs, base, s0, s1, zero, MODE == 1, gb, a);
     }
     if (lane == 0) last[r] = n;
   }
