@@ -335,94 +335,106 @@ __device__ __forceinline__ AdamArgs hist_args(const float* __restrict__ hist, co
 // mode 0 (catch-up): rows with sel[r] == selv (sel NULL: every row) replay
 // last[r] + 1 .. n; mode 1 (adam step n): rows with sel[r] == selv replay
 // last[r] + 1 .. n − 1, then step n with their gradient (cleared); hist[n − 1] = a.
-// A row's cols values: 64 lanes × NV (cols ≤ 64·NV, NV = 4 covers 256); its
-// bias rides as value cols of the same chain (lane cols % 64 of slot cols / 64)
-template <int MODE, int NV>
+// Workgroup = 256 threads over 64 rows: the selected rows are processed
+// 256 / CPR at a time, thread t on value t % CPR of row slot t / CPR (CPR =
+// cols rounded up to a power of two), so every thread carries ONE value's
+// chain of replayed steps and a row's values run in parallel; the thread of
+// value 0 also carries the bias (a second, interleaved chain).  (The first
+// form — one wave per row, each lane 4–5 values — ran the negatives' k ≈ 400
+// step chains at 2 waves per SIMD and cost 1 ms per C3 step at steady state,
+// profiles/r07/lazy_long_c3.txt.)
+template <int MODE, int CPR>
 __global__ __launch_bounds__(256) void k_lazy_rows(LazyTab t, const int32_t* __restrict__ sel, int32_t selv,
                                                    int32_t* __restrict__ last, int64_t rows, int n,
                                                    float* __restrict__ hist, AdamArgs a, float zero) {
+  constexpr int RPP = 256 / CPR;   // rows per pass
   __shared__ float hs[6 * LAZY_WIN];
   __shared__ int s_lo;
-  const int lane = threadIdx.x & 63;
-  const int nr = MODE == 1 ? n - 1 : n;                 // newest replayed step
-  if (MODE == 1 && blockIdx.x == 0 && threadIdx.x == 0) {
+  __shared__ int32_t rlist[64], rfirst[64];
+  __shared__ int nsel;
+  const int tid = threadIdx.x;
+  const int nr = MODE == 1 ? n - 1 : n;   // newest replayed step
+  if (MODE == 1 && blockIdx.x == 0 && tid == 0) {
     float* h = hist + 6 * (int64_t)(n - 1);
     h[0] = a.w1; h[1] = a.beta2; h[2] = a.c2; h[3] = a.bc2_sqrt; h[4] = a.eps; h[5] = a.neg_step;
   }
-  if (threadIdx.x == 0) s_lo = INT32_MAX;
-  __syncthreads();
-  const int64_t r0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 64;
-  const int64_t rl = r0 + lane;
-  const bool hit = rl < rows && (sel == nullptr || sel[rl] == selv);
-  const int32_t lst = hit ? last[rl] : 0;
-  const bool go = hit && (MODE == 1 || lst < n);
-  if (go) atomicMin(&s_lo, lst + 1);   // (LDS) the oldest step this workgroup replays
-  __syncthreads();
-  if (s_lo == INT32_MAX) return;       // no selected row in this workgroup (uniform)
-  // the scalars of the steps replayed here, newest LAZY_WIN of them, into LDS
-  const int base = max(s_lo, nr - LAZY_WIN + 1);
-  for (int i = threadIdx.x; i < 6 * (nr - base + 1); i += blockDim.x) hs[i] = hist[6 * (int64_t)(base - 1) + i];
-  __syncthreads();
-  if (r0 >= rows) return;
-  uint64_t mask = __ballot(go);
-  while (mask) {
-    const int j = __builtin_ctzll(mask);
-    mask &= mask - 1;
-    const int64_t r = r0 + j;
-    const int s0 = __builtin_amdgcn_readfirstlane(__shfl(lst, j)) + 1, s1 = nr;
-    const int64_t base_r = r * t.cols;
-    // the row's values (lane + 64u < cols) and, in slot NV of lane 0, its bias: one
-    // interleaved chain per lane, the k replayed steps back to back
-    float p[NV + 1], m[NV + 1], v[NV + 1], g[NV + 1];
-    const bool bias_lane = t.Pb != nullptr && lane == 0;
+  const int64_t r0 = (int64_t)blockIdx.x * 64;
+  if (tid < 64) {   // wave 0: this workgroup's selected rows, compacted in row order
+    const int64_t rl = r0 + tid;
+    const bool hit = rl < rows && (sel == nullptr || sel[rl] == selv);
+    const int32_t lst = hit ? last[rl] : 0;
+    const bool go = hit && (MODE == 1 || lst < n);
+    const uint64_t mask = __ballot(go);
+    if (go) {
+      const int pos = __builtin_popcountll(mask & ((1ull << tid) - 1));
+      rlist[pos] = tid;
+      rfirst[pos] = lst + 1;
+    }
+    const int lo = go ? lst + 1 : INT32_MAX;
+    int m = lo;
 #pragma unroll
-    for (int u = 0; u <= NV; ++u) {
-      const int c = lane + 64 * u;
-      const bool ok = u < NV ? c < t.cols : bias_lane;
-      // (every address valid whether used or not: the bias slot of a lane that carries no
-      // bias points at the row's first value)
-      float* P = u < NV || !bias_lane ? t.P + base_r + (ok ? c : 0) : t.Pb + r;
-      float* Mm = u < NV || !bias_lane ? t.M + base_r + (ok ? c : 0) : t.Mb + r;
-      float* Vv = u < NV || !bias_lane ? t.V + base_r + (ok ? c : 0) : t.Vb + r;
-      p[u] = ok ? *P : 0.f;
-      m[u] = ok ? *Mm : 0.f;
-      v[u] = ok ? *Vv : 0.f;
-      g[u] = 0.f;
-      if (MODE == 1 && ok) {
-        float* G = u < NV ? t.G + base_r + c : t.Gb + r;   // (ok: a valid address)
-        g[u] = *G;
-        *G = 0.f;
+    for (int d = 1; d < 64; d *= 2) m = min(m, __shfl_xor(m, d));
+    if (tid == 0) {
+      nsel = __builtin_popcountll(mask);
+      s_lo = m;
+    }
+  }
+  __syncthreads();
+  const int ns = nsel;
+  if (ns == 0) return;   // (uniform)
+  // the scalars of the steps replayed here, the newest LAZY_WIN of them, into LDS
+  const int base = max(s_lo, nr - LAZY_WIN + 1);
+  for (int i = tid; i < 6 * (nr - base + 1); i += 256) hs[i] = hist[6 * (int64_t)(base - 1) + i];
+  __syncthreads();
+  const int slot = tid / CPR, c = tid % CPR;
+  for (int q0 = 0; q0 < ns; q0 += RPP) {
+    const int q = q0 + slot;
+    if (q >= ns) break;
+    const int64_t r = r0 + rlist[q];
+    const int s0 = rfirst[q];
+    const bool val = c < t.cols;
+    const bool bia = t.Pb != nullptr && c == 0;
+    if (!val && !bia) continue;
+    const int64_t i = r * t.cols + (val ? c : 0);
+    float p0 = val ? t.P[i] : 0.f, m0 = val ? t.M[i] : 0.f, v0 = val ? t.V[i] : 0.f;
+    float p1 = bia ? t.Pb[r] : 0.f, m1 = bia ? t.Mb[r] : 0.f, v1 = bia ? t.Vb[r] : 0.f;
+    float g0 = 0.f, g1 = 0.f;
+    if (MODE == 1) {
+      if (val) {
+        g0 = t.G[i];
+        t.G[i] = 0.f;
+      }
+      if (bia) {
+        g1 = t.Gb[r];
+        t.Gb[r] = 0.f;
       }
     }
 #pragma unroll 2
-    for (int s = s0; s <= s1; ++s) {
+    for (int s = s0; s <= nr; ++s) {
       const AdamArgs as = hist_args(hist, hs, base, s);
-#pragma unroll
-      for (int u = 0; u <= NV; ++u) adam_elem(p[u], m[u], v[u], zero, as);
+      adam_elem(p0, m0, v0, zero, as);
+      adam_elem(p1, m1, v1, zero, as);
     }
     if (MODE == 1) {
-#pragma unroll
-      for (int u = 0; u <= NV; ++u) adam_elem(p[u], m[u], v[u], g[u], a);
+      adam_elem(p0, m0, v0, g0, a);
+      adam_elem(p1, m1, v1, g1, a);
     }
-#pragma unroll
-    for (int u = 0; u <= NV; ++u) {
-      const int c = lane + 64 * u;
-      const bool ok = u < NV ? c < t.cols : bias_lane;
-      if (!ok) continue;
-      if (u < NV) {
-        t.P[base_r + c] = p[u];
-        t.M[base_r + c] = m[u];
-        t.V[base_r + c] = v[u];
-        if (t.P16) t.P16[base_r + c] = __float2half_rn(p[u]);
-      } else {
-        t.Pb[r] = p[u];
-        t.Mb[r] = m[u];
-        t.Vb[r] = v[u];
-      }
+    if (val) {
+      t.P[i] = p0;
+      t.M[i] = m0;
+      t.V[i] = v0;
+      if (t.P16) t.P16[i] = __float2half_rn(p0);
     }
-    if (lane == 0) last[r] = n;
+    if (bia) {
+      t.Pb[r] = p1;
+      t.Mb[r] = m1;
+      t.Vb[r] = v1;
+    }
+    if (c == 0) last[r] = n;
   }
 }
+
+static inline unsigned lazy_grid(int64_t rows) { return (unsigned)((rows + 63) / 64); }
 
 // need[id] = stamp for the n ids (int64) in [0, rows) and, with S > 0, the S
 // negatives of draw `counter` (draw_id over [0, rows), csrc/common.h)
@@ -441,7 +453,6 @@ static inline bool lazy_tab_ok(const LazyTab& t) {
   return t.P && t.M && t.V && t.cols > 0 && (!t.Pb || (t.Mb && t.Vb));
 }
 
-static inline unsigned lazy_grid(int64_t rows) { return (unsigned)((rows + 255) / 256); }
 
 extern "C" int rg_lazy_mark_rows(const int64_t* ids, int64_t n, int64_t rows, uint64_t seed, uint64_t counter, int S,
                                  int32_t* need, int32_t stamp, hipStream_t stream) {
@@ -458,11 +469,12 @@ extern "C" int rg_lazy_catch_up(float* P, float* M, float* V, int cols, uint16_t
   const LazyTab t{P, M, V, nullptr, reinterpret_cast<__half*>(P16), Pb, Mb, Vb, nullptr, cols};
   if (!lazy_tab_ok(t) || rows <= 0 || !last || n_steps < 0 || (n_steps > 0 && !hist)) return RG_ERR_ARG;
   if (n_steps == 0) return RG_OK;
-#define LZ(NV) hipLaunchKernelGGL((k_lazy_rows<0, NV>), dim3(lazy_grid(rows)), dim3(256), 0, stream, t, need, stamp, \
+#define LZ(CPR) hipLaunchKernelGGL((k_lazy_rows<0, CPR>), dim3(lazy_grid(rows)), dim3(256), 0, stream, t, need, stamp, \
                                  last, rows, n_steps, hist, AdamArgs{}, 0.f)
-  if (cols <= 64) LZ(1);
-  else if (cols <= 128) LZ(2);
-  else if (cols <= 256) LZ(4);
+  if (cols <= 32) LZ(32);
+  else if (cols <= 64) LZ(64);
+  else if (cols <= 128) LZ(128);
+  else if (cols <= 256) LZ(256);
   else return RG_ERR_SHAPE;
 #undef LZ
   RG_LAUNCH_CHECK();
@@ -475,11 +487,12 @@ extern "C" int rg_lazy_adam_rows(float* P, float* M, float* V, float* G, int col
   const LazyTab t{P, M, V, G, reinterpret_cast<__half*>(P16), Pb, Mb, Vb, Gb, cols};
   if (!lazy_tab_ok(t) || !G || (Pb && !Gb) || rows <= 0 || !last || !tags || step < 1 || !hist || !adam6)
     return RG_ERR_ARG;
-#define LZ(NV) hipLaunchKernelGGL((k_lazy_rows<1, NV>), dim3(lazy_grid(rows)), dim3(256), 0, stream, t, tags, tag, last, \
+#define LZ(CPR) hipLaunchKernelGGL((k_lazy_rows<1, CPR>), dim3(lazy_grid(rows)), dim3(256), 0, stream, t, tags, tag, last, \
                                  rows, step, hist, to_args(adam6), 0.f)
-  if (cols <= 64) LZ(1);
-  else if (cols <= 128) LZ(2);
-  else if (cols <= 256) LZ(4);
+  if (cols <= 32) LZ(32);
+  else if (cols <= 64) LZ(64);
+  else if (cols <= 128) LZ(128);
+  else if (cols <= 256) LZ(256);
   else return RG_ERR_SHAPE;
 #undef LZ
   RG_LAUNCH_CHECK();
