@@ -147,7 +147,6 @@ def q_side_stream(net):
 # the screening argmax, Q_boot(s', a*)) on its own stream beside the main
 # state's forward and the supervised head's pass 1, joined before the TD loss
 TARGET_SIDE_STREAM = True
-PASS2_BEFORE_TARGET = True
 # (round 6: starting it only after the previous step's pass 2, so that it shares the CUs with
 # pass 1 instead, measured 214.5K vs 215.1K session-steps/s at C4 — not kept,
 # profiles/r07/ab_c4_target_after_pass2.txt)
@@ -249,12 +248,11 @@ def double_q_step(nets, clocks, k, s, a, r, s_next, true_len, true_next_len, is_
     # whose kernels found the CUs busy with pass 1 used to run between pass 1 and pass 2,
     # profiles/r06/c4_timeline_target_stream.txt); pass 2 overlaps the target's tail, the TD
     # loss, the Q heads' backward / Adam and the trunk
-    if PASS2_BEFORE_TARGET:
-        main.sup_head_output.backward_step(h, a, dh, adam6, slot="main", overlap=True)
+    # (same box, C4: 225.3-227.1K vs 214.2-215.9K session-steps/s with pass 2 after the
+    # join, profiles/r07/ab_c4_pass2_before_target.txt)
+    main.sup_head_output.backward_step(h, a, dh, adam6, slot="main", overlap=True)
     if ts is not None:
         cur.wait_stream(ts)
-    if not PASS2_BEFORE_TARGET:
-        main.sup_head_output.backward_step(h, a, dh, adam6, slot="main", overlap=True)
     if smorl is None:
         r64 = _dev(r, dev, torch.float64)
         sq = main.buf("sq", (B,), torch.float64)
