@@ -409,11 +409,16 @@ __global__ __launch_bounds__(256) void k_lazy_rows(LazyTab t, const int32_t* __r
         t.Gb[r] = 0.f;
       }
     }
+    if (__any(bia)) {   // (wave-uniform: only the wave holding a value-0 thread runs the bias chains)
 #pragma unroll 2
-    for (int s = s0; s <= nr; ++s) {
-      const AdamArgs as = hist_args(hist, hs, base, s);
-      adam_elem(p0, m0, v0, zero, as);
-      adam_elem(p1, m1, v1, zero, as);
+      for (int s = s0; s <= nr; ++s) {
+        const AdamArgs as = hist_args(hist, hs, base, s);
+        adam_elem(p0, m0, v0, zero, as);
+        adam_elem(p1, m1, v1, zero, as);
+      }
+    } else {
+#pragma unroll 2
+      for (int s = s0; s <= nr; ++s) adam_elem(p0, m0, v0, zero, hist_args(hist, hs, base, s));
     }
     if (MODE == 1) {
       adam_elem(p0, m0, v0, g0, a);
