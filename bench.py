@@ -100,6 +100,9 @@ def parse():
     ap.add_argument("--no-native-side", action="store_true", help="skip the native-f32 side run")
     ap.add_argument("--extra-steps", type=int, default=10,
                     help="C2 at N=1: timed steps of the short C3 / C4 side lines (configs_extra); 0 skips them")
+    ap.add_argument("--extra-settle", type=int, default=1500,
+                    help="untimed steps before the C3 side line's warmup (the catch-up Adam's steady state, "
+                         "about 3·A/S steps for the sampled head's negatives)")
     return ap.parse_args()
 
 
@@ -596,15 +599,21 @@ def describe(cfg, N, E, L, B, world, S):
             f"q_weights [1,1,1], gamma 0.5, alpha 1")
 
 
-def side_line(cfg, args, dev, batches, tok, steps, warmup):
+def side_line(cfg, args, dev, batches, tok, steps, warmup, settle=0):
     """A short line of another BASELINE config on one GPU, same stream and
     device as the C2 line (C3: BidirGRU4Rec with 2048 sampled negatives,
     configs[2]; C4: SMORL 3-reward double-Q, configs[3] at its global batch on
-    one GPU): value, step times, roofline and kernel times — no CPU leg."""
+    one GPU): value, step times, roofline and kernel times — no CPU leg.
+    ``settle`` untimed steps first (the stream's batches cycled): the catch-up
+    Adam's replay of a sampled head's negatives grows over the first ~3·A/S
+    steps, so the C3 line is timed at that steady state, not on a
+    fresh table."""
     B, N, E, L = args.batch, args.items, args.dim, args.seq
     tr = make_trainer(cfg, args, dev, False)
     apply_stored_logits(tr, args.stored_logits)
     tr.set_train()
+    for i in range(settle):
+        tr.train_step(*step_args(cfg, batches[i % len(batches)]))
     dt, losses, kern, per_step = timed_run(tr, batches, warmup, steps, 1, True, cfg)
     terms = LOGIT_TERMS.get(args.precision, 0)
     roof = None
@@ -625,8 +634,8 @@ def side_line(cfg, args, dev, batches, tok, steps, warmup):
     metric, workload = describe(cfg, N, E, L, B, 1, args.negatives)
     ps = np.array(per_step) * 1e3
     return {"metric": metric, "workload": workload, "value": round(B * steps / dt, 2), "unit": "session-steps/sec",
-            "n_gpus": 1, "steps": steps, "warmup": warmup, "ms_per_step": round(dt / steps * 1e3, 3),
-            "step_ms": {"median": round(float(np.median(ps)), 3), "p10": round(float(np.percentile(ps, 10)), 3),
+            "n_gpus": 1, "steps": steps, "warmup": warmup, "settle_steps": settle,
+            "ms_per_step": round(dt / steps * 1e3, 3), "step_ms": {"median": round(float(np.median(ps)), 3), "p10": round(float(np.percentile(ps, 10)), 3),
                         "p90": round(float(np.percentile(ps, 90)), 3)},
             "roofline": roof, "kernel_ms": kern, "loss_first_last": [round(losses[0], 5), round(losses[-1], 5)],
             "top_scanned_rows": scanned}
@@ -918,7 +927,8 @@ def main():
                 wx = min(3, args.warmup)
                 nx = min(args.extra_steps, len(batches) - wx)
                 for c in ("c3", "c4"):
-                    extra[c] = side_line(c, args, dev, batches, tok, nx, wx)
+                    extra[c] = side_line(c, args, dev, batches, tok, nx, wx,
+                                         settle=args.extra_settle if c == "c3" else 0)
     else:
         target = target_step(kern, T, B, args.negatives, E, HF, 2, terms)
         roof = dict(target) if target else None

@@ -301,16 +301,11 @@ extern "C" int rg_adam_slabs(float* P, float* M, float* V, const float* slabs, i
 // head's targets and negatives) the eager sweep is 24 B of HBM traffic per
 // parameter and step for rows nobody reads.  Here a row's zero-gradient steps
 // are replayed only when it is next read: last[r] = the table steps already
-// applied to row r; hist[s − 1] = step s's six fp32 scalars (written by step
-// s's own rg_lazy_adam_rows).  A replayed step is adam_elem with a gradient of
-// runtime value 0 and that step's scalars — the same fp32 operations in the
-// same order as k_adam_rows4's untagged rows, so the table after any sequence
-// of reads equals the eager one bitwise (tests/test_gpu_lazy_adam.py).
-//
-// One wave per 64 rows: lane i tests row r0 + i, the wave then walks the
-// selected rows (ballot) and updates each row's cols values 64 lanes at a
-// time; a 1-column companion table (the bias of a head: Pb / Mb / Vb / Gb)
-// shares last[] and is updated by lane 0 of the same wave.
+// applied to row r; hist row s − 1 = step s's scalars (written by step s's own
+// rg_lazy_adam_rows).  A replayed step is adam_zero_step: adam_elem with g = 0
+// in fewer operations but the same fp32 results (argued at adam_zero_step),
+// so the table after any sequence of reads equals the eager one bitwise
+// (tests/test_gpu_lazy_adam.py against k_adam_rows4's untagged rows).
 struct LazyTab {
   float* P;
   float* M;
@@ -324,39 +319,77 @@ struct LazyTab {
   int cols;
 };
 
-// the six scalars of step s: from the workgroup's LDS window of the newest
-// LAZY_WIN steps (hs: steps base .. base + LAZY_WIN − 1), older ones from hist
+// hist row s − 1 = step s's scalars, LAZY_HS floats: the six of AdamArgs, then
+// RN(1 / bc2_sqrt) (written by the step's own kernel) and a pad to 32 bytes
+constexpr int LAZY_HS = 8;
+// the newest LAZY_WIN steps a workgroup replays are staged in LDS
 constexpr int LAZY_WIN = 1024;
-__device__ __forceinline__ AdamArgs hist_args(const float* __restrict__ hist, const float* hs, int base, int s) {
-  const float* h = s >= base ? hs + 6 * (s - base) : hist + 6 * (int64_t)(s - 1);
-  return AdamArgs{h[0], h[1], h[2], h[3], h[4], h[5]};
+
+// One replayed step, g = 0: adam_elem(p, m, v, 0, a) bit for bit, in fewer
+// operations (h0 = (w1, β2, c2, bc2_sqrt), h1 = (ε, neg_step, RN(1/bc2_sqrt), ·)):
+//  * m: w1·(0 − m) + m — 0 − m and −m differ only at m = ±0, where the fma
+//    gives +0 either way;
+//  * v: β2·v + c2·0·0 = β2·v (v ≥ +0: + (+0) changes nothing);
+//  * √v / bc2_sqrt by Markstein's correction with the step's exact reciprocal
+//    r: q0 = x·r, q = fma(fma(−q0, d, x), r, q0) = RN(x / d) when r = RN(1/d)
+//    and the residual does not underflow (x = √v ≥ 2^-75); checked against the
+//    division for 1.5e9 quotients over the first 20000 steps' d at β2 ∈ {0.9 …
+//    0.999} (tools/markstein_check.c; every mantissa at six exponents for
+//    some d); x = ∞ keeps the division's ∞.
+__device__ __forceinline__ void adam_zero_step(float& p, float& m, float& v, const f4 h0, const f4 h1) {
+#pragma clang fp contract(off)
+  m = __builtin_fmaf(h0.x, -m, m);
+  v = v * h0.y;
+  const float x = sqrtf(v);
+  const float q0 = x * h1.z;
+  const float q = __builtin_fmaf(__builtin_fmaf(-q0, h0.w, x), h1.z, q0);
+  const float denom = (__builtin_isinf(x) ? x : q) + h1.x;
+  p = p + h1.y * (m / denom);
+}
+
+// steps lo .. hi (inclusive) of one value (and, with BIAS, of the companion
+// value) from rows of h (hist in global memory or the LDS window)
+template <bool BIAS>
+__device__ __forceinline__ void lazy_replay(float& p0, float& m0, float& v0, float& p1, float& m1, float& v1,
+                                            const float* h, int lo, int hi) {
+#pragma unroll 2
+  for (int s = lo; s <= hi; ++s) {
+    const f4* r = reinterpret_cast<const f4*>(h + LAZY_HS * s);
+    const f4 h0 = r[0], h1 = r[1];
+    adam_zero_step(p0, m0, v0, h0, h1);
+    if (BIAS) adam_zero_step(p1, m1, v1, h0, h1);
+  }
 }
 
 // mode 0 (catch-up): rows with sel[r] == selv (sel NULL: every row) replay
 // last[r] + 1 .. n; mode 1 (adam step n): rows with sel[r] == selv replay
-// last[r] + 1 .. n − 1, then step n with their gradient (cleared); hist[n − 1] = a.
+// last[r] + 1 .. n − 1, then step n with their gradient (cleared); hist row n − 1 = a.
 // Workgroup = 256 threads over 64 rows: the selected rows are processed
 // 256 / CPR at a time, thread t on value t % CPR of row slot t / CPR (CPR =
-// cols rounded up to a power of two), so every thread carries ONE value's
-// chain of replayed steps and a row's values run in parallel; the thread of
-// value 0 also carries the bias (a second, interleaved chain).  (The first
-// form — one wave per row, each lane 4–5 values — ran the negatives' k ≈ 400
-// step chains at 2 waves per SIMD and cost 1 ms per C3 step at steady state,
-// profiles/r07/lazy_long_c3.txt.)
+// cols rounded up to a power of two, at least 64, so a row slot is whole waves
+// and its step loop runs on scalar bounds), so every thread carries ONE
+// value's chain of replayed steps and a row's values run in parallel; the
+// thread of value 0 also carries the bias (a second, interleaved chain).  (The
+// first form — one wave per row, each lane 4–5 values — ran the negatives' k ≈
+// 400 step chains at 2 waves per SIMD and cost 1 ms per C3 step at steady
+// state, profiles/r07/lazy_long_c3_v1.txt.)
 template <int MODE, int CPR>
 __global__ __launch_bounds__(256) void k_lazy_rows(LazyTab t, const int32_t* __restrict__ sel, int32_t selv,
                                                    int32_t* __restrict__ last, int64_t rows, int n,
-                                                   float* __restrict__ hist, AdamArgs a, float zero) {
+                                                   float* __restrict__ hist, AdamArgs a) {
+  static_assert(CPR >= 64 && CPR <= 256, "a row slot is whole waves");
   constexpr int RPP = 256 / CPR;   // rows per pass
-  __shared__ float hs[6 * LAZY_WIN];
+  __shared__ f4 hs4[LAZY_WIN * LAZY_HS / 4];
   __shared__ int s_lo;
   __shared__ int32_t rlist[64], rfirst[64];
   __shared__ int nsel;
   const int tid = threadIdx.x;
   const int nr = MODE == 1 ? n - 1 : n;   // newest replayed step
   if (MODE == 1 && blockIdx.x == 0 && tid == 0) {
-    float* h = hist + 6 * (int64_t)(n - 1);
+    float* h = hist + LAZY_HS * (int64_t)(n - 1);
     h[0] = a.w1; h[1] = a.beta2; h[2] = a.c2; h[3] = a.bc2_sqrt; h[4] = a.eps; h[5] = a.neg_step;
+    h[6] = 1.0f / a.bc2_sqrt;
+    h[7] = 0.f;
   }
   const int64_t r0 = (int64_t)blockIdx.x * 64;
   if (tid < 64) {   // wave 0: this workgroup's selected rows, compacted in row order
@@ -382,19 +415,24 @@ __global__ __launch_bounds__(256) void k_lazy_rows(LazyTab t, const int32_t* __r
   __syncthreads();
   const int ns = nsel;
   if (ns == 0) return;   // (uniform)
-  // the scalars of the steps replayed here, the newest LAZY_WIN of them, into LDS
+  // the scalars of the steps replayed here, the newest LAZY_WIN of them, into
+  // LDS (hs row j = step base + j; hist row s − 1 = step s)
   const int base = max(s_lo, nr - LAZY_WIN + 1);
-  for (int i = tid; i < 6 * (nr - base + 1); i += 256) hs[i] = hist[6 * (int64_t)(base - 1) + i];
+  {
+    const f4* src = reinterpret_cast<const f4*>(hist + LAZY_HS * (int64_t)(base - 1));
+    for (int i = tid; i < (LAZY_HS / 4) * (nr - base + 1); i += 256) hs4[i] = src[i];
+  }
   __syncthreads();
+  const float* hs = reinterpret_cast<const float*>(hs4) - LAZY_HS * base;   // hs + LAZY_HS·s = step s
+  const float* hg = hist - LAZY_HS;                                          // hg + LAZY_HS·s = step s
   const int slot = tid / CPR, c = tid % CPR;
   for (int q0 = 0; q0 < ns; q0 += RPP) {
-    const int q = q0 + slot;
+    const int q = q0 + slot;   // (wave-uniform)
     if (q >= ns) break;
     const int64_t r = r0 + rlist[q];
-    const int s0 = rfirst[q];
+    const int s0 = __builtin_amdgcn_readfirstlane(rfirst[q]);
     const bool val = c < t.cols;
     const bool bia = t.Pb != nullptr && c == 0;
-    if (!val && !bia) continue;
     const int64_t i = r * t.cols + (val ? c : 0);
     float p0 = val ? t.P[i] : 0.f, m0 = val ? t.M[i] : 0.f, v0 = val ? t.V[i] : 0.f;
     float p1 = bia ? t.Pb[r] : 0.f, m1 = bia ? t.Mb[r] : 0.f, v1 = bia ? t.Vb[r] : 0.f;
@@ -409,16 +447,15 @@ __global__ __launch_bounds__(256) void k_lazy_rows(LazyTab t, const int32_t* __r
         t.Gb[r] = 0.f;
       }
     }
+    // steps s0 .. base − 1 from hist, max(s0, base) .. nr from the LDS window
+    // (idle lanes of a partial row run the chain on zeros: no branch per lane)
+    const int split = min(base - 1, nr);
     if (__any(bia)) {   // (wave-uniform: only the wave holding a value-0 thread runs the bias chains)
-#pragma unroll 2
-      for (int s = s0; s <= nr; ++s) {
-        const AdamArgs as = hist_args(hist, hs, base, s);
-        adam_elem(p0, m0, v0, zero, as);
-        adam_elem(p1, m1, v1, zero, as);
-      }
+      lazy_replay<true>(p0, m0, v0, p1, m1, v1, hg, s0, split);
+      lazy_replay<true>(p0, m0, v0, p1, m1, v1, hs, max(s0, base), nr);
     } else {
-#pragma unroll 2
-      for (int s = s0; s <= nr; ++s) adam_elem(p0, m0, v0, zero, hist_args(hist, hs, base, s));
+      lazy_replay<false>(p0, m0, v0, p1, m1, v1, hg, s0, split);
+      lazy_replay<false>(p0, m0, v0, p1, m1, v1, hs, max(s0, base), nr);
     }
     if (MODE == 1) {
       adam_elem(p0, m0, v0, g0, a);
@@ -475,9 +512,8 @@ extern "C" int rg_lazy_catch_up(float* P, float* M, float* V, int cols, uint16_t
   if (!lazy_tab_ok(t) || rows <= 0 || !last || n_steps < 0 || (n_steps > 0 && !hist)) return RG_ERR_ARG;
   if (n_steps == 0) return RG_OK;
 #define LZ(CPR) hipLaunchKernelGGL((k_lazy_rows<0, CPR>), dim3(lazy_grid(rows)), dim3(256), 0, stream, t, need, stamp, \
-                                 last, rows, n_steps, hist, AdamArgs{}, 0.f)
-  if (cols <= 32) LZ(32);
-  else if (cols <= 64) LZ(64);
+                                 last, rows, n_steps, hist, AdamArgs{})
+  if (cols <= 64) LZ(64);
   else if (cols <= 128) LZ(128);
   else if (cols <= 256) LZ(256);
   else return RG_ERR_SHAPE;
@@ -493,9 +529,8 @@ extern "C" int rg_lazy_adam_rows(float* P, float* M, float* V, float* G, int col
   if (!lazy_tab_ok(t) || !G || (Pb && !Gb) || rows <= 0 || !last || !tags || step < 1 || !hist || !adam6)
     return RG_ERR_ARG;
 #define LZ(CPR) hipLaunchKernelGGL((k_lazy_rows<1, CPR>), dim3(lazy_grid(rows)), dim3(256), 0, stream, t, tags, tag, last, \
-                                 rows, step, hist, to_args(adam6), 0.f)
-  if (cols <= 32) LZ(32);
-  else if (cols <= 64) LZ(64);
+                                 rows, step, hist, to_args(adam6))
+  if (cols <= 64) LZ(64);
   else if (cols <= 128) LZ(128);
   else if (cols <= 256) LZ(256);
   else return RG_ERR_SHAPE;

@@ -372,6 +372,47 @@ __global__ void k_dd_write(const int32_t* __restrict__ tok_id, const uint32_t* _
   uids[u] = k - 1;   // (same value from every token of an id)
 }
 
+// Host-routed dedup (rg_shard_dedup_ids): the batch's distinct ids come with
+// it from the host (dist.distinct_ids, which the exchange's splits are counted
+// from anyway), sorted, −1 first — the order k_dd_write gives.  map[k] = u for
+// the U distinct mark indices k (only entries of this batch's ids are read
+// afterwards, so the map is never cleared); the tail [T, n_max) of the
+// backward's sort pairs gets the sentinel key.
+__global__ void k_dd_map(const int32_t* __restrict__ uids, int U, int64_t N1, int32_t* __restrict__ map,
+                         const int32_t* __restrict__ n_ptr, int n_max, uint32_t* __restrict__ keys,
+                         int32_t* __restrict__ vals) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < U) map[dd_index(uids[i], N1)] = i;
+  if (i < n_max && i >= *n_ptr) {
+    keys[i] = SENT;
+    vals[i] = i;
+  }
+}
+
+// one workgroup per sorted row r (k_token_ids' layout, csrc/emb_shard.hip):
+// packed token t = offs[r] + τ of s[perm[r]][τ]: tok_id[t] (−1 outside
+// [0, N1), err), uslot[t] = its distinct index, and the backward's sort pair
+// (keys[t], vals[t]) = (uslot[t], t)
+__global__ __launch_bounds__(64) void k_dd_tokens(const int64_t* __restrict__ s, int L,
+                                                  const int32_t* __restrict__ perm, const int32_t* __restrict__ lsort,
+                                                  const int32_t* __restrict__ offs, int64_t N1,
+                                                  const int32_t* __restrict__ map, int32_t* __restrict__ tok_id,
+                                                  int32_t* __restrict__ uslot, uint32_t* __restrict__ keys,
+                                                  int32_t* __restrict__ vals, int32_t* __restrict__ err) {
+  const int r = blockIdx.x;
+  const int b = perm[r], len = lsort[r], base = offs[r];
+  for (int t = threadIdx.x; t < len; t += blockDim.x) {
+    const int64_t id = s[(int64_t)b * L + t];
+    const bool ok = id >= 0 && id < N1;
+    const int u = map[ok ? id + 1 : 0];
+    tok_id[base + t] = ok ? (int32_t)id : -1;
+    uslot[base + t] = u;
+    keys[base + t] = (uint32_t)u;
+    vals[base + t] = base + t;
+    if (!ok && err) atomicOr(err, 1);
+  }
+}
+
 struct DedupLayout {
   size_t keys_in, keys_out, vals_in, vals_out, marks, pos, part_first, part_last, tmp, total, sort_bytes,
       scan_bytes;
@@ -433,6 +474,31 @@ extern "C" int rg_shard_dedup(const int32_t* tok_id, const int32_t* n_ptr, int n
     return RG_ERR_LAUNCH;
   hipLaunchKernelGGL(k_dd_write, g, dim3(256), 0, stream, tok_id, bits, pos, L.nwords, n_ptr, n_max, N1, W, uslot,
                      uids, (uint32_t*)(w + L.keys_in), (int32_t*)(w + L.vals_in), counts, nuniq);
+  RG_LAUNCH_CHECK();
+  return RG_OK;
+}
+
+// rg_shard_dedup with the distinct ids given (sorted, −1 first: uids[0, U))
+// and k_token_ids fused in: two launches instead of six (memset, mark, scan
+// init + scan, write, token ids).  Same uslot / tok_id / sort pairs; the
+// counts and U are the host's.  map: N1 + 1 int32 (one per pass in flight).
+extern "C" int rg_shard_dedup_ids(const int64_t* s, int B, int L, const int32_t* perm, const int32_t* lsort,
+                                  const int32_t* offs, const int32_t* n_ptr, int n_max, int64_t N1,
+                                  const int32_t* uids, int U, int32_t* map, int32_t* tok_id, int32_t* uslot,
+                                  int32_t* err, int E, void* work, int64_t work_bytes, hipStream_t stream) {
+  if (B <= 0 || L <= 0 || n_max <= 0 || N1 <= 0 || N1 >= INT32_MAX || U < 0 || U > n_max + 1 || E <= 0 || !s ||
+      !perm || !lsort || !offs || !n_ptr || !map || !tok_id || !uslot || !work || (U > 0 && !uids))
+    return RG_ERR_ARG;
+  const DedupLayout Ly = dedup_layout(n_max, E, N1);
+  if (work_bytes < (int64_t)Ly.total) return RG_ERR_ARG;
+  char* w = static_cast<char*>(work);
+  uint32_t* keys = (uint32_t*)(w + Ly.keys_in);
+  int32_t* vals = (int32_t*)(w + Ly.vals_in);
+  const int nthr = U > n_max ? U : n_max;
+  hipLaunchKernelGGL(k_dd_map, dim3((unsigned)((nthr + 255) / 256)), dim3(256), 0, stream, uids, U, N1, map, n_ptr,
+                     n_max, keys, vals);
+  hipLaunchKernelGGL(k_dd_tokens, dim3(B), dim3(64), 0, stream, s, L, perm, lsort, offs, N1, map, tok_id, uslot,
+                     keys, vals, err);
   RG_LAUNCH_CHECK();
   return RG_OK;
 }

@@ -134,6 +134,7 @@ SIGNATURES = {
     "rg_shard_dedup_work_bytes": [I, I, I64],
     "rg_shard_dedup": [P, P, I, I64, I, I, P, P, P, P, P, I64, P],
     "rg_shard_dedup_grads": [P, I, I, I64, P, P, I64, P],
+    "rg_shard_dedup_ids": [P, I, I, P, P, P, P, I, I64, P, I, P, P, P, P, I, P, I64, P],
     "rg_neg_pick": [U64, U64, I64, I, I, I64, I64, P, P, P, P, P, P, P],
     "rg_neg_planes": [P, I, I, P, P],
     "rg_target_ids": [P, I, I64, P, P, P],

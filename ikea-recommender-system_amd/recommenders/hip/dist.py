@@ -187,29 +187,43 @@ def item_shard(A, world, rank):
     return (rank * A) // world, ((rank + 1) * A) // world
 
 
-def owner_counts(s, lens, L, packed, n_rows, world):
-    """Per owner rank, the number of DISTINCT item ids among this batch's
-    packed tokens whose table row it holds — the splits of the deduplicated
-    exchange (host restatement of csrc/emb_shard.hip k_token_ids +
-    csrc/segsum.hip rg_shard_dedup: tokens t < clamp(len, 1, L) of every row,
-    all L when unpacked; owner ⌈(id+1)·W/N1⌉ − 1; every id outside [0, N1)
-    is one entry (−1) of rank 0)."""
+def distinct_ids(s, lens, L, packed, n_rows):
+    """The distinct item ids among this batch's packed tokens, sorted, −1
+    first when a token's id is outside [0, n_rows) — the ids the row-sharded
+    table's exchange requests, in the order csrc/segsum.hip rg_shard_dedup
+    ranks them (tokens t < clamp(len, 1, L) of every row, all L when
+    unpacked).  int32."""
     s = np.asarray(s)
     B = s.shape[0]
     ln = np.clip(np.asarray(lens, dtype=np.int64), 1, L) if packed else np.full(B, L, dtype=np.int64)
     ids = s[np.arange(L)[None, :] < ln[:, None]]
     ok = (ids >= 0) & (ids < n_rows)
     # distinct ids through a reusable bitmap over the table (cheaper than a sort
-    # at ~90K tokens): mark, count per owner range, unmark
+    # at ~90K tokens): mark, list, unmark
     mark = _BITMAPS.get(n_rows)
     if mark is None:
         mark = _BITMAPS[n_rows] = np.zeros(n_rows, dtype=np.bool_)
     good = ids[ok]
     mark[good] = True
-    bounds = [(r * n_rows) // world for r in range(world + 1)]
-    out = np.array([np.count_nonzero(mark[bounds[r]:bounds[r + 1]]) for r in range(world)], dtype=np.int64)
+    u = np.flatnonzero(mark).astype(np.int32)
     mark[good] = False
-    out[0] += int(not ok.all())
+    if not ok.all():
+        u = np.concatenate([np.full(1, -1, dtype=np.int32), u])
+    return u
+
+
+def owner_counts(s, lens, L, packed, n_rows, world, uids=None):
+    """Per owner rank, the number of DISTINCT item ids among this batch's
+    packed tokens whose table row it holds — the splits of the deduplicated
+    exchange (host restatement of csrc/emb_shard.hip k_token_ids +
+    csrc/segsum.hip rg_shard_dedup; owner ⌈(id+1)·W/N1⌉ − 1 = the item_shard
+    range holding id; every id outside [0, N1) is one entry (−1) of rank 0).
+    ``uids``: distinct_ids of the batch, when already computed."""
+    u = distinct_ids(s, lens, L, packed, n_rows) if uids is None else uids
+    bad = int(u.size > 0 and u[0] < 0)
+    bounds = [(r * n_rows) // world for r in range(world + 1)]
+    out = np.diff(np.searchsorted(u[bad:], bounds)).astype(np.int64)
+    out[0] += bad
     return out
 
 
@@ -220,10 +234,30 @@ def target_owner_counts(a, n_items, world):
     """Per owner rank, the number of this batch's targets whose output row it
     holds (host restatement of csrc/sampled_shard.hip k_target_ids +
     k_shard_route: owner ⌈(a+1)·W/A⌉ − 1, targets outside [0, A) to rank 0)."""
+    return np.bincount(_target_owners(a, n_items, world), minlength=world).astype(np.int64)
+
+
+def _target_owners(a, n_items, world):
     a = np.asarray(a, dtype=np.int64).reshape(-1)
     ok = (a >= 0) & (a < n_items)
-    own = np.where(ok, ((a + 1) * world + n_items - 1) // n_items - 1, 0)
-    return np.bincount(own, minlength=world).astype(np.int64)
+    return np.where(ok, ((a + 1) * world + n_items - 1) // n_items - 1, 0)
+
+
+def target_route(a, n_items, world):
+    """The sharded sampled head's target exchange from the host batch, as
+    k_target_ids + k_shard_route compute it on the device: one int32 array
+    [t32 | slot | send] of 3·B — t32[b] = a[b] (−1 outside [0, A)), the stable
+    partition of the rows by owner (slot[b] = send position of row b) and
+    send[slot[b]] = t32[b]."""
+    a = np.asarray(a, dtype=np.int64).reshape(-1)
+    B = a.size
+    t32 = np.where((a >= 0) & (a < n_items), a, -1).astype(np.int32)
+    order = np.argsort(_target_owners(a, n_items, world), kind="stable")
+    out = np.empty(3 * B, dtype=np.int32)
+    out[:B] = t32
+    out[B + order] = np.arange(B, dtype=np.int32)
+    out[2 * B:] = t32[order]
+    return out
 
 
 def host_routes(comm, trunk, passes, targets=None):
@@ -232,19 +266,51 @@ def host_routes(comm, trunk, passes, targets=None):
     over the gloo group (W × passes × W ints).  passes: [(s, lens)] host tensors; targets:
     optional (a, n_items) — the item-sharded sampled head's target-row
     exchange, routed the same way (appended last).  Returns
-    [(send_splits, recv_splits)] or None when a batch is already on the device
-    (then the exchange routes on the device and reads the counts back)."""
+    [(send_splits, recv_splits, plan)] — plan: the pass's distinct_ids (the
+    device then skips the dedup's mark / scan, rg_shard_dedup_ids) or, for
+    the targets, their target_route — or None when a batch is already on the
+    device (then the exchange routes on the device and reads the counts back)."""
     for s, ln in passes:
         if torch.as_tensor(s).device.type != "cpu" or torch.as_tensor(ln).device.type != "cpu":
             return None
     if targets is not None and torch.as_tensor(targets[0]).device.type != "cpu":
         return None
-    rows = [owner_counts(torch.as_tensor(s).numpy(), torch.as_tensor(ln).numpy(), torch.as_tensor(s).shape[1],
-                         trunk.packed, trunk.N1, comm.world) for s, ln in passes]
+    plans, rows = [], []
+    for s, ln in passes:
+        s_np = torch.as_tensor(s).numpy()
+        u = distinct_ids(s_np, torch.as_tensor(ln).numpy(), s_np.shape[1], trunk.packed, trunk.N1)
+        plans.append(u)
+        rows.append(owner_counts(None, None, None, None, trunk.N1, comm.world, uids=u))
     if targets is not None:
-        rows.append(target_owner_counts(torch.as_tensor(targets[0]).numpy(), int(targets[1]), comm.world))
+        a_np = torch.as_tensor(targets[0]).numpy()
+        rows.append(target_owner_counts(a_np, int(targets[1]), comm.world))
+        plans.append(target_route(a_np, int(targets[1]), comm.world))
     mine = np.stack(rows)
-    passes = rows
     allc = comm.host_all_gather(torch.from_numpy(mine)).numpy()   # (W, P, W): [q, p, r]
     r = comm.rank
-    return [(allc[r, p, :].tolist(), allc[:, p, r].tolist()) for p in range(len(passes))]
+    return [(allc[r, p, :].tolist(), allc[:, p, r].tolist(), plans[p]) for p in range(len(rows))]
+
+
+class HostStage:
+    """A pinned host buffer for one small per-step host → device copy (the
+    exchange plans of host_routes): the previous copy out of it is waited for
+    before it is overwritten."""
+
+    def __init__(self):
+        self.buf = None
+        self.ev = None
+
+    def to_device(self, arr, dst):
+        """dst[:arr.size] ← arr (int32 numpy) on the current stream; returns that view."""
+        n = int(arr.size)
+        if self.buf is None or self.buf.numel() < n:
+            self.buf = torch.empty(max(n, 1024), dtype=torch.int32).pin_memory()
+            self.ev = None
+        if self.ev is not None:
+            self.ev.synchronize()
+        self.buf.numpy()[:n] = arr
+        out = dst[:n]
+        out.copy_(self.buf[:n], non_blocking=True)
+        self.ev = torch.cuda.Event()
+        self.ev.record()
+        return out

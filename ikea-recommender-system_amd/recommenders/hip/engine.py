@@ -128,12 +128,14 @@ def _round_up(x, m):
 # row moves every step), without the sweep over every row (C3: 1.6 of 3.7 ms).
 # False: the eager sweeps (rg_adam_rows), e.g. for A/B checks.
 LAZY_ADAM = True
+# floats per step of the catch-up history (csrc/optim.hip LAZY_HS)
+LAZY_HS = 8
 
 
 class LazyRows:
     """Catch-up bookkeeping of one table (and an optional one-column
     companion, a head's bias): last[r] = table steps applied to row r, hist
-    = every step's six Adam scalars (written by the step's own kernel), need /
+    = every step's Adam scalars, LAZY_HS floats (written by the step's own kernel), need /
     stamp = the rows a read is about to touch.  ``tab``: (P, M, V, cols, P16,
     Pb, Mb, Vb) device pointers / widths of the table."""
 
@@ -145,7 +147,7 @@ class LazyRows:
         self.stamp = 0
         self.n = 0        # table steps so far
         self.full = 0     # n at the last catch-up of every row
-        self.hist = torch.zeros(256, 6, device=device)
+        self.hist = torch.zeros(256, LAZY_HS, device=device)
 
     def catch_up(self, tab, ids=None, n_ids=0, seed=0, counter=0, S=0, more=()):
         """Bring the rows a read is about to touch — ``n_ids`` int64 ids at
@@ -175,7 +177,7 @@ class LazyRows:
         """Table step n + 1 on the rows tagged ``tag`` (their gradient rows G / Gb)."""
         n = self.n + 1
         if n > self.hist.shape[0]:
-            grown = torch.zeros(2 * self.hist.shape[0], 6, device=self.device)
+            grown = torch.zeros(2 * self.hist.shape[0], LAZY_HS, device=self.device)
             grown[:self.hist.shape[0]].copy_(self.hist)
             self.hist = grown
         P, M, V, cols, P16, Pb, Mb, Vb = tab
@@ -622,12 +624,27 @@ class Trunk:
         need = int(call("rg_shard_dedup_work_bytes", n_max, self.E, self.N1))
         dd = self._xbuf(w, "dd_work", need, dtype=torch.uint8)
         w.dd_nmax = n_max
-        call("rg_token_ids", s.data_ptr(), B, L, w.perm.data_ptr(), w.lsort.data_ptr(), w.offs.data_ptr(), self.N1,
-             w.tok_id[0].data_ptr(), self.err.data_ptr(), st)
-        call("rg_shard_dedup", w.tok_id[0].data_ptr(), w.ntok_ptr, n_max, self.N1, W, self.E, w.uslot.data_ptr(),
-             w.uids.data_ptr(), w.counts.data_ptr(), w.nuniq.data_ptr(), dd.data_ptr(), dd.numel(), st)
+        plan = route[2] if route is not None and len(route) > 2 else None
+        if plan is not None:   # the distinct ids from the host batch: token ids + slots in two launches
+            if getattr(w, "dd_map", None) is None:
+                from .dist import HostStage
+                w.dd_map = torch.empty(self.N1 + 1, dtype=torch.int32, device=self.device)
+                w.dd_stage = HostStage()
+            U = int(plan.size)
+            w.dd_stage.to_device(plan, w.uids)
+            call("rg_shard_dedup_ids", s.data_ptr(), B, L, w.perm.data_ptr(), w.lsort.data_ptr(), w.offs.data_ptr(),
+                 w.ntok_ptr, n_max, self.N1, w.uids.data_ptr(), U, w.dd_map.data_ptr(), w.tok_id[0].data_ptr(),
+                 w.uslot.data_ptr(), self.err.data_ptr(), self.E, dd.data_ptr(), dd.numel(), st)
+        else:
+            call("rg_token_ids", s.data_ptr(), B, L, w.perm.data_ptr(), w.lsort.data_ptr(), w.offs.data_ptr(),
+                 self.N1, w.tok_id[0].data_ptr(), self.err.data_ptr(), st)
+            call("rg_shard_dedup", w.tok_id[0].data_ptr(), w.ntok_ptr, n_max, self.N1, W, self.E,
+                 w.uslot.data_ptr(), w.uids.data_ptr(), w.counts.data_ptr(), w.nuniq.data_ptr(), dd.data_ptr(),
+                 dd.numel(), st)
         if route is not None:
             w.send_splits, w.recv_splits = list(route[0]), list(route[1])
+            if plan is not None and sum(w.send_splits) != U:
+                raise RuntimeError(f"host exchange plan: {U} distinct ids, splits {w.send_splits}")
         else:
             comm.all_gather(w.counts_all, w.counts)
             M = w.counts_all.view(W, W).cpu()            # M[q][r]: distinct ids of rank q owned by rank r (one sync)
@@ -1672,8 +1689,11 @@ class ShardedSampledHead(SampledSoftmaxHead):
             w.Wp = torch.empty(S * HF * 6, dtype=torch.uint8, device=dev)
             w.nloc = z(S, dt=torch.int32)
             w.nS = torch.full((1,), S, dtype=torch.int32, device=dev)
-            w.t32, w.nt = z(B, dt=torch.int32), z(1, dt=torch.int32)
-            w.tslot, w.tsend = z(B, dt=torch.int32), z(B, dt=torch.int32)
+            w.troute = z(3 * B, dt=torch.int32)   # t32 | slot | send (one host → device copy)
+            w.t32, w.tslot, w.tsend = w.troute[:B], w.troute[B:2 * B], w.troute[2 * B:]
+            w.nt = z(1, dt=torch.int32)
+            from .dist import HostStage
+            w.tstage = HostStage()
             w.tcounts = z(self.comm.world, dt=torch.int32)
             w.tW, w.tb = z(B, HF), z(B)
             w.trow = z(B, dt=torch.int64)
@@ -1708,9 +1728,13 @@ class ShardedSampledHead(SampledSoftmaxHead):
             comm.all_reduce(w.wgb)
             call("rg_neg_planes", w.Wg.data_ptr(), S, HF, w.Wp.data_ptr(), st)
             # the rank's targets' rows and biases from their owners
-            call("rg_target_ids", tgt.data_ptr(), B, self.A_full, w.t32.data_ptr(), w.nt.data_ptr(), st)
-            call("rg_shard_route", w.t32.data_ptr(), w.nt.data_ptr(), self.A_full, comm.world, w.tslot.data_ptr(),
-                 w.tsend.data_ptr(), w.tcounts.data_ptr(), st)
+            plan = route[2] if route is not None and len(route) > 2 else None
+            if plan is not None:   # t32 | slot | send from the host batch (dist.target_route)
+                w.tstage.to_device(plan, w.troute)
+            else:
+                call("rg_target_ids", tgt.data_ptr(), B, self.A_full, w.t32.data_ptr(), w.nt.data_ptr(), st)
+                call("rg_shard_route", w.t32.data_ptr(), w.nt.data_ptr(), self.A_full, comm.world,
+                     w.tslot.data_ptr(), w.tsend.data_ptr(), w.tcounts.data_ptr(), st)
             if route is not None:
                 w.send_splits, w.recv_splits = list(route[0]), list(route[1])
             else:

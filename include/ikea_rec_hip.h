@@ -295,15 +295,15 @@ int rg_adam_dense(float* P, float* M, float* V, float* G, int64_t n, const float
 int rg_adam_rows(float* P, float* M, float* V, float* G, const int32_t* tags, int32_t tag, int64_t rows, int cols,
                  const float* adam6, rg_stream_t stream);
 /* Catch-up Adam (dense semantics, bitwise): a table read a few rows at a time (the
- * embedding, the sampled head) keeps last[r] = table steps applied to row r and hist (float[6] per
- * step, step s at 6·(s − 1)) = every step's adam6; a row's zero-gradient steps are replayed only
+ * embedding, the sampled head) keeps last[r] = table steps applied to row r and hist (float[8] per
+ * step, step s at 8·(s − 1): adam6, RN(1 / adam6[3]), 0) = every step's scalars; a row's zero-gradient steps are replayed only
  * before it is read.  Replaces rg_adam_rows' sweep over every row (GRU4Rec/model.py:124-127,153).
  * rg_lazy_mark_rows: need[id] = stamp for the n int64 ids in [0, rows) and, with S > 0, the S
  *   negatives of draw `counter` (rg_sample_uniform's stream over [0, rows)).
  * rg_lazy_catch_up: rows with need[r] == stamp (need NULL: every row) replay steps
  *   last[r] + 1 .. n_steps with g = 0; P16 (optional) = fp16(P) of those rows; Pb / Mb / Vb
  *   (optional): a one-column companion table (a head's bias) sharing last[].
- * rg_lazy_adam_rows: table step `step` (hist[step − 1] = adam6): rows with tags[r] == tag replay
+ * rg_lazy_adam_rows: table step `step` (writes hist row step − 1): rows with tags[r] == tag replay
  *   last[r] + 1 .. step − 1, then step with their gradient rows G (Gb), cleared; last[r] = step.
  *   Rows without a gradient are not touched. */
 int rg_lazy_mark_rows(const int64_t* ids, int64_t n, int64_t rows, uint64_t seed, uint64_t counter, int S,
@@ -515,6 +515,10 @@ int rg_bpr_dz(float* Z, int64_t zsb, int64_t zss, const float* zpos, int B, int 
  * rg_shard_dedup_grads: gsend[u] = Σ_{t : uslot[t] = u} src[t] (E floats per row, summed in token
  *   order — a stable sort of the pairs by u, then segmented sums: deterministic), for the pass's
  *   last rg_shard_dedup on `work` (same n_max, n_rows).
+ * rg_shard_dedup_ids: rg_token_ids + rg_shard_dedup in two launches when the host batch gives the
+ *   distinct ids (uids[0..U), sorted, -1 first: dist.distinct_ids, which the host counts the
+ *   exchange's splits from): the same tok_id / uslot and the (u, t) pairs in `work` for
+ *   rg_shard_dedup_grads; map: n_rows + 1 int32 scratch (never cleared; one per pass in flight).
  * rg_shard_route: stable partition of the T = *ntok_ptr rows by owner rank: slot[t] (send
  *   position), send_ids[slot[t]] = tok_id[t], counts[world] (world <= 8; the sharded sampled
  *   head's per-row target exchange).
@@ -533,6 +537,10 @@ int rg_shard_dedup(const int32_t* tok_id, const int32_t* n_ptr, int n_max, int64
                    rg_stream_t stream);
 int rg_shard_dedup_grads(const float* src, int E, int n_max, int64_t n_rows, float* gsend, void* work,
                          int64_t work_bytes, rg_stream_t stream);
+int rg_shard_dedup_ids(const int64_t* s, int B, int L, const int32_t* perm, const int32_t* lsort, const int32_t* offs,
+                       const int32_t* n_ptr, int n_max, int64_t n_rows, const int32_t* uids, int U, int32_t* map,
+                       int32_t* tok_id, int32_t* uslot, int32_t* err, int E, void* work, int64_t work_bytes,
+                       rg_stream_t stream);
 int rg_shard_route(const int32_t* tok_id, const int32_t* ntok_ptr, int64_t n_rows, int world, int32_t* slot,
                    int32_t* send_ids, int32_t* counts, rg_stream_t stream);
 int rg_rows_gather(const int32_t* ids, int n, int64_t lo, int64_t n_local, const void* table, int E, int half,

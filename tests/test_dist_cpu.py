@@ -175,3 +175,33 @@ def test_target_owner_counts_match_item_shard():
                 o = next(r for r in range(W) if item_shard(A, W, r)[0] <= t < item_shard(A, W, r)[1])
             exp[o] += 1
         np.testing.assert_array_equal(target_owner_counts(a, A, W), exp)
+
+
+def test_distinct_ids_and_target_route_match_the_device_rules():
+    """dist.distinct_ids = the sorted distinct ids rg_shard_dedup ranks (−1
+    first for invalid tokens), and dist.target_route = k_target_ids +
+    k_shard_route's stable partition of the targets by owner."""
+    import numpy as np
+    sys.path.insert(0, os.path.join(REPO, "ikea-recommender-system_amd"))
+    from recommenders.hip.dist import distinct_ids, item_shard, target_route
+    rng = np.random.default_rng(5)
+    for N1, L, packed, lo_id in ((1001, 7, True, -2), (50, 5, False, 0), (9, 4, True, -2)):
+        s = rng.integers(lo_id, N1 + (3 if lo_id < 0 else 0), size=(13, L))
+        lens = rng.integers(0, L + 3, size=13)
+        toks = set()
+        for b in range(13):
+            n = L if not packed else min(max(int(lens[b]), 1), L)
+            toks |= {int(x) if 0 <= x < N1 else -1 for x in s[b, :n]}
+        u = distinct_ids(s, lens, L, packed, N1)
+        assert u.dtype == np.int32 and u.tolist() == sorted(toks)
+    for A, W in ((9001, 3), (37, 2), (1000, 1)):
+        a = rng.integers(-3, A + 3, size=200)
+        plan = target_route(a, A, W)
+        B = a.size
+        t32 = [int(x) if 0 <= x < A else -1 for x in a]
+        owner = [0 if t < 0 else next(r for r in range(W) if item_shard(A, W, r)[0] <= t < item_shard(A, W, r)[1])
+                 for t in t32]
+        order = [b for o in range(W) for b in range(B) if owner[b] == o]
+        assert plan[:B].tolist() == t32
+        assert plan[2 * B:].tolist() == [t32[b] for b in order]
+        assert [int(plan[B + b]) for b in order] == list(range(B))

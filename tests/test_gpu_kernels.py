@@ -582,6 +582,69 @@ def test_shard_dedup_distinct_ids_and_sums(n_rows, W, n, n_max, E, zipf):
     assert torch.equal(g1[:U], g2[:U])   # fixed order: bitwise repeatable, stored not added
 
 
+@pytest.mark.parametrize("n_rows,B,L,packed,bad", [(1_000_001, 4096, 50, True, True), (53, 37, 9, False, False),
+                                                   (9001, 64, 20, True, False), (5_000_001, 512, 50, True, True)])
+def test_shard_dedup_ids_equals_the_device_dedup(n_rows, B, L, packed, bad):
+    """rg_shard_dedup_ids (the distinct ids from the host batch, dist.distinct_ids)
+    against rg_token_ids + rg_shard_dedup on the same packed batch: tok_id,
+    uslot, the distinct ids, the error flag and rg_shard_dedup_grads' per-id
+    sums from the work pairs — all bitwise; the map is reused across batches
+    without clearing."""
+    from recommenders.hip.dist import distinct_ids
+    rng = np.random.default_rng(n_rows + B)
+    call = C().call
+    E = 64
+    for rep in range(2):
+        s = ((rng.zipf(1.3, size=(B, L)) - 1) % n_rows).astype(np.int64)
+        if bad:
+            s[rng.integers(0, B, 4), rng.integers(0, 3, 4)] = -1
+            s[rng.integers(0, B, 2), 0] = n_rows + 5
+        lens = rng.integers(0, L + 2, size=B).astype(np.int64)
+        sd, ld = D(torch.from_numpy(s)), D(torch.from_numpy(lens))
+        perm = torch.empty(B, dtype=torch.int32, device=dev)
+        lsort = torch.empty(B, dtype=torch.int32, device=dev)
+        offs = torch.empty(B + 1, dtype=torch.int32, device=dev)
+        call("rg_pack", ld.data_ptr(), B, L, 0 if packed else 1, perm.data_ptr(), lsort.data_ptr(), offs.data_ptr(),
+             st())
+        nptr = offs.data_ptr() + 4 * B
+        n_max = B * L
+        wb = call("rg_shard_dedup_work_bytes", n_max, E, n_rows)
+        outs = []
+        for host in (False, True):
+            work = torch.full((wb,), 0x5A, dtype=torch.uint8, device=dev)
+            tok = torch.full((n_max,), -9, dtype=torch.int32, device=dev)
+            uslot = torch.full((n_max,), -9, dtype=torch.int32, device=dev)
+            uids = torch.full((n_max,), -9, dtype=torch.int32, device=dev)
+            err = torch.zeros(1, dtype=torch.int32, device=dev)
+            if host:
+                u = distinct_ids(s, lens, L, packed, n_rows)
+                uids[:u.size] = D(torch.from_numpy(u))
+                if rep == 0:
+                    dd_map = torch.full((n_rows + 1,), 0x7FFF, dtype=torch.int32, device=dev)
+                call("rg_shard_dedup_ids", sd.data_ptr(), B, L, perm.data_ptr(), lsort.data_ptr(), offs.data_ptr(),
+                     nptr, n_max, n_rows, uids.data_ptr(), int(u.size), dd_map.data_ptr(), tok.data_ptr(),
+                     uslot.data_ptr(), err.data_ptr(), E, work.data_ptr(), wb, st())
+                U = int(u.size)
+            else:
+                nuniq = torch.zeros(1, dtype=torch.int32, device=dev)
+                call("rg_token_ids", sd.data_ptr(), B, L, perm.data_ptr(), lsort.data_ptr(), offs.data_ptr(), n_rows,
+                     tok.data_ptr(), err.data_ptr(), st())
+                call("rg_shard_dedup", tok.data_ptr(), nptr, n_max, n_rows, 4, E, uslot.data_ptr(), uids.data_ptr(),
+                     torch.zeros(4, dtype=torch.int32, device=dev).data_ptr(), nuniq.data_ptr(), work.data_ptr(), wb,
+                     st())
+                U = int(nuniq.item())
+            T = int(offs[B].item())
+            src = D(torch.from_numpy(rng.standard_normal((n_max, E)).astype(np.float32))) if not host else outs[0][5]
+            g = torch.full((n_max, E), 3.0, device=dev)
+            call("rg_shard_dedup_grads", src.data_ptr(), E, n_max, n_rows, g.data_ptr(), work.data_ptr(), wb, st())
+            torch.cuda.synchronize()
+            outs.append((tok[:T].clone(), uslot[:T].clone(), uids[:U].clone(), int(err.item()), g[:U].clone(), src))
+        (t0, s0, u0, e0, g0, _), (t1, s1, u1, e1, g1, _) = outs
+        assert torch.equal(t0, t1) and torch.equal(s0, s1) and torch.equal(u0, u1) and e0 == e1
+        assert e1 == (1 if bad else 0)
+        assert torch.equal(g0, g1)
+
+
 @pytest.mark.parametrize("nplanes", [3, 1])
 @pytest.mark.parametrize("A,HF,nh", [(20011, 128, 3), (777, 256, 2), (1000, 64, 3), (4096, 32, 1)])
 def test_qcomb_equals_weighted_sum_planes_norm(A, HF, nh, nplanes):

@@ -91,6 +91,70 @@ def test_lazy_rows_equal_the_eager_sweep_bitwise(rows, cols, bias, half):
     assert torch.count_nonzero(lG) == 0 and int((lz.last != 20).sum()) == 0
 
 
+@pytest.mark.parametrize("cols,bias", [(64, False), (256, True)])
+def test_lazy_chains_longer_than_the_lds_window_bitwise(cols, bias):
+    """1100 table steps (the kernel stages the newest 1024 steps' scalars in
+    LDS and reads older ones from hist): rows 0–9 get gradients every step
+    (magnitudes 1e-3 down to 1e-22, so v reaches the denormal range and √v
+    the scaled path), rows 10–19 are read every step, rows 20–39 at step 500
+    only, the rest never until the end (m = v = 0 rows included).  Every row
+    equals the eager sweep bit for bit."""
+    from recommenders.hip.engine import AdamClock, LazyRows
+    rows, steps = 300, 1100
+    g = torch.Generator().manual_seed(cols)
+    P0 = torch.randn(rows, cols, generator=g) * 0.05
+    b0 = torch.randn(rows, generator=g) * 0.05
+    eP, eM, eV = P0.clone().to(dev), torch.zeros(rows, cols, device=dev), torch.zeros(rows, cols, device=dev)
+    eb, ebm, ebv = b0.clone().to(dev), torch.zeros(rows, device=dev), torch.zeros(rows, device=dev)
+    lP, lM, lV = P0.clone().to(dev), torch.zeros(rows, cols, device=dev), torch.zeros(rows, cols, device=dev)
+    lb, lbm, lbv = b0.clone().to(dev), torch.zeros(rows, device=dev), torch.zeros(rows, device=dev)
+    lz = LazyRows(rows, dev)
+    tab = (lP.data_ptr(), lM.data_ptr(), lV.data_ptr(), cols, None,
+           lb.data_ptr() if bias else None, lbm.data_ptr() if bias else None, lbv.data_ptr() if bias else None)
+    eG, lG = torch.zeros(rows, cols, device=dev), torch.zeros(rows, cols, device=dev)
+    eGb, lGb = torch.zeros(rows, device=dev), torch.zeros(rows, device=dev)
+    etags = torch.zeros(rows, dtype=torch.int32, device=dev)
+    ltags = torch.zeros(rows, dtype=torch.int32, device=dev)
+    scale = (10.0 ** -torch.linspace(3, 22, 10)).view(10, 1)
+    # the first 60 steps carry gradients on rows 0-39 (so the rows read late have non-zero moments)
+    early = torch.arange(40, device=dev)
+    hot = torch.arange(10, device=dev)
+    reads = torch.arange(10, 20, device=dev).long()
+    mid = torch.arange(20, 40, device=dev).long()
+    clock = AdamClock(0.01)
+    st = _st()
+    for step in range(1, steps + 1):
+        sd = early if step <= 60 else hot
+        G = torch.randn(sd.numel(), cols, generator=g) * (scale.repeat(4, 1) if step <= 60 else scale)
+        Gb = G[:, 0].clone()
+        eG[sd] = G.to(dev)
+        lG[sd] = G.to(dev)
+        eGb[sd] = Gb.to(dev)
+        lGb[sd] = Gb.to(dev)
+        etags[sd] = step
+        ltags[sd] = step
+        a6 = clock.next_args()
+        _call("rg_adam_rows", eP.data_ptr(), eM.data_ptr(), eV.data_ptr(), eG.data_ptr(), etags.data_ptr(), step,
+              rows, cols, a6, st)
+        if bias:
+            _call("rg_adam_rows", eb.data_ptr(), ebm.data_ptr(), ebv.data_ptr(), eGb.data_ptr(), etags.data_ptr(),
+                  step, rows, 1, a6, st)
+        lz.adam(tab, lG.data_ptr(), lGb.data_ptr() if bias else None, ltags.data_ptr(), step, a6)
+        lz.catch_up(tab, reads.data_ptr(), reads.numel())
+        if step == 500:
+            lz.catch_up(tab, mid.data_ptr(), mid.numel())
+            assert torch.equal(lP[mid], eP[mid]) and torch.equal(lV[mid], eV[mid])
+    assert torch.equal(lP[reads], eP[reads]) and torch.equal(lM[reads], eM[reads])
+    assert float(eV[20:40].min()) < 1.2e-38   # denormal second moments are replayed
+    lz.materialize(tab)
+    torch.cuda.synchronize()
+    for a, e in ((lP, eP), (lM, eM), (lV, eV)):
+        assert torch.equal(a, e)
+    if bias:
+        for a, e in ((lb, eb), (lbm, ebm), (lbv, ebv)):
+            assert torch.equal(a, e)
+
+
 def _pair(monkeypatch, make):
     """(eager trainer, catch-up trainer) built the same way."""
     from recommenders.hip import engine
