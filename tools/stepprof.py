@@ -22,6 +22,7 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--config", default="c5")
 ap.add_argument("--steps", type=int, default=4)
 ap.add_argument("--warmup", type=int, default=2)
+ap.add_argument("--nbatch", type=int, default=0, help="distinct batches, cycled (0: one per step)")
 ap.add_argument("--shard", action="store_true",
                 help="item-sharded trainer over a one-rank process group (RANK / WORLD_SIZE / MASTER_* from the env)")
 a = ap.parse_args()
@@ -37,9 +38,10 @@ if a.shard:
     torch.distributed.init_process_group("nccl")
 B, L, N = args.batch, args.seq, args.items
 n = a.warmup + a.steps
-st = SessionStream(N, L, B * n, seed=2)
+nb = min(n, a.nbatch) if a.nbatch > 0 else n
+st = SessionStream(N, L, B * nb, seed=2)
 args.item_counts = st.item_counts()
-batches = [bench.pinned(st.batch(i, B)) for i in range(n)]
+batches = [bench.pinned(st.batch(i, B)) for i in range(nb)]
 tr = bench.make_trainer(a.config, args, dev, a.shard)
 tr.set_train()
 x = torch.zeros(4, device=dev)
@@ -53,10 +55,10 @@ def marker():
 
 
 for i in range(a.warmup):
-    tr.train_step(*bench.step_args(a.config, batches[i]))
+    tr.train_step(*bench.step_args(a.config, batches[i % nb]))
 marker()
 for i in range(a.warmup, n):
-    tr.train_step(*bench.step_args(a.config, batches[i]))
+    tr.train_step(*bench.step_args(a.config, batches[i % nb]))
 marker()
 print(f"stepprof: {a.config} {a.steps} steps between the markers", flush=True)
 if a.shard:
