@@ -322,8 +322,12 @@ struct LazyTab {
 // hist row s − 1 = step s's scalars, LAZY_HS floats: the six of AdamArgs, then
 // RN(1 / bc2_sqrt) (written by the step's own kernel) and a pad to 32 bytes
 constexpr int LAZY_HS = 8;
-// the newest LAZY_WIN steps a workgroup replays are staged in LDS
-constexpr int LAZY_WIN = 1024;
+// the newest LAZY_WIN steps a workgroup replays are staged in LDS (0: none,
+// every step's scalars by scalar loads from hist)
+#ifndef LAZY_WIN_STEPS
+#define LAZY_WIN_STEPS 1024
+#endif
+constexpr int LAZY_WIN = LAZY_WIN_STEPS;
 
 // One replayed step, g = 0: adam_elem(p, m, v, 0, a) bit for bit, in fewer
 // operations (h0 = (w1, β2, c2, bc2_sqrt), h1 = (ε, neg_step, RN(1/bc2_sqrt), ·)):
@@ -379,7 +383,7 @@ __global__ __launch_bounds__(256) void k_lazy_rows(LazyTab t, const int32_t* __r
                                                    float* __restrict__ hist, AdamArgs a) {
   static_assert(CPR >= 64 && CPR <= 256, "a row slot is whole waves");
   constexpr int RPP = 256 / CPR;   // rows per pass
-  __shared__ f4 hs4[LAZY_WIN * LAZY_HS / 4];
+  __shared__ f4 hs4[LAZY_WIN > 0 ? LAZY_WIN * LAZY_HS / 4 : 1];
   __shared__ int s_lo;
   __shared__ int32_t rlist[64], rfirst[64];
   __shared__ int nsel;
@@ -417,8 +421,8 @@ __global__ __launch_bounds__(256) void k_lazy_rows(LazyTab t, const int32_t* __r
   if (ns == 0) return;   // (uniform)
   // the scalars of the steps replayed here, the newest LAZY_WIN of them, into
   // LDS (hs row j = step base + j; hist row s − 1 = step s)
-  const int base = max(s_lo, nr - LAZY_WIN + 1);
-  {
+  const int base = LAZY_WIN > 0 ? max(s_lo, nr - LAZY_WIN + 1) : nr + 1;
+  if (LAZY_WIN > 0) {
     const f4* src = reinterpret_cast<const f4*>(hist + LAZY_HS * (int64_t)(base - 1));
     for (int i = tid; i < (LAZY_HS / 4) * (nr - base + 1); i += 256) hs4[i] = src[i];
   }

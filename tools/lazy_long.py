@@ -26,6 +26,7 @@ ap.add_argument("--config", default="c3")
 ap.add_argument("--steps", type=int, default=800)
 ap.add_argument("--window", type=int, default=100)
 ap.add_argument("--nbatch", type=int, default=100)
+ap.add_argument("--lazy-only", action="store_true", help="no eager twin (A/B of catch-up variants)")
 a = ap.parse_args()
 sys.argv = [sys.argv[0]]
 args = bench.parse()
@@ -35,14 +36,15 @@ st = SessionStream(N, L, B * a.nbatch, seed=2)
 args.item_counts = st.item_counts()
 batches = [bench.pinned(st.batch(i, B)) for i in range(a.nbatch)]
 trs = {}
-for lazy in (True, False):
+modes = (True,) if a.lazy_only else (True, False)
+for lazy in modes:
     engine.LAZY_ADAM = lazy
     trs[lazy] = bench.make_trainer(a.config, args, dev, False)
     trs[lazy].set_train()
 engine.LAZY_ADAM = True
 for w0 in range(0, a.steps, a.window):
     out = []
-    for lazy in (True, False):
+    for lazy in modes:
         tr = trs[lazy]
         torch.cuda.synchronize()
         t0 = time.perf_counter()
