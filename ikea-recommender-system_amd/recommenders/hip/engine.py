@@ -130,6 +130,9 @@ def _round_up(x, m):
 LAZY_ADAM = True
 # floats per step of the catch-up history (csrc/optim.hip LAZY_HS)
 LAZY_HS = 8
+# a sampled head's backward queues the catch-up of the next draw's negatives on
+# a side stream (LazyRows.catch_up_async), under the trunk backward
+PREFETCH_NEGATIVES = True
 
 
 class LazyRows:
@@ -148,6 +151,8 @@ class LazyRows:
         self.n = 0        # table steps so far
         self.full = 0     # n at the last catch-up of every row
         self.hist = torch.zeros(256, LAZY_HS, device=device)
+        self.side = None      # stream of catch_up_async
+        self.pending = None   # its event, until a use of the table joins it
 
     def catch_up(self, tab, ids=None, n_ids=0, seed=0, counter=0, S=0, more=()):
         """Bring the rows a read is about to touch — ``n_ids`` int64 ids at
@@ -155,6 +160,7 @@ class LazyRows:
         id sets of ``more`` — up to date.  On the stream every read of the
         table is ordered behind (two streams must not catch up one table
         concurrently: the double-Q step catches up all its passes' rows first)."""
+        self.join()
         if self.n == self.full or n_ids + S + sum(n for _, n in more) == 0:
             return
         st = stream_ptr()
@@ -165,9 +171,34 @@ class LazyRows:
         call("rg_lazy_catch_up", *tab, self.rows, self.last.data_ptr(), self.need.data_ptr(), self.stamp, self.n,
              self.hist.data_ptr(), st)
 
+    def catch_up_async(self, tab, seed, counter, S):
+        """catch_up of the S negatives of draw ``counter`` on a side stream,
+        ordered after everything queued so far on the current stream (the
+        step's own Adam): it runs under the rest of the step (the trunk
+        backward, the next step's trunk forward).  The next use of the table
+        on any stream — catch_up, adam, materialize — joins it first."""
+        self.join()
+        if self.n == self.full or S == 0:
+            return
+        cur = torch.cuda.current_stream(self.device)
+        if self.side is None:
+            self.side = torch.cuda.Stream(device=self.device)
+        self.side.wait_stream(cur)
+        with torch.cuda.stream(self.side):
+            self.catch_up(tab, None, 0, seed, counter, S)
+        self.pending = torch.cuda.Event()
+        self.pending.record(self.side)
+
+    def join(self):
+        """Order the current stream after a pending catch_up_async."""
+        if self.pending is not None:
+            torch.cuda.current_stream(self.device).wait_event(self.pending)
+            self.pending = None
+
     def materialize(self, tab):
         """Every row up to date (before a read of the whole table: evaluation,
         state_dict, the optimizer state, a load)."""
+        self.join()
         if self.n > self.full:
             call("rg_lazy_catch_up", *tab, self.rows, self.last.data_ptr(), None, 0, self.n, self.hist.data_ptr(),
                  stream_ptr())
@@ -175,6 +206,7 @@ class LazyRows:
 
     def adam(self, tab, G, Gb, tags, tag, adam6):
         """Table step n + 1 on the rows tagged ``tag`` (their gradient rows G / Gb)."""
+        self.join()
         n = self.n + 1
         if n > self.hist.shape[0]:
             grown = torch.zeros(2 * self.hist.shape[0], LAZY_HS, device=self.device)
@@ -1471,6 +1503,7 @@ class SampledSoftmaxHead(SoftmaxHead):
         # every row before any other read — the W / b properties, named_params, evaluation
         self.lazy = LazyRows(self.A, device) if LAZY_ADAM and shard is None else None
         self._ready_draw = -1
+        self._neg_draw = -1   # the draw whose negatives catch_up_async already queued
 
     # the step's own kernels use _Wp / _bp (their rows are caught up by
     # prepare_rows); every other access goes through these properties
@@ -1510,7 +1543,8 @@ class SampledSoftmaxHead(SoftmaxHead):
         """Catch up the rows the next forward_loss reads: its B targets (device
         int64) and the S negatives of draw ``self.draws``."""
         if self.lazy is not None and self._ready_draw != self.draws:
-            self.lazy.catch_up(self._lazy_tab(), tgt.data_ptr(), B, self.seed, self.draws, self.S)
+            S = 0 if self._neg_draw == self.draws else self.S   # (the negatives: queued by the last backward)
+            self.lazy.catch_up(self._lazy_tab(), tgt.data_ptr(), B, self.seed, self.draws, S)
             self._ready_draw = self.draws
 
     def split_terms(self, B):
@@ -1643,6 +1677,9 @@ class SampledSoftmaxHead(SoftmaxHead):
             if self.lazy is not None:   # the touched rows only (catch-up Adam)
                 self.lazy.adam(self._lazy_tab(), self.G.data_ptr(), self.Gb.data_ptr(), self.tags.data_ptr(),
                                self.tag, adam6)
+                if PREFETCH_NEGATIVES:   # the next draw's negatives, caught up under the rest of the step
+                    self.lazy.catch_up_async(self._lazy_tab(), self.seed, self.draws, self.S)
+                    self._neg_draw = self.draws
                 return
             call("rg_adam_rows", self.W.p.data_ptr(), self.W.m.data_ptr(), self.W.v.data_ptr(), self.G.data_ptr(),
                  self.tags.data_ptr(), self.tag, self.A, HF, adam6, st)

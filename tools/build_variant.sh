@@ -12,6 +12,6 @@ mkdir -p abvar
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++17 -Wno-unused-result "$@" \
   -I ikea-recommender-system_amd/csrc -c "ikea-recommender-system_amd/csrc/$base.hip" -o abvar/${base}_$name.o
 others=$(ls $obj/*.o | grep -v "/$base.o\$")
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC abvar/${base}_$name.o $others -o abvar/lib_$name.so
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC abvar/${base}_$name.o $others -L/opt/rocm/lib -lrccl -o abvar/lib_$name.so
 rm -f abvar/${base}_$name.o
 echo abvar/lib_$name.so

@@ -27,6 +27,7 @@ ap.add_argument("--steps", type=int, default=800)
 ap.add_argument("--window", type=int, default=100)
 ap.add_argument("--nbatch", type=int, default=100)
 ap.add_argument("--lazy-only", action="store_true", help="no eager twin (A/B of catch-up variants)")
+ap.add_argument("--prefetch", type=int, default=1, help="engine.PREFETCH_NEGATIVES")
 a = ap.parse_args()
 sys.argv = [sys.argv[0]]
 args = bench.parse()
@@ -36,6 +37,7 @@ st = SessionStream(N, L, B * a.nbatch, seed=2)
 args.item_counts = st.item_counts()
 batches = [bench.pinned(st.batch(i, B)) for i in range(a.nbatch)]
 trs = {}
+engine.PREFETCH_NEGATIVES = bool(a.prefetch)
 modes = (True,) if a.lazy_only else (True, False)
 for lazy in modes:
     engine.LAZY_ADAM = lazy
