@@ -322,13 +322,6 @@ struct LazyTab {
 // hist row s − 1 = step s's scalars, LAZY_HS floats: the six of AdamArgs, then
 // RN(1 / bc2_sqrt) (written by the step's own kernel) and a pad to 32 bytes
 constexpr int LAZY_HS = 8;
-// the newest LAZY_WIN steps a workgroup replays are staged in LDS (0: none,
-// every step's scalars by scalar loads from hist)
-#ifndef LAZY_WIN_STEPS
-#define LAZY_WIN_STEPS 1024
-#endif
-constexpr int LAZY_WIN = LAZY_WIN_STEPS;
-
 // One replayed step, g = 0: adam_elem(p, m, v, 0, a) bit for bit, in fewer
 // operations (h0 = (w1, β2, c2, bc2_sqrt), h1 = (ε, neg_step, RN(1/bc2_sqrt), ·)):
 //  * m: w1·(0 − m) + m — 0 − m and −m differ only at m = ±0, where the fma
@@ -352,13 +345,16 @@ __device__ __forceinline__ void adam_zero_step(float& p, float& m, float& v, con
 }
 
 // steps lo .. hi (inclusive) of one value (and, with BIAS, of the companion
-// value) from rows of h (hist in global memory or the LDS window)
+// value); the step scalars by scalar loads from hist (wave-uniform addresses:
+// every workgroup reads the same rows, L2 / scalar-cache hits — staging them
+// in LDS measured slower, 2.40 vs 2.43 (256 steps) vs 2.45 ms (1024) per C3
+// step at steady state, profiles/r07/ab_lazy_window_prefetch.txt)
 template <bool BIAS>
 __device__ __forceinline__ void lazy_replay(float& p0, float& m0, float& v0, float& p1, float& m1, float& v1,
-                                            const float* h, int lo, int hi) {
+                                            const float* __restrict__ h, int lo, int hi) {
 #pragma unroll 2
   for (int s = lo; s <= hi; ++s) {
-    const f4* r = reinterpret_cast<const f4*>(h + LAZY_HS * s);
+    const f4* r = reinterpret_cast<const f4*>(h + LAZY_HS * (int64_t)s);
     const f4 h0 = r[0], h1 = r[1];
     adam_zero_step(p0, m0, v0, h0, h1);
     if (BIAS) adam_zero_step(p1, m1, v1, h0, h1);
@@ -383,8 +379,6 @@ __global__ __launch_bounds__(256) void k_lazy_rows(LazyTab t, const int32_t* __r
                                                    float* __restrict__ hist, AdamArgs a) {
   static_assert(CPR >= 64 && CPR <= 256, "a row slot is whole waves");
   constexpr int RPP = 256 / CPR;   // rows per pass
-  __shared__ f4 hs4[LAZY_WIN > 0 ? LAZY_WIN * LAZY_HS / 4 : 1];
-  __shared__ int s_lo;
   __shared__ int32_t rlist[64], rfirst[64];
   __shared__ int nsel;
   const int tid = threadIdx.x;
@@ -407,28 +401,12 @@ __global__ __launch_bounds__(256) void k_lazy_rows(LazyTab t, const int32_t* __r
       rlist[pos] = tid;
       rfirst[pos] = lst + 1;
     }
-    const int lo = go ? lst + 1 : INT32_MAX;
-    int m = lo;
-#pragma unroll
-    for (int d = 1; d < 64; d *= 2) m = min(m, __shfl_xor(m, d));
-    if (tid == 0) {
-      nsel = __builtin_popcountll(mask);
-      s_lo = m;
-    }
+    if (tid == 0) nsel = __builtin_popcountll(mask);
   }
   __syncthreads();
   const int ns = nsel;
   if (ns == 0) return;   // (uniform)
-  // the scalars of the steps replayed here, the newest LAZY_WIN of them, into
-  // LDS (hs row j = step base + j; hist row s − 1 = step s)
-  const int base = LAZY_WIN > 0 ? max(s_lo, nr - LAZY_WIN + 1) : nr + 1;
-  if (LAZY_WIN > 0) {
-    const f4* src = reinterpret_cast<const f4*>(hist + LAZY_HS * (int64_t)(base - 1));
-    for (int i = tid; i < (LAZY_HS / 4) * (nr - base + 1); i += 256) hs4[i] = src[i];
-  }
-  __syncthreads();
-  const float* hs = reinterpret_cast<const float*>(hs4) - LAZY_HS * base;   // hs + LAZY_HS·s = step s
-  const float* hg = hist - LAZY_HS;                                          // hg + LAZY_HS·s = step s
+  const float* hg = hist - LAZY_HS;   // hg + LAZY_HS·s = step s's scalars (hist row s − 1)
   const int slot = tid / CPR, c = tid % CPR;
   for (int q0 = 0; q0 < ns; q0 += RPP) {
     const int q = q0 + slot;   // (wave-uniform)
@@ -451,16 +429,11 @@ __global__ __launch_bounds__(256) void k_lazy_rows(LazyTab t, const int32_t* __r
         t.Gb[r] = 0.f;
       }
     }
-    // steps s0 .. base − 1 from hist, max(s0, base) .. nr from the LDS window
-    // (idle lanes of a partial row run the chain on zeros: no branch per lane)
-    const int split = min(base - 1, nr);
-    if (__any(bia)) {   // (wave-uniform: only the wave holding a value-0 thread runs the bias chains)
-      lazy_replay<true>(p0, m0, v0, p1, m1, v1, hg, s0, split);
-      lazy_replay<true>(p0, m0, v0, p1, m1, v1, hs, max(s0, base), nr);
-    } else {
-      lazy_replay<false>(p0, m0, v0, p1, m1, v1, hg, s0, split);
-      lazy_replay<false>(p0, m0, v0, p1, m1, v1, hs, max(s0, base), nr);
-    }
+    // steps s0 .. nr (idle lanes of a partial row run the chain on zeros: no branch per lane)
+    if (__any(bia))   // (wave-uniform: only the wave holding a value-0 thread runs the bias chains)
+      lazy_replay<true>(p0, m0, v0, p1, m1, v1, hg, s0, nr);
+    else
+      lazy_replay<false>(p0, m0, v0, p1, m1, v1, hg, s0, nr);
     if (MODE == 1) {
       adam_elem(p0, m0, v0, g0, a);
       adam_elem(p1, m1, v1, g1, a);
