@@ -476,51 +476,6 @@ def test_scatter_rows_deterministic(E, n_rows, n, n_max):
     assert torch.equal(tags == 9, touched)
 
 
-@pytest.mark.parametrize("H", [128, 64])
-def test_gru_two_row_tiles_equal_one(H):
-    """Bidir at B = 2567 has 2 × 161 row tiles — more than one round of the
-    CUs — so rg_gru_fwd_dirs / rg_gru_bwd_dirs run two 16-row tiles per
-    workgroup; each direction alone (161 tiles) runs one.  Final h, the saved
-    states, dGi and dGh bitwise equal (the per-row arithmetic is the same)."""
-    B, L, ndir = 2567, 8, 2
-    g = torch.Generator().manual_seed(H)
-    lens = torch.randint(1, L + 1, (B,), generator=g)
-    perm, ls, offs = pack(lens, L)
-    T = int(lens.sum())
-    k = 1 / H ** 0.5
-    Gi = [(torch.randn(T, 3 * H, generator=g) * 0.5).to(dev) for _ in range(ndir)]
-    Whh = [((torch.rand(3 * H, H, generator=g) * 2 - 1) * k).to(dev) for _ in range(ndir)]
-    bhh = [((torch.rand(3 * H, generator=g) * 2 - 1) * k).to(dev) for _ in range(ndir)]
-    dh = D(torch.randn(B, ndir * H, generator=g))
-    HF = ndir * H
-    outs = []
-    for joint in (True, False):
-        hout = torch.zeros(B, HF, device=dev)
-        saved = [torch.zeros(5, T, H, device=dev) for _ in range(ndir)]
-        dGi = [torch.zeros(T, 3 * H, device=dev) for _ in range(ndir)]
-        dGh = [torch.zeros(T, 3 * H, device=dev) for _ in range(ndir)]
-        if joint:
-            C().call("rg_gru_fwd_dirs", C().host_ptr_array(Gi), C().host_ptr_array(Whh), C().host_ptr_array(bhh),
-                     C().host_ptr_array(saved), ndir, perm.data_ptr(), ls.data_ptr(), offs.data_ptr(), B, H,
-                     hout.data_ptr(), HF, 0, T * H, st())
-            C().call("rg_gru_bwd_dirs", C().host_ptr_array(saved), C().host_ptr_array(Whh), C().host_ptr_array(dGi),
-                     C().host_ptr_array(dGh), ndir, T * H, perm.data_ptr(), ls.data_ptr(), offs.data_ptr(), B, H,
-                     dh.data_ptr(), HF, 0, st())
-        else:
-            for d in range(ndir):
-                C().call("rg_gru_fwd", Gi[d].data_ptr(), Whh[d].data_ptr(), bhh[d].data_ptr(), perm.data_ptr(),
-                         ls.data_ptr(), offs.data_ptr(), B, H, hout.data_ptr(), HF, d * H, saved[d].data_ptr(), T * H,
-                         st())
-                C().call("rg_gru_bwd", saved[d].data_ptr(), T * H, Whh[d].data_ptr(), perm.data_ptr(), ls.data_ptr(),
-                         offs.data_ptr(), B, H, dh.data_ptr(), HF, d * H, dGi[d].data_ptr(), dGh[d].data_ptr(), st())
-        torch.cuda.synchronize()
-        outs.append((hout, saved, dGi, dGh))
-    assert torch.equal(outs[0][0], outs[1][0])
-    for i in (1, 2, 3):
-        for d in range(ndir):
-            assert torch.equal(outs[0][i][d], outs[1][i][d])
-
-
 @pytest.mark.parametrize("H,ndir,B,L", [(128, 1, 100, 9), (128, 2, 70, 6), (64, 2, 70, 6), (32, 1, 33, 5),
                                         (16, 2, 64, 4)])
 def test_gru_forward_emits_h_planes(H, ndir, B, L):
