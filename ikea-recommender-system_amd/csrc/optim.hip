@@ -468,6 +468,16 @@ __global__ void k_lazy_mark(const int64_t* __restrict__ ids, int64_t n, int64_t 
   }
 }
 
+// need[id − lo] = stamp for the n int32 global ids in [lo, lo + rows) (the
+// row-sharded table: the ids the other ranks requested from this shard)
+__global__ void k_lazy_mark32(const int32_t* __restrict__ ids, int n, int64_t lo, int64_t rows,
+                              int32_t* __restrict__ need, int32_t stamp) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int64_t l = (int64_t)ids[i] - lo;
+  if (l >= 0 && l < rows) need[l] = stamp;
+}
+
 static inline bool lazy_tab_ok(const LazyTab& t) {
   return t.P && t.M && t.V && t.cols > 0 && (!t.Pb || (t.Mb && t.Vb));
 }
@@ -478,6 +488,16 @@ extern "C" int rg_lazy_mark_rows(const int64_t* ids, int64_t n, int64_t rows, ui
   if (n < 0 || S < 0 || rows <= 0 || !need || (n > 0 && !ids) || n + S == 0) return RG_ERR_ARG;
   hipLaunchKernelGGL(k_lazy_mark, dim3((unsigned)((n + S + 255) / 256)), dim3(256), 0, stream, ids, n, rows, seed,
                      counter, S, need, stamp);
+  RG_LAUNCH_CHECK();
+  return RG_OK;
+}
+
+extern "C" int rg_lazy_mark_rows32(const int32_t* ids, int n, int64_t lo, int64_t rows, int32_t* need, int32_t stamp,
+                                   hipStream_t stream) {
+  if (n < 0 || rows <= 0 || !need || (n > 0 && !ids)) return RG_ERR_ARG;
+  if (n == 0) return RG_OK;
+  hipLaunchKernelGGL(k_lazy_mark32, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, ids, n, lo, rows, need,
+                     stamp);
   RG_LAUNCH_CHECK();
   return RG_OK;
 }

@@ -144,6 +144,7 @@ SIGNATURES = {
     "rg_gemm_x6": [P, I64, P, I64, I, P, I64, P, I, P, I, I, I, P],
     "rg_wgrad_x6": [P, I, P, I, I, P, I, P, P, I, P],
     "rg_lazy_mark_rows": [P, I64, I64, U64, U64, I, P, I32, P],
+    "rg_lazy_mark_rows32": [P, I, I64, I64, P, I32, P],
     "rg_lazy_catch_up": [P, P, P, I, P, P, P, P, I64, P, P, I32, I32, P, P],
     "rg_lazy_adam_rows": [P, P, P, P, I, P, P, P, P, P, I64, P, P, I32, I32, P, P, P],
 }

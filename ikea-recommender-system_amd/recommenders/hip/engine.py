@@ -154,20 +154,23 @@ class LazyRows:
         self.side = None      # stream of catch_up_async
         self.pending = None   # its event, until a use of the table joins it
 
-    def catch_up(self, tab, ids=None, n_ids=0, seed=0, counter=0, S=0, more=()):
+    def catch_up(self, tab, ids=None, n_ids=0, seed=0, counter=0, S=0, more=(), ids32=None):
         """Bring the rows a read is about to touch — ``n_ids`` int64 ids at
         ``ids`` (device), the S negatives of draw ``counter`` and the (ptr, n)
         id sets of ``more`` — up to date.  On the stream every read of the
         table is ordered behind (two streams must not catch up one table
         concurrently: the double-Q step catches up all its passes' rows first)."""
         self.join()
-        if self.n == self.full or n_ids + S + sum(n for _, n in more) == 0:
+        n32 = ids32[1] if ids32 is not None else 0
+        if self.n == self.full or n_ids + S + n32 + sum(n for _, n in more) == 0:
             return
         st = stream_ptr()
         self.stamp += 1
         for p, n, sd, cn, ns in [(ids, n_ids, seed, counter, S)] + [(p, n, 0, 0, 0) for p, n in more]:
             if n + ns:
                 call("rg_lazy_mark_rows", p, n, self.rows, sd, cn, ns, self.need.data_ptr(), self.stamp, st)
+        if n32:   # (ptr, n, lo): int32 global ids of a row shard starting at lo
+            call("rg_lazy_mark_rows32", ids32[0], n32, ids32[2], self.rows, self.need.data_ptr(), self.stamp, st)
         call("rg_lazy_catch_up", *tab, self.rows, self.last.data_ptr(), self.need.data_ptr(), self.stamp, self.n,
              self.hist.data_ptr(), st)
 
@@ -333,8 +336,9 @@ class Trunk:
         # keeps the fp32 master and refreshes it in the same sweep
         self.emb16 = torch.empty(self.n_local, E, dtype=torch.float16, device=device) if fp16_embeddings else None
         self.refresh_half()
-        # catch-up Adam of the table (one GPU; the row-sharded table keeps the eager sweep)
-        self.lazy = LazyRows(self.n_local, device) if LAZY_ADAM and comm is None else None
+        # catch-up Adam of the table (row-sharded: of this rank's rows, caught up on
+        # the owner for the ids the ranks request, _exchange_rows)
+        self.lazy = LazyRows(self.n_local, device) if LAZY_ADAM else None
 
     def _lazy_tab(self):
         return (self.emb.p.data_ptr(), self.emb.m.data_ptr(), self.emb.v.data_ptr(), self.E,
@@ -349,7 +353,7 @@ class Trunk:
         """Catch up every row the trunk passes over ``states`` (device int64
         (B, L) tensors) will read, on the current stream — for passes that then
         run on other streams (forward(..., catch_up=False))."""
-        if self.lazy is not None and states:
+        if self.lazy is not None and states and self.comm is None:   # (row-sharded: in _exchange_rows)
             sts = [x.contiguous() for x in states]
             self._keep = sts   # (alive until the kernels reading them have run: the next call replaces it)
             self.lazy.catch_up(self._lazy_tab(), sts[0].data_ptr(), sts[0].numel(),
@@ -399,7 +403,7 @@ class Trunk:
                 for d in range(self.ndir):
                     call("rg_place_rows", w.rows_in.data_ptr(), 1 if self.emb16 is not None else 0,
                          w.slot.data_ptr(), w.lsort.data_ptr(), w.offs.data_ptr(), B, E, d, w.X[d].data_ptr(), st)
-        if self.lazy is not None and catch_up:   # the rows this pass reads (every position of s), caught up
+        if self.lazy is not None and catch_up and self.comm is None:   # the rows this pass reads (every position of s)
             s = s.contiguous()
             self.lazy.catch_up(self._lazy_tab(), s.data_ptr(), B * L)
         # a sampled head's negatives row gather rides in the first gather launch
@@ -689,6 +693,8 @@ class Trunk:
         recv_ids = self._xbuf(w, "recv_ids", max(R, 1))
         w.local_ids = self._xbuf(w, "local_ids_buf", max(R, 1))
         comm.all_to_all(recv_ids[:R], w.uids[:U], w.recv_splits, w.send_splits)
+        if self.lazy is not None:   # the requested rows of this shard, caught up before they are read
+            self.lazy.catch_up(self._lazy_tab(), ids32=(recv_ids.data_ptr(), R, self.lo))
         rows_out = self._xbuf(w, "rows_out", max(R, 1), self.E, rdt)
         call("rg_rows_gather", recv_ids.data_ptr(), R, self.lo, self.n_local,
              (self.emb16 if half else self.emb.p).data_ptr(), self.E, 1 if half else 0, rows_out.data_ptr(),

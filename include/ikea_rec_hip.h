@@ -308,6 +308,10 @@ int rg_adam_rows(float* P, float* M, float* V, float* G, const int32_t* tags, in
  *   Rows without a gradient are not touched. */
 int rg_lazy_mark_rows(const int64_t* ids, int64_t n, int64_t rows, uint64_t seed, uint64_t counter, int S,
                       int32_t* need, int32_t stamp, rg_stream_t stream);
+/* rg_lazy_mark_rows32: need[id − lo] = stamp for the n int32 global ids in [lo, lo + rows) (a row
+ *   shard: the ids the ranks requested from it). */
+int rg_lazy_mark_rows32(const int32_t* ids, int n, int64_t lo, int64_t rows, int32_t* need, int32_t stamp,
+                        rg_stream_t stream);
 int rg_lazy_catch_up(float* P, float* M, float* V, int cols, uint16_t* P16, float* Pb, float* Mb, float* Vb,
                      int64_t rows, int32_t* last, const int32_t* need, int32_t stamp, int32_t n_steps, float* hist,
                      rg_stream_t stream);

@@ -225,3 +225,51 @@ def test_item_sharded_step_over_native_rccl_one_rank(extra):
         d = np.abs(g[k] - v)
         assert d.max() <= 2 * lr + 1e-5, (k, float(d.max()))
         assert (d > 1e-4).mean() < 1e-3, k
+
+
+def _rank_lazy(rank, port, out, lazy):
+    sys.path.insert(0, REPO)
+    sys.path.insert(0, os.path.join(REPO, "ikea-recommender-system_amd"))
+    import torch.distributed as dist
+    from recommenders.hip import engine
+    engine.LAZY_ADAM = lazy
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=WORLD)
+    try:
+        from recommenders.data_utils.synthetic import SessionStream
+        from recommenders.models.GRU4Rec.model import GRU4Rec_trainer
+        tr = GRU4Rec_trainer(device="cuda:0", shard_items=True, matmul_precision="f32x6d3", **CFG)
+        assert (tr.gru_model.trunk.lazy is not None) == lazy
+        st = SessionStream(CFG["item_num"], CFG["state_size"], WORLD * B * 6, seed=33)
+        losses = []
+        for i in range(6):
+            s, a, r, sn, ln, nln, e = st.batch(i, WORLD * B)
+            sl = slice(rank * B, (rank + 1) * B)
+            losses.append(tr.train_step(s[sl], a[sl], ln[sl]))
+            if i == 2:   # a mid-run read of the whole shard (state_dict materializes every row)
+                mid = tr.gru_model.state_dict()["embedding.weight"].cpu().numpy()
+        sd = {k: v.cpu().numpy() for k, v in tr.gru_model.state_dict().items()}
+        np.savez(os.path.join(out, f"rank{rank}_{int(lazy)}.npz"), losses=np.array(losses), mid=mid, **sd)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_item_sharded_catch_up_adam_equals_eager_bitwise():
+    """The row-sharded embedding table with catch-up Adam (each owner catches
+    up the rows the ranks request, engine.Trunk._exchange_rows) against the
+    eager sweep of the shard: 2 ranks (gloo), 6 steps, a mid-run state_dict —
+    losses and every parameter bitwise equal."""
+    out = tempfile.mkdtemp()
+    ctx = mp.get_context("spawn")
+    for lazy in (True, False):
+        port = _port()
+        procs = [ctx.Process(target=_rank_lazy, args=(r, port, out, lazy)) for r in range(WORLD)]
+        for p in procs:
+            p.start()
+        for p in procs:
+            p.join(timeout=300)
+            assert p.exitcode == 0
+    for rank in range(WORLD):
+        a = np.load(os.path.join(out, f"rank{rank}_1.npz"))
+        b = np.load(os.path.join(out, f"rank{rank}_0.npz"))
+        for k in a.files:
+            assert np.array_equal(a[k], b[k]), (rank, k)
