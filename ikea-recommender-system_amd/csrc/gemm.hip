@@ -462,41 +462,53 @@ __device__ __forceinline__ void gx_stage_mfma(const __bf16* __restrict__ ap, con
   }
 }
 
-// C = A · Bᵀ (+ bias): A (M × K) k-contiguous, B (N × K) k-contiguous
-// (B_KCONTIG) or (K × N) n-contiguous; K % 32 == 0; M may come from the
-// device.  128 × 128 tile per 256-thread workgroup, two per CU (one 60 KB
-// plane stage each; the next stage's fp32 pieces are prefetched into
-// registers under this stage's MFMAs).
-template <int NT, bool B_KCONTIG>
+// C = A · Bᵀ (+ bias): A (M × K) k-contiguous (A_KCONTIG) or (K × M)
+// m-contiguous, B (N × K) k-contiguous (B_KCONTIG) or (K × N) n-contiguous;
+// K % 32 == 0; M may come from the device.  128 × 128 tile per 256-thread
+// workgroup, two per CU (one 60 KB plane stage each; the next stage's fp32
+// pieces are prefetched into registers under this stage's MFMAs).  Split-K:
+// workgroup z takes k in [z·kchunk, (z+1)·kchunk) and writes slab z of C
+// (C + z·slab; rg_reduce_slabs sums them in slab order).
+template <int NT, bool A_KCONTIG, bool B_KCONTIG>
 __global__ __launch_bounds__(256, 2) void k_gemm_x6(const float* __restrict__ A, int64_t lda,
                                                     const float* __restrict__ Bm, int64_t ldb,
                                                     float* __restrict__ C, int64_t ldc, const float* __restrict__ bias,
-                                                    int M_, const int32_t* __restrict__ Mptr, int N, int K) {
+                                                    int M_, const int32_t* __restrict__ Mptr, int N, int K,
+                                                    int kchunk, int64_t slab) {
   constexpr int PL = GX_T * GX_RS;
   __shared__ __attribute__((aligned(16))) __bf16 As[3 * PL];
   __shared__ __attribute__((aligned(16))) __bf16 Bs[3 * PL];
   const int M = Mptr ? *Mptr : M_;
   const int m0 = blockIdx.y * GX_T, n0 = blockIdx.x * GX_T;
   if (m0 >= M) return;
+  const int kb = blockIdx.z * kchunk, ke = min(K, kb + kchunk);
+  C += (int64_t)blockIdx.z * slab;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, wm = w >> 1, wn = w & 1;
   // this thread's four 16-B pieces of each stage (rows clamped: rows past M /
   // columns past N compute values that are never stored)
-  // (B n-contiguous: thread = column n0 + (tid & 127), k = 16·(tid >> 7) .. +15
-  // of the stage, one coalesced 4-B load per k, written as whole 16-B k-runs)
+  // (an m- / n-contiguous operand: thread = column c0 + (tid & 127), k =
+  // 16·(tid >> 7) .. +15 of the stage, one coalesced 4-B load per k, written
+  // as whole 16-B k-runs)
   const float* ap[4];
   const float* bq[4];
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     const int e = tid + 256 * q;
-    ap[q] = A + (int64_t)min(m0 + (e >> 3), M - 1) * lda + 4 * (e & 7);
+    if (A_KCONTIG) ap[q] = A + (int64_t)min(m0 + (e >> 3), M - 1) * lda + 4 * (e & 7);
     if (B_KCONTIG) bq[q] = Bm + (int64_t)min(n0 + (e >> 3), N - 1) * ldb + 4 * (e & 7);
   }
+  const float* acol = A + min(m0 + (tid & 127), M - 1) + (int64_t)(16 * (tid >> 7)) * lda;
   const float* bcol = Bm + min(n0 + (tid & 127), N - 1) + (int64_t)(16 * (tid >> 7)) * ldb;
   f4 ra[4], rb[4];
   auto load = [&](int k0) __attribute__((always_inline)) {
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      ra[q] = *reinterpret_cast<const f4*>(ap[q] + k0);
+      if (A_KCONTIG) {
+        ra[q] = *reinterpret_cast<const f4*>(ap[q] + k0);
+      } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) ra[q][i] = acol[(int64_t)(k0 + 4 * q + i) * lda];
+      }
       if (B_KCONTIG) {
         rb[q] = *reinterpret_cast<const f4*>(bq[q] + k0);
       } else {
@@ -511,13 +523,14 @@ __global__ __launch_bounds__(256, 2) void k_gemm_x6(const float* __restrict__ A,
       const int e = tid + 256 * q;
       bf16x4 p0, p1, p2;
       split3x4(ra[q], p0, p1, p2);
-      const int ao = (e >> 3) * GX_RS + 4 * (e & 7);
+      const int ko = (e >> 3) * GX_RS + 4 * (e & 7);
+      const int co = (tid & 127) * GX_RS + 16 * (tid >> 7) + 4 * q;   // (this thread's k-run of column tid & 127)
+      const int ao = A_KCONTIG ? ko : co;
       *reinterpret_cast<bf16x4*>(&As[ao]) = p0;
       *reinterpret_cast<bf16x4*>(&As[PL + ao]) = p1;
       *reinterpret_cast<bf16x4*>(&As[2 * PL + ao]) = p2;
       split3x4(rb[q], p0, p1, p2);
-      // (n-contiguous B: this thread's k-run 16·(tid >> 7) + 4q .. +3 of column tid & 127)
-      const int bo = B_KCONTIG ? ao : (tid & 127) * GX_RS + 16 * (tid >> 7) + 4 * q;
+      const int bo = B_KCONTIG ? ko : co;
       *reinterpret_cast<bf16x4*>(&Bs[bo]) = p0;
       *reinterpret_cast<bf16x4*>(&Bs[PL + bo]) = p1;
       *reinterpret_cast<bf16x4*>(&Bs[2 * PL + bo]) = p2;
@@ -528,11 +541,11 @@ __global__ __launch_bounds__(256, 2) void k_gemm_x6(const float* __restrict__ A,
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
-  load(0);
-  for (int k0 = 0; k0 < K; k0 += GX_K) {
+  if (kb < ke) load(kb);
+  for (int k0 = kb; k0 < ke; k0 += GX_K) {
     store();
     __syncthreads();
-    if (k0 + GX_K < K) load(k0 + GX_K);
+    if (k0 + GX_K < ke) load(k0 + GX_K);
     gx_stage_mfma<NT>(As, Bs, wm, wn, lane, acc);
     __syncthreads();
   }
@@ -552,25 +565,50 @@ __global__ __launch_bounds__(256, 2) void k_gemm_x6(const float* __restrict__ A,
   }
 }
 
-extern "C" int rg_gemm_x6(const float* A, int64_t lda, const float* B, int64_t ldb, int b_kcontig, float* C,
-                          int64_t ldc, const float* bias, int M, const int32_t* Mptr, int N, int K, int terms,
-                          hipStream_t stream) {
-  if (M <= 0 || N < 4 || K <= 0 || K % GX_K || N % 4 || lda % 4 || ldb % 4 || ldc < N || (terms != 6 && terms != 9))
+static int gemm_x6_launch(const float* A, int64_t lda, int a_kcontig, const float* B, int64_t ldb, int b_kcontig,
+                          float* C, int64_t ldc, int64_t slab, const float* bias, int M, const int32_t* Mptr, int N,
+                          int K, int splits, int terms, hipStream_t stream) {
+  if (M <= 0 || N < 4 || K <= 0 || K % GX_K || N % 4 || lda % 4 || ldb % 4 || ldc < N || splits < 1 ||
+      (terms != 6 && terms != 9))
     return RG_ERR_ARG;
   if (((reinterpret_cast<uintptr_t>(A) | reinterpret_cast<uintptr_t>(B)) & 15) != 0) return RG_ERR_ARG;
-  const dim3 grid((N + GX_T - 1) / GX_T, (M + GX_T - 1) / GX_T);
-#define GX(NTV, BK)                                                                                        \
-  hipLaunchKernelGGL((k_gemm_x6<NTV, BK>), grid, dim3(256), 0, stream, A, lda, B, ldb, C, ldc, bias, M, Mptr, N, K)
+  const int kchunk = (K / GX_K + splits - 1) / splits * GX_K;   // (a multiple of the 32-deep stage)
+  const dim3 grid((N + GX_T - 1) / GX_T, (M + GX_T - 1) / GX_T, splits);
+#define GX(NTV, AK, BK)                                                                                             \
+  hipLaunchKernelGGL((k_gemm_x6<NTV, AK, BK>), grid, dim3(256), 0, stream, A, lda, B, ldb, C, ldc, bias, M, Mptr, N, \
+                     K, kchunk, slab)
+#define GXB(NTV, AK) \
+  do {               \
+    if (b_kcontig)   \
+      GX(NTV, AK, true); \
+    else             \
+      GX(NTV, AK, false); \
+  } while (0)
   if (terms == 6) {
-    if (b_kcontig) GX(6, true);
-    else GX(6, false);
+    if (a_kcontig) GXB(6, true);
+    else GXB(6, false);
   } else {
-    if (b_kcontig) GX(9, true);
-    else GX(9, false);
+    if (a_kcontig) GXB(9, true);
+    else GXB(9, false);
   }
+#undef GXB
 #undef GX
   RG_LAUNCH_CHECK();
   return RG_OK;
+}
+
+extern "C" int rg_gemm_x6(const float* A, int64_t lda, const float* B, int64_t ldb, int b_kcontig, float* C,
+                          int64_t ldc, const float* bias, int M, const int32_t* Mptr, int N, int K, int terms,
+                          hipStream_t stream) {
+  return gemm_x6_launch(A, lda, 1, B, ldb, b_kcontig, C, ldc, 0, bias, M, Mptr, N, K, 1, terms, stream);
+}
+
+extern "C" int rg_gemm_x6_sk(const float* A, int64_t lda, int a_kcontig, const float* B, int64_t ldb, int b_kcontig,
+                             float* C, int64_t ldc, int64_t slab, int M, int N, int K, int splits, int terms,
+                             hipStream_t stream) {
+  if (splits > 1 && slab < (int64_t)M * ldc) return RG_ERR_ARG;
+  return gemm_x6_launch(A, lda, a_kcontig, B, ldb, b_kcontig, C, ldc, slab, nullptr, M, nullptr, N, K, splits, terms,
+                        stream);
 }
 
 // Split-bf16 weight gradient over packed tokens (rg_wgrad's contract):

@@ -142,6 +142,7 @@ SIGNATURES = {
     "rg_rows_unslot": [P, I, P, P, I, I, P, P, P, P],
     "rg_rows_slot": [P, P, P, I, I, I, P, P],
     "rg_gemm_x6": [P, I64, P, I64, I, P, I64, P, I, P, I, I, I, P],
+    "rg_gemm_x6_sk": [P, I64, I, P, I64, I, P, I64, I64, I, I, I, I, I, P],
     "rg_wgrad_x6": [P, I, P, I, I, P, I, P, P, I, P],
     "rg_lazy_mark_rows": [P, I64, I64, U64, U64, I, P, I32, P],
     "rg_lazy_mark_rows32": [P, I, I64, I64, P, I32, P],

@@ -1553,6 +1553,23 @@ class SampledSoftmaxHead(SoftmaxHead):
             self.lazy.catch_up(self._lazy_tab(), tgt.data_ptr(), B, self.seed, self.draws, S)
             self._ready_draw = self.draws
 
+    @staticmethod
+    def _dz_gemms(w, h, B, S, HF, st):
+        """dh slabs 1.. = dZ · Wg and dw slabs = dZᵀ · h (split-K): at a split
+        precision on the bf16 planes of exact 3-way splits (rg_gemm_x6_sk, 6 or
+        9 products, the logits' arithmetic), else fp32 MFMA (rg_gemm_f32)."""
+        if w.terms and w.zrow:
+            t = 9 if w.terms == 9 else 6
+            call("rg_gemm_x6_sk", w.ZT.data_ptr(), w.ldz, 1, w.Wg.data_ptr(), HF, 0,
+                 w.dh_slabs.data_ptr() + 4 * B * HF, HF, B * HF, B, HF, S, w.dh_splits, t, st)
+            call("rg_gemm_x6_sk", w.ZT.data_ptr(), w.ldz, 0, h.data_ptr(), HF, 0, w.dw_slabs.data_ptr(), HF, S * HF,
+                 S, HF, B, w.dw_splits, t, st)
+        else:
+            call("rg_gemm_f32", w.ZT.data_ptr(), w.zs_b, w.zs_s, w.Wg.data_ptr(), HF, 1,
+                 w.dh_slabs.data_ptr() + 4 * B * HF, HF, None, B, None, HF, S, None, w.dh_splits, st)
+            call("rg_gemm_f32", w.ZT.data_ptr(), w.zs_s, w.zs_b, h.data_ptr(), HF, 1, w.dw_slabs.data_ptr(), HF, None,
+                 S, None, HF, B, None, w.dw_splits, st)
+
     def split_terms(self, B):
         """bf16 terms of the forward for batch B (0: native fp32 MFMA)."""
         if self.precision == "f32" or B % 32 or self.S % 32:
@@ -1664,14 +1681,11 @@ class SampledSoftmaxHead(SoftmaxHead):
                      w.gb.data_ptr(), st)
             else:
                 call("rg_sampled_dz", w.ZT.data_ptr(), w.ldz, w.lse.data_ptr(), B, S, g, w.gb.data_ptr(), st)
-            # dh = dZ · Wg (+ the positive part already in slab 0)
-            call("rg_gemm_f32", w.ZT.data_ptr(), w.zs_b, w.zs_s, w.Wg.data_ptr(), HF, 1,
-                 w.dh_slabs.data_ptr() + 4 * B * HF, HF, None, B, None, HF, S, None, w.dh_splits, st)
+            # dh = dZ · Wg (+ the positive part already in slab 0); dWg = dZᵀ · h -> rows [0, S) of the
+            # scatter list.  Split precisions: the logits' split-bf16 planes (rg_gemm_x6_sk), else fp32 MFMA
+            self._dz_gemms(w, h, B, S, HF, st)
             call("rg_reduce_slabs", w.dh_slabs.data_ptr(), w.dh_splits + 1, B * HF, dh_out.data_ptr(), None, HF, 0,
                  st)
-            # dWg = dZᵀ · h  -> rows [0, S) of the scatter list
-            call("rg_gemm_f32", w.ZT.data_ptr(), w.zs_s, w.zs_b, h.data_ptr(), HF, 1, w.dw_slabs.data_ptr(), HF, None,
-                 S, None, HF, B, None, w.dw_splits, st)
             call("rg_reduce_slabs", w.dw_slabs.data_ptr(), w.dw_splits, S * HF, w.grows.data_ptr(), None, HF, 0,
                  st)
             self.tag += 1
@@ -1822,12 +1836,9 @@ class ShardedSampledHead(SampledSoftmaxHead):
         with region("sampled_bwd"):
             call("rg_sampled_dz_rows", w.ZT.data_ptr(), w.ldz, w.lse.data_ptr(), B, S, g, w.dbslabs.data_ptr(),
                  w.gb.data_ptr(), st)
-            call("rg_gemm_f32", w.ZT.data_ptr(), w.zs_b, w.zs_s, w.Wg.data_ptr(), HF, 1,
-                 w.dh_slabs.data_ptr() + 4 * B * HF, HF, None, B, None, HF, S, None, w.dh_splits, st)
+            self._dz_gemms(w, h, B, S, HF, st)
             call("rg_reduce_slabs", w.dh_slabs.data_ptr(), w.dh_splits + 1, B * HF, dh_out.data_ptr(), None, HF, 0,
                  st)
-            call("rg_gemm_f32", w.ZT.data_ptr(), w.zs_s, w.zs_b, h.data_ptr(), HF, 1, w.dw_slabs.data_ptr(), HF, None,
-                 S, None, HF, B, None, w.dw_splits, st)
             call("rg_reduce_slabs", w.dw_slabs.data_ptr(), w.dw_splits, S * HF, w.grows.data_ptr(), None, HF, 0,
                  st)
         R = w.R

@@ -326,6 +326,12 @@ int rg_lazy_adam_rows(float* P, float* M, float* V, float* G, int cols, uint16_t
  * rg_wgrad_x6: rg_wgrad's contract (dW, db token-split slabs) on the same arithmetic. */
 int rg_gemm_x6(const float* A, int64_t lda, const float* B, int64_t ldb, int b_kcontig, float* C, int64_t ldc,
                const float* bias, int M, const int32_t* Mptr, int N, int K, int terms, rg_stream_t stream);
+/* rg_gemm_x6_sk: rg_gemm_x6 with split-K (slab z of C at C + z·slab covers k in the z-th of `splits`
+ *   equal 32-aligned ranges; rg_reduce_slabs sums them) and A either (M × K) k-contiguous
+ *   (a_kcontig = 1) or (K × M) m-contiguous (a_kcontig = 0, lda = the stride between k rows);
+ *   no bias, M from the host (the sampled head's dh = dZ·W_neg and dW_neg = dZᵀ·h). */
+int rg_gemm_x6_sk(const float* A, int64_t lda, int a_kcontig, const float* B, int64_t ldb, int b_kcontig, float* C,
+                  int64_t ldc, int64_t slab, int M, int N, int K, int splits, int terms, rg_stream_t stream);
 int rg_wgrad_x6(const float* G, int M, const float* X, int N, int T_max, const int32_t* Tptr, int splits,
                 float* dw_slabs, float* db_slabs, int terms, rg_stream_t stream);
 /* split-K weight-gradient slabs summed in order, then Adam (or g_out). */

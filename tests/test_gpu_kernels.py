@@ -745,6 +745,40 @@ def test_gemm_x6_split_bf16(terms, M, N, K, bk):
 
 
 @pytest.mark.parametrize("terms", [6, 9])
+@pytest.mark.parametrize("M,N,K,splits,ak,bk", [(4096, 256, 2048, 8, 1, 0), (2048, 256, 4096, 16, 0, 0),
+                                                (300, 128, 320, 3, 1, 1), (130, 64, 96, 5, 0, 1),
+                                                (512, 32, 512, 1, 0, 0)])
+def test_gemm_x6_split_k(terms, M, N, K, splits, ak, bk):
+    """rg_gemm_x6_sk (the sampled head's dh = dZ·W_neg, A k-contiguous, and
+    dW_neg = dZᵀ·h, A m-contiguous; split-K slabs, a ragged last chunk, more
+    splits than stages): the slabs' sum against fp64 within 2× the native
+    fp32 split-K kernel's error (rg_gemm_f32 with the same splits)."""
+    g = torch.Generator().manual_seed(7 + M + K + splits)
+    A = torch.randn(M, K, generator=g)
+    Bnk = torch.randn(N, K, generator=g) * 0.1
+    ref = A.double() @ Bnk.double().t()
+    Ad = D(A) if ak else D(A.t().contiguous())
+    lda = K if ak else M
+    Bd = D(Bnk) if bk else D(Bnk.t().contiguous())
+    ldb = K if bk else N
+    out = torch.full((splits, M, N), float("nan"), device=dev)
+    C().call("rg_gemm_x6_sk", Ad.data_ptr(), lda, ak, Bd.data_ptr(), ldb, bk, out.data_ptr(), N, M * N, M, N, K,
+             splits, terms, st())
+    nat = torch.full((splits, M, N), float("nan"), device=dev)
+    C().call("rg_gemm_f32", Ad.data_ptr(), K if ak else 1, 1 if ak else M, Bd.data_ptr(), 1 if bk else N,
+             K if bk else 1, nat.data_ptr(), N, None, M, None, N, K, None, splits, st())
+    torch.cuda.synchronize()
+    kchunk = (K // 32 + splits - 1) // splits * 32
+    used = (K + kchunk - 1) // kchunk   # slabs past the last k chunk are zero
+    got = out[:used].sum(0).cpu().double()
+    assert torch.count_nonzero(out[used:].nan_to_num(1.0)) == 0
+    e_x6 = (got - ref).abs().max().item()
+    e_nat = (nat.sum(0).cpu().double() - ref).abs().max().item()
+    ulp = ref.abs().max().item() * 2.0 ** -24
+    assert e_x6 <= 2 * e_nat + 2 * splits * ulp, (e_x6, e_nat, ulp)
+
+
+@pytest.mark.parametrize("terms", [6, 9])
 @pytest.mark.parametrize("M,N,T,splits", [(384, 128, 5000, 16), (384, 256, 3000, 7), (192, 64, 3000, 128),
                                           (96, 32, 777, 3), (384, 128, 85000, 128)])
 def test_wgrad_x6_split_bf16(terms, M, N, T, splits):
