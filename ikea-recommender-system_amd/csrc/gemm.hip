@@ -568,8 +568,9 @@ __global__ __launch_bounds__(256, 2) void k_gemm_x6(const float* __restrict__ A,
 static int gemm_x6_launch(const float* A, int64_t lda, int a_kcontig, const float* B, int64_t ldb, int b_kcontig,
                           float* C, int64_t ldc, int64_t slab, const float* bias, int M, const int32_t* Mptr, int N,
                           int K, int splits, int terms, hipStream_t stream) {
-  if (M <= 0 || N < 4 || K <= 0 || K % GX_K || N % 4 || lda % 4 || ldb % 4 || ldc < N || splits < 1 ||
-      (terms != 6 && terms != 9))
+  // (16-B loads along k need k-contiguous rows at 4-float strides; the other layouts load 4 B per element)
+  if (M <= 0 || N < 4 || K <= 0 || K % GX_K || N % 4 || (a_kcontig && lda % 4) || (b_kcontig && ldb % 4) ||
+      ldc < N || splits < 1 || (terms != 6 && terms != 9))
     return RG_ERR_ARG;
   if (((reinterpret_cast<uintptr_t>(A) | reinterpret_cast<uintptr_t>(B)) & 15) != 0) return RG_ERR_ARG;
   const int kchunk = (K / GX_K + splits - 1) / splits * GX_K;   // (a multiple of the 32-deep stage)
