@@ -150,6 +150,10 @@ TARGET_SIDE_STREAM = True
 # (round 6: starting it only after the previous step's pass 2, so that it shares the CUs with
 # pass 1 instead, measured 214.5K vs 215.1K session-steps/s at C4 — not kept,
 # profiles/r07/ab_c4_target_after_pass2.txt)
+# queue the target on the host after the supervised head's pass 1 (device order
+# unchanged: after the step's catch-up), so the main state's trunk forward and
+# pass 1 are dispatched first and the target fills in beside pass 2
+TARGET_AFTER_PASS1 = False
 
 
 def target_stream(net):
@@ -223,15 +227,20 @@ def double_q_step(nets, clocks, k, s, a, r, s_next, true_len, true_next_len, is_
     # main state's forward and pass 1, instead of ahead of pass 1 on the
     # serial chain; joined before the TD loss reads qn
     ts = target_stream(main) if TARGET_SIDE_STREAM else None
+    late = ts is not None and TARGET_AFTER_PASS1
     if ts is not None:
         ts.wait_stream(cur)
-        with torch.cuda.stream(ts):
-            qn = target()
+        if not late:
+            with torch.cuda.stream(ts):
+                qn = target()
     with region("sqn_trunk_main"):
         h = main.trunk.forward(s, true_len, slot="main", save=True, catch_up=False)
     if ts is None:
         qn = target()
     sup_loss, _ = main.sup_head_output.forward_loss(h, a, slot="main")
+    if late:   # queued behind pass 1 on the host, ordered on the device only after the catch-up above
+        with torch.cuda.stream(ts):
+            qn = target()
     q = main.gather_q(h, idx64=a, out=main.buf("q", (B, nh)))
     dq = main.buf("dq", (B, nh))
     if smorl is not None:   # the rewards' top-k re-scores pass 1's candidates with W: before pass 2 moves it

@@ -294,7 +294,7 @@ int rg_adam_dense(float* P, float* M, float* V, float* G, int64_t n, const float
  * untagged rows take g = 0 (moments still decay, p still moves). */
 int rg_adam_rows(float* P, float* M, float* V, float* G, const int32_t* tags, int32_t tag, int64_t rows, int cols,
                  const float* adam6, rg_stream_t stream);
-/* Catch-up Adam (dense semantics, bitwise; DESIGN §7): a table read a few rows at a time (the
+/* Catch-up Adam (dense semantics, bitwise; DESIGN §7a): a table read a few rows at a time (the
  * embedding, the sampled head) keeps last[r] = table steps applied to row r and hist (float[8] per
  * step, step s at 8·(s − 1): adam6, RN(1 / adam6[3]), 0) = every step's scalars; a row's zero-gradient steps are replayed only
  * before it is read.  Replaces rg_adam_rows' sweep over every row (GRU4Rec/model.py:124-127,153).
