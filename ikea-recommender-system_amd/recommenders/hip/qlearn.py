@@ -152,7 +152,9 @@ TARGET_SIDE_STREAM = True
 # profiles/r07/ab_c4_target_after_pass2.txt)
 # queue the target on the host after the supervised head's pass 1 (device order
 # unchanged: after the step's catch-up), so the main state's trunk forward and
-# pass 1 are dispatched first and the target fills in beside pass 2
+# pass 1 are dispatched first and the target fills in beside pass 2: neutral at C4
+# (228.5K vs 228.3K session-steps/s over three same-box pairs,
+# profiles/r07/ab_c4_target_after_pass1.txt), so the target stays queued first
 TARGET_AFTER_PASS1 = False
 
 
