@@ -81,11 +81,11 @@ def test_lazy_rows_equal_the_eager_sweep_bitwise(rows, cols, bias, half):
         assert torch.equal(lP[rl], eP[rl]) and torch.equal(lM[rl], eM[rl]) and torch.equal(lV[rl], eV[rl])
     lz.materialize(tab)
     torch.cuda.synchronize()
-    for a, e in ((lP, eP), (lM, eM), (lV, eV)):
-        assert torch.equal(a, e)
+    for a, e in ((lP, eP), (lM, eM), (lV, eV)):   # bit patterns: ±0 told apart
+        assert torch.equal(a.view(torch.int32), e.view(torch.int32))
     if bias:
         for a, e in ((lb, eb), (lbm, ebm), (lbv, ebv)):
-            assert torch.equal(a, e)
+            assert torch.equal(a.view(torch.int32), e.view(torch.int32))
     if half:
         assert torch.equal(l16, lP.half())
     assert torch.count_nonzero(lG) == 0 and int((lz.last != 20).sum()) == 0
@@ -148,11 +148,11 @@ def test_lazy_chains_longer_than_the_lds_window_bitwise(cols, bias):
     assert float(eV[20:40].min()) < 1.2e-38   # denormal second moments are replayed
     lz.materialize(tab)
     torch.cuda.synchronize()
-    for a, e in ((lP, eP), (lM, eM), (lV, eV)):
-        assert torch.equal(a, e)
+    for a, e in ((lP, eP), (lM, eM), (lV, eV)):   # bit patterns: ±0 told apart
+        assert torch.equal(a.view(torch.int32), e.view(torch.int32))
     if bias:
         for a, e in ((lb, eb), (lbm, ebm), (lbv, ebv)):
-            assert torch.equal(a, e)
+            assert torch.equal(a.view(torch.int32), e.view(torch.int32))
 
 
 def _pair(monkeypatch, make):
