@@ -381,15 +381,16 @@ class Trunk:
             self._ws[key] = w
         return w
 
-    def forward(self, s, lens, slot="main", save=False, route=None, catch_up=True):
+    def forward(self, s, lens, slot="main", save=False, route=None, catch_up=True, lens_dev=None):
         """s: int64 (B, L) device; lens: int64 (B,) device or CPU. Returns h (B, ndir*H).
         route (item-sharded table): this pass's (send_splits, recv_splits) from
         the host batch (dist.host_routes); None routes on the device and reads
-        the counts back (one sync)."""
+        the counts back (one sync).  lens_dev: lens already on the device (the
+        step's InputStage copy), copied from instead of the host lens."""
         B, L = s.shape
         w = self.ws(slot, B, L, save)
         st = stream_ptr()
-        w.lens.copy_(lens, non_blocking=True)
+        w.lens.copy_(lens_dev if lens_dev is not None else lens, non_blocking=True)
         # host bound of the packed token count (the scatter sorts this many keys)
         lt = torch.as_tensor(lens)
         w.T_host = int(lt.clamp(1, L).sum()) if self.packed and lt.device.type == "cpu" else B * L

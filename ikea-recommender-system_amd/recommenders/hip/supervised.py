@@ -11,6 +11,7 @@ from __future__ import annotations
 
 import torch
 
+from .hostsync import InputStage
 from .nets import HipNet
 
 
@@ -34,13 +35,14 @@ def supervised_step(net: SupervisedNet, clock, s, a, true_len, host=None):
     with ``host`` (hostsync.HostScalars), reads the loss captured as soon as
     it is final."""
     dev = net.device
-    s = s.to(dev, non_blocking=True)
-    a = a.to(dev, non_blocking=True)
+    if getattr(net, "_inputs", None) is None:
+        net._inputs = InputStage(dev)
+    s, a, lens_dev = net._inputs.put(s, a, true_len)   # on the copy stream (hostsync.InputStage)
     head = next(iter(net.heads.values()))
     # sampled head: its negatives' row gather joins the embedding-gather launch
     # (and, catch-up Adam, the step's target and negative rows are brought up to date first)
     net.trunk.neg_job = head.neg_job("main", s.shape[0], tgt=a) if hasattr(head, "neg_job") else None
-    h = net.trunk.forward(s, true_len, slot="main", save=True)
+    h = net.trunk.forward(s, true_len, slot="main", save=True, lens_dev=lens_dev)
     B = h.shape[0]
     mask = None
     if net.training and net.dropout_p > 0:
