@@ -478,6 +478,10 @@ __global__ __launch_bounds__(256, 2) void k_gemm_x6(const float* __restrict__ A,
   constexpr int PL = GX_T * GX_RS;
   __shared__ __attribute__((aligned(16))) __bf16 As[3 * PL];
   __shared__ __attribute__((aligned(16))) __bf16 Bs[3 * PL];
+  // raised wave priority over the side streams' VALU work (the catch-up replay,
+  // the head's pass 2): C2 +0.5 %, C3 +1.3 %, C4 −0.5 % (noise), same box,
+  // profiles/r07/ab_x6_setprio.txt
+  __builtin_amdgcn_s_setprio(2);
   const int M = Mptr ? *Mptr : M_;
   const int m0 = blockIdx.y * GX_T, n0 = blockIdx.x * GX_T;
   if (m0 >= M) return;
@@ -625,6 +629,7 @@ __global__ __launch_bounds__(256, 2) void k_wgrad_x6(const float* __restrict__ G
   __shared__ __attribute__((aligned(16))) __bf16 As[3 * PL];
   __shared__ __attribute__((aligned(16))) __bf16 Bs[3 * PL];
   __shared__ float csum[2][GX_T];
+  __builtin_amdgcn_s_setprio(2);   // as in k_gemm_x6
   const int T = *Tptr;
   const int ntile_m = (M + GX_T - 1) / GX_T;
   const int mt = blockIdx.x % ntile_m, nt = blockIdx.x / ntile_m;

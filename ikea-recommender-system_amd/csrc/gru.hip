@@ -46,6 +46,10 @@ __global__ __launch_bounds__(H * 4) void k_gru_fwd(GruDirs dirs, const int32_t* 
                                                    const int32_t* __restrict__ lsort,
                                                    const int32_t* __restrict__ offs, int B, float* __restrict__ hout,
                                                    int ldh, int hoff0, int64_t plane, bf16x8* __restrict__ hk) {
+  // raised wave priority: the recurrence is the step's serial chain, and the
+  // catch-up replay (VALU-bound, side stream) shares its CUs — this wave wins
+  // issue on the SIMD (C3 +3 %, C2 +0.4 %, same box, profiles/r07/ab_gru_setprio.txt)
+  __builtin_amdgcn_s_setprio(3);
   const int dir = blockIdx.y;
   const float* __restrict__ Gi = dirs.Gi[dir];
   const float* __restrict__ Whh = dirs.Whh[dir];
@@ -166,6 +170,7 @@ __global__ __launch_bounds__(H * 4) void k_gru_bwd(GruBwdDirs dirs, int64_t plan
                                                    const int32_t* __restrict__ lsort,
                                                    const int32_t* __restrict__ offs, int B,
                                                    const float* __restrict__ dhout, int lddh, int dhoff0) {
+  __builtin_amdgcn_s_setprio(3);   // as in k_gru_fwd
   const int dir = blockIdx.y;
   const float* __restrict__ saved = dirs.saved[dir];
   const float* __restrict__ Whh = dirs.Whh[dir];
