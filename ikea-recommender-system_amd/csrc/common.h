@@ -130,6 +130,18 @@ __device__ __forceinline__ void rg_blds16(__amdgpu_buffer_rsrc_t r, void* lds_wa
                                            soff, 0, 0);
 }
 
+// Issue priority of the launch stream's short serial kernels over the side
+// streams' VALU work (the catch-up replay, the head's pass 2); s_setprio is a
+// SOPP instruction, it only changes the wave's issue arbitration (DESIGN §4d;
+// the segmented scatter, the Adam updates, the direction sum: C4 +1 %, C2 / C3
+// unchanged, same box, profiles/r07/ab_main_setprio.txt)
+#ifndef RG_MAIN_PRIO
+#define RG_MAIN_PRIO 2
+#endif
+__device__ __forceinline__ void rg_main_prio() {
+  if constexpr (RG_MAIN_PRIO > 0) __builtin_amdgcn_s_setprio(RG_MAIN_PRIO);
+}
+
 // 8 consecutive fp32 values -> their three bf16 planes
 __device__ __forceinline__ void split3x8(const f4& lo, const f4& hi, bf16x8& p0, bf16x8& p1, bf16x8& p2) {
 #pragma unroll

@@ -180,6 +180,7 @@ __global__ __launch_bounds__(256) void k_place_rows(const TE* __restrict__ rows_
 __global__ __launch_bounds__(256) void k_combine_dirs(float* __restrict__ dX0, const float* __restrict__ dX1,
                                                       const int32_t* __restrict__ lsort,
                                                       const int32_t* __restrict__ offs, int E) {
+  rg_main_prio();
   const int r = blockIdx.x;
   const int len = lsort[r], base = offs[r];
   const int v4 = E / 4;

@@ -255,6 +255,7 @@ extern "C" int rg_f32_to_f16(const float* x, int64_t n, uint16_t* out, hipStream
 __global__ __launch_bounds__(256) void k_adam_slabs(float* __restrict__ P, float* __restrict__ M,
                                                     float* __restrict__ V, const float* __restrict__ slabs,
                                                     int nslab, int64_t n, AdamArgs a, float* __restrict__ g_out) {
+  rg_main_prio();
   __shared__ float part[8][33];
   const int c = threadIdx.x & 31, q = threadIdx.x >> 5;
   const int64_t i = (int64_t)blockIdx.x * 32 + c;
@@ -377,6 +378,7 @@ template <int MODE, int CPR>
 __global__ __launch_bounds__(256) void k_lazy_rows(LazyTab t, const int32_t* __restrict__ sel, int32_t selv,
                                                    int32_t* __restrict__ last, int64_t rows, int n,
                                                    float* __restrict__ hist, AdamArgs a) {
+  if constexpr (MODE == 1) rg_main_prio();   // the step's own update (the replay-only mode stays at 0)
   static_assert(CPR >= 64 && CPR <= 256, "a row slot is whole waves");
   constexpr int RPP = 256 / CPR;   // rows per pass
   __shared__ int32_t rlist[64], rfirst[64];

@@ -41,6 +41,7 @@ int key_bits(int64_t n_rows) {
 
 __global__ void k_seg_keys(const int32_t* __restrict__ ids, const int32_t* __restrict__ n_ptr, int n_max,
                            int64_t n_rows, int skip_id, uint32_t* __restrict__ keys, int32_t* __restrict__ vals) {
+  rg_main_prio();
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n_max) return;
   const int n = *n_ptr;
@@ -79,6 +80,7 @@ __global__ __launch_bounds__(256) void k_seg_blocks(const uint32_t* __restrict__
                                                     int n_max, const float* __restrict__ src, int E, int lds,
                                                     float* __restrict__ G, int32_t* __restrict__ tags, int32_t tag,
                                                     float* __restrict__ part_first, float* __restrict__ part_last) {
+  rg_main_prio();
   using T = typename vec_t<V>::T;
   const int lane = threadIdx.x & 63;
   const int blk = blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -149,6 +151,7 @@ __global__ __launch_bounds__(256) void k_seg_cross(const uint32_t* __restrict__ 
                                                    float* __restrict__ G, int32_t* __restrict__ tags, int32_t tag,
                                                    const float* __restrict__ part_first,
                                                    const float* __restrict__ part_last) {
+  rg_main_prio();
   const int lane = threadIdx.x & 63;
   const int blk = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int p0 = blk * SB, p1 = p0 + SB;
