@@ -19,6 +19,7 @@ LinearHead   a Linear(H→A) used only through row gathers / argmax (Q heads).
 from __future__ import annotations
 
 import math
+import os
 import weakref
 
 import numpy as np
@@ -133,6 +134,10 @@ LAZY_HS = 8
 # a sampled head's backward queues the catch-up of the next draw's negatives on
 # a side stream (LazyRows.catch_up_async), under the trunk backward
 PREFETCH_NEGATIVES = True
+# ... and the step's targets are caught up on that side stream beside the trunk
+# forward (SampledSoftmaxHead.prepare_rows(early=True)); RG_TARGETS_ASYNC=0: on
+# the launch stream before it (A/B; default off until measured)
+TARGETS_ASYNC = os.environ.get("RG_TARGETS_ASYNC", "0") != "0"
 
 
 class LazyRows:
@@ -174,21 +179,22 @@ class LazyRows:
         call("rg_lazy_catch_up", *tab, self.rows, self.last.data_ptr(), self.need.data_ptr(), self.stamp, self.n,
              self.hist.data_ptr(), st)
 
-    def catch_up_async(self, tab, seed, counter, S):
-        """catch_up of the S negatives of draw ``counter`` on a side stream,
-        ordered after everything queued so far on the current stream (the
-        step's own Adam): it runs under the rest of the step (the trunk
-        backward, the next step's trunk forward).  The next use of the table
-        on any stream — catch_up, adam, materialize — joins it first."""
+    def catch_up_async(self, tab, seed, counter, S, ids=None, n_ids=0):
+        """catch_up of the S negatives of draw ``counter`` (and of ``n_ids``
+        int64 ids at ``ids``) on a side stream, ordered after everything
+        queued so far on the current stream (the step's own Adam): it runs
+        under the rest of the step (the trunk backward, the next step's trunk
+        forward).  The next use of the table on any stream — catch_up, adam,
+        materialize, join — waits for it first."""
         self.join()
-        if self.n == self.full or S == 0:
+        if self.n == self.full or S + n_ids == 0:
             return
         cur = torch.cuda.current_stream(self.device)
         if self.side is None:
             self.side = torch.cuda.Stream(device=self.device)
         self.side.wait_stream(cur)
         with torch.cuda.stream(self.side):
-            self.catch_up(tab, None, 0, seed, counter, S)
+            self.catch_up(tab, ids, n_ids, seed, counter, S)
         self.pending = torch.cuda.Event()
         self.pending.record(self.side)
 
@@ -1546,12 +1552,18 @@ class SampledSoftmaxHead(SoftmaxHead):
         if lz is not None:
             lz.materialize(self._lazy_tab())
 
-    def prepare_rows(self, tgt, B):
+    def prepare_rows(self, tgt, B, early=False):
         """Catch up the rows the next forward_loss reads: its B targets (device
-        int64) and the S negatives of draw ``self.draws``."""
+        int64) and the S negatives of draw ``self.draws``.  ``early`` (neg_job,
+        before the trunk's forward): when the negatives were already caught up
+        by the last backward, the targets' catch-up goes to the side stream
+        and runs beside the trunk's forward; forward_loss joins it."""
         if self.lazy is not None and self._ready_draw != self.draws:
             S = 0 if self._neg_draw == self.draws else self.S   # (the negatives: queued by the last backward)
-            self.lazy.catch_up(self._lazy_tab(), tgt.data_ptr(), B, self.seed, self.draws, S)
+            if early and S == 0 and TARGETS_ASYNC:
+                self.lazy.catch_up_async(self._lazy_tab(), 0, 0, 0, ids=tgt.data_ptr(), n_ids=B)
+            else:
+                self.lazy.catch_up(self._lazy_tab(), tgt.data_ptr(), B, self.seed, self.draws, S)
             self._ready_draw = self.draws
 
     @staticmethod
@@ -1594,7 +1606,7 @@ class SampledSoftmaxHead(SoftmaxHead):
         the negatives') are caught up here, before the trunk's gather launch
         reads the negatives (catch-up Adam)."""
         if tgt is not None:
-            self.prepare_rows(tgt, B)
+            self.prepare_rows(tgt, B, early=True)
         w = self.sws(slot, B)
         if w.terms == 0 or not w.zrow:
             return None
@@ -1622,6 +1634,8 @@ class SampledSoftmaxHead(SoftmaxHead):
         logits read their planes (draw = 2)."""
         B = h.shape[0]
         self.prepare_rows(tgt, B)   # (a no-op when neg_job already did it for this draw)
+        if self.lazy is not None:
+            self.lazy.join()        # (the targets' catch-up queued by neg_job on the side stream)
         w = self.sws(slot, B)
         st = stream_ptr()
         g = _f32(1.0 / B)
