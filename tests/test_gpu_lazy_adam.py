@@ -169,13 +169,19 @@ def _nets(tr):
     return [getattr(tr, n) for n in ("gru_model", "SMORL_1", "SMORL_2", "DQN_1", "DQN_2") if hasattr(tr, n)]
 
 
-@pytest.mark.parametrize("kind", ["gru4rec_sampled", "bidir_sampled", "gru4rec_full", "smorl"])
+@pytest.mark.parametrize("kind", ["gru4rec_sampled", "bidir_sampled", "gru4rec_full", "smorl",
+                                  "gru4rec_sampled_targets_async"])
 def test_trainers_with_catch_up_adam_equal_eager_bitwise(monkeypatch, kind):
     """20 steps of a trainer with catch-up Adam vs the eager dense sweeps:
     identical losses, and after a mid-run evaluation (model forward + the
     device eval path) and a state_dict / optimizer-state read, every parameter
-    and Adam moment bitwise equal — also after the run."""
+    and Adam moment bitwise equal — also after the run.  *_targets_async: the
+    targets' catch-up on the side stream (engine.TARGETS_ASYNC)."""
     import random
+    if kind.endswith("_targets_async"):
+        from recommenders.hip import engine
+        monkeypatch.setattr(engine, "TARGETS_ASYNC", True)
+        kind = kind[:-len("_targets_async")]
     from recommenders.data_utils.synthetic import SessionStream, unpopular_items
     from recommenders.hip.evalpath import eval_batch
     N, L, E, B = 3000, 12, 64, 256
