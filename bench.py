@@ -98,7 +98,7 @@ def parse():
                          "hip/engine.py ZSTORE_MAX_BYTES) or pass 2 recomputes them (off)")
     ap.add_argument("--no-target", action="store_true", help="skip the north-star gather+sampled-logits side run")
     ap.add_argument("--no-native-side", action="store_true", help="skip the native-f32 side run")
-    ap.add_argument("--extra-steps", type=int, default=10,
+    ap.add_argument("--extra-steps", type=int, default=20,
                     help="C2 at N=1: timed steps of the short C3 / C4 side lines (configs_extra); 0 skips them")
     ap.add_argument("--extra-settle", type=int, default=1500,
                     help="untimed steps before the C3 side line's warmup (the catch-up Adam's steady state, "
@@ -641,6 +641,37 @@ def side_line(cfg, args, dev, batches, tok, steps, warmup, settle=0):
             "top_scanned_rows": scanned}
 
 
+SIDE_KEYS = ("metric", "workload", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "step_ms", "roofline",
+             "kernel_ms", "loss_first_last", "top_scanned_rows")
+
+
+def side_line_process(cfg, args, steps, warmup):
+    """The side line of ``cfg`` in a child process: ``bench.py --config cfg``
+    with the C2 line's precision / stored-logit settings, same seeded stream.
+    A step that spreads its kernels over several HIP streams measures what it
+    would in a process of its own only if its streams get their own hardware
+    queues; after the C2 and C3 trainers created theirs, the C4 trainer's
+    streams are assigned round-robin onto queues those already hold (C4 in
+    process 217.0K, median 18.81 ms, against 224.5K, median 18.11 ms, as its
+    own line on the same box, profiles/r07/bench_c4_side_in_process.json).
+    None when the child fails (the caller then times it in process)."""
+    import subprocess
+    cmd = [sys.executable, os.path.join(HERE, "bench.py"), "--config", cfg, "--steps", str(steps), "--warmup",
+           str(warmup), "--no-cpu-baseline", "--no-eval", "--no-native-side", "--no-target", "--extra-steps", "0",
+           "--precision", args.precision, "--stored-logits", args.stored_logits]
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE")}
+    try:
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env)
+        d = json.loads(r.stdout.strip().splitlines()[-1]) if r.returncode == 0 else None
+    except (subprocess.SubprocessError, ValueError, IndexError):
+        d = None
+    if not d or "value" not in d:
+        return None
+    out = {k: d.get(k) for k in SIDE_KEYS}
+    out.update(settle_steps=0, process="child")
+    return out
+
+
 def pinned(b):
     return tuple(x.pin_memory() for x in b)
 
@@ -924,11 +955,13 @@ def main():
             if world == 1 and args.extra_steps > 0:
                 # driver-visible C3 / C4 lines (BASELINE configs[2] / [3] on one GPU) on the same stream
                 extra = {}
-                wx = min(3, args.warmup)
+                wx = min(5, args.warmup)
                 nx = min(args.extra_steps, len(batches) - wx)
                 for c in ("c3", "c4"):
-                    extra[c] = side_line(c, args, dev, batches, tok, nx, wx,
-                                         settle=args.extra_settle if c == "c3" else 0)
+                    # C4 (four side streams per double-Q step) in a process of its own
+                    ln = side_line_process(c, args, nx, wx) if c == "c4" else None
+                    extra[c] = ln if ln is not None else side_line(c, args, dev, batches, tok, nx, wx,
+                                                                   settle=args.extra_settle if c == "c3" else 0)
     else:
         target = target_step(kern, T, B, args.negatives, E, HF, 2, terms)
         roof = dict(target) if target else None
