@@ -100,6 +100,9 @@ def parse():
     ap.add_argument("--no-native-side", action="store_true", help="skip the native-f32 side run")
     ap.add_argument("--extra-steps", type=int, default=20,
                     help="C2 at N=1: timed steps of the short C3 / C4 side lines (configs_extra); 0 skips them")
+    ap.add_argument("--settle", type=int, default=0,
+                    help="untimed steps (batches cycled) before the warmup of this run's own line (C3 in a "
+                         "child process: the catch-up Adam's steady state)")
     ap.add_argument("--extra-settle", type=int, default=1500,
                     help="untimed steps before the C3 side line's warmup (the catch-up Adam's steady state, "
                          "about 3·A/S steps for the sampled head's negatives)")
@@ -641,11 +644,13 @@ def side_line(cfg, args, dev, batches, tok, steps, warmup, settle=0):
             "top_scanned_rows": scanned}
 
 
+# side lines timed in a child process (RG_SIDE_CHILD, comma-separated configs)
+SIDE_CHILD = tuple(c for c in os.environ.get("RG_SIDE_CHILD", "c4").split(",") if c)
 SIDE_KEYS = ("metric", "workload", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "step_ms", "roofline",
              "kernel_ms", "loss_first_last", "top_scanned_rows")
 
 
-def side_line_process(cfg, args, steps, warmup):
+def side_line_process(cfg, args, steps, warmup, settle=0):
     """The side line of ``cfg`` in a child process: ``bench.py --config cfg``
     with the C2 line's precision / stored-logit settings, same seeded stream.
     A step that spreads its kernels over several HIP streams measures what it
@@ -658,7 +663,7 @@ def side_line_process(cfg, args, steps, warmup):
     import subprocess
     cmd = [sys.executable, os.path.join(HERE, "bench.py"), "--config", cfg, "--steps", str(steps), "--warmup",
            str(warmup), "--no-cpu-baseline", "--no-eval", "--no-native-side", "--no-target", "--extra-steps", "0",
-           "--precision", args.precision, "--stored-logits", args.stored_logits]
+           "--precision", args.precision, "--stored-logits", args.stored_logits, "--settle", str(settle)]
     env = {k: v for k, v in os.environ.items() if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE")}
     try:
         r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env)
@@ -668,7 +673,7 @@ def side_line_process(cfg, args, steps, warmup):
     if not d or "value" not in d:
         return None
     out = {k: d.get(k) for k in SIDE_KEYS}
-    out.update(settle_steps=0, process="child")
+    out.update(settle_steps=settle, process="child")
     return out
 
 
@@ -858,6 +863,8 @@ def main():
     tr.set_train()
     print(f"bench: trainer built in {time.perf_counter() - t_init:.1f} s, "
           f"{torch.cuda.memory_allocated(dev) / 2**30:.1f} GiB on the device", file=sys.stderr, flush=True)
+    for i in range(args.settle):
+        tr.train_step(*step_args(args.config, batches[i % len(batches)]))
     dt, losses, kern, per_step = timed_run(tr, batches, args.warmup, args.steps, world, not args.no_kernel_timing,
                                            args.config)
     scanned = top_scanned(tr)   # over the timed steps (exact either way; each costs one whole-row scan)
@@ -959,7 +966,8 @@ def main():
                 nx = min(args.extra_steps, len(batches) - wx)
                 for c in ("c3", "c4"):
                     # C4 (four side streams per double-Q step) in a process of its own
-                    ln = side_line_process(c, args, nx, wx) if c == "c4" else None
+                    ln = (side_line_process(c, args, nx, wx, args.extra_settle if c == "c3" else 0)
+                          if c in SIDE_CHILD else None)
                     extra[c] = ln if ln is not None else side_line(c, args, dev, batches, tok, nx, wx,
                                                                    settle=args.extra_settle if c == "c3" else 0)
     else:
@@ -989,7 +997,8 @@ def main():
     line = {
         "metric": metric,
         "value": round(value, 2), "unit": "session-steps/sec", "n_gpus": world, "steps": args.steps,
-        "warmup": args.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True,
+        "warmup": args.warmup, **({"settle_steps": args.settle} if args.settle else {}),
+        "ms_per_step": round(ms, 3), "higher_is_better": True,
         "scaling": "strong" if args.config in ("c4", "c5") else "weak",
         "vs_baseline": None, "dtype": "f32", "matmul_precision": args.precision, "stored_logits": args.stored_logits,
         "data": "synthetic (seeded Zipf session stream, random-init weights)",
