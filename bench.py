@@ -645,7 +645,7 @@ def side_line(cfg, args, dev, batches, tok, steps, warmup, settle=0):
 
 
 # side lines timed in a child process (RG_SIDE_CHILD, comma-separated configs)
-SIDE_CHILD = tuple(c for c in os.environ.get("RG_SIDE_CHILD", "c4").split(",") if c)
+SIDE_CHILD = tuple(c for c in os.environ.get("RG_SIDE_CHILD", "c3,c4").split(",") if c)
 SIDE_KEYS = ("metric", "workload", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "step_ms", "roofline",
              "kernel_ms", "loss_first_last", "top_scanned_rows")
 
@@ -965,7 +965,7 @@ def main():
                 wx = min(5, args.warmup)
                 nx = min(args.extra_steps, len(batches) - wx)
                 for c in ("c3", "c4"):
-                    # C4 (four side streams per double-Q step) in a process of its own
+                    # C3 and C4 (several side streams per step) each in a process of its own
                     ln = (side_line_process(c, args, nx, wx, args.extra_settle if c == "c3" else 0)
                           if c in SIDE_CHILD else None)
                     extra[c] = ln if ln is not None else side_line(c, args, dev, batches, tok, nx, wx,
